@@ -1,0 +1,167 @@
+"""Replicated-KVS throughput of the MI355X HermesKV data path (BASELINE.json metric).
+
+A step is one protocol round (hermes_worker.c:438-546) of every virtual worker of every
+replica: refill -> local batch -> INV broadcast -> incoming INV batch -> ACK batch -> incoming
+VAL batch, with the reference's commit counting (inline-util.h:189-217). value = committed
+local ops (GET_COMPLETE + PUT_COMPLETE [+ RMW_COMPLETE]) of all ranks / max-over-ranks time.
+
+N=1: configs[1] of BASELINE.json -- 100M keys, 31-byte values, Zipf 0.99, 20 % writes, INVs and
+VALs from 2 virtual replicas that also ACK every local write. N>1 (torchrun): one replica per
+GPU, INV/VAL slabs all-gathered and ACKs returned over RCCL (hermes_amd.replica_group).
+
+Prints one JSON line on rank 0 (see DESIGN.md "Measurement").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# algorithmic bytes per element, SURVEY.md 8(d): S_op=56, bucket=64, entry=64, S_msg=16
+BYTES = {"get": 56 + 64 + 64 + 56, "put": 56 + 64 + 2 * 64 + 56, "inv": 56 + 64 + 2 * 64 + 56,
+         "ack": 16 + 64 + 2 * 64 + 16, "val": 16 + 64 + 2 * 64 + 16}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--keys", type=int, default=100_000_000)
+    p.add_argument("--workers", type=int, default=4096, help="virtual workers (250-op buffers) per GPU")
+    p.add_argument("--zipf", type=float, default=0.99)
+    p.add_argument("--write-permille", type=int, default=200)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (0 = skip)")
+    p.add_argument("--cpu-workers", type=int, default=64)
+    p.add_argument("--seed", type=int, default=0x5EED)
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from hermes_amd import layout as L
+    from hermes_amd.kvs import HermesKV, sized_geometry
+    from hermes_amd.workload import Round, zipf_params
+
+    t0 = time.time()
+    bkts, cap = sized_geometry(a.keys)
+    kvs = HermesKV(a.keys, bkts, cap, machine_id=rank if world > 1 else 0, device=local_rank)
+    torch.cuda.synchronize()
+    t_pop = time.time() - t0
+    z = zipf_params(a.keys, a.zipf)
+    total_steps = a.warmup + a.steps
+
+    if world > 1:
+        from hermes_amd.replica_group import ReplicaGroupRound
+        rnd = ReplicaGroupRound(kvs, a.workers, z, a.write_permille, seed=a.seed, world=world, rank=rank)
+    else:
+        rnd = Round(kvs, a.workers, L.membership(3, 0), [1, 2], z, a.write_permille, seed=a.seed,
+                    max_steps=total_steps + 1)
+    torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        rnd.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    c0 = rnd.counters.clone()
+    inv0 = rnd.inv_total.clone() if hasattr(rnd, "inv_total") else None
+    events: dict = {}
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(a.steps):
+        rnd.step(events)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t
+    c1 = rnd.counters.clone()
+    committed = int((c1[0] - c0[0]).item())
+    writes = int((c1[2] - c0[2]).item())
+    puts_ok = int((rnd.inv_total - inv0).item()) if inv0 is not None else writes
+
+    if world > 1:
+        tt = torch.tensor([committed, elapsed * 1e9], dtype=torch.float64, device="cuda")
+        allc = [torch.zeros_like(tt) for _ in range(world)]
+        dist.all_gather(allc, tt)
+        committed_all = int(sum(x[0].item() for x in allc))
+        elapsed_max = max(x[1].item() for x in allc) / 1e9
+    else:
+        committed_all, elapsed_max = committed, elapsed
+
+    # live per-batch kernel time (HIP events on the stream the batches run on)
+    ms = {k: sum(s.elapsed_time(e) for s, e in v) / len(v) for k, v in events.items()}
+    W, S = a.workers, Round.LOCAL
+    per_launch_bytes = {
+        "local": W * S * BYTES["get"] + (puts_ok / a.steps) * (BYTES["put"] - BYTES["get"]),
+        "invs": W * rnd.rstride * BYTES["inv"],
+        "acks": (puts_ok / a.steps) * rnd.R * BYTES["ack"],
+        "vals": W * rnd.rstride * BYTES["val"],
+    }
+    dom = max(ms, key=ms.get) if ms else "local"
+    ach = per_launch_bytes[dom] / (ms[dom] / 1e3) / 1e9 if ms else 0.0
+    value = committed_all / elapsed_max
+    out = {
+        "metric": "replicated KVS ops/s (reads+writes committed)",
+        "value": value,
+        "unit": "ops/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed_max * 1e3 / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded Zipf traces, CityHash keys, virtual or RCCL peers)",
+        "config": {
+            "workload": ("cfg2: 1xMI355X, 100M keys, 31 B values, Zipf 0.99, 20% writes, "
+                         "INV/ACK/VAL from 2 virtual replicas" if world == 1 else
+                         f"cfg4: {world}-replica Hermes group over RCCL, {a.keys} keys/replica"),
+            "keys": a.keys, "buckets": bkts, "log_cap": cap, "workers_per_gpu": W,
+            "local_batch": S, "zipf": a.zipf, "write_permille": a.write_permille,
+            "remote_invs_per_worker": rnd.rstride, "parallelism": f"replicas{world}",
+        },
+        "roofline": {
+            "bound": "hbm", "kernel": f"{dom} batch (k_lookup + radix sort + k_segment_exec)",
+            "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "traffic": None, "launch_ms": ms.get(dom), "algorithmic_bytes_per_launch": per_launch_bytes[dom],
+            "batch_ms": ms,
+        },
+        "detail": {
+            "committed_per_step_rank0": committed / a.steps, "writes_completed_rank0": writes,
+            "puts_succeeded_rank0": puts_ok, "populate_s": t_pop,
+            "step_bytes_per_committed_op_model": 554,
+        },
+    }
+    if rank == 0 and world == 1 and a.cpu_seconds > 0:
+        from oracle.cpu_baseline import run_cpu_baseline
+        out["cpu_baseline"] = run_cpu_baseline(kvs, z, a.write_permille, a.cpu_workers, a.cpu_seconds, a.seed)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

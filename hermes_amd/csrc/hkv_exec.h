@@ -1,0 +1,336 @@
+// hkv_exec.h -- per-entry state machine of the HermesKV protocol, device side.
+//
+// A segment (all elements of one launch that hit one log entry, in concatenation order) is
+// applied by ONE owner lane: it loads the entry's object meta into registers, runs every
+// element of the segment through the Hermes transitions below, and stores the meta once.
+// Because exactly one lane owns an entry during the launch, the reference's per-key seqlock
+// (concur_ctrl.h:144-224) has no work to do; only its NET effect on the version survives a
+// batch boundary, so the lock/unlock pair is folded into the version arithmetic:
+//   lock+unlock_dec -> +0, lock+unlock_inc -> +2, lock+unlock_inc_by_three -> +4,
+//   lock+unlock_custom(v) -> v, and "locked version - 1" reads are the plain version.
+// Each function cites the reference function whose observable behaviour it reproduces.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "hkv_codes.h"
+
+namespace hkv {
+
+struct Meta {        // spacetime_object_meta (spacetime.h:138-148) + log val_len
+    uint32_t w4;     // entry bytes 16..19: opcode, val_len, state, ack_bv
+    uint32_t w5;     // 20..23: RMW_flag|last_writer_id, op_buffer_index, lock, ts.cid
+    uint32_t ver;    // 24..27: ts.version
+    uint32_t llw_ver;
+    uint8_t llw_cid;
+    uint8_t b32_dirty;  // (unused flag slot, keeps the struct 4-byte aligned)
+};
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
+__device__ __forceinline__ uint64_t ld64(const uint8_t *p) { return *reinterpret_cast<const uint64_t *>(p); }
+__device__ __forceinline__ void st32(uint8_t *p, uint32_t v) { *reinterpret_cast<uint32_t *>(p) = v; }
+
+// field accessors on the register copy
+__device__ __forceinline__ uint8_t m_val_len(const Meta &m) { return (uint8_t)(m.w4 >> 8); }
+__device__ __forceinline__ void m_set_val_len(Meta &m, uint8_t v) { m.w4 = (m.w4 & 0xFFFF00FFu) | ((uint32_t)v << 8); }
+__device__ __forceinline__ uint8_t m_state(const Meta &m) { return (uint8_t)(m.w4 >> 16); }
+__device__ __forceinline__ void m_set_state(Meta &m, uint8_t v) { m.w4 = (m.w4 & 0xFF00FFFFu) | ((uint32_t)v << 16); }
+__device__ __forceinline__ uint8_t m_ack_bv(const Meta &m) { return (uint8_t)(m.w4 >> 24); }
+__device__ __forceinline__ void m_set_ack_bv(Meta &m, uint8_t v) { m.w4 = (m.w4 & 0x00FFFFFFu) | ((uint32_t)v << 24); }
+__device__ __forceinline__ uint8_t m_rmw(const Meta &m) { return (uint8_t)(m.w5 & 1u); }
+__device__ __forceinline__ void m_set_rmw(Meta &m, uint8_t f) { m.w5 = (m.w5 & ~1u) | (f & 1u); }
+__device__ __forceinline__ uint8_t m_lwid(const Meta &m) { return (uint8_t)((m.w5 >> 1) & 0x7Fu); }
+__device__ __forceinline__ void m_set_lwid(Meta &m, uint8_t w) { m.w5 = (m.w5 & ~0xFEu) | ((uint32_t)(w & 0x7Fu) << 1); }
+__device__ __forceinline__ uint8_t m_obi(const Meta &m) { return (uint8_t)(m.w5 >> 8); }
+__device__ __forceinline__ void m_set_obi(Meta &m, uint8_t v) { m.w5 = (m.w5 & 0xFFFF00FFu) | ((uint32_t)v << 8); }
+__device__ __forceinline__ uint8_t m_cid(const Meta &m) { return (uint8_t)(m.w5 >> 24); }
+__device__ __forceinline__ void m_set_cid(Meta &m, uint8_t v) { m.w5 = (m.w5 & 0x00FFFFFFu) | ((uint32_t)v << 24); }
+
+__device__ __forceinline__ void meta_load(const uint8_t *e, Meta &m)
+{
+    m.w4 = ld32(e + 16);
+    m.w5 = ld32(e + 20);
+    m.ver = ld32(e + 24);
+    uint32_t w7 = ld32(e + 28);
+    m.llw_cid = (uint8_t)w7;
+    m.llw_ver = (w7 >> 8) | ((uint32_t)e[32] << 24);
+}
+
+__device__ __forceinline__ void meta_store(uint8_t *e, const Meta &m)
+{
+    st32(e + 16, m.w4);
+    st32(e + 20, m.w5 & 0xFF00FFFFu);  // the seqlock byte is free at batch boundaries
+    st32(e + 24, m.ver);
+    st32(e + 28, (uint32_t)m.llw_cid | (m.llw_ver << 8));
+    e[32] = (uint8_t)(m.llw_ver >> 24);
+}
+
+// Lamport order on (version, cid): concur_ctrl.h:63-75
+__device__ __forceinline__ uint64_t pack_ts(uint32_t ver, uint8_t cid) { return ((uint64_t)ver << 8) | cid; }
+
+// element header (spacetime_op_meta_t, spacetime.h:151-166)
+__device__ __forceinline__ uint8_t e_opcode(const uint8_t *x) { return x[8]; }
+__device__ __forceinline__ uint8_t e_state(const uint8_t *x) { return x[9]; }
+__device__ __forceinline__ uint64_t e_ts(const uint8_t *x) { return pack_ts(ld32(x + 12), x[11]); }
+__device__ __forceinline__ void e_set_ts(uint8_t *x, uint32_t ver, uint8_t cid) { x[11] = cid; st32(x + 12, ver); }
+__device__ __forceinline__ uint8_t e_rmw(const uint8_t *x) { return x[16] & 1u; }
+__device__ __forceinline__ void e_set_rmw(uint8_t *x, uint8_t f) { x[16] = (uint8_t)((x[16] & 0xFEu) | (f & 1u)); }
+
+template <int SV>
+__device__ __forceinline__ void copy_value(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint32_t n)
+{
+    if (SV > 0) {
+#pragma unroll 8
+        for (int k = 0; k < SV; ++k) dst[k] = src[k];
+    } else {
+        for (uint32_t k = 0; k < n; ++k) dst[k] = src[k];
+    }
+}
+
+struct Ctx {           // per-launch constants
+    Geometry g;
+    uint8_t g_membership;
+    uint8_t w_ack_init;
+    uint8_t *rw;       // this element's batch read_write_ops (ACKs)
+};
+
+__device__ __forceinline__ bool is_last_ack(uint8_t bv, const Ctx &c)  // spacetime.h:253-259
+{
+    return (uint8_t)(bv & c.g_membership) == c.g_membership;
+}
+
+// hermes_local_state_to_op, hermesKV.c:143-153
+template <int SV>
+__device__ __forceinline__ void local_state_to_op(uint8_t *op, const Meta &m, const uint8_t *entry, const Ctx &c)
+{
+    e_set_rmw(op, m_rmw(m));
+    op[9] = kReplaySuccess;
+    e_set_ts(op, m.ver, m_cid(m));
+    op[10] = (uint8_t)(c.g.st_value >> c.g.shift);
+    copy_value<SV>(op + kOpValueOff, entry + kEntryValueOff, c.g.st_value);
+}
+
+// hermes_write_replay_actions, hermesKV.c:155-175
+template <int SV>
+__device__ __forceinline__ void write_replay(uint8_t *op, uint8_t idx, Meta &m, const uint8_t *entry, const Ctx &c)
+{
+    m_set_state(m, kReplay);
+    m_set_obi(m, idx);
+    m.llw_ver = m.ver;
+    m.llw_cid = m_cid(m);
+    m_set_ack_bv(m, c.w_ack_init);
+    local_state_to_op<SV>(op, m, entry, c);
+}
+
+// hermes_check_membership_n_write_replay_actions, hermesKV.c:179-194
+template <int SV>
+__device__ __forceinline__ void membership_replay(uint8_t *op, uint8_t idx, Meta &m, const uint8_t *entry, const Ctx &c)
+{
+    uint8_t node = m_lwid(m);
+    if (node < 8 && ((c.g_membership >> node) & 1u)) op[9] = kGetStall;
+    else if (m_obi(m) == kObiEmpty) write_replay<SV>(op, idx, m, entry, c);
+}
+
+// hermes_update_actions_n_unlock, hermesKV.c:100-141 (net of lock + unlock_inc[_by_three])
+template <int SV>
+__device__ __forceinline__ void update_actions(uint8_t *op, uint8_t *entry, uint8_t idx, Meta &m, const Ctx &c, uint8_t rmw_flag)
+{
+    copy_value<SV>(entry + kEntryValueOff, op + kOpValueOff, c.g.st_value);
+    m_set_val_len(m, (uint8_t)((op[10] >> c.g.shift) + kOpMetaSize));
+    m_set_rmw(m, rmw_flag);
+    m_set_state(m, kWrite);
+    m_set_obi(m, idx);
+    uint32_t step = (!c.g.rmw_enabled || rmw_flag == 1) ? 2u : 4u;
+    uint8_t node = (uint8_t)c.g.machine_id;
+    m.llw_ver = m.ver + step;
+    m.llw_cid = node;
+    m_set_ack_bv(m, c.w_ack_init);
+    m.ver += step;
+    m_set_cid(m, node);
+    e_set_ts(op, m.ver, node);
+    e_set_rmw(op, rmw_flag);
+    op[9] = rmw_flag ? kRmwSuccess : kPutSuccess;
+}
+
+// hermes_exec_read, hermesKV.c:251-311
+template <int SV>
+__device__ __forceinline__ void exec_read(uint8_t *op, uint8_t *entry, uint8_t idx, Meta &m, const Ctx &c)
+{
+    uint8_t st = m_state(m);
+    if (st == kValid) {
+        copy_value<SV>(op + kOpValueOff, entry + kEntryValueOff, c.g.st_value);
+        op[9] = kGetComplete;
+        op[10] = (uint8_t)((m_val_len(m) >> c.g.shift) - kOpMetaSize);
+    } else if (st == kInvalidWrite || st == kWrite || st == kReplay) {
+        op[9] = kGetStall;
+    } else {
+        op[9] = kEmpty;
+        if (st == kInvalid) membership_replay<SV>(op, idx, m, entry, c);
+    }
+}
+
+// hermes_exec_write, hermesKV.c:314-356 (write coalescing off, config.h:80)
+template <int SV>
+__device__ __forceinline__ void exec_write(uint8_t *op, uint8_t *entry, uint8_t idx, Meta &m, const Ctx &c)
+{
+    uint8_t st = m_state(m);
+    if ((st == kValid || st == kInvalid) && m_obi(m) == kObiEmpty) update_actions<SV>(op, entry, idx, m, c, 0);
+    else op[9] = kPutStall;
+}
+
+// hermes_exec_rmw, hermesKV.c:358-428
+template <int SV>
+__device__ __forceinline__ void exec_rmw(uint8_t *op, uint8_t *entry, uint8_t idx, Meta &m, const Ctx &c)
+{
+    if (op[9] == kInProgressRmw) {
+        uint64_t ots = e_ts(op);
+        if (ots < pack_ts(m.ver, m_cid(m))) {
+            op[9] = kRmwAbort;
+            if (ots == pack_ts(m.llw_ver, m.llw_cid)) m_set_obi(m, kObiEmpty);
+        }
+        return;
+    }
+    op[9] = kEmpty;
+    uint8_t st = m_state(m);
+    if (st == kValid) {
+        if (m_obi(m) == kObiEmpty) update_actions<SV>(op, entry, idx, m, c, 1);
+    } else if (st == kInvalid) {
+        membership_replay<SV>(op, idx, m, entry, c);
+    }
+    if (op[9] != kRmwSuccess && op[9] != kReplaySuccess) op[9] = kRmwStall;
+}
+
+// hermes_exec_check_update_completion, hermesKV.c:430-484
+__device__ __forceinline__ void exec_update_completion(uint8_t *op, Meta &m, const Ctx &c)
+{
+    if (!is_last_ack(m_ack_bv(m), c)) return;
+    m_set_obi(m, kObiEmpty);
+    uint8_t st = m_state(m);
+    if (st == kInvalidWrite || st == kValid || st == kInvalid) {
+        if (st == kInvalidWrite) m_set_state(m, kInvalid);
+        op[9] = op[8] == kOpPut ? kPutComplete : kRmwComplete;
+    } else if (st == kWrite || st == kReplay) {
+        e_set_ts(op, m.ver, m_cid(m));
+        if (st == kWrite) op[9] = op[8] == kOpPut ? kPutCompleteSendVals : kRmwCompleteSendVals;
+        else op[9] = kReplayCompleteSendVals;
+        m_set_state(m, kValid);
+    }
+}
+
+// hermes_exec_inv, hermesKV.c:489-588
+template <int SV>
+__device__ __forceinline__ void exec_inv(uint8_t *inv, uint8_t *entry, Meta &m, const Ctx &c)
+{
+    const bool rmw_on = c.g.rmw_enabled != 0;
+    const uint64_t its = e_ts(inv);
+    const uint64_t cur = pack_ts(m.ver, m_cid(m));
+    const uint8_t inv_rmw = e_rmw(inv);
+    if (its >= cur || (rmw_on && inv_rmw)) {
+        if (cur < its) {
+            uint8_t st = m_state(m);
+            if (st == kValid) m_set_state(m, kInvalid);
+            else if (st == kWrite || st == kReplay) m_set_state(m, (rmw_on && m_rmw(m)) ? kInvalid : kInvalidWrite);
+            m_set_val_len(m, (uint8_t)c.g.kvs_value);
+            m_set_rmw(m, inv_rmw);
+            m_set_lwid(m, inv[9]);
+            copy_value<SV>(entry + kEntryValueOff, inv + kOpValueOff, c.g.st_value);
+            m.ver = (uint32_t)(its >> 8);
+            m_set_cid(m, (uint8_t)its);
+        } else if (cur == its) {
+            if (m_state(m) == kWrite) inv[8] = kInvOutOfGroup;
+            m_set_lwid(m, inv[9]);
+        } else {  // smaller, RMW INV: answer with an INV-abort carrying the local state
+            uint8_t sender = inv[9];
+            local_state_to_op<SV>(inv, m, entry, c);
+            inv[9] = sender;
+            inv[8] = kOpInvAbort;
+        }
+    }
+    if (inv[8] != kOpInvAbort && inv[8] != kInvOutOfGroup) inv[8] = kInvSuccess;
+}
+
+// hermes_exec_ack, hermesKV.c:591-674
+__device__ __forceinline__ void exec_ack(uint8_t *ack, Meta &m, const Ctx &c)
+{
+    int done = kObiEmpty;
+    uint64_t ats = e_ts(ack);
+    if (ats == pack_ts(m.llw_ver, m.llw_cid) && m_obi(m) != kObiEmpty) {
+        uint8_t sender = ack[9];
+        if (sender < 8) m_set_ack_bv(m, (uint8_t)(m_ack_bv(m) | (1u << sender)));
+        if (is_last_ack(m_ack_bv(m), c)) {
+            done = m_obi(m);
+            uint8_t st = m_state(m);
+            if (st == kValid || st == kInvalid || st == kInvalidWrite) {
+                if (st == kInvalidWrite) m_set_state(m, kInvalid);
+                ack[8] = kLastAckNoBcast;
+                m_set_obi(m, kObiEmpty);
+            } else if (st == kWrite || st == kReplay) {
+                m_set_state(m, kValid);
+                ack[8] = kLastAckSuccess;
+                m_set_obi(m, kObiEmpty);
+            }
+        }
+    }
+    if ((ack[8] == kLastAckSuccess || ack[8] == kLastAckNoBcast) && done != kObiEmpty && c.rw != nullptr) {
+        // every completer of this slot writes the same byte (it depends only on the slot's
+        // own opcode), so concurrent segments completing one slot are benign
+        uint8_t *w = c.rw + (size_t)done * c.g.op_size;
+        uint8_t oc = w[8];
+        if (oc == kOpGet) w[9] = kNew;
+        else if (oc == kOpPut) w[9] = kPutComplete;
+        else if (oc == kOpRmw) w[9] = kRmwComplete;
+    }
+    if (ack[8] != kLastAckSuccess) ack[8] = kAckSuccess;
+}
+
+// hermes_exec_val, hermesKV.c:676-703
+__device__ __forceinline__ void exec_val(uint8_t *val, Meta &m)
+{
+    if (e_ts(val) == pack_ts(m.ver, m_cid(m))) m_set_state(m, kValid);
+    val[8] = kValSuccess;
+}
+
+// hermes_exec_dispatcher, hermesKV.c:847-897
+template <int SV>
+__device__ __forceinline__ void dispatch(int type, uint8_t *x, uint8_t *entry, uint8_t idx, Meta &m, const Ctx &c)
+{
+    switch (type) {
+    case kLocal: {
+        uint8_t oc = x[8];
+        if (oc == kOpGet) exec_read<SV>(x, entry, idx, m, c);
+        else if (oc == kOpPut) exec_write<SV>(x, entry, idx, m, c);
+        else if (c.g.rmw_enabled && oc == kOpRmw) exec_rmw<SV>(x, entry, idx, m, c);
+        break;
+    }
+    case kLocalAfterMemb:
+        if (x[8] == kOpPut || x[8] == kOpRmw || x[9] == kInProgressReplay) exec_update_completion(x, m, c);
+        break;
+    case kInvs: exec_inv<SV>(x, entry, m, c); break;
+    case kAcks:
+        if (!c.g.rmw_enabled || x[8] == kOpAck) exec_ack(x, m, c);
+        else if (x[8] == kOpInvAbort) {
+            exec_inv<SV>(x, entry, m, c);
+            x[8] = kAckSuccess;
+        }
+        break;
+    case kVals: exec_val(x, m); break;
+    default: break;
+    }
+}
+
+// hermes_skip_dispatcher, hermesKV.c:709-769 (the INV membership-change side effect is
+// handled by the lookup kernel, which records the last such element per batch)
+__device__ __forceinline__ bool skip_elem(int type, const uint8_t *x)
+{
+    uint8_t st = x[9];
+    switch (type) {
+    case kLocal:
+        return st == kPutSuccess || st == kRmwSuccess || st == kReplaySuccess || st == kInProgressPut ||
+               st == kInProgressReplay || st == kOpMembChange || st == kPutCompleteSendVals;
+    case kLocalAfterMemb:
+        return !(st == kInProgressPut || st == kInProgressRmw || st == kInProgressReplay);
+    case kInvs: return x[8] == kOpMembChange;
+    case kAcks: return st == kOpMembChange;
+    default: return false;
+    }
+}
+
+}  // namespace hkv

@@ -1,0 +1,524 @@
+// hkv_runtime.hip -- host runtime and C ABI of libhermeskv.so (include/hermeskv.h).
+//
+// Owns the HBM image of one MICA-herd table per hkv_table (index buckets + circular log,
+// mica.h:62-91, byte layout identical to the reference), the per-launch scratch (sort keys,
+// temp storage), and a HIP stream. The reference entry points run on a process-wide default
+// table and block until the batch is applied, like the reference's synchronous C call.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#define HKV_IMPLEMENTATION 1
+#include "../../include/hermeskv.h"
+#include "hkv_internal.h"
+
+using namespace hkv;
+
+struct hkv_table {
+    hkv_config cfg;
+    Geometry geo;
+    hipStream_t stream = nullptr;
+    uint8_t *d_index = nullptr;
+    uint8_t *d_log = nullptr;
+    unsigned long long *d_evictions = nullptr;
+    int64_t inserted = 0;
+    uint32_t skip_key = 0;
+    int key_bits = 0;
+    // batch scratch
+    uint32_t *d_keys_a = nullptr, *d_keys_b = nullptr, *d_vals_a = nullptr, *d_vals_b = nullptr;
+    int64_t scratch_n = 0;
+    void *d_sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    int32_t *d_ns_idx = nullptr;
+    int32_t ns_cap = 0;
+    // staging for the host-pointer reference API
+    uint8_t *d_stage_ops = nullptr;
+    size_t stage_ops_cap = 0;
+    uint8_t *d_stage_rw = nullptr;
+    size_t stage_rw_cap = 0;
+    int32_t *d_stage_ns = nullptr;
+    uint8_t *h_stage = nullptr;  // pinned: ops | rw | node_suspected
+    std::mutex mu;
+};
+
+static thread_local std::string g_err;
+static const bool g_trace = getenv("HKV_TRACE") != nullptr;
+#define TRACE(...)                                       \
+    do {                                                 \
+        if (g_trace) {                                   \
+            fprintf(stderr, "[hkv] " __VA_ARGS__);       \
+            fputc('\n', stderr);                         \
+        }                                                \
+    } while (0)
+static std::mutex g_default_mu;
+static hkv_table *g_default = nullptr;
+static bool g_default_cfg_set = false;
+static hkv_config g_default_cfg;
+
+extern "C" {
+// reference global `struct spacetime_kv kv` (spacetime.c:15): callers only take its address
+struct spacetime_kv {
+    void *handle;
+    uint8_t pad[120];
+} kv;
+}
+
+static int fail(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) return fail(-5, "%s: %s", #expr, hipGetErrorString(e_));     \
+    } while (0)
+
+static bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
+
+static hkv_config reference_defaults()
+{
+    hkv_config c;
+    memset(&c, 0, sizeof c);
+    c.abi_version = HKV_ABI_VERSION;
+    c.machine_id = 0;
+    c.rw_len = 250;                       // MAX_BATCH_KVS_OPS_SIZE, config.h:42
+    c.num_keys = 1000 * 1000;             // SPACETIME_NUM_KEYS, spacetime.h:21
+    c.num_bkts = 2 * 1024 * 1024;         // SPACETIME_NUM_BKTS, spacetime.h:22
+    c.log_cap = 1024ull * 1024 * 1024;    // SPACETIME_LOG_CAP, spacetime.h:23
+    return c;
+}
+
+static void make_geometry(const hkv_config &c, Geometry &g)
+{
+    uint32_t kvs_value = c.big_objects ? c.extra_cache_lines * 64u + 46u : 46u;  // hrd.h:47
+    g.bkt_mask = c.num_bkts - 1;
+    g.log_cap = c.log_cap;
+    g.log_mask = c.log_cap - 1;
+    g.log_head = 0;
+    g.kvs_value = kvs_value;
+    g.st_value = kvs_value - kObjMetaSize;
+    g.entry_size = (kEntryMetaOff + kvs_value + 7u) & ~7u;
+    g.shift = c.big_objects ? 3u : 0u;
+    g.op_size = (kOpMetaSize + 2u + g.st_value + 7u) & ~7u;
+    g.entry_unit = (c.log_cap % g.entry_size == 0) ? g.entry_size : 8u;
+    g.rmw_enabled = c.rmw_enabled ? 1u : 0u;
+    g.machine_id = c.machine_id;
+}
+
+static int bit_width(uint64_t x)
+{
+    int b = 0;
+    while (x) {
+        ++b;
+        x >>= 1;
+    }
+    return b;
+}
+
+static int ensure_scratch(hkv_table *t, int64_t n, int key_bits)
+{
+    if (n > t->scratch_n) {
+        int64_t cap = n + n / 4 + 1024;
+        hipFree(t->d_keys_a);
+        hipFree(t->d_keys_b);
+        hipFree(t->d_vals_a);
+        hipFree(t->d_vals_b);
+        t->d_keys_a = t->d_keys_b = t->d_vals_a = t->d_vals_b = nullptr;
+        t->scratch_n = 0;
+        HIP_TRY(hipMalloc(&t->d_keys_a, cap * 4));
+        HIP_TRY(hipMalloc(&t->d_keys_b, cap * 4));
+        HIP_TRY(hipMalloc(&t->d_vals_a, cap * 4));
+        HIP_TRY(hipMalloc(&t->d_vals_b, cap * 4));
+        t->scratch_n = cap;
+    }
+    size_t need = sort_temp_bytes(t->scratch_n, key_bits > 0 ? key_bits : 32);
+    size_t need32 = sort_temp_bytes(t->scratch_n, 32);
+    if (need32 > need) need = need32;
+    if (need > t->sort_tmp_bytes) {
+        hipFree(t->d_sort_tmp);
+        t->d_sort_tmp = nullptr;
+        t->sort_tmp_bytes = 0;
+        HIP_TRY(hipMalloc(&t->d_sort_tmp, need));
+        t->sort_tmp_bytes = need;
+    }
+    return 0;
+}
+
+// Virtual log offsets of a run of inserts (mica_insert_one, mica.c:119-145): the head advances
+// by one entry per insert and wraps once, when fewer than MICA_MAX_VALUE + 32 bytes remain;
+// after that the unsigned "remaining" test underflows and the head never wraps again.
+static void plan_log(uint64_t h0, uint64_t cap, uint32_t e, uint32_t maxv, uint64_t n,
+                     uint64_t &k, uint64_t &hw, uint64_t &final_head)
+{
+    const uint64_t T = (uint64_t)maxv + 32, mask = cap - 1;
+    k = UINT64_MAX;
+    hw = 0;
+    if (h0 <= cap) {
+        uint64_t lo = cap > T ? cap - T : 0;
+        uint64_t kk = (h0 + e >= lo) ? 1 : (lo - h0 + e - 1) / e;
+        if (h0 + kk * e <= cap) {
+            k = kk;
+            hw = (h0 + kk * e + cap) & ~mask;
+        }
+    }
+    final_head = (n < k) ? h0 + n * e : hw + (n - k) * e;
+}
+
+extern "C" {
+
+int hkv_abi_version(void) { return HKV_ABI_VERSION; }
+
+const char *hkv_last_error(void) { return g_err.c_str(); }
+
+int hkv_table_create(const hkv_config *cfg, hkv_table **out)
+{
+    if (!cfg || !out) return fail(-1, "null argument");
+    if (cfg->abi_version != HKV_ABI_VERSION) return fail(-1, "abi_version %u != %d", cfg->abi_version, HKV_ABI_VERSION);
+    if (!is_pow2(cfg->num_bkts) || cfg->num_bkts > (1ull << 31)) return fail(-1, "num_bkts must be a power of two <= 2^31");
+    if (!is_pow2(cfg->log_cap) || cfg->log_cap < 4096) return fail(-1, "log_cap must be a power of two >= 4096");
+    if (cfg->machine_id > 127) return fail(-1, "machine_id must be < 128");
+    hkv_table *t = new hkv_table();
+    t->cfg = *cfg;
+    if (t->cfg.rw_len == 0) t->cfg.rw_len = 250;
+    make_geometry(t->cfg, t->geo);
+    uint64_t slots = t->geo.log_cap / t->geo.entry_unit;
+    if (slots >= 0xFFFFFFFFull) {
+        delete t;
+        return fail(-1, "log too large for 32-bit entry ids");
+    }
+    t->skip_key = (uint32_t)slots;
+    t->key_bits = bit_width(slots);
+    int rc = 0;
+    do {
+        if (hipSetDevice(cfg->device) != hipSuccess) { rc = fail(-5, "hipSetDevice(%d) failed", cfg->device); break; }
+        if (hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking) != hipSuccess) { rc = fail(-5, "stream"); break; }
+        if (hipMalloc(&t->d_index, t->cfg.num_bkts * 64) != hipSuccess) { rc = fail(-6, "index alloc %llu B", (unsigned long long)(t->cfg.num_bkts * 64)); break; }
+        if (hipMalloc(&t->d_log, t->cfg.log_cap + t->geo.entry_size) != hipSuccess) { rc = fail(-6, "log alloc %llu B", (unsigned long long)t->cfg.log_cap); break; }
+        if (hipMalloc(&t->d_evictions, sizeof(unsigned long long)) != hipSuccess) { rc = fail(-6, "alloc"); break; }
+        if (hipMemsetAsync(t->d_index, 0, t->cfg.num_bkts * 64, t->stream) != hipSuccess) { rc = fail(-5, "memset"); break; }
+        if (hipMemsetAsync(t->d_log, 0, t->cfg.log_cap + t->geo.entry_size, t->stream) != hipSuccess) { rc = fail(-5, "memset"); break; }
+        if (hipMemsetAsync(t->d_evictions, 0, sizeof(unsigned long long), t->stream) != hipSuccess) { rc = fail(-5, "memset"); break; }
+        if (hipStreamSynchronize(t->stream) != hipSuccess) { rc = fail(-5, "sync"); break; }
+    } while (0);
+    if (rc) {
+        hkv_table_destroy(t);
+        return rc;
+    }
+    *out = t;
+    return 0;
+}
+
+int hkv_table_destroy(hkv_table *t)
+{
+    if (!t) return 0;
+    if (t->stream) hipStreamSynchronize(t->stream);
+    hipFree(t->d_index);
+    hipFree(t->d_log);
+    hipFree(t->d_evictions);
+    hipFree(t->d_keys_a);
+    hipFree(t->d_keys_b);
+    hipFree(t->d_vals_a);
+    hipFree(t->d_vals_b);
+    hipFree(t->d_sort_tmp);
+    hipFree(t->d_ns_idx);
+    hipFree(t->d_stage_ops);
+    hipFree(t->d_stage_rw);
+    hipFree(t->d_stage_ns);
+    hipHostFree(t->h_stage);
+    if (t->stream) hipStreamDestroy(t->stream);
+    delete t;
+    return 0;
+}
+
+int hkv_table_config(const hkv_table *t, hkv_config *out)
+{
+    if (!t || !out) return fail(-1, "null argument");
+    *out = t->cfg;
+    return 0;
+}
+
+int hkv_table_populate(hkv_table *t, int64_t n, int val_len)
+{
+    if (!t) return fail(-1, "null table");
+    if (n <= 0) return fail(-1, "populate: n must be > 0");
+    if (val_len <= 0 || (uint32_t)val_len > t->geo.kvs_value) return fail(-1, "populate: bad val_len %d", val_len);
+    if (n > 0x7FFFFFFFll) return fail(-1, "populate: at most 2^31-1 keys (32-bit key ids)");
+    std::lock_guard<std::mutex> lk(t->mu);
+    HIP_TRY(hipSetDevice(t->cfg.device));
+    int bbits = bit_width(t->cfg.num_bkts - 1);
+    if (bbits == 0) bbits = 1;
+    int rc = ensure_scratch(t, n, bbits);
+    if (rc) return rc;
+    uint64_t *d_first = nullptr, *d_second = nullptr;
+    HIP_TRY(hipMalloc(&d_first, n * 8));
+    HIP_TRY(hipMalloc(&d_second, n * 8));
+    PopulateLaunch pl;
+    memset(&pl, 0, sizeof pl);
+    pl.first = d_first;
+    pl.second = d_second;
+    pl.keys_a = t->d_keys_a;
+    pl.keys_b = t->d_keys_b;
+    pl.vals_a = t->d_vals_a;
+    pl.vals_b = t->d_vals_b;
+    pl.sort_tmp = t->d_sort_tmp;
+    pl.sort_tmp_bytes = t->sort_tmp_bytes;
+    pl.index = t->d_index;
+    pl.log = t->d_log;
+    pl.evictions = t->d_evictions;
+    pl.n = n;
+    pl.bkt_mask = t->geo.bkt_mask;
+    pl.log_cap = t->geo.log_cap;
+    pl.log_mask = t->geo.log_mask;
+    pl.entry_size = t->geo.entry_size;
+    pl.key_bits = bbits;
+    pl.val_len_byte = (uint8_t)(val_len >> t->geo.shift);  // spacetime.c:45
+    uint64_t final_head;
+    pl.h0 = t->geo.log_head;
+    plan_log(t->geo.log_head, t->geo.log_cap, t->geo.entry_size, t->geo.kvs_value, (uint64_t)n, pl.k, pl.hw, final_head);
+    rc = launch_populate(pl, t->stream);
+    hipError_t se = hipStreamSynchronize(t->stream);
+    hipFree(d_first);
+    hipFree(d_second);
+    if (rc) return fail(rc, "populate launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));
+    if (se != hipSuccess) return fail(-5, "populate: %s", hipGetErrorString(se));
+    t->geo.log_head = final_head;
+    t->inserted += n;
+    return 0;
+}
+
+int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
+{
+    if (!t || !d) return fail(-1, "null argument");
+    if (d->type < 0 || d->type > 4) return fail(-1, "bad batch type %d", d->type);
+    if (d->n_batches < 0 || d->stride <= 0) return fail(-1, "bad batch geometry");
+    if (d->elem_size < kOpMetaSize || (d->elem_size & 7)) return fail(-1, "elem_size %u must be >= 16 and a multiple of 8", d->elem_size);
+    const bool needs_value = d->type == kLocal || d->type == kLocalAfterMemb || d->type == kInvs;
+    if (needs_value && d->elem_size < kOpValueOff + t->geo.st_value)
+        return fail(-1, "elem_size %u too small for %u-byte values", d->elem_size, t->geo.st_value);
+    if (d->type == kLocal && d->stride > 255)
+        return fail(-1, "local batches hold at most 255 ops (uint8 op_buffer_index)");
+    int64_t n = (int64_t)d->n_batches * d->stride;
+    if (n == 0) return 0;
+    if (n > 0x7FFFFFFFll) return fail(-1, "too many elements in one launch");
+    hipStream_t s = stream ? (hipStream_t)stream : t->stream;
+    int rc = ensure_scratch(t, n, t->key_bits);
+    if (rc) return rc;
+    int32_t *ns_idx = nullptr;
+    if (d->type == kInvs && d->d_node_suspected) {
+        if (d->n_batches > t->ns_cap) {
+            hipFree(t->d_ns_idx);
+            t->d_ns_idx = nullptr;
+            t->ns_cap = 0;
+            HIP_TRY(hipMalloc(&t->d_ns_idx, (size_t)d->n_batches * 4 + 64));
+            t->ns_cap = d->n_batches;
+        }
+        HIP_TRY(hipMemsetAsync(t->d_ns_idx, 0xFF, (size_t)d->n_batches * 4, s));
+        ns_idx = t->d_ns_idx;
+    }
+    BatchLaunch bl;
+    memset(&bl, 0, sizeof bl);
+    bl.g = t->geo;
+    bl.elems = d->d_elems;
+    bl.counts = d->d_counts;
+    bl.index = t->d_index;
+    bl.log = t->d_log;
+    bl.rw = d->type == kAcks ? d->d_rw : nullptr;
+    bl.rw_stride = d->rw_stride_bytes;
+    bl.ns_idx = ns_idx;
+    bl.node_suspected = d->d_node_suspected;
+    bl.keys_a = t->d_keys_a;
+    bl.keys_b = t->d_keys_b;
+    bl.vals_a = t->d_vals_a;
+    bl.vals_b = t->d_vals_b;
+    bl.sort_tmp = t->d_sort_tmp;
+    bl.sort_tmp_bytes = t->sort_tmp_bytes;
+    bl.n = n;
+    bl.n_batches = d->n_batches;
+    bl.stride = d->stride;
+    bl.esz = d->elem_size;
+    bl.type = d->type;
+    bl.skip_key = t->skip_key;
+    bl.key_bits = t->key_bits;
+    bl.g_membership = d->membership[1];
+    bl.w_ack_init = d->membership[2];
+    TRACE("batch_async type=%d n=%lld key_bits=%d", d->type, (long long)n, t->key_bits);
+    rc = launch_batch(bl, s);
+    if (rc) return fail(rc, "batch launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));
+    return 0;
+}
+
+int hkv_sync(hkv_table *t, void *stream)
+{
+    if (!t) return fail(-1, "null table");
+    HIP_TRY(hipStreamSynchronize(stream ? (hipStream_t)stream : t->stream));
+    return 0;
+}
+
+int hkv_copy_index(hkv_table *t, void *dst, uint64_t off, uint64_t bytes)
+{
+    if (!t || !dst) return fail(-1, "null argument");
+    if (off + bytes > t->cfg.num_bkts * 64) return fail(-1, "index range out of bounds");
+    HIP_TRY(hipStreamSynchronize(t->stream));
+    HIP_TRY(hipMemcpy(dst, t->d_index + off, bytes, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int hkv_copy_log(hkv_table *t, void *dst, uint64_t off, uint64_t bytes)
+{
+    if (!t || !dst) return fail(-1, "null argument");
+    if (off + bytes > t->cfg.log_cap + t->geo.entry_size) return fail(-1, "log range out of bounds");
+    HIP_TRY(hipStreamSynchronize(t->stream));
+    HIP_TRY(hipMemcpy(dst, t->d_log + off, bytes, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+uint64_t hkv_log_head(const hkv_table *t) { return t ? t->geo.log_head : 0; }
+
+int64_t hkv_num_index_evictions(const hkv_table *t)
+{
+    if (!t) return -1;
+    unsigned long long v = 0;
+    if (hipMemcpy(&v, t->d_evictions, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return (int64_t)v;
+}
+
+void *hkv_device_index(hkv_table *t) { return t ? t->d_index : nullptr; }
+void *hkv_device_log(hkv_table *t) { return t ? t->d_log : nullptr; }
+
+int hkv_hash_ids(const uint32_t *d_ids, uint64_t *d_keys_second, int64_t n, void *stream)
+{
+    if (launch_hash_ids(d_ids, d_keys_second, n, (hipStream_t)stream)) return fail(-5, "hash launch failed");
+    return 0;
+}
+
+int hkv_set_default_config(const hkv_config *cfg)
+{
+    std::lock_guard<std::mutex> lk(g_default_mu);
+    if (g_default) return fail(-1, "default table already exists");
+    g_default_cfg = *cfg;
+    g_default_cfg_set = true;
+    return 0;
+}
+
+hkv_table *hkv_default_table(void) { return g_default; }
+
+// ------------------------------------------------------------------ reference entry points
+[[noreturn]] static void die(const char *where)
+{
+    fprintf(stderr, "libhermeskv: %s: %s\n", where, g_err.c_str());
+    abort();
+}
+
+static hkv_table *default_table_locked(int instance_id)
+{
+    if (!g_default) {
+        hkv_config c = g_default_cfg_set ? g_default_cfg : reference_defaults();
+        if (!g_default_cfg_set && instance_id >= 0) c.machine_id = (uint32_t)instance_id;
+        if (hkv_table_create(&c, &g_default)) die("table create");
+        kv.handle = g_default;
+    }
+    return g_default;
+}
+
+void spacetime_init(int instance_id)
+{
+    std::lock_guard<std::mutex> lk(g_default_mu);
+    hkv_table *t = default_table_locked(instance_id);
+    if (hkv_table_populate(t, (int64_t)t->cfg.num_keys, (int)t->geo.kvs_value)) die("spacetime_init populate");
+}
+
+void spacetime_populate_fixed_len(struct spacetime_kv *, int n, int val_len)
+{
+    std::lock_guard<std::mutex> lk(g_default_mu);
+    hkv_table *t = default_table_locked(-1);
+    if (hkv_table_populate(t, n, val_len)) die("spacetime_populate_fixed_len");
+}
+
+// see the ABI note in hermeskv.h: curr_membership arrives as gcc passes the reference struct
+void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, int op_num,
+                             uint16_t sizeof_op_elem, uint64_t curr_membership,
+                             int *node_suspected, spacetime_op_t *read_write_ops, uint8_t thread_id)
+{
+    static_assert(sizeof(spacetime_group_membership) == sizeof(uint64_t), "membership is 8 bytes");
+    (void)thread_id;
+    TRACE("hermes_batch_ops_to_KVS type=%d op_num=%d esz=%u rw=%p ns=%p", (int)type, op_num,
+          (unsigned)sizeof_op_elem, (void *)read_write_ops, (void *)node_suspected);
+    if (op_num <= 0) return;
+    hkv_table *t;
+    {
+        std::lock_guard<std::mutex> lk(g_default_mu);
+        t = g_default;
+    }
+    if (!t) {
+        g_err = "spacetime_init was not called";
+        die("hermes_batch_ops_to_KVS");
+    }
+    std::lock_guard<std::mutex> lk(t->mu);
+    if (hipSetDevice(t->cfg.device) != hipSuccess) die("hipSetDevice");
+    const size_t ops_bytes = (size_t)op_num * sizeof_op_elem;
+    const bool with_rw = type == acks && read_write_ops != nullptr;
+    const size_t rw_bytes = (size_t)t->cfg.rw_len * t->geo.op_size;
+    // device buffers + pinned host mirrors (pageable async copies are avoided on purpose)
+    if (ops_bytes > t->stage_ops_cap || (with_rw && rw_bytes > t->stage_rw_cap) || !t->d_stage_ns) {
+        size_t oc = ops_bytes > t->stage_ops_cap ? ops_bytes : t->stage_ops_cap;
+        size_t rc = rw_bytes > t->stage_rw_cap ? rw_bytes : t->stage_rw_cap;
+        hipFree(t->d_stage_ops);
+        hipFree(t->d_stage_rw);
+        hipFree(t->d_stage_ns);
+        hipHostFree(t->h_stage);
+        t->d_stage_ops = t->d_stage_rw = nullptr;
+        t->d_stage_ns = nullptr;
+        t->h_stage = nullptr;
+        t->stage_ops_cap = t->stage_rw_cap = 0;
+        if (hipMalloc(&t->d_stage_ops, oc) != hipSuccess || hipMalloc(&t->d_stage_rw, rc) != hipSuccess ||
+            hipMalloc(&t->d_stage_ns, 64) != hipSuccess ||
+            hipHostMalloc((void **)&t->h_stage, oc + rc + 64, hipHostMallocDefault) != hipSuccess)
+            die("staging alloc");
+        t->stage_ops_cap = oc;
+        t->stage_rw_cap = rc;
+    }
+    uint8_t *h_ops = t->h_stage, *h_rw = t->h_stage + t->stage_ops_cap;
+    int32_t *h_ns = reinterpret_cast<int32_t *>(t->h_stage + t->stage_ops_cap + t->stage_rw_cap);
+    hipStream_t s = t->stream;
+    memcpy(h_ops, op_array, ops_bytes);
+    if (with_rw) memcpy(h_rw, read_write_ops, rw_bytes);
+    *h_ns = node_suspected ? *node_suspected : -1;
+    if (hipMemcpyAsync(t->d_stage_ops, h_ops, ops_bytes, hipMemcpyHostToDevice, s) != hipSuccess) die("copy in");
+    if (with_rw && hipMemcpyAsync(t->d_stage_rw, h_rw, rw_bytes, hipMemcpyHostToDevice, s) != hipSuccess) die("copy in");
+    if (hipMemcpyAsync(t->d_stage_ns, h_ns, 4, hipMemcpyHostToDevice, s) != hipSuccess) die("copy in");
+    hkv_batch_desc d;
+    memset(&d, 0, sizeof d);
+    d.type = (int32_t)type;
+    d.n_batches = 1;
+    d.stride = op_num;
+    d.elem_size = sizeof_op_elem;
+    d.d_elems = t->d_stage_ops;
+    d.d_rw = with_rw ? t->d_stage_rw : nullptr;
+    d.d_node_suspected = (type == invs && node_suspected) ? t->d_stage_ns : nullptr;
+    memcpy(d.membership, &curr_membership, 8);
+    TRACE("staged in; launching");
+    if (hkv_batch_async(t, &d, s)) die("hermes_batch_ops_to_KVS");
+    TRACE("launched");
+    if (hipMemcpyAsync(h_ops, t->d_stage_ops, ops_bytes, hipMemcpyDeviceToHost, s) != hipSuccess) die("copy out");
+    if (with_rw && hipMemcpyAsync(h_rw, t->d_stage_rw, rw_bytes, hipMemcpyDeviceToHost, s) != hipSuccess) die("copy out");
+    if (d.d_node_suspected && hipMemcpyAsync(h_ns, t->d_stage_ns, 4, hipMemcpyDeviceToHost, s) != hipSuccess) die("copy out");
+    if (hipStreamSynchronize(s) != hipSuccess) die("sync");
+    memcpy(op_array, h_ops, ops_bytes);
+    if (with_rw) memcpy(read_write_ops, h_rw, rw_bytes);
+    if (d.d_node_suspected) *node_suspected = *h_ns;
+    TRACE("done");
+}
+
+}  // extern "C"

@@ -1,0 +1,339 @@
+// hkv_workload.hip -- device kernels around the batch path (include/hermeskv_workload.h):
+// seeded traces, refill + commit counting, and the worker loop's message marshalling, so a
+// protocol round never leaves HBM. One 256-thread workgroup per virtual worker where the
+// reference walks a worker's op buffer in order (refill, INV marshalling): the slot order
+// is kept with a wave-ballot prefix count instead of a serial loop.
+#include <hip/hip_runtime.h>
+
+#include "../../include/hermeskv_workload.h"
+#include "hkv_codes.h"
+
+namespace hkv {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9e3779b97f4a7c15ULL;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+    return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ double unit_double(uint64_t r) { return (double)(r >> 11) * (1.0 / 9007199254740992.0); }
+
+// Gray et al. "Quickly generating billion-record synthetic databases" (the YCSB Zipfian
+// generator); rank == key id, so id 0 is the hottest key as in parse_trace (util.c:337-343)
+__device__ __forceinline__ uint64_t zipf_draw(const hkv_zipf &z, double u)
+{
+    if (z.theta <= 0.0) {
+        uint64_t id = (uint64_t)(u * (double)z.n);
+        return id < z.n ? id : z.n - 1;
+    }
+    double uz = u * z.zetan;
+    if (uz < 1.0) return 0;
+    if (uz < z.half_pow) return 1;
+    uint64_t id = (uint64_t)((double)z.n * pow(z.eta * u - z.eta + 1.0, z.alpha));
+    return id < z.n ? id : z.n - 1;
+}
+
+__device__ __forceinline__ uint64_t ch_mix16(uint64_t u, uint64_t v)
+{
+    const uint64_t mul = 0x9ddfea08eb382d69ULL;
+    uint64_t a = (u ^ v) * mul;
+    a ^= a >> 47;
+    uint64_t b = (v ^ a) * mul;
+    b ^= b >> 47;
+    return b * mul;
+}
+
+// CityHash128(&id, 4).second (city.c:276-308 short path; see hkv_kernels.hip)
+__device__ __forceinline__ uint64_t key_of_id(uint32_t id)
+{
+    const uint64_t k0 = 0xc3a5c85c97cb3127ULL, k1 = 0xb492b66fbe98f273ULL;
+    uint64_t a = k0 * k1;
+    a = (a ^ (a >> 47)) * k1;
+    uint64_t c = k1 * k1 + ch_mix16(4u + ((uint64_t)id << 3), (uint64_t)id);
+    uint64_t d = (a + c) ^ ((a + c) >> 47);
+    uint64_t aa = ch_mix16(a, c);
+    uint64_t bb = ch_mix16(d, k1);
+    return ch_mix16(bb, aa);
+}
+
+// exclusive prefix count of `flag` over a 256-thread workgroup, in thread order
+__device__ __forceinline__ int block_rank(bool flag, int &total)
+{
+    __shared__ int wave_tot[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long m = __ballot(flag);
+    int in_wave = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_tot[wave] = __popcll(m);
+    __syncthreads();
+    int before = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        if (w < wave) before += wave_tot[w];
+        total += wave_tot[w];
+    }
+    __syncthreads();
+    return before + in_wave;
+}
+
+__device__ __forceinline__ int block_sum(int v)
+{
+    __shared__ int part[4];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int s = part[0] + part[1] + part[2] + part[3];
+    __syncthreads();
+    return s;
+}
+
+__global__ void k_gen_trace(uint64_t *tkey, uint8_t *top, uint32_t *tid, int32_t n_workers, int32_t len,
+                            hkv_zipf z, uint32_t write_pm, uint32_t rmw_pm, uint64_t seed)
+{
+    int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (int64_t)n_workers * len) return;
+    uint64_t r1 = splitmix64(seed ^ (0x1000003ull * (uint64_t)g));
+    uint64_t r2 = splitmix64(r1 ^ 0x5EEDull);
+    uint32_t id = (uint32_t)zipf_draw(z, unit_double(r1));
+    uint32_t coin = (uint32_t)(r2 % 1000u);
+    uint8_t op = kOpGet;
+    if (coin < write_pm) {  // create_uni_trace, util.c:236-240
+        op = kOpPut;
+        if (rmw_pm && (uint32_t)((r2 >> 32) % 1000u) < rmw_pm) op = kOpRmw;
+    }
+    tkey[g] = key_of_id(id);
+    top[g] = op;
+    if (tid) tid[g] = id;
+}
+
+// refill_ops, inline-util.h:149-303 (hot-key coalescing and latency probes off)
+__global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, uint32_t op_size, uint32_t st_value,
+                                                uint32_t shift, const uint64_t *tkey, const uint8_t *top,
+                                                int32_t tlen, uint32_t *cursor, uint32_t machine_id,
+                                                int32_t first_iter, unsigned long long *counters)
+{
+    const int w = blockIdx.x, i = threadIdx.x;
+    const bool live = i < stride;
+    uint8_t *op = ops + ((int64_t)w * stride + i) * op_size;
+    uint8_t st = live ? op[9] : 0;
+    bool done = live && (first_iter || st == kMiss || st == kPutComplete || st == kRmwAbort ||
+                         st == kRmwComplete || st == kOpMembComplete || st == kGetComplete);
+    int commits = (done && !first_iter && st != kMiss && st != kRmwAbort) ? 1 : 0;
+    int misses = (done && !first_iter && st == kMiss) ? 1 : 0;
+    int writes = (done && !first_iter && st == kPutComplete) ? 1 : 0;
+    int total;
+    int rank = block_rank(done, total);
+    uint32_t base = cursor[w];
+    int c = block_sum(commits), m = block_sum(misses), wr = block_sum(writes);
+    if (i == 0) {
+        cursor[w] = (uint32_t)((base + (uint32_t)total) % (uint32_t)tlen);
+        if (c) atomicAdd(&counters[0], (unsigned long long)c);
+        if (m) atomicAdd(&counters[1], (unsigned long long)m);
+        if (wr) atomicAdd(&counters[2], (unsigned long long)wr);
+    }
+    if (!done) return;
+    int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)rank) % (uint32_t)tlen);
+    uint8_t oc = top[t];
+    *reinterpret_cast<uint64_t *>(op) = tkey[t];
+    op[8] = oc;
+    op[9] = kNew;
+    op[10] = oc == kOpGet ? 0 : (uint8_t)(st_value >> shift);
+    uint16_t flags = (uint16_t)((oc == kOpRmw ? 1u : 0u) | (first_iter ? 0u : 2u));  // RMW_flag, no_coales = 1
+    *reinterpret_cast<uint16_t *>(op + 16) = flags;
+    if (oc != kOpGet) {
+        uint8_t v = (uint8_t)('a' + machine_id);
+        for (uint32_t k = 0; k < st_value; ++k) op[kOpValueOff + k] = v;
+    }
+}
+
+// wings_issue_pkts(inv) with the INV callbacks of hermes_worker.c:12-65
+__global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stride, uint32_t op_size, uint8_t *out,
+                                                      int32_t *count, uint32_t machine_id)
+{
+    const int w = blockIdx.x, i = threadIdx.x;
+    const bool live = i < stride;
+    uint8_t *op = ops + ((int64_t)w * stride + i) * op_size;
+    uint8_t st = live ? op[9] : 0;
+    bool send = live && (st == kPutSuccess || st == kRmwSuccess || st == kReplaySuccess || st == kOpMembChange);
+    int total;
+    int rank = block_rank(send, total);
+    if (i == 0) count[w] = total;
+    if (!send) return;
+    uint8_t *dst = out + ((int64_t)w * stride + rank) * op_size;
+    const uint64_t *s64 = reinterpret_cast<const uint64_t *>(op);
+    uint64_t *d64 = reinterpret_cast<uint64_t *>(dst);
+    for (uint32_t k = 0; k < op_size / 8; ++k) d64[k] = s64[k];
+    dst[9] = (uint8_t)machine_id;
+    dst[8] = kOpInv;
+    op[9] = st == kPutSuccess ? kInProgressPut : st == kRmwSuccess ? kInProgressRmw
+          : st == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
+}
+
+__global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32_t inv_stride, uint32_t op_size,
+                            uint8_t *acks, int32_t out_stride, int32_t *ack_count, const uint8_t *peers,
+                            int32_t n_peers, int64_t total)
+{
+    int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= total) return;
+    int64_t per_w = (int64_t)inv_stride * n_peers;
+    int32_t w = (int32_t)(g / per_w);
+    int32_t rem = (int32_t)(g - (int64_t)w * per_w);
+    int32_t j = rem / n_peers, r = rem - j * n_peers;
+    int32_t n = inv_count[w];
+    if (rem == 0) ack_count[w] = n * n_peers;
+    if (j >= n) return;
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(invs + ((int64_t)w * inv_stride + j) * op_size);
+    uint64_t *dst = reinterpret_cast<uint64_t *>(acks + ((int64_t)w * out_stride + rem) * kOpMetaSize);
+    uint64_t h1 = src[1];
+    h1 = (h1 & ~0xFFFFull) | kOpAck | ((uint64_t)peers[r] << 8);  // ack_copy_and_modify_elem
+    dst[0] = src[0];
+    dst[1] = h1;
+}
+
+// ack_skip_or_get_sender_id + ack_copy_and_modify_elem + ack_modify_elem_after_send
+__global__ void k_marshal_acks(uint8_t *invs, int64_t n, uint32_t op_size, uint8_t *out, uint32_t ack_size,
+                               uint32_t machine_id)
+{
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint8_t *x = invs + i * op_size;
+    uint8_t *y = out + i * ack_size;
+    uint8_t oc = x[8];
+    if (oc == kInvSuccess || (oc == kOpInvAbort && ack_size >= op_size)) {
+        uint32_t words = (oc == kInvSuccess ? kOpMetaSize : op_size) / 8;
+        for (uint32_t k = 0; k < words; ++k)
+            reinterpret_cast<uint64_t *>(y)[k] = reinterpret_cast<const uint64_t *>(x)[k];
+        y[9] = (uint8_t)machine_id;
+        y[8] = oc == kInvSuccess ? kOpAck : kOpInvAbort;
+    } else {
+        y[8] = kEmpty;
+    }
+    if (oc == kInvSuccess || oc == kOpInvAbort || oc == kOpMembChange) x[8] = kEmpty;
+}
+
+// val_skip_or_get_sender_id + val_copy_and_modify_elem + val_modify_elem_after_send
+__global__ void k_marshal_vals(uint8_t *acks, int64_t n, uint32_t ack_size, uint8_t *out, uint32_t machine_id)
+{
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint8_t *x = acks + i * ack_size;
+    uint8_t *y = out + i * kOpMetaSize;
+    uint8_t oc = x[8];
+    if (oc == kLastAckSuccess) {
+        reinterpret_cast<uint64_t *>(y)[0] = reinterpret_cast<const uint64_t *>(x)[0];
+        reinterpret_cast<uint64_t *>(y)[1] = reinterpret_cast<const uint64_t *>(x)[1];
+        y[8] = kOpVal;
+        y[9] = (uint8_t)machine_id;
+    } else {
+        y[8] = kEmpty;
+    }
+    if (oc == kLastAckSuccess || oc == kAckSuccess || oc == kOpMembChange) x[8] = kEmpty;
+}
+
+__global__ void k_gen_remote(uint8_t *invs, uint8_t *vals, int32_t per_peer, const uint8_t *peers, int32_t n_peers,
+                             uint32_t op_size, uint32_t st_value, uint32_t shift, hkv_zipf z, uint32_t clock,
+                             uint64_t seed, int64_t total)
+{
+    int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= total) return;
+    int32_t r = (int32_t)((g / per_peer) % n_peers);
+    uint64_t r1 = splitmix64(seed ^ ((uint64_t)clock << 40) ^ (0x9E37ull * (uint64_t)g));
+    uint32_t id = (uint32_t)zipf_draw(z, unit_double(r1));
+    uint32_t ver = 2u * (clock + 1u + (uint32_t)((r1 >> 7) & 1u));
+    uint8_t peer = peers[r];
+    uint64_t key = key_of_id(id);
+    uint64_t h1 = (uint64_t)kOpInv | ((uint64_t)peer << 8) | ((uint64_t)(st_value >> shift) << 16) |
+                  ((uint64_t)peer << 24) | ((uint64_t)ver << 32);
+    uint64_t *x = reinterpret_cast<uint64_t *>(invs + g * op_size);
+    x[0] = key;
+    x[1] = h1;
+    uint64_t vv = 0x0101010101010101ULL * (uint8_t)('a' + peer);
+    // bytes 16..17: RMW_flag 0, no_coales 0; value from byte 18
+    x[2] = vv << 16;
+    for (uint32_t k = 3; k < op_size / 8; ++k) x[k] = vv;
+    uint64_t *v = reinterpret_cast<uint64_t *>(vals + g * kOpMetaSize);
+    v[0] = key;
+    v[1] = (h1 & ~0xFFull) | kOpVal;
+}
+
+}  // namespace hkv
+
+using namespace hkv;
+
+static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
+static inline int ok() { return hipGetLastError() == hipSuccess ? 0 : -5; }
+
+extern "C" {
+
+int hkv_wl_gen_trace(uint64_t *tkey, uint8_t *top, uint32_t *tid, int32_t n_workers, int32_t len, const hkv_zipf *z,
+                     uint32_t write_pm, uint32_t rmw_pm, uint64_t seed, void *stream)
+{
+    int64_t n = (int64_t)n_workers * len;
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_gen_trace, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, tkey, top, tid, n_workers,
+                       len, *z, write_pm, rmw_pm, seed);
+    return ok();
+}
+
+int hkv_wl_refill(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint32_t st_value, uint32_t shift,
+                  const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor, uint32_t machine_id,
+                  int32_t first_iter, unsigned long long *counters, void *stream)
+{
+    if (stride > 256 || n_workers <= 0) return -1;
+    hipLaunchKernelGGL(k_refill, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, st_value,
+                       shift, tkey, top, tlen, cursor, machine_id, first_iter, counters);
+    return ok();
+}
+
+int hkv_wl_marshal_invs(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint8_t *out,
+                        int32_t *count, uint32_t machine_id, void *stream)
+{
+    if (stride > 256 || n_workers <= 0) return -1;
+    hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
+                       count, machine_id);
+    return ok();
+}
+
+int hkv_wl_marshal_acks(uint8_t *invs, int64_t n, uint32_t op_size, uint8_t *out, uint32_t ack_size,
+                        uint32_t machine_id, void *stream)
+{
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_marshal_acks, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, invs, n, op_size, out,
+                       ack_size, machine_id);
+    return ok();
+}
+
+int hkv_wl_marshal_vals(uint8_t *acks, int64_t n, uint32_t ack_size, uint8_t *out, uint32_t machine_id, void *stream)
+{
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_marshal_vals, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, acks, n, ack_size, out,
+                       machine_id);
+    return ok();
+}
+
+int hkv_wl_peer_acks(const uint8_t *inv_out, const int32_t *inv_count, int32_t n_workers, int32_t inv_stride,
+                     uint32_t op_size, uint8_t *acks, int32_t out_stride, int32_t *ack_count, const uint8_t *peer_ids,
+                     int32_t n_peers, void *stream)
+{
+    if (n_peers <= 0 || n_workers <= 0) return -1;
+    if (out_stride != inv_stride * n_peers) return -1;
+    int64_t total = (int64_t)n_workers * inv_stride * n_peers;
+    hipLaunchKernelGGL(k_peer_acks, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, inv_out, inv_count,
+                       inv_stride, op_size, acks, out_stride, ack_count, peer_ids, n_peers, total);
+    return ok();
+}
+
+int hkv_wl_gen_remote(uint8_t *invs, uint8_t *vals, int32_t n_workers, int32_t per_peer, const uint8_t *peer_ids,
+                      int32_t n_peers, uint32_t op_size, uint32_t st_value, uint32_t shift, const hkv_zipf *z,
+                      uint32_t clock, uint64_t seed, void *stream)
+{
+    int64_t total = (int64_t)n_workers * per_peer * n_peers;
+    if (total <= 0) return 0;
+    hipLaunchKernelGGL(k_gen_remote, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, invs, vals, per_peer,
+                       peer_ids, n_peers, op_size, st_value, shift, *z, clock, seed, total);
+    return ok();
+}
+
+}  // extern "C"

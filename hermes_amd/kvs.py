@@ -1,0 +1,247 @@
+"""Host-side mirror of the reference's KVS interface, on top of libhermeskv.so.
+
+Two ways in, matching the two halves of include/hermeskv.h:
+
+* reference entry points -- `spacetime_init`, `spacetime_populate_fixed_len`,
+  `hermes_batch_ops_to_KVS` -- same names, argument meaning and error behaviour as
+  include/hermes/spacetime.h:211-230 (they call the exported C symbols: the drop-in path);
+* `HermesKV`, one HBM-resident table per replica with the device fast path: many batches
+  (one per virtual worker) concatenated into one launch on torch tensors, on torch's stream.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import layout as L
+from .lib import HkvBatchDesc, HkvConfig, Membership, check, raw
+
+_L = raw()
+
+
+def _membership_struct(mb: bytes) -> Membership:
+    return Membership(int.from_bytes(bytes(mb[:8]).ljust(8, b"\0"), "little"))
+
+
+# ---------------------------------------------------------------- reference entry points
+def set_default_config(**kw) -> None:
+    """hkv_set_default_config: must precede spacetime_init (e.g. machine_id, num_keys, rmw)."""
+    cfg = make_config(**kw)
+    check(_L.hkv_set_default_config(ctypes.byref(cfg)), "hkv_set_default_config")
+
+
+def spacetime_init(instance_id: int) -> None:
+    """spacetime.h:211 -- build and populate the default table in HBM."""
+    _L.spacetime_init(int(instance_id))
+
+
+def spacetime_populate_fixed_len(n: int, val_len: int) -> None:
+    """spacetime.h:212."""
+    _L.spacetime_populate_fixed_len(None, int(n), int(val_len))
+
+
+def hermes_batch_ops_to_KVS(btype: int, op_array: np.ndarray, op_num: int, sizeof_op_elem: int,
+                            curr_membership: bytes, node_suspected: list | None,
+                            read_write_ops: np.ndarray | None, thread_id: int = 0) -> None:
+    """spacetime.h:228-230 on host numpy arrays, mutated in place. `node_suspected` is a
+    one-element list standing for the int* out-parameter (or None for NULL). As in the
+    reference, read_write_ops must hold the table's rw_len (max_batch_size, 250) ops."""
+    assert op_array.flags["C_CONTIGUOUS"]
+    ns = ctypes.c_int(node_suspected[0] if node_suspected else -1)
+    _L.hermes_batch_ops_to_KVS(int(btype), op_array.ctypes.data_as(ctypes.c_void_p), int(op_num),
+                               int(sizeof_op_elem), _membership_struct(curr_membership),
+                               ctypes.byref(ns) if node_suspected is not None else None,
+                               read_write_ops.ctypes.data_as(ctypes.c_void_p) if read_write_ops is not None else None,
+                               int(thread_id))
+    if node_suspected is not None:
+        node_suspected[0] = ns.value
+
+
+# ---------------------------------------------------------------- tables
+def make_config(num_keys: int = 1_000_000, num_bkts: int = 2 * 1024 * 1024, log_cap: int = 1 << 30,
+                machine_id: int = 0, rmw: bool = False, big_objects: bool = False,
+                extra_cache_lines: int = 0, device: int = 0, rw_len: int = 250) -> HkvConfig:
+    return HkvConfig(1, machine_id, int(rmw), int(big_objects), int(extra_cache_lines), device, rw_len, 0,
+                     num_keys, num_bkts, log_cap)
+
+
+def sized_geometry(num_keys: int, sizes: L.Sizes = L.DEFAULT) -> tuple[int, int]:
+    """Buckets and log capacity for `num_keys` (powers of two; about 2 keys per bucket as in
+    the reference's 1M keys / 2^21 buckets, and a log that never wraps)."""
+    bkts = 1 << max(4, (2 * num_keys - 1).bit_length())
+    need = num_keys * sizes.entry + sizes.kvs_value + 64
+    cap = 1 << max(16, (need - 1).bit_length())
+    return min(bkts, 1 << 27), cap
+
+
+class HermesKV:
+    """One HermesKV replica: a MICA-herd table in HBM plus the batch path on it."""
+
+    def __init__(self, num_keys: int | None = 1_000_000, num_bkts: int | None = None,
+                 log_cap: int | None = None, machine_id: int = 0, rmw: bool = False,
+                 big_objects: bool = False, extra_cache_lines: int = 0, device: int = 0,
+                 rw_len: int = 250, populate: bool = True):
+        self.sizes = L.Sizes(big_objects, extra_cache_lines if big_objects else 0)
+        nk = num_keys or 0
+        if num_bkts is None or log_cap is None:
+            b, c = sized_geometry(max(nk, 1), self.sizes)
+            num_bkts = num_bkts or b
+            log_cap = log_cap or c
+        self.cfg = make_config(nk, num_bkts, log_cap, machine_id, rmw, big_objects,
+                               extra_cache_lines, device, rw_len)
+        self.device = device
+        self.machine_id = machine_id
+        self.rmw = rmw
+        self.num_keys = nk
+        h = ctypes.c_void_p()
+        check(_L.hkv_table_create(ctypes.byref(self.cfg), ctypes.byref(h)), "hkv_table_create")
+        self.h = h
+        self._owned = True
+        if populate and nk:
+            self.populate(nk, self.sizes.kvs_value)
+
+    @classmethod
+    def default_table(cls) -> "HermesKV":
+        """Non-owning view of the table the reference entry points use (spacetime_init)."""
+        h = _L.hkv_default_table()
+        if not h:
+            raise RuntimeError("spacetime_init has not been called")
+        self = cls.__new__(cls)
+        self.h = ctypes.c_void_p(h)
+        self._owned = False
+        self.cfg = HkvConfig()
+        check(_L.hkv_table_config(self.h, ctypes.byref(self.cfg)), "hkv_table_config")
+        self.sizes = L.Sizes(bool(self.cfg.big_objects), self.cfg.extra_cache_lines if self.cfg.big_objects else 0)
+        self.device, self.machine_id = self.cfg.device, self.cfg.machine_id
+        self.rmw, self.num_keys = bool(self.cfg.rmw_enabled), self.cfg.num_keys
+        return self
+
+    def close(self) -> None:
+        if getattr(self, "h", None) and getattr(self, "_owned", False):
+            _L.hkv_table_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- setup
+    def populate(self, n: int, val_len: int) -> None:
+        check(_L.hkv_table_populate(self.h, int(n), int(val_len)), "hkv_table_populate")
+
+    @property
+    def log_head(self) -> int:
+        return _L.hkv_log_head(self.h)
+
+    @property
+    def evictions(self) -> int:
+        return _L.hkv_num_index_evictions(self.h)
+
+    # -- device fast path
+    def batch(self, btype: int, elems: torch.Tensor, n_batches: int, stride: int, elem_size: int,
+              membership: bytes, counts: torch.Tensor | None = None, rw: torch.Tensor | None = None,
+              rw_stride_bytes: int = 0, node_suspected: torch.Tensor | None = None,
+              stream: torch.cuda.Stream | None = None) -> None:
+        """Apply n_batches batches of one type, concatenated in `elems` (uint8, on the GPU),
+        in concatenation order, asynchronously on `stream` (default: torch's current)."""
+        assert elems.is_cuda and elems.dtype == torch.uint8
+        assert elems.numel() >= n_batches * stride * elem_size
+        d = HkvBatchDesc()
+        d.type = int(btype)
+        d.n_batches = int(n_batches)
+        d.stride = int(stride)
+        d.elem_size = int(elem_size)
+        d.d_elems = elems.data_ptr()
+        if counts is not None:
+            assert counts.is_cuda and counts.dtype == torch.int32 and counts.numel() >= n_batches
+            d.d_counts = counts.data_ptr()
+        if rw is not None:
+            assert rw.is_cuda and rw.dtype == torch.uint8
+            d.d_rw = rw.data_ptr()
+            d.rw_stride_bytes = int(rw_stride_bytes)
+        if node_suspected is not None:
+            assert node_suspected.is_cuda and node_suspected.dtype == torch.int32
+            d.d_node_suspected = node_suspected.data_ptr()
+        for i, b in enumerate(membership[:8]):
+            d.membership[i] = b
+        s = (stream or torch.cuda.current_stream(self.device)).cuda_stream
+        check(_L.hkv_batch_async(self.h, ctypes.byref(d), ctypes.c_void_p(s)), "hkv_batch_async")
+
+    def batch_host(self, btype: int, elems: np.ndarray, membership: bytes, rw: np.ndarray | None = None,
+                   n_batches: int = 1, stride: int | None = None, counts: np.ndarray | None = None,
+                   rw_stride_elems: int = 0, node_suspected: np.ndarray | None = None) -> None:
+        """Round-trip numpy arrays through the device path (parity tests)."""
+        dev = torch.device("cuda", self.device)
+        stride = len(elems) // n_batches if stride is None else stride
+        esz = elems.dtype.itemsize
+        t = torch.from_numpy(elems.view(np.uint8).reshape(-1).copy()).to(dev)
+        tc = torch.from_numpy(np.ascontiguousarray(counts, dtype=np.int32)).to(dev) if counts is not None else None
+        tr = torch.from_numpy(rw.view(np.uint8).reshape(-1).copy()).to(dev) if rw is not None else None
+        tn = torch.from_numpy(np.ascontiguousarray(node_suspected, dtype=np.int32)).to(dev) if node_suspected is not None else None
+        self.batch(btype, t, n_batches, stride, esz, membership, tc, tr,
+                   rw_stride_elems * (rw.dtype.itemsize if rw is not None else 0), tn)
+        torch.cuda.synchronize(dev)
+        elems.view(np.uint8).reshape(-1)[:] = t.cpu().numpy()
+        if rw is not None:
+            rw.view(np.uint8).reshape(-1)[:] = tr.cpu().numpy()
+        if node_suspected is not None:
+            node_suspected[:] = tn.cpu().numpy()
+
+    def sync(self) -> None:
+        check(_L.hkv_sync(self.h, None), "hkv_sync")
+
+    # -- HBM image (reference byte layout)
+    def index_bytes(self, offset: int = 0, nbytes: int | None = None) -> np.ndarray:
+        nbytes = self.cfg.num_bkts * 64 - offset if nbytes is None else nbytes
+        out = np.empty(nbytes, dtype=np.uint8)
+        check(_L.hkv_copy_index(self.h, out.ctypes.data_as(ctypes.c_void_p), offset, nbytes), "hkv_copy_index")
+        return out
+
+    def log_bytes(self, offset: int = 0, nbytes: int | None = None) -> np.ndarray:
+        nbytes = self.cfg.log_cap - offset if nbytes is None else nbytes
+        out = np.empty(nbytes, dtype=np.uint8)
+        check(_L.hkv_copy_log(self.h, out.ctypes.data_as(ctypes.c_void_p), offset, nbytes), "hkv_copy_log")
+        return out
+
+    def lookup_offset(self, key: int) -> int | None:
+        """Log offset of a key's entry via the same 3-step lookup the batch path does."""
+        key = int(key)
+        bkt = (key & 0xFFFFFFFFFFFF) & (self.cfg.num_bkts - 1)
+        slots = self.index_bytes(bkt * 64, 64).view("<u8")
+        tag = key >> 48
+        for s in slots:
+            s = int(s)
+            if (s & 1) and ((s >> 1) & 0x7FFFFF) == tag:
+                off = s >> 24
+                if self.log_head - off >= self.cfg.log_cap:
+                    return None
+                phys = off & (self.cfg.log_cap - 1)
+                e = self.log_bytes(phys, 16).view("<u8")
+                return phys if int(e[1]) == key else None
+        return None
+
+    def entry(self, key: int):
+        off = self.lookup_offset(key)
+        if off is None:
+            return None
+        return self.log_bytes(off, self.sizes.entry).view(L.entry_dtype(self.sizes))[0]
+
+    def device_index(self) -> int:
+        return _L.hkv_device_index(self.h)
+
+    def device_log(self) -> int:
+        return _L.hkv_device_log(self.h)
+
+
+def hash_ids(ids: torch.Tensor, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """CityHash128(&id, 4).second for each uint32 id, on the GPU (mica_gen_keys)."""
+    assert ids.is_cuda and ids.dtype == torch.int32
+    out = torch.empty(ids.numel(), dtype=torch.int64, device=ids.device)
+    s = (stream or torch.cuda.current_stream(ids.device)).cuda_stream
+    check(_L.hkv_hash_ids(ctypes.c_void_p(ids.data_ptr()), ctypes.c_void_p(out.data_ptr()), ids.numel(),
+                          ctypes.c_void_p(s)), "hkv_hash_ids")
+    return out

@@ -1,0 +1,199 @@
+"""Device-resident protocol rounds for many virtual workers (one replica), built from the
+batch path plus the worker loop's refill and marshalling (include/hermeskv_workload.h).
+
+One `Round.step()` is one iteration of run_worker's loop (hermes_worker.c:438-546) for every
+virtual worker at once: local batch -> INV broadcast -> incoming INV batch -> ACK batch ->
+incoming VAL batch -> refill (which counts committed ops, inline-util.h:189-217).
+Peers are either virtual (this module synthesises their ACKs and pre-generates their INVs
+and VALs) or real GPUs exchanging slabs over RCCL (hermes_amd.replica_group).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import layout as L
+from .kvs import HermesKV
+from .lib import check, raw
+
+_L = raw()
+_P = ctypes.c_void_p
+
+
+class HkvZipf(ctypes.Structure):
+    _fields_ = [("theta", ctypes.c_double), ("zetan", ctypes.c_double), ("alpha", ctypes.c_double),
+                ("eta", ctypes.c_double), ("half_pow", ctypes.c_double), ("n", ctypes.c_uint64)]
+
+
+_L.hkv_wl_gen_trace.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(HkvZipf),
+                                ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, _P]
+_L.hkv_wl_refill.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                             _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_int32, _P, _P]
+_L.hkv_wl_marshal_invs.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]
+_L.hkv_wl_marshal_acks.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, _P]
+_L.hkv_wl_marshal_vals.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
+_L.hkv_wl_peer_acks.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
+                                _P, ctypes.c_int32, _P]
+_L.hkv_wl_gen_remote.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_uint32,
+                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(HkvZipf), ctypes.c_uint32,
+                                 ctypes.c_uint64, _P]
+
+
+def zipf_params(n: int, theta: float) -> HkvZipf:
+    """Constants of the Gray et al. / YCSB Zipfian generator over ids [0, n)."""
+    if theta <= 0:
+        return HkvZipf(0.0, 0.0, 0.0, 0.0, 0.0, n)
+    zetan = 0.0
+    chunk = 10_000_000
+    for lo in range(1, n + 1, chunk):
+        i = np.arange(lo, min(n, lo + chunk - 1) + 1, dtype=np.float64)
+        zetan += float(np.sum(i ** -theta))
+    zeta2 = 1.0 + 2.0 ** -theta
+    alpha = 1.0 / (1.0 - theta)
+    eta = (1.0 - (2.0 / n) ** (1.0 - theta)) / (1.0 - zeta2 / zetan)
+    return HkvZipf(theta, zetan, alpha, eta, 1.0 + 0.5 ** theta, n)
+
+
+def _ptr(t: torch.Tensor | None):
+    return _P(t.data_ptr()) if t is not None else None
+
+
+def _s(stream=None):
+    return _P((stream or torch.cuda.current_stream()).cuda_stream)
+
+
+class Round:
+    """Buffers and kernels of one replica's protocol round over `n_workers` virtual workers."""
+
+    LOCAL = 250                      # MAX_BATCH_KVS_OPS_SIZE, config.h:42
+
+    def __init__(self, kvs: HermesKV, n_workers: int, membership: bytes, peer_ids: list[int],
+                 zipf: HkvZipf, write_permille: int = 200, rmw_permille: int = 0,
+                 remote_per_peer: int = 50, trace_len: int = 8192, seed: int = 0x5EED,
+                 virtual_peers: bool = True, max_steps: int = 64):
+        self.kvs = kvs
+        self.W = n_workers
+        self.mb = membership
+        self.peers = list(peer_ids)
+        self.zipf = zipf
+        self.sizes = kvs.sizes
+        self.op = kvs.sizes.op
+        self.ack_size = self.op if kvs.rmw else L.OP_META_SIZE
+        self.rpp = remote_per_peer
+        self.R = len(self.peers)
+        self.virtual = virtual_peers
+        self.machine_id = kvs.machine_id
+        dev = torch.device("cuda", kvs.device)
+        W, S = n_workers, self.LOCAL
+        u8 = dict(dtype=torch.uint8, device=dev)
+        self.ops = torch.zeros(W * S * self.op, **u8)
+        self.inv_out = torch.zeros(W * S * self.op, **u8)
+        self.inv_count = torch.zeros(W, dtype=torch.int32, device=dev)
+        self.ack_stride = S * max(self.R, 1)
+        self.acks = torch.zeros(W * self.ack_stride * self.ack_size, **u8)
+        self.ack_count = torch.zeros(W, dtype=torch.int32, device=dev)
+        self.val_out = torch.zeros(W * self.ack_stride * L.OP_META_SIZE, **u8)
+        self.rstride = self.rpp * max(self.R, 1)
+        self.ack_out = torch.zeros(W * self.rstride * self.ack_size, **u8)
+        self.cursor = torch.zeros(W, dtype=torch.int32, device=dev)
+        self.counters = torch.zeros(4, dtype=torch.int64, device=dev)
+        self.inv_total = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.peer_t = torch.tensor(self.peers or [0], dtype=torch.uint8, device=dev)
+        self.trace_len = trace_len
+        self.trace_key = torch.empty(W * trace_len, dtype=torch.int64, device=dev)
+        self.trace_op = torch.empty(W * trace_len, dtype=torch.uint8, device=dev)
+        check(_L.hkv_wl_gen_trace(_ptr(self.trace_key), _ptr(self.trace_op), None, W, trace_len,
+                                  ctypes.byref(zipf), write_permille, rmw_permille,
+                                  ctypes.c_uint64(seed ^ (self.machine_id << 48)), _s()), "gen_trace")
+        self.seed = seed
+        self.clock = 0
+        self.remote_inv = []
+        self.remote_val = []
+        if virtual_peers and self.R:
+            for k in range(max_steps):
+                ri = torch.empty(W * self.rstride * self.op, **u8)
+                rv = torch.empty(W * self.rstride * L.OP_META_SIZE, **u8)
+                check(_L.hkv_wl_gen_remote(_ptr(ri), _ptr(rv), W, self.rpp, _ptr(self.peer_t), self.R, self.op,
+                                           self.sizes.st_value, self.sizes.shift, ctypes.byref(zipf), k,
+                                           ctypes.c_uint64(seed * 7919 + self.machine_id), _s()), "gen_remote")
+                self.remote_inv.append(ri)
+                self.remote_val.append(rv)
+        self.refill(first=True)
+
+    # -- pieces of one round
+    def refill(self, first: bool = False):
+        check(_L.hkv_wl_refill(_ptr(self.ops), self.W, self.LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
+                               _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
+                               self.machine_id, int(first), _ptr(self.counters), _s()), "refill")
+
+    def local_batch(self):
+        self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb)
+
+    def marshal_invs(self):
+        check(_L.hkv_wl_marshal_invs(_ptr(self.ops), self.W, self.LOCAL, self.op, _ptr(self.inv_out),
+                                     _ptr(self.inv_count), self.machine_id, _s()), "marshal_invs")
+
+    def virtual_peer_acks(self):
+        check(_L.hkv_wl_peer_acks(_ptr(self.inv_out), _ptr(self.inv_count), self.W, self.LOCAL, self.op,
+                                  _ptr(self.acks), self.ack_stride, _ptr(self.ack_count), _ptr(self.peer_t),
+                                  self.R, _s()), "peer_acks")
+
+    def inv_batch(self, invs: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None):
+        self.kvs.batch(L.BatchType.invs, invs, n_batches, stride, self.op, self.mb, counts=counts)
+
+    def marshal_acks(self, invs: torch.Tensor, n: int, out: torch.Tensor):
+        check(_L.hkv_wl_marshal_acks(_ptr(invs), n, self.op, _ptr(out), self.ack_size, self.machine_id, _s()),
+              "marshal_acks")
+
+    def ack_batch(self, acks: torch.Tensor | None = None, n_batches: int | None = None, stride: int | None = None,
+                  counts: torch.Tensor | None = None):
+        acks = self.acks if acks is None else acks
+        self.kvs.batch(L.BatchType.acks, acks, n_batches or self.W, stride or self.ack_stride, self.ack_size,
+                       self.mb, counts=self.ack_count if counts is None else counts, rw=self.ops,
+                       rw_stride_bytes=self.LOCAL * self.op)
+
+    def marshal_vals(self, acks: torch.Tensor, n: int, out: torch.Tensor):
+        check(_L.hkv_wl_marshal_vals(_ptr(acks), n, self.ack_size, _ptr(out), self.machine_id, _s()),
+              "marshal_vals")
+
+    def val_batch(self, vals: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None):
+        self.kvs.batch(L.BatchType.vals, vals, n_batches, stride, L.OP_META_SIZE, self.mb, counts=counts)
+
+    # -- a whole round with virtual peers
+    def step(self, events: dict | None = None):
+        """One round of every virtual worker. `events` (name -> list) collects (start, end)
+        torch.cuda.Event pairs per batch for live kernel timing."""
+        def timed(name, fn):
+            if events is None:
+                fn()
+                return
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            events.setdefault(name, []).append((a, b))
+
+        k = self.clock % max(len(self.remote_inv), 1)
+        timed("local", self.local_batch)
+        self.marshal_invs()
+        self.inv_total += self.inv_count.sum()
+        if self.R:
+            self.virtual_peer_acks()
+            ri, rv = self.remote_inv[k], self.remote_val[k]
+            timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride))
+            self.marshal_acks(ri, self.W * self.rstride, self.ack_out)
+            timed("acks", self.ack_batch)
+            self.marshal_vals(self.acks, self.W * self.ack_stride, self.val_out)
+            timed("vals", lambda: self.val_batch(rv, self.W, self.rstride))
+        self.refill()
+        self.clock += 1
+
+    def committed(self) -> int:
+        return int(self.counters[0].item())
+
+    def stats(self) -> dict:
+        c = self.counters.cpu().tolist()
+        return {"committed": c[0], "misses": c[1], "writes_completed": c[2]}

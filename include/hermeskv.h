@@ -1,0 +1,152 @@
+/*
+ * hermeskv.h -- C ABI of libhermeskv.so, the MI355X-native HermesKV data path.
+ *
+ * Drop-in boundary: the three entry points the reference's worker links
+ * against, with the reference's exact signatures and argument meaning:
+ *
+ *   hermes_batch_ops_to_KVS   replaces include/hermes/spacetime.h:228-230 (hermesKV.c:905-996)
+ *   spacetime_init            replaces include/hermes/spacetime.h:211     (spacetime.c:25-30)
+ *   spacetime_populate_fixed_len replaces include/hermes/spacetime.h:212  (spacetime.c:32-68)
+ *
+ * The MICA-herd index and log (mica.h:62-91) live in HBM; op arrays are caller-owned host
+ * memory, mutated in place exactly as the reference mutates them. Errors the reference turns
+ * into asserts make these three calls print a message and abort (fail loudly); the hkv_* calls
+ * return a negative code instead and leave a message in hkv_last_error().
+ *
+ * The hkv_* extensions are the device-resident fast path: tables created explicitly,
+ * op arrays already in HBM, many batches (one per virtual worker) concatenated into one
+ * launch, asynchronous on a caller-supplied HIP stream. Their results are defined as the
+ * reference applied to the batches one after another (concatenation order).
+ *
+ * Plain pointers and sizes only; no HIP or torch types appear in any signature
+ * (streams are passed as void* and interpreted as hipStream_t, NULL = the table's stream).
+ */
+#ifndef HERMESKV_H
+#define HERMESKV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HKV_ABI_VERSION 1
+
+/* ------------------------------------------------------------------ reference types
+ * Declared here only when the reference's own spacetime.h has not been included; the
+ * layouts are the reference's (gcc, x86-64): see hermes_amd/layout.py for every offset. */
+#ifndef HERMES_SPACETIME_H
+enum hermes_batch_type_t {               /* spacetime.h:219-226 */
+    local_ops,
+    local_ops_after_membership_change,
+    invs,
+    acks,
+    vals
+};
+typedef struct { uint8_t bit_array[1]; } bit_vector_t;               /* bit_vector.h:40-44 */
+typedef struct { uint8_t lock; uint32_t version; } __attribute__((packed)) seqlock_t;
+typedef struct {                          /* spacetime.h:188-195, 8 bytes, passed by value */
+    volatile uint8_t num_of_alive_remotes;
+    volatile bit_vector_t g_membership;
+    volatile bit_vector_t w_ack_init;
+    seqlock_t lock;
+} spacetime_group_membership;
+typedef struct hkv_spacetime_op spacetime_op_t; /* 56-byte spacetime_op_t, used by pointer */
+struct spacetime_kv;                            /* opaque; only its address is passed */
+#endif
+
+/* ------------------------------------------------------------------ reference entry points */
+
+/* spacetime.h:228-230. op_array holds op_num elements of sizeof_op_elem bytes (56 for local
+ * ops and INVs, 16 for ACKs/VALs, 56 for ACKs in an RMW build). read_write_ops is the
+ * caller's local-op buffer (hkv_config.rw_len elements), written by ACK completions.
+ * node_suspected is written by INV batches that carry ST_OP_MEMBERSHIP_CHANGE. thread_id is
+ * accepted for signature compatibility (the reference uses it for debug prints only). */
+#ifndef HKV_IMPLEMENTATION
+void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, int op_num,
+                             uint16_t sizeof_op_elem, spacetime_group_membership curr_membership,
+                             int *node_suspected, spacetime_op_t *read_write_ops, uint8_t thread_id);
+#endif
+/* ABI note: the reference's callers are built by gcc, which passes the 8-byte (packed)
+ * spacetime_group_membership in one general-purpose register. clang classifies the same
+ * packed struct as MEMORY (stack), so the library defines this entry point with the 8 bytes
+ * received as a uint64_t (HKV_IMPLEMENTATION), matching what gcc-built callers pass. */
+
+/* spacetime.h:211. Creates the default table in HBM (hkv_set_default_config, else the
+ * reference defaults: 2^21 buckets, 1 GiB log) and populates hkv_config.num_keys keys
+ * (default 1,000,000) exactly as the reference does. instance_id becomes machine_id unless
+ * hkv_set_default_config set one. */
+void spacetime_init(int instance_id);
+
+/* spacetime.h:212. Populates the default table (creating it if needed); kv is accepted for
+ * signature compatibility and may be &kv or NULL. */
+void spacetime_populate_fixed_len(struct spacetime_kv *kv, int n, int val_len);
+
+/* ------------------------------------------------------------------ hkv extensions */
+
+typedef struct hkv_config {
+    uint32_t abi_version;       /* HKV_ABI_VERSION */
+    uint32_t machine_id;        /* reference global machine_id (hrd.h:87) */
+    uint32_t rmw_enabled;       /* ENABLE_RMWs (config.h:37) */
+    uint32_t big_objects;       /* USE_BIG_OBJECTS (hrd.h:36) */
+    uint32_t extra_cache_lines; /* EXTRA_CACHE_LINES (hrd.h:37) */
+    int32_t  device;            /* HIP device ordinal */
+    uint32_t rw_len;            /* elements of read_write_ops (max_batch_size, default 250) */
+    uint32_t reserved;
+    uint64_t num_keys;          /* SPACETIME_NUM_KEYS (spacetime.h:21) */
+    uint64_t num_bkts;          /* SPACETIME_NUM_BKTS (spacetime.h:22), power of two <= 2^31 */
+    uint64_t log_cap;           /* SPACETIME_LOG_CAP (spacetime.h:23), power of two */
+} hkv_config;
+
+typedef struct hkv_table hkv_table;
+
+/* One batch launch: n_batches batches of the same type, batch b owning elements
+ * [b*stride, b*stride + counts[b]) of d_elems, applied in concatenation order. */
+typedef struct hkv_batch_desc {
+    int32_t  type;              /* enum hermes_batch_type_t */
+    int32_t  n_batches;
+    int32_t  stride;            /* elements reserved per batch */
+    uint16_t elem_size;         /* sizeof_op_elem */
+    uint16_t reserved;
+    uint8_t *d_elems;           /* device */
+    const int32_t *d_counts;    /* device, n_batches entries; NULL = stride each */
+    uint8_t *d_rw;              /* device base of batch 0's read_write_ops (ACK batches) */
+    int64_t  rw_stride_bytes;   /* bytes between consecutive batches' read_write_ops */
+    int32_t *d_node_suspected;  /* device, n_batches entries (INV batches); NULL = ignore */
+    uint8_t  membership[8];     /* spacetime_group_membership by value */
+} hkv_batch_desc;
+
+int  hkv_abi_version(void);
+const char *hkv_last_error(void);
+
+int  hkv_table_create(const hkv_config *cfg, hkv_table **out);
+int  hkv_table_destroy(hkv_table *t);
+/* spacetime_populate_fixed_len on the device (reverse id order, MICA slot rules) */
+int  hkv_table_populate(hkv_table *t, int64_t n, int val_len);
+int  hkv_table_config(const hkv_table *t, hkv_config *out);
+
+/* device-resident batch path; stream may be NULL (the table's own stream) */
+int  hkv_batch_async(hkv_table *t, const hkv_batch_desc *desc, void *stream);
+int  hkv_sync(hkv_table *t, void *stream);
+
+/* parity / debugging views of the HBM image (reference byte layout) */
+int  hkv_copy_index(hkv_table *t, void *host_dst, uint64_t offset, uint64_t bytes);
+int  hkv_copy_log(hkv_table *t, void *host_dst, uint64_t offset, uint64_t bytes);
+uint64_t hkv_log_head(const hkv_table *t);
+int64_t  hkv_num_index_evictions(const hkv_table *t);
+void *hkv_device_index(hkv_table *t);
+void *hkv_device_log(hkv_table *t);
+
+/* default table used by the reference entry points */
+int  hkv_set_default_config(const hkv_config *cfg);
+hkv_table *hkv_default_table(void);
+
+/* synthetic workload helpers (device kernels) */
+/* keys_second[i] = CityHash128(&id_i, 4).second for ids[i] (mica_gen_keys, mica.c:149-165) */
+int  hkv_hash_ids(const uint32_t *d_ids, uint64_t *d_keys_second, int64_t n, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HERMESKV_H */

@@ -1,0 +1,87 @@
+/*
+ * hermeskv_workload.h -- device kernels around the batch path:
+ * trace generation, refill with commit counting, and the message marshalling the worker
+ * loop does between batch calls. They let a benchmark or a replica group keep batches in
+ * HBM from one protocol round to the next.
+ *
+ *   hkv_wl_gen_trace      create_uni_trace / parse_trace, util.c:228-343 (seeded, Zipf or uniform)
+ *   hkv_wl_refill         refill_ops, inline-util.h:149-303 (commit counting :205-217)
+ *   hkv_wl_marshal_invs   inv_skip_or_get_sender_id / inv_modify_elem_after_send /
+ *                         inv_copy_and_modify_elem, hermes_worker.c:12-65
+ *   hkv_wl_marshal_acks   ack_skip_or_get_sender_id / ack_copy_and_modify_elem, :69-118
+ *   hkv_wl_marshal_vals   val_skip_or_get_sender_id / val_copy_and_modify_elem, :122-157
+ *   hkv_wl_peer_acks      the ACKs `n_peers` replicas answer to a slab of INVs (the remote
+ *                         side of hermes_worker.c:467-473 for INVs they accept)
+ *   hkv_wl_gen_remote     INVs + VALs written by virtual peer replicas (a coordinator's
+ *                         inv_copy_and_modify_elem + val_copy_and_modify_elem)
+ * All device pointers; stream = hipStream_t or NULL.
+ */
+#ifndef HERMESKV_WORKLOAD_H
+#define HERMESKV_WORKLOAD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct hkv_zipf {
+    double theta;      /* 0 = uniform */
+    double zetan;      /* sum_{i=1..n} 1/i^theta */
+    double alpha;      /* 1 / (1 - theta) */
+    double eta;        /* (1 - (2/n)^(1-theta)) / (1 - zeta(2)/zetan) */
+    double half_pow;   /* 1 + 0.5^theta */
+    uint64_t n;        /* number of key ids */
+} hkv_zipf;
+
+/* trace[w*len + j]: key = CityHash128(&id,4).second, op = ST_OP_PUT with probability
+ * write_permille/1000 (then ST_OP_RMW with probability rmw_permille/1000 when RMWs are on),
+ * else ST_OP_GET; ids drawn from zipf (seeded splitmix64 streams, one per worker) */
+int hkv_wl_gen_trace(uint64_t *d_trace_key, uint8_t *d_trace_op, uint32_t *d_trace_id, int32_t n_workers,
+                     int32_t len, const hkv_zipf *zipf, uint32_t write_permille, uint32_t rmw_permille,
+                     uint64_t seed, void *stream);
+
+/* refill_ops over n_workers buffers of `stride` ops (op_size bytes each). Slots that are
+ * complete (or all slots when first_iter) take the next trace command of their worker.
+ * Adds completed-and-committed ops (everything complete except ST_MISS and ST_RMW_ABORT)
+ * to d_counters[0], misses to d_counters[1], completed writes to d_counters[2]. */
+int hkv_wl_refill(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint32_t st_value,
+                  uint32_t shift, const uint64_t *d_trace_key, const uint8_t *d_trace_op, int32_t trace_len,
+                  uint32_t *d_cursor, uint32_t machine_id, int32_t first_iter,
+                  unsigned long long *d_counters, void *stream);
+
+/* INVs for this round's successful writes/RMWs/replays: per worker, compacted into
+ * d_inv_out[w*stride ..] (op_size-byte spacetime_inv_t, sender = machine_id), count in
+ * d_inv_count[w]; the ops move to ST_IN_PROGRESS_* */
+int hkv_wl_marshal_invs(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size,
+                        uint8_t *d_inv_out, int32_t *d_inv_count, uint32_t machine_id, void *stream);
+
+/* ACKs (or INV-aborts with RMWs) for a batch of received INVs: element i of the INV batch
+ * produces element i of d_ack_out (ack_size bytes: 16, or op_size with RMWs), opcode
+ * ST_EMPTY where nothing is sent; the INV elements become ST_EMPTY (ack_modify_elem_after_send) */
+int hkv_wl_marshal_acks(uint8_t *d_invs, int64_t n, uint32_t op_size, uint8_t *d_ack_out, uint32_t ack_size,
+                        uint32_t machine_id, void *stream);
+
+/* VALs for ACK elements that completed a write (ST_LAST_ACK_SUCCESS): element i of d_val_out
+ * (16 bytes), ST_EMPTY elsewhere; the ACK elements become ST_EMPTY */
+int hkv_wl_marshal_vals(uint8_t *d_acks, int64_t n, uint32_t ack_size, uint8_t *d_val_out,
+                        uint32_t machine_id, void *stream);
+
+/* ACK batch answering a slab of INVs from n_peers replicas: for INV j of worker w,
+ * d_acks[w*out_stride + j*n_peers + r] = {key, ST_OP_ACK, sender = peer_ids[r], ts = inv ts};
+ * d_ack_count[w] = n_peers * d_inv_count[w] */
+int hkv_wl_peer_acks(const uint8_t *d_inv_out, const int32_t *d_inv_count, int32_t n_workers, int32_t inv_stride,
+                     uint32_t op_size, uint8_t *d_acks, int32_t out_stride, int32_t *d_ack_count,
+                     const uint8_t *peer_ids, int32_t n_peers, void *stream);
+
+/* INVs (op_size bytes) and matching VALs (16 bytes) written by n_peers virtual replicas:
+ * per worker w and peer r, `per_peer` INVs on keys drawn from zipf, timestamp
+ * (2*(clock + 1 + coin), peer_ids[r]), value bytes 'a' + peer id. */
+int hkv_wl_gen_remote(uint8_t *d_invs, uint8_t *d_vals, int32_t n_workers, int32_t per_peer,
+                      const uint8_t *peer_ids, int32_t n_peers, uint32_t op_size, uint32_t st_value,
+                      uint32_t shift, const hkv_zipf *zipf, uint32_t clock, uint64_t seed, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,50 @@
+"""bench.py's cpu_baseline leg -- TEST INFRASTRUCTURE ONLY.
+
+Times the oracle (the CPU restatement of the reference batch path, hkv_oracle.c) on the GPU
+host's own cores, single-threaded, on a bounded sample of the same workload (see
+hkv_oracle_bench.c). The table image is copied out of HBM so the CPU starts from the same
+state the device produced (the two populates are bit-identical, tests/test_gpu_parity.py).
+"""
+from __future__ import annotations
+
+import ctypes
+
+from .oracle import Config, build, lib
+
+
+class HkoZipf(ctypes.Structure):
+    _fields_ = [("theta", ctypes.c_double), ("zetan", ctypes.c_double), ("alpha", ctypes.c_double),
+                ("eta", ctypes.c_double), ("half_pow", ctypes.c_double), ("n", ctypes.c_uint64)]
+
+
+def run_cpu_baseline(kvs, zipf, write_permille: int, workers: int, seconds: float, seed: int,
+                     n_peers: int = 2, per_peer: int = 50) -> dict:
+    build()
+    L = lib()
+    L.hko_bench_rounds.restype = ctypes.c_int64
+    L.hko_bench_rounds.argtypes = [ctypes.c_void_p, ctypes.POINTER(Config), ctypes.c_int, ctypes.c_double,
+                                   ctypes.POINTER(HkoZipf), ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_uint64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]
+    L.hko_set_log_head.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    c = kvs.cfg
+    cfg = Config(c.big_objects, c.extra_cache_lines, c.rmw_enabled, c.machine_id, c.num_bkts, c.log_cap)
+    h = L.hko_create(ctypes.byref(cfg))
+    try:
+        from hermes_amd.lib import check, raw
+        R = raw()
+        idx = ctypes.cast(L.hko_index(h), ctypes.c_void_p)
+        log = ctypes.cast(L.hko_log(h), ctypes.c_void_p)
+        check(R.hkv_copy_index(kvs.h, idx, 0, c.num_bkts * 64), "copy index")
+        used = min(kvs.log_head, c.log_cap)
+        check(R.hkv_copy_log(kvs.h, log, 0, used), "copy log")
+        L.hko_set_log_head(h, kvs.log_head)
+        hz = HkoZipf(zipf.theta, zipf.zetan, zipf.alpha, zipf.eta, zipf.half_pow, zipf.n)
+        rounds, secs = ctypes.c_int64(0), ctypes.c_double(0.0)
+        committed = L.hko_bench_rounds(h, ctypes.byref(cfg), workers, seconds, ctypes.byref(hz), write_permille,
+                                       n_peers, per_peer, seed, ctypes.byref(rounds), ctypes.byref(secs))
+    finally:
+        L.hko_destroy(h)
+    return {"value": committed / secs.value, "unit": "ops/s", "cores": 1, "kind": "port",
+            "sample": (f"{rounds.value} rounds x {workers} workers x 250-op local batches (+{n_peers} virtual "
+                       f"peers x {per_peer} INV/VAL per worker-round, 2 ACKs per write) in {secs.value:.1f} s, "
+                       f"same table ({c.num_bkts} buckets) and Zipf/write mix as the GPU run")}

@@ -677,3 +677,6 @@ uint8_t *hko_index(hko_kvs *kv) { return kv->index; }
 uint8_t *hko_log(hko_kvs *kv) { return kv->log; }
 uint64_t hko_log_head(hko_kvs *kv) { return kv->log_head; }
 int64_t hko_num_index_evictions(hko_kvs *kv) { return kv->num_index_evictions; }
+
+/* lets the CPU baseline start from a table image copied out of HBM */
+void hko_set_log_head(hko_kvs *kv, uint64_t head) { kv->log_head = head; }

@@ -1,0 +1,181 @@
+/*
+ * hkv_oracle_bench.c -- TEST INFRASTRUCTURE ONLY: bench.py's cpu_baseline leg.
+ *
+ * Times the CPU restatement (hkv_oracle.c) on the same workload shape as the GPU step: each
+ * virtual worker runs the reference worker loop (hermes_worker.c:438-546) on one core:
+ * refill (inline-util.h:149-303) -> local batch -> INV marshal (hermes_worker.c:12-65) ->
+ * ACKs from the virtual peers -> incoming INV batch -> ACK batch (rw = the worker's ops) ->
+ * VAL marshal -> incoming VAL batch. Traces and peer INV/VAL slabs are generated before the
+ * timed loop with the same generators (splitmix64 streams, Gray/YCSB Zipf, CityHash keys).
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "hkv_oracle.h"
+
+typedef struct hko_zipf { double theta, zetan, alpha, eta, half_pow; uint64_t n; } hko_zipf;
+
+enum { OPC_GET = 111, OPC_PUT = 112, OPC_INV = 114, OPC_ACK = 115, OPC_VAL = 116 };
+
+static uint64_t sm64(uint64_t x)
+{
+    x += 0x9e3779b97f4a7c15ULL;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebULL;
+    return x ^ (x >> 31);
+}
+
+static uint64_t zipf_draw(const hko_zipf *z, double u)
+{
+    if (z->theta <= 0) {
+        uint64_t id = (uint64_t)(u * (double)z->n);
+        return id < z->n ? id : z->n - 1;
+    }
+    double uz = u * z->zetan;
+    if (uz < 1.0) return 0;
+    if (uz < z->half_pow) return 1;
+    uint64_t id = (uint64_t)((double)z->n * pow(z->eta * u - z->eta + 1.0, z->alpha));
+    return id < z->n ? id : z->n - 1;
+}
+
+static uint64_t key_of(uint32_t id)
+{
+    uint64_t f, s;
+    hko_cityhash128(&id, 4, &f, &s);
+    return s;
+}
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+void hko_set_log_head(hko_kvs *kv, uint64_t head);
+
+/* returns committed ops; rounds and seconds through out-params */
+int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, double seconds, const hko_zipf *z,
+                         uint32_t write_pm, int n_peers, int per_peer, uint64_t seed, int64_t *out_rounds,
+                         double *out_secs)
+{
+    const int S = 250, T = 8192, P = 16;
+    const uint32_t osz = hko_op_size(cfg), sv = hko_st_value_size(cfg);
+    const int rstride = n_peers * per_peer;
+    uint8_t *ops = calloc((size_t)n_workers * S, osz);
+    uint8_t *inv_out = calloc(S, osz);
+    uint8_t *acks = calloc((size_t)S * (n_peers ? n_peers : 1), 16);
+    uint8_t *ack_out = calloc(rstride ? rstride : 1, 16);
+    uint8_t *val_out = calloc((size_t)S * (n_peers ? n_peers : 1), 16);
+    uint8_t *rinv_pool = calloc((size_t)n_workers * P * (rstride ? rstride : 1), osz);
+    uint8_t *rval_pool = calloc((size_t)n_workers * P * (rstride ? rstride : 1), 16);
+    uint8_t *rinv = calloc(rstride ? rstride : 1, osz);
+    uint8_t *rval = calloc(rstride ? rstride : 1, 16);
+    uint64_t *tkey = malloc(sizeof(uint64_t) * (size_t)n_workers * T);
+    uint8_t *top = malloc((size_t)n_workers * T);
+    uint32_t *cursor = calloc(n_workers, 4);
+    uint8_t membership[8] = {2, 0x07, 0xF9, 0, 0, 0, 0, 0};
+    const uint8_t mid = (uint8_t)cfg->machine_id;
+    /* traces (create_uni_trace / parse_trace shape) */
+    for (int64_t g = 0; g < (int64_t)n_workers * T; g++) {
+        uint64_t r1 = sm64(seed ^ (0x1000003ull * (uint64_t)g)), r2 = sm64(r1 ^ 0x5EEDull);
+        uint32_t id = (uint32_t)zipf_draw(z, (double)(r1 >> 11) * (1.0 / 9007199254740992.0));
+        tkey[g] = key_of(id);
+        top[g] = (uint32_t)(r2 % 1000u) < write_pm ? OPC_PUT : OPC_GET;
+    }
+    /* peer INVs + VALs, P rounds deep, timestamps 2*(round + 1 + coin) */
+    for (int64_t g = 0; g < (int64_t)n_workers * P * rstride; g++) {
+        int64_t k = g / ((int64_t)n_workers * rstride);
+        int r = (int)((g / per_peer) % n_peers);
+        uint64_t r1 = sm64(seed ^ ((uint64_t)k << 40) ^ (0x9E37ull * (uint64_t)g));
+        uint32_t id = (uint32_t)zipf_draw(z, (double)(r1 >> 11) * (1.0 / 9007199254740992.0));
+        uint32_t ver = 2u * ((uint32_t)k + 1u + (uint32_t)((r1 >> 7) & 1u));
+        uint8_t peer = (uint8_t)(1 + r);
+        uint8_t *x = rinv_pool + g * osz, *v = rval_pool + g * 16;
+        uint64_t key = key_of(id);
+        memcpy(x, &key, 8);
+        x[8] = OPC_INV; x[9] = peer; x[10] = (uint8_t)sv; x[11] = peer;
+        memcpy(x + 12, &ver, 4);
+        memset(x + 18, 'a' + peer, sv);
+        memcpy(v, x, 16);
+        v[8] = OPC_VAL;
+    }
+    int64_t committed = 0, rounds = 0;
+    int first = 1;
+    double t0 = now_s(), t = t0;
+    while (first || t - t0 < seconds) {
+        for (int w = 0; w < n_workers; w++) {
+            uint8_t *ow = ops + (size_t)w * S * osz;
+            /* refill_ops (inline-util.h:149-303) */
+            for (int i = 0; i < S; i++) {
+                uint8_t *o = ow + (size_t)i * osz;
+                uint8_t st = o[9];
+                int done = first || st == 130 || st == 128 || st == 138 || st == 137 || st == 119 || st == 121;
+                if (!done) continue;
+                if (!first && st != 130 && st != 138) committed++;
+                int64_t ti = (int64_t)w * T + cursor[w];
+                cursor[w] = (cursor[w] + 1) % T;
+                memcpy(o, &tkey[ti], 8);
+                o[8] = top[ti];
+                o[9] = 141;
+                o[10] = top[ti] == OPC_GET ? 0 : (uint8_t)sv;
+                o[16] = 0;
+                o[17] = 0;
+                if (top[ti] != OPC_GET) memset(o + 18, 'a' + mid, sv);
+            }
+            hko_batch(kv, 0, ow, S, (uint16_t)osz, membership, NULL, NULL);
+            /* INV marshalling (hermes_worker.c:12-65) + peers' ACKs */
+            int ninv = 0;
+            for (int i = 0; i < S; i++) {
+                uint8_t *o = ow + (size_t)i * osz;
+                if (o[9] != 122) continue;
+                uint8_t *x = inv_out + (size_t)ninv * osz;
+                memcpy(x, o, osz);
+                x[9] = mid;
+                x[8] = OPC_INV;
+                o[9] = 143;
+                for (int r = 0; r < n_peers; r++) {
+                    uint8_t *a = acks + ((size_t)ninv * n_peers + r) * 16;
+                    memcpy(a, x, 16);
+                    a[8] = OPC_ACK;
+                    a[9] = (uint8_t)(1 + r);
+                }
+                ninv++;
+            }
+            if (rstride) {
+                size_t k = (size_t)(rounds % P) * n_workers + w;
+                memcpy(rinv, rinv_pool + k * rstride * osz, (size_t)rstride * osz);
+                memcpy(rval, rval_pool + k * rstride * 16, (size_t)rstride * 16);
+                int ns = -1;
+                hko_batch(kv, 2, rinv, rstride, (uint16_t)osz, membership, &ns, NULL);
+                for (int i = 0; i < rstride; i++) { /* ACKs back to the peers */
+                    uint8_t *x = rinv + (size_t)i * osz, *a = ack_out + (size_t)i * 16;
+                    if (x[8] == 124) { memcpy(a, x, 16); a[8] = OPC_ACK; a[9] = mid; }
+                    x[8] = 140;
+                }
+                hko_batch(kv, 3, acks, ninv * n_peers, 16, membership, NULL, ow);
+                for (int i = 0; i < ninv * n_peers; i++) { /* VALs for completed writes */
+                    uint8_t *a = acks + (size_t)i * 16, *v = val_out + (size_t)i * 16;
+                    if (a[8] == 126) { memcpy(v, a, 16); v[8] = OPC_VAL; v[9] = mid; }
+                    a[8] = 140;
+                }
+                hko_batch(kv, 4, rval, rstride, 16, membership, NULL, NULL);
+            }
+        }
+        rounds++;
+        first = 0;
+        t = now_s();
+    }
+    /* harvest the last round's completions (counted by the next refill in the reference) */
+    for (int64_t i = 0; i < (int64_t)n_workers * S; i++) {
+        uint8_t st = ops[i * osz + 9];
+        if (st == 128 || st == 121 || st == 137) committed++;
+    }
+    *out_rounds = rounds;
+    *out_secs = t - t0;
+    free(ops); free(inv_out); free(acks); free(ack_out); free(val_out); free(rinv_pool); free(rval_pool);
+    free(rinv); free(rval); free(tkey); free(top); free(cursor);
+    return committed;
+}

@@ -1,0 +1,281 @@
+"""Parity of the device path (libhermeskv.so on an MI355X) with the oracle, bit for bit.
+
+Every comparison is on the reference's byte images: element arrays, read_write_ops buffers,
+node_suspected, and the whole MICA index + log after every batch. The oracle is the CPU
+restatement pinned in tests/test_oracle.py.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from hermes_amd import layout as L  # noqa: E402
+from oracle.oracle import OracleKVS, gen_keys  # noqa: E402
+from tests import gen  # noqa: E402
+from tests.helpers import load_golden, run_known_answers  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _kvs():
+    from hermes_amd.kvs import HermesKV
+    return HermesKV
+
+
+def make_pair(n_keys, num_bkts, log_cap, rmw=False, big=False, machine_id=0):
+    sizes = L.BIG if big else L.DEFAULT
+    ecl = 4 if big else 0
+    g = _kvs()(n_keys, num_bkts, log_cap, machine_id, rmw, big, ecl)
+    o = OracleKVS(num_bkts, log_cap, machine_id, rmw, big, ecl)
+    o.populate(n_keys, sizes.kvs_value)
+    return g, o, sizes
+
+
+def assert_tables_equal(g, o, what=""):
+    gi, oi = g.index_bytes(), o.index_bytes()
+    if not np.array_equal(gi, oi):
+        bad = np.nonzero(gi != oi)[0]
+        pytest.fail(f"{what}: index differs at {len(bad)} bytes, first {bad[:8]}")
+    gl, ol = g.log_bytes(), o.log_bytes()[: g.cfg.log_cap]
+    if not np.array_equal(gl, ol):
+        bad = np.nonzero(gl != ol)[0]
+        e = g.sizes.entry
+        pytest.fail(f"{what}: log differs at {len(bad)} bytes; entries {np.unique(bad // e)[:8]} "
+                    f"offsets-in-entry {np.unique(bad % e)[:16]}")
+    assert g.log_head == o.log_head(), what
+
+
+def assert_elems_equal(a, b, what):
+    av, bv = a.view(np.uint8).reshape(len(a), -1), b.view(np.uint8).reshape(len(b), -1)
+    if not np.array_equal(av, bv):
+        rows = np.nonzero((av != bv).any(axis=1))[0]
+        cols = np.nonzero((av != bv).any(axis=0))[0]
+        r = rows[0]
+        pytest.fail(f"{what}: {len(rows)} elems differ (first {rows[:8]}), byte columns {cols[:16]}; "
+                    f"gpu {av[r][:20]} oracle {bv[r][:20]}")
+
+
+# ------------------------------------------------------------------ populate
+@pytest.mark.parametrize("n_keys,num_bkts,log_cap,big", [
+    (20000, 2048, 1 << 21, False),     # ~10 keys per bucket: evictions + same-tag overwrites
+    (3000, 4096, 1 << 17, False),      # log wraps (3000 x 64 B > 128 KiB)
+    (1500, 256, 1 << 20, True),        # big objects, 320-byte entries
+    (2000, 1024, 1 << 18, True),       # big objects whose log wraps past a non-multiple of 320
+])
+def test_populate_bit_exact(n_keys, num_bkts, log_cap, big):
+    g, o, _ = make_pair(n_keys, num_bkts, log_cap, big=big, rmw=big)
+    assert_tables_equal(g, o, "populate")
+    assert g.evictions == o.evictions()
+
+
+def test_populate_reference_default_geometry_lookups():
+    """spacetime_init geometry (1M keys, 2^21 buckets): all keys but the survey's three hit."""
+    ka = load_golden("known_answers.json")
+    c = ka["config"]
+    g = _kvs()(c["num_keys"], c["num_bkts"], c["log_cap"], machine_id=0)
+    keys = gen_keys(c["num_keys"])
+    n = len(keys)
+    ops = np.zeros(n, dtype=L.op_dtype())
+    ops["key"] = keys
+    ops["opcode"] = int(L.Op.GET)
+    ops["state"] = int(L.Bucket.NEW)
+    stride = 250
+    nb = (n + stride - 1) // stride
+    padded = np.zeros(nb * stride, dtype=ops.dtype)
+    padded[:n] = ops
+    counts = np.full(nb, stride, dtype=np.int32)
+    counts[-1] = n - (nb - 1) * stride
+    g.batch_host(L.BatchType.local_ops, padded, L.membership(3, 0), n_batches=nb, stride=stride, counts=counts)
+    st = padded["state"][:n]
+    assert np.nonzero(st == int(L.Resp.MISS))[0].tolist() == ka["always_miss_ids"]
+    ok = st == int(L.Resp.GET_COMPLETE)
+    assert ok.sum() == n - 3
+    ids = np.arange(n)
+    assert (padded["value"][:n][ok, 0] == ord("a") + ids[ok] % 20).all()
+    assert (padded["val_len"][:n][ok] == 30).all()
+
+
+# ------------------------------------------------------------------ known answers
+class _GpuEngine:
+    def __init__(self, kvs):
+        self.kvs = kvs
+
+    def batch(self, btype, elems, mb, rw=None):
+        self.kvs.batch_host(btype, elems, mb, rw=rw)
+
+    def entry(self, key):
+        return self.kvs.entry(key)
+
+
+def test_known_answers_device_path():
+    c = load_golden("known_answers.json")["config"]
+    g = _kvs()(c["num_keys"], c["num_bkts"], c["log_cap"], machine_id=c["machine_id"])
+    run_known_answers(_GpuEngine(g), gen_keys(c["num_keys"]))
+
+
+class _RefApiEngine:
+    """Drives the exported reference entry points (spacetime_init + hermes_batch_ops_to_KVS)."""
+
+    def __init__(self, kvs_mod):
+        self.m = kvs_mod
+
+    def batch(self, btype, elems, mb, rw=None):
+        ns = [-1]
+        full = None
+        if rw is not None:  # the reference's read_write_ops holds max_batch_size (250) ops
+            full = np.zeros(250, dtype=rw.dtype)
+            full[: len(rw)] = rw
+        self.m.hermes_batch_ops_to_KVS(btype, elems, len(elems), elems.dtype.itemsize, mb, ns, full, 0)
+        if rw is not None:
+            rw[:] = full[: len(rw)]
+
+    def entry(self, key):
+        return _kvs().default_table().entry(key)
+
+
+def test_known_answers_reference_entry_points():
+    from hermes_amd import kvs
+    kvs.spacetime_init(0)
+    run_known_answers(_RefApiEngine(kvs), gen_keys(1_000_000))
+
+
+# ------------------------------------------------------------------ randomized protocol rounds
+CONFIGS = [
+    pytest.param(dict(rmw=False, big=False), id="default"),
+    pytest.param(dict(rmw=True, big=False), id="rmw"),
+    pytest.param(dict(rmw=True, big=True), id="big_rmw"),
+]
+
+
+def _run_both(g, o, btype, elems_g, elems_o, mb, n_batches, stride, counts, rw_g=None, rw_o=None,
+              rw_stride=0, ns_g=None, ns_o=None):
+    g.batch_host(btype, elems_g, mb, rw=rw_g, n_batches=n_batches, stride=stride, counts=counts,
+                 rw_stride_elems=rw_stride, node_suspected=ns_g)
+    o.batch_multi(btype, elems_o, n_batches, stride, counts, mb, rw=rw_o, rw_stride_elems=rw_stride,
+                  node_suspected=ns_o)
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_random_protocol_rounds(cfg):
+    rng = np.random.default_rng(20261015)
+    rmw, big = cfg["rmw"], cfg["big"]
+    n_keys, num_bkts = 3000, 512
+    sizes = L.BIG if big else L.DEFAULT
+    log_cap = 1 << max(16, (n_keys * sizes.entry + 1024).bit_length())
+    g, o, sizes = make_pair(n_keys, num_bkts, log_cap, rmw=rmw, big=big, machine_id=0)
+    assert_tables_equal(g, o, "populate")
+    keys = gen_keys(n_keys)
+    tsp = gen.TsPool(rng)
+    mb_full = L.membership(5, 0)
+    mb_fail = L.membership(5, 0, alive=0b01111)     # node 4 dropped
+    W, S, M = 5, 48, 96                              # workers, local stride, message stride
+    for rnd in range(14):
+        pool = gen.key_pool(rng, keys, hot=24 if rnd % 2 else 200)
+        mb = mb_fail if rnd >= 9 else mb_full
+        # local ops
+        loc = gen.local_ops(rng, pool, W * S, sizes, rmw, tsp)
+        counts = rng.integers(S // 2, S + 1, size=W).astype(np.int32)
+        loc_o = gen.bytecopy(loc)
+        _run_both(g, o, L.BatchType.local_ops, loc, loc_o, mb, W, S, counts)
+        assert_elems_equal(loc, loc_o, f"round {rnd} local")
+        gen.harvest_ts(tsp, loc)
+        assert_tables_equal(g, o, f"round {rnd} local")
+        rw_g, rw_o = gen.bytecopy(loc), gen.bytecopy(loc)   # each worker's op buffer is its read_write_ops
+        # invs
+        inv = gen.invs(rng, pool, W * M, sizes, rmw, tsp)
+        counts = rng.integers(0, M + 1, size=W).astype(np.int32)
+        ns_g = np.full(W, -1, np.int32)
+        ns_o = ns_g.copy()
+        inv_o = gen.bytecopy(inv)
+        _run_both(g, o, L.BatchType.invs, inv, inv_o, mb, W, M, counts, ns_g=ns_g, ns_o=ns_o)
+        assert_elems_equal(inv, inv_o, f"round {rnd} invs")
+        np.testing.assert_array_equal(ns_g, ns_o)
+        assert_tables_equal(g, o, f"round {rnd} invs")
+        # acks (read_write_ops = the local buffers)
+        ack = gen.acks(rng, pool, W * M, sizes, rmw, tsp)
+        counts = rng.integers(M // 2, M + 1, size=W).astype(np.int32)
+        ack_o = gen.bytecopy(ack)
+        _run_both(g, o, L.BatchType.acks, ack, ack_o, mb, W, M, counts, rw_g, rw_o, rw_stride=S)
+        assert_elems_equal(ack, ack_o, f"round {rnd} acks")
+        assert_elems_equal(rw_g, rw_o, f"round {rnd} acks rw")
+        assert_tables_equal(g, o, f"round {rnd} acks")
+        # vals
+        val = gen.vals(rng, pool, W * M, sizes, rmw, tsp)
+        val_o = gen.bytecopy(val)
+        _run_both(g, o, L.BatchType.vals, val, val_o, mb, W, M, None)
+        assert_elems_equal(val, val_o, f"round {rnd} vals")
+        assert_tables_equal(g, o, f"round {rnd} vals")
+        # completion after a membership change
+        if rnd >= 9:
+            mem = gen.memb_ops(rng, pool, W * S, sizes, rmw, tsp)
+            mem_o = gen.bytecopy(mem)
+            _run_both(g, o, L.BatchType.local_ops_after_membership_change, mem, mem_o, mb_fail, W, S, None)
+            assert_elems_equal(mem, mem_o, f"round {rnd} membership")
+            assert_tables_equal(g, o, f"round {rnd} membership")
+
+
+def test_empty_and_all_miss_batches():
+    g, o, sizes = make_pair(500, 256, 1 << 16)
+    keys = gen_keys(500)
+    mb = L.membership(3, 0)
+    # zero-length batches are no-ops
+    e = np.zeros(4, dtype=L.op_dtype())
+    g.batch_host(L.BatchType.local_ops, e, mb, n_batches=4, stride=1, counts=np.zeros(4, np.int32))
+    assert (e["state"] == 0).all()
+    # elements whose keys are absent: ST_MISS in byte 9 of every element type
+    rng = np.random.default_rng(3)
+    for bt, msg in ((L.BatchType.local_ops, False), (L.BatchType.invs, False), (L.BatchType.acks, True),
+                    (L.BatchType.vals, True)):
+        a = np.zeros(64, dtype=L.msg_dtype() if msg else L.op_dtype())
+        a["key"] = rng.integers(1, 2**63, size=64, dtype=np.int64).astype(np.uint64)
+        a["opcode"] = {0: 111, 2: 114, 3: 115, 4: 116}[int(bt)]
+        b = gen.bytecopy(a)
+        g.batch_host(bt, a, mb)
+        o.batch(bt, b, mb)
+        assert_elems_equal(a, b, f"miss {bt}")
+        assert (a.view(np.uint8).reshape(64, -1)[:, 9] == int(L.Resp.MISS)).all()
+    assert_tables_equal(g, o, "misses")
+    del keys, sizes
+
+
+def test_max_size_batches_single_hot_key():
+    """Maximum batch sizes (250 local / 900 msg per worker) all on one key: one long segment."""
+    g, o, sizes = make_pair(1000, 1024, 1 << 17)
+    keys = gen_keys(1000)
+    rng = np.random.default_rng(7)
+    tsp = gen.TsPool(rng)
+    pool = keys[[17]]
+    mb = L.membership(3, 0)
+    W = 8
+    loc = gen.local_ops(rng, pool, W * 250, sizes, False, tsp)
+    loc_o = gen.bytecopy(loc)
+    _run_both(g, o, L.BatchType.local_ops, loc, loc_o, mb, W, 250, None)
+    assert_elems_equal(loc, loc_o, "hot local")
+    gen.harvest_ts(tsp, loc)
+    inv = gen.invs(rng, pool, W * 900, sizes, False, tsp, machine_num=3)
+    inv_o = gen.bytecopy(inv)
+    _run_both(g, o, L.BatchType.invs, inv, inv_o, mb, W, 900, None)
+    assert_elems_equal(inv, inv_o, "hot invs")
+    ack = gen.acks(rng, pool, W * 900, sizes, False, tsp, machine_num=3)
+    ack_o = gen.bytecopy(ack)
+    rw_g, rw_o = gen.bytecopy(loc), gen.bytecopy(loc)
+    _run_both(g, o, L.BatchType.acks, ack, ack_o, mb, W, 900, None, rw_g, rw_o, rw_stride=250)
+    assert_elems_equal(ack, ack_o, "hot acks")
+    assert_elems_equal(rw_g, rw_o, "hot rw")
+    assert_tables_equal(g, o, "hot")
+
+
+def test_hash_ids_matches_oracle():
+    from hermes_amd.kvs import hash_ids
+    ids = np.concatenate([np.arange(0, 5000), np.array([631343, 2**31 - 1, 99_999_999])]).astype(np.int32)
+    got = hash_ids(torch.from_numpy(ids).cuda()).cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(got[:5000], gen_keys(5000))
+    from oracle.oracle import cityhash128
+    for k, i in enumerate(ids[5000:]):
+        assert got[5000 + k] == cityhash128(int(i).to_bytes(4, "little"))[1]

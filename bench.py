@@ -66,6 +66,11 @@ def main():
     t_pop = time.time() - t0
     z = zipf_params(a.keys, a.zipf)
     total_steps = a.warmup + a.steps
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_seconds > 0:
+        # CPU baseline first, on the freshly populated table image (copied out of HBM)
+        from oracle.cpu_baseline import run_cpu_baseline
+        cpu = run_cpu_baseline(kvs, z, a.write_permille, a.cpu_workers, a.cpu_seconds, a.seed)
 
     if world > 1:
         from hermes_amd.replica_group import ReplicaGroupRound
@@ -154,9 +159,8 @@ def main():
             "step_bytes_per_committed_op_model": 554,
         },
     }
-    if rank == 0 and world == 1 and a.cpu_seconds > 0:
-        from oracle.cpu_baseline import run_cpu_baseline
-        out["cpu_baseline"] = run_cpu_baseline(kvs, z, a.write_permille, a.cpu_workers, a.cpu_seconds, a.seed)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -21,7 +21,6 @@ struct Meta {        // spacetime_object_meta (spacetime.h:138-148) + log val_le
     uint32_t ver;    // 24..27: ts.version
     uint32_t llw_ver;
     uint8_t llw_cid;
-    uint8_t b32_dirty;  // (unused flag slot, keeps the struct 4-byte aligned)
 };
 
 __device__ __forceinline__ uint32_t ld32(const uint8_t *p) { return *reinterpret_cast<const uint32_t *>(p); }
@@ -314,6 +313,62 @@ __device__ __forceinline__ void dispatch(int type, uint8_t *x, uint8_t *entry, u
     case kVals: exec_val(x, m); break;
     default: break;
     }
+}
+
+// Sound over-approximation of "executing element x on an entry whose meta is m would change
+// m". When it returns false, dispatch() provably leaves m untouched (it may still write the
+// element and, for GET/INV-abort, read the entry value). The long-segment engine relies on
+// exactly this: non-candidates are resolved in parallel against one snapshot of the meta,
+// candidates are applied one at a time in element order.
+__device__ __forceinline__ bool would_mutate(int type, const uint8_t *x, const Meta &m, const Ctx &c)
+{
+    const uint8_t st = m_state(m);
+    const bool obi_empty = m_obi(m) == kObiEmpty;
+    const uint8_t lw = m_lwid(m);
+    const bool lw_alive = lw < 8 && ((c.g_membership >> lw) & 1u);
+    const uint64_t cur = pack_ts(m.ver, m_cid(m));
+    switch (type) {
+    case kLocal: {
+        const uint8_t oc = x[8];
+        if (oc == kOpGet) return st == kInvalid && !lw_alive && obi_empty;              // replay
+        if (oc == kOpPut) return (st == kValid || st == kInvalid) && obi_empty;         // write
+        if (oc == kOpRmw && c.g.rmw_enabled) {
+            if (x[9] == kInProgressRmw) {                                               // abort + obi clear
+                uint64_t ots = e_ts(x);
+                return ots < cur && ots == pack_ts(m.llw_ver, m.llw_cid);
+            }
+            return obi_empty && (st == kValid || (st == kInvalid && !lw_alive));
+        }
+        return false;
+    }
+    case kLocalAfterMemb: {
+        bool eligible = x[8] == kOpPut || x[8] == kOpRmw || x[9] == kInProgressReplay;
+        return eligible && is_last_ack(m_ack_bv(m), c) &&
+               (!obi_empty || st == kInvalidWrite || st == kWrite || st == kReplay);
+    }
+    case kAcks:
+        if (!c.g.rmw_enabled || x[8] == kOpAck) {
+            if (e_ts(x) != pack_ts(m.llw_ver, m.llw_cid) || obi_empty) return false;
+            uint8_t s = x[9];
+            uint8_t nb = (uint8_t)(m_ack_bv(m) | (s < 8 ? (1u << s) : 0u));
+            return nb != m_ack_bv(m) || is_last_ack(nb, c);
+        }
+        if (x[8] != kOpInvAbort) return false;
+        // an INV-abort element runs hermes_exec_inv: fall through
+        [[fallthrough]];
+    case kInvs: {
+        uint64_t its = e_ts(x);
+        return its > cur || (its == cur && lw != (x[9] & 0x7Fu));
+    }
+    case kVals: return e_ts(x) == cur && st != kValid;
+    default: return true;
+    }
+}
+
+__device__ __forceinline__ bool meta_equal(const Meta &a, const Meta &b)
+{
+    return a.w4 == b.w4 && (a.w5 & 0xFF00FFFFu) == (b.w5 & 0xFF00FFFFu) && a.ver == b.ver &&
+           a.llw_ver == b.llw_ver && a.llw_cid == b.llw_cid;
 }
 
 // hermes_skip_dispatcher, hermesKV.c:709-769 (the INV membership-change side effect is

@@ -19,6 +19,8 @@ struct BatchLaunch {
     int32_t *ns_idx;
     int32_t *node_suspected;
     uint32_t *keys_a, *keys_b, *vals_a, *vals_b;
+    uint32_t *long_start, *long_len, *long_count;  // hot-key work list (k_segment_exec -> k_long_exec)
+    unsigned int *error_flags;                       // checked builds: unsound would_mutate()
     void *sort_tmp;
     size_t sort_tmp_bytes;
     int64_t n;

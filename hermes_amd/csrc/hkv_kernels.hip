@@ -118,6 +118,9 @@ __global__ __launch_bounds__(256) void k_lookup(LookupArgs a)
 
 // ------------------------------------------------------------------ batch stage 3: segments
 struct SegmentArgs {
+    uint32_t *long_start;
+    uint32_t *long_len;
+    uint32_t *long_count;
     uint8_t *elems;
     uint8_t *log;
     uint8_t *rw;
@@ -134,6 +137,10 @@ struct SegmentArgs {
     uint8_t w_ack_init;
 };
 
+// Segments of at most kShortSeg elements are applied serially by their owner lane; longer
+// ones (hot keys) are handed to k_long_exec through a compact work list.
+constexpr int kShortSeg = 24;
+
 template <int SV>
 __global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
 {
@@ -142,6 +149,26 @@ __global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
     uint32_t key = a.keys[p];
     if (key == a.skip_key) return;
     if (p > 0 && a.keys[p - 1] == key) return;  // not the segment head
+    if (p + kShortSeg < a.n && a.keys[p + kShortSeg] == key) {
+        // long segment: gallop to its end on the sorted keys, then queue it
+        int64_t lo = p + kShortSeg, step = 2 * kShortSeg, hi;
+        for (;;) {
+            hi = lo + step;
+            if (hi >= a.n || a.keys[hi] != key) break;
+            lo = hi;
+            step *= 2;
+        }
+        if (hi > a.n) hi = a.n;
+        while (hi - lo > 1) {  // keys[lo] == key, keys[hi] != key (or hi == n)
+            int64_t mid = (lo + hi) / 2;
+            if (a.keys[mid] == key) lo = mid;
+            else hi = mid;
+        }
+        uint32_t slot = atomicAdd(a.long_count, 1u);
+        a.long_start[slot] = (uint32_t)p;
+        a.long_len[slot] = (uint32_t)(hi - p);
+        return;
+    }
     uint8_t *entry = a.log + (uint64_t)key * a.g.entry_unit;
     Meta m;
     meta_load(entry, m);
@@ -157,6 +184,104 @@ __global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
         dispatch<SV>(a.type, a.elems + (int64_t)gi * a.esz, entry, (uint8_t)idx, m, c);
     }
     meta_store(entry, m);
+}
+
+__device__ __forceinline__ int block_min_256(int v, int *lds4)
+{
+    for (int o = 32; o > 0; o >>= 1) {
+        int u = __shfl_xor(v, o, 64);
+        v = u < v ? u : v;
+    }
+    if ((threadIdx.x & 63) == 0) lds4[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int r = lds4[0];
+    for (int w = 1; w < 4; ++w) r = lds4[w] < r ? lds4[w] : r;
+    return r;
+}
+
+// One 256-thread workgroup per long segment (one hot key), in chunks of 256 elements.
+// Per chunk, repeat: every unresolved element asks would_mutate() against the shared meta;
+// the first candidate f is found with a block min; elements before f are resolved in parallel,
+// each running the serial exec function on a private copy of the meta (it cannot change it);
+// after a barrier, f alone runs the exec function on the shared meta. A chunk without a
+// candidate takes one pass, so a hot key costs one pass per 256 elements plus one per
+// mutation. In checked builds, a non-candidate that did change its copy sets bit 0 of
+// *error_flags (the predicate would be unsound).
+struct LongArgs {
+    uint8_t *elems;
+    uint8_t *log;
+    uint8_t *rw;
+    const uint32_t *keys;
+    const uint32_t *vals;
+    const uint32_t *long_start;
+    const uint32_t *long_len;
+    const uint32_t *long_count;
+    unsigned int *error_flags;
+    Geometry g;
+    int64_t rw_stride;
+    int32_t stride;
+    int32_t esz;
+    int32_t type;
+    uint8_t g_membership;
+    uint8_t w_ack_init;
+};
+
+template <int SV>
+__global__ __launch_bounds__(256) void k_long_exec(LongArgs a)
+{
+    __shared__ Meta sm;
+    __shared__ int red[4];
+    const int tid = threadIdx.x;
+    const uint32_t nseg = *a.long_count;
+    Ctx c;
+    c.g = a.g;
+    c.g_membership = a.g_membership;
+    c.w_ack_init = a.w_ack_init;
+    for (uint32_t s = blockIdx.x; s < nseg; s += gridDim.x) {
+        const uint32_t start = a.long_start[s], len = a.long_len[s];
+        const uint32_t key = a.keys[start];
+        uint8_t *entry = a.log + (uint64_t)key * a.g.entry_unit;
+        if (tid == 0) {
+            Meta m;
+            meta_load(entry, m);
+            sm = m;
+        }
+        __syncthreads();
+        for (uint32_t base = 0; base < len; base += 256) {
+            const bool have = base + tid < len;
+            uint8_t *x = nullptr;
+            uint8_t idx = 0;
+            if (have) {
+                uint32_t gi = a.vals[start + base + tid];
+                int32_t b = (int32_t)(gi / (uint32_t)a.stride);
+                idx = (uint8_t)(gi - (uint32_t)b * (uint32_t)a.stride);
+                c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
+                x = a.elems + (int64_t)gi * a.esz;
+            }
+            bool resolved = !have;
+            for (;;) {
+                Meta m = sm;
+                const bool cand = !resolved && would_mutate(a.type, x, m, c);
+                const int f = block_min_256(cand ? tid : 256, red);
+                if (!resolved && tid < f) {
+                    Meta t = m;
+                    dispatch<SV>(a.type, x, entry, idx, t, c);
+                    if (a.error_flags && !meta_equal(t, m)) atomicOr(a.error_flags, 1u);
+                    resolved = true;
+                }
+                __syncthreads();  // every read of the entry value precedes the mutation
+                if (tid == f) {
+                    dispatch<SV>(a.type, x, entry, idx, m, c);
+                    sm = m;
+                    resolved = true;
+                }
+                __syncthreads();
+                if (f >= 256) break;
+            }
+        }
+        if (tid == 0) meta_store(entry, sm);
+        __syncthreads();
+    }
 }
 
 __global__ void k_node_suspected(const uint8_t *elems, const int32_t *ns_idx, int32_t *out,
@@ -319,9 +444,40 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     sa.skip_key = bl.skip_key;
     sa.g_membership = bl.g_membership;
     sa.w_ack_init = bl.w_ack_init;
-    if (bl.g.st_value == 31) hipLaunchKernelGGL(k_segment_exec<31>, dim3(grid), dim3(256), 0, s, sa);
-    else if (bl.g.st_value == 287) hipLaunchKernelGGL(k_segment_exec<287>, dim3(grid), dim3(256), 0, s, sa);
-    else hipLaunchKernelGGL(k_segment_exec<0>, dim3(grid), dim3(256), 0, s, sa);
+    sa.long_start = bl.long_start;
+    sa.long_len = bl.long_len;
+    sa.long_count = bl.long_count;
+    if (hipMemsetAsync(bl.long_count, 0, sizeof(uint32_t), s) != hipSuccess) return -3;
+    LongArgs la2;
+    la2.elems = bl.elems;
+    la2.log = bl.log;
+    la2.rw = bl.rw;
+    la2.keys = bl.keys_b;
+    la2.vals = bl.vals_b;
+    la2.long_start = bl.long_start;
+    la2.long_len = bl.long_len;
+    la2.long_count = bl.long_count;
+    la2.error_flags = bl.error_flags;
+    la2.g = bl.g;
+    la2.rw_stride = bl.rw_stride;
+    la2.stride = bl.stride;
+    la2.esz = bl.esz;
+    la2.type = bl.type;
+    la2.g_membership = bl.g_membership;
+    la2.w_ack_init = bl.w_ack_init;
+    // a segment longer than kShortSeg needs kShortSeg + 1 elements: cap the long-exec grid
+    int64_t max_long = n / (kShortSeg + 1) + 1;
+    const unsigned lgrid = (unsigned)(max_long < 1024 ? max_long : 1024);
+    if (bl.g.st_value == 31) {
+        hipLaunchKernelGGL(k_segment_exec<31>, dim3(grid), dim3(256), 0, s, sa);
+        hipLaunchKernelGGL(k_long_exec<31>, dim3(lgrid), dim3(256), 0, s, la2);
+    } else if (bl.g.st_value == 287) {
+        hipLaunchKernelGGL(k_segment_exec<287>, dim3(grid), dim3(256), 0, s, sa);
+        hipLaunchKernelGGL(k_long_exec<287>, dim3(lgrid), dim3(256), 0, s, la2);
+    } else {
+        hipLaunchKernelGGL(k_segment_exec<0>, dim3(grid), dim3(256), 0, s, sa);
+        hipLaunchKernelGGL(k_long_exec<0>, dim3(lgrid), dim3(256), 0, s, la2);
+    }
     if (hipGetLastError() != hipSuccess) return -3;
     if (bl.type == kInvs && bl.ns_idx && bl.node_suspected) {
         hipLaunchKernelGGL(k_node_suspected, dim3((bl.n_batches + 255) / 256), dim3(256), 0, s, bl.elems,

@@ -31,6 +31,8 @@ struct hkv_table {
     int key_bits = 0;
     // batch scratch
     uint32_t *d_keys_a = nullptr, *d_keys_b = nullptr, *d_vals_a = nullptr, *d_vals_b = nullptr;
+    uint32_t *d_long = nullptr;        // [count | starts... | lens...] hot-key work list
+    unsigned int *d_error_flags = nullptr;
     int64_t scratch_n = 0;
     void *d_sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
@@ -135,12 +137,14 @@ static int ensure_scratch(hkv_table *t, int64_t n, int key_bits)
         hipFree(t->d_keys_b);
         hipFree(t->d_vals_a);
         hipFree(t->d_vals_b);
-        t->d_keys_a = t->d_keys_b = t->d_vals_a = t->d_vals_b = nullptr;
+        hipFree(t->d_long);
+        t->d_keys_a = t->d_keys_b = t->d_vals_a = t->d_vals_b = t->d_long = nullptr;
         t->scratch_n = 0;
         HIP_TRY(hipMalloc(&t->d_keys_a, cap * 4));
         HIP_TRY(hipMalloc(&t->d_keys_b, cap * 4));
         HIP_TRY(hipMalloc(&t->d_vals_a, cap * 4));
         HIP_TRY(hipMalloc(&t->d_vals_b, cap * 4));
+        HIP_TRY(hipMalloc(&t->d_long, (2 * (cap / 16 + 2) + 64) * 4));
         t->scratch_n = cap;
     }
     size_t need = sort_temp_bytes(t->scratch_n, key_bits > 0 ? key_bits : 32);
@@ -207,6 +211,8 @@ int hkv_table_create(const hkv_config *cfg, hkv_table **out)
         if (hipMalloc(&t->d_index, t->cfg.num_bkts * 64) != hipSuccess) { rc = fail(-6, "index alloc %llu B", (unsigned long long)(t->cfg.num_bkts * 64)); break; }
         if (hipMalloc(&t->d_log, t->cfg.log_cap + t->geo.entry_size) != hipSuccess) { rc = fail(-6, "log alloc %llu B", (unsigned long long)t->cfg.log_cap); break; }
         if (hipMalloc(&t->d_evictions, sizeof(unsigned long long)) != hipSuccess) { rc = fail(-6, "alloc"); break; }
+        if (hipMalloc(&t->d_error_flags, sizeof(unsigned int)) != hipSuccess) { rc = fail(-6, "alloc"); break; }
+        if (hipMemsetAsync(t->d_error_flags, 0, sizeof(unsigned int), t->stream) != hipSuccess) { rc = fail(-5, "memset"); break; }
         if (hipMemsetAsync(t->d_index, 0, t->cfg.num_bkts * 64, t->stream) != hipSuccess) { rc = fail(-5, "memset"); break; }
         if (hipMemsetAsync(t->d_log, 0, t->cfg.log_cap + t->geo.entry_size, t->stream) != hipSuccess) { rc = fail(-5, "memset"); break; }
         if (hipMemsetAsync(t->d_evictions, 0, sizeof(unsigned long long), t->stream) != hipSuccess) { rc = fail(-5, "memset"); break; }
@@ -231,6 +237,8 @@ int hkv_table_destroy(hkv_table *t)
     hipFree(t->d_keys_b);
     hipFree(t->d_vals_a);
     hipFree(t->d_vals_b);
+    hipFree(t->d_long);
+    hipFree(t->d_error_flags);
     hipFree(t->d_sort_tmp);
     hipFree(t->d_ns_idx);
     hipFree(t->d_stage_ops);
@@ -312,7 +320,7 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     int64_t n = (int64_t)d->n_batches * d->stride;
     if (n == 0) return 0;
     if (n > 0x7FFFFFFFll) return fail(-1, "too many elements in one launch");
-    hipStream_t s = stream ? (hipStream_t)stream : t->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream, as in every HIP API
     int rc = ensure_scratch(t, n, t->key_bits);
     if (rc) return rc;
     int32_t *ns_idx = nullptr;
@@ -344,6 +352,10 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.vals_b = t->d_vals_b;
     bl.sort_tmp = t->d_sort_tmp;
     bl.sort_tmp_bytes = t->sort_tmp_bytes;
+    bl.long_count = t->d_long;
+    bl.long_start = t->d_long + 64;
+    bl.long_len = t->d_long + 64 + (t->scratch_n / 16 + 2);
+    bl.error_flags = t->d_error_flags;
     bl.n = n;
     bl.n_batches = d->n_batches;
     bl.stride = d->stride;
@@ -362,7 +374,8 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
 int hkv_sync(hkv_table *t, void *stream)
 {
     if (!t) return fail(-1, "null table");
-    HIP_TRY(hipStreamSynchronize(stream ? (hipStream_t)stream : t->stream));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(hipStreamSynchronize(t->stream));
     return 0;
 }
 
@@ -395,6 +408,15 @@ int64_t hkv_num_index_evictions(const hkv_table *t)
 }
 
 void *hkv_device_index(hkv_table *t) { return t ? t->d_index : nullptr; }
+
+int hkv_take_error_flags(hkv_table *t, uint32_t *out)
+{
+    if (!t || !out) return fail(-1, "null argument");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, t->d_error_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(t->d_error_flags, 0, sizeof(uint32_t)));
+    return 0;
+}
 void *hkv_device_log(hkv_table *t) { return t ? t->d_log : nullptr; }
 
 int hkv_hash_ids(const uint32_t *d_ids, uint64_t *d_keys_second, int64_t n, void *stream)

@@ -191,6 +191,12 @@ class HermesKV:
         if node_suspected is not None:
             node_suspected[:] = tn.cpu().numpy()
 
+    def take_error_flags(self) -> int:
+        """Internal-consistency flags raised by the device path since the last call (0 = none)."""
+        v = ctypes.c_uint32(0)
+        check(_L.hkv_take_error_flags(self.h, ctypes.byref(v)), "hkv_take_error_flags")
+        return v.value
+
     def sync(self) -> None:
         check(_L.hkv_sync(self.h, None), "hkv_sync")
 

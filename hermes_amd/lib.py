@@ -63,6 +63,7 @@ _L.hkv_num_index_evictions.restype = ctypes.c_int64
 _L.hkv_num_index_evictions.argtypes = [_P]
 _L.hkv_device_index.restype = _P
 _L.hkv_device_index.argtypes = [_P]
+_L.hkv_take_error_flags.argtypes = [_P, ctypes.POINTER(ctypes.c_uint32)]
 _L.hkv_device_log.restype = _P
 _L.hkv_device_log.argtypes = [_P]
 _L.hkv_set_default_config.argtypes = [ctypes.POINTER(HkvConfig)]

@@ -19,7 +19,7 @@
  * reference applied to the batches one after another (concatenation order).
  *
  * Plain pointers and sizes only; no HIP or torch types appear in any signature
- * (streams are passed as void* and interpreted as hipStream_t, NULL = the table's stream).
+ * (streams are passed as void* and interpreted as hipStream_t; NULL is the HIP null stream).
  */
 #ifndef HERMESKV_H
 #define HERMESKV_H
@@ -126,7 +126,8 @@ int  hkv_table_destroy(hkv_table *t);
 int  hkv_table_populate(hkv_table *t, int64_t n, int val_len);
 int  hkv_table_config(const hkv_table *t, hkv_config *out);
 
-/* device-resident batch path; stream may be NULL (the table's own stream) */
+/* device-resident batch path, asynchronous on `stream` (NULL = the HIP null stream). One
+ * stream at a time per table: launches share the table's sort scratch. */
 int  hkv_batch_async(hkv_table *t, const hkv_batch_desc *desc, void *stream);
 int  hkv_sync(hkv_table *t, void *stream);
 
@@ -136,6 +137,9 @@ int  hkv_copy_log(hkv_table *t, void *host_dst, uint64_t offset, uint64_t bytes)
 uint64_t hkv_log_head(const hkv_table *t);
 int64_t  hkv_num_index_evictions(const hkv_table *t);
 void *hkv_device_index(hkv_table *t);
+/* internal-consistency flags raised by the device path since the last call (0 = none);
+ * bit 0: the hot-key engine saw a non-candidate element change the entry meta */
+int  hkv_take_error_flags(hkv_table *t, uint32_t *out);
 void *hkv_device_log(hkv_table *t);
 
 /* default table used by the reference entry points */

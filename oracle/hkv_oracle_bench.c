@@ -85,13 +85,14 @@ int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, doub
         tkey[g] = key_of(id);
         top[g] = (uint32_t)(r2 % 1000u) < write_pm ? OPC_PUT : OPC_GET;
     }
-    /* peer INVs + VALs, P rounds deep, timestamps 2*(round + 1 + coin) */
+    /* peer INVs + VALs, P rounds deep; the version field holds the coin until use, when it
+     * becomes 2*(round + 1 + coin) -- the same peer clock as the GPU run */
     for (int64_t g = 0; g < (int64_t)n_workers * P * rstride; g++) {
         int64_t k = g / ((int64_t)n_workers * rstride);
         int r = (int)((g / per_peer) % n_peers);
         uint64_t r1 = sm64(seed ^ ((uint64_t)k << 40) ^ (0x9E37ull * (uint64_t)g));
         uint32_t id = (uint32_t)zipf_draw(z, (double)(r1 >> 11) * (1.0 / 9007199254740992.0));
-        uint32_t ver = 2u * ((uint32_t)k + 1u + (uint32_t)((r1 >> 7) & 1u));
+        uint32_t ver = (uint32_t)((r1 >> 7) & 1u);
         uint8_t peer = (uint8_t)(1 + r);
         uint8_t *x = rinv_pool + g * osz, *v = rval_pool + g * 16;
         uint64_t key = key_of(id);
@@ -148,6 +149,13 @@ int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, doub
                 size_t k = (size_t)(rounds % P) * n_workers + w;
                 memcpy(rinv, rinv_pool + k * rstride * osz, (size_t)rstride * osz);
                 memcpy(rval, rval_pool + k * rstride * 16, (size_t)rstride * 16);
+                for (int i = 0; i < rstride; i++) {
+                    uint32_t coin, ver;
+                    memcpy(&coin, rinv + (size_t)i * osz + 12, 4);
+                    ver = 2u * ((uint32_t)rounds + 1u + coin);
+                    memcpy(rinv + (size_t)i * osz + 12, &ver, 4);
+                    memcpy(rval + (size_t)i * 16 + 12, &ver, 4);
+                }
                 int ns = -1;
                 hko_batch(kv, 2, rinv, rstride, (uint16_t)osz, membership, &ns, NULL);
                 for (int i = 0; i < rstride; i++) { /* ACKs back to the peers */

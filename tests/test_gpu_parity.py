@@ -49,6 +49,7 @@ def assert_tables_equal(g, o, what=""):
         pytest.fail(f"{what}: log differs at {len(bad)} bytes; entries {np.unique(bad // e)[:8]} "
                     f"offsets-in-entry {np.unique(bad % e)[:16]}")
     assert g.log_head == o.log_head(), what
+    assert g.take_error_flags() == 0, f"{what}: device consistency flags raised"
 
 
 def assert_elems_equal(a, b, what):
@@ -244,31 +245,67 @@ def test_empty_and_all_miss_batches():
     del keys, sizes
 
 
-def test_max_size_batches_single_hot_key():
-    """Maximum batch sizes (250 local / 900 msg per worker) all on one key: one long segment."""
-    g, o, sizes = make_pair(1000, 1024, 1 << 17)
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_max_size_batches_single_hot_key(cfg):
+    """Maximum batch sizes (250 local / 900 msg per worker) all on one or two keys: every batch
+    type goes through the hot-key workgroup engine (segments far longer than kShortSeg)."""
+    rmw, big = cfg["rmw"], cfg["big"]
+    g, o, sizes = make_pair(1000, 1024, 1 << 19 if big else 1 << 17, rmw=rmw, big=big)
     keys = gen_keys(1000)
     rng = np.random.default_rng(7)
     tsp = gen.TsPool(rng)
-    pool = keys[[17]]
     mb = L.membership(3, 0)
     W = 8
-    loc = gen.local_ops(rng, pool, W * 250, sizes, False, tsp)
-    loc_o = gen.bytecopy(loc)
-    _run_both(g, o, L.BatchType.local_ops, loc, loc_o, mb, W, 250, None)
-    assert_elems_equal(loc, loc_o, "hot local")
-    gen.harvest_ts(tsp, loc)
-    inv = gen.invs(rng, pool, W * 900, sizes, False, tsp, machine_num=3)
+    for rnd, pool in enumerate((keys[[17]], keys[[17, 18]], keys[[17]])):
+        loc = gen.local_ops(rng, pool, W * 250, sizes, rmw, tsp)
+        loc_o = gen.bytecopy(loc)
+        _run_both(g, o, L.BatchType.local_ops, loc, loc_o, mb, W, 250, None)
+        assert_elems_equal(loc, loc_o, f"hot local {rnd}")
+        gen.harvest_ts(tsp, loc)
+        inv = gen.invs(rng, pool, W * 900, sizes, rmw, tsp, machine_num=3)
+        inv_o = gen.bytecopy(inv)
+        ns_g = np.full(W, -1, np.int32)
+        ns_o = ns_g.copy()
+        _run_both(g, o, L.BatchType.invs, inv, inv_o, mb, W, 900, None, ns_g=ns_g, ns_o=ns_o)
+        assert_elems_equal(inv, inv_o, f"hot invs {rnd}")
+        np.testing.assert_array_equal(ns_g, ns_o)
+        ack = gen.acks(rng, pool, W * 900, sizes, rmw, tsp, machine_num=3)
+        ack_o = gen.bytecopy(ack)
+        rw_g, rw_o = gen.bytecopy(loc), gen.bytecopy(loc)
+        _run_both(g, o, L.BatchType.acks, ack, ack_o, mb, W, 900, None, rw_g, rw_o, rw_stride=250)
+        assert_elems_equal(ack, ack_o, f"hot acks {rnd}")
+        assert_elems_equal(rw_g, rw_o, f"hot rw {rnd}")
+        val = gen.vals(rng, pool, W * 900, sizes, rmw, tsp, machine_num=3)
+        val_o = gen.bytecopy(val)
+        _run_both(g, o, L.BatchType.vals, val, val_o, mb, W, 900, None)
+        assert_elems_equal(val, val_o, f"hot vals {rnd}")
+        mem = gen.memb_ops(rng, pool, W * 250, sizes, rmw, tsp)
+        mem_o = gen.bytecopy(mem)
+        _run_both(g, o, L.BatchType.local_ops_after_membership_change, mem, mem_o,
+                  L.membership(3, 0, alive=0b011), W, 250, None)
+        assert_elems_equal(mem, mem_o, f"hot membership {rnd}")
+        assert_tables_equal(g, o, f"hot {rnd}")
+
+
+def test_adversarial_inv_alternating_equal_timestamps():
+    """Equal-timestamp INVs from alternating senders: every one rewrites last_writer_id, so the
+    hot-key engine has one candidate per element (its slowest case) and must stay exact."""
+    g, o, sizes = make_pair(500, 512, 1 << 16)
+    keys = gen_keys(500)
+    mb = L.membership(3, 0)
+    n = 4 * 900
+    inv = np.zeros(n, dtype=L.op_dtype())
+    inv["key"] = keys[3]
+    inv["opcode"] = int(L.Op.INV)
+    inv["state"] = np.arange(n) % 3
+    inv["ts_ver"] = 2 * (1 + (np.arange(n) // 1000))
+    inv["ts_cid"] = 1
+    inv["val_len"] = 31
+    inv["value"] = (np.arange(n) % 251)[:, None]
     inv_o = gen.bytecopy(inv)
-    _run_both(g, o, L.BatchType.invs, inv, inv_o, mb, W, 900, None)
-    assert_elems_equal(inv, inv_o, "hot invs")
-    ack = gen.acks(rng, pool, W * 900, sizes, False, tsp, machine_num=3)
-    ack_o = gen.bytecopy(ack)
-    rw_g, rw_o = gen.bytecopy(loc), gen.bytecopy(loc)
-    _run_both(g, o, L.BatchType.acks, ack, ack_o, mb, W, 900, None, rw_g, rw_o, rw_stride=250)
-    assert_elems_equal(ack, ack_o, "hot acks")
-    assert_elems_equal(rw_g, rw_o, "hot rw")
-    assert_tables_equal(g, o, "hot")
+    _run_both(g, o, L.BatchType.invs, inv, inv_o, mb, 4, 900, None)
+    assert_elems_equal(inv, inv_o, "alternating invs")
+    assert_tables_equal(g, o, "alternating invs")
 
 
 def test_hash_ids_matches_oracle():

@@ -40,6 +40,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (0 = skip)")
     p.add_argument("--cpu-workers", type=int, default=64)
     p.add_argument("--seed", type=int, default=0x5EED)
+    p.add_argument("--retry", action="store_true",
+                   help="refill_ops semantics: stalled ops keep their slot (default: fresh batch per step)")
     return p.parse_args()
 
 
@@ -70,14 +72,15 @@ def main():
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
         # CPU baseline first, on the freshly populated table image (copied out of HBM)
         from oracle.cpu_baseline import run_cpu_baseline
-        cpu = run_cpu_baseline(kvs, z, a.write_permille, a.cpu_workers, a.cpu_seconds, a.seed)
+        cpu = run_cpu_baseline(kvs, z, a.write_permille, a.cpu_workers, a.cpu_seconds, a.seed,
+                               refill_all=not a.retry)
 
     if world > 1:
         from hermes_amd.replica_group import ReplicaGroupRound
         rnd = ReplicaGroupRound(kvs, a.workers, z, a.write_permille, seed=a.seed, world=world, rank=rank)
     else:
         rnd = Round(kvs, a.workers, L.membership(3, 0), [1, 2], z, a.write_permille, seed=a.seed,
-                    max_steps=total_steps + 1)
+                    max_steps=total_steps + 1, retry_stalled=a.retry)
     torch.cuda.synchronize()
 
     for _ in range(a.warmup):

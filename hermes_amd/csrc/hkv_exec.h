@@ -73,15 +73,38 @@ __device__ __forceinline__ void e_set_ts(uint8_t *x, uint32_t ver, uint8_t cid) 
 __device__ __forceinline__ uint8_t e_rmw(const uint8_t *x) { return x[16] & 1u; }
 __device__ __forceinline__ void e_set_rmw(uint8_t *x, uint8_t f) { x[16] = (uint8_t)((x[16] & 0xFEu) | (f & 1u)); }
 
+// Byte-exact copy between the op value (offset 18) and the log value (offset 33): the two
+// never share an alignment, so the middle moves as aligned dwords built with v_alignbyte from
+// the aligned source dwords that overlap the range (both objects are 8-byte aligned and a
+// multiple of 8 long, so no dword outside the source object is touched), and only the < 4
+// head/tail bytes move one by one.
+__device__ __forceinline__ void copy_bytes(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint32_t n)
+{
+    uint32_t head = (4u - ((uint32_t)(uintptr_t)dst & 3u)) & 3u;
+    if (head > n) head = n;
+    for (uint32_t k = 0; k < head; ++k) dst[k] = src[k];
+    const uint8_t *s = src + head;
+    const uint32_t sh = (uint32_t)(uintptr_t)s & 3u;
+    const uint32_t *sa = reinterpret_cast<const uint32_t *>((uintptr_t)s & ~(uintptr_t)3);
+    uint32_t *da = reinterpret_cast<uint32_t *>(dst + head);
+    const uint32_t nw = (n - head) >> 2;
+    if (sh == 0) {
+        for (uint32_t j = 0; j < nw; ++j) da[j] = sa[j];
+    } else {
+        uint32_t lo = nw ? sa[0] : 0u;
+        for (uint32_t j = 0; j < nw; ++j) {
+            uint32_t hi = sa[j + 1];
+            da[j] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+            lo = hi;
+        }
+    }
+    for (uint32_t k = head + 4 * nw; k < n; ++k) dst[k] = src[k];
+}
+
 template <int SV>
 __device__ __forceinline__ void copy_value(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint32_t n)
 {
-    if (SV > 0) {
-#pragma unroll 8
-        for (int k = 0; k < SV; ++k) dst[k] = src[k];
-    } else {
-        for (uint32_t k = 0; k < n; ++k) dst[k] = src[k];
-    }
+    copy_bytes(dst, src, SV > 0 ? (uint32_t)SV : n);
 }
 
 struct Ctx {           // per-launch constants

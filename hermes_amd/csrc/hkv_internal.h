@@ -19,7 +19,8 @@ struct BatchLaunch {
     int32_t *ns_idx;
     int32_t *node_suspected;
     uint32_t *keys_a, *keys_b, *vals_a, *vals_b;
-    uint32_t *long_start, *long_len, *long_count;  // hot-key work list (k_segment_exec -> k_long_exec)
+    uint32_t *long_start, *long_len, *long_count;  // hot/mid segment work lists (k_segment_exec ->
+    uint32_t list_cap;                              //   k_long_exec / k_wave_exec), cap each
     unsigned int *error_flags;                       // checked builds: unsound would_mutate()
     void *sort_tmp;
     size_t sort_tmp_bytes;

@@ -18,7 +18,8 @@
 // bucket, one owner lane per bucket replays the MICA slot rules, entries are written in
 // parallel.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <cstring>
+#include <rocprim/rocprim.hpp>
 
 #include "hkv_exec.h"
 #include "hkv_internal.h"
@@ -118,9 +119,10 @@ __global__ __launch_bounds__(256) void k_lookup(LookupArgs a)
 
 // ------------------------------------------------------------------ batch stage 3: segments
 struct SegmentArgs {
-    uint32_t *long_start;
+    uint32_t *long_start;   // hot list: [0, cap)   mid list: [cap, 2*cap)
     uint32_t *long_len;
-    uint32_t *long_count;
+    uint32_t *long_count;   // [0] hot, [1] mid
+    uint32_t list_cap;
     uint8_t *elems;
     uint8_t *log;
     uint8_t *rw;
@@ -137,20 +139,45 @@ struct SegmentArgs {
     uint8_t w_ack_init;
 };
 
-// Segments of at most kShortSeg elements are applied serially by their owner lane; longer
-// ones (hot keys) are handed to k_long_exec through a compact work list.
-constexpr int kShortSeg = 24;
+// Three tiers by segment length: at most kShortSeg elements are applied serially by the
+// segment's owner lane (k_segment_exec); up to kMidSeg by one wavefront (k_wave_exec); longer
+// ones (the hottest keys) by a 1024-thread workgroup (k_long_exec). The last two receive their
+// segments through compact work lists written by k_segment_exec.
+constexpr int kShortSeg = 4;
+constexpr int kMidSeg = 4096;
 
-template <int SV>
+// Queue a segment on one of the two work lists with one atomic per wavefront and list
+// (a per-lane atomic on a shared counter serialises hundreds of thousands of heads).
+__device__ __forceinline__ void enqueue_segment(const SegmentArgs &a, bool want, int tier, uint32_t start,
+                                                uint32_t len)
+{
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const unsigned long long m = __ballot(want && tier == t);
+        if (!m) continue;
+        const int leader = __ffsll((long long)m) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&a.long_count[t], (uint32_t)__popcll(m));
+        base = __shfl(base, leader, 64);
+        if (want && tier == t) {
+            const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull)) + (uint32_t)t * a.list_cap;
+            a.long_start[slot] = start;
+            a.long_len[slot] = len;
+        }
+    }
+}
+
+template <int TYPE, int SV>
 __global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
 {
-    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.n) return;
-    uint32_t key = a.keys[p];
-    if (key == a.skip_key) return;
-    if (p > 0 && a.keys[p - 1] == key) return;  // not the segment head
-    if (p + kShortSeg < a.n && a.keys[p + kShortSeg] == key) {
-        // long segment: gallop to its end on the sorted keys, then queue it
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t key = p < a.n ? a.keys[p] : a.skip_key;
+    const bool head = key != a.skip_key && (p == 0 || a.keys[p - 1] != key);
+    const bool longseg = head && p + kShortSeg < a.n && a.keys[p + kShortSeg] == key;
+    uint32_t len = 0;
+    if (longseg) {
+        // gallop to the end of the segment on the sorted keys
         int64_t lo = p + kShortSeg, step = 2 * kShortSeg, hi;
         for (;;) {
             hi = lo + step;
@@ -164,11 +191,10 @@ __global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
             if (a.keys[mid] == key) lo = mid;
             else hi = mid;
         }
-        uint32_t slot = atomicAdd(a.long_count, 1u);
-        a.long_start[slot] = (uint32_t)p;
-        a.long_len[slot] = (uint32_t)(hi - p);
-        return;
+        len = (uint32_t)(hi - p);
     }
+    enqueue_segment(a, longseg, len > (uint32_t)kMidSeg ? 0 : 1, (uint32_t)p, len);
+    if (!head || longseg) return;
     uint8_t *entry = a.log + (uint64_t)key * a.g.entry_unit;
     Meta m;
     meta_load(entry, m);
@@ -181,32 +207,53 @@ __global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
         int32_t b = (int32_t)(gi / (uint32_t)a.stride);
         uint32_t idx = gi - (uint32_t)b * (uint32_t)a.stride;
         c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
-        dispatch<SV>(a.type, a.elems + (int64_t)gi * a.esz, entry, (uint8_t)idx, m, c);
+        dispatch<SV>(TYPE, a.elems + (int64_t)gi * a.esz, entry, (uint8_t)idx, m, c);
     }
     meta_store(entry, m);
 }
 
-__device__ __forceinline__ int block_min_256(int v, int *lds4)
+template <int NT>
+__device__ __forceinline__ int block_min(int v, int *lds)
 {
     for (int o = 32; o > 0; o >>= 1) {
         int u = __shfl_xor(v, o, 64);
         v = u < v ? u : v;
     }
-    if ((threadIdx.x & 63) == 0) lds4[threadIdx.x >> 6] = v;
+    if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
     __syncthreads();
-    int r = lds4[0];
-    for (int w = 1; w < 4; ++w) r = lds4[w] < r ? lds4[w] : r;
+    int r = lds[0];
+#pragma unroll
+    for (int w = 1; w < NT / 64; ++w) r = lds[w] < r ? lds[w] : r;
     return r;
 }
 
-// One 256-thread workgroup per long segment (one hot key), in chunks of 256 elements.
+__device__ __forceinline__ int wave_min(int v)
+{
+    for (int o = 32; o > 0; o >>= 1) {
+        int u = __shfl_xor(v, o, 64);
+        v = u < v ? u : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ void meta_bcast(Meta &m, int src)
+{
+    m.w4 = __shfl(m.w4, src, 64);
+    m.w5 = __shfl(m.w5, src, 64);
+    m.ver = __shfl(m.ver, src, 64);
+    m.llw_ver = __shfl(m.llw_ver, src, 64);
+    m.llw_cid = (uint8_t)__shfl((int)m.llw_cid, src, 64);
+}
+
+// One 1024-thread workgroup per long segment (one hot key), in chunks of kLongChunk elements
+// (kPerThread per lane, lane-strided so the sorted element ids are read coalesced).
 // Per chunk, repeat: every unresolved element asks would_mutate() against the shared meta;
 // the first candidate f is found with a block min; elements before f are resolved in parallel,
 // each running the serial exec function on a private copy of the meta (it cannot change it);
 // after a barrier, f alone runs the exec function on the shared meta. A chunk without a
-// candidate takes one pass, so a hot key costs one pass per 256 elements plus one per
-// mutation. In checked builds, a non-candidate that did change its copy sets bit 0 of
-// *error_flags (the predicate would be unsound).
+// candidate takes one pass, so a hot key costs one pass per kLongChunk elements plus one per
+// mutation. A non-candidate that did change its copy sets bit 0 of *error_flags (that would
+// mean would_mutate() is unsound).
 struct LongArgs {
     uint8_t *elems;
     uint8_t *log;
@@ -216,6 +263,7 @@ struct LongArgs {
     const uint32_t *long_start;
     const uint32_t *long_len;
     const uint32_t *long_count;
+    uint32_t list_cap;
     unsigned int *error_flags;
     Geometry g;
     int64_t rw_stride;
@@ -226,17 +274,22 @@ struct LongArgs {
     uint8_t w_ack_init;
 };
 
-template <int SV>
-__global__ __launch_bounds__(256) void k_long_exec(LongArgs a)
+constexpr int kLongThreads = 1024;
+constexpr int kPerThread = 8;
+constexpr int kLongChunk = kLongThreads * kPerThread;
+
+template <int TYPE, int SV>
+__global__ __launch_bounds__(kLongThreads) void k_long_exec(LongArgs a)
 {
     __shared__ Meta sm;
-    __shared__ int red[4];
+    __shared__ int red[kLongThreads / 64];
     const int tid = threadIdx.x;
-    const uint32_t nseg = *a.long_count;
+    const uint32_t nseg = a.long_count[0];
     Ctx c;
     c.g = a.g;
     c.g_membership = a.g_membership;
     c.w_ack_init = a.w_ack_init;
+    c.rw = nullptr;
     for (uint32_t s = blockIdx.x; s < nseg; s += gridDim.x) {
         const uint32_t start = a.long_start[s], len = a.long_len[s];
         const uint32_t key = a.keys[start];
@@ -247,40 +300,124 @@ __global__ __launch_bounds__(256) void k_long_exec(LongArgs a)
             sm = m;
         }
         __syncthreads();
-        for (uint32_t base = 0; base < len; base += 256) {
-            const bool have = base + tid < len;
-            uint8_t *x = nullptr;
-            uint8_t idx = 0;
-            if (have) {
-                uint32_t gi = a.vals[start + base + tid];
-                int32_t b = (int32_t)(gi / (uint32_t)a.stride);
-                idx = (uint8_t)(gi - (uint32_t)b * (uint32_t)a.stride);
-                c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
-                x = a.elems + (int64_t)gi * a.esz;
-            }
-            bool resolved = !have;
+        for (uint32_t base = 0; base < len; base += kLongChunk) {
+            uint32_t pending = 0;  // bit j: element base + j*kLongThreads + tid still to apply
+#pragma unroll
+            for (int j = 0; j < kPerThread; ++j)
+                if (base + j * kLongThreads + tid < len) pending |= 1u << j;
             for (;;) {
-                Meta m = sm;
-                const bool cand = !resolved && would_mutate(a.type, x, m, c);
-                const int f = block_min_256(cand ? tid : 256, red);
-                if (!resolved && tid < f) {
+                const Meta m = sm;
+                int mine = kLongChunk;
+#pragma unroll
+                for (int j = kPerThread - 1; j >= 0; --j) {
+                    if (!(pending >> j & 1u)) continue;
+                    const uint32_t gi = a.vals[start + base + j * kLongThreads + tid];
+                    if (would_mutate(TYPE, a.elems + (int64_t)gi * a.esz, m, c)) mine = j * kLongThreads + tid;
+                }
+                const int f = block_min<kLongThreads>(mine, red);
+#pragma unroll
+                for (int j = 0; j < kPerThread; ++j) {
+                    const int pos = j * kLongThreads + tid;
+                    if (!(pending >> j & 1u) || pos >= f) continue;
+                    const uint32_t gi = a.vals[start + base + pos];
+                    const int32_t b = (int32_t)(gi / (uint32_t)a.stride);
                     Meta t = m;
-                    dispatch<SV>(a.type, x, entry, idx, t, c);
+                    c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
+                    dispatch<SV>(TYPE, a.elems + (int64_t)gi * a.esz, entry,
+                                 (uint8_t)(gi - (uint32_t)b * (uint32_t)a.stride), t, c);
                     if (a.error_flags && !meta_equal(t, m)) atomicOr(a.error_flags, 1u);
-                    resolved = true;
+                    pending &= ~(1u << j);
                 }
                 __syncthreads();  // every read of the entry value precedes the mutation
-                if (tid == f) {
-                    dispatch<SV>(a.type, x, entry, idx, m, c);
-                    sm = m;
-                    resolved = true;
+                if (f < kLongChunk && (f % kLongThreads) == tid) {
+                    const int j = f / kLongThreads;
+                    const uint32_t gi = a.vals[start + base + f];
+                    const int32_t b = (int32_t)(gi / (uint32_t)a.stride);
+                    Meta mm = m;
+                    c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
+                    dispatch<SV>(TYPE, a.elems + (int64_t)gi * a.esz, entry,
+                                 (uint8_t)(gi - (uint32_t)b * (uint32_t)a.stride), mm, c);
+                    pending &= ~(1u << j);
+                    sm = mm;
                 }
                 __syncthreads();
-                if (f >= 256) break;
+                if (f >= kLongChunk) break;
             }
         }
         if (tid == 0) meta_store(entry, sm);
         __syncthreads();
+    }
+}
+
+// One wavefront per medium segment: the same first-candidate rounds as k_long_exec, in chunks
+// of 64 * kWavePer elements, with the meta replicated in every lane's registers (the owner of
+// a mutation broadcasts it by shuffles). Within a wavefront program order separates the
+// resolving lanes' entry-value reads from the mutation's writes, so no barrier is needed.
+constexpr int kWavePer = 4;
+
+template <int TYPE, int SV>
+__global__ __launch_bounds__(256) void k_wave_exec(LongArgs a)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t wid = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t nseg = a.long_count[1];
+    Ctx c;
+    c.g = a.g;
+    c.g_membership = a.g_membership;
+    c.w_ack_init = a.w_ack_init;
+    c.rw = nullptr;
+    for (uint32_t s = wid; s < nseg; s += gridDim.x * 4u) {
+        const uint32_t start = a.long_start[a.list_cap + s], len = a.long_len[a.list_cap + s];
+        const uint32_t key = a.keys[start];
+        uint8_t *entry = a.log + (uint64_t)key * a.g.entry_unit;
+        Meta m;
+        meta_load(entry, m);
+        for (uint32_t base = 0; base < len; base += 64 * kWavePer) {
+            uint32_t gis[kWavePer];
+            uint32_t pending = 0;
+#pragma unroll
+            for (int j = 0; j < kWavePer; ++j) {
+                const uint32_t pos = base + j * 64 + lane;
+                gis[j] = pos < len ? a.vals[start + pos] : 0u;
+                if (pos < len) pending |= 1u << j;
+            }
+            for (;;) {
+                int mine = 64 * kWavePer;
+#pragma unroll
+                for (int j = kWavePer - 1; j >= 0; --j)
+                    if ((pending >> j & 1u) && would_mutate(TYPE, a.elems + (int64_t)gis[j] * a.esz, m, c))
+                        mine = j * 64 + lane;
+                const int f = wave_min(mine);
+#pragma unroll
+                for (int j = 0; j < kWavePer; ++j) {
+                    if (!(pending >> j & 1u) || j * 64 + lane >= f) continue;
+                    const uint32_t gi = gis[j];
+                    const int32_t b = (int32_t)(gi / (uint32_t)a.stride);
+                    Meta t = m;
+                    c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
+                    dispatch<SV>(TYPE, a.elems + (int64_t)gi * a.esz, entry,
+                                 (uint8_t)(gi - (uint32_t)b * (uint32_t)a.stride), t, c);
+                    if (a.error_flags && !meta_equal(t, m)) atomicOr(a.error_flags, 1u);
+                    pending &= ~(1u << j);
+                }
+                if (f >= 64 * kWavePer) break;
+                const int owner = f & 63, j = f >> 6;
+                if (lane == owner) {
+#pragma unroll
+                    for (int jj = 0; jj < kWavePer; ++jj) {
+                        if (jj != j) continue;
+                        const uint32_t gi = gis[jj];
+                        const int32_t b = (int32_t)(gi / (uint32_t)a.stride);
+                        c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
+                        dispatch<SV>(TYPE, a.elems + (int64_t)gi * a.esz, entry,
+                                     (uint8_t)(gi - (uint32_t)b * (uint32_t)a.stride), m, c);
+                        pending &= ~(1u << jj);
+                    }
+                }
+                meta_bcast(m, owner);
+            }
+        }
+        if (lane == 0) meta_store(entry, m);
     }
 }
 
@@ -391,18 +528,26 @@ int launch_hash_ids(const uint32_t *ids, uint64_t *out, int64_t n, hipStream_t s
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// Stable LSD radix sort of (entry id, element) pairs. rocPRIM picks a merge sort below 1M
+// items by default; a merge_sort_limit of 0 keeps every size on the Onesweep radix passes
+// (ceil(key_bits / 8) passes over 8-byte pairs), which is what the key width makes cheapest.
+using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                              rocprim::default_config, 0>;
+
 size_t sort_temp_bytes(int64_t n, int key_bits)
 {
     size_t bytes = 0;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                       (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, 0, key_bits);
+    rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                          (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)n, 0u,
+                                          (unsigned)key_bits);
     return bytes;
 }
 
 int sort_pairs(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
                uint32_t *vout, int64_t n, int key_bits, hipStream_t s)
 {
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, kin, kout, vin, vout, (int)n, 0, key_bits, s);
+    hipError_t e = rocprim::radix_sort_pairs<SortConfig>(tmp, tmp_bytes, kin, kout, vin, vout, (size_t)n, 0u,
+                                                         (unsigned)key_bits, s);
     return e == hipSuccess ? 0 : -1;
 }
 
@@ -447,7 +592,8 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     sa.long_start = bl.long_start;
     sa.long_len = bl.long_len;
     sa.long_count = bl.long_count;
-    if (hipMemsetAsync(bl.long_count, 0, sizeof(uint32_t), s) != hipSuccess) return -3;
+    sa.list_cap = bl.list_cap;
+    if (hipMemsetAsync(bl.long_count, 0, 2 * sizeof(uint32_t), s) != hipSuccess) return -3;
     LongArgs la2;
     la2.elems = bl.elems;
     la2.log = bl.log;
@@ -457,6 +603,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     la2.long_start = bl.long_start;
     la2.long_len = bl.long_len;
     la2.long_count = bl.long_count;
+    la2.list_cap = bl.list_cap;
     la2.error_flags = bl.error_flags;
     la2.g = bl.g;
     la2.rw_stride = bl.rw_stride;
@@ -465,19 +612,31 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     la2.type = bl.type;
     la2.g_membership = bl.g_membership;
     la2.w_ack_init = bl.w_ack_init;
-    // a segment longer than kShortSeg needs kShortSeg + 1 elements: cap the long-exec grid
-    int64_t max_long = n / (kShortSeg + 1) + 1;
-    const unsigned lgrid = (unsigned)(max_long < 1024 ? max_long : 1024);
-    if (bl.g.st_value == 31) {
-        hipLaunchKernelGGL(k_segment_exec<31>, dim3(grid), dim3(256), 0, s, sa);
-        hipLaunchKernelGGL(k_long_exec<31>, dim3(lgrid), dim3(256), 0, s, la2);
-    } else if (bl.g.st_value == 287) {
-        hipLaunchKernelGGL(k_segment_exec<287>, dim3(grid), dim3(256), 0, s, sa);
-        hipLaunchKernelGGL(k_long_exec<287>, dim3(lgrid), dim3(256), 0, s, la2);
-    } else {
-        hipLaunchKernelGGL(k_segment_exec<0>, dim3(grid), dim3(256), 0, s, sa);
-        hipLaunchKernelGGL(k_long_exec<0>, dim3(lgrid), dim3(256), 0, s, la2);
+    // grids sized by how many segments each tier can hold at most
+    int64_t max_hot = n / (kMidSeg + 1) + 1, max_mid = n / (kShortSeg + 1) + 1;
+    const unsigned lgrid = (unsigned)(max_hot < 256 ? max_hot : 256);
+    const unsigned wgrid = (unsigned)((max_mid + 3) / 4 < 2048 ? (max_mid + 3) / 4 : 2048);
+#define HKV_LAUNCH_SEG(T, V)                                                                       \
+    do {                                                                                           \
+        hipLaunchKernelGGL((k_segment_exec<T, V>), dim3(grid), dim3(256), 0, s, sa);               \
+        hipLaunchKernelGGL((k_wave_exec<T, V>), dim3(wgrid), dim3(256), 0, s, la2);               \
+        hipLaunchKernelGGL((k_long_exec<T, V>), dim3(lgrid), dim3(kLongThreads), 0, s, la2);      \
+    } while (0)
+#define HKV_LAUNCH_SV(T)                                      \
+    do {                                                      \
+        if (bl.g.st_value == 31) HKV_LAUNCH_SEG(T, 31);       \
+        else if (bl.g.st_value == 287) HKV_LAUNCH_SEG(T, 287); \
+        else HKV_LAUNCH_SEG(T, 0);                            \
+    } while (0)
+    switch (bl.type) {
+    case kLocal: HKV_LAUNCH_SV(kLocal); break;
+    case kLocalAfterMemb: HKV_LAUNCH_SV(kLocalAfterMemb); break;
+    case kInvs: HKV_LAUNCH_SV(kInvs); break;
+    case kAcks: HKV_LAUNCH_SV(kAcks); break;
+    default: HKV_LAUNCH_SV(kVals); break;
     }
+#undef HKV_LAUNCH_SV
+#undef HKV_LAUNCH_SEG
     if (hipGetLastError() != hipSuccess) return -3;
     if (bl.type == kInvs && bl.ns_idx && bl.node_suspected) {
         hipLaunchKernelGGL(k_node_suspected, dim3((bl.n_batches + 255) / 256), dim3(256), 0, s, bl.elems,

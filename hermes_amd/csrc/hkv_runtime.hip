@@ -144,7 +144,7 @@ static int ensure_scratch(hkv_table *t, int64_t n, int key_bits)
         HIP_TRY(hipMalloc(&t->d_keys_b, cap * 4));
         HIP_TRY(hipMalloc(&t->d_vals_a, cap * 4));
         HIP_TRY(hipMalloc(&t->d_vals_b, cap * 4));
-        HIP_TRY(hipMalloc(&t->d_long, (2 * (cap / 16 + 2) + 64) * 4));
+        HIP_TRY(hipMalloc(&t->d_long, (4 * (cap / 4 + 2) + 64) * 4));
         t->scratch_n = cap;
     }
     size_t need = sort_temp_bytes(t->scratch_n, key_bits > 0 ? key_bits : 32);
@@ -352,9 +352,11 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.vals_b = t->d_vals_b;
     bl.sort_tmp = t->d_sort_tmp;
     bl.sort_tmp_bytes = t->sort_tmp_bytes;
+    // d_long = [counts (64) | starts (2*cap) | lens (2*cap)], cap = scratch_n / 4 + 2
+    bl.list_cap = (uint32_t)(t->scratch_n / 4 + 2);
     bl.long_count = t->d_long;
     bl.long_start = t->d_long + 64;
-    bl.long_len = t->d_long + 64 + (t->scratch_n / 16 + 2);
+    bl.long_len = t->d_long + 64 + 2 * (int64_t)bl.list_cap;
     bl.error_flags = t->d_error_flags;
     bl.n = n;
     bl.n_batches = d->n_batches;

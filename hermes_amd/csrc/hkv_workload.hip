@@ -112,17 +112,18 @@ __global__ void k_gen_trace(uint64_t *tkey, uint8_t *top, uint32_t *tid, int32_t
 __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, uint32_t op_size, uint32_t st_value,
                                                 uint32_t shift, const uint64_t *tkey, const uint8_t *top,
                                                 int32_t tlen, uint32_t *cursor, uint32_t machine_id,
-                                                int32_t first_iter, unsigned long long *counters)
+                                                int32_t first_iter, int32_t refill_all, unsigned long long *counters)
 {
     const int w = blockIdx.x, i = threadIdx.x;
     const bool live = i < stride;
     uint8_t *op = ops + ((int64_t)w * stride + i) * op_size;
     uint8_t st = live ? op[9] : 0;
-    bool done = live && (first_iter || st == kMiss || st == kPutComplete || st == kRmwAbort ||
-                         st == kRmwComplete || st == kOpMembComplete || st == kGetComplete);
-    int commits = (done && !first_iter && st != kMiss && st != kRmwAbort) ? 1 : 0;
-    int misses = (done && !first_iter && st == kMiss) ? 1 : 0;
-    int writes = (done && !first_iter && st == kPutComplete) ? 1 : 0;
+    const bool complete = st == kMiss || st == kPutComplete || st == kRmwAbort || st == kRmwComplete ||
+                          st == kOpMembComplete || st == kGetComplete;
+    bool done = live && (first_iter || refill_all || complete);
+    int commits = (live && complete && !first_iter && st != kMiss && st != kRmwAbort) ? 1 : 0;
+    int misses = (live && !first_iter && st == kMiss) ? 1 : 0;
+    int writes = (live && !first_iter && st == kPutComplete) ? 1 : 0;
     int total;
     int rank = block_rank(done, total);
     uint32_t base = cursor[w];
@@ -279,11 +280,11 @@ int hkv_wl_gen_trace(uint64_t *tkey, uint8_t *top, uint32_t *tid, int32_t n_work
 
 int hkv_wl_refill(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint32_t st_value, uint32_t shift,
                   const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor, uint32_t machine_id,
-                  int32_t first_iter, unsigned long long *counters, void *stream)
+                  int32_t first_iter, int32_t refill_all, unsigned long long *counters, void *stream)
 {
     if (stride > 256 || n_workers <= 0) return -1;
     hipLaunchKernelGGL(k_refill, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, st_value,
-                       shift, tkey, top, tlen, cursor, machine_id, first_iter, counters);
+                       shift, tkey, top, tlen, cursor, machine_id, first_iter, refill_all, counters);
     return ok();
 }
 

@@ -31,7 +31,7 @@ class HkvZipf(ctypes.Structure):
 _L.hkv_wl_gen_trace.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(HkvZipf),
                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, _P]
 _L.hkv_wl_refill.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
-                             _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_int32, _P, _P]
+                             _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, _P, _P]
 _L.hkv_wl_marshal_invs.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_acks.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_vals.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
@@ -73,7 +73,7 @@ class Round:
     def __init__(self, kvs: HermesKV, n_workers: int, membership: bytes, peer_ids: list[int],
                  zipf: HkvZipf, write_permille: int = 200, rmw_permille: int = 0,
                  remote_per_peer: int = 50, trace_len: int = 8192, seed: int = 0x5EED,
-                 virtual_peers: bool = True, max_steps: int = 64):
+                 virtual_peers: bool = True, max_steps: int = 64, retry_stalled: bool = False):
         self.kvs = kvs
         self.W = n_workers
         self.mb = membership
@@ -85,6 +85,7 @@ class Round:
         self.rpp = remote_per_peer
         self.R = len(self.peers)
         self.virtual = virtual_peers
+        self.retry = retry_stalled     # True: refill_ops semantics (stalled ops keep their slot)
         self.machine_id = kvs.machine_id
         dev = torch.device("cuda", kvs.device)
         W, S = n_workers, self.LOCAL
@@ -127,7 +128,8 @@ class Round:
     def refill(self, first: bool = False):
         check(_L.hkv_wl_refill(_ptr(self.ops), self.W, self.LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
                                _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
-                               self.machine_id, int(first), _ptr(self.counters), _s()), "refill")
+                               self.machine_id, int(first), int(not self.retry), _ptr(self.counters), _s()),
+              "refill")
 
     def local_batch(self):
         self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb)

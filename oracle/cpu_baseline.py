@@ -18,13 +18,14 @@ class HkoZipf(ctypes.Structure):
 
 
 def run_cpu_baseline(kvs, zipf, write_permille: int, workers: int, seconds: float, seed: int,
-                     n_peers: int = 2, per_peer: int = 50) -> dict:
+                     n_peers: int = 2, per_peer: int = 50, refill_all: bool = True) -> dict:
     build()
     L = lib()
     L.hko_bench_rounds.restype = ctypes.c_int64
     L.hko_bench_rounds.argtypes = [ctypes.c_void_p, ctypes.POINTER(Config), ctypes.c_int, ctypes.c_double,
                                    ctypes.POINTER(HkoZipf), ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
-                                   ctypes.c_uint64, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]
+                                   ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
+                                   ctypes.POINTER(ctypes.c_double)]
     L.hko_set_log_head.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
     c = kvs.cfg
     cfg = Config(c.big_objects, c.extra_cache_lines, c.rmw_enabled, c.machine_id, c.num_bkts, c.log_cap)
@@ -41,10 +42,12 @@ def run_cpu_baseline(kvs, zipf, write_permille: int, workers: int, seconds: floa
         hz = HkoZipf(zipf.theta, zipf.zetan, zipf.alpha, zipf.eta, zipf.half_pow, zipf.n)
         rounds, secs = ctypes.c_int64(0), ctypes.c_double(0.0)
         committed = L.hko_bench_rounds(h, ctypes.byref(cfg), workers, seconds, ctypes.byref(hz), write_permille,
-                                       n_peers, per_peer, seed, ctypes.byref(rounds), ctypes.byref(secs))
+                                       n_peers, per_peer, seed, int(refill_all), ctypes.byref(rounds),
+                                       ctypes.byref(secs))
     finally:
         L.hko_destroy(h)
     return {"value": committed / secs.value, "unit": "ops/s", "cores": 1, "kind": "port",
-            "sample": (f"{rounds.value} rounds x {workers} workers x 250-op local batches (+{n_peers} virtual "
+            "sample": (f"{rounds.value} rounds x {workers} workers x 250-op {'fresh' if refill_all else 'refilled'} "
+                       f"local batches (+{n_peers} virtual "
                        f"peers x {per_peer} INV/VAL per worker-round, 2 ACKs per write) in {secs.value:.1f} s, "
                        f"same table ({c.num_bkts} buckets) and Zipf/write mix as the GPU run")}

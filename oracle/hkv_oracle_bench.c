@@ -7,6 +7,8 @@
  * ACKs from the virtual peers -> incoming INV batch -> ACK batch (rw = the worker's ops) ->
  * VAL marshal -> incoming VAL batch. Traces and peer INV/VAL slabs are generated before the
  * timed loop with the same generators (splitmix64 streams, Gray/YCSB Zipf, CityHash keys).
+ * refill_all = 1 gives every worker a fresh batch each round (bench.py's default), 0 keeps
+ * stalled ops in their slots as refill_ops does.
  */
 #include <math.h>
 #include <stdlib.h>
@@ -58,7 +60,7 @@ void hko_set_log_head(hko_kvs *kv, uint64_t head);
 
 /* returns committed ops; rounds and seconds through out-params */
 int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, double seconds, const hko_zipf *z,
-                         uint32_t write_pm, int n_peers, int per_peer, uint64_t seed, int64_t *out_rounds,
+                         uint32_t write_pm, int n_peers, int per_peer, uint64_t seed, int refill_all, int64_t *out_rounds,
                          double *out_secs)
 {
     const int S = 250, T = 8192, P = 16;
@@ -113,9 +115,9 @@ int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, doub
             for (int i = 0; i < S; i++) {
                 uint8_t *o = ow + (size_t)i * osz;
                 uint8_t st = o[9];
-                int done = first || st == 130 || st == 128 || st == 138 || st == 137 || st == 119 || st == 121;
-                if (!done) continue;
-                if (!first && st != 130 && st != 138) committed++;
+                int complete = st == 130 || st == 128 || st == 138 || st == 137 || st == 119 || st == 121;
+                if (!first && complete && st != 130 && st != 138) committed++;
+                if (!(first || refill_all || complete)) continue;  /* stalled ops retry unless refill_all */
                 int64_t ti = (int64_t)w * T + cursor[w];
                 cursor[w] = (cursor[w] + 1) % T;
                 memcpy(o, &tkey[ti], 8);

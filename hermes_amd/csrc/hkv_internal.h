@@ -19,8 +19,11 @@ struct BatchLaunch {
     int32_t *ns_idx;
     int32_t *node_suspected;
     uint32_t *keys_a, *keys_b, *vals_a, *vals_b;
-    uint32_t *long_start, *long_len, *long_count;  // hot/mid segment work lists (k_segment_exec ->
-    uint32_t list_cap;                              //   k_long_exec / k_wave_exec), cap each
+    // long-segment round state (see hkv_kernels.hip, stage 3)
+    uint32_t *seg_start, *seg_len, *seg_count, *seg_fallback, *seg_of, *seg_mut;
+    void *seg_meta;
+    uint8_t *seg_done, *seg_snap;
+    uint32_t seg_cap;
     unsigned int *error_flags;                       // checked builds: unsound would_mutate()
     void *sort_tmp;
     size_t sort_tmp_bytes;
@@ -56,5 +59,8 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s);
 int launch_populate(const PopulateLaunch &pl, hipStream_t s);
 int launch_hash_ids(const uint32_t *ids, uint64_t *out, int64_t n, hipStream_t s);
 size_t sort_temp_bytes(int64_t n, int key_bits);
+// long-segment scratch for launches of up to n elements: size, and carving into bl.seg_*
+size_t seg_scratch_bytes(int64_t n, uint32_t entry_size);
+void seg_carve(BatchLaunch &bl, uint8_t *base, int64_t n, uint32_t entry_size);
 
 }  // namespace hkv

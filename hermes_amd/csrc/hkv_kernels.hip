@@ -118,16 +118,55 @@ __global__ __launch_bounds__(256) void k_lookup(LookupArgs a)
 }
 
 // ------------------------------------------------------------------ batch stage 3: segments
+// After the sort every log entry touched by the launch owns one contiguous segment of the
+// sorted order, whose elements are in concatenation order. A segment of at most kShortSeg
+// elements is applied serially by its first lane (k_segment_exec). Longer ones (hot keys)
+// go through chip-wide rounds:
+//
+//   round r (k_round_cand + k_round_apply), for every long segment not yet finished:
+//     every element after the previous round's mutation asks would_mutate() against the
+//     segment's meta S_r; the first such position F_r is found with a wave-segmented min and
+//     one atomicMin per wavefront and segment; one lane then snapshots the entry (image of
+//     S_r), applies element F_r with the serial exec function and records S_{r+1}. A segment
+//     whose round finds no candidate is finished: S_r is its final meta, stored to the entry.
+//   k_round_resolve: every other element of a long segment lies strictly between two
+//     consecutive mutations F_{r-1} < pos < F_r and is therefore a non-candidate under S_r:
+//     it runs the serial exec function on a private copy of S_r against the snapshot of S_r
+//     (so GETs read the value as it was at their point of the order) -- all in parallel.
+//   k_long_exec: segments that still mutate after kMaxRounds rounds finish on one workgroup
+//     from F_{R-1}+1 with S_R (first-candidate passes, see below).
+//
+// Exactness only needs would_mutate() to be sound (a false answer guarantees the exec
+// function leaves the meta unchanged); every element still runs the reference's exec
+// function once, against the meta the sequential order gives it. Checked by bit 0 of
+// *error_flags, which a non-candidate that did change its private copy would raise.
+constexpr int kShortSeg = 4;
+constexpr int kMaxRounds = 4;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint8_t kNotDone = 0xFF;
+
+struct SegState {            // per long segment, all in device scratch
+    uint32_t *start;         // [cap] first sorted position
+    uint32_t *len;           // [cap]
+    uint32_t *count;         // [2]: [1] = segments left to k_long_exec
+    uint32_t *fallback;      // [cap] slots of segments left to k_long_exec
+    const uint32_t *lidx;    // [n] long-segment heads at or before each sorted position (scan)
+    uint32_t *seg_of;        // [n] long-segment slot of every sorted position (kNone if short/skip)
+    Meta *meta;              // [cap][kMaxRounds + 1]
+    uint32_t *mut;           // [cap][kMaxRounds] F_r (position within segment), kNone if none
+    uint8_t *done;           // [cap] round whose meta is final, kNotDone while mutating
+    uint8_t *snap;           // [cap][kMaxRounds] entry images of S_r
+    uint32_t cap;
+};
+
 struct SegmentArgs {
-    uint32_t *long_start;   // hot list: [0, cap)   mid list: [cap, 2*cap)
-    uint32_t *long_len;
-    uint32_t *long_count;   // [0] hot, [1] mid
-    uint32_t list_cap;
+    SegState st;
     uint8_t *elems;
     uint8_t *log;
     uint8_t *rw;
     const uint32_t *keys;
     const uint32_t *vals;
+    unsigned int *error_flags;
     Geometry g;
     int64_t n;
     int64_t rw_stride;
@@ -139,77 +178,165 @@ struct SegmentArgs {
     uint8_t w_ack_init;
 };
 
-// Three tiers by segment length: at most kShortSeg elements are applied serially by the
-// segment's owner lane (k_segment_exec); up to kMidSeg by one wavefront (k_wave_exec); longer
-// ones (the hottest keys) by a 1024-thread workgroup (k_long_exec). The last two receive their
-// segments through compact work lists written by k_segment_exec.
-constexpr int kShortSeg = 4;
-constexpr int kMidSeg = 4096;
-
-// Queue a segment on one of the two work lists with one atomic per wavefront and list
-// (a per-lane atomic on a shared counter serialises hundreds of thousands of heads).
-__device__ __forceinline__ void enqueue_segment(const SegmentArgs &a, bool want, int tier, uint32_t start,
-                                                uint32_t len)
+__device__ __forceinline__ Ctx make_ctx(const SegmentArgs &a)
 {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        const unsigned long long m = __ballot(want && tier == t);
-        if (!m) continue;
-        const int leader = __ffsll((long long)m) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&a.long_count[t], (uint32_t)__popcll(m));
-        base = __shfl(base, leader, 64);
-        if (want && tier == t) {
-            const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull)) + (uint32_t)t * a.list_cap;
-            a.long_start[slot] = start;
-            a.long_len[slot] = len;
-        }
-    }
-}
-
-template <int TYPE, int SV>
-__global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
-{
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t key = p < a.n ? a.keys[p] : a.skip_key;
-    const bool head = key != a.skip_key && (p == 0 || a.keys[p - 1] != key);
-    const bool longseg = head && p + kShortSeg < a.n && a.keys[p + kShortSeg] == key;
-    uint32_t len = 0;
-    if (longseg) {
-        // gallop to the end of the segment on the sorted keys
-        int64_t lo = p + kShortSeg, step = 2 * kShortSeg, hi;
-        for (;;) {
-            hi = lo + step;
-            if (hi >= a.n || a.keys[hi] != key) break;
-            lo = hi;
-            step *= 2;
-        }
-        if (hi > a.n) hi = a.n;
-        while (hi - lo > 1) {  // keys[lo] == key, keys[hi] != key (or hi == n)
-            int64_t mid = (lo + hi) / 2;
-            if (a.keys[mid] == key) lo = mid;
-            else hi = mid;
-        }
-        len = (uint32_t)(hi - p);
-    }
-    enqueue_segment(a, longseg, len > (uint32_t)kMidSeg ? 0 : 1, (uint32_t)p, len);
-    if (!head || longseg) return;
-    uint8_t *entry = a.log + (uint64_t)key * a.g.entry_unit;
-    Meta m;
-    meta_load(entry, m);
     Ctx c;
     c.g = a.g;
     c.g_membership = a.g_membership;
     c.w_ack_init = a.w_ack_init;
-    for (int64_t q = p; q < a.n && a.keys[q] == key; ++q) {
-        uint32_t gi = a.vals[q];
-        int32_t b = (int32_t)(gi / (uint32_t)a.stride);
-        uint32_t idx = gi - (uint32_t)b * (uint32_t)a.stride;
-        c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
-        dispatch<SV>(TYPE, a.elems + (int64_t)gi * a.esz, entry, (uint8_t)idx, m, c);
+    c.rw = nullptr;
+    return c;
+}
+
+__device__ __forceinline__ void elem_at(const SegmentArgs &a, uint32_t gi, uint8_t *&x, uint8_t &idx, Ctx &c)
+{
+    const int32_t b = (int32_t)(gi / (uint32_t)a.stride);
+    idx = (uint8_t)(gi - (uint32_t)b * (uint32_t)a.stride);
+    c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
+    x = a.elems + (int64_t)gi * a.esz;
+}
+
+__device__ __forceinline__ uint8_t *entry_of(const SegmentArgs &a, uint32_t key)
+{
+    return a.log + (uint64_t)key * a.g.entry_unit;
+}
+
+// Serial tier + long-segment registration. A long segment's slot is its rank among long heads
+// (the scan in lidx), so registration needs no atomics.
+template <int TYPE, int SV>
+__global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
+{
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n) return;
+    const uint32_t key = a.keys[p];
+    const bool head = key != a.skip_key && (p == 0 || a.keys[p - 1] != key);
+    if (!head) return;
+    const bool longseg = p + kShortSeg < a.n && a.keys[p + kShortSeg] == key;
+    if (longseg) {
+        const uint32_t s = a.st.lidx[p] - 1;
+        a.st.start[s] = (uint32_t)p;
+        Meta m0;
+        meta_load(entry_of(a, key), m0);
+        a.st.meta[(size_t)s * (kMaxRounds + 1)] = m0;
+#pragma unroll
+        for (int r = 0; r < kMaxRounds; ++r) a.st.mut[(size_t)s * kMaxRounds + r] = kNone;
+        a.st.done[s] = kNotDone;
+        return;
     }
-    meta_store(entry, m);
+    uint8_t *entry = entry_of(a, key);
+    Meta mm;
+    meta_load(entry, mm);
+    Ctx c = make_ctx(a);
+    for (int64_t q = p; q < a.n && a.keys[q] == key; ++q) {
+        uint8_t *x;
+        uint8_t idx;
+        elem_at(a, a.vals[q], x, idx, c);
+        dispatch<SV>(TYPE, x, entry, idx, mm, c);
+    }
+    meta_store(entry, mm);
+}
+
+// seg_of[p] for every sorted position; the last position of a long segment records its length
+__global__ __launch_bounds__(256) void k_seg_map(SegmentArgs a)
+{
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n) return;
+    const uint32_t key = a.keys[p];
+    uint32_t s = kNone;
+    const uint32_t l = a.st.lidx[p];
+    if (key != a.skip_key && l && a.keys[a.st.start[l - 1]] == key) {  // inside the last long segment begun
+        s = l - 1;
+        if (p + 1 == a.n || a.keys[p + 1] != key) a.st.len[s] = (uint32_t)(p + 1) - a.st.start[s];
+    }
+    a.st.seg_of[p] = s;
+}
+
+template <int TYPE>
+__global__ __launch_bounds__(256) void k_round_cand(SegmentArgs a, int r)
+{
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    uint32_t s = p < a.n ? a.st.seg_of[p] : kNone;
+    bool cand = false;
+    uint32_t rel = 0;
+    if (s != kNone && a.st.done[s] == kNotDone) {
+        rel = (uint32_t)p - a.st.start[s];
+        const uint32_t prev = r > 0 ? a.st.mut[(size_t)s * kMaxRounds + r - 1] : kNone;
+        if (r == 0 || rel > prev) {
+            Ctx c = make_ctx(a);
+            uint8_t *x;
+            uint8_t idx;
+            elem_at(a, a.vals[p], x, idx, c);
+            const Meta m = a.st.meta[(size_t)s * (kMaxRounds + 1) + r];
+            cand = would_mutate(TYPE, x, m, c);
+        }
+    }
+    // candidates of one segment are consecutive among a wavefront's candidate lanes (sorted
+    // order): only the first of each run issues the atomicMin
+    const unsigned long long cm = __ballot(cand);
+    const unsigned long long below = cm & ((1ull << lane) - 1ull);
+    const int prev_lane = below ? 63 - __clzll((long long)below) : -1;
+    const uint32_t prev_s = __shfl(s, prev_lane < 0 ? lane : prev_lane, 64);
+    if (cand && (prev_lane < 0 || prev_s != s)) {
+        uint32_t *f = &a.st.mut[(size_t)s * kMaxRounds + r];
+        if (rel < __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(f, rel);
+    }
+}
+
+template <int TYPE, int SV>
+__global__ __launch_bounds__(256) void k_round_apply(SegmentArgs a, int r)
+{
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.st.lidx[a.n - 1] || a.st.done[s] != kNotDone) return;
+    const uint32_t start = a.st.start[s];
+    uint8_t *entry = entry_of(a, a.keys[start]);
+    const uint32_t f = a.st.mut[(size_t)s * kMaxRounds + r];
+    Meta m = a.st.meta[(size_t)s * (kMaxRounds + 1) + r];
+    if (f == kNone) {
+        a.st.done[s] = (uint8_t)r;
+        meta_store(entry, m);
+        return;
+    }
+    // image of S_r for the elements resolved before F_r (entries are 8-byte aligned)
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(entry);
+    uint64_t *dst = reinterpret_cast<uint64_t *>(a.st.snap + ((size_t)s * kMaxRounds + r) * a.g.entry_size);
+    for (uint32_t w = 0; w < a.g.entry_size / 8; ++w) dst[w] = src[w];
+    Ctx c = make_ctx(a);
+    uint8_t *x;
+    uint8_t idx;
+    elem_at(a, a.vals[start + f], x, idx, c);
+    dispatch<SV>(TYPE, x, entry, idx, m, c);
+    a.st.meta[(size_t)s * (kMaxRounds + 1) + r + 1] = m;
+    if (r == kMaxRounds - 1) a.st.fallback[atomicAdd(&a.st.count[1], 1u)] = s;
+}
+
+template <int TYPE, int SV>
+__global__ __launch_bounds__(256) void k_round_resolve(SegmentArgs a)
+{
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n) return;
+    const uint32_t s = a.st.seg_of[p];
+    if (s == kNone) return;
+    const uint32_t rel = (uint32_t)p - a.st.start[s];
+    const uint8_t done = a.st.done[s];
+    int r = 0;
+    uint32_t f = kNone;
+    for (; r < kMaxRounds; ++r) {
+        f = (done != kNotDone && r == done) ? kNone : a.st.mut[(size_t)s * kMaxRounds + r];
+        if (rel <= f) break;
+    }
+    if (r == kMaxRounds || rel == f) return;  // left to k_long_exec, or applied by a round
+    const uint8_t *img = f == kNone ? entry_of(a, a.keys[p])
+                                    : a.st.snap + ((size_t)s * kMaxRounds + r) * a.g.entry_size;
+    const Meta m = a.st.meta[(size_t)s * (kMaxRounds + 1) + r];
+    Meta t = m;
+    Ctx c = make_ctx(a);
+    uint8_t *x;
+    uint8_t idx;
+    elem_at(a, a.vals[p], x, idx, c);
+    // non-candidates only read the entry (the value), so the snapshot stands in for it
+    dispatch<SV>(TYPE, x, const_cast<uint8_t *>(img), idx, t, c);
+    if (a.error_flags && !meta_equal(t, m)) atomicOr(a.error_flags, 1u);
 }
 
 template <int NT>
@@ -227,81 +354,31 @@ __device__ __forceinline__ int block_min(int v, int *lds)
     return r;
 }
 
-__device__ __forceinline__ int wave_min(int v)
-{
-    for (int o = 32; o > 0; o >>= 1) {
-        int u = __shfl_xor(v, o, 64);
-        v = u < v ? u : v;
-    }
-    return v;
-}
-
-__device__ __forceinline__ void meta_bcast(Meta &m, int src)
-{
-    m.w4 = __shfl(m.w4, src, 64);
-    m.w5 = __shfl(m.w5, src, 64);
-    m.ver = __shfl(m.ver, src, 64);
-    m.llw_ver = __shfl(m.llw_ver, src, 64);
-    m.llw_cid = (uint8_t)__shfl((int)m.llw_cid, src, 64);
-}
-
-// One 1024-thread workgroup per long segment (one hot key), in chunks of kLongChunk elements
-// (kPerThread per lane, lane-strided so the sorted element ids are read coalesced).
-// Per chunk, repeat: every unresolved element asks would_mutate() against the shared meta;
-// the first candidate f is found with a block min; elements before f are resolved in parallel,
-// each running the serial exec function on a private copy of the meta (it cannot change it);
-// after a barrier, f alone runs the exec function on the shared meta. A chunk without a
-// candidate takes one pass, so a hot key costs one pass per kLongChunk elements plus one per
-// mutation. A non-candidate that did change its copy sets bit 0 of *error_flags (that would
-// mean would_mutate() is unsound).
-struct LongArgs {
-    uint8_t *elems;
-    uint8_t *log;
-    uint8_t *rw;
-    const uint32_t *keys;
-    const uint32_t *vals;
-    const uint32_t *long_start;
-    const uint32_t *long_len;
-    const uint32_t *long_count;
-    uint32_t list_cap;
-    unsigned int *error_flags;
-    Geometry g;
-    int64_t rw_stride;
-    int32_t stride;
-    int32_t esz;
-    int32_t type;
-    uint8_t g_membership;
-    uint8_t w_ack_init;
-};
-
+// Fallback for segments still mutating after kMaxRounds rounds: one 1024-thread workgroup per
+// segment continues from F_{R-1}+1 with S_R, in chunks of kLongChunk elements: repeat
+// {block min of the first candidate f; resolve elements before f on private copies; barrier;
+// f applies on the shared meta; barrier} until a chunk has no candidate left.
 constexpr int kLongThreads = 1024;
 constexpr int kPerThread = 8;
 constexpr int kLongChunk = kLongThreads * kPerThread;
 
 template <int TYPE, int SV>
-__global__ __launch_bounds__(kLongThreads) void k_long_exec(LongArgs a)
+__global__ __launch_bounds__(kLongThreads) void k_long_exec(SegmentArgs a)
 {
     __shared__ Meta sm;
     __shared__ int red[kLongThreads / 64];
     const int tid = threadIdx.x;
-    const uint32_t nseg = a.long_count[0];
-    Ctx c;
-    c.g = a.g;
-    c.g_membership = a.g_membership;
-    c.w_ack_init = a.w_ack_init;
-    c.rw = nullptr;
-    for (uint32_t s = blockIdx.x; s < nseg; s += gridDim.x) {
-        const uint32_t start = a.long_start[s], len = a.long_len[s];
-        const uint32_t key = a.keys[start];
-        uint8_t *entry = a.log + (uint64_t)key * a.g.entry_unit;
-        if (tid == 0) {
-            Meta m;
-            meta_load(entry, m);
-            sm = m;
-        }
+    const uint32_t nfb = a.st.count[1];
+    Ctx c = make_ctx(a);
+    for (uint32_t i = blockIdx.x; i < nfb; i += gridDim.x) {
+        const uint32_t s = a.st.fallback[i];
+        const uint32_t start = a.st.start[s], len = a.st.len[s];
+        const uint32_t first = a.st.mut[(size_t)s * kMaxRounds + kMaxRounds - 1] + 1;
+        uint8_t *entry = entry_of(a, a.keys[start]);
+        if (tid == 0) sm = a.st.meta[(size_t)s * (kMaxRounds + 1) + kMaxRounds];
         __syncthreads();
-        for (uint32_t base = 0; base < len; base += kLongChunk) {
-            uint32_t pending = 0;  // bit j: element base + j*kLongThreads + tid still to apply
+        for (uint32_t base = first; base < len; base += kLongChunk) {
+            uint32_t pending = 0;
 #pragma unroll
             for (int j = 0; j < kPerThread; ++j)
                 if (base + j * kLongThreads + tid < len) pending |= 1u << j;
@@ -311,33 +388,32 @@ __global__ __launch_bounds__(kLongThreads) void k_long_exec(LongArgs a)
 #pragma unroll
                 for (int j = kPerThread - 1; j >= 0; --j) {
                     if (!(pending >> j & 1u)) continue;
-                    const uint32_t gi = a.vals[start + base + j * kLongThreads + tid];
-                    if (would_mutate(TYPE, a.elems + (int64_t)gi * a.esz, m, c)) mine = j * kLongThreads + tid;
+                    uint8_t *x;
+                    uint8_t idx;
+                    elem_at(a, a.vals[start + base + j * kLongThreads + tid], x, idx, c);
+                    if (would_mutate(TYPE, x, m, c)) mine = j * kLongThreads + tid;
                 }
                 const int f = block_min<kLongThreads>(mine, red);
 #pragma unroll
                 for (int j = 0; j < kPerThread; ++j) {
                     const int pos = j * kLongThreads + tid;
                     if (!(pending >> j & 1u) || pos >= f) continue;
-                    const uint32_t gi = a.vals[start + base + pos];
-                    const int32_t b = (int32_t)(gi / (uint32_t)a.stride);
+                    uint8_t *x;
+                    uint8_t idx;
+                    elem_at(a, a.vals[start + base + pos], x, idx, c);
                     Meta t = m;
-                    c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
-                    dispatch<SV>(TYPE, a.elems + (int64_t)gi * a.esz, entry,
-                                 (uint8_t)(gi - (uint32_t)b * (uint32_t)a.stride), t, c);
+                    dispatch<SV>(TYPE, x, entry, idx, t, c);
                     if (a.error_flags && !meta_equal(t, m)) atomicOr(a.error_flags, 1u);
                     pending &= ~(1u << j);
                 }
                 __syncthreads();  // every read of the entry value precedes the mutation
                 if (f < kLongChunk && (f % kLongThreads) == tid) {
-                    const int j = f / kLongThreads;
-                    const uint32_t gi = a.vals[start + base + f];
-                    const int32_t b = (int32_t)(gi / (uint32_t)a.stride);
+                    uint8_t *x;
+                    uint8_t idx;
+                    elem_at(a, a.vals[start + base + f], x, idx, c);
                     Meta mm = m;
-                    c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
-                    dispatch<SV>(TYPE, a.elems + (int64_t)gi * a.esz, entry,
-                                 (uint8_t)(gi - (uint32_t)b * (uint32_t)a.stride), mm, c);
-                    pending &= ~(1u << j);
+                    dispatch<SV>(TYPE, x, entry, idx, mm, c);
+                    pending &= ~(1u << (f / kLongThreads));
                     sm = mm;
                 }
                 __syncthreads();
@@ -346,78 +422,6 @@ __global__ __launch_bounds__(kLongThreads) void k_long_exec(LongArgs a)
         }
         if (tid == 0) meta_store(entry, sm);
         __syncthreads();
-    }
-}
-
-// One wavefront per medium segment: the same first-candidate rounds as k_long_exec, in chunks
-// of 64 * kWavePer elements, with the meta replicated in every lane's registers (the owner of
-// a mutation broadcasts it by shuffles). Within a wavefront program order separates the
-// resolving lanes' entry-value reads from the mutation's writes, so no barrier is needed.
-constexpr int kWavePer = 4;
-
-template <int TYPE, int SV>
-__global__ __launch_bounds__(256) void k_wave_exec(LongArgs a)
-{
-    const int lane = threadIdx.x & 63;
-    const uint32_t wid = blockIdx.x * 4u + (threadIdx.x >> 6);
-    const uint32_t nseg = a.long_count[1];
-    Ctx c;
-    c.g = a.g;
-    c.g_membership = a.g_membership;
-    c.w_ack_init = a.w_ack_init;
-    c.rw = nullptr;
-    for (uint32_t s = wid; s < nseg; s += gridDim.x * 4u) {
-        const uint32_t start = a.long_start[a.list_cap + s], len = a.long_len[a.list_cap + s];
-        const uint32_t key = a.keys[start];
-        uint8_t *entry = a.log + (uint64_t)key * a.g.entry_unit;
-        Meta m;
-        meta_load(entry, m);
-        for (uint32_t base = 0; base < len; base += 64 * kWavePer) {
-            uint32_t gis[kWavePer];
-            uint32_t pending = 0;
-#pragma unroll
-            for (int j = 0; j < kWavePer; ++j) {
-                const uint32_t pos = base + j * 64 + lane;
-                gis[j] = pos < len ? a.vals[start + pos] : 0u;
-                if (pos < len) pending |= 1u << j;
-            }
-            for (;;) {
-                int mine = 64 * kWavePer;
-#pragma unroll
-                for (int j = kWavePer - 1; j >= 0; --j)
-                    if ((pending >> j & 1u) && would_mutate(TYPE, a.elems + (int64_t)gis[j] * a.esz, m, c))
-                        mine = j * 64 + lane;
-                const int f = wave_min(mine);
-#pragma unroll
-                for (int j = 0; j < kWavePer; ++j) {
-                    if (!(pending >> j & 1u) || j * 64 + lane >= f) continue;
-                    const uint32_t gi = gis[j];
-                    const int32_t b = (int32_t)(gi / (uint32_t)a.stride);
-                    Meta t = m;
-                    c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
-                    dispatch<SV>(TYPE, a.elems + (int64_t)gi * a.esz, entry,
-                                 (uint8_t)(gi - (uint32_t)b * (uint32_t)a.stride), t, c);
-                    if (a.error_flags && !meta_equal(t, m)) atomicOr(a.error_flags, 1u);
-                    pending &= ~(1u << j);
-                }
-                if (f >= 64 * kWavePer) break;
-                const int owner = f & 63, j = f >> 6;
-                if (lane == owner) {
-#pragma unroll
-                    for (int jj = 0; jj < kWavePer; ++jj) {
-                        if (jj != j) continue;
-                        const uint32_t gi = gis[jj];
-                        const int32_t b = (int32_t)(gi / (uint32_t)a.stride);
-                        c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
-                        dispatch<SV>(TYPE, a.elems + (int64_t)gi * a.esz, entry,
-                                     (uint8_t)(gi - (uint32_t)b * (uint32_t)a.stride), m, c);
-                        pending &= ~(1u << jj);
-                    }
-                }
-                meta_bcast(m, owner);
-            }
-        }
-        if (lane == 0) meta_store(entry, m);
     }
 }
 
@@ -531,16 +535,38 @@ int launch_hash_ids(const uint32_t *ids, uint64_t *out, int64_t n, hipStream_t s
 // Stable LSD radix sort of (entry id, element) pairs. rocPRIM picks a merge sort below 1M
 // items by default; a merge_sort_limit of 0 keeps every size on the Onesweep radix passes
 // (ceil(key_bits / 8) passes over 8-byte pairs), which is what the key width makes cheapest.
-using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                              rocprim::default_config, 0>;
+// Onesweep with 10-bit digits (3 passes for the 28-bit entry ids of a 100M-key table) and
+// 1024x8 tiles: measured fastest on gfx950 for 0.8M-8M pairs (tools/sort_bench.hip,
+// profiles/r01_sort_configs.txt); rocPRIM's default (1024x16, 8-bit) is 20-30% slower here.
+using SortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>, rocprim::kernel_config<1024, 8>, 10,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
+
+// heads of long segments (more than kShortSeg elements) of the sorted keys, 0/1 for the scan
+struct LongHeadFlag {
+    const uint32_t *keys;
+    uint32_t skip_key;
+    uint32_t n;
+    __device__ uint32_t operator()(uint32_t p) const
+    {
+        const uint32_t k = keys[p];
+        return (k != skip_key && (p == 0 || keys[p - 1] != k) && p + kShortSeg < n && keys[p + kShortSeg] == k) ? 1u
+                                                                                                                : 0u;
+    }
+};
+using HeadIter = rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, LongHeadFlag, uint32_t>;
 
 size_t sort_temp_bytes(int64_t n, int key_bits)
 {
-    size_t bytes = 0;
+    size_t bytes = 0, scan = 0;
     rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                                           (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)n, 0u,
                                           (unsigned)key_bits);
-    return bytes;
+    HeadIter it(rocprim::counting_iterator<uint32_t>(0), LongHeadFlag{nullptr, 0, 0});
+    rocprim::inclusive_scan(nullptr, scan, it, (uint32_t *)nullptr, (size_t)n, rocprim::plus<uint32_t>());
+    return bytes > scan ? bytes : scan;
 }
 
 int sort_pairs(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout, const uint32_t *vin,
@@ -549,6 +575,37 @@ int sort_pairs(void *tmp, size_t tmp_bytes, const uint32_t *kin, uint32_t *kout,
     hipError_t e = rocprim::radix_sort_pairs<SortConfig>(tmp, tmp_bytes, kin, kout, vin, vout, (size_t)n, 0u,
                                                          (unsigned)key_bits, s);
     return e == hipSuccess ? 0 : -1;
+}
+
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+size_t seg_scratch_bytes(int64_t n, uint32_t entry_size)
+{
+    const size_t cap = (size_t)(n / (kShortSeg + 1) + 1);
+    return align256(4 * (size_t)n) * 2 + align256(4 * cap) * 2 + 256 + align256(sizeof(Meta) * cap * (kMaxRounds + 1)) +
+           align256(4 * cap * kMaxRounds) + align256(cap) + (size_t)entry_size * cap * kMaxRounds;
+}
+
+void seg_carve(BatchLaunch &bl, uint8_t *base, int64_t n, uint32_t entry_size)
+{
+    (void)entry_size;
+    const size_t cap = (size_t)(n / (kShortSeg + 1) + 1);
+    uint8_t *p = base;
+    auto take = [&](size_t bytes) {
+        uint8_t *r = p;
+        p += align256(bytes);
+        return r;
+    };
+    bl.seg_fallback = reinterpret_cast<uint32_t *>(take(4 * cap));
+    bl.seg_of = reinterpret_cast<uint32_t *>(take(4 * (size_t)n));
+    bl.seg_start = reinterpret_cast<uint32_t *>(take(4 * cap));
+    bl.seg_len = reinterpret_cast<uint32_t *>(take(4 * cap));
+    bl.seg_count = reinterpret_cast<uint32_t *>(take(8));
+    bl.seg_meta = take(sizeof(Meta) * cap * (kMaxRounds + 1));
+    bl.seg_mut = reinterpret_cast<uint32_t *>(take(4 * cap * kMaxRounds));
+    bl.seg_done = take(cap);
+    bl.seg_snap = p;
+    bl.seg_cap = (uint32_t)cap;
 }
 
 int launch_batch(const BatchLaunch &bl, hipStream_t s)
@@ -575,11 +632,23 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     if (sort_pairs(bl.sort_tmp, bl.sort_tmp_bytes, bl.keys_a, bl.keys_b, bl.vals_a, bl.vals_b, n, bl.key_bits, s))
         return -2;
     SegmentArgs sa;
+    sa.st.start = bl.seg_start;
+    sa.st.len = bl.seg_len;
+    sa.st.count = bl.seg_count;
+    sa.st.fallback = bl.seg_fallback;
+    sa.st.lidx = bl.keys_a;  // the sort's input keys are free again
+    sa.st.seg_of = bl.seg_of;
+    sa.st.meta = reinterpret_cast<Meta *>(bl.seg_meta);
+    sa.st.mut = bl.seg_mut;
+    sa.st.done = bl.seg_done;
+    sa.st.snap = bl.seg_snap;
+    sa.st.cap = bl.seg_cap;
     sa.elems = bl.elems;
     sa.log = bl.log;
     sa.rw = bl.rw;
     sa.keys = bl.keys_b;
     sa.vals = bl.vals_b;
+    sa.error_flags = bl.error_flags;
     sa.g = bl.g;
     sa.n = n;
     sa.rw_stride = bl.rw_stride;
@@ -589,44 +658,32 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     sa.skip_key = bl.skip_key;
     sa.g_membership = bl.g_membership;
     sa.w_ack_init = bl.w_ack_init;
-    sa.long_start = bl.long_start;
-    sa.long_len = bl.long_len;
-    sa.long_count = bl.long_count;
-    sa.list_cap = bl.list_cap;
-    if (hipMemsetAsync(bl.long_count, 0, 2 * sizeof(uint32_t), s) != hipSuccess) return -3;
-    LongArgs la2;
-    la2.elems = bl.elems;
-    la2.log = bl.log;
-    la2.rw = bl.rw;
-    la2.keys = bl.keys_b;
-    la2.vals = bl.vals_b;
-    la2.long_start = bl.long_start;
-    la2.long_len = bl.long_len;
-    la2.long_count = bl.long_count;
-    la2.list_cap = bl.list_cap;
-    la2.error_flags = bl.error_flags;
-    la2.g = bl.g;
-    la2.rw_stride = bl.rw_stride;
-    la2.stride = bl.stride;
-    la2.esz = bl.esz;
-    la2.type = bl.type;
-    la2.g_membership = bl.g_membership;
-    la2.w_ack_init = bl.w_ack_init;
-    // grids sized by how many segments each tier can hold at most
-    int64_t max_hot = n / (kMidSeg + 1) + 1, max_mid = n / (kShortSeg + 1) + 1;
-    const unsigned lgrid = (unsigned)(max_hot < 256 ? max_hot : 256);
-    const unsigned wgrid = (unsigned)((max_mid + 3) / 4 < 2048 ? (max_mid + 3) / 4 : 2048);
-#define HKV_LAUNCH_SEG(T, V)                                                                       \
-    do {                                                                                           \
-        hipLaunchKernelGGL((k_segment_exec<T, V>), dim3(grid), dim3(256), 0, s, sa);               \
-        hipLaunchKernelGGL((k_wave_exec<T, V>), dim3(wgrid), dim3(256), 0, s, la2);               \
-        hipLaunchKernelGGL((k_long_exec<T, V>), dim3(lgrid), dim3(kLongThreads), 0, s, la2);      \
+    if (hipMemsetAsync(bl.seg_count, 0, 2 * sizeof(uint32_t), s) != hipSuccess) return -3;
+    {
+        HeadIter it(rocprim::counting_iterator<uint32_t>(0), LongHeadFlag{bl.keys_b, bl.skip_key, (uint32_t)n});
+        size_t tb = bl.sort_tmp_bytes;
+        if (rocprim::inclusive_scan(bl.sort_tmp, tb, it, bl.keys_a, (size_t)n, rocprim::plus<uint32_t>(), s) !=
+            hipSuccess)
+            return -2;
+    }
+    const int64_t max_long = n / (kShortSeg + 1) + 1;
+    const unsigned sgrid = (unsigned)((max_long + 255) / 256);
+#define HKV_LAUNCH_SEG(T, V)                                                                        \
+    do {                                                                                            \
+        hipLaunchKernelGGL((k_segment_exec<T, V>), dim3(grid), dim3(256), 0, s, sa);                \
+        hipLaunchKernelGGL(k_seg_map, dim3(grid), dim3(256), 0, s, sa);                             \
+        for (int r = 0; r < kMaxRounds; ++r) {                                                      \
+            hipLaunchKernelGGL((k_round_cand<T>), dim3(grid), dim3(256), 0, s, sa, r);              \
+            hipLaunchKernelGGL((k_round_apply<T, V>), dim3(sgrid), dim3(256), 0, s, sa, r);         \
+        }                                                                                           \
+        hipLaunchKernelGGL((k_round_resolve<T, V>), dim3(grid), dim3(256), 0, s, sa);               \
+        hipLaunchKernelGGL((k_long_exec<T, V>), dim3(64), dim3(kLongThreads), 0, s, sa);            \
     } while (0)
-#define HKV_LAUNCH_SV(T)                                      \
-    do {                                                      \
-        if (bl.g.st_value == 31) HKV_LAUNCH_SEG(T, 31);       \
+#define HKV_LAUNCH_SV(T)                                       \
+    do {                                                       \
+        if (bl.g.st_value == 31) HKV_LAUNCH_SEG(T, 31);        \
         else if (bl.g.st_value == 287) HKV_LAUNCH_SEG(T, 287); \
-        else HKV_LAUNCH_SEG(T, 0);                            \
+        else HKV_LAUNCH_SEG(T, 0);                             \
     } while (0)
     switch (bl.type) {
     case kLocal: HKV_LAUNCH_SV(kLocal); break;

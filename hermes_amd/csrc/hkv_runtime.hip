@@ -31,7 +31,7 @@ struct hkv_table {
     int key_bits = 0;
     // batch scratch
     uint32_t *d_keys_a = nullptr, *d_keys_b = nullptr, *d_vals_a = nullptr, *d_vals_b = nullptr;
-    uint32_t *d_long = nullptr;        // [count | starts... | lens...] hot-key work list
+    uint8_t *d_seg = nullptr;          // long-segment round state (seg_carve)
     unsigned int *d_error_flags = nullptr;
     int64_t scratch_n = 0;
     void *d_sort_tmp = nullptr;
@@ -137,14 +137,15 @@ static int ensure_scratch(hkv_table *t, int64_t n, int key_bits)
         hipFree(t->d_keys_b);
         hipFree(t->d_vals_a);
         hipFree(t->d_vals_b);
-        hipFree(t->d_long);
-        t->d_keys_a = t->d_keys_b = t->d_vals_a = t->d_vals_b = t->d_long = nullptr;
+        hipFree(t->d_seg);
+        t->d_keys_a = t->d_keys_b = t->d_vals_a = t->d_vals_b = nullptr;
+        t->d_seg = nullptr;
         t->scratch_n = 0;
         HIP_TRY(hipMalloc(&t->d_keys_a, cap * 4));
         HIP_TRY(hipMalloc(&t->d_keys_b, cap * 4));
         HIP_TRY(hipMalloc(&t->d_vals_a, cap * 4));
         HIP_TRY(hipMalloc(&t->d_vals_b, cap * 4));
-        HIP_TRY(hipMalloc(&t->d_long, (4 * (cap / 4 + 2) + 64) * 4));
+        HIP_TRY(hipMalloc(&t->d_seg, seg_scratch_bytes(cap, t->geo.entry_size)));
         t->scratch_n = cap;
     }
     size_t need = sort_temp_bytes(t->scratch_n, key_bits > 0 ? key_bits : 32);
@@ -237,7 +238,7 @@ int hkv_table_destroy(hkv_table *t)
     hipFree(t->d_keys_b);
     hipFree(t->d_vals_a);
     hipFree(t->d_vals_b);
-    hipFree(t->d_long);
+    hipFree(t->d_seg);
     hipFree(t->d_error_flags);
     hipFree(t->d_sort_tmp);
     hipFree(t->d_ns_idx);
@@ -352,11 +353,7 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.vals_b = t->d_vals_b;
     bl.sort_tmp = t->d_sort_tmp;
     bl.sort_tmp_bytes = t->sort_tmp_bytes;
-    // d_long = [counts (64) | starts (2*cap) | lens (2*cap)], cap = scratch_n / 4 + 2
-    bl.list_cap = (uint32_t)(t->scratch_n / 4 + 2);
-    bl.long_count = t->d_long;
-    bl.long_start = t->d_long + 64;
-    bl.long_len = t->d_long + 64 + 2 * (int64_t)bl.list_cap;
+    seg_carve(bl, t->d_seg, t->scratch_n, t->geo.entry_size);
     bl.error_flags = t->d_error_flags;
     bl.n = n;
     bl.n_batches = d->n_batches;

@@ -109,14 +109,46 @@ __global__ void k_gen_trace(uint64_t *tkey, uint8_t *top, uint32_t *tid, int32_t
 }
 
 // refill_ops, inline-util.h:149-303 (hot-key coalescing and latency probes off)
+constexpr int kStripes = (HKV_WL_COUNTER_WORDS - HKV_WL_STRIPE_BASE) / 16;
+
+// folds the refill stripes into counters[0..2] and clears them
+__global__ __launch_bounds__(256) void k_fold_counters(unsigned long long *counters)
+{
+    __shared__ unsigned long long part[4][3];
+    unsigned long long v[3] = {0, 0, 0};
+    for (int s = threadIdx.x; s < kStripes; s += 256) {
+        unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + s * 16;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            v[k] += stripe[k];
+            stripe[k] = 0;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_down(v[k], o, 64);
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6][k] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) counters[threadIdx.x] += part[0][threadIdx.x] + part[1][threadIdx.x] +
+                                                 part[2][threadIdx.x] + part[3][threadIdx.x];
+}
+
+// The worker's op slab (stride * op_size contiguous bytes) is staged through LDS so HBM sees
+// full-width coalesced reads and writes; the per-op byte edits then happen in LDS.
 __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, uint32_t op_size, uint32_t st_value,
                                                 uint32_t shift, const uint64_t *tkey, const uint8_t *top,
                                                 int32_t tlen, uint32_t *cursor, uint32_t machine_id,
                                                 int32_t first_iter, int32_t refill_all, unsigned long long *counters)
 {
+    extern __shared__ uint64_t slab[];
     const int w = blockIdx.x, i = threadIdx.x;
     const bool live = i < stride;
-    uint8_t *op = ops + ((int64_t)w * stride + i) * op_size;
+    uint64_t *gslab = reinterpret_cast<uint64_t *>(ops + (int64_t)w * stride * op_size);
+    const int words = (int)((uint32_t)stride * op_size / 8u);
+    for (int k = i; k < words; k += 256) slab[k] = gslab[k];
+    __syncthreads();
+    uint8_t *op = reinterpret_cast<uint8_t *>(slab) + (uint32_t)i * op_size;
     uint8_t st = live ? op[9] : 0;
     const bool complete = st == kMiss || st == kPutComplete || st == kRmwAbort || st == kRmwComplete ||
                           st == kOpMembComplete || st == kGetComplete;
@@ -130,23 +162,27 @@ __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, ui
     int c = block_sum(commits), m = block_sum(misses), wr = block_sum(writes);
     if (i == 0) {
         cursor[w] = (uint32_t)((base + (uint32_t)total) % (uint32_t)tlen);
-        if (c) atomicAdd(&counters[0], (unsigned long long)c);
-        if (m) atomicAdd(&counters[1], (unsigned long long)m);
-        if (wr) atomicAdd(&counters[2], (unsigned long long)wr);
+        unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + (w % kStripes) * 16;
+        if (c) atomicAdd(&stripe[0], (unsigned long long)c);
+        if (m) atomicAdd(&stripe[1], (unsigned long long)m);
+        if (wr) atomicAdd(&stripe[2], (unsigned long long)wr);
     }
-    if (!done) return;
-    int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)rank) % (uint32_t)tlen);
-    uint8_t oc = top[t];
-    *reinterpret_cast<uint64_t *>(op) = tkey[t];
-    op[8] = oc;
-    op[9] = kNew;
-    op[10] = oc == kOpGet ? 0 : (uint8_t)(st_value >> shift);
-    uint16_t flags = (uint16_t)((oc == kOpRmw ? 1u : 0u) | (first_iter ? 0u : 2u));  // RMW_flag, no_coales = 1
-    *reinterpret_cast<uint16_t *>(op + 16) = flags;
-    if (oc != kOpGet) {
-        uint8_t v = (uint8_t)('a' + machine_id);
-        for (uint32_t k = 0; k < st_value; ++k) op[kOpValueOff + k] = v;
+    if (done) {
+        int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)rank) % (uint32_t)tlen);
+        uint8_t oc = top[t];
+        *reinterpret_cast<uint64_t *>(op) = tkey[t];
+        op[8] = oc;
+        op[9] = kNew;
+        op[10] = oc == kOpGet ? 0 : (uint8_t)(st_value >> shift);
+        uint16_t flags = (uint16_t)((oc == kOpRmw ? 1u : 0u) | (first_iter ? 0u : 2u));  // RMW_flag, no_coales = 1
+        *reinterpret_cast<uint16_t *>(op + 16) = flags;
+        if (oc != kOpGet) {
+            uint8_t v = (uint8_t)('a' + machine_id);
+            for (uint32_t k = 0; k < st_value; ++k) op[kOpValueOff + k] = v;
+        }
     }
+    __syncthreads();
+    for (int k = i; k < words; k += 256) gslab[k] = slab[k];
 }
 
 // wings_issue_pkts(inv) with the INV callbacks of hermes_worker.c:12-65
@@ -282,9 +318,15 @@ int hkv_wl_refill(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_s
                   const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor, uint32_t machine_id,
                   int32_t first_iter, int32_t refill_all, unsigned long long *counters, void *stream)
 {
-    if (stride > 256 || n_workers <= 0) return -1;
-    hipLaunchKernelGGL(k_refill, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, st_value,
+    if (stride > 256 || n_workers <= 0 || op_size % 8) return -1;
+    const size_t lds = (size_t)stride * op_size;
+    if (lds > 160 * 1024 - 64) return -1;
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void *)k_refill, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return -1;
+    hipLaunchKernelGGL(k_refill, dim3(n_workers), dim3(256), lds, (hipStream_t)stream, ops, stride, op_size, st_value,
                        shift, tkey, top, tlen, cursor, machine_id, first_iter, refill_all, counters);
+    hipLaunchKernelGGL(k_fold_counters, dim3(1), dim3(256), 0, (hipStream_t)stream, counters);
     return ok();
 }
 

@@ -100,7 +100,7 @@ class Round:
         self.rstride = self.rpp * max(self.R, 1)
         self.ack_out = torch.zeros(W * self.rstride * self.ack_size, **u8)
         self.cursor = torch.zeros(W, dtype=torch.int32, device=dev)
-        self.counters = torch.zeros(4, dtype=torch.int64, device=dev)
+        self.counters = torch.zeros(4096, dtype=torch.int64, device=dev)  # HKV_WL_COUNTER_WORDS
         self.inv_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.peer_t = torch.tensor(self.peers or [0], dtype=torch.uint8, device=dev)
         self.trace_len = trace_len

@@ -45,7 +45,12 @@ int hkv_wl_gen_trace(uint64_t *d_trace_key, uint8_t *d_trace_op, uint32_t *d_tra
  * complete take the next trace command of their worker (all slots when first_iter, or when
  * refill_all: then stalled ops are dropped instead of retried -- one fresh batch per round).
  * Adds completed-and-committed ops (everything complete except ST_MISS and ST_RMW_ABORT)
- * to d_counters[0], misses to d_counters[1], completed writes to d_counters[2]. */
+ * to d_counters[0], misses to d_counters[1], completed writes to d_counters[2].
+ * d_counters holds HKV_WL_COUNTER_WORDS words, zeroed by the caller once: words from
+ * HKV_WL_STRIPE_BASE on are per-worker-group partial sums the call folds back into [0..2]
+ * (one counter address hit by every worker serialises in L2). */
+#define HKV_WL_COUNTER_WORDS 4096
+#define HKV_WL_STRIPE_BASE 64
 int hkv_wl_refill(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint32_t st_value,
                   uint32_t shift, const uint64_t *d_trace_key, const uint8_t *d_trace_op, int32_t trace_len,
                   uint32_t *d_cursor, uint32_t machine_id, int32_t first_iter, int32_t refill_all,

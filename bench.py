@@ -33,8 +33,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--keys", type=int, default=100_000_000)
-    p.add_argument("--workers", type=int, default=4096, help="virtual workers (250-op buffers) per GPU")
+    p.add_argument("--keys", type=int, default=None,
+                   help="keys per replica (default: 100M at N=1, configs[1]; 1B at N>1, configs[3])")
+    p.add_argument("--workers", type=int, default=8192, help="virtual workers (250-op buffers) per GPU")
     p.add_argument("--zipf", type=float, default=0.99)
     p.add_argument("--write-permille", type=int, default=200)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (0 = skip)")
@@ -61,6 +62,8 @@ def main():
     from hermes_amd.kvs import HermesKV, sized_geometry
     from hermes_amd.workload import Round, zipf_params
 
+    if a.keys is None:
+        a.keys = 100_000_000 if world == 1 else 1_000_000_000
     t0 = time.time()
     bkts, cap = sized_geometry(a.keys)
     kvs = HermesKV(a.keys, bkts, cap, machine_id=rank if world > 1 else 0, device=local_rank)
@@ -77,7 +80,8 @@ def main():
 
     if world > 1:
         from hermes_amd.replica_group import ReplicaGroupRound
-        rnd = ReplicaGroupRound(kvs, a.workers, z, a.write_permille, seed=a.seed, world=world, rank=rank)
+        rnd = ReplicaGroupRound(kvs, a.workers, z, a.write_permille, seed=a.seed, world=world, rank=rank,
+                                retry_stalled=a.retry)
     else:
         rnd = Round(kvs, a.workers, L.membership(3, 0), [1, 2], z, a.write_permille, seed=a.seed,
                     max_steps=total_steps + 1, retry_stalled=a.retry)
@@ -88,7 +92,8 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    c0 = rnd.counters.clone()
+    c0 = rnd.counters[:4].clone()
+    e0 = rnd.elem_totals.clone()
     inv0 = rnd.inv_total.clone() if hasattr(rnd, "inv_total") else None
     events: dict = {}
     torch.cuda.synchronize()
@@ -103,7 +108,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t
-    c1 = rnd.counters.clone()
+    c1 = rnd.counters[:4].clone()
+    e1 = rnd.elem_totals.clone()
+    n_inv, n_ack, n_val = ((e1 - e0).double() / a.steps).tolist()
     committed = int((c1[0] - c0[0]).item())
     writes = int((c1[2] - c0[2]).item())
     puts_ok = int((rnd.inv_total - inv0).item()) if inv0 is not None else writes
@@ -122,9 +129,9 @@ def main():
     W, S = a.workers, Round.LOCAL
     per_launch_bytes = {
         "local": W * S * BYTES["get"] + (puts_ok / a.steps) * (BYTES["put"] - BYTES["get"]),
-        "invs": W * rnd.rstride * BYTES["inv"],
-        "acks": (puts_ok / a.steps) * rnd.R * BYTES["ack"],
-        "vals": W * rnd.rstride * BYTES["val"],
+        "invs": n_inv * BYTES["inv"],
+        "acks": n_ack * BYTES["ack"],
+        "vals": n_val * BYTES["val"],
     }
     dom = max(ms, key=ms.get) if ms else "local"
     ach = per_launch_bytes[dom] / (ms[dom] / 1e3) / 1e9 if ms else 0.0
@@ -149,6 +156,7 @@ def main():
             "keys": a.keys, "buckets": bkts, "log_cap": cap, "workers_per_gpu": W,
             "local_batch": S, "zipf": a.zipf, "write_permille": a.write_permille,
             "remote_invs_per_worker": rnd.rstride, "parallelism": f"replicas{world}",
+            "elements_per_step": {"inv": n_inv, "ack": n_ack, "val": n_val},
         },
         "roofline": {
             "bound": "hbm", "kernel": f"{dom} batch (k_lookup + radix sort + k_segment_exec)",

@@ -185,9 +185,12 @@ __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, ui
     for (int k = i; k < words; k += 256) gslab[k] = slab[k];
 }
 
-// wings_issue_pkts(inv) with the INV callbacks of hermes_worker.c:12-65
+// wings_issue_pkts(inv) with the INV callbacks of hermes_worker.c:12-65. At most out_stride
+// INVs per worker go out per round (the send credits); the rest keep their state and are
+// sent by a later round, as with the reference's credit-limited wings sends.
 __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stride, uint32_t op_size, uint8_t *out,
-                                                      int32_t *count, uint32_t machine_id)
+                                                      int32_t out_stride, int32_t *count, uint32_t machine_id,
+                                                      unsigned long long *held)
 {
     const int w = blockIdx.x, i = threadIdx.x;
     const bool live = i < stride;
@@ -196,9 +199,12 @@ __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stri
     bool send = live && (st == kPutSuccess || st == kRmwSuccess || st == kReplaySuccess || st == kOpMembChange);
     int total;
     int rank = block_rank(send, total);
-    if (i == 0) count[w] = total;
-    if (!send) return;
-    uint8_t *dst = out + ((int64_t)w * stride + rank) * op_size;
+    if (i == 0) {
+        count[w] = total < out_stride ? total : out_stride;
+        if (total > out_stride && held) atomicAdd(held, (unsigned long long)(total - out_stride));
+    }
+    if (!send || rank >= out_stride) return;
+    uint8_t *dst = out + ((int64_t)w * out_stride + rank) * op_size;
     const uint64_t *s64 = reinterpret_cast<const uint64_t *>(op);
     uint64_t *d64 = reinterpret_cast<uint64_t *>(dst);
     for (uint32_t k = 0; k < op_size / 8; ++k) d64[k] = s64[k];
@@ -206,6 +212,87 @@ __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stri
     dst[8] = kOpInv;
     op[9] = st == kPutSuccess ? kInProgressPut : st == kRmwSuccess ? kInProgressRmw
           : st == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
+}
+
+// ACKs for received INV rows: row r holds in_count[r] INVs (row stride C); its ACKs are
+// compacted to the front of output row r (ack_skip_or_get_sender_id + ack_copy_and_modify_elem
+// + ack_modify_elem_after_send, hermes_worker.c:67-110)
+__global__ __launch_bounds__(256) void k_marshal_acks_rows(uint8_t *invs, const int32_t *in_count, int32_t C,
+                                                           uint32_t op_size, uint8_t *out, uint32_t ack_size,
+                                                           int32_t *out_count, uint32_t machine_id)
+{
+    const int64_t r = blockIdx.x;
+    const int n = in_count[r];
+    int base = 0;
+    for (int j0 = 0; j0 < n; j0 += 256) {
+        const int j = j0 + (int)threadIdx.x;
+        uint8_t *x = invs + (r * C + j) * (int64_t)op_size;
+        const uint8_t oc = j < n ? x[8] : 0;
+        const bool send = j < n && (oc == kInvSuccess || (oc == kOpInvAbort && ack_size >= op_size));
+        int total;
+        const int rank = block_rank(send, total);
+        if (send) {
+            uint8_t *y = out + (r * C + base + rank) * (int64_t)ack_size;
+            const uint32_t words = (oc == kInvSuccess ? kOpMetaSize : op_size) / 8;
+            for (uint32_t k = 0; k < words; ++k)
+                reinterpret_cast<uint64_t *>(y)[k] = reinterpret_cast<const uint64_t *>(x)[k];
+            y[9] = (uint8_t)machine_id;
+            y[8] = oc == kInvSuccess ? kOpAck : kOpInvAbort;
+        }
+        if (j < n && (oc == kInvSuccess || oc == kOpInvAbort || oc == kOpMembChange)) x[8] = kEmpty;
+        base += total;
+    }
+    if (threadIdx.x == 0) out_count[r] = base;
+}
+
+// [P][W][C] rows with counts[P][W] -> per-worker batches [W][out_stride], peers' elements
+// back to back (one worker's receive poll over all peers)
+__global__ __launch_bounds__(256) void k_regroup(const uint8_t *in, const int32_t *counts, int32_t P, int32_t W,
+                                                 int32_t C, uint32_t esz, uint8_t *out, int32_t out_stride,
+                                                 int32_t *out_count)
+{
+    const int w = blockIdx.x;
+    int off = 0;
+    for (int p = 0; p < P; ++p) {
+        const int n = counts[(int64_t)p * W + w];
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(in + ((int64_t)p * W + w) * C * esz);
+        uint64_t *dst = reinterpret_cast<uint64_t *>(out + ((int64_t)w * out_stride + off) * esz);
+        const int words = (int)((uint32_t)n * esz / 8u);
+        for (int k = threadIdx.x; k < words; k += 256) dst[k] = src[k];
+        off += n;
+    }
+    if (threadIdx.x == 0) out_count[w] = off;
+}
+
+// VALs of the writes an ACK batch completed (ST_LAST_ACK_SUCCESS), compacted per worker into
+// [W][C]; the ACK elements become ST_EMPTY (hermes_worker.c:112-160)
+__global__ __launch_bounds__(256) void k_collect_vals(uint8_t *acks, const int32_t *count, int32_t stride,
+                                                      uint32_t ack_size, uint8_t *out, int32_t C, int32_t *out_count,
+                                                      uint32_t machine_id, unsigned long long *held)
+{
+    const int64_t w = blockIdx.x;
+    const int n = count[w];
+    int base = 0;
+    for (int j0 = 0; j0 < n; j0 += 256) {
+        const int j = j0 + (int)threadIdx.x;
+        uint8_t *x = acks + (w * stride + j) * (int64_t)ack_size;
+        const uint8_t oc = j < n ? x[8] : 0;
+        const bool send = j < n && oc == kLastAckSuccess;
+        int total;
+        const int rank = block_rank(send, total);
+        if (send && base + rank < C) {
+            uint64_t *y = reinterpret_cast<uint64_t *>(out + (w * C + base + rank) * (int64_t)kOpMetaSize);
+            y[0] = reinterpret_cast<const uint64_t *>(x)[0];
+            uint64_t h = reinterpret_cast<const uint64_t *>(x)[1];
+            y[1] = (h & ~0xFFFFull) | kOpVal | ((uint64_t)(machine_id & 0xFF) << 8);
+        }
+        if (j < n && (oc == kLastAckSuccess || oc == kAckSuccess || oc == kOpMembChange)) x[8] = kEmpty;
+        base += total;
+    }
+    if (threadIdx.x == 0) {
+        out_count[w] = base < C ? base : C;
+        if (base > C && held) atomicAdd(held, (unsigned long long)(base - C));
+    }
 }
 
 __global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32_t inv_stride, uint32_t op_size,
@@ -335,7 +422,7 @@ int hkv_wl_marshal_invs(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_
 {
     if (stride > 256 || n_workers <= 0) return -1;
     hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
-                       count, machine_id);
+                       stride, count, machine_id, (unsigned long long *)nullptr);
     return ok();
 }
 
@@ -376,6 +463,47 @@ int hkv_wl_gen_remote(uint8_t *invs, uint8_t *vals, int32_t n_workers, int32_t p
     if (total <= 0) return 0;
     hipLaunchKernelGGL(k_gen_remote, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, invs, vals, per_peer,
                        peer_ids, n_peers, op_size, st_value, shift, *z, clock, seed, total);
+    return ok();
+}
+
+int hkv_wl_marshal_invs_cap(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint8_t *out,
+                            int32_t out_stride, int32_t *count, uint32_t machine_id, unsigned long long *held,
+                            void *stream)
+{
+    if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
+    hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
+                       out_stride, count, machine_id, held);
+    return ok();
+}
+
+int hkv_wl_marshal_acks_rows(uint8_t *invs, const int32_t *in_count, int32_t rows, int32_t C, uint32_t op_size,
+                             uint8_t *out, uint32_t ack_size, int32_t *out_count, uint32_t machine_id, void *stream)
+{
+    if (rows <= 0) return 0;
+    if (C <= 0 || op_size % 8 || ack_size % 8) return -1;
+    hipLaunchKernelGGL(k_marshal_acks_rows, dim3(rows), dim3(256), 0, (hipStream_t)stream, invs, in_count, C, op_size,
+                       out, ack_size, out_count, machine_id);
+    return ok();
+}
+
+int hkv_wl_regroup(const uint8_t *in, const int32_t *counts, int32_t n_peers, int32_t n_workers, int32_t C,
+                   uint32_t elem_size, uint8_t *out, int32_t out_stride, int32_t *out_count, void *stream)
+{
+    if (n_workers <= 0) return 0;
+    if (n_peers <= 0 || C <= 0 || elem_size % 8 || out_stride < n_peers * C) return -1;
+    hipLaunchKernelGGL(k_regroup, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, in, counts, n_peers, n_workers,
+                       C, elem_size, out, out_stride, out_count);
+    return ok();
+}
+
+int hkv_wl_collect_vals(uint8_t *acks, const int32_t *count, int32_t n_workers, int32_t stride, uint32_t ack_size,
+                        uint8_t *out, int32_t C, int32_t *out_count, uint32_t machine_id, unsigned long long *held,
+                        void *stream)
+{
+    if (n_workers <= 0) return 0;
+    if (C <= 0 || ack_size % 8) return -1;
+    hipLaunchKernelGGL(k_collect_vals, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, acks, count, stride,
+                       ack_size, out, C, out_count, machine_id, held);
     return ok();
 }
 

@@ -69,11 +69,12 @@ def make_config(num_keys: int = 1_000_000, num_bkts: int = 2 * 1024 * 1024, log_
 
 def sized_geometry(num_keys: int, sizes: L.Sizes = L.DEFAULT) -> tuple[int, int]:
     """Buckets and log capacity for `num_keys` (powers of two; about 2 keys per bucket as in
-    the reference's 1M keys / 2^21 buckets, and a log that never wraps)."""
+    the reference's 1M keys / 2^21 buckets, at most 2^27 buckets up to 2^28 keys and 2^29
+    beyond (1B keys per replica: 32 GiB of index), and a log that never wraps)."""
     bkts = 1 << max(4, (2 * num_keys - 1).bit_length())
     need = num_keys * sizes.entry + sizes.kvs_value + 64
     cap = 1 << max(16, (need - 1).bit_length())
-    return min(bkts, 1 << 27), cap
+    return min(bkts, 1 << (27 if num_keys <= 1 << 28 else 29)), cap
 
 
 class HermesKV:

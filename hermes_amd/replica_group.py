@@ -1,0 +1,255 @@
+"""A Hermes replica group with one replica per GPU.
+
+Hermes replicates every key on every node, so N GPUs form an N-replica group (N <= 8: the
+membership bit vectors are 8 bits wide, spacetime.h:188-195). The wings RDMA layer
+(wings.h:770-916) becomes three collectives per protocol round, on torch's current stream so
+they order with the batch kernels without host synchronisation:
+
+  1. all-gather of fixed-capacity INV slabs: worker w of every replica sends at most C INVs
+     per round (C = the send credits, sized so a round's writes fit); [N][W][C] x op_size
+  2. every replica applies its peers' INVs as one INV batch launch (n_batches = N*W, its own
+     row masked out by a zero count), then ACKs (INV-aborts with RMWs) go back to the
+     coordinators with an all-to-all: row p of the ACK slab holds rank p's ACKs
+  3. coordinators regroup the ACKs per worker (one receive poll over all peers), apply them as
+     an ACK batch against the worker's op buffer (read_write_ops), and all-gather the VALs of
+     the writes that completed; every replica applies its peers' VALs as one VAL batch.
+
+Per-worker counts travel with each slab in a second (small) collective. `ReplicaRound` holds
+one replica's buffers and phases; `ReplicaGroupRound` drives one replica per process over
+torch.distributed (RCCL); `LoopbackGroup` drives N replicas in one process (tests: the same
+phases and kernels, with the collectives done by tensor copies).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import layout as L
+from .kvs import HermesKV
+from .lib import check, raw
+from .workload import HkvZipf, _ptr, _s
+
+_L = raw()
+_P = ctypes.c_void_p
+_L.hkv_wl_marshal_invs_cap.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
+                                       ctypes.c_uint32, _P, _P]
+_L.hkv_wl_marshal_acks_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P,
+                                        ctypes.c_uint32, _P, ctypes.c_uint32, _P]
+_L.hkv_wl_regroup.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P,
+                              ctypes.c_int32, _P, _P]
+_L.hkv_wl_collect_vals.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
+                                   _P, ctypes.c_uint32, _P, _P]
+
+MAX_REPLICAS = 8
+LOCAL = 250  # MAX_BATCH_KVS_OPS_SIZE, config.h:42
+
+
+def slots_per_worker(write_permille: int, rmw_permille: int = 0, batch: int = LOCAL) -> int:
+    """INV slots per worker and round (the send credits): the mean number of writes in a
+    250-op batch plus 8 standard deviations, rounded up to 8, at most the batch. Writes beyond
+    it stay in PUT_SUCCESS and go out in a later round (counted in `held`)."""
+    p = min(1.0, write_permille / 1000.0)
+    mean = batch * p
+    sd = math.sqrt(batch * p * (1 - p))
+    c = int(math.ceil((mean + 8 * sd + 1) / 8.0) * 8)
+    return max(8, min(batch, c))
+
+
+class ReplicaRound:
+    """Buffers and phases of one replica (machine id = rank) of an N-replica group."""
+
+    def __init__(self, kvs: HermesKV, n_workers: int, world: int, rank: int, zipf: HkvZipf,
+                 write_permille: int = 200, rmw_permille: int = 0, seed: int = 0x5EED,
+                 trace_len: int = 8192, retry_stalled: bool = False, slots: int | None = None):
+        if not 2 <= world <= MAX_REPLICAS:
+            raise ValueError(f"a replica group has 2..{MAX_REPLICAS} replicas, got {world}")
+        if kvs.machine_id != rank:
+            raise ValueError("the replica's table must use machine_id == rank")
+        self.kvs, self.W, self.N, self.rank = kvs, n_workers, world, rank
+        self.sizes = kvs.sizes
+        self.op = kvs.sizes.op
+        self.ack_size = self.op if kvs.rmw else L.OP_META_SIZE
+        self.mb = L.membership(world, rank)
+        self.retry = retry_stalled
+        self.C = slots or slots_per_worker(write_permille, rmw_permille)
+        W, N, C = n_workers, world, self.C
+        dev = torch.device("cuda", kvs.device)
+        u8 = dict(dtype=torch.uint8, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.ops = torch.zeros(W * LOCAL * self.op, **u8)
+        self.inv_slab = torch.zeros(W * C * self.op, **u8)
+        self.inv_count = torch.zeros(W, **i32)
+        self.inv_recv = torch.zeros(N * W * C * self.op, **u8)
+        self.inv_recv_count = torch.zeros(N * W, **i32)
+        self.ack_slab = torch.zeros(N * W * C * self.ack_size, **u8)
+        self.ack_slab_count = torch.zeros(N * W, **i32)
+        self.ack_recv = torch.zeros(N * W * C * self.ack_size, **u8)
+        self.ack_recv_count = torch.zeros(N * W, **i32)
+        self.ack_batch = torch.zeros(W * N * C * self.ack_size, **u8)
+        self.ack_batch_count = torch.zeros(W, **i32)
+        self.val_slab = torch.zeros(W * C * L.OP_META_SIZE, **u8)
+        self.val_count = torch.zeros(W, **i32)
+        self.val_recv = torch.zeros(N * W * C * L.OP_META_SIZE, **u8)
+        self.val_recv_count = torch.zeros(N * W, **i32)
+        self.held = torch.zeros(2, dtype=torch.int64, device=dev)    # INVs held back, VALs dropped
+        self.cursor = torch.zeros(W, **i32)
+        self.counters = torch.zeros(4096, dtype=torch.int64, device=dev)  # HKV_WL_COUNTER_WORDS
+        self.inv_total = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.elem_totals = torch.zeros(3, dtype=torch.int64, device=dev)  # INV, ACK, VAL elements applied
+        self.trace_len = trace_len
+        self.trace_key = torch.empty(W * trace_len, dtype=torch.int64, device=dev)
+        self.trace_op = torch.empty(W * trace_len, **u8)
+        check(_L.hkv_wl_gen_trace(_ptr(self.trace_key), _ptr(self.trace_op), None, W, trace_len,
+                                  ctypes.byref(zipf), write_permille, rmw_permille,
+                                  ctypes.c_uint64(seed ^ (rank << 48)), _s()), "gen_trace")
+        self.refill(first=True)
+
+    # -- phases (all asynchronous on torch's current stream)
+    def refill(self, first: bool = False):
+        check(_L.hkv_wl_refill(_ptr(self.ops), self.W, LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
+                               _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
+                               self.rank, int(first), int(not self.retry), _ptr(self.counters), _s()), "refill")
+
+    def local(self):
+        """Local batch, then this round's INVs into the outgoing slab (inv_slab, inv_count)."""
+        self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, LOCAL, self.op, self.mb)
+        check(_L.hkv_wl_marshal_invs_cap(_ptr(self.ops), self.W, LOCAL, self.op, _ptr(self.inv_slab), self.C,
+                                         _ptr(self.inv_count), self.rank, _ptr(self.held), _s()), "marshal_invs")
+        self.inv_total += self.inv_count.sum()
+
+    def _own_row(self, counts: torch.Tensor) -> torch.Tensor:
+        return counts[self.rank * self.W:(self.rank + 1) * self.W]
+
+    def invs(self):
+        """Apply the gathered INVs of the peers (inv_recv [N][W][C], inv_recv_count [N][W]);
+        their ACKs go to ack_slab row p (for rank p), counts in ack_slab_count."""
+        self._own_row(self.inv_recv_count).zero_()
+        self.elem_totals[0] += self.inv_recv_count.sum()
+        self.kvs.batch(L.BatchType.invs, self.inv_recv, self.N * self.W, self.C, self.op, self.mb,
+                       counts=self.inv_recv_count)
+        check(_L.hkv_wl_marshal_acks_rows(_ptr(self.inv_recv), _ptr(self.inv_recv_count), self.N * self.W, self.C,
+                                          self.op, _ptr(self.ack_slab), self.ack_size, _ptr(self.ack_slab_count),
+                                          self.rank, _s()), "marshal_acks")
+
+    def acks(self):
+        """Apply the ACKs returned by the peers (ack_recv [N][W][C] from rank p in row p),
+        regrouped per worker; VALs of completed writes into val_slab / val_count."""
+        N, W, C = self.N, self.W, self.C
+        check(_L.hkv_wl_regroup(_ptr(self.ack_recv), _ptr(self.ack_recv_count), N, W, C, self.ack_size,
+                                _ptr(self.ack_batch), N * C, _ptr(self.ack_batch_count), _s()), "regroup")
+        self.elem_totals[1] += self.ack_batch_count.sum()
+        self.kvs.batch(L.BatchType.acks, self.ack_batch, W, N * C, self.ack_size, self.mb,
+                       counts=self.ack_batch_count, rw=self.ops, rw_stride_bytes=LOCAL * self.op)
+        check(_L.hkv_wl_collect_vals(_ptr(self.ack_batch), _ptr(self.ack_batch_count), W, N * C, self.ack_size,
+                                     _ptr(self.val_slab), C, _ptr(self.val_count), self.rank,
+                                     _ptr(self.held[1:]), _s()), "collect_vals")
+
+    def vals(self):
+        """Apply the gathered VALs of the peers (val_recv [N][W][C], val_recv_count [N][W])."""
+        self._own_row(self.val_recv_count).zero_()
+        self.elem_totals[2] += self.val_recv_count.sum()
+        self.kvs.batch(L.BatchType.vals, self.val_recv, self.N * self.W, self.C, L.OP_META_SIZE, self.mb,
+                       counts=self.val_recv_count)
+
+    def stats(self) -> dict:
+        c = self.counters[:3].cpu().tolist()
+        h = self.held.cpu().tolist()
+        return {"committed": c[0], "misses": c[1], "writes_completed": c[2], "invs_held": h[0], "vals_dropped": h[1]}
+
+
+def _timed(events, name, fn):
+    if events is None:
+        fn()
+        return
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    fn()
+    b.record()
+    events.setdefault(name, []).append((a, b))
+
+
+class ReplicaGroupRound:
+    """One replica per process; the exchanges are RCCL collectives (torch.distributed "nccl",
+    or any backend whose all_gather_into_tensor / all_to_all_single take these tensors)."""
+
+    LOCAL = LOCAL
+
+    def __init__(self, kvs: HermesKV | None, n_workers: int, zipf: HkvZipf | None, write_permille: int = 200, *,
+                 seed: int = 0x5EED, world: int, rank: int, group=None, replica=None, **kw):
+        """`replica`: drive an existing ReplicaRound-shaped object instead of building one."""
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.r = replica if replica is not None else ReplicaRound(kvs, n_workers, world, rank, zipf,
+                                                                  write_permille, seed=seed, **kw)
+        self.R = world - 1
+        self.rstride = self.r.C * self.R
+        self.counters = self.r.counters
+        self.inv_total = self.r.inv_total
+        self.elem_totals = self.r.elem_totals
+
+    def _gather(self, out, inp):
+        self.dist.all_gather_into_tensor(out, inp, group=self.group)
+
+    def _a2a(self, out, inp):
+        self.dist.all_to_all_single(out, inp, group=self.group)
+
+    def step(self, events: dict | None = None):
+        r = self.r
+        _timed(events, "local", r.local)
+        self._gather(r.inv_recv, r.inv_slab)
+        self._gather(r.inv_recv_count, r.inv_count)
+        _timed(events, "invs", r.invs)
+        self._a2a(r.ack_recv, r.ack_slab)
+        self._a2a(r.ack_recv_count, r.ack_slab_count)
+        _timed(events, "acks", r.acks)
+        self._gather(r.val_recv, r.val_slab)
+        self._gather(r.val_recv_count, r.val_count)
+        _timed(events, "vals", r.vals)
+        r.refill()
+
+    def stats(self) -> dict:
+        return self.r.stats()
+
+
+class LoopbackGroup:
+    """N replicas driven phase by phase in one process; the collectives are tensor copies with
+    exactly the layouts the RCCL driver produces (all-gather: row p = rank p's slab;
+    all-to-all: row p of the output = row `rank` of rank p's input)."""
+
+    def __init__(self, rounds: list[ReplicaRound]):
+        self.rounds = rounds
+        self.N = len(rounds)
+
+    @staticmethod
+    def _gather(outs, ins):
+        for o in outs:
+            torch.cat([x.to(o.device) for x in ins], out=o)
+
+    def _a2a(self, outs, ins):
+        N = self.N
+        for q, o in enumerate(outs):
+            ov = o.view(N, -1)
+            for p, x in enumerate(ins):
+                ov[p].copy_(x.view(N, -1)[q])
+
+    def step(self):
+        rs = self.rounds
+        for r in rs:
+            r.local()
+        self._gather([r.inv_recv for r in rs], [r.inv_slab for r in rs])
+        self._gather([r.inv_recv_count for r in rs], [r.inv_count for r in rs])
+        for r in rs:
+            r.invs()
+        self._a2a([r.ack_recv for r in rs], [r.ack_slab for r in rs])
+        self._a2a([r.ack_recv_count for r in rs], [r.ack_slab_count for r in rs])
+        for r in rs:
+            r.acks()
+        self._gather([r.val_recv for r in rs], [r.val_slab for r in rs])
+        self._gather([r.val_recv_count for r in rs], [r.val_count for r in rs])
+        for r in rs:
+            r.vals()
+        for r in rs:
+            r.refill()

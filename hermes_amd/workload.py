@@ -102,6 +102,7 @@ class Round:
         self.cursor = torch.zeros(W, dtype=torch.int32, device=dev)
         self.counters = torch.zeros(4096, dtype=torch.int64, device=dev)  # HKV_WL_COUNTER_WORDS
         self.inv_total = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.elem_totals = torch.zeros(3, dtype=torch.int64, device=dev)  # INV, ACK, VAL elements applied
         self.peer_t = torch.tensor(self.peers or [0], dtype=torch.uint8, device=dev)
         self.trace_len = trace_len
         self.trace_key = torch.empty(W * trace_len, dtype=torch.int64, device=dev)
@@ -188,9 +189,13 @@ class Round:
             timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride))
             self.marshal_acks(ri, self.W * self.rstride, self.ack_out)
             timed("acks", self.ack_batch)
+            self.elem_totals[1] += self.ack_count.sum()
             self.marshal_vals(self.acks, self.W * self.ack_stride, self.val_out)
             timed("vals", lambda: self.val_batch(rv, self.W, self.rstride))
         self.refill()
+        if self.R:
+            self.elem_totals[0] += self.W * self.rstride
+            self.elem_totals[2] += self.W * self.rstride
         self.clock += 1
 
     def committed(self) -> int:

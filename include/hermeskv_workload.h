@@ -87,6 +87,34 @@ int hkv_wl_gen_remote(uint8_t *d_invs, uint8_t *d_vals, int32_t n_workers, int32
                       const uint8_t *peer_ids, int32_t n_peers, uint32_t op_size, uint32_t st_value,
                       uint32_t shift, const hkv_zipf *zipf, uint32_t clock, uint64_t seed, void *stream);
 
+/* ---- replica groups (one replica per GPU, slabs exchanged over RCCL) ------------------ */
+
+/* hkv_wl_marshal_invs with at most out_stride INVs per worker per round (d_inv_out rows of
+ * out_stride); further sendable ops keep their state for a later round and are counted in
+ * *d_held (may be NULL). */
+int hkv_wl_marshal_invs_cap(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size,
+                            uint8_t *d_inv_out, int32_t out_stride, int32_t *d_inv_count, uint32_t machine_id,
+                            unsigned long long *d_held, void *stream);
+
+/* ACKs for `rows` rows of received INVs (row r: d_in_count[r] INVs at d_invs + r*C*op_size),
+ * compacted to the front of row r of d_ack_out (row stride C), d_out_count[r] ACKs; INV
+ * elements become ST_EMPTY as in hkv_wl_marshal_acks */
+int hkv_wl_marshal_acks_rows(uint8_t *d_invs, const int32_t *d_in_count, int32_t rows, int32_t C,
+                             uint32_t op_size, uint8_t *d_ack_out, uint32_t ack_size, int32_t *d_out_count,
+                             uint32_t machine_id, void *stream);
+
+/* rows [n_peers][n_workers][C] (counts [n_peers][n_workers]) -> per-worker batches
+ * [n_workers][out_stride], the peers' elements back to back in peer order */
+int hkv_wl_regroup(const uint8_t *d_in, const int32_t *d_counts, int32_t n_peers, int32_t n_workers, int32_t C,
+                   uint32_t elem_size, uint8_t *d_out, int32_t out_stride, int32_t *d_out_count, void *stream);
+
+/* VALs (16 B) for the ACK elements of per-worker ACK batches ([n_workers][stride], counts)
+ * that completed a write, compacted into [n_workers][C]; the ACK elements become ST_EMPTY as
+ * in hkv_wl_marshal_vals. VALs beyond C are dropped and counted in *d_held (may be NULL). */
+int hkv_wl_collect_vals(uint8_t *d_acks, const int32_t *d_count, int32_t n_workers, int32_t stride,
+                        uint32_t ack_size, uint8_t *d_val_out, int32_t C, int32_t *d_val_count,
+                        uint32_t machine_id, unsigned long long *d_held, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,124 @@
+"""N-replica Hermes groups on one GPU (hermes_amd.replica_group.LoopbackGroup): the phases,
+kernels and slab layouts of the RCCL group, with the collectives done by tensor copies.
+
+Two checks per round:
+* every batch launch of every replica is mirrored into an oracle table of the same replica
+  (same input bytes, same counts, same read_write_ops) and the outputs -- elements,
+  read_write_ops and the whole index + log -- must be bit-exact. This is the reference's
+  batch functions under real cross-replica traffic: conflicting writes from several
+  coordinators, cid tie-breaks, ACK quorums from real peers.
+* at the end of each round every key is VALID on every replica with the same timestamp and
+  value (Hermes' invariant after all INV/ACK/VAL exchanges of a round have been applied).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from hermes_amd import layout as L  # noqa: E402
+from oracle.oracle import OracleKVS, gen_keys  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+class Mirror:
+    """Runs every batch launch of a device table on an oracle twin and compares."""
+
+    def __init__(self, g, o, name):
+        self.g, self.o, self.name = g, o, name
+        self.launches = 0
+        self._orig = g.batch
+        g.batch = self.batch
+
+    def batch(self, btype, elems, n_batches, stride, elem_size, membership, counts=None, rw=None,
+              rw_stride_bytes=0, node_suspected=None, stream=None):
+        torch.cuda.synchronize()
+        n = n_batches * stride * elem_size
+        vt = np.dtype((np.void, elem_size))
+        e_in = elems[:n].cpu().numpy().copy().view(vt)
+        c_in = counts[:n_batches].cpu().numpy().copy() if counts is not None else None
+        rw_in = rw_op = None
+        if rw is not None:
+            rw_in = rw.cpu().numpy().copy().view(np.dtype((np.void, self.g.sizes.op)))
+        self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
+                   node_suspected, stream)
+        torch.cuda.synchronize()
+        self.o.batch_multi(int(btype), e_in, n_batches, stride, c_in, membership, rw_in,
+                           rw_stride_bytes // self.g.sizes.op if rw is not None else 0)
+        what = f"{self.name} launch {self.launches} type {int(btype)}"
+        got = elems[:n].cpu().numpy()
+        if not np.array_equal(got, e_in.view(np.uint8)):
+            bad = np.nonzero(got != e_in.view(np.uint8))[0]
+            pytest.fail(f"{what}: elements differ at {len(bad)} bytes, first elems {np.unique(bad // elem_size)[:8]}")
+        if rw is not None:
+            rw_op = rw.cpu().numpy()
+            assert np.array_equal(rw_op, rw_in.view(np.uint8)), f"{what}: read_write_ops differ"
+        gl, ol = self.g.log_bytes(), self.o.log_bytes()[: self.g.cfg.log_cap]
+        if not np.array_equal(gl, ol):
+            bad = np.nonzero(gl != ol)[0]
+            e = self.g.sizes.entry
+            pytest.fail(f"{what}: log differs in entries {np.unique(bad // e)[:8]}, "
+                        f"bytes-in-entry {np.unique(bad % e)[:16]}")
+        assert np.array_equal(self.g.index_bytes(), self.o.index_bytes()), f"{what}: index differs"
+        assert self.g.take_error_flags() == 0, f"{what}: device consistency flags"
+        self.launches += 1
+
+
+def _key_images(g, o, keys):
+    """(state, cid, version, value) of every key's log entry, via the oracle's index."""
+    log = g.log_bytes()
+    e = g.sizes.entry
+    rows = []
+    for k in keys:
+        off = o.lookup(int(k))
+        if off is None:
+            rows.append(None)
+            continue
+        ent = log[off:off + e]
+        rows.append((int(ent[18]), int(ent[23]), int(ent[24:28].view(np.uint32)[0]), ent[33:33 + g.sizes.st_value].tobytes()))
+    return rows
+
+
+@pytest.mark.parametrize("n_rep,workers,write_pm,rounds", [(2, 24, 300, 4), (3, 16, 400, 4), (4, 8, 500, 3)])
+def test_loopback_group_parity_and_convergence(n_rep, workers, write_pm, rounds):
+    from hermes_amd.kvs import HermesKV
+    from hermes_amd.replica_group import LoopbackGroup, ReplicaRound
+    from hermes_amd.workload import zipf_params
+
+    n_keys, bkts, cap = 4000, 8192, 1 << 20
+    z = zipf_params(n_keys, 0.99)
+    reps, mirrors = [], []
+    for r in range(n_rep):
+        g = HermesKV(n_keys, bkts, cap, machine_id=r)
+        o = OracleKVS(bkts, cap, r)
+        o.populate(n_keys, L.DEFAULT.kvs_value)
+        mirrors.append(Mirror(g, o, f"replica {r}"))
+        reps.append(ReplicaRound(g, workers, n_rep, r, z, write_pm, seed=77 + r, trace_len=512))
+    grp = LoopbackGroup(reps)
+    keys = gen_keys(n_keys)
+    for step in range(rounds):
+        grp.step()
+        torch.cuda.synchronize()
+        imgs = [_key_images(m.g, m.o, keys) for m in mirrors]
+        for i, k in enumerate(keys):
+            base = imgs[0][i]
+            if base is None:
+                assert all(im[i] is None for im in imgs)
+                continue
+            assert base[0] == L.State.VALID, f"round {step}: key #{i} state {base[0]} on replica 0"
+            for r in range(1, n_rep):
+                assert imgs[r][i] == base, f"round {step}: key #{i} differs between replica 0 and {r}"
+    for rep in reps:
+        st = rep.stats()
+        assert st["invs_held"] == 0 and st["vals_dropped"] == 0, st
+        assert st["committed"] > 0 and st["writes_completed"] > 0, st
+    # every write of the group was applied somewhere as an INV on every peer
+    inv_sent = sum(int(r.inv_total.item()) for r in reps)
+    inv_applied = sum(int(r.elem_totals[0].item()) for r in reps)
+    assert inv_applied == inv_sent * (n_rep - 1)

@@ -122,3 +122,68 @@ def test_loopback_group_parity_and_convergence(n_rep, workers, write_pm, rounds)
     inv_sent = sum(int(r.inv_total.item()) for r in reps)
     inv_applied = sum(int(r.elem_totals[0].item()) for r in reps)
     assert inv_applied == inv_sent * (n_rep - 1)
+
+
+def _dist_child(rank, world, port, q):
+    import os
+
+    import torch.distributed as dist
+
+    from hermes_amd.kvs import HermesKV
+    from hermes_amd.replica_group import ReplicaGroupRound
+    from hermes_amd.workload import zipf_params
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        n_keys = 4000
+        g = HermesKV(n_keys, 8192, 1 << 20, machine_id=rank)
+        drv = ReplicaGroupRound(g, 16, zipf_params(n_keys, 0.99), 400, seed=99, world=world, rank=rank,
+                                trace_len=512)
+        for _ in range(3):
+            drv.step()
+        torch.cuda.synchronize()
+        log = g.log_bytes()
+        imgs = []
+        for k in gen_keys(n_keys):
+            off = g.lookup_offset(int(k))
+            if off is None:
+                imgs.append(None)
+                continue
+            ent = log[off:off + g.sizes.entry]
+            imgs.append((int(ent[18]), int(ent[23]), int(ent[24:28].view(np.uint32)[0]), ent[33:64].tobytes()))
+        q.put((rank, imgs, drv.stats(), int(g.take_error_flags()), None))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, None, None, 0, repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_group_driver_one_gpu(world):
+    """ReplicaGroupRound itself (the driver bench.py runs over RCCL), with `world` processes
+    sharing one GPU over gloo (which takes CUDA tensors): every key converges across ranks."""
+    import socket
+
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dist_child, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+    for rank, imgs, st, flags, err in res:
+        assert err is None, f"rank {rank}: {err}"
+        assert flags == 0
+        assert st["invs_held"] == 0 and st["vals_dropped"] == 0 and st["writes_completed"] > 0, st
+    base = res[0][1]
+    for i, b in enumerate(base):
+        if b is None:
+            continue
+        assert b[0] == L.State.VALID, f"key #{i} state {b[0]}"
+        for rank, imgs, *_ in res[1:]:
+            assert imgs[i] == b, f"key #{i} differs between rank 0 and rank {rank}"

@@ -41,9 +41,43 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (0 = skip)")
     p.add_argument("--cpu-workers", type=int, default=64)
     p.add_argument("--seed", type=int, default=0x5EED)
+    p.add_argument("--host-api-seconds", type=float, default=1.0,
+                   help="time the host-pointer entry point for this long (0 = skip; N=1 only)")
     p.add_argument("--retry", action="store_true",
                    help="refill_ops semantics: stalled ops keep their slot (default: fresh batch per step)")
     return p.parse_args()
+
+
+def host_api_rate(seconds: float) -> dict:
+    """The drop-in entry point hermes_batch_ops_to_KVS on host buffers (configs[0] shape: the
+    reference's default 1M-key table, uniform keys, 5 % PUTs, 250-op local batches): every call
+    copies its batch over PCIe, runs it and copies it back. Reported beside `value`, never as it."""
+    import numpy as np
+    import torch
+    from hermes_amd import kvs as K, layout as L
+    K.spacetime_init(0)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    pool = 256
+    ids = torch.randint(0, 1_000_000, (pool * 250,), generator=g, dtype=torch.int32).cuda()
+    keys = K.hash_ids(ids).cpu().numpy().view(np.uint64)
+    puts = (torch.rand(pool * 250, generator=g) < 0.05).numpy()
+    ops = np.zeros(250, dtype=L.op_dtype())
+    mb = L.membership(3, 0)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        j = (n % pool) * 250
+        ops[:] = 0
+        ops["key"] = keys[j:j + 250]
+        ops["state"] = int(L.Bucket.NEW)
+        p = puts[j:j + 250]
+        ops["opcode"] = np.where(p, int(L.Op.PUT), int(L.Op.GET))
+        ops["value"][p] = ord("x")
+        ops["val_len"][p] = L.DEFAULT.st_value
+        K.hermes_batch_ops_to_KVS(L.BatchType.local_ops, ops, 250, ops.dtype.itemsize, mb, None, None)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": n * 250 / dt, "unit": "elements/s", "calls": n, "us_per_call": dt / n * 1e6,
+            "what": "hermes_batch_ops_to_KVS on host buffers (PCIe round trip per call), 1M keys, 5% PUT"}
 
 
 def main():
@@ -172,6 +206,8 @@ def main():
     }
     if cpu is not None:
         out["cpu_baseline"] = cpu
+    if rank == 0 and world == 1 and a.host_api_seconds > 0:
+        out["detail"]["host_api"] = host_api_rate(a.host_api_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -287,6 +287,50 @@ def test_max_size_batches_single_hot_key(cfg):
         assert_tables_equal(g, o, f"hot {rnd}")
 
 
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_tag_collisions_in_segments(cfg):
+    """Keys absent from the table whose bucket and tag equal a present key's: the reference
+    finds the present key's slot, fails the 8-byte compare and reports ST_MISS. The device
+    defers that compare to the segment engines, so these elements sit inside the present key's
+    segments (short and hot) and must come out ST_MISS without touching the entry."""
+    rmw, big = cfg["rmw"], cfg["big"]
+    g, o, sizes = make_pair(1000, 1024, 1 << 19 if big else 1 << 17, rmw=rmw, big=big)
+    keys = gen_keys(1000)
+    rng = np.random.default_rng(11)
+    tsp = gen.TsPool(rng)
+    mb = L.membership(3, 0)
+    W = 6
+    hot = keys[[21, 22]]
+    fake = np.array([int(k) ^ (1 << 40) for k in hot] + [int(hot[0]) ^ (1 << 33)], dtype=np.uint64)
+    assert all(o.lookup(int(f)) is None for f in fake)
+    for rnd, pool in enumerate((np.concatenate([hot, fake]), np.concatenate([keys[100:400], fake]),
+                                np.concatenate([hot[:1], fake[:1]]))):
+        loc = gen.local_ops(rng, pool, W * 250, sizes, rmw, tsp)
+        loc_o = gen.bytecopy(loc)
+        _run_both(g, o, L.BatchType.local_ops, loc, loc_o, mb, W, 250, None)
+        assert_elems_equal(loc, loc_o, f"collide local {rnd}")
+        gen.harvest_ts(tsp, loc)
+        inv = gen.invs(rng, pool, W * 900, sizes, rmw, tsp, machine_num=3)
+        inv_o = gen.bytecopy(inv)
+        ns_g = np.full(W, -1, np.int32)
+        ns_o = ns_g.copy()
+        _run_both(g, o, L.BatchType.invs, inv, inv_o, mb, W, 900, None, ns_g=ns_g, ns_o=ns_o)
+        assert_elems_equal(inv, inv_o, f"collide invs {rnd}")
+        ack = gen.acks(rng, pool, W * 900, sizes, rmw, tsp, machine_num=3)
+        ack_o = gen.bytecopy(ack)
+        rw_g, rw_o = gen.bytecopy(loc), gen.bytecopy(loc)
+        _run_both(g, o, L.BatchType.acks, ack, ack_o, mb, W, 900, None, rw_g, rw_o, rw_stride=250)
+        assert_elems_equal(ack, ack_o, f"collide acks {rnd}")
+        assert_elems_equal(rw_g, rw_o, f"collide rw {rnd}")
+        val = gen.vals(rng, pool, W * 900, sizes, rmw, tsp, machine_num=3)
+        val_o = gen.bytecopy(val)
+        _run_both(g, o, L.BatchType.vals, val, val_o, mb, W, 900, None)
+        assert_elems_equal(val, val_o, f"collide vals {rnd}")
+        miss = np.isin(loc["key"], fake)
+        assert (loc["state"][miss] == int(L.Resp.MISS)).sum() > miss.sum() // 2  # the rest were skipped
+        assert_tables_equal(g, o, f"collide {rnd}")
+
+
 def test_adversarial_inv_alternating_equal_timestamps():
     """Equal-timestamp INVs from alternating senders: every one rewrites last_writer_id, so the
     hot-key engine has one candidate per element (its slowest case) and must stay exact."""

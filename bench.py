@@ -202,6 +202,7 @@ def main():
             "committed_per_step_rank0": committed / a.steps, "writes_completed_rank0": writes,
             "puts_succeeded_rank0": puts_ok, "populate_s": t_pop,
             "step_bytes_per_committed_op_model": 554,
+            "round_stats_rank0": rnd.stats(),
         },
     }
     if cpu is not None:

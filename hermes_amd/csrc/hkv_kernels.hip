@@ -207,6 +207,7 @@ template <int TYPE, int SV>
 __global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
 {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p == 0) a.st.count[1] = 0;  // fallback list of this launch (read after the rounds)
     if (p >= a.n) return;
     const uint32_t key = a.keys[p];
     const bool head = key != a.skip_key && (p == 0 || a.keys[p - 1] != key);
@@ -236,19 +237,16 @@ __global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
     meta_store(entry, mm);
 }
 
-// seg_of[p] for every sorted position; the last position of a long segment records its length
-__global__ __launch_bounds__(256) void k_seg_map(SegmentArgs a)
+// long-segment slot of sorted position p (kNone if short or skipped); the last position of a
+// long segment records its length
+__device__ __forceinline__ uint32_t seg_map(const SegmentArgs &a, int64_t p)
 {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.n) return;
     const uint32_t key = a.keys[p];
-    uint32_t s = kNone;
     const uint32_t l = a.st.lidx[p];
-    if (key != a.skip_key && l && a.keys[a.st.start[l - 1]] == key) {  // inside the last long segment begun
-        s = l - 1;
-        if (p + 1 == a.n || a.keys[p + 1] != key) a.st.len[s] = (uint32_t)(p + 1) - a.st.start[s];
-    }
-    a.st.seg_of[p] = s;
+    if (key == a.skip_key || !l || a.keys[a.st.start[l - 1]] != key) return kNone;  // not in the last long segment begun
+    const uint32_t s = l - 1;
+    if (p + 1 == a.n || a.keys[p + 1] != key) a.st.len[s] = (uint32_t)(p + 1) - a.st.start[s];
+    return s;
 }
 
 template <int TYPE>
@@ -256,7 +254,11 @@ __global__ __launch_bounds__(256) void k_round_cand(SegmentArgs a, int r)
 {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
-    uint32_t s = p < a.n ? a.st.seg_of[p] : kNone;
+    uint32_t s = kNone;
+    if (p < a.n) {
+        if (r == 0) a.st.seg_of[p] = s = seg_map(a, p);
+        else s = a.st.seg_of[p];
+    }
     bool cand = false;
     uint32_t rel = 0;
     if (s != kNone && a.st.done[s] == kNotDone) {
@@ -658,7 +660,6 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     sa.skip_key = bl.skip_key;
     sa.g_membership = bl.g_membership;
     sa.w_ack_init = bl.w_ack_init;
-    if (hipMemsetAsync(bl.seg_count, 0, 2 * sizeof(uint32_t), s) != hipSuccess) return -3;
     {
         HeadIter it(rocprim::counting_iterator<uint32_t>(0), LongHeadFlag{bl.keys_b, bl.skip_key, (uint32_t)n});
         size_t tb = bl.sort_tmp_bytes;
@@ -671,7 +672,6 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
 #define HKV_LAUNCH_SEG(T, V)                                                                        \
     do {                                                                                            \
         hipLaunchKernelGGL((k_segment_exec<T, V>), dim3(grid), dim3(256), 0, s, sa);                \
-        hipLaunchKernelGGL(k_seg_map, dim3(grid), dim3(256), 0, s, sa);                             \
         for (int r = 0; r < kMaxRounds; ++r) {                                                      \
             hipLaunchKernelGGL((k_round_cand<T>), dim3(grid), dim3(256), 0, s, sa, r);              \
             hipLaunchKernelGGL((k_round_apply<T, V>), dim3(sgrid), dim3(256), 0, s, sa, r);         \

@@ -22,19 +22,16 @@ phases and kernels, with the collectives done by tensor copies).
 from __future__ import annotations
 
 import ctypes
-import math
 
 import torch
 
 from . import layout as L
 from .kvs import HermesKV
 from .lib import check, raw
-from .workload import HkvZipf, _ptr, _s
+from .workload import HkvZipf, _ptr, _s, slots_per_worker  # noqa: F401 (re-exported)
 
 _L = raw()
 _P = ctypes.c_void_p
-_L.hkv_wl_marshal_invs_cap.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
-                                       ctypes.c_uint32, _P, _P]
 _L.hkv_wl_marshal_acks_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P,
                                         ctypes.c_uint32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_regroup.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P,
@@ -44,17 +41,6 @@ _L.hkv_wl_collect_vals.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctype
 
 MAX_REPLICAS = 8
 LOCAL = 250  # MAX_BATCH_KVS_OPS_SIZE, config.h:42
-
-
-def slots_per_worker(write_permille: int, rmw_permille: int = 0, batch: int = LOCAL) -> int:
-    """INV slots per worker and round (the send credits): the mean number of writes in a
-    250-op batch plus 8 standard deviations, rounded up to 8, at most the batch. Writes beyond
-    it stay in PUT_SUCCESS and go out in a later round (counted in `held`)."""
-    p = min(1.0, write_permille / 1000.0)
-    mean = batch * p
-    sd = math.sqrt(batch * p * (1 - p))
-    c = int(math.ceil((mean + 8 * sd + 1) / 8.0) * 8)
-    return max(8, min(batch, c))
 
 
 class ReplicaRound:

@@ -33,6 +33,8 @@ _L.hkv_wl_gen_trace.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctyp
 _L.hkv_wl_refill.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                              _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, _P, _P]
 _L.hkv_wl_marshal_invs.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]
+_L.hkv_wl_marshal_invs_cap.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
+                                       ctypes.c_uint32, _P, _P]
 _L.hkv_wl_marshal_acks.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_vals.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_peer_acks.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
@@ -40,6 +42,17 @@ _L.hkv_wl_peer_acks.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c
 _L.hkv_wl_gen_remote.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_uint32,
                                  ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(HkvZipf), ctypes.c_uint32,
                                  ctypes.c_uint64, _P]
+
+
+def slots_per_worker(write_permille: int, rmw_permille: int = 0, batch: int = 250) -> int:
+    """INV slots per worker and round (the send credits): the mean number of writes in a
+    250-op batch plus 8 standard deviations, rounded up to 8, at most the batch. Writes beyond
+    it stay in PUT_SUCCESS and go out in a later round (counted in `held`)."""
+    p = min(1.0, write_permille / 1000.0)
+    mean = batch * p
+    sd = math.sqrt(batch * p * (1 - p))
+    c = int(math.ceil((mean + 8 * sd + 1) / 8.0) * 8)
+    return max(8, min(batch, c))
 
 
 def zipf_params(n: int, theta: float) -> HkvZipf:
@@ -91,9 +104,11 @@ class Round:
         W, S = n_workers, self.LOCAL
         u8 = dict(dtype=torch.uint8, device=dev)
         self.ops = torch.zeros(W * S * self.op, **u8)
-        self.inv_out = torch.zeros(W * S * self.op, **u8)
+        self.C = slots_per_worker(write_permille, rmw_permille)   # INV send credits per worker
+        self.inv_out = torch.zeros(W * self.C * self.op, **u8)
         self.inv_count = torch.zeros(W, dtype=torch.int32, device=dev)
-        self.ack_stride = S * max(self.R, 1)
+        self.held = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.ack_stride = self.C * max(self.R, 1)
         self.acks = torch.zeros(W * self.ack_stride * self.ack_size, **u8)
         self.ack_count = torch.zeros(W, dtype=torch.int32, device=dev)
         self.val_out = torch.zeros(W * self.ack_stride * L.OP_META_SIZE, **u8)
@@ -136,11 +151,12 @@ class Round:
         self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb)
 
     def marshal_invs(self):
-        check(_L.hkv_wl_marshal_invs(_ptr(self.ops), self.W, self.LOCAL, self.op, _ptr(self.inv_out),
-                                     _ptr(self.inv_count), self.machine_id, _s()), "marshal_invs")
+        check(_L.hkv_wl_marshal_invs_cap(_ptr(self.ops), self.W, self.LOCAL, self.op, _ptr(self.inv_out), self.C,
+                                         _ptr(self.inv_count), self.machine_id, _ptr(self.held), _s()),
+              "marshal_invs")
 
     def virtual_peer_acks(self):
-        check(_L.hkv_wl_peer_acks(_ptr(self.inv_out), _ptr(self.inv_count), self.W, self.LOCAL, self.op,
+        check(_L.hkv_wl_peer_acks(_ptr(self.inv_out), _ptr(self.inv_count), self.W, self.C, self.op,
                                   _ptr(self.acks), self.ack_stride, _ptr(self.ack_count), _ptr(self.peer_t),
                                   self.R, _s()), "peer_acks")
 
@@ -202,5 +218,5 @@ class Round:
         return int(self.counters[0].item())
 
     def stats(self) -> dict:
-        c = self.counters.cpu().tolist()
-        return {"committed": c[0], "misses": c[1], "writes_completed": c[2]}
+        c = self.counters[:3].cpu().tolist()
+        return {"committed": c[0], "misses": c[1], "writes_completed": c[2], "invs_held": int(self.held.item())}

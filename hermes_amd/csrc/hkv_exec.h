@@ -396,19 +396,20 @@ __device__ __forceinline__ bool meta_equal(const Meta &a, const Meta &b)
 
 // hermes_skip_dispatcher, hermesKV.c:709-769 (the INV membership-change side effect is
 // handled by the lookup kernel, which records the last such element per batch)
-__device__ __forceinline__ bool skip_elem(int type, const uint8_t *x)
+__device__ __forceinline__ bool skip_elem_os(int type, uint8_t oc, uint8_t st)
 {
-    uint8_t st = x[9];
     switch (type) {
     case kLocal:
         return st == kPutSuccess || st == kRmwSuccess || st == kReplaySuccess || st == kInProgressPut ||
                st == kInProgressReplay || st == kOpMembChange || st == kPutCompleteSendVals;
     case kLocalAfterMemb:
         return !(st == kInProgressPut || st == kInProgressRmw || st == kInProgressReplay);
-    case kInvs: return x[8] == kOpMembChange;
+    case kInvs: return oc == kOpMembChange;
     case kAcks: return st == kOpMembChange;
     default: return false;
     }
 }
+
+__device__ __forceinline__ bool skip_elem(int type, const uint8_t *x) { return skip_elem_os(type, x[8], x[9]); }
 
 }  // namespace hkv

@@ -77,44 +77,65 @@ struct LookupArgs {
     uint32_t skip_key;
 };
 
+// Four lanes per element: each lane reads 16 bytes (two slots) of the element's 64-byte
+// bucket, so one load instruction covers a whole bucket line per element and the vector
+// memory pipeline sees one request per bucket instead of four. Slots are searched in the
+// reference's order (first tag match wins, hermesKV.c:954-975).
+constexpr int kLookupPerBlock = 64;
 __global__ __launch_bounds__(256) void k_lookup(LookupArgs a)
 {
-    int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gi >= a.n) return;
-    int32_t b = (int32_t)(gi / a.stride);
-    int32_t idx = (int32_t)(gi - (int64_t)b * a.stride);
-    uint32_t key_out = a.skip_key;
-    a.vals[gi] = (uint32_t)gi;
-    if (a.counts == nullptr || idx < a.counts[b]) {
-        uint8_t *x = a.elems + gi * a.esz;
-        if (skip_elem(a.type, x)) {
-            if (a.type == kInvs && a.ns_idx) atomicMax(&a.ns_idx[b], idx);
-        } else {
-            uint64_t key = ld64(x);
-            const uint4 *bkt = reinterpret_cast<const uint4 *>(a.index + ((key & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u);
-            uint4 q[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) q[j] = bkt[j];
-            const uint64_t *slots = reinterpret_cast<const uint64_t *>(q);
-            uint32_t tag = (uint32_t)(key >> 48);
-            bool hit = false;
-            uint64_t off = 0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                uint64_t s = slots[j];
-                if (!hit && (s & 1u) && ((uint32_t)(s >> 1) & 0x7FFFFFu) == tag) {
-                    hit = true;
-                    off = s >> 24;
-                }
+    const int q = threadIdx.x & 3;
+    const int lane = threadIdx.x & 63;
+    const int64_t gi = (int64_t)blockIdx.x * kLookupPerBlock + (threadIdx.x >> 2);
+    const bool in = gi < a.n;
+    int32_t b = 0, idx = 0;
+    uint8_t *x = nullptr;
+    uint64_t key = 0;
+    int probe = 0;
+    if (in && q == 0) {
+        b = (int32_t)(gi / a.stride);
+        idx = (int32_t)(gi - (int64_t)b * a.stride);
+        if (a.counts == nullptr || idx < a.counts[b]) {
+            x = a.elems + gi * a.esz;
+            key = ld64(x);
+            const uint32_t w2 = ld32(x + 8);
+            if (skip_elem_os(a.type, (uint8_t)w2, (uint8_t)(w2 >> 8))) {
+                if (a.type == kInvs && a.ns_idx) atomicMax(&a.ns_idx[b], idx);
+            } else {
+                probe = 1;
             }
-            if (hit && a.g.log_head - off < a.g.log_cap) {
-                uint64_t phys = off & a.g.log_mask;
-                if (ld64(a.log + phys + 8) == key) key_out = (uint32_t)(phys / a.g.entry_unit);
-            }
-            if (key_out == a.skip_key) x[9] = kMiss;
         }
     }
+    probe = __shfl(probe, 0, 4);
+    key = __shfl(key, 0, 4);
+    uint64_t s0 = 0, s1 = 0;
+    if (probe) {
+        const uint4 v = reinterpret_cast<const uint4 *>(a.index + ((key & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u)[q];
+        s0 = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        s1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    }
+    const uint32_t tag = (uint32_t)(key >> 48);
+    const bool m0 = probe && (s0 & 1u) && ((uint32_t)(s0 >> 1) & 0x7FFFFFu) == tag;
+    const bool m1 = probe && (s1 & 1u) && ((uint32_t)(s1 >> 1) & 0x7FFFFFu) == tag;
+    const int gbase = lane & ~3;
+    const uint32_t g0 = (uint32_t)(__ballot(m0) >> gbase) & 0xFu;
+    const uint32_t g1 = (uint32_t)(__ballot(m1) >> gbase) & 0xFu;
+    uint32_t order = 0;  // bit 2*l + j: slot 2*l + j matches
+#pragma unroll
+    for (int l = 0; l < 4; ++l) order |= ((g0 >> l) & 1u) << (2 * l) | ((g1 >> l) & 1u) << (2 * l + 1);
+    const int first = order ? __ffs(order) - 1 : 0;
+    const uint64_t off = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
+    if (!in || q != 0) return;
+    uint32_t key_out = a.skip_key;
+    if (probe) {
+        if (order && a.g.log_head - off < a.g.log_cap) {
+            const uint64_t phys = off & a.g.log_mask;
+            if (ld64(a.log + phys + 8) == key) key_out = (uint32_t)(phys / a.g.entry_unit);
+        }
+        if (key_out == a.skip_key) x[9] = kMiss;
+    }
     a.keys[gi] = key_out;
+    a.vals[gi] = (uint32_t)gi;
 }
 
 // ------------------------------------------------------------------ batch stage 3: segments
@@ -629,7 +650,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     la.esz = bl.esz;
     la.type = bl.type;
     la.skip_key = bl.skip_key;
-    hipLaunchKernelGGL(k_lookup, dim3(grid), dim3(256), 0, s, la);
+    hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n + kLookupPerBlock - 1) / kLookupPerBlock)), dim3(256), 0, s, la);
     if (hipGetLastError() != hipSuccess) return -1;
     if (sort_pairs(bl.sort_tmp, bl.sort_tmp_bytes, bl.keys_a, bl.keys_b, bl.vals_a, bl.vals_b, n, bl.key_bits, s))
         return -2;

@@ -224,38 +224,98 @@ __device__ __forceinline__ uint8_t *entry_of(const SegmentArgs &a, uint32_t key)
 
 // Serial tier + long-segment registration. A long segment's slot is its rank among long heads
 // (the scan in lidx), so registration needs no atomics.
-template <int TYPE, int SV>
+//
+// Short segments (at most kShortSeg elements) run on LDS copies: the workgroup covers BP sorted
+// positions; the head lane of each short segment marks the positions it owns (its segment may
+// run up to kShortSeg-1 positions past the range), the ops and the heads' log entries are
+// copied in with eight lanes per object (one memory request per object line instead of one
+// per field), every head applies its segment with the serial exec functions on LDS, and the
+// owned ops and entries are copied back the same way.
+template <int TYPE, int SV, int BP>
 __global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
 {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p == 0) a.st.count[1] = 0;  // fallback list of this launch (read after the rounds)
-    if (p >= a.n) return;
-    const uint32_t key = a.keys[p];
-    const bool head = key != a.skip_key && (p == 0 || a.keys[p - 1] != key);
-    if (!head) return;
-    const bool longseg = p + kShortSeg < a.n && a.keys[p + kShortSeg] == key;
-    if (longseg) {
-        const uint32_t s = a.st.lidx[p] - 1;
-        a.st.start[s] = (uint32_t)p;
-        Meta m0;
-        meta_load(entry_of(a, key), m0);
-        a.st.meta[(size_t)s * (kMaxRounds + 1)] = m0;
+    extern __shared__ uint64_t smem[];
+    constexpr int kSpan = BP + kShortSeg - 1;              // staged positions
+    uint8_t *own = reinterpret_cast<uint8_t *>(smem);       // [kSpan] owned by a short head here
+    uint8_t *hflag = own + ((kSpan + 7) & ~7);              // [BP] short head at this position
+    uint64_t *ops = reinterpret_cast<uint64_t *>(hflag + BP);
+    const uint32_t esz = (uint32_t)a.esz, ew = esz / 8u, entw = a.g.entry_size / 8u;
+    uint64_t *ents = ops + (size_t)kSpan * ew;             // [BP] entries of short heads
+    const int t = threadIdx.x;
+    const int64_t P0 = (int64_t)blockIdx.x * BP;
+    if (blockIdx.x == 0 && t == 0) a.st.count[1] = 0;  // fallback list of this launch (read after the rounds)
+    for (int i = t; i < kSpan; i += blockDim.x) own[i] = 0;
+    __syncthreads();
+    const int64_t p = P0 + t;
+    int L = 0;
+    uint32_t key = a.skip_key;
+    if (t < BP && p < a.n) {
+        key = a.keys[p];
+        const bool head = key != a.skip_key && (p == 0 || a.keys[p - 1] != key);
+        if (head) {
+            const bool longseg = p + kShortSeg < a.n && a.keys[p + kShortSeg] == key;
+            if (longseg) {
+                const uint32_t s = a.st.lidx[p] - 1;
+                a.st.start[s] = (uint32_t)p;
+                Meta m0;
+                meta_load(entry_of(a, key), m0);
+                a.st.meta[(size_t)s * (kMaxRounds + 1)] = m0;
 #pragma unroll
-        for (int r = 0; r < kMaxRounds; ++r) a.st.mut[(size_t)s * kMaxRounds + r] = kNone;
-        a.st.done[s] = kNotDone;
-        return;
+                for (int r = 0; r < kMaxRounds; ++r) a.st.mut[(size_t)s * kMaxRounds + r] = kNone;
+                a.st.done[s] = kNotDone;
+            } else {
+                L = 1;
+                while (L < kShortSeg && p + L < a.n && a.keys[p + L] == key) ++L;
+                for (int j = 0; j < L; ++j) own[t + j] = 1;
+            }
+        }
     }
-    uint8_t *entry = entry_of(a, key);
-    Meta mm;
-    meta_load(entry, mm);
-    Ctx c = make_ctx(a);
-    for (int64_t q = p; q < a.n && a.keys[q] == key; ++q) {
-        uint8_t *x;
-        uint8_t idx;
-        elem_at(a, a.vals[q], x, idx, c);
-        dispatch<SV>(TYPE, x, entry, idx, mm, c);
+    if (t < BP) hflag[t] = L ? 1 : 0;
+    __syncthreads();
+    const int g = t >> 3, l8 = t & 7, ng = blockDim.x >> 3;
+    for (int i = g; i < kSpan; i += ng) {
+        if (!own[i]) continue;
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(a.elems + (int64_t)a.vals[P0 + i] * esz);
+        for (uint32_t w = l8; w < ew; w += 8) ops[(size_t)i * ew + w] = src[w];
     }
-    meta_store(entry, mm);
+    for (int h = g; h < BP; h += ng) {
+        if (!hflag[h]) continue;
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(entry_of(a, a.keys[P0 + h]));
+        for (uint32_t w = l8; w < entw; w += 8) ents[(size_t)h * entw + w] = src[w];
+    }
+    __syncthreads();
+    if (L) {
+        uint8_t *entry = reinterpret_cast<uint8_t *>(ents + (size_t)t * entw);
+        Meta mm;
+        meta_load(entry, mm);
+        Ctx c = make_ctx(a);
+        for (int j = 0; j < L; ++j) {
+            const uint32_t gi = a.vals[p + j];
+            const int32_t b = (int32_t)(gi / (uint32_t)a.stride);
+            const uint8_t idx = (uint8_t)(gi - (uint32_t)b * (uint32_t)a.stride);
+            c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
+            dispatch<SV>(TYPE, reinterpret_cast<uint8_t *>(ops + (size_t)(t + j) * ew), entry, idx, mm, c);
+        }
+        meta_store(entry, mm);
+    }
+    __syncthreads();
+    for (int i = g; i < kSpan; i += ng) {
+        if (!own[i]) continue;
+        uint64_t *dst = reinterpret_cast<uint64_t *>(a.elems + (int64_t)a.vals[P0 + i] * esz);
+        for (uint32_t w = l8; w < ew; w += 8) dst[w] = ops[(size_t)i * ew + w];
+    }
+    for (int h = g; h < BP; h += ng) {
+        if (!hflag[h]) continue;
+        uint64_t *dst = reinterpret_cast<uint64_t *>(entry_of(a, a.keys[P0 + h]));
+        for (uint32_t w = l8; w < entw; w += 8) dst[w] = ents[(size_t)h * entw + w];
+    }
+}
+
+template <int BP>
+static size_t segment_exec_lds(uint32_t esz, uint32_t entry_size)
+{
+    const int span = BP + kShortSeg - 1;
+    return (size_t)((span + 7) & ~7) + BP + (size_t)span * esz + (size_t)BP * entry_size;
 }
 
 // long-segment slot of sorted position p (kNone if short or skipped); the last position of a
@@ -692,7 +752,17 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     const unsigned sgrid = (unsigned)((max_long + 255) / 256);
 #define HKV_LAUNCH_SEG(T, V)                                                                        \
     do {                                                                                            \
-        hipLaunchKernelGGL((k_segment_exec<T, V>), dim3(grid), dim3(256), 0, s, sa);                \
+        if (V == 287 || bl.esz > 64) {                                                              \
+            const size_t lds = segment_exec_lds<128>(bl.esz, bl.g.entry_size);                      \
+            if (lds > 64 * 1024)                                                                    \
+                hipFuncSetAttribute((const void *)k_segment_exec<T, V, 128>,                        \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);          \
+            hipLaunchKernelGGL((k_segment_exec<T, V, 128>), dim3((unsigned)((n + 127) / 128)),     \
+                               dim3(128), lds, s, sa);                                              \
+        } else {                                                                                    \
+            hipLaunchKernelGGL((k_segment_exec<T, V, 256>), dim3(grid), dim3(256),                  \
+                               segment_exec_lds<256>(bl.esz, bl.g.entry_size), s, sa);              \
+        }                                                                                           \
         for (int r = 0; r < kMaxRounds; ++r) {                                                      \
             hipLaunchKernelGGL((k_round_cand<T>), dim3(grid), dim3(256), 0, s, sa, r);              \
             hipLaunchKernelGGL((k_round_apply<T, V>), dim3(sgrid), dim3(256), 0, s, sa, r);         \

@@ -23,6 +23,7 @@ struct BatchLaunch {
     uint32_t *seg_start, *seg_len, *seg_count, *seg_fallback, *seg_of, *seg_mut;
     void *seg_meta;
     uint8_t *seg_done, *seg_snap;
+    uint64_t *seg_hdr;
     uint32_t seg_cap;
     unsigned int *error_flags;                       // checked builds: unsound would_mutate()
     void *sort_tmp;

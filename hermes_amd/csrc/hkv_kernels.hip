@@ -173,6 +173,7 @@ struct SegState {            // per long segment, all in device scratch
     uint32_t *fallback;      // [cap] slots of segments left to k_long_exec
     const uint32_t *lidx;    // [n] long-segment heads at or before each sorted position (scan)
     uint32_t *seg_of;        // [n] long-segment slot of every sorted position (kNone if short/skip)
+    uint64_t *hdr;           // [n] header bytes 8..15 of long-segment elements, sorted order
     Meta *meta;              // [cap][kMaxRounds + 1]
     uint32_t *mut;           // [cap][kMaxRounds] F_r (position within segment), kNone if none
     uint8_t *done;           // [cap] round whose meta is final, kNotDone while mutating
@@ -336,9 +337,19 @@ __global__ __launch_bounds__(256) void k_round_cand(SegmentArgs a, int r)
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
     uint32_t s = kNone;
+    // would_mutate reads header bytes 8..15 only. Round 0 loads them from the element (issued
+    // before the segment lookups, which do not depend on it) and keeps a sorted-order copy that
+    // later rounds read coalesced.
+    uint64_t hdr[2] = {0, 0};
     if (p < a.n) {
-        if (r == 0) a.st.seg_of[p] = s = seg_map(a, p);
-        else s = a.st.seg_of[p];
+        if (r == 0) {
+            const uint32_t gi = a.vals[p];
+            hdr[1] = a.keys[p] != a.skip_key ? ld64(a.elems + (int64_t)gi * a.esz + 8) : 0;
+            a.st.seg_of[p] = s = seg_map(a, p);
+            if (s != kNone) a.st.hdr[p] = hdr[1];
+        } else {
+            s = a.st.seg_of[p];
+        }
     }
     bool cand = false;
     uint32_t rel = 0;
@@ -347,11 +358,9 @@ __global__ __launch_bounds__(256) void k_round_cand(SegmentArgs a, int r)
         const uint32_t prev = r > 0 ? a.st.mut[(size_t)s * kMaxRounds + r - 1] : kNone;
         if (r == 0 || rel > prev) {
             Ctx c = make_ctx(a);
-            uint8_t *x;
-            uint8_t idx;
-            elem_at(a, a.vals[p], x, idx, c);
+            if (r > 0) hdr[1] = a.st.hdr[p];
             const Meta m = a.st.meta[(size_t)s * (kMaxRounds + 1) + r];
-            cand = would_mutate(TYPE, x, m, c);
+            cand = would_mutate(TYPE, reinterpret_cast<const uint8_t *>(hdr), m, c);
         }
     }
     // candidates of one segment are consecutive among a wavefront's candidate lanes (sorted
@@ -665,7 +674,7 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 size_t seg_scratch_bytes(int64_t n, uint32_t entry_size)
 {
     const size_t cap = (size_t)(n / (kShortSeg + 1) + 1);
-    return align256(4 * (size_t)n) * 2 + align256(4 * cap) * 2 + 256 + align256(sizeof(Meta) * cap * (kMaxRounds + 1)) +
+    return align256(4 * (size_t)n) * 2 + align256(8 * (size_t)n) + align256(4 * cap) * 2 + 256 + align256(sizeof(Meta) * cap * (kMaxRounds + 1)) +
            align256(4 * cap * kMaxRounds) + align256(cap) + (size_t)entry_size * cap * kMaxRounds;
 }
 
@@ -681,6 +690,7 @@ void seg_carve(BatchLaunch &bl, uint8_t *base, int64_t n, uint32_t entry_size)
     };
     bl.seg_fallback = reinterpret_cast<uint32_t *>(take(4 * cap));
     bl.seg_of = reinterpret_cast<uint32_t *>(take(4 * (size_t)n));
+    bl.seg_hdr = reinterpret_cast<uint64_t *>(take(8 * (size_t)n));
     bl.seg_start = reinterpret_cast<uint32_t *>(take(4 * cap));
     bl.seg_len = reinterpret_cast<uint32_t *>(take(4 * cap));
     bl.seg_count = reinterpret_cast<uint32_t *>(take(8));
@@ -721,6 +731,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     sa.st.fallback = bl.seg_fallback;
     sa.st.lidx = bl.keys_a;  // the sort's input keys are free again
     sa.st.seg_of = bl.seg_of;
+    sa.st.hdr = bl.seg_hdr;
     sa.st.meta = reinterpret_cast<Meta *>(bl.seg_meta);
     sa.st.mut = bl.seg_mut;
     sa.st.done = bl.seg_done;

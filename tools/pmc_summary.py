@@ -1,19 +1,33 @@
-"""Per-kernel HBM traffic from tools/pmc.sh output: python tools/pmc_summary.py TAG
-FETCH_SIZE is doubled (gfx950: it reports half the bytes of wide reads, MI355X_MICROARCH.md)."""
-import csv, sys, collections
+"""Per-kernel PMC summary from tools/pmc.sh output: python tools/pmc_summary.py TAG
+Prints the mean per dispatch of every counter collected (FETCH_SIZE/WRITE_SIZE in MB; FETCH_SIZE
+also doubled: on gfx950 it reports half the bytes of wide reads, MI355X_MICROARCH.md)."""
+import collections
+import csv
+import glob
+import os
+import sys
+
 tag = sys.argv[1]
-res = collections.defaultdict(lambda: {"FETCH_SIZE": [], "WRITE_SIZE": []})
-for c in ("FETCH_SIZE", "WRITE_SIZE"):
-    for r in csv.DictReader(open(f"gpurun_out/{tag}/pmc/{c}/run_counter_collection.csv")):
+res = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(f"gpurun_out/{tag}/pmc/*/run_counter_collection.csv"):
+    for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
         short = name.split("(")[0].replace("void ", "").replace("hkv::", "")
         if "rocprim" in name:
             short = "rocprim:" + ("onesweep" if "onesweep" in name else "scan" if "scan" in name else "other")
-        grid = r.get("Grid_Size", "")
-        res[(short, grid)][c].append(float(r["Counter_Value"]))
-print(f"{'kernel':44s} {'grid':>9s} {'n':>4s} {'fetch MB':>9s} {'x2 MB':>8s} {'write MB':>9s}")
-for (k, g), v in sorted(res.items(), key=lambda kv: -sum(kv[1]["FETCH_SIZE"] or [0]) / max(1, len(kv[1]["FETCH_SIZE"]))):
-    f = v["FETCH_SIZE"]; w = v["WRITE_SIZE"]
-    fa = sum(f) / len(f) / 1024 if f else float("nan")   # KB -> MB
-    wa = sum(w) / len(w) / 1024 if w else float("nan")
-    print(f"{k[:44]:44s} {g:>9s} {len(f):4d} {fa:9.1f} {2*fa:8.1f} {wa:9.1f}")
+        res[(short, r.get("Grid_Size", ""))][r["Counter_Name"]].append(float(r["Counter_Value"]))
+cols = sorted({c for v in res.values() for c in v})
+hdr = f"{'kernel':40s} {'grid':>9s} " + " ".join(f"{c[:14]:>14s}" for c in cols)
+print(hdr)
+def key(kv):
+    v = kv[1].get(cols[0], [0])
+    return -sum(v) / max(1, len(v))
+for (k, g), v in sorted(res.items(), key=key):
+    vals = []
+    for c in cols:
+        x = v.get(c, [])
+        m = sum(x) / len(x) if x else float("nan")
+        if c in ("FETCH_SIZE", "WRITE_SIZE"):
+            m /= 1024.0  # KB -> MB
+        vals.append(f"{m:14.1f}")
+    print(f"{k[:40]:40s} {g:>9s} " + " ".join(vals))

@@ -26,6 +26,15 @@ for r in rows[a:b]:
     if "--full" in sys.argv:
         print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} {short[:60]}")
 tot = (int(rows[b]["Start_Timestamp"]) - t0) / 1e3
+BATCH = ("k_lookup", "__amd_rocclr_fillBufferAligned", "rocprim", "k_segment_exec", "k_round_cand",
+         "k_round_apply", "k_round_resolve", "k_long_exec")
+sums = collections.OrderedDict()
+for k, (d, c, g) in agg.items():
+    ph, name = k.split(":", 1)
+    if name in BATCH:
+        sums[ph] = sums.get(ph, 0.0) + d
+print("batch launch = sum of its kernels (compare bench.py roofline.batch_ms):",
+      {k: round(v / 1e3, 4) for k, v in sums.items()}, "ms")
 for k, (d, c, g) in agg.items():
     print(f"{k:32s} {d:8.1f} us  x{c:<3d} gaps {g:6.1f}")
 print(f"step total {tot:.1f} us")

@@ -20,11 +20,13 @@ struct BatchLaunch {
     int32_t *node_suspected;
     uint32_t *keys_a, *keys_b, *vals_a, *vals_b;
     // long-segment round state (see hkv_kernels.hip, stage 3)
-    uint32_t *seg_start, *seg_len, *seg_count, *seg_fallback, *seg_of, *seg_mut;
+    uint32_t *seg_start, *seg_end, *seg_count, *seg_fallback, *seg_of;
+    unsigned long long *seg_mut;              // epoch-tagged, all-ones when allocated
     void *seg_meta;
     uint8_t *seg_done, *seg_snap;
     uint64_t *seg_hdr;
     uint32_t seg_cap;
+    uint32_t epoch;                           // launch counter of the table, >= 1
     unsigned int *error_flags;                       // checked builds: unsound would_mutate()
     void *sort_tmp;
     size_t sort_tmp_bytes;

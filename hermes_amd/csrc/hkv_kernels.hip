@@ -144,12 +144,13 @@ __global__ __launch_bounds__(256) void k_lookup(LookupArgs a)
 // elements is applied serially by its first lane (k_segment_exec). Longer ones (hot keys)
 // go through chip-wide rounds:
 //
-//   round r (k_round_cand + k_round_apply), for every long segment not yet finished:
-//     every element after the previous round's mutation asks would_mutate() against the
-//     segment's meta S_r; the first such position F_r is found with a wave-segmented min and
-//     one atomicMin per wavefront and segment; one lane then snapshots the entry (image of
-//     S_r), applies element F_r with the serial exec function and records S_{r+1}. A segment
-//     whose round finds no candidate is finished: S_r is its final meta, stored to the entry.
+//   round r, for every long segment not yet finished: every element after the previous round's
+//     mutation asks would_mutate() against the segment's meta S_r; the first such sorted
+//     position F_r is found with a wave-segmented min and one atomicMin per wavefront and
+//     segment (round 0 inside k_segment_exec, later rounds in k_round_cand); k_round_apply
+//     then snapshots the entry (image of S_r), applies element F_r alone with the serial exec
+//     function and records S_{r+1}. A segment whose round finds no candidate is finished: S_r
+//     is its final meta, stored to the entry.
 //   k_round_resolve: every other element of a long segment lies strictly between two
 //     consecutive mutations F_{r-1} < pos < F_r and is therefore a non-candidate under S_r:
 //     it runs the serial exec function on a private copy of S_r against the snapshot of S_r
@@ -161,6 +162,10 @@ __global__ __launch_bounds__(256) void k_lookup(LookupArgs a)
 // function leaves the meta unchanged); every element still runs the reference's exec
 // function once, against the meta the sequential order gives it. Checked by bit 0 of
 // *error_flags, which a non-candidate that did change its private copy would raise.
+//
+// F_r lives in a 64-bit word tagged with the launch's epoch ((~epoch << 32) | position), so
+// it needs no per-launch initialisation: a newer epoch's tag is smaller, atomicMin replaces
+// stale words, and a word whose tag is not this launch's reads as "no candidate".
 constexpr int kShortSeg = 4;
 constexpr int kMaxRounds = 4;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -168,17 +173,18 @@ constexpr uint8_t kNotDone = 0xFF;
 
 struct SegState {            // per long segment, all in device scratch
     uint32_t *start;         // [cap] first sorted position
-    uint32_t *len;           // [cap]
+    uint32_t *end;           // [cap] one past the last sorted position
     uint32_t *count;         // [2]: [1] = segments left to k_long_exec
     uint32_t *fallback;      // [cap] slots of segments left to k_long_exec
     const uint32_t *lidx;    // [n] long-segment heads at or before each sorted position (scan)
     uint32_t *seg_of;        // [n] long-segment slot of every sorted position (kNone if short/skip)
     uint64_t *hdr;           // [n] header bytes 8..15 of long-segment elements, sorted order
     Meta *meta;              // [cap][kMaxRounds + 1]
-    uint32_t *mut;           // [cap][kMaxRounds] F_r (position within segment), kNone if none
+    unsigned long long *mut; // [cap][kMaxRounds] epoch-tagged F_r (sorted position)
     uint8_t *done;           // [cap] round whose meta is final, kNotDone while mutating
     uint8_t *snap;           // [cap][kMaxRounds] entry images of S_r
     uint32_t cap;
+    uint32_t epoch;          // this launch, >= 1
 };
 
 struct SegmentArgs {
@@ -223,8 +229,31 @@ __device__ __forceinline__ uint8_t *entry_of(const SegmentArgs &a, uint32_t key)
     return a.log + (uint64_t)key * a.g.entry_unit;
 }
 
-// Serial tier + long-segment registration. A long segment's slot is its rank among long heads
-// (the scan in lidx), so registration needs no atomics.
+__device__ __forceinline__ uint64_t mut_tag(const SegmentArgs &a) { return (uint64_t)(~a.st.epoch) << 32; }
+
+__device__ __forceinline__ uint32_t mut_read(const SegmentArgs &a, uint32_t s, int r)
+{
+    const uint64_t v = a.st.mut[(size_t)s * kMaxRounds + r];
+    return (v >> 32) == (uint32_t)~a.st.epoch ? (uint32_t)v : kNone;
+}
+
+// Candidates of one segment are consecutive among a wavefront's candidate lanes (sorted
+// order): only the first of each run issues the atomicMin, and only if it would lower F_r.
+__device__ __forceinline__ void offer_candidate(const SegmentArgs &a, bool cand, uint32_t s, int r, uint32_t p)
+{
+    const int lane = threadIdx.x & 63;
+    const unsigned long long cm = __ballot(cand);
+    const unsigned long long below = cm & ((1ull << lane) - 1ull);
+    const int prev_lane = below ? 63 - __clzll((long long)below) : -1;
+    const uint32_t prev_s = __shfl(s, prev_lane < 0 ? lane : prev_lane, 64);
+    if (cand && (prev_lane < 0 || prev_s != s)) {
+        unsigned long long *f = &a.st.mut[(size_t)s * kMaxRounds + r];
+        const unsigned long long v = mut_tag(a) | p;
+        if (v < __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(f, v);
+    }
+}
+
+// Serial tier, long-segment registration and round 0's candidate search.
 //
 // Short segments (at most kShortSeg elements) run on LDS copies: the workgroup covers BP sorted
 // positions; the head lane of each short segment marks the positions it owns (its segment may
@@ -232,12 +261,19 @@ __device__ __forceinline__ uint8_t *entry_of(const SegmentArgs &a, uint32_t key)
 // copied in with eight lanes per object (one memory request per object line instead of one
 // per field), every head applies its segment with the serial exec functions on LDS, and the
 // owned ops and entries are copied back the same way.
+//
+// A position is in a long segment iff some window of kShortSeg+1 equal sorted keys covers it;
+// its slot is its segment's rank among long heads (the scan in lidx), so registration needs
+// no atomics. Every long position caches its header for later rounds and offers itself as
+// round 0's candidate against the entry's meta as stored (S_0).
 template <int TYPE, int SV, int BP>
 __global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
 {
     extern __shared__ uint64_t smem[];
     constexpr int kSpan = BP + kShortSeg - 1;              // staged positions
-    uint8_t *own = reinterpret_cast<uint8_t *>(smem);       // [kSpan] owned by a short head here
+    constexpr int kKeys = BP + 2 * kShortSeg;              // sorted keys [P0 - kShortSeg, P0 + BP + kShortSeg)
+    uint32_t *ks = reinterpret_cast<uint32_t *>(smem);
+    uint8_t *own = reinterpret_cast<uint8_t *>(ks + kKeys); // [kSpan] owned by a short head here
     uint8_t *hflag = own + ((kSpan + 7) & ~7);              // [BP] short head at this position
     uint64_t *ops = reinterpret_cast<uint64_t *>(hflag + BP);
     const uint32_t esz = (uint32_t)a.esz, ew = esz / 8u, entw = a.g.entry_size / 8u;
@@ -245,35 +281,51 @@ __global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
     const int t = threadIdx.x;
     const int64_t P0 = (int64_t)blockIdx.x * BP;
     if (blockIdx.x == 0 && t == 0) a.st.count[1] = 0;  // fallback list of this launch (read after the rounds)
+    for (int i = t; i < kKeys; i += blockDim.x) {
+        const int64_t q = P0 - kShortSeg + i;
+        ks[i] = (q >= 0 && q < a.n) ? a.keys[q] : a.skip_key;
+    }
     for (int i = t; i < kSpan; i += blockDim.x) own[i] = 0;
     __syncthreads();
     const int64_t p = P0 + t;
-    int L = 0;
-    uint32_t key = a.skip_key;
-    if (t < BP && p < a.n) {
-        key = a.keys[p];
-        const bool head = key != a.skip_key && (p == 0 || a.keys[p - 1] != key);
-        if (head) {
-            const bool longseg = p + kShortSeg < a.n && a.keys[p + kShortSeg] == key;
-            if (longseg) {
-                const uint32_t s = a.st.lidx[p] - 1;
-                a.st.start[s] = (uint32_t)p;
-                Meta m0;
-                meta_load(entry_of(a, key), m0);
-                a.st.meta[(size_t)s * (kMaxRounds + 1)] = m0;
+    const bool valid = p < a.n;
+    const uint32_t key = valid ? ks[t + kShortSeg] : a.skip_key;
+    const bool live = key != a.skip_key;
+    const bool head = live && ks[t + kShortSeg - 1] != key;
+    bool in_long = false;
+    if (live) {
 #pragma unroll
-                for (int r = 0; r < kMaxRounds; ++r) a.st.mut[(size_t)s * kMaxRounds + r] = kNone;
-                a.st.done[s] = kNotDone;
-            } else {
-                L = 1;
-                while (L < kShortSeg && p + L < a.n && a.keys[p + L] == key) ++L;
-                for (int j = 0; j < L; ++j) own[t + j] = 1;
-            }
-        }
+        for (int j = 0; j <= kShortSeg; ++j)  // window [p - j, p - j + kShortSeg]
+            in_long |= ks[t + kShortSeg - j] == key && ks[t + 2 * kShortSeg - j] == key;
     }
-    if (t < BP) hflag[t] = L ? 1 : 0;
+    const uint32_t s = in_long ? a.st.lidx[p] - 1 : kNone;
+    int L = 0;
+    bool cand = false;
+    if (in_long) {
+        uint8_t *entry = entry_of(a, key);
+        Meta m0;
+        meta_load(entry, m0);
+        if (head) {
+            a.st.start[s] = (uint32_t)p;
+            a.st.meta[(size_t)s * (kMaxRounds + 1)] = m0;
+            a.st.done[s] = kNotDone;
+        }
+        if (ks[t + kShortSeg + 1] != key) a.st.end[s] = (uint32_t)(p + 1);
+        const uint64_t h = ld64(a.elems + (int64_t)a.vals[p] * esz + 8);
+        a.st.hdr[p] = h;
+        uint64_t hdr[2] = {0, h};
+        Ctx c = make_ctx(a);
+        cand = would_mutate(TYPE, reinterpret_cast<const uint8_t *>(hdr), m0, c);
+    } else if (head) {
+        L = 1;
+        while (L < kShortSeg && ks[t + kShortSeg + L] == key) ++L;
+        for (int j = 0; j < L; ++j) own[t + j] = 1;
+    }
+    if (valid) a.st.seg_of[p] = s;
+    offer_candidate(a, cand, s, 0, (uint32_t)p);
+    hflag[t] = L ? 1 : 0;
     __syncthreads();
-    const int g = t >> 3, l8 = t & 7, ng = blockDim.x >> 3;
+    const int g = t >> 3, l8 = t & 7, ng = BP >> 3;
     for (int i = g; i < kSpan; i += ng) {
         if (!own[i]) continue;
         const uint64_t *src = reinterpret_cast<const uint64_t *>(a.elems + (int64_t)a.vals[P0 + i] * esz);
@@ -281,7 +333,7 @@ __global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
     }
     for (int h = g; h < BP; h += ng) {
         if (!hflag[h]) continue;
-        const uint64_t *src = reinterpret_cast<const uint64_t *>(entry_of(a, a.keys[P0 + h]));
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(entry_of(a, ks[h + kShortSeg]));
         for (uint32_t w = l8; w < entw; w += 8) ents[(size_t)h * entw + w] = src[w];
     }
     __syncthreads();
@@ -307,7 +359,7 @@ __global__ __launch_bounds__(256) void k_segment_exec(SegmentArgs a)
     }
     for (int h = g; h < BP; h += ng) {
         if (!hflag[h]) continue;
-        uint64_t *dst = reinterpret_cast<uint64_t *>(entry_of(a, a.keys[P0 + h]));
+        uint64_t *dst = reinterpret_cast<uint64_t *>(entry_of(a, ks[h + kShortSeg]));
         for (uint32_t w = l8; w < entw; w += 8) dst[w] = ents[(size_t)h * entw + w];
     }
 }
@@ -316,63 +368,24 @@ template <int BP>
 static size_t segment_exec_lds(uint32_t esz, uint32_t entry_size)
 {
     const int span = BP + kShortSeg - 1;
-    return (size_t)((span + 7) & ~7) + BP + (size_t)span * esz + (size_t)BP * entry_size;
+    return (size_t)4 * (BP + 2 * kShortSeg) + (size_t)((span + 7) & ~7) + BP + (size_t)span * esz +
+           (size_t)BP * entry_size;
 }
 
-// long-segment slot of sorted position p (kNone if short or skipped); the last position of a
-// long segment records its length
-__device__ __forceinline__ uint32_t seg_map(const SegmentArgs &a, int64_t p)
-{
-    const uint32_t key = a.keys[p];
-    const uint32_t l = a.st.lidx[p];
-    if (key == a.skip_key || !l || a.keys[a.st.start[l - 1]] != key) return kNone;  // not in the last long segment begun
-    const uint32_t s = l - 1;
-    if (p + 1 == a.n || a.keys[p + 1] != key) a.st.len[s] = (uint32_t)(p + 1) - a.st.start[s];
-    return s;
-}
-
+// round r >= 1: candidates after F_{r-1}, against S_r, from the cached headers
 template <int TYPE>
 __global__ __launch_bounds__(256) void k_round_cand(SegmentArgs a, int r)
 {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int lane = threadIdx.x & 63;
-    uint32_t s = kNone;
-    // would_mutate reads header bytes 8..15 only. Round 0 loads them from the element (issued
-    // before the segment lookups, which do not depend on it) and keeps a sorted-order copy that
-    // later rounds read coalesced.
-    uint64_t hdr[2] = {0, 0};
-    if (p < a.n) {
-        if (r == 0) {
-            const uint32_t gi = a.vals[p];
-            hdr[1] = a.keys[p] != a.skip_key ? ld64(a.elems + (int64_t)gi * a.esz + 8) : 0;
-            a.st.seg_of[p] = s = seg_map(a, p);
-            if (s != kNone) a.st.hdr[p] = hdr[1];
-        } else {
-            s = a.st.seg_of[p];
-        }
-    }
+    const uint32_t s = p < a.n ? a.st.seg_of[p] : kNone;
     bool cand = false;
-    uint32_t rel = 0;
-    if (s != kNone && a.st.done[s] == kNotDone) {
-        rel = (uint32_t)p - a.st.start[s];
-        const uint32_t prev = r > 0 ? a.st.mut[(size_t)s * kMaxRounds + r - 1] : kNone;
-        if (r == 0 || rel > prev) {
-            Ctx c = make_ctx(a);
-            if (r > 0) hdr[1] = a.st.hdr[p];
-            const Meta m = a.st.meta[(size_t)s * (kMaxRounds + 1) + r];
-            cand = would_mutate(TYPE, reinterpret_cast<const uint8_t *>(hdr), m, c);
-        }
+    if (s != kNone && a.st.done[s] == kNotDone && (uint32_t)p > mut_read(a, s, r - 1)) {
+        uint64_t hdr[2] = {0, a.st.hdr[p]};
+        const Meta m = a.st.meta[(size_t)s * (kMaxRounds + 1) + r];
+        Ctx c = make_ctx(a);
+        cand = would_mutate(TYPE, reinterpret_cast<const uint8_t *>(hdr), m, c);
     }
-    // candidates of one segment are consecutive among a wavefront's candidate lanes (sorted
-    // order): only the first of each run issues the atomicMin
-    const unsigned long long cm = __ballot(cand);
-    const unsigned long long below = cm & ((1ull << lane) - 1ull);
-    const int prev_lane = below ? 63 - __clzll((long long)below) : -1;
-    const uint32_t prev_s = __shfl(s, prev_lane < 0 ? lane : prev_lane, 64);
-    if (cand && (prev_lane < 0 || prev_s != s)) {
-        uint32_t *f = &a.st.mut[(size_t)s * kMaxRounds + r];
-        if (rel < __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(f, rel);
-    }
+    offer_candidate(a, cand, s, r, (uint32_t)p);
 }
 
 template <int TYPE, int SV>
@@ -380,9 +393,8 @@ __global__ __launch_bounds__(256) void k_round_apply(SegmentArgs a, int r)
 {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= a.st.lidx[a.n - 1] || a.st.done[s] != kNotDone) return;
-    const uint32_t start = a.st.start[s];
-    uint8_t *entry = entry_of(a, a.keys[start]);
-    const uint32_t f = a.st.mut[(size_t)s * kMaxRounds + r];
+    uint8_t *entry = entry_of(a, a.keys[a.st.start[s]]);
+    const uint32_t f = mut_read(a, s, r);
     Meta m = a.st.meta[(size_t)s * (kMaxRounds + 1) + r];
     if (f == kNone) {
         a.st.done[s] = (uint8_t)r;
@@ -396,7 +408,7 @@ __global__ __launch_bounds__(256) void k_round_apply(SegmentArgs a, int r)
     Ctx c = make_ctx(a);
     uint8_t *x;
     uint8_t idx;
-    elem_at(a, a.vals[start + f], x, idx, c);
+    elem_at(a, a.vals[f], x, idx, c);
     dispatch<SV>(TYPE, x, entry, idx, m, c);
     a.st.meta[(size_t)s * (kMaxRounds + 1) + r + 1] = m;
     if (r == kMaxRounds - 1) a.st.fallback[atomicAdd(&a.st.count[1], 1u)] = s;
@@ -409,15 +421,14 @@ __global__ __launch_bounds__(256) void k_round_resolve(SegmentArgs a)
     if (p >= a.n) return;
     const uint32_t s = a.st.seg_of[p];
     if (s == kNone) return;
-    const uint32_t rel = (uint32_t)p - a.st.start[s];
     const uint8_t done = a.st.done[s];
     int r = 0;
     uint32_t f = kNone;
     for (; r < kMaxRounds; ++r) {
-        f = (done != kNotDone && r == done) ? kNone : a.st.mut[(size_t)s * kMaxRounds + r];
-        if (rel <= f) break;
+        f = (done != kNotDone && r == done) ? kNone : mut_read(a, s, r);
+        if ((uint32_t)p <= f) break;
     }
-    if (r == kMaxRounds || rel == f) return;  // left to k_long_exec, or applied by a round
+    if (r == kMaxRounds || (uint32_t)p == f) return;  // left to k_long_exec, or applied by a round
     const uint8_t *img = f == kNone ? entry_of(a, a.keys[p])
                                     : a.st.snap + ((size_t)s * kMaxRounds + r) * a.g.entry_size;
     const Meta m = a.st.meta[(size_t)s * (kMaxRounds + 1) + r];
@@ -464,16 +475,15 @@ __global__ __launch_bounds__(kLongThreads) void k_long_exec(SegmentArgs a)
     Ctx c = make_ctx(a);
     for (uint32_t i = blockIdx.x; i < nfb; i += gridDim.x) {
         const uint32_t s = a.st.fallback[i];
-        const uint32_t start = a.st.start[s], len = a.st.len[s];
-        const uint32_t first = a.st.mut[(size_t)s * kMaxRounds + kMaxRounds - 1] + 1;
-        uint8_t *entry = entry_of(a, a.keys[start]);
+        const uint32_t first = mut_read(a, s, kMaxRounds - 1) + 1, end = a.st.end[s];
+        uint8_t *entry = entry_of(a, a.keys[first - 1]);
         if (tid == 0) sm = a.st.meta[(size_t)s * (kMaxRounds + 1) + kMaxRounds];
         __syncthreads();
-        for (uint32_t base = first; base < len; base += kLongChunk) {
+        for (uint32_t base = first; base < end; base += kLongChunk) {
             uint32_t pending = 0;
 #pragma unroll
             for (int j = 0; j < kPerThread; ++j)
-                if (base + j * kLongThreads + tid < len) pending |= 1u << j;
+                if (base + j * kLongThreads + tid < end) pending |= 1u << j;
             for (;;) {
                 const Meta m = sm;
                 int mine = kLongChunk;
@@ -482,7 +492,7 @@ __global__ __launch_bounds__(kLongThreads) void k_long_exec(SegmentArgs a)
                     if (!(pending >> j & 1u)) continue;
                     uint8_t *x;
                     uint8_t idx;
-                    elem_at(a, a.vals[start + base + j * kLongThreads + tid], x, idx, c);
+                    elem_at(a, a.vals[base + j * kLongThreads + tid], x, idx, c);
                     if (would_mutate(TYPE, x, m, c)) mine = j * kLongThreads + tid;
                 }
                 const int f = block_min<kLongThreads>(mine, red);
@@ -492,7 +502,7 @@ __global__ __launch_bounds__(kLongThreads) void k_long_exec(SegmentArgs a)
                     if (!(pending >> j & 1u) || pos >= f) continue;
                     uint8_t *x;
                     uint8_t idx;
-                    elem_at(a, a.vals[start + base + pos], x, idx, c);
+                    elem_at(a, a.vals[base + pos], x, idx, c);
                     Meta t = m;
                     dispatch<SV>(TYPE, x, entry, idx, t, c);
                     if (a.error_flags && !meta_equal(t, m)) atomicOr(a.error_flags, 1u);
@@ -502,7 +512,7 @@ __global__ __launch_bounds__(kLongThreads) void k_long_exec(SegmentArgs a)
                 if (f < kLongChunk && (f % kLongThreads) == tid) {
                     uint8_t *x;
                     uint8_t idx;
-                    elem_at(a, a.vals[start + base + f], x, idx, c);
+                    elem_at(a, a.vals[base + f], x, idx, c);
                     Meta mm = m;
                     dispatch<SV>(TYPE, x, entry, idx, mm, c);
                     pending &= ~(1u << (f / kLongThreads));
@@ -674,8 +684,9 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 size_t seg_scratch_bytes(int64_t n, uint32_t entry_size)
 {
     const size_t cap = (size_t)(n / (kShortSeg + 1) + 1);
-    return align256(4 * (size_t)n) * 2 + align256(8 * (size_t)n) + align256(4 * cap) * 2 + 256 + align256(sizeof(Meta) * cap * (kMaxRounds + 1)) +
-           align256(4 * cap * kMaxRounds) + align256(cap) + (size_t)entry_size * cap * kMaxRounds;
+    return align256(4 * (size_t)n) * 2 + align256(8 * (size_t)n) + align256(4 * cap) * 2 + 256 +
+           align256(sizeof(Meta) * cap * (kMaxRounds + 1)) + align256(8 * cap * kMaxRounds) + align256(cap) +
+           (size_t)entry_size * cap * kMaxRounds;
 }
 
 void seg_carve(BatchLaunch &bl, uint8_t *base, int64_t n, uint32_t entry_size)
@@ -692,10 +703,10 @@ void seg_carve(BatchLaunch &bl, uint8_t *base, int64_t n, uint32_t entry_size)
     bl.seg_of = reinterpret_cast<uint32_t *>(take(4 * (size_t)n));
     bl.seg_hdr = reinterpret_cast<uint64_t *>(take(8 * (size_t)n));
     bl.seg_start = reinterpret_cast<uint32_t *>(take(4 * cap));
-    bl.seg_len = reinterpret_cast<uint32_t *>(take(4 * cap));
+    bl.seg_end = reinterpret_cast<uint32_t *>(take(4 * cap));
     bl.seg_count = reinterpret_cast<uint32_t *>(take(8));
     bl.seg_meta = take(sizeof(Meta) * cap * (kMaxRounds + 1));
-    bl.seg_mut = reinterpret_cast<uint32_t *>(take(4 * cap * kMaxRounds));
+    bl.seg_mut = reinterpret_cast<unsigned long long *>(take(8 * cap * kMaxRounds));
     bl.seg_done = take(cap);
     bl.seg_snap = p;
     bl.seg_cap = (uint32_t)cap;
@@ -726,7 +737,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
         return -2;
     SegmentArgs sa;
     sa.st.start = bl.seg_start;
-    sa.st.len = bl.seg_len;
+    sa.st.end = bl.seg_end;
     sa.st.count = bl.seg_count;
     sa.st.fallback = bl.seg_fallback;
     sa.st.lidx = bl.keys_a;  // the sort's input keys are free again
@@ -737,6 +748,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     sa.st.done = bl.seg_done;
     sa.st.snap = bl.seg_snap;
     sa.st.cap = bl.seg_cap;
+    sa.st.epoch = bl.epoch;
     sa.elems = bl.elems;
     sa.log = bl.log;
     sa.rw = bl.rw;
@@ -775,7 +787,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
                                segment_exec_lds<256>(bl.esz, bl.g.entry_size), s, sa);              \
         }                                                                                           \
         for (int r = 0; r < kMaxRounds; ++r) {                                                      \
-            hipLaunchKernelGGL((k_round_cand<T>), dim3(grid), dim3(256), 0, s, sa, r);              \
+            if (r > 0) hipLaunchKernelGGL((k_round_cand<T>), dim3(grid), dim3(256), 0, s, sa, r);   \
             hipLaunchKernelGGL((k_round_apply<T, V>), dim3(sgrid), dim3(256), 0, s, sa, r);         \
         }                                                                                           \
         hipLaunchKernelGGL((k_round_resolve<T, V>), dim3(grid), dim3(256), 0, s, sa);               \

@@ -32,6 +32,7 @@ struct hkv_table {
     // batch scratch
     uint32_t *d_keys_a = nullptr, *d_keys_b = nullptr, *d_vals_a = nullptr, *d_vals_b = nullptr;
     uint8_t *d_seg = nullptr;          // long-segment round state (seg_carve)
+    uint32_t epoch = 0;                // batch launches since d_seg was initialised
     unsigned int *d_error_flags = nullptr;
     int64_t scratch_n = 0;
     void *d_sort_tmp = nullptr;
@@ -146,6 +147,9 @@ static int ensure_scratch(hkv_table *t, int64_t n, int key_bits)
         HIP_TRY(hipMalloc(&t->d_vals_a, cap * 4));
         HIP_TRY(hipMalloc(&t->d_vals_b, cap * 4));
         HIP_TRY(hipMalloc(&t->d_seg, seg_scratch_bytes(cap, t->geo.entry_size)));
+        // all-ones: the epoch-tagged round words then read as "no candidate" for every epoch
+        HIP_TRY(hipMemset(t->d_seg, 0xFF, seg_scratch_bytes(cap, t->geo.entry_size)));
+        t->epoch = 0;
         t->scratch_n = cap;
     }
     size_t need = sort_temp_bytes(t->scratch_n, key_bits > 0 ? key_bits : 32);
@@ -354,6 +358,11 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.sort_tmp = t->d_sort_tmp;
     bl.sort_tmp_bytes = t->sort_tmp_bytes;
     seg_carve(bl, t->d_seg, t->scratch_n, t->geo.entry_size);
+    if (++t->epoch == 0xFFFFFFFFu) {  // tag ~epoch would reach 0: start the words over
+        HIP_TRY(hipMemsetAsync(t->d_seg, 0xFF, seg_scratch_bytes(t->scratch_n, t->geo.entry_size), s));
+        t->epoch = 1;
+    }
+    bl.epoch = t->epoch;
     bl.error_flags = t->d_error_flags;
     bl.n = n;
     bl.n_batches = d->n_batches;

@@ -118,7 +118,7 @@ def main():
                                 retry_stalled=a.retry)
     else:
         rnd = Round(kvs, a.workers, L.membership(3, 0), [1, 2], z, a.write_permille, seed=a.seed,
-                    max_steps=total_steps + 1, retry_stalled=a.retry)
+                    max_steps=total_steps + 2, retry_stalled=a.retry)
     torch.cuda.synchronize()
 
     for _ in range(a.warmup):
@@ -127,8 +127,7 @@ def main():
     if world > 1:
         dist.barrier()
     c0 = rnd.counters[:4].clone()
-    e0 = rnd.elem_totals.clone()
-    inv0 = rnd.inv_total.clone() if hasattr(rnd, "inv_total") else None
+    rnd.count_elems = False  # element bookkeeping runs in one probe step after the timed region
     events: dict = {}
     torch.cuda.synchronize()
     if world > 1:
@@ -143,11 +142,16 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t
     c1 = rnd.counters[:4].clone()
-    e1 = rnd.elem_totals.clone()
-    n_inv, n_ack, n_val = ((e1 - e0).double() / a.steps).tolist()
     committed = int((c1[0] - c0[0]).item())
     writes = int((c1[2] - c0[2]).item())
-    puts_ok = int((rnd.inv_total - inv0).item()) if inv0 is not None else writes
+    # probe step (untimed): elements each batch launch applies, for the roofline's bytes
+    rnd.count_elems = True
+    e0, inv0 = rnd.elem_totals.clone(), rnd.inv_total.clone()
+    rnd.step()
+    torch.cuda.synchronize()
+    n_inv, n_ack, n_val = (rnd.elem_totals - e0).double().tolist()
+    puts_per_step = float((rnd.inv_total - inv0).item())
+    puts_ok = puts_per_step * a.steps
 
     if world > 1:
         tt = torch.tensor([committed, elapsed * 1e9], dtype=torch.float64, device="cuda")

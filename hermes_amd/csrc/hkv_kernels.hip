@@ -204,7 +204,16 @@ struct SegmentArgs {
     uint32_t skip_key;
     uint8_t g_membership;
     uint8_t w_ack_init;
+    int32_t rounds;          // chip-wide rounds before k_long_exec (<= kMaxRounds)
 };
+
+// Rounds per batch type: how many mutations a hot key usually sees in one launch. A local
+// batch has one write per key (later writes stall on its WRITE state), a VAL batch validates
+// once, an ACK batch sets one ack bit and completes; INVs with rising timestamps keep mutating.
+__host__ __device__ constexpr int rounds_for(int type)
+{
+    return type == kLocal || type == kVals ? 2 : type == kAcks ? 3 : kMaxRounds;
+}
 
 __device__ __forceinline__ Ctx make_ctx(const SegmentArgs &a)
 {
@@ -411,7 +420,7 @@ __global__ __launch_bounds__(256) void k_round_apply(SegmentArgs a, int r)
     elem_at(a, a.vals[f], x, idx, c);
     dispatch<SV>(TYPE, x, entry, idx, m, c);
     a.st.meta[(size_t)s * (kMaxRounds + 1) + r + 1] = m;
-    if (r == kMaxRounds - 1) a.st.fallback[atomicAdd(&a.st.count[1], 1u)] = s;
+    if (r == a.rounds - 1) a.st.fallback[atomicAdd(&a.st.count[1], 1u)] = s;
 }
 
 template <int TYPE, int SV>
@@ -424,11 +433,11 @@ __global__ __launch_bounds__(256) void k_round_resolve(SegmentArgs a)
     const uint8_t done = a.st.done[s];
     int r = 0;
     uint32_t f = kNone;
-    for (; r < kMaxRounds; ++r) {
+    for (; r < a.rounds; ++r) {
         f = (done != kNotDone && r == done) ? kNone : mut_read(a, s, r);
         if ((uint32_t)p <= f) break;
     }
-    if (r == kMaxRounds || (uint32_t)p == f) return;  // left to k_long_exec, or applied by a round
+    if (r == a.rounds || (uint32_t)p == f) return;  // left to k_long_exec, or applied by a round
     const uint8_t *img = f == kNone ? entry_of(a, a.keys[p])
                                     : a.st.snap + ((size_t)s * kMaxRounds + r) * a.g.entry_size;
     const Meta m = a.st.meta[(size_t)s * (kMaxRounds + 1) + r];
@@ -475,9 +484,9 @@ __global__ __launch_bounds__(kLongThreads) void k_long_exec(SegmentArgs a)
     Ctx c = make_ctx(a);
     for (uint32_t i = blockIdx.x; i < nfb; i += gridDim.x) {
         const uint32_t s = a.st.fallback[i];
-        const uint32_t first = mut_read(a, s, kMaxRounds - 1) + 1, end = a.st.end[s];
+        const uint32_t first = mut_read(a, s, a.rounds - 1) + 1, end = a.st.end[s];
         uint8_t *entry = entry_of(a, a.keys[first - 1]);
-        if (tid == 0) sm = a.st.meta[(size_t)s * (kMaxRounds + 1) + kMaxRounds];
+        if (tid == 0) sm = a.st.meta[(size_t)s * (kMaxRounds + 1) + a.rounds];
         __syncthreads();
         for (uint32_t base = first; base < end; base += kLongChunk) {
             uint32_t pending = 0;
@@ -764,6 +773,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     sa.skip_key = bl.skip_key;
     sa.g_membership = bl.g_membership;
     sa.w_ack_init = bl.w_ack_init;
+    sa.rounds = rounds_for(bl.type);
     {
         HeadIter it(rocprim::counting_iterator<uint32_t>(0), LongHeadFlag{bl.keys_b, bl.skip_key, (uint32_t)n});
         size_t tb = bl.sort_tmp_bytes;
@@ -786,7 +796,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
             hipLaunchKernelGGL((k_segment_exec<T, V, 256>), dim3(grid), dim3(256),                  \
                                segment_exec_lds<256>(bl.esz, bl.g.entry_size), s, sa);              \
         }                                                                                           \
-        for (int r = 0; r < kMaxRounds; ++r) {                                                      \
+        for (int r = 0; r < sa.rounds; ++r) {                                                       \
             if (r > 0) hipLaunchKernelGGL((k_round_cand<T>), dim3(grid), dim3(256), 0, s, sa, r);   \
             hipLaunchKernelGGL((k_round_apply<T, V>), dim3(sgrid), dim3(256), 0, s, sa, r);         \
         }                                                                                           \

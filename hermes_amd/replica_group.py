@@ -84,6 +84,7 @@ class ReplicaRound:
         self.counters = torch.zeros(4096, dtype=torch.int64, device=dev)  # HKV_WL_COUNTER_WORDS
         self.inv_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.elem_totals = torch.zeros(3, dtype=torch.int64, device=dev)  # INV, ACK, VAL elements applied
+        self.count_elems = True        # keep inv_total / elem_totals (small torch ops per phase)
         self.trace_len = trace_len
         self.trace_key = torch.empty(W * trace_len, dtype=torch.int64, device=dev)
         self.trace_op = torch.empty(W * trace_len, **u8)
@@ -103,7 +104,8 @@ class ReplicaRound:
         self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, LOCAL, self.op, self.mb)
         check(_L.hkv_wl_marshal_invs_cap(_ptr(self.ops), self.W, LOCAL, self.op, _ptr(self.inv_slab), self.C,
                                          _ptr(self.inv_count), self.rank, _ptr(self.held), _s()), "marshal_invs")
-        self.inv_total += self.inv_count.sum()
+        if self.count_elems:
+            self.inv_total += self.inv_count.sum()
 
     def _own_row(self, counts: torch.Tensor) -> torch.Tensor:
         return counts[self.rank * self.W:(self.rank + 1) * self.W]
@@ -112,7 +114,8 @@ class ReplicaRound:
         """Apply the gathered INVs of the peers (inv_recv [N][W][C], inv_recv_count [N][W]);
         their ACKs go to ack_slab row p (for rank p), counts in ack_slab_count."""
         self._own_row(self.inv_recv_count).zero_()
-        self.elem_totals[0] += self.inv_recv_count.sum()
+        if self.count_elems:
+            self.elem_totals[0] += self.inv_recv_count.sum()
         self.kvs.batch(L.BatchType.invs, self.inv_recv, self.N * self.W, self.C, self.op, self.mb,
                        counts=self.inv_recv_count)
         check(_L.hkv_wl_marshal_acks_rows(_ptr(self.inv_recv), _ptr(self.inv_recv_count), self.N * self.W, self.C,
@@ -125,7 +128,8 @@ class ReplicaRound:
         N, W, C = self.N, self.W, self.C
         check(_L.hkv_wl_regroup(_ptr(self.ack_recv), _ptr(self.ack_recv_count), N, W, C, self.ack_size,
                                 _ptr(self.ack_batch), N * C, _ptr(self.ack_batch_count), _s()), "regroup")
-        self.elem_totals[1] += self.ack_batch_count.sum()
+        if self.count_elems:
+            self.elem_totals[1] += self.ack_batch_count.sum()
         self.kvs.batch(L.BatchType.acks, self.ack_batch, W, N * C, self.ack_size, self.mb,
                        counts=self.ack_batch_count, rw=self.ops, rw_stride_bytes=LOCAL * self.op)
         check(_L.hkv_wl_collect_vals(_ptr(self.ack_batch), _ptr(self.ack_batch_count), W, N * C, self.ack_size,
@@ -135,7 +139,8 @@ class ReplicaRound:
     def vals(self):
         """Apply the gathered VALs of the peers (val_recv [N][W][C], val_recv_count [N][W])."""
         self._own_row(self.val_recv_count).zero_()
-        self.elem_totals[2] += self.val_recv_count.sum()
+        if self.count_elems:
+            self.elem_totals[2] += self.val_recv_count.sum()
         self.kvs.batch(L.BatchType.vals, self.val_recv, self.N * self.W, self.C, L.OP_META_SIZE, self.mb,
                        counts=self.val_recv_count)
 
@@ -175,6 +180,14 @@ class ReplicaGroupRound:
         self.counters = self.r.counters
         self.inv_total = self.r.inv_total
         self.elem_totals = self.r.elem_totals
+
+    @property
+    def count_elems(self) -> bool:
+        return self.r.count_elems
+
+    @count_elems.setter
+    def count_elems(self, v: bool) -> None:
+        self.r.count_elems = v
 
     def _gather(self, out, inp):
         self.dist.all_gather_into_tensor(out, inp, group=self.group)

@@ -118,6 +118,7 @@ class Round:
         self.counters = torch.zeros(4096, dtype=torch.int64, device=dev)  # HKV_WL_COUNTER_WORDS
         self.inv_total = torch.zeros(1, dtype=torch.int64, device=dev)
         self.elem_totals = torch.zeros(3, dtype=torch.int64, device=dev)  # INV, ACK, VAL elements applied
+        self.count_elems = True        # keep inv_total / elem_totals (small torch ops per step)
         self.peer_t = torch.tensor(self.peers or [0], dtype=torch.uint8, device=dev)
         self.trace_len = trace_len
         self.trace_key = torch.empty(W * trace_len, dtype=torch.int64, device=dev)
@@ -198,18 +199,20 @@ class Round:
         k = self.clock % max(len(self.remote_inv), 1)
         timed("local", self.local_batch)
         self.marshal_invs()
-        self.inv_total += self.inv_count.sum()
+        if self.count_elems:
+            self.inv_total += self.inv_count.sum()
         if self.R:
             self.virtual_peer_acks()
             ri, rv = self.remote_inv[k], self.remote_val[k]
             timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride))
             self.marshal_acks(ri, self.W * self.rstride, self.ack_out)
             timed("acks", self.ack_batch)
-            self.elem_totals[1] += self.ack_count.sum()
+            if self.count_elems:
+                self.elem_totals[1] += self.ack_count.sum()
             self.marshal_vals(self.acks, self.W * self.ack_stride, self.val_out)
             timed("vals", lambda: self.val_batch(rv, self.W, self.rstride))
         self.refill()
-        if self.R:
+        if self.R and self.count_elems:
             self.elem_totals[0] += self.W * self.rstride
             self.elem_totals[2] += self.W * self.rstride
         self.clock += 1

@@ -197,7 +197,7 @@ def main():
             "elements_per_step": {"inv": n_inv, "ack": n_ack, "val": n_val},
         },
         "roofline": {
-            "bound": "hbm", "kernel": f"{dom} batch (k_lookup + radix sort + k_segment_exec)",
+            "bound": "hbm", "kernel": f"{dom} batch launch (k_lookup + element-order rounds, hkv_batch.hip)",
             "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
             "traffic": None, "launch_ms": ms.get(dom), "algorithmic_bytes_per_launch": per_launch_bytes[dom],
             "batch_ms": ms,

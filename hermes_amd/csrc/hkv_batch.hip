@@ -1,0 +1,645 @@
+// hkv_batch.hip -- the HermesKV batch path on gfx950 (hermes_batch_ops_to_KVS, hermesKV.c:905-996).
+//
+// One launch applies n_batches batches of one type. Its result is defined as the reference
+// applying them element by element in concatenation order. Nothing is sorted: elements stay in
+// element order, and the elements of each key are resolved in rounds.
+//
+//   k_lookup    one element per 4 lanes, in element order: skip test (hermesKV.c:709-769),
+//               bucket probe over the 64-B bucket (hermesKV.c:952-975), wrap test, 8-B key
+//               compare (hermesKV.c:977-993; a miss writes ST_MISS into byte 9). A hit claims its
+//               key's slot g in the launch's group table, reads the key's object meta S_0 from
+//               the same log line, and offers itself as round 0's first candidate if
+//               would_mutate(elem, S_0) (hkv_exec.h).
+//   round r     every key keeps F_r, the smallest element index among its candidates (one
+//               atomicMin on the slot's F word). Then
+//                 k_resolve: an element before F_r (or of a key without a candidate) sees S_r in
+//                   the sequential order and S_r does not change under it: it runs the
+//                   reference's exec function on a private copy of S_r against the live entry,
+//                   in parallel with everything else. F_r itself goes to the apply list, later
+//                   elements to the pending list of round r+1.
+//                 k_apply: F_r runs the exec function on the entry, S_r -> S_{r+1}.
+//                 k_cand (r+1): every pending element tests would_mutate against S_{r+1}.
+//               Value reads of a round (GETs, INV-aborts) all happen in k_resolve, before the
+//               round's one mutation per key in k_apply, so they see the value of S_r.
+//   fallback    elements still pending after the last round (keys mutated in every round) are
+//               gathered per key, sorted by element index, and finished by one workgroup per
+//               key with first-candidate passes over chunks (k_fb_exec).
+//
+// Exactness rests on one property: would_mutate() is sound (false => the exec function leaves
+// the meta unchanged). Every resolved element checks it: a private copy that did change raises
+// bit 0 of *error_flags, which every parity test asserts is zero.
+//
+// Slots and F words are tagged with the launch (key word) and the round (F word), so no scratch
+// is cleared between launches: a slot whose tag is older reads as empty, and a newer round's F
+// value is numerically smaller than every older one, so atomicMin replaces stale words.
+#include <hip/hip_runtime.h>
+
+#include "hkv_exec.h"
+#include "hkv_internal.h"
+
+namespace hkv {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+enum : uint8_t { kStDone = 0, kStApply = 1, kStPend = 2, kStCand0 = 3 };  // per-element stage between passes
+enum { kCtrFbK = 0, kCtrFbM = 1 };                           // fallback keys, fallback member cursor
+
+struct BatchArgs {
+    uint8_t *elems;
+    const int32_t *counts;
+    const uint8_t *index;
+    uint8_t *log;
+    uint8_t *rw;
+    int32_t *ns_idx;
+    unsigned long long *fw;      // [log_cap / 64] F word per 64-B log line (table-wide), see fw_index
+    uint32_t fw_mask;
+    uint32_t *ent;               // [n] entry id of every element (kNone: skipped or missing)
+    uint8_t *st;                 // [n] stage (kSt*)
+    uint32_t *mem;               // [2 cap] fallback members, per key padded to a power of two
+    uint32_t *fbk;               // [cap] fallback keys: entry id
+    uint32_t *fbc;               // [cap] member count
+    uint32_t *fbo;               // [cap] member offset
+    uint32_t *fbf;               // [cap] fill cursor
+    uint32_t *ctr;               // kCtr*
+    unsigned int *error_flags;
+    Geometry g;
+    int64_t n;
+    int64_t rw_stride;
+    int32_t stride;
+    int32_t esz;
+    int32_t type;
+    uint32_t rtag0;              // round 0's tag; round r uses rtag0 + r
+    int32_t rounds;              // rounds after round 0 before the fallback
+    uint8_t g_membership;
+    uint8_t w_ack_init;
+};
+
+// Rounds per batch type: mutations a hot key usually sees in one launch. A local batch has one
+// write per key (later writes stall on its WRITE state), a VAL batch validates once, an ACK batch
+// sets an ack bit and completes, INVs from two peers with two versions mutate up to four times.
+__host__ __device__ constexpr int rounds_for(int type)
+{
+    return type == kLocal || type == kVals ? 1 : type == kInvs ? 4 : 2;
+}
+
+__device__ __forceinline__ Ctx make_ctx(const BatchArgs &a)
+{
+    Ctx c;
+    c.g = a.g;
+    c.g_membership = a.g_membership;
+    c.w_ack_init = a.w_ack_init;
+    c.rw = nullptr;
+    return c;
+}
+
+__device__ __forceinline__ void elem_at(const BatchArgs &a, uint32_t i, uint8_t *&x, uint8_t &idx, Ctx &c)
+{
+    const uint32_t b = i / (uint32_t)a.stride;
+    idx = (uint8_t)(i - b * (uint32_t)a.stride);
+    c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
+    x = a.elems + (int64_t)i * a.esz;
+}
+
+__device__ __forceinline__ uint64_t phys_of(const BatchArgs &a, uint32_t e) { return (uint64_t)e * a.g.entry_unit; }
+__device__ __forceinline__ uint8_t *entry_of(const BatchArgs &a, uint32_t e) { return a.log + phys_of(a, e); }
+// Live entries never overlap and are at least 64 B long, so their first 64-B lines are distinct.
+// The F word of line l sits at l * odd mod 2^k (a bijection on the log's 2^k lines): keys that are
+// neighbours in the log -- the hottest ids of a populated table are -- get F words on different
+// lines, and memory-side atomics on one line serialise.
+__device__ __forceinline__ uint32_t fw_index(const BatchArgs &a, uint64_t phys)
+{
+    return (uint32_t)(((phys >> 6) * 0x9E3779B1ull) & a.fw_mask);
+}
+__device__ __forceinline__ unsigned long long *fw_of(const BatchArgs &a, uint32_t e) { return a.fw + fw_index(a, phys_of(a, e)); }
+
+__device__ __forceinline__ uint32_t first_cand(unsigned long long f, uint32_t rtag)
+{
+    return (uint32_t)(f >> 32) == ~rtag ? (uint32_t)f : kNone;
+}
+
+// F_r: atomicMin of ((~round tag) << 32 | element). The load filters most offers of a hot key:
+// F only falls, and elements are dispatched roughly in element order.
+__device__ __forceinline__ void offer(unsigned long long *f, uint32_t rtag, uint32_t i)
+{
+    const unsigned long long v = ((unsigned long long)(~rtag) << 32) | i;
+    if (v < __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(f, v);
+}
+
+// Wave-aggregated atomicAdd(&arr[j], 1): one atomic per distinct j in the wave; each active lane
+// gets its own ticket. All 64 lanes must call it.
+__device__ __forceinline__ uint32_t agg_ticket(uint32_t *arr, uint32_t j, bool active)
+{
+    const int lane = threadIdx.x & 63;
+    uint32_t ticket = 0;
+    unsigned long long left = __ballot(active);
+    while (left) {
+        const int leader = __ffsll((long long)left) - 1;
+        const uint32_t jl = __shfl(j, leader, 64);
+        const unsigned long long m = left & __ballot(active && j == jl);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&arr[jl], (uint32_t)__popcll(m));
+        base = __shfl(base, leader, 64);
+        if ((m >> lane) & 1ull) ticket = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        left &= ~m;
+    }
+    return ticket;
+}
+
+template <int TYPE, int SV>
+__device__ __forceinline__ void resolve_elem(const BatchArgs &a, uint32_t i, uint8_t *entry)
+{
+    Ctx c = make_ctx(a);
+    uint8_t *x;
+    uint8_t idx;
+    elem_at(a, i, x, idx, c);
+    Meta m;
+    meta_load(entry, m);
+    Meta t = m;
+    dispatch<SV>(TYPE, x, entry, idx, t, c);
+    if (a.error_flags && !meta_equal(t, m)) atomicOr(a.error_flags, 1u);
+}
+
+// ------------------------------------------------------------------ k_lookup (+ round 0 candidates)
+// A hit that would mutate the meta as it stands (S_0) is marked kStCand0 for k_cand's round 0.
+// Four lanes per element: each lane reads 16 bytes (two slots) of the element's 64-byte bucket,
+// so one load instruction covers a whole bucket line per element. Slots are searched in the
+// reference's order (first tag match wins, hermesKV.c:954-975).
+constexpr int kLookupPerBlock = 64;
+__global__ __launch_bounds__(256) void k_lookup(BatchArgs a)
+{
+    const int q = threadIdx.x & 3;
+    const int lane = threadIdx.x & 63;
+    const int64_t gi = (int64_t)blockIdx.x * kLookupPerBlock + (threadIdx.x >> 2);
+    const bool in = gi < a.n;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.ctr[kCtrFbK] = 0;
+        a.ctr[kCtrFbM] = 0;
+    }
+    int32_t b = 0, idx = 0;
+    uint8_t *x = nullptr;
+    uint64_t key = 0, hdr = 0;
+    int probe = 0;
+    if (in && q == 0) {
+        b = (int32_t)(gi / a.stride);
+        idx = (int32_t)(gi - (int64_t)b * a.stride);
+        if (a.counts == nullptr || idx < a.counts[b]) {
+            x = a.elems + gi * a.esz;
+            key = ld64(x);
+            hdr = ld64(x + 8);
+            if (skip_elem_os(a.type, (uint8_t)hdr, (uint8_t)(hdr >> 8))) {
+                if (a.type == kInvs && a.ns_idx) atomicMax(&a.ns_idx[b], idx);
+            } else {
+                probe = 1;
+            }
+        }
+    }
+    probe = __shfl(probe, 0, 4);
+    key = __shfl(key, 0, 4);
+    uint64_t s0 = 0, s1 = 0;
+    if (probe) {
+        const uint4 v = reinterpret_cast<const uint4 *>(a.index + ((key & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u)[q];
+        s0 = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        s1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    }
+    const uint32_t tag = (uint32_t)(key >> 48);
+    const bool m0 = probe && (s0 & 1u) && ((uint32_t)(s0 >> 1) & 0x7FFFFFu) == tag;
+    const bool m1 = probe && (s1 & 1u) && ((uint32_t)(s1 >> 1) & 0x7FFFFFu) == tag;
+    const int gbase = lane & ~3;
+    const uint32_t g0 = (uint32_t)(__ballot(m0) >> gbase) & 0xFu;
+    const uint32_t g1 = (uint32_t)(__ballot(m1) >> gbase) & 0xFu;
+    uint32_t order = 0;  // bit 2*l + j: slot 2*l + j matches
+#pragma unroll
+    for (int l = 0; l < 4; ++l) order |= ((g0 >> l) & 1u) << (2 * l) | ((g1 >> l) & 1u) << (2 * l + 1);
+    const int first = order ? __ffs(order) - 1 : 0;
+    const uint64_t off = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
+    if (!in || q != 0) return;
+    uint32_t e = kNone;
+    uint8_t st = kStDone;
+    if (probe) {
+        bool hit = false;
+        uint64_t phys = 0;
+        if (order && a.g.log_head - off < a.g.log_cap) {
+            phys = off & a.g.log_mask;
+            hit = ld64(a.log + phys + 8) == key;
+        }
+        if (hit) {
+            Meta m0;
+            meta_load(a.log + phys, m0);
+            e = (uint32_t)(phys / a.g.entry_unit);
+            uint64_t h2[2] = {0, hdr};
+            Ctx c = make_ctx(a);
+            if (would_mutate(a.type, reinterpret_cast<const uint8_t *>(h2), m0, c)) st = kStCand0;
+        } else {
+            x[9] = kMiss;
+        }
+    }
+    a.ent[gi] = e;
+    a.st[gi] = st;
+}
+
+// ------------------------------------------------------------------ rounds (passes over all elements)
+// Candidates of round r, aggregated per key in LDS over kCandPer * 256 elements, so a hot key costs
+// one atomicMin per block instead of one per candidate (atomics execute at the memory side, and
+// one address serialises them). Round 0's candidates were marked by k_lookup; later rounds test
+// pending elements against S_r, the entry as round r-1 left it.
+constexpr int kCandPer = 4;
+constexpr int kCandSlots = 2048;  // >= 2 * kCandPer * 256: the probe always ends
+template <int TYPE>
+__global__ __launch_bounds__(256) void k_cand(BatchArgs a, int r)
+{
+    __shared__ uint32_t lk[kCandSlots], lv[kCandSlots];
+    for (int j = threadIdx.x; j < kCandSlots; j += 256) {
+        lk[j] = kNone;
+        lv[j] = kNone;
+    }
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * 256 * kCandPer;
+#pragma unroll
+    for (int k = 0; k < kCandPer; ++k) {
+        const int64_t i = base + k * 256 + threadIdx.x;
+        if (i >= a.n) break;
+        const uint8_t st = a.st[i];
+        if (st != (r == 0 ? kStCand0 : kStPend)) continue;
+        const uint32_t e = a.ent[i];
+        if (r > 0) {
+            Meta m;
+            meta_load(entry_of(a, e), m);
+            uint64_t h2[2] = {0, ld64(a.elems + i * a.esz + 8)};
+            Ctx c = make_ctx(a);
+            if (!would_mutate(TYPE, reinterpret_cast<const uint8_t *>(h2), m, c)) continue;
+        }
+        const uint32_t fi = fw_index(a, phys_of(a, e));
+        uint32_t h = (fi * 0x9E3779B1u) >> 21;
+        for (;;) {
+            const uint32_t old = atomicCAS(&lk[h], kNone, fi);
+            if (old == kNone || old == fi) {
+                atomicMin(&lv[h], (uint32_t)i);
+                break;
+            }
+            h = (h + 1) & (kCandSlots - 1);
+        }
+    }
+    __syncthreads();
+    const uint32_t rtag = a.rtag0 + (uint32_t)r;
+    for (int j = threadIdx.x; j < kCandSlots; j += 256)
+        if (lk[j] != kNone) offer(a.fw + lk[j], rtag, lv[j]);
+}
+
+// Round 0's resolve over every element, on LDS copies of the block's contiguous op slab (copied
+// in and out with 16-B accesses, so the byte-wise result writes never reach memory one by one).
+// Before F_0 (or no candidate) -> resolved now; == F_0 -> apply; after -> pending.
+template <int TYPE, int SV, int BP>
+__global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
+{
+    extern __shared__ uint4 sops[];
+    const int64_t i0 = (int64_t)blockIdx.x * BP;
+    const int cnt = a.n - i0 < BP ? (int)(a.n - i0) : BP;
+    const uint32_t bytes = (uint32_t)cnt * (uint32_t)a.esz;  // a multiple of 8
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.elems + i0 * a.esz);
+    for (uint32_t w = threadIdx.x; w < bytes / 16; w += BP) sops[w] = src[w];
+    if ((bytes & 8) && threadIdx.x == 0)
+        reinterpret_cast<uint64_t *>(sops)[bytes / 8 - 1] = reinterpret_cast<const uint64_t *>(src)[bytes / 8 - 1];
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < cnt) {
+        const int64_t i = i0 + t;
+        const uint32_t e = a.ent[i];
+        uint8_t st = kStDone;
+        if (e != kNone) {
+            const uint32_t f = first_cand(*fw_of(a, e), a.rtag0);
+            if (f == kNone || (uint32_t)i < f) {
+                Ctx c = make_ctx(a);
+                uint8_t *xg;
+                uint8_t idx;
+                elem_at(a, (uint32_t)i, xg, idx, c);
+                uint8_t *entry = entry_of(a, e);
+                Meta m;
+                meta_load(entry, m);
+                Meta tm = m;
+                dispatch<SV>(TYPE, reinterpret_cast<uint8_t *>(sops) + (uint32_t)t * a.esz, entry, idx, tm, c);
+                if (a.error_flags && !meta_equal(tm, m)) atomicOr(a.error_flags, 1u);
+            } else {
+                st = (uint32_t)i == f ? kStApply : kStPend;
+            }
+        }
+        a.st[i] = st;
+    }
+    __syncthreads();
+    uint4 *dst = reinterpret_cast<uint4 *>(a.elems + i0 * a.esz);
+    for (uint32_t w = threadIdx.x; w < bytes / 16; w += BP) dst[w] = sops[w];
+    if ((bytes & 8) && threadIdx.x == 0)
+        reinterpret_cast<uint64_t *>(dst)[bytes / 8 - 1] = reinterpret_cast<const uint64_t *>(sops)[bytes / 8 - 1];
+}
+
+// Round r >= 1 resolve over the pending elements (sparse: direct global access).
+template <int TYPE, int SV>
+__global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n || a.st[i] != kStPend) return;
+    const uint32_t e = a.ent[i];
+    const uint32_t f = first_cand(*fw_of(a, e), a.rtag0 + (uint32_t)r);
+    if (f == kNone || (uint32_t)i < f) {
+        resolve_elem<TYPE, SV>(a, (uint32_t)i, entry_of(a, e));
+        a.st[i] = kStDone;
+    } else if ((uint32_t)i == f) {
+        a.st[i] = kStApply;
+    }
+}
+
+// Round r's mutation per key. After the last round, a key that may still have pending elements
+// registers for the fallback; its F word then holds the registration (a value every later
+// launch's offers replace).
+template <int TYPE, int SV>
+__global__ __launch_bounds__(256) void k_apply(BatchArgs a, int r)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n || a.st[i] != kStApply) return;
+    const uint32_t e = a.ent[i];
+    uint8_t *entry = entry_of(a, e);
+    Ctx c = make_ctx(a);
+    uint8_t *x;
+    uint8_t idx;
+    elem_at(a, (uint32_t)i, x, idx, c);
+    Meta m;
+    meta_load(entry, m);
+    dispatch<SV>(TYPE, x, entry, idx, m, c);
+    meta_store(entry, m);
+    a.st[i] = kStDone;
+    if (r == a.rounds) {
+        const uint32_t j = atomicAdd(&a.ctr[kCtrFbK], 1u);
+        a.fbk[j] = e;
+        a.fbc[j] = 0;
+        a.fbf[j] = 0;
+        *fw_of(a, e) = 0xFFFFFFFF00000000ull | j;
+    }
+}
+
+// ------------------------------------------------------------------ fallback
+__device__ __forceinline__ uint32_t pow2ceil(uint32_t c) { return c <= 1 ? 1u : 1u << (32 - __clz(c - 1)); }
+
+__global__ __launch_bounds__(256) void k_fb_count(BatchArgs a)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (a.ctr[kCtrFbK] == 0) return;  // uniform: nothing fell back
+    const bool p = i < a.n && a.st[i] == kStPend;
+    const uint32_t j = p ? (uint32_t)*fw_of(a, a.ent[i]) : 0u;
+    agg_ticket(a.fbc, j, p);
+}
+
+__global__ __launch_bounds__(256) void k_fb_offsets(BatchArgs a)
+{
+    const uint32_t nk = a.ctr[kCtrFbK];
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nk; j += gridDim.x * blockDim.x)
+        a.fbo[j] = a.fbc[j] ? atomicAdd(&a.ctr[kCtrFbM], pow2ceil(a.fbc[j])) : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_fb_scatter(BatchArgs a)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (a.ctr[kCtrFbK] == 0) return;
+    const bool p = i < a.n && a.st[i] == kStPend;
+    const uint32_t j = p ? (uint32_t)*fw_of(a, a.ent[i]) : 0u;
+    const uint32_t t = agg_ticket(a.fbf, j, p);
+    if (p) a.mem[a.fbo[j] + t] = (uint32_t)i;
+}
+
+constexpr int kFbThreads = 1024;
+constexpr int kFbPerThread = 8;
+constexpr int kFbChunk = kFbThreads * kFbPerThread;
+constexpr int kFbLdsSort = 8192;
+
+__device__ __forceinline__ int block_min(int v, int *lds)
+{
+    for (int o = 32; o > 0; o >>= 1) {
+        const int u = __shfl_xor(v, o, 64);
+        v = u < v ? u : v;
+    }
+    if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int r = lds[0];
+#pragma unroll
+    for (int w = 1; w < kFbThreads / 64; ++w) r = lds[w] < r ? lds[w] : r;
+    return r;
+}
+
+// ascending bitonic sort of n (a power of two) words, by the whole workgroup
+__device__ void bitonic_sort(uint32_t *s, uint32_t n)
+{
+    for (uint32_t k = 2; k <= n; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
+                const uint32_t u = t ^ j;
+                if (u > t) {
+                    const uint32_t x = s[t], y = s[u];
+                    if ((x > y) == ((t & k) == 0)) {
+                        s[t] = y;
+                        s[u] = x;
+                    }
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+    }
+}
+
+// One workgroup per fallback key: sort its members by element index, then repeat {block min of
+// the first candidate f against the shared meta; resolve members before f on private copies;
+// barrier; f applies; barrier} over chunks of kFbChunk members until a chunk has no candidate.
+template <int TYPE, int SV>
+__global__ __launch_bounds__(kFbThreads) void k_fb_exec(BatchArgs a)
+{
+    __shared__ uint32_t srt[kFbLdsSort];
+    __shared__ Meta sm;
+    __shared__ int red[kFbThreads / 64];
+    const int tid = threadIdx.x;
+    const uint32_t nk = a.ctr[kCtrFbK];
+    Ctx c = make_ctx(a);
+    for (uint32_t kk = blockIdx.x; kk < nk; kk += gridDim.x) {
+        const uint32_t cnt = a.fbc[kk], p2 = pow2ceil(cnt);
+        if (cnt == 0) continue;  // uniform
+        uint32_t *mem = a.mem + a.fbo[kk];
+        uint8_t *entry = entry_of(a, a.fbk[kk]);
+        const uint32_t *ord = mem;
+        if (p2 <= (uint32_t)kFbLdsSort) {
+            for (uint32_t j = tid; j < p2; j += kFbThreads) srt[j] = j < cnt ? mem[j] : kNone;
+            __syncthreads();
+            bitonic_sort(srt, p2);
+            ord = srt;
+        } else {
+            for (uint32_t j = cnt + tid; j < p2; j += kFbThreads) mem[j] = kNone;
+            __threadfence_block();
+            __syncthreads();
+            bitonic_sort(mem, p2);
+        }
+        if (tid == 0) meta_load(entry, sm);
+        __threadfence_block();
+        __syncthreads();
+        for (uint32_t base = 0; base < cnt; base += kFbChunk) {
+            uint32_t pending = 0;
+#pragma unroll
+            for (int j = 0; j < kFbPerThread; ++j)
+                if (base + j * kFbThreads + tid < cnt) pending |= 1u << j;
+            for (;;) {
+                const Meta m = sm;
+                int mine = kFbChunk;
+#pragma unroll
+                for (int j = kFbPerThread - 1; j >= 0; --j) {
+                    if (!(pending >> j & 1u)) continue;
+                    uint8_t *x;
+                    uint8_t idx;
+                    elem_at(a, ord[base + j * kFbThreads + tid], x, idx, c);
+                    if (would_mutate(TYPE, x, m, c)) mine = j * kFbThreads + tid;
+                }
+                const int f = block_min(mine, red);
+#pragma unroll
+                for (int j = 0; j < kFbPerThread; ++j) {
+                    const int pos = j * kFbThreads + tid;
+                    if (!(pending >> j & 1u) || pos >= f) continue;
+                    uint8_t *x;
+                    uint8_t idx;
+                    elem_at(a, ord[base + pos], x, idx, c);
+                    Meta t = m;
+                    dispatch<SV>(TYPE, x, entry, idx, t, c);
+                    if (a.error_flags && !meta_equal(t, m)) atomicOr(a.error_flags, 1u);
+                    pending &= ~(1u << j);
+                }
+                __syncthreads();  // every read of the entry value precedes the mutation
+                if (f < kFbChunk && (f % kFbThreads) == tid) {
+                    uint8_t *x;
+                    uint8_t idx;
+                    elem_at(a, ord[base + f], x, idx, c);
+                    Meta mm = m;
+                    dispatch<SV>(TYPE, x, entry, idx, mm, c);
+                    pending &= ~(1u << (f / kFbThreads));
+                    sm = mm;
+                }
+                __threadfence_block();
+                __syncthreads();
+                if (f >= kFbChunk) break;
+            }
+        }
+        if (tid == 0) meta_store(entry, sm);
+        __syncthreads();
+    }
+}
+
+__global__ void k_node_suspected(const uint8_t *elems, const int32_t *ns_idx, int32_t *out, int32_t n_batches,
+                                 int32_t stride, int32_t esz)
+{
+    const int32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n_batches) return;
+    const int32_t i = ns_idx[b];
+    if (i >= 0) out[b] = elems[((int64_t)b * stride + i) * esz + kOpValueOff];
+}
+
+// ------------------------------------------------------------------ host side
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+size_t batch_scratch_bytes(int64_t cap)
+{
+    return align256(4 * (size_t)cap) * 5 + align256((size_t)cap) + align256(8 * (size_t)cap) + 256;
+}
+
+void batch_carve(BatchLaunch &bl, uint8_t *base, int64_t cap)
+{
+    uint8_t *p = base;
+    auto take = [&](size_t bytes) {
+        uint8_t *r = p;
+        p += align256(bytes);
+        return r;
+    };
+    bl.ent = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
+    bl.st = take((size_t)cap);
+    bl.mem = reinterpret_cast<uint32_t *>(take(8 * (size_t)cap));
+    bl.fbk = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
+    bl.fbc = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
+    bl.fbo = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
+    bl.fbf = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
+    bl.ctr = reinterpret_cast<uint32_t *>(take(256));
+    bl.cap = (uint32_t)cap;
+}
+
+size_t batch_fw_words(uint64_t log_cap) { return (size_t)(log_cap >> 6); }
+
+uint32_t batch_max_epoch() { return (1u << 29) - 1; }
+
+int launch_batch(const BatchLaunch &bl, hipStream_t s)
+{
+    const int64_t n = bl.n;
+    if (n <= 0) return 0;
+    BatchArgs a;
+    a.elems = bl.elems;
+    a.counts = bl.counts;
+    a.index = bl.index;
+    a.log = bl.log;
+    a.rw = bl.rw;
+    a.ns_idx = bl.ns_idx;
+    a.fw = bl.fw;
+    a.fw_mask = (uint32_t)((bl.g.log_cap >> 6) - 1);
+    a.ent = bl.ent;
+    a.st = bl.st;
+    a.mem = bl.mem;
+    a.fbk = bl.fbk;
+    a.fbc = bl.fbc;
+    a.fbo = bl.fbo;
+    a.fbf = bl.fbf;
+    a.ctr = bl.ctr;
+    a.error_flags = bl.error_flags;
+    a.g = bl.g;
+    a.n = n;
+    a.rw_stride = bl.rw_stride;
+    a.stride = bl.stride;
+    a.esz = bl.esz;
+    a.type = bl.type;
+    a.rtag0 = bl.epoch << 3;
+    a.rounds = rounds_for(bl.type);
+    a.g_membership = bl.g_membership;
+    a.w_ack_init = bl.w_ack_init;
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    const unsigned cgrid = (unsigned)((n + 256 * kCandPer - 1) / (256 * kCandPer));
+    const bool big = bl.esz > 64;
+    const unsigned rgrid = (unsigned)(big ? (n + 127) / 128 : grid);
+    const size_t rlds = (size_t)(big ? 128 : 256) * (size_t)bl.esz;
+    hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n + kLookupPerBlock - 1) / kLookupPerBlock)), dim3(256), 0, s, a);
+#define HKV_ROUNDS(T, V)                                                                          \
+    do {                                                                                          \
+        hipLaunchKernelGGL((k_cand<T>), dim3(cgrid), dim3(256), 0, s, a, 0);                      \
+        if (big) hipLaunchKernelGGL((k_resolve0<T, V, 128>), dim3(rgrid), dim3(128), rlds, s, a); \
+        else hipLaunchKernelGGL((k_resolve0<T, V, 256>), dim3(rgrid), dim3(256), rlds, s, a);     \
+        hipLaunchKernelGGL((k_apply<T, V>), dim3(grid), dim3(256), 0, s, a, 0);                   \
+        for (int r = 1; r <= a.rounds; ++r) {                                                     \
+            hipLaunchKernelGGL((k_cand<T>), dim3(cgrid), dim3(256), 0, s, a, r);                  \
+            hipLaunchKernelGGL((k_resolve<T, V>), dim3(grid), dim3(256), 0, s, a, r);             \
+            hipLaunchKernelGGL((k_apply<T, V>), dim3(grid), dim3(256), 0, s, a, r);               \
+        }                                                                                         \
+        hipLaunchKernelGGL(k_fb_count, dim3(grid), dim3(256), 0, s, a);                           \
+        hipLaunchKernelGGL(k_fb_offsets, dim3(64), dim3(256), 0, s, a);                           \
+        hipLaunchKernelGGL(k_fb_scatter, dim3(grid), dim3(256), 0, s, a);                         \
+        hipLaunchKernelGGL((k_fb_exec<T, V>), dim3(64), dim3(kFbThreads), 0, s, a);               \
+    } while (0)
+#define HKV_ROUNDS_SV(T)                                      \
+    do {                                                      \
+        if (bl.g.st_value == 31) HKV_ROUNDS(T, 31);           \
+        else if (bl.g.st_value == 287) HKV_ROUNDS(T, 287);    \
+        else HKV_ROUNDS(T, 0);                                \
+    } while (0)
+    switch (bl.type) {
+    case kLocal: HKV_ROUNDS_SV(kLocal); break;
+    case kLocalAfterMemb: HKV_ROUNDS_SV(kLocalAfterMemb); break;
+    case kInvs: HKV_ROUNDS_SV(kInvs); break;
+    case kAcks: HKV_ROUNDS_SV(kAcks); break;
+    default: HKV_ROUNDS_SV(kVals); break;
+    }
+#undef HKV_ROUNDS_SV
+#undef HKV_ROUNDS
+    if (hipGetLastError() != hipSuccess) return -3;
+    if (bl.type == kInvs && bl.ns_idx && bl.node_suspected) {
+        hipLaunchKernelGGL(k_node_suspected, dim3((bl.n_batches + 255) / 256), dim3(256), 0, s, bl.elems, bl.ns_idx,
+                           bl.node_suspected, bl.n_batches, bl.stride, bl.esz);
+        if (hipGetLastError() != hipSuccess) return -4;
+    }
+    return 0;
+}
+
+}  // namespace hkv

@@ -18,25 +18,19 @@ struct BatchLaunch {
     int64_t rw_stride;
     int32_t *ns_idx;
     int32_t *node_suspected;
-    uint32_t *keys_a, *keys_b, *vals_a, *vals_b;
-    // long-segment round state (see hkv_kernels.hip, stage 3)
-    uint32_t *seg_start, *seg_end, *seg_count, *seg_fallback, *seg_of;
-    unsigned long long *seg_mut;              // epoch-tagged, all-ones when allocated
-    void *seg_meta;
-    uint8_t *seg_done, *seg_snap;
-    uint64_t *seg_hdr;
-    uint32_t seg_cap;
-    uint32_t epoch;                           // launch counter of the table, >= 1
-    unsigned int *error_flags;                       // checked builds: unsound would_mutate()
-    void *sort_tmp;
-    size_t sort_tmp_bytes;
+    // round state (see hkv_batch.hip): F words per log line (table-wide, all-ones when
+    // allocated) and per-launch scratch carved by batch_carve
+    unsigned long long *fw;
+    uint32_t *ent, *mem, *fbk, *fbc, *fbo, *fbf, *ctr;
+    uint8_t *st;
+    uint32_t cap;                             // elements the scratch was carved for
+    uint32_t epoch;                           // launch counter of the table, 1..batch_max_epoch()
+    unsigned int *error_flags;                // checked builds: unsound would_mutate()
     int64_t n;
     int32_t n_batches;
     int32_t stride;
     int32_t esz;
     int32_t type;
-    uint32_t skip_key;
-    int32_t key_bits;
     uint8_t g_membership;
     uint8_t w_ack_init;
 };
@@ -62,8 +56,11 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s);
 int launch_populate(const PopulateLaunch &pl, hipStream_t s);
 int launch_hash_ids(const uint32_t *ids, uint64_t *out, int64_t n, hipStream_t s);
 size_t sort_temp_bytes(int64_t n, int key_bits);
-// long-segment scratch for launches of up to n elements: size, and carving into bl.seg_*
-size_t seg_scratch_bytes(int64_t n, uint32_t entry_size);
-void seg_carve(BatchLaunch &bl, uint8_t *base, int64_t n, uint32_t entry_size);
+// batch scratch for launches of up to cap elements (size, carving into bl); the table-wide F
+// words (one per 64-B log line, all-ones when allocated and whenever the epoch wraps)
+size_t batch_scratch_bytes(int64_t cap);
+void batch_carve(BatchLaunch &bl, uint8_t *base, int64_t cap);
+size_t batch_fw_words(uint64_t log_cap);
+uint32_t batch_max_epoch();
 
 }  // namespace hkv

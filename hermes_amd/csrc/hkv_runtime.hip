@@ -29,14 +29,12 @@ struct hkv_table {
     int64_t inserted = 0;
     uint32_t skip_key = 0;
     int key_bits = 0;
-    // batch scratch
-    uint32_t *d_keys_a = nullptr, *d_keys_b = nullptr, *d_vals_a = nullptr, *d_vals_b = nullptr;
-    uint8_t *d_seg = nullptr;          // long-segment round state (seg_carve)
-    uint32_t epoch = 0;                // batch launches since d_seg was initialised
+    // batch scratch (batch_carve)
+    uint8_t *d_batch = nullptr;
+    int64_t batch_cap = 0;
+    unsigned long long *d_fw = nullptr;  // F words, one per 64-B log line
+    uint32_t epoch = 0;                // batch launches since d_fw was all-ones
     unsigned int *d_error_flags = nullptr;
-    int64_t scratch_n = 0;
-    void *d_sort_tmp = nullptr;
-    size_t sort_tmp_bytes = 0;
     int32_t *d_ns_idx = nullptr;
     int32_t ns_cap = 0;
     // staging for the host-pointer reference API
@@ -130,38 +128,22 @@ static int bit_width(uint64_t x)
     return b;
 }
 
-static int ensure_scratch(hkv_table *t, int64_t n, int key_bits)
+static int ensure_batch_scratch(hkv_table *t, int64_t n)
 {
-    if (n > t->scratch_n) {
-        int64_t cap = n + n / 4 + 1024;
-        hipFree(t->d_keys_a);
-        hipFree(t->d_keys_b);
-        hipFree(t->d_vals_a);
-        hipFree(t->d_vals_b);
-        hipFree(t->d_seg);
-        t->d_keys_a = t->d_keys_b = t->d_vals_a = t->d_vals_b = nullptr;
-        t->d_seg = nullptr;
-        t->scratch_n = 0;
-        HIP_TRY(hipMalloc(&t->d_keys_a, cap * 4));
-        HIP_TRY(hipMalloc(&t->d_keys_b, cap * 4));
-        HIP_TRY(hipMalloc(&t->d_vals_a, cap * 4));
-        HIP_TRY(hipMalloc(&t->d_vals_b, cap * 4));
-        HIP_TRY(hipMalloc(&t->d_seg, seg_scratch_bytes(cap, t->geo.entry_size)));
-        // all-ones: the epoch-tagged round words then read as "no candidate" for every epoch
-        HIP_TRY(hipMemset(t->d_seg, 0xFF, seg_scratch_bytes(cap, t->geo.entry_size)));
+    if (!t->d_fw) {
+        const size_t bytes = 8 * batch_fw_words(t->cfg.log_cap);
+        HIP_TRY(hipMalloc(&t->d_fw, bytes));
+        // all-ones: every F word reads as stale for every epoch
+        HIP_TRY(hipMemset(t->d_fw, 0xFF, bytes));
         t->epoch = 0;
-        t->scratch_n = cap;
     }
-    size_t need = sort_temp_bytes(t->scratch_n, key_bits > 0 ? key_bits : 32);
-    size_t need32 = sort_temp_bytes(t->scratch_n, 32);
-    if (need32 > need) need = need32;
-    if (need > t->sort_tmp_bytes) {
-        hipFree(t->d_sort_tmp);
-        t->d_sort_tmp = nullptr;
-        t->sort_tmp_bytes = 0;
-        HIP_TRY(hipMalloc(&t->d_sort_tmp, need));
-        t->sort_tmp_bytes = need;
-    }
+    if (n <= t->batch_cap) return 0;
+    const int64_t cap = n + n / 4 + 1024;
+    hipFree(t->d_batch);
+    t->d_batch = nullptr;
+    t->batch_cap = 0;
+    HIP_TRY(hipMalloc(&t->d_batch, batch_scratch_bytes(cap)));
+    t->batch_cap = cap;
     return 0;
 }
 
@@ -238,13 +220,9 @@ int hkv_table_destroy(hkv_table *t)
     hipFree(t->d_index);
     hipFree(t->d_log);
     hipFree(t->d_evictions);
-    hipFree(t->d_keys_a);
-    hipFree(t->d_keys_b);
-    hipFree(t->d_vals_a);
-    hipFree(t->d_vals_b);
-    hipFree(t->d_seg);
+    hipFree(t->d_batch);
+    hipFree(t->d_fw);
     hipFree(t->d_error_flags);
-    hipFree(t->d_sort_tmp);
     hipFree(t->d_ns_idx);
     hipFree(t->d_stage_ops);
     hipFree(t->d_stage_rw);
@@ -272,21 +250,32 @@ int hkv_table_populate(hkv_table *t, int64_t n, int val_len)
     HIP_TRY(hipSetDevice(t->cfg.device));
     int bbits = bit_width(t->cfg.num_bkts - 1);
     if (bbits == 0) bbits = 1;
-    int rc = ensure_scratch(t, n, bbits);
-    if (rc) return rc;
+    // populate temporaries: hashes, sort pairs and sort storage, freed before returning
     uint64_t *d_first = nullptr, *d_second = nullptr;
-    HIP_TRY(hipMalloc(&d_first, n * 8));
-    HIP_TRY(hipMalloc(&d_second, n * 8));
+    uint32_t *d_pairs = nullptr;
+    void *d_tmp = nullptr;
+    const size_t tmp_bytes = sort_temp_bytes(n, bbits);
+    auto release = [&]() {
+        hipFree(d_first);
+        hipFree(d_second);
+        hipFree(d_pairs);
+        hipFree(d_tmp);
+    };
+    if (hipMalloc(&d_first, n * 8) != hipSuccess || hipMalloc(&d_second, n * 8) != hipSuccess ||
+        hipMalloc(&d_pairs, n * 16) != hipSuccess || hipMalloc(&d_tmp, tmp_bytes) != hipSuccess) {
+        release();
+        return fail(-6, "populate: temporary allocation of %lld keys failed", (long long)n);
+    }
     PopulateLaunch pl;
     memset(&pl, 0, sizeof pl);
     pl.first = d_first;
     pl.second = d_second;
-    pl.keys_a = t->d_keys_a;
-    pl.keys_b = t->d_keys_b;
-    pl.vals_a = t->d_vals_a;
-    pl.vals_b = t->d_vals_b;
-    pl.sort_tmp = t->d_sort_tmp;
-    pl.sort_tmp_bytes = t->sort_tmp_bytes;
+    pl.keys_a = d_pairs;
+    pl.keys_b = d_pairs + n;
+    pl.vals_a = d_pairs + 2 * n;
+    pl.vals_b = d_pairs + 3 * n;
+    pl.sort_tmp = d_tmp;
+    pl.sort_tmp_bytes = tmp_bytes;
     pl.index = t->d_index;
     pl.log = t->d_log;
     pl.evictions = t->d_evictions;
@@ -300,10 +289,9 @@ int hkv_table_populate(hkv_table *t, int64_t n, int val_len)
     uint64_t final_head;
     pl.h0 = t->geo.log_head;
     plan_log(t->geo.log_head, t->geo.log_cap, t->geo.entry_size, t->geo.kvs_value, (uint64_t)n, pl.k, pl.hw, final_head);
-    rc = launch_populate(pl, t->stream);
+    int rc = launch_populate(pl, t->stream);
     hipError_t se = hipStreamSynchronize(t->stream);
-    hipFree(d_first);
-    hipFree(d_second);
+    release();
     if (rc) return fail(rc, "populate launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));
     if (se != hipSuccess) return fail(-5, "populate: %s", hipGetErrorString(se));
     t->geo.log_head = final_head;
@@ -324,9 +312,10 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
         return fail(-1, "local batches hold at most 255 ops (uint8 op_buffer_index)");
     int64_t n = (int64_t)d->n_batches * d->stride;
     if (n == 0) return 0;
+    if ((uintptr_t)d->d_elems & 15) return fail(-1, "d_elems must be 16-byte aligned");
     if (n > 0x7FFFFFFFll) return fail(-1, "too many elements in one launch");
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream, as in every HIP API
-    int rc = ensure_scratch(t, n, t->key_bits);
+    int rc = ensure_batch_scratch(t, n);
     if (rc) return rc;
     int32_t *ns_idx = nullptr;
     if (d->type == kInvs && d->d_node_suspected) {
@@ -351,15 +340,10 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.rw_stride = d->rw_stride_bytes;
     bl.ns_idx = ns_idx;
     bl.node_suspected = d->d_node_suspected;
-    bl.keys_a = t->d_keys_a;
-    bl.keys_b = t->d_keys_b;
-    bl.vals_a = t->d_vals_a;
-    bl.vals_b = t->d_vals_b;
-    bl.sort_tmp = t->d_sort_tmp;
-    bl.sort_tmp_bytes = t->sort_tmp_bytes;
-    seg_carve(bl, t->d_seg, t->scratch_n, t->geo.entry_size);
-    if (++t->epoch == 0xFFFFFFFFu) {  // tag ~epoch would reach 0: start the words over
-        HIP_TRY(hipMemsetAsync(t->d_seg, 0xFF, seg_scratch_bytes(t->scratch_n, t->geo.entry_size), s));
+    batch_carve(bl, t->d_batch, t->batch_cap);
+    bl.fw = t->d_fw;
+    if (++t->epoch > batch_max_epoch()) {  // round tags would wrap: start the F words over
+        HIP_TRY(hipMemsetAsync(t->d_fw, 0xFF, 8 * batch_fw_words(t->cfg.log_cap), s));
         t->epoch = 1;
     }
     bl.epoch = t->epoch;
@@ -369,11 +353,9 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.stride = d->stride;
     bl.esz = d->elem_size;
     bl.type = d->type;
-    bl.skip_key = t->skip_key;
-    bl.key_bits = t->key_bits;
     bl.g_membership = d->membership[1];
     bl.w_ack_init = d->membership[2];
-    TRACE("batch_async type=%d n=%lld key_bits=%d", d->type, (long long)n, t->key_bits);
+    TRACE("batch_async type=%d n=%lld", d->type, (long long)n);
     rc = launch_batch(bl, s);
     if (rc) return fail(rc, "batch launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));
     return 0;

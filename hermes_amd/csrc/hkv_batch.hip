@@ -41,7 +41,7 @@ namespace hkv {
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 enum : uint8_t { kStDone = 0, kStApply = 1, kStPend = 2, kStCand0 = 3 };  // per-element stage between passes
-enum { kCtrFbK = 0, kCtrFbM = 1 };                           // fallback keys, fallback member cursor
+enum { kCtrFbK = 0, kCtrFbM = 1, kCtrFbL = 2 };  // fallback keys, member cursor, list length
 
 struct BatchArgs {
     uint8_t *elems;
@@ -54,11 +54,9 @@ struct BatchArgs {
     uint32_t fw_mask;
     uint32_t *ent;               // [n] entry id of every element (kNone: skipped or missing)
     uint8_t *st;                 // [n] stage (kSt*)
-    uint32_t *mem;               // [2 cap] fallback members, per key padded to a power of two
+    uint32_t *mem;               // [2 cap] fallback members of keys with more than kFbLdsSort
     uint32_t *fbk;               // [cap] fallback keys: entry id
-    uint32_t *fbc;               // [cap] member count
-    uint32_t *fbo;               // [cap] member offset
-    uint32_t *fbf;               // [cap] fill cursor
+    uint32_t *fbl;               // [cap] fallback list: elements still pending after the last round
     uint32_t *ctr;               // kCtr*
     unsigned int *error_flags;
     Geometry g;
@@ -73,12 +71,13 @@ struct BatchArgs {
     uint8_t w_ack_init;
 };
 
-// Rounds per batch type: mutations a hot key usually sees in one launch. A local batch has one
-// write per key (later writes stall on its WRITE state), a VAL batch validates once, an ACK batch
-// sets an ack bit and completes, INVs from two peers with two versions mutate up to four times.
+// Rounds after round 0 per batch type: how often a hot key usually mutates in one launch beyond
+// the first time. A local batch writes once (later writes stall on its WRITE state), a VAL batch
+// validates once, an ACK batch sets an ack bit and then completes, INVs carry at most a few
+// distinct timestamps per key and round. Keys that mutate more go to the fallback.
 __host__ __device__ constexpr int rounds_for(int type)
 {
-    return type == kLocal || type == kVals ? 1 : type == kInvs ? 4 : 2;
+    return type == kLocal || type == kVals ? 1 : 2;
 }
 
 __device__ __forceinline__ Ctx make_ctx(const BatchArgs &a)
@@ -159,7 +158,9 @@ __device__ __forceinline__ void resolve_elem(const BatchArgs &a, uint32_t i, uin
 }
 
 // ------------------------------------------------------------------ k_lookup (+ round 0 candidates)
-// A hit that would mutate the meta as it stands (S_0) is marked kStCand0 for k_cand's round 0.
+// A hit that would mutate the meta as it stands (S_0) is marked kStCand0 and stores itself into
+// its key's F word: some candidate's store survives, and k_cand's round 0 only needs an atomic
+// where a smaller candidate exists (a key with one candidate -- most keys -- needs none).
 // Four lanes per element: each lane reads 16 bytes (two slots) of the element's 64-byte bucket,
 // so one load instruction covers a whole bucket line per element. Slots are searched in the
 // reference's order (first tag match wins, hermesKV.c:954-975).
@@ -173,6 +174,7 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a)
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.ctr[kCtrFbK] = 0;
         a.ctr[kCtrFbM] = 0;
+        a.ctr[kCtrFbL] = 0;
     }
     int32_t b = 0, idx = 0;
     uint8_t *x = nullptr;
@@ -227,7 +229,11 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a)
             e = (uint32_t)(phys / a.g.entry_unit);
             uint64_t h2[2] = {0, hdr};
             Ctx c = make_ctx(a);
-            if (would_mutate(a.type, reinterpret_cast<const uint8_t *>(h2), m0, c)) st = kStCand0;
+            if (would_mutate(a.type, reinterpret_cast<const uint8_t *>(h2), m0, c)) {
+                // pre-claim F_0 with a plain store; k_cand's round 0 lowers it to the minimum
+                *fw_of(a, e) = ((unsigned long long)(~a.rtag0) << 32) | (uint32_t)gi;
+                st = kStCand0;
+            }
         } else {
             x[9] = kMiss;
         }
@@ -280,8 +286,16 @@ __global__ __launch_bounds__(256) void k_cand(BatchArgs a, int r)
     }
     __syncthreads();
     const uint32_t rtag = a.rtag0 + (uint32_t)r;
-    for (int j = threadIdx.x; j < kCandSlots; j += 256)
-        if (lk[j] != kNone) offer(a.fw + lk[j], rtag, lv[j]);
+    for (int j = threadIdx.x; j < kCandSlots; j += 256) {
+        if (lk[j] == kNone) continue;
+        unsigned long long *f = a.fw + lk[j];
+        const unsigned long long v = ((unsigned long long)(~rtag) << 32) | lv[j];
+        if (r == 0) {
+            if (v < *f) atomicMin(f, v);  // the pre-claims of k_lookup are visible (kernel boundary)
+        } else {
+            offer(f, rtag, lv[j]);
+        }
+    }
 }
 
 // Round 0's resolve over every element, on LDS copies of the block's contiguous op slab (copied
@@ -331,24 +345,32 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
 }
 
 // Round r >= 1 resolve over the pending elements (sparse: direct global access).
+// After the last round, elements still pending go to the fallback list.
 template <int TYPE, int SV>
 __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
 {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.n || a.st[i] != kStPend) return;
-    const uint32_t e = a.ent[i];
-    const uint32_t f = first_cand(*fw_of(a, e), a.rtag0 + (uint32_t)r);
-    if (f == kNone || (uint32_t)i < f) {
-        resolve_elem<TYPE, SV>(a, (uint32_t)i, entry_of(a, e));
-        a.st[i] = kStDone;
-    } else if ((uint32_t)i == f) {
-        a.st[i] = kStApply;
+    bool left = false;
+    if (i < a.n && a.st[i] == kStPend) {
+        const uint32_t e = a.ent[i];
+        const uint32_t f = first_cand(*fw_of(a, e), a.rtag0 + (uint32_t)r);
+        if (f == kNone || (uint32_t)i < f) {
+            resolve_elem<TYPE, SV>(a, (uint32_t)i, entry_of(a, e));
+            a.st[i] = kStDone;
+        } else if ((uint32_t)i == f) {
+            a.st[i] = kStApply;
+        } else {
+            left = r == a.rounds;
+        }
+    }
+    if (r == a.rounds) {  // wave-aggregated append (uniform branch)
+        const uint32_t t = agg_ticket(&a.ctr[kCtrFbL], 0u, left);
+        if (left) a.fbl[t] = (uint32_t)i;
     }
 }
 
-// Round r's mutation per key. After the last round, a key that may still have pending elements
-// registers for the fallback; its F word then holds the registration (a value every later
-// launch's offers replace).
+// Round r's mutation per key. After the last round, the key registers for the fallback (its
+// later elements, if any, are in the fallback list).
 template <int TYPE, int SV>
 __global__ __launch_bounds__(256) void k_apply(BatchArgs a, int r)
 {
@@ -365,43 +387,11 @@ __global__ __launch_bounds__(256) void k_apply(BatchArgs a, int r)
     dispatch<SV>(TYPE, x, entry, idx, m, c);
     meta_store(entry, m);
     a.st[i] = kStDone;
-    if (r == a.rounds) {
-        const uint32_t j = atomicAdd(&a.ctr[kCtrFbK], 1u);
-        a.fbk[j] = e;
-        a.fbc[j] = 0;
-        a.fbf[j] = 0;
-        *fw_of(a, e) = 0xFFFFFFFF00000000ull | j;
-    }
+    if (r == a.rounds) a.fbk[atomicAdd(&a.ctr[kCtrFbK], 1u)] = e;  // may have members in the fallback list
 }
 
 // ------------------------------------------------------------------ fallback
 __device__ __forceinline__ uint32_t pow2ceil(uint32_t c) { return c <= 1 ? 1u : 1u << (32 - __clz(c - 1)); }
-
-__global__ __launch_bounds__(256) void k_fb_count(BatchArgs a)
-{
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (a.ctr[kCtrFbK] == 0) return;  // uniform: nothing fell back
-    const bool p = i < a.n && a.st[i] == kStPend;
-    const uint32_t j = p ? (uint32_t)*fw_of(a, a.ent[i]) : 0u;
-    agg_ticket(a.fbc, j, p);
-}
-
-__global__ __launch_bounds__(256) void k_fb_offsets(BatchArgs a)
-{
-    const uint32_t nk = a.ctr[kCtrFbK];
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nk; j += gridDim.x * blockDim.x)
-        a.fbo[j] = a.fbc[j] ? atomicAdd(&a.ctr[kCtrFbM], pow2ceil(a.fbc[j])) : 0u;
-}
-
-__global__ __launch_bounds__(256) void k_fb_scatter(BatchArgs a)
-{
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (a.ctr[kCtrFbK] == 0) return;
-    const bool p = i < a.n && a.st[i] == kStPend;
-    const uint32_t j = p ? (uint32_t)*fw_of(a, a.ent[i]) : 0u;
-    const uint32_t t = agg_ticket(a.fbf, j, p);
-    if (p) a.mem[a.fbo[j] + t] = (uint32_t)i;
-}
 
 constexpr int kFbThreads = 1024;
 constexpr int kFbPerThread = 8;
@@ -443,35 +433,50 @@ __device__ void bitonic_sort(uint32_t *s, uint32_t n)
     }
 }
 
-// One workgroup per fallback key: sort its members by element index, then repeat {block min of
-// the first candidate f against the shared meta; resolve members before f on private copies;
-// barrier; f applies; barrier} over chunks of kFbChunk members until a chunk has no candidate.
+// One workgroup per fallback key: gather its members from the fallback list (into LDS, or into
+// a region of mem when there are more than kFbLdsSort), sort them by element index, then repeat
+// {block min of the first candidate f against the shared meta; resolve members before f on
+// private copies; barrier; f applies; barrier} over chunks of kFbChunk members until a chunk has
+// no candidate.
 template <int TYPE, int SV>
 __global__ __launch_bounds__(kFbThreads) void k_fb_exec(BatchArgs a)
 {
     __shared__ uint32_t srt[kFbLdsSort];
     __shared__ Meta sm;
     __shared__ int red[kFbThreads / 64];
+    __shared__ uint32_t lcnt, loff;
     const int tid = threadIdx.x;
-    const uint32_t nk = a.ctr[kCtrFbK];
+    const uint32_t nk = a.ctr[kCtrFbK], nl = a.ctr[kCtrFbL];
     Ctx c = make_ctx(a);
-    for (uint32_t kk = blockIdx.x; kk < nk; kk += gridDim.x) {
-        const uint32_t cnt = a.fbc[kk], p2 = pow2ceil(cnt);
+    for (uint32_t kk = blockIdx.x; kk < nk && nl > 0; kk += gridDim.x) {
+        const uint32_t key = a.fbk[kk];
+        __syncthreads();  // every thread has read the previous key's lcnt
+        if (tid == 0) lcnt = 0;
+        __syncthreads();
+        for (uint32_t j = tid; j < nl; j += kFbThreads)
+            if (a.ent[a.fbl[j]] == key) atomicAdd(&lcnt, 1u);
+        __syncthreads();
+        const uint32_t cnt = lcnt, p2 = pow2ceil(cnt);
         if (cnt == 0) continue;  // uniform
-        uint32_t *mem = a.mem + a.fbo[kk];
-        uint8_t *entry = entry_of(a, a.fbk[kk]);
-        const uint32_t *ord = mem;
-        if (p2 <= (uint32_t)kFbLdsSort) {
-            for (uint32_t j = tid; j < p2; j += kFbThreads) srt[j] = j < cnt ? mem[j] : kNone;
+        const bool in_lds = p2 <= (uint32_t)kFbLdsSort;
+        uint32_t *ord = srt;
+        if (!in_lds) {
+            if (tid == 0) loff = atomicAdd(&a.ctr[kCtrFbM], p2);
             __syncthreads();
-            bitonic_sort(srt, p2);
-            ord = srt;
-        } else {
-            for (uint32_t j = cnt + tid; j < p2; j += kFbThreads) mem[j] = kNone;
-            __threadfence_block();
-            __syncthreads();
-            bitonic_sort(mem, p2);
+            ord = a.mem + loff;
         }
+        __syncthreads();
+        if (tid == 0) lcnt = 0;
+        __syncthreads();
+        for (uint32_t j = tid; j < nl; j += kFbThreads) {
+            const uint32_t i = a.fbl[j];
+            if (a.ent[i] == key) ord[atomicAdd(&lcnt, 1u)] = i;
+        }
+        for (uint32_t j = cnt + tid; j < p2; j += kFbThreads) ord[j] = kNone;
+        __threadfence_block();
+        __syncthreads();
+        bitonic_sort(ord, p2);
+        uint8_t *entry = entry_of(a, key);
         if (tid == 0) meta_load(entry, sm);
         __threadfence_block();
         __syncthreads();
@@ -538,7 +543,7 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t batch_scratch_bytes(int64_t cap)
 {
-    return align256(4 * (size_t)cap) * 5 + align256((size_t)cap) + align256(8 * (size_t)cap) + 256;
+    return align256(4 * (size_t)cap) * 3 + align256((size_t)cap) + align256(8 * (size_t)cap) + 256;
 }
 
 void batch_carve(BatchLaunch &bl, uint8_t *base, int64_t cap)
@@ -553,9 +558,7 @@ void batch_carve(BatchLaunch &bl, uint8_t *base, int64_t cap)
     bl.st = take((size_t)cap);
     bl.mem = reinterpret_cast<uint32_t *>(take(8 * (size_t)cap));
     bl.fbk = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
-    bl.fbc = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
-    bl.fbo = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
-    bl.fbf = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
+    bl.fbl = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
     bl.ctr = reinterpret_cast<uint32_t *>(take(256));
     bl.cap = (uint32_t)cap;
 }
@@ -581,9 +584,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.st = bl.st;
     a.mem = bl.mem;
     a.fbk = bl.fbk;
-    a.fbc = bl.fbc;
-    a.fbo = bl.fbo;
-    a.fbf = bl.fbf;
+    a.fbl = bl.fbl;
     a.ctr = bl.ctr;
     a.error_flags = bl.error_flags;
     a.g = bl.g;
@@ -613,9 +614,6 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
             hipLaunchKernelGGL((k_resolve<T, V>), dim3(grid), dim3(256), 0, s, a, r);             \
             hipLaunchKernelGGL((k_apply<T, V>), dim3(grid), dim3(256), 0, s, a, r);               \
         }                                                                                         \
-        hipLaunchKernelGGL(k_fb_count, dim3(grid), dim3(256), 0, s, a);                           \
-        hipLaunchKernelGGL(k_fb_offsets, dim3(64), dim3(256), 0, s, a);                           \
-        hipLaunchKernelGGL(k_fb_scatter, dim3(grid), dim3(256), 0, s, a);                         \
         hipLaunchKernelGGL((k_fb_exec<T, V>), dim3(64), dim3(kFbThreads), 0, s, a);               \
     } while (0)
 #define HKV_ROUNDS_SV(T)                                      \

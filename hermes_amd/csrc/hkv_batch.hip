@@ -15,12 +15,11 @@
 //                 k_resolve: an element before F_r (or of a key without a candidate) sees S_r in
 //                   the sequential order and S_r does not change under it: it runs the
 //                   reference's exec function on a private copy of S_r against the live entry,
-//                   in parallel with everything else. F_r itself goes to the apply list, later
-//                   elements to the pending list of round r+1.
-//                 k_apply: F_r runs the exec function on the entry, S_r -> S_{r+1}.
-//                 k_cand (r+1): every pending element tests would_mutate against S_{r+1}.
-//               Value reads of a round (GETs, INV-aborts) all happen in k_resolve, before the
-//               round's one mutation per key in k_apply, so they see the value of S_r.
+//                   in parallel with everything else. F_r itself runs the exec function on a
+//                   shadow image of the entry (S_r -> S_{r+1}), so the entry still holds S_r for
+//                   every concurrent reader; later elements stay pending.
+//                 k_cand (r+1): commits the shadows to the entries, and every pending element
+//                   tests would_mutate against S_{r+1}.
 //   fallback    elements still pending after the last round (keys mutated in every round) are
 //               gathered per key, sorted by element index, and finished by one workgroup per
 //               key with first-candidate passes over chunks (k_fb_exec).
@@ -34,13 +33,18 @@
 // value is numerically smaller than every older one, so atomicMin replaces stale words.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "hkv_exec.h"
 #include "hkv_internal.h"
 
 namespace hkv {
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-enum : uint8_t { kStDone = 0, kStApply = 1, kStPend = 2, kStCand0 = 3 };  // per-element stage between passes
+// per-element stage between passes; kStCommit: the element's shadow holds its key's latest state
+// (committed to the entry by k_fb_exec unless a later round's first candidate supersedes it);
+// kStFb: the same for a key with a first candidate in the last round (k_fb_exec finishes it)
+enum : uint8_t { kStDone = 0, kStCommit = 1, kStPend = 2, kStFb = 3 };
 enum { kCtrFbK = 0, kCtrFbM = 1, kCtrFbL = 2 };  // fallback keys, member cursor, list length
 
 struct BatchArgs {
@@ -54,8 +58,11 @@ struct BatchArgs {
     uint32_t fw_mask;
     uint32_t *ent;               // [n] entry id of every element (kNone: skipped or missing)
     uint8_t *st;                 // [n] stage (kSt*)
+    uint32_t *pf;                // [n] pending element: its key's first candidate of the last round
+    uint8_t *shadow;             // [cap][entry_size] entry image a round's first candidate produced
     uint32_t *mem;               // [2 cap] fallback members of keys with more than kFbLdsSort
     uint32_t *fbk;               // [cap] fallback keys: entry id
+    uint32_t *fbi;               // [cap] fallback keys: element whose shadow holds the key's state
     uint32_t *fbl;               // [cap] fallback list: elements still pending after the last round
     uint32_t *ctr;               // kCtr*
     unsigned int *error_flags;
@@ -157,19 +164,59 @@ __device__ __forceinline__ void resolve_elem(const BatchArgs &a, uint32_t i, uin
     if (a.error_flags && !meta_equal(t, m)) atomicOr(a.error_flags, 1u);
 }
 
+__device__ __forceinline__ uint8_t *shadow_of(const BatchArgs &a, uint32_t i)
+{
+    return a.shadow + (size_t)i * a.g.entry_size;
+}
+
+// entries and shadows are 8-byte aligned and a multiple of 8 long
+__device__ __forceinline__ void copy_entry(uint8_t *dst, const uint8_t *src, uint32_t bytes)
+{
+    for (uint32_t w = 0; w < bytes / 8; ++w)
+        reinterpret_cast<uint64_t *>(dst)[w] = reinterpret_cast<const uint64_t *>(src)[w];
+}
+
+// The round's first candidate of a key: S_r (read from src: the entry in round 0, the previous
+// round's shadow later) -> S_{r+1}, written to the element's own shadow image, so the round's
+// other elements, resolved concurrently, still read S_r. Later rounds read the shadow; the key's
+// last shadow is committed to the entry once, by k_fb_exec.
+template <int TYPE, int SV>
+__device__ __forceinline__ void apply_to_shadow(const BatchArgs &a, uint8_t *x, uint32_t i, const uint8_t *src)
+{
+    uint8_t *sh = shadow_of(a, i);
+    Meta m;
+    meta_load(src, m);
+    if (SV == 31) {  // 64-B entries and shadows are 16-byte aligned
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+        uint4 *d4 = reinterpret_cast<uint4 *>(sh);
+        const uint4 w0 = s4[0], w1 = s4[1], w2 = s4[2], w3 = s4[3];
+        d4[0] = w0;
+        d4[1] = w1;
+        d4[2] = w2;
+        d4[3] = w3;
+    } else {
+        copy_entry(sh, src, a.g.entry_size);
+    }
+    Ctx c = make_ctx(a);
+    uint8_t *xg;
+    uint8_t idx;
+    elem_at(a, i, xg, idx, c);
+    dispatch<SV>(TYPE, x ? x : xg, sh, idx, m, c);
+    meta_store(sh, m);
+}
+
 // ------------------------------------------------------------------ k_lookup (+ round 0 candidates)
-// A hit that would mutate the meta as it stands (S_0) is marked kStCand0 and stores itself into
-// its key's F word: some candidate's store survives, and k_cand's round 0 only needs an atomic
-// where a smaller candidate exists (a key with one candidate -- most keys -- needs none).
 // Four lanes per element: each lane reads 16 bytes (two slots) of the element's 64-byte bucket,
 // so one load instruction covers a whole bucket line per element. Slots are searched in the
-// reference's order (first tag match wins, hermesKV.c:954-975).
-constexpr int kLookupPerBlock = 64;
+// reference's order (first tag match wins, hermesKV.c:954-975). A hit that would mutate its key's
+// meta as it stands (S_0) offers itself as round 0's first candidate. The key compare, the meta
+// and the F word load together once the slot is known; the F word filters the offer (a hot key's
+// later candidates see a smaller F and issue no atomic).
 __global__ __launch_bounds__(256) void k_lookup(BatchArgs a)
 {
     const int q = threadIdx.x & 3;
     const int lane = threadIdx.x & 63;
-    const int64_t gi = (int64_t)blockIdx.x * kLookupPerBlock + (threadIdx.x >> 2);
+    const int64_t gi = (int64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
     const bool in = gi < a.n;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         a.ctr[kCtrFbK] = 0;
@@ -215,38 +262,31 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a)
     const uint64_t off = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
     if (!in || q != 0) return;
     uint32_t e = kNone;
-    uint8_t st = kStDone;
     if (probe) {
-        bool hit = false;
-        uint64_t phys = 0;
         if (order && a.g.log_head - off < a.g.log_cap) {
-            phys = off & a.g.log_mask;
-            hit = ld64(a.log + phys + 8) == key;
-        }
-        if (hit) {
+            const uint64_t phys = off & a.g.log_mask;
+            const uint8_t *entry = a.log + phys;
+            unsigned long long *f = a.fw + fw_index(a, phys);
+            const uint64_t ekey = ld64(entry + 8);
             Meta m0;
-            meta_load(a.log + phys, m0);
-            e = (uint32_t)(phys / a.g.entry_unit);
-            uint64_t h2[2] = {0, hdr};
-            Ctx c = make_ctx(a);
-            if (would_mutate(a.type, reinterpret_cast<const uint8_t *>(h2), m0, c)) {
-                // pre-claim F_0 with a plain store; k_cand's round 0 lowers it to the minimum
-                *fw_of(a, e) = ((unsigned long long)(~a.rtag0) << 32) | (uint32_t)gi;
-                st = kStCand0;
+            meta_load(entry, m0);
+            const unsigned long long fv = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (ekey == key) {
+                e = (uint32_t)(phys / a.g.entry_unit);
+                uint64_t h2[2] = {0, hdr};
+                Ctx c = make_ctx(a);
+                const unsigned long long v = ((unsigned long long)(~a.rtag0) << 32) | (uint32_t)gi;
+                if (v < fv && would_mutate(a.type, reinterpret_cast<const uint8_t *>(h2), m0, c)) atomicMin(f, v);
             }
-        } else {
-            x[9] = kMiss;
         }
+        if (e == kNone) x[9] = kMiss;
     }
     a.ent[gi] = e;
-    a.st[gi] = st;
 }
 
 // ------------------------------------------------------------------ rounds (passes over all elements)
-// Candidates of round r, aggregated per key in LDS over kCandPer * 256 elements, so a hot key costs
-// one atomicMin per block instead of one per candidate (atomics execute at the memory side, and
-// one address serialises them). Round 0's candidates were marked by k_lookup; later rounds test
-// pending elements against S_r, the entry as round r-1 left it.
+// Candidates of round r >= 1: pending elements against S_r, which round r-1's first candidate left
+// in its shadow. Aggregated per key in LDS over kCandPer * 256 elements (see k_lookup).
 constexpr int kCandPer = 4;
 constexpr int kCandSlots = 2048;  // >= 2 * kCandPer * 256: the probe always ends
 template <int TYPE>
@@ -263,17 +303,13 @@ __global__ __launch_bounds__(256) void k_cand(BatchArgs a, int r)
     for (int k = 0; k < kCandPer; ++k) {
         const int64_t i = base + k * 256 + threadIdx.x;
         if (i >= a.n) break;
-        const uint8_t st = a.st[i];
-        if (st != (r == 0 ? kStCand0 : kStPend)) continue;
-        const uint32_t e = a.ent[i];
-        if (r > 0) {
-            Meta m;
-            meta_load(entry_of(a, e), m);
-            uint64_t h2[2] = {0, ld64(a.elems + i * a.esz + 8)};
-            Ctx c = make_ctx(a);
-            if (!would_mutate(TYPE, reinterpret_cast<const uint8_t *>(h2), m, c)) continue;
-        }
-        const uint32_t fi = fw_index(a, phys_of(a, e));
+        if (a.st[i] != kStPend) continue;
+        Meta m;
+        meta_load(shadow_of(a, a.pf[i]), m);
+        uint64_t h2[2] = {0, ld64(a.elems + i * a.esz + 8)};
+        Ctx c = make_ctx(a);
+        if (!would_mutate(TYPE, reinterpret_cast<const uint8_t *>(h2), m, c)) continue;
+        const uint32_t fi = fw_index(a, phys_of(a, a.ent[i]));
         uint32_t h = (fi * 0x9E3779B1u) >> 21;
         for (;;) {
             const uint32_t old = atomicCAS(&lk[h], kNone, fi);
@@ -286,21 +322,13 @@ __global__ __launch_bounds__(256) void k_cand(BatchArgs a, int r)
     }
     __syncthreads();
     const uint32_t rtag = a.rtag0 + (uint32_t)r;
-    for (int j = threadIdx.x; j < kCandSlots; j += 256) {
-        if (lk[j] == kNone) continue;
-        unsigned long long *f = a.fw + lk[j];
-        const unsigned long long v = ((unsigned long long)(~rtag) << 32) | lv[j];
-        if (r == 0) {
-            if (v < *f) atomicMin(f, v);  // the pre-claims of k_lookup are visible (kernel boundary)
-        } else {
-            offer(f, rtag, lv[j]);
-        }
-    }
+    for (int j = threadIdx.x; j < kCandSlots; j += 256)
+        if (lk[j] != kNone) offer(a.fw + lk[j], rtag, lv[j]);
 }
 
 // Round 0's resolve over every element, on LDS copies of the block's contiguous op slab (copied
 // in and out with 16-B accesses, so the byte-wise result writes never reach memory one by one).
-// Before F_0 (or no candidate) -> resolved now; == F_0 -> apply; after -> pending.
+// Before F_0 (or no candidate) -> resolved now; F_0 -> applied to its shadow; after -> pending.
 template <int TYPE, int SV, int BP>
 __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
 {
@@ -331,8 +359,13 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
                 Meta tm = m;
                 dispatch<SV>(TYPE, reinterpret_cast<uint8_t *>(sops) + (uint32_t)t * a.esz, entry, idx, tm, c);
                 if (a.error_flags && !meta_equal(tm, m)) atomicOr(a.error_flags, 1u);
+            } else if ((uint32_t)i == f) {
+                apply_to_shadow<TYPE, SV>(a, reinterpret_cast<uint8_t *>(sops) + (uint32_t)t * a.esz, (uint32_t)i,
+                                          entry_of(a, e));
+                st = kStCommit;
             } else {
-                st = (uint32_t)i == f ? kStApply : kStPend;
+                a.pf[i] = f;
+                st = kStPend;
             }
         }
         a.st[i] = st;
@@ -344,7 +377,8 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
         reinterpret_cast<uint64_t *>(dst)[bytes / 8 - 1] = reinterpret_cast<const uint64_t *>(sops)[bytes / 8 - 1];
 }
 
-// Round r >= 1 resolve over the pending elements (sparse: direct global access).
+// Round r >= 1 resolve over the pending elements (sparse: direct global access), against S_r in
+// the shadow of round r-1's first candidate of the element's key.
 // After the last round, elements still pending go to the fallback list.
 template <int TYPE, int SV>
 __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
@@ -354,12 +388,23 @@ __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
     if (i < a.n && a.st[i] == kStPend) {
         const uint32_t e = a.ent[i];
         const uint32_t f = first_cand(*fw_of(a, e), a.rtag0 + (uint32_t)r);
+        const uint32_t prev = a.pf[i];  // S_r lives in the shadow of round r-1's first candidate
         if (f == kNone || (uint32_t)i < f) {
-            resolve_elem<TYPE, SV>(a, (uint32_t)i, entry_of(a, e));
+            resolve_elem<TYPE, SV>(a, (uint32_t)i, shadow_of(a, prev));
             a.st[i] = kStDone;
         } else if ((uint32_t)i == f) {
-            a.st[i] = kStApply;
+            apply_to_shadow<TYPE, SV>(a, nullptr, (uint32_t)i, shadow_of(a, prev));
+            a.st[prev] = kStDone;  // superseded
+            if (r == a.rounds) {   // k_fb_exec commits it and finishes the key's later elements, if any
+                const uint32_t j = atomicAdd(&a.ctr[kCtrFbK], 1u);
+                a.fbk[j] = e;
+                a.fbi[j] = (uint32_t)i;
+                a.st[i] = kStFb;
+            } else {
+                a.st[i] = kStCommit;
+            }
         } else {
+            a.pf[i] = f;
             left = r == a.rounds;
         }
     }
@@ -367,27 +412,6 @@ __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
         const uint32_t t = agg_ticket(&a.ctr[kCtrFbL], 0u, left);
         if (left) a.fbl[t] = (uint32_t)i;
     }
-}
-
-// Round r's mutation per key. After the last round, the key registers for the fallback (its
-// later elements, if any, are in the fallback list).
-template <int TYPE, int SV>
-__global__ __launch_bounds__(256) void k_apply(BatchArgs a, int r)
-{
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.n || a.st[i] != kStApply) return;
-    const uint32_t e = a.ent[i];
-    uint8_t *entry = entry_of(a, e);
-    Ctx c = make_ctx(a);
-    uint8_t *x;
-    uint8_t idx;
-    elem_at(a, (uint32_t)i, x, idx, c);
-    Meta m;
-    meta_load(entry, m);
-    dispatch<SV>(TYPE, x, entry, idx, m, c);
-    meta_store(entry, m);
-    a.st[i] = kStDone;
-    if (r == a.rounds) a.fbk[atomicAdd(&a.ctr[kCtrFbK], 1u)] = e;  // may have members in the fallback list
 }
 
 // ------------------------------------------------------------------ fallback
@@ -433,7 +457,8 @@ __device__ void bitonic_sort(uint32_t *s, uint32_t n)
     }
 }
 
-// One workgroup per fallback key: gather its members from the fallback list (into LDS, or into
+// Final pass of a launch. Every key's last shadow is committed to its entry. Then one workgroup
+// per key with a first candidate in the last round: commit its shadow, gather its members from the fallback list (into LDS, or into
 // a region of mem when there are more than kFbLdsSort), sort them by element index, then repeat
 // {block min of the first candidate f against the shared meta; resolve members before f on
 // private copies; barrier; f applies; barrier} over chunks of kFbChunk members until a chunk has
@@ -448,10 +473,32 @@ __global__ __launch_bounds__(kFbThreads) void k_fb_exec(BatchArgs a)
     const int tid = threadIdx.x;
     const uint32_t nk = a.ctr[kCtrFbK], nl = a.ctr[kCtrFbL];
     Ctx c = make_ctx(a);
-    for (uint32_t kk = blockIdx.x; kk < nk && nl > 0; kk += gridDim.x) {
+    // every key's last shadow becomes its entry (keys of the last round: below, per key)
+    for (int64_t i = (int64_t)blockIdx.x * kFbThreads + tid; i < a.n; i += (int64_t)gridDim.x * kFbThreads) {
+        if (a.st[i] != kStCommit) continue;
+        uint8_t *dst = entry_of(a, a.ent[i]);
+        const uint8_t *src = shadow_of(a, (uint32_t)i);
+        if (SV == 31) {
+            const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+            uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+            const uint4 w0 = s4[0], w1 = s4[1], w2 = s4[2], w3 = s4[3];
+            d4[0] = w0;
+            d4[1] = w1;
+            d4[2] = w2;
+            d4[3] = w3;
+        } else {
+            copy_entry(dst, src, a.g.entry_size);
+        }
+    }
+    for (uint32_t kk = blockIdx.x; kk < nk; kk += gridDim.x) {
         const uint32_t key = a.fbk[kk];
         __syncthreads();  // every thread has read the previous key's lcnt
+        uint8_t *entry = entry_of(a, key);
+        // the last round's shadow becomes the entry
+        for (uint32_t w = tid; w < a.g.entry_size / 8; w += kFbThreads)
+            reinterpret_cast<uint64_t *>(entry)[w] = reinterpret_cast<const uint64_t *>(shadow_of(a, a.fbi[kk]))[w];
         if (tid == 0) lcnt = 0;
+        __threadfence_block();
         __syncthreads();
         for (uint32_t j = tid; j < nl; j += kFbThreads)
             if (a.ent[a.fbl[j]] == key) atomicAdd(&lcnt, 1u);
@@ -476,7 +523,6 @@ __global__ __launch_bounds__(kFbThreads) void k_fb_exec(BatchArgs a)
         __threadfence_block();
         __syncthreads();
         bitonic_sort(ord, p2);
-        uint8_t *entry = entry_of(a, key);
         if (tid == 0) meta_load(entry, sm);
         __threadfence_block();
         __syncthreads();
@@ -541,12 +587,13 @@ __global__ void k_node_suspected(const uint8_t *elems, const int32_t *ns_idx, in
 // ------------------------------------------------------------------ host side
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-size_t batch_scratch_bytes(int64_t cap)
+size_t batch_scratch_bytes(int64_t cap, uint32_t entry_size)
 {
-    return align256(4 * (size_t)cap) * 3 + align256((size_t)cap) + align256(8 * (size_t)cap) + 256;
+    return align256(4 * (size_t)cap) * 5 + align256((size_t)cap) + align256(8 * (size_t)cap) + 256 +
+           align256((size_t)entry_size * (size_t)cap);
 }
 
-void batch_carve(BatchLaunch &bl, uint8_t *base, int64_t cap)
+void batch_carve(BatchLaunch &bl, uint8_t *base, int64_t cap, uint32_t entry_size)
 {
     uint8_t *p = base;
     auto take = [&](size_t bytes) {
@@ -559,6 +606,9 @@ void batch_carve(BatchLaunch &bl, uint8_t *base, int64_t cap)
     bl.mem = reinterpret_cast<uint32_t *>(take(8 * (size_t)cap));
     bl.fbk = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
     bl.fbl = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
+    bl.fbi = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
+    bl.pf = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
+    bl.shadow = take((size_t)entry_size * (size_t)cap);
     bl.ctr = reinterpret_cast<uint32_t *>(take(256));
     bl.cap = (uint32_t)cap;
 }
@@ -585,6 +635,9 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.mem = bl.mem;
     a.fbk = bl.fbk;
     a.fbl = bl.fbl;
+    a.fbi = bl.fbi;
+    a.pf = bl.pf;
+    a.shadow = bl.shadow;
     a.ctr = bl.ctr;
     a.error_flags = bl.error_flags;
     a.g = bl.g;
@@ -602,19 +655,17 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     const bool big = bl.esz > 64;
     const unsigned rgrid = (unsigned)(big ? (n + 127) / 128 : grid);
     const size_t rlds = (size_t)(big ? 128 : 256) * (size_t)bl.esz;
-    hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n + kLookupPerBlock - 1) / kLookupPerBlock)), dim3(256), 0, s, a);
+    const unsigned fgrid = (unsigned)std::min<int64_t>(512, (n + 4 * kFbThreads - 1) / (4 * kFbThreads));
+    hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, a);
 #define HKV_ROUNDS(T, V)                                                                          \
     do {                                                                                          \
-        hipLaunchKernelGGL((k_cand<T>), dim3(cgrid), dim3(256), 0, s, a, 0);                      \
         if (big) hipLaunchKernelGGL((k_resolve0<T, V, 128>), dim3(rgrid), dim3(128), rlds, s, a); \
         else hipLaunchKernelGGL((k_resolve0<T, V, 256>), dim3(rgrid), dim3(256), rlds, s, a);     \
-        hipLaunchKernelGGL((k_apply<T, V>), dim3(grid), dim3(256), 0, s, a, 0);                   \
         for (int r = 1; r <= a.rounds; ++r) {                                                     \
             hipLaunchKernelGGL((k_cand<T>), dim3(cgrid), dim3(256), 0, s, a, r);                  \
             hipLaunchKernelGGL((k_resolve<T, V>), dim3(grid), dim3(256), 0, s, a, r);             \
-            hipLaunchKernelGGL((k_apply<T, V>), dim3(grid), dim3(256), 0, s, a, r);               \
         }                                                                                         \
-        hipLaunchKernelGGL((k_fb_exec<T, V>), dim3(64), dim3(kFbThreads), 0, s, a);               \
+        hipLaunchKernelGGL((k_fb_exec<T, V>), dim3(fgrid), dim3(kFbThreads), 0, s, a);            \
     } while (0)
 #define HKV_ROUNDS_SV(T)                                      \
     do {                                                      \

@@ -21,8 +21,8 @@ struct BatchLaunch {
     // round state (see hkv_batch.hip): F words per log line (table-wide, all-ones when
     // allocated) and per-launch scratch carved by batch_carve
     unsigned long long *fw;
-    uint32_t *ent, *mem, *fbk, *fbl, *ctr;
-    uint8_t *st;
+    uint32_t *ent, *mem, *fbk, *fbl, *fbi, *pf, *ctr;
+    uint8_t *st, *shadow;
     uint32_t cap;                             // elements the scratch was carved for
     uint32_t epoch;                           // launch counter of the table, 1..batch_max_epoch()
     unsigned int *error_flags;                // checked builds: unsound would_mutate()
@@ -58,8 +58,8 @@ int launch_hash_ids(const uint32_t *ids, uint64_t *out, int64_t n, hipStream_t s
 size_t sort_temp_bytes(int64_t n, int key_bits);
 // batch scratch for launches of up to cap elements (size, carving into bl); the table-wide F
 // words (one per 64-B log line, all-ones when allocated and whenever the epoch wraps)
-size_t batch_scratch_bytes(int64_t cap);
-void batch_carve(BatchLaunch &bl, uint8_t *base, int64_t cap);
+size_t batch_scratch_bytes(int64_t cap, uint32_t entry_size);
+void batch_carve(BatchLaunch &bl, uint8_t *base, int64_t cap, uint32_t entry_size);
 size_t batch_fw_words(uint64_t log_cap);
 uint32_t batch_max_epoch();
 

@@ -133,8 +133,10 @@ static int ensure_batch_scratch(hkv_table *t, int64_t n)
     if (!t->d_fw) {
         const size_t bytes = 8 * batch_fw_words(t->cfg.log_cap);
         HIP_TRY(hipMalloc(&t->d_fw, bytes));
-        // all-ones: every F word reads as stale for every epoch
+        // all-ones: every F word reads as stale for every epoch. hipMemset runs on the null
+        // stream, which does not order the table's non-blocking streams: wait for it here.
         HIP_TRY(hipMemset(t->d_fw, 0xFF, bytes));
+        HIP_TRY(hipDeviceSynchronize());
         t->epoch = 0;
     }
     if (n <= t->batch_cap) return 0;
@@ -142,7 +144,7 @@ static int ensure_batch_scratch(hkv_table *t, int64_t n)
     hipFree(t->d_batch);
     t->d_batch = nullptr;
     t->batch_cap = 0;
-    HIP_TRY(hipMalloc(&t->d_batch, batch_scratch_bytes(cap)));
+    HIP_TRY(hipMalloc(&t->d_batch, batch_scratch_bytes(cap, t->geo.entry_size)));
     t->batch_cap = cap;
     return 0;
 }
@@ -340,7 +342,7 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.rw_stride = d->rw_stride_bytes;
     bl.ns_idx = ns_idx;
     bl.node_suspected = d->d_node_suspected;
-    batch_carve(bl, t->d_batch, t->batch_cap);
+    batch_carve(bl, t->d_batch, t->batch_cap, t->geo.entry_size);
     bl.fw = t->d_fw;
     if (++t->epoch > batch_max_epoch()) {  // round tags would wrap: start the F words over
         HIP_TRY(hipMemsetAsync(t->d_fw, 0xFF, 8 * batch_fw_words(t->cfg.log_cap), s));
@@ -405,6 +407,7 @@ int hkv_take_error_flags(hkv_table *t, uint32_t *out)
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(out, t->d_error_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemset(t->d_error_flags, 0, sizeof(uint32_t)));
+    HIP_TRY(hipDeviceSynchronize());  // null-stream memset vs the non-blocking launch streams
     return 0;
 }
 void *hkv_device_log(hkv_table *t) { return t ? t->d_log : nullptr; }

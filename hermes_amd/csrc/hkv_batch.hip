@@ -34,6 +34,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "hkv_exec.h"
 #include "hkv_internal.h"
@@ -211,14 +213,18 @@ __device__ __forceinline__ void apply_to_shadow(const BatchArgs &a, uint8_t *x, 
 // reference's order (first tag match wins, hermesKV.c:954-975). A hit that would mutate its key's
 // meta as it stands (S_0) offers itself as round 0's first candidate. The key compare, the meta
 // and the F word load together once the slot is known; the F word filters the offer (a hot key's
-// later candidates see a smaller F and issue no atomic).
-__global__ __launch_bounds__(256) void k_lookup(BatchArgs a)
+// later candidates see a smaller F and issue no atomic). The launch is split: a short head over
+// the first kLookupHead elements gives every hot key a small F first, because at the start of
+// one big launch some 10^5 elements are in flight before any F is set, and a hot key's
+// candidates among them would all reach its F word (atomics on one address serialise).
+constexpr int64_t kLookupHead = 8192;
+__global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, int64_t i_end)
 {
     const int q = threadIdx.x & 3;
     const int lane = threadIdx.x & 63;
-    const int64_t gi = (int64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
-    const bool in = gi < a.n;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t gi = i_begin + (int64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+    const bool in = gi < i_end;
+    if (i_begin == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
         a.ctr[kCtrFbK] = 0;
         a.ctr[kCtrFbM] = 0;
         a.ctr[kCtrFbL] = 0;
@@ -656,7 +662,10 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     const unsigned rgrid = (unsigned)(big ? (n + 127) / 128 : grid);
     const size_t rlds = (size_t)(big ? 128 : 256) * (size_t)bl.esz;
     const unsigned fgrid = (unsigned)std::min<int64_t>(512, (n + 4 * kFbThreads - 1) / (4 * kFbThreads));
-    hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, a);
+    const int64_t head = n < kLookupHead ? n : kLookupHead;
+    hipLaunchKernelGGL(k_lookup, dim3((unsigned)((head + 63) / 64)), dim3(256), 0, s, a, (int64_t)0, head);
+    if (n > head)
+        hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n - head + 63) / 64)), dim3(256), 0, s, a, head, n);
 #define HKV_ROUNDS(T, V)                                                                          \
     do {                                                                                          \
         if (big) hipLaunchKernelGGL((k_resolve0<T, V, 128>), dim3(rgrid), dim3(128), rlds, s, a); \
@@ -683,6 +692,14 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
 #undef HKV_ROUNDS_SV
 #undef HKV_ROUNDS
     if (hipGetLastError() != hipSuccess) return -3;
+    static const bool stats = getenv("HKV_STATS") != nullptr;
+    if (stats) {  // debug: what reached the fallback (synchronises the stream)
+        uint32_t c[4] = {0, 0, 0, 0};
+        hipMemcpyAsync(c, bl.ctr, sizeof c, hipMemcpyDeviceToHost, s);
+        hipStreamSynchronize(s);
+        fprintf(stderr, "[hkv] batch type %d n %lld: last-round keys %u, fallback members %u\n", bl.type,
+                (long long)n, c[kCtrFbK], c[kCtrFbL]);
+    }
     if (bl.type == kInvs && bl.ns_idx && bl.node_suspected) {
         hipLaunchKernelGGL(k_node_suspected, dim3((bl.n_batches + 255) / 256), dim3(256), 0, s, bl.elems, bl.ns_idx,
                            bl.node_suspected, bl.n_batches, bl.stride, bl.esz);

@@ -75,18 +75,33 @@ struct BatchArgs {
     int32_t esz;
     int32_t type;
     uint32_t rtag0;              // round 0's tag; round r uses rtag0 + r
+    uint8_t ltag;                // launch tag (1..255) in the seqlock byte of keys with a round-0 candidate
     int32_t rounds;              // rounds after round 0 before the fallback
     uint8_t g_membership;
     uint8_t w_ack_init;
 };
 
 // Rounds after round 0 per batch type: how often a hot key usually mutates in one launch beyond
-// the first time. A local batch writes once (later writes stall on its WRITE state), a VAL batch
-// validates once, an ACK batch sets an ack bit and then completes, INVs carry at most a few
-// distinct timestamps per key and round. Keys that mutate more go to the fallback.
-__host__ __device__ constexpr int rounds_for(int type)
+// the first time. An ACK batch sets an ack bit and then completes; INVs carry at most a few
+// distinct timestamps per key and launch. Keys that mutate more go to the fallback.
+// None for VAL batches and for local batches without RMWs: their first mutation leaves the key in
+// an absorbing state (absorbing_state), so k_resolve0 finishes every key.
+__host__ __device__ constexpr int rounds_for(int type, bool rmw)
 {
-    return type == kLocal || type == kVals ? 1 : 2;
+    return type == kVals || (type == kLocal && !rmw) ? 0 : 2;
+}
+
+// The state a key is in after any mutation by an element of this batch type, when that state
+// makes every later element of the launch a non-mutating one whose result depends on the state
+// alone (rounds_for == 0):
+//   local, RMWs off: a mutation is a PUT (update_actions -> WRITE, hermesKV.c:100-141) or a GET
+//     replay (-> REPLAY, :155-175); under either, GETs stall (:279-282) and PUTs stall (:352-354).
+//   VALs: hermes_exec_val only ever sets VALID (:676-703) and its opcode is VAL_SUCCESS whatever
+//     the state; under VALID no VAL mutates.
+template <int TYPE>
+__device__ __forceinline__ uint8_t absorbing_state()
+{
+    return TYPE == kVals ? kValid : kWrite;
 }
 
 __device__ __forceinline__ Ctx make_ctx(const BatchArgs &a)
@@ -282,7 +297,13 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                 uint64_t h2[2] = {0, hdr};
                 Ctx c = make_ctx(a);
                 const unsigned long long v = ((unsigned long long)(~a.rtag0) << 32) | (uint32_t)gi;
-                if (v < fv && would_mutate(a.type, reinterpret_cast<const uint8_t *>(h2), m0, c)) atomicMin(f, v);
+                if (would_mutate(a.type, reinterpret_cast<const uint8_t *>(h2), m0, c)) {
+                    if (v < fv) atomicMin(f, v);
+                    // the seqlock byte is free at batch boundaries (concur_ctrl.h: the lock is
+                    // held only inside one exec call): it tells k_resolve0 which keys have a
+                    // candidate, so the others skip the F word; the key's commit clears it
+                    if ((uint8_t)(m0.w5 >> 16) != a.ltag) const_cast<uint8_t *>(entry)[kEntryMetaOff + 4] = a.ltag;
+                }
             }
         }
         if (e == kNone) x[9] = kMiss;
@@ -341,6 +362,10 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
     extern __shared__ uint4 sops[];
     const int64_t i0 = (int64_t)blockIdx.x * BP;
     const int cnt = a.n - i0 < BP ? (int)(a.n - i0) : BP;
+    // the element's entry id and meta load while the block copies its op slab in
+    const uint32_t e = (int)threadIdx.x < cnt ? a.ent[i0 + threadIdx.x] : kNone;
+    Meta m{};
+    if (e != kNone) meta_load(entry_of(a, e), m);
     const uint32_t bytes = (uint32_t)cnt * (uint32_t)a.esz;  // a multiple of 8
     const uint4 *src = reinterpret_cast<const uint4 *>(a.elems + i0 * a.esz);
     for (uint32_t w = threadIdx.x; w < bytes / 16; w += BP) sops[w] = src[w];
@@ -350,18 +375,16 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
     const int t = threadIdx.x;
     if (t < cnt) {
         const int64_t i = i0 + t;
-        const uint32_t e = a.ent[i];
         uint8_t st = kStDone;
         if (e != kNone) {
-            const uint32_t f = first_cand(*fw_of(a, e), a.rtag0);
+            // only keys flagged by k_lookup can have a first candidate
+            const uint32_t f = (uint8_t)(m.w5 >> 16) == a.ltag ? first_cand(*fw_of(a, e), a.rtag0) : kNone;
             if (f == kNone || (uint32_t)i < f) {
                 Ctx c = make_ctx(a);
                 uint8_t *xg;
                 uint8_t idx;
                 elem_at(a, (uint32_t)i, xg, idx, c);
                 uint8_t *entry = entry_of(a, e);
-                Meta m;
-                meta_load(entry, m);
                 Meta tm = m;
                 dispatch<SV>(TYPE, reinterpret_cast<uint8_t *>(sops) + (uint32_t)t * a.esz, entry, idx, tm, c);
                 if (a.error_flags && !meta_equal(tm, m)) atomicOr(a.error_flags, 1u);
@@ -369,6 +392,16 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
                 apply_to_shadow<TYPE, SV>(a, reinterpret_cast<uint8_t *>(sops) + (uint32_t)t * a.esz, (uint32_t)i,
                                           entry_of(a, e));
                 st = kStCommit;
+            } else if (a.rounds == 0) {  // after the key's only mutation: absorbing state
+                Ctx c = make_ctx(a);
+                uint8_t *xg;
+                uint8_t idx;
+                elem_at(a, (uint32_t)i, xg, idx, c);
+                Meta m1 = m;
+                m_set_state(m1, absorbing_state<TYPE>());
+                Meta tm = m1;
+                dispatch<SV>(TYPE, reinterpret_cast<uint8_t *>(sops) + (uint32_t)t * a.esz, entry_of(a, e), idx, tm, c);
+                if (a.error_flags && !meta_equal(tm, m1)) atomicOr(a.error_flags, 1u);
             } else {
                 a.pf[i] = f;
                 st = kStPend;
@@ -653,7 +686,8 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.esz = bl.esz;
     a.type = bl.type;
     a.rtag0 = bl.epoch << 3;
-    a.rounds = rounds_for(bl.type);
+    a.ltag = (uint8_t)(bl.epoch % 255u + 1u);
+    a.rounds = rounds_for(bl.type, bl.g.rmw_enabled != 0);
     a.g_membership = bl.g_membership;
     a.w_ack_init = bl.w_ack_init;
     const unsigned grid = (unsigned)((n + 255) / 256);

@@ -44,10 +44,9 @@ namespace hkv {
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 // per-element stage between passes; kStCommit: the element's shadow holds its key's latest state
-// (committed to the entry by k_fb_exec unless a later round's first candidate supersedes it);
-// kStFb: the same for a key with a first candidate in the last round (k_fb_exec finishes it)
-enum : uint8_t { kStDone = 0, kStCommit = 1, kStPend = 2, kStFb = 3 };
-enum { kCtrFbK = 0, kCtrFbM = 1, kCtrFbL = 2 };  // fallback keys, member cursor, list length
+// (committed to the entry by k_commit unless a later round's first candidate supersedes it)
+enum : uint8_t { kStDone = 0, kStCommit = 1, kStPend = 2 };
+enum { kCtrFbM = 1, kCtrFbL = 2 };  // fallback: mem cursor, list length
 
 struct BatchArgs {
     uint8_t *elems;
@@ -62,9 +61,7 @@ struct BatchArgs {
     uint8_t *st;                 // [n] stage (kSt*)
     uint32_t *pf;                // [n] pending element: its key's first candidate of the last round
     uint8_t *shadow;             // [cap][entry_size] entry image a round's first candidate produced
-    uint32_t *mem;               // [2 cap] fallback members of keys with more than kFbLdsSort
-    uint32_t *fbk;               // [cap] fallback keys: entry id
-    uint32_t *fbi;               // [cap] fallback keys: element whose shadow holds the key's state
+    unsigned long long *mem;     // [2 cap] fallback (F_R, element) pairs of workgroups with more than kFbLds
     uint32_t *fbl;               // [cap] fallback list: elements still pending after the last round
     uint32_t *ctr;               // kCtr*
     unsigned int *error_flags;
@@ -240,7 +237,6 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
     const int64_t gi = i_begin + (int64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
     const bool in = gi < i_end;
     if (i_begin == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
-        a.ctr[kCtrFbK] = 0;
         a.ctr[kCtrFbM] = 0;
         a.ctr[kCtrFbL] = 0;
     }
@@ -434,16 +430,9 @@ __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
         } else if ((uint32_t)i == f) {
             apply_to_shadow<TYPE, SV>(a, nullptr, (uint32_t)i, shadow_of(a, prev));
             a.st[prev] = kStDone;  // superseded
-            if (r == a.rounds) {   // k_fb_exec commits it and finishes the key's later elements, if any
-                const uint32_t j = atomicAdd(&a.ctr[kCtrFbK], 1u);
-                a.fbk[j] = e;
-                a.fbi[j] = (uint32_t)i;
-                a.st[i] = kStFb;
-            } else {
-                a.st[i] = kStCommit;
-            }
+            a.st[i] = kStCommit;
         } else {
-            a.pf[i] = f;
+            a.pf[i] = f;  // after the last round: identifies the key's run in k_fb_exec
             left = r == a.rounds;
         }
     }
@@ -456,10 +445,32 @@ __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
 // ------------------------------------------------------------------ fallback
 __device__ __forceinline__ uint32_t pow2ceil(uint32_t c) { return c <= 1 ? 1u : 1u << (32 - __clz(c - 1)); }
 
+// Final commit of a launch: every key's last shadow becomes its entry.
+template <int SV>
+__global__ __launch_bounds__(256) void k_commit(BatchArgs a)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n || a.st[i] != kStCommit) return;
+    uint8_t *dst = entry_of(a, a.ent[i]);
+    const uint8_t *src = shadow_of(a, (uint32_t)i);
+    if (SV == 31) {  // 64-B entries and shadows are 16-byte aligned
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
+        uint4 *d4 = reinterpret_cast<uint4 *>(dst);
+        const uint4 w0 = s4[0], w1 = s4[1], w2 = s4[2], w3 = s4[3];
+        d4[0] = w0;
+        d4[1] = w1;
+        d4[2] = w2;
+        d4[3] = w3;
+    } else {
+        copy_entry(dst, src, a.g.entry_size);
+    }
+}
+
 constexpr int kFbThreads = 1024;
 constexpr int kFbPerThread = 8;
 constexpr int kFbChunk = kFbThreads * kFbPerThread;
-constexpr int kFbLdsSort = 8192;
+constexpr int kFbLds = 8192;    // (F_R, element) pairs sorted in LDS
+constexpr int kFbSerial = 32;   // runs up to this long are applied by one thread
 
 __device__ __forceinline__ int block_min(int v, int *lds)
 {
@@ -476,14 +487,14 @@ __device__ __forceinline__ int block_min(int v, int *lds)
 }
 
 // ascending bitonic sort of n (a power of two) words, by the whole workgroup
-__device__ void bitonic_sort(uint32_t *s, uint32_t n)
+__device__ void bitonic_sort(unsigned long long *s, uint32_t n)
 {
     for (uint32_t k = 2; k <= n; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
             for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
                 const uint32_t u = t ^ j;
                 if (u > t) {
-                    const uint32_t x = s[t], y = s[u];
+                    const unsigned long long x = s[t], y = s[u];
                     if ((x > y) == ((t & k) == 0)) {
                         s[t] = y;
                         s[u] = x;
@@ -496,80 +507,90 @@ __device__ void bitonic_sort(uint32_t *s, uint32_t n)
     }
 }
 
-// Final pass of a launch. Every key's last shadow is committed to its entry. Then one workgroup
-// per key with a first candidate in the last round: commit its shadow, gather its members from the fallback list (into LDS, or into
-// a region of mem when there are more than kFbLdsSort), sort them by element index, then repeat
-// {block min of the first candidate f against the shared meta; resolve members before f on
-// private copies; barrier; f applies; barrier} over chunks of kFbChunk members until a chunk has
-// no candidate.
+// Elements still pending after the last round (the fallback list), after k_commit: every such
+// element's key had a first candidate F_R in the last round, whose index it holds in pf. Workgroup
+// b owns the keys with F_R % gridDim == b: it gathers their members as (F_R, element) pairs (LDS,
+// or a region of mem beyond kFbLds pairs), sorts them (each key is then one run in element order)
+// and finishes each run from the committed entry with first-candidate passes: repeat {block min
+// of the first candidate f against the shared meta; resolve members before f on private copies;
+// barrier; f applies; barrier} over chunks of kFbChunk members until a chunk has no candidate.
 template <int TYPE, int SV>
 __global__ __launch_bounds__(kFbThreads) void k_fb_exec(BatchArgs a)
 {
-    __shared__ uint32_t srt[kFbLdsSort];
+    __shared__ unsigned long long srt[kFbLds];
     __shared__ Meta sm;
     __shared__ int red[kFbThreads / 64];
     __shared__ uint32_t lcnt, loff;
     const int tid = threadIdx.x;
-    const uint32_t nk = a.ctr[kCtrFbK], nl = a.ctr[kCtrFbL];
-    Ctx c = make_ctx(a);
-    // every key's last shadow becomes its entry (keys of the last round: below, per key)
-    for (int64_t i = (int64_t)blockIdx.x * kFbThreads + tid; i < a.n; i += (int64_t)gridDim.x * kFbThreads) {
-        if (a.st[i] != kStCommit) continue;
-        uint8_t *dst = entry_of(a, a.ent[i]);
-        const uint8_t *src = shadow_of(a, (uint32_t)i);
-        if (SV == 31) {
-            const uint4 *s4 = reinterpret_cast<const uint4 *>(src);
-            uint4 *d4 = reinterpret_cast<uint4 *>(dst);
-            const uint4 w0 = s4[0], w1 = s4[1], w2 = s4[2], w3 = s4[3];
-            d4[0] = w0;
-            d4[1] = w1;
-            d4[2] = w2;
-            d4[3] = w3;
-        } else {
-            copy_entry(dst, src, a.g.entry_size);
-        }
+    const uint32_t nl = a.ctr[kCtrFbL];
+    if (nl == 0) return;  // uniform
+    const uint32_t G = gridDim.x, me = blockIdx.x;
+    if (tid == 0) lcnt = 0;
+    __syncthreads();
+    for (uint32_t j = tid; j < nl; j += kFbThreads)
+        if (a.pf[a.fbl[j]] % G == me) atomicAdd(&lcnt, 1u);
+    __syncthreads();
+    const uint32_t cnt = lcnt, p2 = pow2ceil(cnt);
+    if (cnt == 0) return;  // uniform
+    unsigned long long *ord = srt;
+    if (p2 > (uint32_t)kFbLds) {
+        if (tid == 0) loff = atomicAdd(&a.ctr[kCtrFbM], p2);
+        __syncthreads();
+        ord = a.mem + loff;
     }
-    for (uint32_t kk = blockIdx.x; kk < nk; kk += gridDim.x) {
-        const uint32_t key = a.fbk[kk];
-        __syncthreads();  // every thread has read the previous key's lcnt
-        uint8_t *entry = entry_of(a, key);
-        // the last round's shadow becomes the entry
-        for (uint32_t w = tid; w < a.g.entry_size / 8; w += kFbThreads)
-            reinterpret_cast<uint64_t *>(entry)[w] = reinterpret_cast<const uint64_t *>(shadow_of(a, a.fbi[kk]))[w];
-        if (tid == 0) lcnt = 0;
+    __syncthreads();
+    if (tid == 0) lcnt = 0;
+    __syncthreads();
+    for (uint32_t j = tid; j < nl; j += kFbThreads) {
+        const uint32_t i = a.fbl[j], f = a.pf[i];
+        if (f % G == me) ord[atomicAdd(&lcnt, 1u)] = ((unsigned long long)f << 32) | i;
+    }
+    for (uint32_t j = cnt + tid; j < p2; j += kFbThreads) ord[j] = ~0ull;
+    __threadfence_block();
+    __syncthreads();
+    bitonic_sort(ord, p2);
+    Ctx c = make_ctx(a);
+    // serial tier: the head of a run of at most kFbSerial members applies it alone, in order
+    for (uint32_t p = tid; p < cnt; p += kFbThreads) {
+        const uint32_t kf = (uint32_t)(ord[p] >> 32);
+        if (p > 0 && (uint32_t)(ord[p - 1] >> 32) == kf) continue;
+        uint32_t re = p + 1;
+        while (re < cnt && re - p <= (uint32_t)kFbSerial && (uint32_t)(ord[re] >> 32) == kf) ++re;
+        if (re - p > (uint32_t)kFbSerial) continue;
+        uint8_t *entry = entry_of(a, a.ent[(uint32_t)ord[p]]);
+        Meta m;
+        meta_load(entry, m);
+        for (uint32_t q = p; q < re; ++q) {
+            uint8_t *x;
+            uint8_t idx;
+            elem_at(a, (uint32_t)ord[q], x, idx, c);
+            dispatch<SV>(TYPE, x, entry, idx, m, c);
+        }
+        meta_store(entry, m);
+    }
+    __syncthreads();
+    for (uint32_t rs = 0; rs < cnt;) {  // longer runs: one at a time, by the whole workgroup
+        const uint32_t key_f = (uint32_t)(ord[rs] >> 32);
+        if (tid == 0) {
+            uint32_t re = rs + 1;
+            while (re < cnt && (uint32_t)(ord[re] >> 32) == key_f) ++re;
+            loff = re;
+            if (re - rs > (uint32_t)kFbSerial) meta_load(entry_of(a, a.ent[(uint32_t)ord[rs]]), sm);
+        }
         __threadfence_block();
         __syncthreads();
-        for (uint32_t j = tid; j < nl; j += kFbThreads)
-            if (a.ent[a.fbl[j]] == key) atomicAdd(&lcnt, 1u);
-        __syncthreads();
-        const uint32_t cnt = lcnt, p2 = pow2ceil(cnt);
-        if (cnt == 0) continue;  // uniform
-        const bool in_lds = p2 <= (uint32_t)kFbLdsSort;
-        uint32_t *ord = srt;
-        if (!in_lds) {
-            if (tid == 0) loff = atomicAdd(&a.ctr[kCtrFbM], p2);
+        const uint32_t re = loff;
+        if (re - rs <= (uint32_t)kFbSerial) {  // uniform: done by the serial tier
             __syncthreads();
-            ord = a.mem + loff;
+            rs = re;
+            continue;
         }
-        __syncthreads();
-        if (tid == 0) lcnt = 0;
-        __syncthreads();
-        for (uint32_t j = tid; j < nl; j += kFbThreads) {
-            const uint32_t i = a.fbl[j];
-            if (a.ent[i] == key) ord[atomicAdd(&lcnt, 1u)] = i;
-        }
-        for (uint32_t j = cnt + tid; j < p2; j += kFbThreads) ord[j] = kNone;
-        __threadfence_block();
-        __syncthreads();
-        bitonic_sort(ord, p2);
-        if (tid == 0) meta_load(entry, sm);
-        __threadfence_block();
-        __syncthreads();
-        for (uint32_t base = 0; base < cnt; base += kFbChunk) {
+        uint8_t *entry = entry_of(a, a.ent[(uint32_t)ord[rs]]);
+        for (uint32_t base = rs; base < re; base += kFbChunk) {
             uint32_t pending = 0;
 #pragma unroll
             for (int j = 0; j < kFbPerThread; ++j)
-                if (base + j * kFbThreads + tid < cnt) pending |= 1u << j;
+                if (base + j * kFbThreads + tid < re) pending |= 1u << j;
             for (;;) {
                 const Meta m = sm;
                 int mine = kFbChunk;
@@ -578,7 +599,7 @@ __global__ __launch_bounds__(kFbThreads) void k_fb_exec(BatchArgs a)
                     if (!(pending >> j & 1u)) continue;
                     uint8_t *x;
                     uint8_t idx;
-                    elem_at(a, ord[base + j * kFbThreads + tid], x, idx, c);
+                    elem_at(a, (uint32_t)ord[base + j * kFbThreads + tid], x, idx, c);
                     if (would_mutate(TYPE, x, m, c)) mine = j * kFbThreads + tid;
                 }
                 const int f = block_min(mine, red);
@@ -588,7 +609,7 @@ __global__ __launch_bounds__(kFbThreads) void k_fb_exec(BatchArgs a)
                     if (!(pending >> j & 1u) || pos >= f) continue;
                     uint8_t *x;
                     uint8_t idx;
-                    elem_at(a, ord[base + pos], x, idx, c);
+                    elem_at(a, (uint32_t)ord[base + pos], x, idx, c);
                     Meta t = m;
                     dispatch<SV>(TYPE, x, entry, idx, t, c);
                     if (a.error_flags && !meta_equal(t, m)) atomicOr(a.error_flags, 1u);
@@ -598,7 +619,7 @@ __global__ __launch_bounds__(kFbThreads) void k_fb_exec(BatchArgs a)
                 if (f < kFbChunk && (f % kFbThreads) == tid) {
                     uint8_t *x;
                     uint8_t idx;
-                    elem_at(a, ord[base + f], x, idx, c);
+                    elem_at(a, (uint32_t)ord[base + f], x, idx, c);
                     Meta mm = m;
                     dispatch<SV>(TYPE, x, entry, idx, mm, c);
                     pending &= ~(1u << (f / kFbThreads));
@@ -610,7 +631,9 @@ __global__ __launch_bounds__(kFbThreads) void k_fb_exec(BatchArgs a)
             }
         }
         if (tid == 0) meta_store(entry, sm);
+        __threadfence_block();
         __syncthreads();
+        rs = re;
     }
 }
 
@@ -628,7 +651,7 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t batch_scratch_bytes(int64_t cap, uint32_t entry_size)
 {
-    return align256(4 * (size_t)cap) * 5 + align256((size_t)cap) + align256(8 * (size_t)cap) + 256 +
+    return align256(4 * (size_t)cap) * 3 + align256((size_t)cap) + align256(16 * (size_t)cap) + 256 +
            align256((size_t)entry_size * (size_t)cap);
 }
 
@@ -642,10 +665,8 @@ void batch_carve(BatchLaunch &bl, uint8_t *base, int64_t cap, uint32_t entry_siz
     };
     bl.ent = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
     bl.st = take((size_t)cap);
-    bl.mem = reinterpret_cast<uint32_t *>(take(8 * (size_t)cap));
-    bl.fbk = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
+    bl.mem = reinterpret_cast<unsigned long long *>(take(16 * (size_t)cap));
     bl.fbl = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
-    bl.fbi = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
     bl.pf = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
     bl.shadow = take((size_t)entry_size * (size_t)cap);
     bl.ctr = reinterpret_cast<uint32_t *>(take(256));
@@ -672,9 +693,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.ent = bl.ent;
     a.st = bl.st;
     a.mem = bl.mem;
-    a.fbk = bl.fbk;
     a.fbl = bl.fbl;
-    a.fbi = bl.fbi;
     a.pf = bl.pf;
     a.shadow = bl.shadow;
     a.ctr = bl.ctr;
@@ -695,7 +714,6 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     const bool big = bl.esz > 64;
     const unsigned rgrid = (unsigned)(big ? (n + 127) / 128 : grid);
     const size_t rlds = (size_t)(big ? 128 : 256) * (size_t)bl.esz;
-    const unsigned fgrid = (unsigned)std::min<int64_t>(512, (n + 4 * kFbThreads - 1) / (4 * kFbThreads));
     const int64_t head = n < kLookupHead ? n : kLookupHead;
     hipLaunchKernelGGL(k_lookup, dim3((unsigned)((head + 63) / 64)), dim3(256), 0, s, a, (int64_t)0, head);
     if (n > head)
@@ -708,7 +726,8 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
             hipLaunchKernelGGL((k_cand<T>), dim3(cgrid), dim3(256), 0, s, a, r);                  \
             hipLaunchKernelGGL((k_resolve<T, V>), dim3(grid), dim3(256), 0, s, a, r);             \
         }                                                                                         \
-        hipLaunchKernelGGL((k_fb_exec<T, V>), dim3(fgrid), dim3(kFbThreads), 0, s, a);            \
+        hipLaunchKernelGGL((k_commit<V>), dim3(grid), dim3(256), 0, s, a);                         \
+        if (a.rounds > 0) hipLaunchKernelGGL((k_fb_exec<T, V>), dim3(256), dim3(kFbThreads), 0, s, a); \
     } while (0)
 #define HKV_ROUNDS_SV(T)                                      \
     do {                                                      \
@@ -731,8 +750,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
         uint32_t c[4] = {0, 0, 0, 0};
         hipMemcpyAsync(c, bl.ctr, sizeof c, hipMemcpyDeviceToHost, s);
         hipStreamSynchronize(s);
-        fprintf(stderr, "[hkv] batch type %d n %lld: last-round keys %u, fallback members %u\n", bl.type,
-                (long long)n, c[kCtrFbK], c[kCtrFbL]);
+        fprintf(stderr, "[hkv] batch type %d n %lld: fallback members %u\n", bl.type, (long long)n, c[kCtrFbL]);
     }
     if (bl.type == kInvs && bl.ns_idx && bl.node_suspected) {
         hipLaunchKernelGGL(k_node_suspected, dim3((bl.n_batches + 255) / 256), dim3(256), 0, s, bl.elems, bl.ns_idx,

@@ -21,7 +21,8 @@ struct BatchLaunch {
     // round state (see hkv_batch.hip): F words per log line (table-wide, all-ones when
     // allocated) and per-launch scratch carved by batch_carve
     unsigned long long *fw;
-    uint32_t *ent, *mem, *fbk, *fbl, *fbi, *pf, *ctr;
+    unsigned long long *mem;
+    uint32_t *ent, *fbl, *pf, *ctr;
     uint8_t *st, *shadow;
     uint32_t cap;                             // elements the scratch was carved for
     uint32_t epoch;                           // launch counter of the table, 1..batch_max_epoch()

@@ -193,7 +193,7 @@ __device__ __forceinline__ void copy_entry(uint8_t *dst, const uint8_t *src, uin
 // The round's first candidate of a key: S_r (read from src: the entry in round 0, the previous
 // round's shadow later) -> S_{r+1}, written to the element's own shadow image, so the round's
 // other elements, resolved concurrently, still read S_r. Later rounds read the shadow; the key's
-// last shadow is committed to the entry once, by k_fb_exec.
+// last shadow is committed to the entry once, by k_commit.
 template <int TYPE, int SV>
 __device__ __forceinline__ void apply_to_shadow(const BatchArgs &a, uint8_t *x, uint32_t i, const uint8_t *src)
 {
@@ -222,89 +222,137 @@ __device__ __forceinline__ void apply_to_shadow(const BatchArgs &a, uint8_t *x, 
 // ------------------------------------------------------------------ k_lookup (+ round 0 candidates)
 // Four lanes per element: each lane reads 16 bytes (two slots) of the element's 64-byte bucket,
 // so one load instruction covers a whole bucket line per element. Slots are searched in the
-// reference's order (first tag match wins, hermesKV.c:954-975). A hit that would mutate its key's
-// meta as it stands (S_0) offers itself as round 0's first candidate. The key compare, the meta
-// and the F word load together once the slot is known; the F word filters the offer (a hot key's
-// later candidates see a smaller F and issue no atomic). The launch is split: a short head over
-// the first kLookupHead elements gives every hot key a small F first, because at the start of
-// one big launch some 10^5 elements are in flight before any F is set, and a hot key's
-// candidates among them would all reach its F word (atomics on one address serialise).
+// reference's order (first tag match wins, hermesKV.c:954-975). Each lane group carries
+// kLookupPair elements through the three dependent loads (op header, bucket, log line) side by
+// side, so twice as many loads are in flight per wave. A hit that would mutate its key's meta as
+// it stands (S_0) offers itself as round 0's first candidate. The key compare, the meta and the F
+// word load together once the slot is known; the F word filters the offer (a hot key's later
+// candidates see a smaller F and issue no atomic). The launch is split: a short head over the
+// first kLookupHead elements gives every hot key a small F first, because at the start of one big
+// launch some 10^5 elements are in flight before any F is set, and a hot key's candidates among
+// them would all reach its F word (atomics on one address serialise).
+//
+// VAL batches finish here: hermes_exec_val (hermesKV.c:676-703) never changes a timestamp, so
+// every VAL of a launch compares against its key's timestamp at launch start, sets VALID iff they
+// match and reports VAL_SUCCESS whatever the state. The VALs of a key commute, and the matching
+// ones all store the same state byte.
 constexpr int64_t kLookupHead = 8192;
+constexpr int kLookupPair = 2;
 __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, int64_t i_end)
 {
     const int q = threadIdx.x & 3;
     const int lane = threadIdx.x & 63;
-    const int64_t gi = i_begin + (int64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
-    const bool in = gi < i_end;
+    const int gbase = lane & ~3;
     if (i_begin == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
         a.ctr[kCtrFbM] = 0;
         a.ctr[kCtrFbL] = 0;
     }
-    int32_t b = 0, idx = 0;
-    uint8_t *x = nullptr;
-    uint64_t key = 0, hdr = 0;
-    int probe = 0;
-    if (in && q == 0) {
-        b = (int32_t)(gi / a.stride);
-        idx = (int32_t)(gi - (int64_t)b * a.stride);
-        if (a.counts == nullptr || idx < a.counts[b]) {
-            x = a.elems + gi * a.esz;
-            key = ld64(x);
-            hdr = ld64(x + 8);
-            if (skip_elem_os(a.type, (uint8_t)hdr, (uint8_t)(hdr >> 8))) {
-                if (a.type == kInvs && a.ns_idx) atomicMax(&a.ns_idx[b], idx);
-            } else {
-                probe = 1;
-            }
-        }
-    }
-    probe = __shfl(probe, 0, 4);
-    key = __shfl(key, 0, 4);
-    uint64_t s0 = 0, s1 = 0;
-    if (probe) {
-        const uint4 v = reinterpret_cast<const uint4 *>(a.index + ((key & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u)[q];
-        s0 = (uint64_t)v.x | ((uint64_t)v.y << 32);
-        s1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
-    }
-    const uint32_t tag = (uint32_t)(key >> 48);
-    const bool m0 = probe && (s0 & 1u) && ((uint32_t)(s0 >> 1) & 0x7FFFFFu) == tag;
-    const bool m1 = probe && (s1 & 1u) && ((uint32_t)(s1 >> 1) & 0x7FFFFFu) == tag;
-    const int gbase = lane & ~3;
-    const uint32_t g0 = (uint32_t)(__ballot(m0) >> gbase) & 0xFu;
-    const uint32_t g1 = (uint32_t)(__ballot(m1) >> gbase) & 0xFu;
-    uint32_t order = 0;  // bit 2*l + j: slot 2*l + j matches
+    const bool vals_direct = a.type == kVals;
+    int64_t gi[kLookupPair];
+    uint64_t key[kLookupPair], hdr[kLookupPair];
+    int probe[kLookupPair];
 #pragma unroll
-    for (int l = 0; l < 4; ++l) order |= ((g0 >> l) & 1u) << (2 * l) | ((g1 >> l) & 1u) << (2 * l + 1);
-    const int first = order ? __ffs(order) - 1 : 0;
-    const uint64_t off = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
-    if (!in || q != 0) return;
-    uint32_t e = kNone;
-    if (probe) {
-        if (order && a.g.log_head - off < a.g.log_cap) {
-            const uint64_t phys = off & a.g.log_mask;
-            const uint8_t *entry = a.log + phys;
-            unsigned long long *f = a.fw + fw_index(a, phys);
-            const uint64_t ekey = ld64(entry + 8);
-            Meta m0;
-            meta_load(entry, m0);
-            const unsigned long long fv = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (ekey == key) {
-                e = (uint32_t)(phys / a.g.entry_unit);
-                uint64_t h2[2] = {0, hdr};
-                Ctx c = make_ctx(a);
-                const unsigned long long v = ((unsigned long long)(~a.rtag0) << 32) | (uint32_t)gi;
-                if (would_mutate(a.type, reinterpret_cast<const uint8_t *>(h2), m0, c)) {
-                    if (v < fv) atomicMin(f, v);
-                    // the seqlock byte is free at batch boundaries (concur_ctrl.h: the lock is
-                    // held only inside one exec call): it tells k_resolve0 which keys have a
-                    // candidate, so the others skip the F word; the key's commit clears it
-                    if ((uint8_t)(m0.w5 >> 16) != a.ltag) const_cast<uint8_t *>(entry)[kEntryMetaOff + 4] = a.ltag;
+    for (int k = 0; k < kLookupPair; ++k) {
+        gi[k] = i_begin + ((int64_t)blockIdx.x * kLookupPair + k) * 64 + (threadIdx.x >> 2);
+        uint64_t kk = 0, hh = 0;
+        int p = 0;
+        if (gi[k] < i_end && q == 0) {
+            const int32_t b = (int32_t)(gi[k] / a.stride);
+            const int32_t idx = (int32_t)(gi[k] - (int64_t)b * a.stride);
+            if (a.counts == nullptr || idx < a.counts[b]) {
+                const uint8_t *x = a.elems + gi[k] * a.esz;
+                kk = ld64(x);
+                hh = ld64(x + 8);
+                if (skip_elem_os(a.type, (uint8_t)hh, (uint8_t)(hh >> 8))) {
+                    if (a.type == kInvs && a.ns_idx) atomicMax(&a.ns_idx[b], idx);
+                } else {
+                    p = 1;
                 }
             }
         }
-        if (e == kNone) x[9] = kMiss;
+        key[k] = kk;
+        hdr[k] = hh;
+        probe[k] = p;
     }
-    a.ent[gi] = e;
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        const int p = __shfl(probe[k], 0, 4);
+        const uint64_t kk = __shfl(key[k], 0, 4);
+        probe[k] = p;
+        key[k] = kk;
+    }
+    uint4 v[kLookupPair];
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k)
+        v[k] = probe[k] ? reinterpret_cast<const uint4 *>(a.index + ((key[k] & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u)[q]
+                        : make_uint4(0u, 0u, 0u, 0u);
+    uint64_t off[kLookupPair];
+    uint32_t order[kLookupPair];
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        const uint64_t s0 = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
+        const uint64_t s1 = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
+        const uint32_t tag = (uint32_t)(key[k] >> 48);
+        const bool mt0 = probe[k] && (s0 & 1u) && ((uint32_t)(s0 >> 1) & 0x7FFFFFu) == tag;
+        const bool mt1 = probe[k] && (s1 & 1u) && ((uint32_t)(s1 >> 1) & 0x7FFFFFu) == tag;
+        const uint32_t g0 = (uint32_t)(__ballot(mt0) >> gbase) & 0xFu;
+        const uint32_t g1 = (uint32_t)(__ballot(mt1) >> gbase) & 0xFu;
+        uint32_t o = 0;  // bit 2*l + j: slot 2*l + j matches
+#pragma unroll
+        for (int l = 0; l < 4; ++l) o |= ((g0 >> l) & 1u) << (2 * l) | ((g1 >> l) & 1u) << (2 * l + 1);
+        order[k] = o;
+        const int first = o ? __ffs(o) - 1 : 0;
+        off[k] = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
+    }
+    if (q != 0) return;
+    // the log line (key, meta) and the F word of every element, all in flight together
+    bool ok[kLookupPair];
+    uint64_t phys[kLookupPair], ekey[kLookupPair];
+    Meta m0[kLookupPair];
+    unsigned long long fv[kLookupPair];
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        ok[k] = probe[k] && order[k] && a.g.log_head - off[k] < a.g.log_cap;
+        phys[k] = off[k] & a.g.log_mask;
+        ekey[k] = 0;
+        fv[k] = 0;
+        m0[k] = Meta{};
+        if (ok[k]) {
+            const uint8_t *entry = a.log + phys[k];
+            ekey[k] = ld64(entry + 8);
+            meta_load(entry, m0[k]);
+            if (!vals_direct)
+                fv[k] = __hip_atomic_load(a.fw + fw_index(a, phys[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        if (gi[k] >= i_end) continue;
+        uint8_t *x = a.elems + gi[k] * a.esz;
+        uint32_t e = kNone;
+        if (ok[k] && ekey[k] == key[k]) {
+            e = (uint32_t)(phys[k] / a.g.entry_unit);
+            uint8_t *entry = a.log + phys[k];
+            if (vals_direct) {
+                const uint64_t its = pack_ts((uint32_t)(hdr[k] >> 32), (uint8_t)(hdr[k] >> 24));
+                if (its == pack_ts(m0[k].ver, m_cid(m0[k])) && m_state(m0[k]) != kValid) entry[kEntryMetaOff] = kValid;
+                x[8] = kValSuccess;
+            } else {
+                uint64_t h2[2] = {0, hdr[k]};
+                Ctx c = make_ctx(a);
+                if (would_mutate(a.type, reinterpret_cast<const uint8_t *>(h2), m0[k], c)) {
+                    const unsigned long long vv = ((unsigned long long)(~a.rtag0) << 32) | (uint32_t)gi[k];
+                    if (vv < fv[k]) atomicMin(a.fw + fw_index(a, phys[k]), vv);
+                    // the seqlock byte is free at batch boundaries (concur_ctrl.h: the lock is held
+                    // only inside one exec call): it tells k_resolve0 which keys have a candidate,
+                    // so the others skip the F word; the key's commit clears it
+                    if ((uint8_t)(m0[k].w5 >> 16) != a.ltag) entry[kEntryMetaOff + 4] = a.ltag;
+                }
+            }
+        }
+        if (probe[k] && e == kNone) x[9] = kMiss;
+        a.ent[gi[k]] = e;
+    }
 }
 
 // ------------------------------------------------------------------ rounds (passes over all elements)
@@ -714,10 +762,15 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     const bool big = bl.esz > 64;
     const unsigned rgrid = (unsigned)(big ? (n + 127) / 128 : grid);
     const size_t rlds = (size_t)(big ? 128 : 256) * (size_t)bl.esz;
+    constexpr int64_t kPer = 64 * kLookupPair;  // elements per k_lookup block
+    if (bl.type == kVals) {                    // one pass (see k_lookup)
+        hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, n);
+        return hipGetLastError() == hipSuccess ? 0 : -3;
+    }
     const int64_t head = n < kLookupHead ? n : kLookupHead;
-    hipLaunchKernelGGL(k_lookup, dim3((unsigned)((head + 63) / 64)), dim3(256), 0, s, a, (int64_t)0, head);
+    hipLaunchKernelGGL(k_lookup, dim3((unsigned)((head + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, head);
     if (n > head)
-        hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n - head + 63) / 64)), dim3(256), 0, s, a, head, n);
+        hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n - head + kPer - 1) / kPer)), dim3(256), 0, s, a, head, n);
 #define HKV_ROUNDS(T, V)                                                                          \
     do {                                                                                          \
         if (big) hipLaunchKernelGGL((k_resolve0<T, V, 128>), dim3(rgrid), dim3(128), rlds, s, a); \

@@ -150,8 +150,8 @@ class ReplicaRound:
         return {"committed": c[0], "misses": c[1], "writes_completed": c[2], "invs_held": h[0], "vals_dropped": h[1]}
 
 
-def _timed(events, name, fn):
-    if events is None:
+def _timed(events, name, fn, only=None):
+    if events is None or (only is not None and name not in only):
         fn()
         return
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -195,18 +195,18 @@ class ReplicaGroupRound:
     def _a2a(self, out, inp):
         self.dist.all_to_all_single(out, inp, group=self.group)
 
-    def step(self, events: dict | None = None):
+    def step(self, events: dict | None = None, timed_batches=None):
         r = self.r
-        _timed(events, "local", r.local)
+        _timed(events, "local", r.local, timed_batches)
         self._gather(r.inv_recv, r.inv_slab)
         self._gather(r.inv_recv_count, r.inv_count)
-        _timed(events, "invs", r.invs)
+        _timed(events, "invs", r.invs, timed_batches)
         self._a2a(r.ack_recv, r.ack_slab)
         self._a2a(r.ack_recv_count, r.ack_slab_count)
-        _timed(events, "acks", r.acks)
+        _timed(events, "acks", r.acks, timed_batches)
         self._gather(r.val_recv, r.val_slab)
         self._gather(r.val_recv_count, r.val_count)
-        _timed(events, "vals", r.vals)
+        _timed(events, "vals", r.vals, timed_batches)
         r.refill()
 
     def stats(self) -> dict:

@@ -183,11 +183,12 @@ class Round:
         self.kvs.batch(L.BatchType.vals, vals, n_batches, stride, L.OP_META_SIZE, self.mb, counts=counts)
 
     # -- a whole round with virtual peers
-    def step(self, events: dict | None = None):
+    def step(self, events: dict | None = None, timed_batches=("local", "invs", "acks", "vals")):
         """One round of every virtual worker. `events` (name -> list) collects (start, end)
-        torch.cuda.Event pairs per batch for live kernel timing."""
+        torch.cuda.Event pairs for the batches named in `timed_batches` (each event record costs
+        a few microseconds of GPU time, so a timed region records only what it reports)."""
         def timed(name, fn):
-            if events is None:
+            if events is None or name not in timed_batches:
                 fn()
                 return
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

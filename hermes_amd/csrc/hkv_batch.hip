@@ -76,6 +76,7 @@ struct BatchArgs {
     int32_t rounds;              // rounds after round 0 before the fallback
     uint8_t g_membership;
     uint8_t w_ack_init;
+    uint32_t var;                // experiment switches (HKV_VAR)
 };
 
 // Rounds after round 0 per batch type: how often a hot key usually mutates in one launch beyond
@@ -225,9 +226,11 @@ __device__ __forceinline__ void apply_to_shadow(const BatchArgs &a, uint8_t *x, 
 // reference's order (first tag match wins, hermesKV.c:954-975). Each lane group carries
 // kLookupPair elements through the three dependent loads (op header, bucket, log line) side by
 // side, so twice as many loads are in flight per wave. A hit that would mutate its key's meta as
-// it stands (S_0) offers itself as round 0's first candidate. The key compare, the meta and the F
-// word load together once the slot is known; the F word filters the offer (a hot key's later
-// candidates see a smaller F and issue no atomic). The launch is split: a short head over the
+// it stands (S_0) offers itself as round 0's first candidate. The key compare and the meta load
+// together once the slot is known; a candidate then loads its F word, which filters the offer (a
+// hot key's later candidates see a smaller F and issue no atomic). Non-candidates never touch F:
+// the batch is bound by random 64-B lines, and one less per element beats the shorter dependence
+// chain of loading F beside the meta. The launch is split: a short head over the
 // first kLookupHead elements gives every hot key a small F first, because at the start of one big
 // launch some 10^5 elements are in flight before any F is set, and a hot key's candidates among
 // them would all reach its F word (atomics on one address serialise).
@@ -305,24 +308,21 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
         off[k] = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
     }
     if (q != 0) return;
-    // the log line (key, meta) and the F word of every element, all in flight together
+    // the log lines (key, meta) of both elements in flight together; the F word only for a
+    // candidate (a dependent load, but one random line less for the ~80 % that never mutate)
     bool ok[kLookupPair];
     uint64_t phys[kLookupPair], ekey[kLookupPair];
     Meta m0[kLookupPair];
-    unsigned long long fv[kLookupPair];
 #pragma unroll
     for (int k = 0; k < kLookupPair; ++k) {
         ok[k] = probe[k] && order[k] && a.g.log_head - off[k] < a.g.log_cap;
         phys[k] = off[k] & a.g.log_mask;
         ekey[k] = 0;
-        fv[k] = 0;
         m0[k] = Meta{};
         if (ok[k]) {
             const uint8_t *entry = a.log + phys[k];
             ekey[k] = ld64(entry + 8);
             meta_load(entry, m0[k]);
-            if (!vals_direct)
-                fv[k] = __hip_atomic_load(a.fw + fw_index(a, phys[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 #pragma unroll
@@ -342,7 +342,8 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                 Ctx c = make_ctx(a);
                 if (would_mutate(a.type, reinterpret_cast<const uint8_t *>(h2), m0[k], c)) {
                     const unsigned long long vv = ((unsigned long long)(~a.rtag0) << 32) | (uint32_t)gi[k];
-                    if (vv < fv[k]) atomicMin(a.fw + fw_index(a, phys[k]), vv);
+                    unsigned long long *fw = a.fw + fw_index(a, phys[k]);
+                    if (vv < __hip_atomic_load(fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(fw, vv);
                     // the seqlock byte is free at batch boundaries (concur_ctrl.h: the lock is held
                     // only inside one exec call): it tells k_resolve0 which keys have a candidate,
                     // so the others skip the F word; the key's commit clears it
@@ -757,6 +758,8 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.rounds = rounds_for(bl.type, bl.g.rmw_enabled != 0);
     a.g_membership = bl.g_membership;
     a.w_ack_init = bl.w_ack_init;
+    static const uint32_t var = getenv("HKV_VAR") ? (uint32_t)atoi(getenv("HKV_VAR")) : 0u;
+    a.var = var;
     const unsigned grid = (unsigned)((n + 255) / 256);
     const unsigned cgrid = (unsigned)((n + 256 * kCandPer - 1) / (256 * kCandPer));
     const bool big = bl.esz > 64;

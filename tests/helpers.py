@@ -5,6 +5,7 @@ import json
 import os
 
 import numpy as np
+import pytest
 
 from hermes_amd import layout as L
 
@@ -71,3 +72,47 @@ def run_known_answers(engine, keys: np.ndarray):
     miss = make_elems([{"id": i, "opcode": "GET"} for i in ka["always_miss_ids"]], keys, L.DEFAULT, False)
     engine.batch(L.BatchType.local_ops, miss, mb)
     assert (miss["state"] == int(L.Resp.MISS)).all()
+
+
+class Mirror:
+    """Runs every batch launch of a device table on an oracle twin and compares."""
+
+    def __init__(self, g, o, name):
+        self.g, self.o, self.name = g, o, name
+        self.launches = 0
+        self._orig = g.batch
+        g.batch = self.batch
+
+    def batch(self, btype, elems, n_batches, stride, elem_size, membership, counts=None, rw=None,
+              rw_stride_bytes=0, node_suspected=None, stream=None):
+        import torch
+        torch.cuda.synchronize()
+        n = n_batches * stride * elem_size
+        vt = np.dtype((np.void, elem_size))
+        e_in = elems[:n].cpu().numpy().copy().view(vt)
+        c_in = counts[:n_batches].cpu().numpy().copy() if counts is not None else None
+        rw_in = rw_op = None
+        if rw is not None:
+            rw_in = rw.cpu().numpy().copy().view(np.dtype((np.void, self.g.sizes.op)))
+        self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
+                   node_suspected, stream)
+        torch.cuda.synchronize()
+        self.o.batch_multi(int(btype), e_in, n_batches, stride, c_in, membership, rw_in,
+                           rw_stride_bytes // self.g.sizes.op if rw is not None else 0)
+        what = f"{self.name} launch {self.launches} type {int(btype)}"
+        got = elems[:n].cpu().numpy()
+        if not np.array_equal(got, e_in.view(np.uint8)):
+            bad = np.nonzero(got != e_in.view(np.uint8))[0]
+            pytest.fail(f"{what}: elements differ at {len(bad)} bytes, first elems {np.unique(bad // elem_size)[:8]}")
+        if rw is not None:
+            rw_op = rw.cpu().numpy()
+            assert np.array_equal(rw_op, rw_in.view(np.uint8)), f"{what}: read_write_ops differ"
+        gl, ol = self.g.log_bytes(), self.o.log_bytes()[: self.g.cfg.log_cap]
+        if not np.array_equal(gl, ol):
+            bad = np.nonzero(gl != ol)[0]
+            e = self.g.sizes.entry
+            pytest.fail(f"{what}: log differs in entries {np.unique(bad // e)[:8]}, "
+                        f"bytes-in-entry {np.unique(bad % e)[:16]}")
+        assert np.array_equal(self.g.index_bytes(), self.o.index_bytes()), f"{what}: index differs"
+        assert self.g.take_error_flags() == 0, f"{what}: device consistency flags"
+        self.launches += 1

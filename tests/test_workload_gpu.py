@@ -1,0 +1,41 @@
+"""The N=1 bench round (hermes_amd.workload.Round, virtual peers) on the GPU: every batch launch
+of a Round over more than kLookupHead (8192) local elements -- so the split lookup, the
+absorbing-state shortcut, the INV/ACK rounds and the fallback all run as in bench.py -- is
+mirrored into an oracle table and must be bit-exact (elements, read_write_ops, index, log).
+"""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from hermes_amd import layout as L  # noqa: E402
+from oracle.oracle import OracleKVS  # noqa: E402
+from tests.helpers import Mirror  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.mark.parametrize("theta,workers", [(0.99, 40), (0.0, 40), (0.99, 160)])
+def test_bench_round_mirrored(theta, workers):
+    from hermes_amd.kvs import HermesKV
+    from hermes_amd.workload import Round, zipf_params
+    n_keys, bkts, cap = 60_000, 1 << 16, 1 << 23
+    steps = 3                         # 10,000 / 40,000 local elements per launch
+    g = HermesKV(n_keys, bkts, cap, machine_id=0)
+    o = OracleKVS(bkts, cap, 0)
+    o.populate(n_keys, L.DEFAULT.kvs_value)
+    m = Mirror(g, o, "bench round")
+    r = Round(g, workers, L.membership(3, 0), [1, 2], zipf_params(n_keys, theta), 200, seed=0x5EED,
+              max_steps=8, trace_len=1024)
+    for _ in range(steps):
+        r.step()
+    torch.cuda.synchronize()
+    assert m.launches == steps * 4
+    st = r.stats()
+    assert st["committed"] > 0 and st["writes_completed"] > 0, st
+    assert g.take_error_flags() == 0

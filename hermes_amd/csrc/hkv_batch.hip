@@ -216,7 +216,10 @@ __device__ __forceinline__ void apply_to_shadow(const BatchArgs &a, uint8_t *x, 
     uint8_t *xg;
     uint8_t idx;
     elem_at(a, i, xg, idx, c);
-    dispatch<SV>(TYPE, x ? x : xg, sh, idx, m, c);
+    // x: the element's LDS copy (k_resolve0), or null: the element in global memory. Two calls,
+    // not one on a select of the two, so each keeps its address space (no flat accesses).
+    if (x) dispatch<SV>(TYPE, x, sh, idx, m, c);
+    else dispatch<SV>(TYPE, xg, sh, idx, m, c);
     meta_store(sh, m);
 }
 
@@ -239,6 +242,11 @@ __device__ __forceinline__ void apply_to_shadow(const BatchArgs &a, uint8_t *x, 
 // every VAL of a launch compares against its key's timestamp at launch start, sets VALID iff they
 // match and reports VAL_SUCCESS whatever the state. The VALs of a key commute, and the matching
 // ones all store the same state byte.
+// 16 bytes at an 8-byte aligned address (op headers, log lines): one dwordx4 access
+struct __attribute__((aligned(8))) U64x2 {
+    uint64_t a, b;
+};
+
 constexpr int64_t kLookupHead = 8192;
 constexpr int kLookupPair = 2;
 __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, int64_t i_end)
@@ -263,9 +271,9 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
             const int32_t b = (int32_t)(gi[k] / a.stride);
             const int32_t idx = (int32_t)(gi[k] - (int64_t)b * a.stride);
             if (a.counts == nullptr || idx < a.counts[b]) {
-                const uint8_t *x = a.elems + gi[k] * a.esz;
-                kk = ld64(x);
-                hh = ld64(x + 8);
+                const U64x2 h = *reinterpret_cast<const U64x2 *>(a.elems + gi[k] * a.esz);
+                kk = h.a;
+                hh = h.b;
                 if (skip_elem_os(a.type, (uint8_t)hh, (uint8_t)(hh >> 8))) {
                     if (a.type == kInvs && a.ns_idx) atomicMax(&a.ns_idx[b], idx);
                 } else {
@@ -307,24 +315,32 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
         const int first = o ? __ffs(o) - 1 : 0;
         off[k] = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
     }
-    if (q != 0) return;
-    // the log lines (key, meta) of both elements in flight together; the F word only for a
-    // candidate (a dependent load, but one random line less for the ~80 % that never mutate)
+    // the log line of every element: the group's four lanes read 16 B each (bytes 8..32 hold the
+    // key and the meta), one access per lane for both elements in flight together; lane 0 gathers.
+    // The F word only for a candidate (a dependent load, but one random line less for the ~80 %
+    // that never mutate).
     bool ok[kLookupPair];
     uint64_t phys[kLookupPair], ekey[kLookupPair];
     Meta m0[kLookupPair];
+    U64x2 ln[kLookupPair];
 #pragma unroll
     for (int k = 0; k < kLookupPair; ++k) {
         ok[k] = probe[k] && order[k] && a.g.log_head - off[k] < a.g.log_cap;
         phys[k] = off[k] & a.g.log_mask;
-        ekey[k] = 0;
-        m0[k] = Meta{};
-        if (ok[k]) {
-            const uint8_t *entry = a.log + phys[k];
-            ekey[k] = ld64(entry + 8);
-            meta_load(entry, m0[k]);
-        }
+        ln[k] = ok[k] ? reinterpret_cast<const U64x2 *>(a.log + phys[k])[q] : U64x2{0, 0};
     }
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        ekey[k] = __shfl(ln[k].b, 0, 4);
+        const uint64_t w45 = __shfl(ln[k].a, 1, 4), w67 = __shfl(ln[k].b, 1, 4);
+        const uint32_t b32 = (uint32_t)__shfl(ln[k].a, 2, 4) & 0xFFu;
+        m0[k].w4 = (uint32_t)w45;
+        m0[k].w5 = (uint32_t)(w45 >> 32);
+        m0[k].ver = (uint32_t)w67;
+        m0[k].llw_cid = (uint8_t)(w67 >> 32);
+        m0[k].llw_ver = (uint32_t)(w67 >> 40) | (b32 << 24);
+    }
+    if (q != 0) return;
 #pragma unroll
     for (int k = 0; k < kLookupPair; ++k) {
         if (gi[k] >= i_end) continue;
@@ -405,12 +421,33 @@ template <int TYPE, int SV, int BP>
 __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
 {
     extern __shared__ uint4 sops[];
+    // 64-B entries: each thread reads bytes 16..63 (meta + value) in three 16-B accesses; the meta
+    // comes from registers, the value from the thread's LDS copy
+    constexpr bool kStage = SV == 31;
+    __shared__ U64x2 sent[kStage ? 3 * BP : 1];
     const int64_t i0 = (int64_t)blockIdx.x * BP;
     const int cnt = a.n - i0 < BP ? (int)(a.n - i0) : BP;
     // the element's entry id and meta load while the block copies its op slab in
     const uint32_t e = (int)threadIdx.x < cnt ? a.ent[i0 + threadIdx.x] : kNone;
     Meta m{};
-    if (e != kNone) meta_load(entry_of(a, e), m);
+    if (e != kNone) {
+        if (kStage) {
+            const U64x2 *p = reinterpret_cast<const U64x2 *>(entry_of(a, e));
+            const U64x2 l1 = p[1], l2 = p[2], l3 = p[3];
+            m.w4 = (uint32_t)l1.a;
+            m.w5 = (uint32_t)(l1.a >> 32);
+            m.ver = (uint32_t)l1.b;
+            m.llw_cid = (uint8_t)(l1.b >> 32);
+            m.llw_ver = (uint32_t)(l1.b >> 40) | ((uint32_t)(l2.a & 0xFFu) << 24);
+            sent[3 * threadIdx.x] = l1;
+            sent[3 * threadIdx.x + 1] = l2;
+            sent[3 * threadIdx.x + 2] = l3;
+        } else {
+            meta_load(entry_of(a, e), m);
+        }
+    }
+    // what the non-mutating elements read the entry value from (bytes below 16 are never read)
+    uint8_t *rentry = kStage ? reinterpret_cast<uint8_t *>(&sent[3 * threadIdx.x]) - 16 : entry_of(a, e);
     const uint32_t bytes = (uint32_t)cnt * (uint32_t)a.esz;  // a multiple of 8
     const uint4 *src = reinterpret_cast<const uint4 *>(a.elems + i0 * a.esz);
     for (uint32_t w = threadIdx.x; w < bytes / 16; w += BP) sops[w] = src[w];
@@ -429,9 +466,8 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
                 uint8_t *xg;
                 uint8_t idx;
                 elem_at(a, (uint32_t)i, xg, idx, c);
-                uint8_t *entry = entry_of(a, e);
                 Meta tm = m;
-                dispatch<SV>(TYPE, reinterpret_cast<uint8_t *>(sops) + (uint32_t)t * a.esz, entry, idx, tm, c);
+                dispatch<SV>(TYPE, reinterpret_cast<uint8_t *>(sops) + (uint32_t)t * a.esz, rentry, idx, tm, c);
                 if (a.error_flags && !meta_equal(tm, m)) atomicOr(a.error_flags, 1u);
             } else if ((uint32_t)i == f) {
                 apply_to_shadow<TYPE, SV>(a, reinterpret_cast<uint8_t *>(sops) + (uint32_t)t * a.esz, (uint32_t)i,
@@ -445,7 +481,7 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
                 Meta m1 = m;
                 m_set_state(m1, absorbing_state<TYPE>());
                 Meta tm = m1;
-                dispatch<SV>(TYPE, reinterpret_cast<uint8_t *>(sops) + (uint32_t)t * a.esz, entry_of(a, e), idx, tm, c);
+                dispatch<SV>(TYPE, reinterpret_cast<uint8_t *>(sops) + (uint32_t)t * a.esz, rentry, idx, tm, c);
                 if (a.error_flags && !meta_equal(tm, m1)) atomicOr(a.error_flags, 1u);
             } else {
                 a.pf[i] = f;

@@ -85,7 +85,9 @@ __device__ __forceinline__ void copy_bytes(uint8_t *__restrict__ dst, const uint
     for (uint32_t k = 0; k < head; ++k) dst[k] = src[k];
     const uint8_t *s = src + head;
     const uint32_t sh = (uint32_t)(uintptr_t)s & 3u;
-    const uint32_t *sa = reinterpret_cast<const uint32_t *>((uintptr_t)s & ~(uintptr_t)3);
+    // aligned down by pointer arithmetic, not through an integer, so an LDS or global source
+    // keeps its address space (an int-to-pointer cast would make every access a flat one)
+    const uint32_t *sa = reinterpret_cast<const uint32_t *>(s - sh);
     uint32_t *da = reinterpret_cast<uint32_t *>(dst + head);
     const uint32_t nw = (n - head) >> 2;
     if (sh == 0) {

@@ -165,13 +165,14 @@ __device__ __forceinline__ uint32_t agg_ticket(uint32_t *arr, uint32_t j, bool a
     return ticket;
 }
 
+// x: the element (global), or its LDS copy
 template <int TYPE, int SV>
-__device__ __forceinline__ void resolve_elem(const BatchArgs &a, uint32_t i, uint8_t *entry)
+__device__ __forceinline__ void resolve_elem(const BatchArgs &a, uint32_t i, uint8_t *x, uint8_t *entry)
 {
     Ctx c = make_ctx(a);
-    uint8_t *x;
+    uint8_t *xg;
     uint8_t idx;
-    elem_at(a, i, x, idx, c);
+    elem_at(a, i, xg, idx, c);
     Meta m;
     meta_load(entry, m);
     Meta t = m;
@@ -246,6 +247,14 @@ __device__ __forceinline__ void apply_to_shadow(const BatchArgs &a, uint8_t *x, 
 struct __attribute__((aligned(8))) U64x2 {
     uint64_t a, b;
 };
+
+// esz (a multiple of 8) bytes between 8-byte aligned buffers, 16 B per access
+__device__ __forceinline__ void copy_elem(uint8_t *dst, const uint8_t *src, int32_t esz)
+{
+    for (int32_t o = 0; o + 16 <= esz; o += 16)
+        *reinterpret_cast<U64x2 *>(dst + o) = *reinterpret_cast<const U64x2 *>(src + o);
+    if (esz & 8) *reinterpret_cast<uint64_t *>(dst + esz - 8) = *reinterpret_cast<const uint64_t *>(src + esz - 8);
+}
 
 constexpr int64_t kLookupHead = 8192;
 constexpr int kLookupPair = 2;
@@ -503,19 +512,31 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
 template <int TYPE, int SV>
 __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
 {
+    // 16-B messages (ACKs, VALs): the element is dispatched on an LDS copy, one 16-B access in and
+    // one out instead of the exec functions' byte-wise global accesses. (A 56-B op costs more to
+    // write back whole than the one or two bytes an INV changes.)
+    extern __shared__ uint64_t sx[];
+    const bool kStage = SV == 31 && (a.esz <= 16 || (a.var & 1));
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     bool left = false;
     if (i < a.n && a.st[i] == kStPend) {
         const uint32_t e = a.ent[i];
         const uint32_t f = first_cand(*fw_of(a, e), a.rtag0 + (uint32_t)r);
         const uint32_t prev = a.pf[i];  // S_r lives in the shadow of round r-1's first candidate
-        if (f == kNone || (uint32_t)i < f) {
-            resolve_elem<TYPE, SV>(a, (uint32_t)i, shadow_of(a, prev));
-            a.st[i] = kStDone;
-        } else if ((uint32_t)i == f) {
-            apply_to_shadow<TYPE, SV>(a, nullptr, (uint32_t)i, shadow_of(a, prev));
-            a.st[prev] = kStDone;  // superseded
-            a.st[i] = kStCommit;
+        if (f == kNone || (uint32_t)i <= f) {
+            uint8_t *xg = a.elems + i * a.esz;
+            uint8_t *xl = reinterpret_cast<uint8_t *>(sx) + threadIdx.x * (uint32_t)a.esz;
+            if (kStage) copy_elem(xl, xg, a.esz);
+            if ((uint32_t)i != f) {
+                if (kStage) resolve_elem<TYPE, SV>(a, (uint32_t)i, xl, shadow_of(a, prev));
+                else resolve_elem<TYPE, SV>(a, (uint32_t)i, xg, shadow_of(a, prev));
+                a.st[i] = kStDone;
+            } else {
+                apply_to_shadow<TYPE, SV>(a, kStage ? xl : nullptr, (uint32_t)i, shadow_of(a, prev));
+                a.st[prev] = kStDone;  // superseded
+                a.st[i] = kStCommit;
+            }
+            if (kStage) copy_elem(xg, xl, a.esz);
         } else {
             a.pf[i] = f;  // after the last round: identifies the key's run in k_fb_exec
             left = r == a.rounds;
@@ -816,7 +837,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
         else hipLaunchKernelGGL((k_resolve0<T, V, 256>), dim3(rgrid), dim3(256), rlds, s, a);     \
         for (int r = 1; r <= a.rounds; ++r) {                                                     \
             hipLaunchKernelGGL((k_cand<T>), dim3(cgrid), dim3(256), 0, s, a, r);                  \
-            hipLaunchKernelGGL((k_resolve<T, V>), dim3(grid), dim3(256), 0, s, a, r);             \
+            hipLaunchKernelGGL((k_resolve<T, V>), dim3(grid), dim3(256), V == 31 ? 256 * bl.esz : 0, s, a, r); \
         }                                                                                         \
         hipLaunchKernelGGL((k_commit<V>), dim3(grid), dim3(256), 0, s, a);                         \
         if (a.rounds > 0) hipLaunchKernelGGL((k_fb_exec<T, V>), dim3(256), dim3(kFbThreads), 0, s, a); \

@@ -43,22 +43,24 @@ __device__ __forceinline__ void m_set_obi(Meta &m, uint8_t v) { m.w5 = (m.w5 & 0
 __device__ __forceinline__ uint8_t m_cid(const Meta &m) { return (uint8_t)(m.w5 >> 24); }
 __device__ __forceinline__ void m_set_cid(Meta &m, uint8_t v) { m.w5 = (m.w5 & 0x00FFFFFFu) | ((uint32_t)v << 24); }
 
+// Entries and shadows are 8-byte aligned: the meta moves as two 8-byte words (bytes 16..31) and
+// byte 32, three memory instructions instead of five.
 __device__ __forceinline__ void meta_load(const uint8_t *e, Meta &m)
 {
-    m.w4 = ld32(e + 16);
-    m.w5 = ld32(e + 20);
-    m.ver = ld32(e + 24);
-    uint32_t w7 = ld32(e + 28);
-    m.llw_cid = (uint8_t)w7;
-    m.llw_ver = (w7 >> 8) | ((uint32_t)e[32] << 24);
+    const uint64_t a = *reinterpret_cast<const uint64_t *>(e + 16);
+    const uint64_t b = *reinterpret_cast<const uint64_t *>(e + 24);
+    m.w4 = (uint32_t)a;
+    m.w5 = (uint32_t)(a >> 32);
+    m.ver = (uint32_t)b;
+    m.llw_cid = (uint8_t)(b >> 32);
+    m.llw_ver = (uint32_t)(b >> 40) | ((uint32_t)e[32] << 24);
 }
 
 __device__ __forceinline__ void meta_store(uint8_t *e, const Meta &m)
 {
-    st32(e + 16, m.w4);
-    st32(e + 20, m.w5 & 0xFF00FFFFu);  // the seqlock byte is free at batch boundaries
-    st32(e + 24, m.ver);
-    st32(e + 28, (uint32_t)m.llw_cid | (m.llw_ver << 8));
+    // the seqlock byte is free at batch boundaries
+    *reinterpret_cast<uint64_t *>(e + 16) = (uint64_t)m.w4 | ((uint64_t)(m.w5 & 0xFF00FFFFu) << 32);
+    *reinterpret_cast<uint64_t *>(e + 24) = (uint64_t)m.ver | ((uint64_t)m.llw_cid << 32) | ((uint64_t)m.llw_ver << 40);
     e[32] = (uint8_t)(m.llw_ver >> 24);
 }
 

@@ -13,7 +13,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libhermeskv.so")
+# HKV_LIB: another build of the same library (A/B timing of two revisions in one GPU session)
+LIB_PATH = os.environ.get("HKV_LIB") or os.path.join(HERE, "libhermeskv.so")
 ABI_VERSION = 1
 
 if not os.path.exists(LIB_PATH):

@@ -56,6 +56,7 @@ struct BatchArgs {
     uint8_t *rw;
     int32_t *ns_idx;
     unsigned long long *fw;      // [log_cap / 64] F word per 64-B log line (table-wide), see fw_index
+    unsigned long long *fx, *fy; // [log_cap / 64] INV words X, Y (INV direct path; zero between launches)
     uint32_t fw_mask;
     uint32_t *ent;               // [n] entry id of every element (kNone: skipped or missing)
     uint8_t *st;                 // [n] stage (kSt*)
@@ -74,6 +75,7 @@ struct BatchArgs {
     uint32_t rtag0;              // round 0's tag; round r uses rtag0 + r
     uint8_t ltag;                // launch tag (1..255) in the seqlock byte of keys with a round-0 candidate
     int32_t rounds;              // rounds after round 0 before the fallback
+    int32_t inv_direct;          // INV launch on the direct path (k_inv_resolve)
     uint8_t g_membership;
     uint8_t w_ack_init;
     uint32_t var;                // experiment switches (HKV_VAR)
@@ -100,6 +102,33 @@ template <int TYPE>
 __device__ __forceinline__ uint8_t absorbing_state()
 {
     return TYPE == kVals ? kValid : kWrite;
+}
+
+// INV direct path (INV launches without RMWs, fewer than 2^23 elements). Without RMWs,
+// hermes_exec_inv (hermesKV.c:489-588) on one key, element by element from S_0, comes to this:
+// let M be the largest INV timestamp of the key's elements.
+//   M > ts_0:  the first element with ts M (A) installs its value, RMW flag and M; the state moves
+//              once (VALID -> INVALID, WRITE/REPLAY -> INVALID_WRITE, others stay), val_len :=
+//              KVS_VALUE_SIZE; last_writer_id := sender of the last element with ts M (B).
+//   M = ts_0:  last_writer_id := sender of the last element with ts ts_0 (B); nothing else.
+//   M < ts_0:  nothing.
+// Every element's opcode is INV_SUCCESS (an INV_ABORT / OUT_OF_GROUP input stays), except
+// OUT_OF_GROUP for an element with ts = ts_0 in state WRITE, which holds until the first element
+// with a larger ts (P). Per key (log line) three words:
+//   X = max over raising elements of (ts << 24 | ~i) -> M and A (k_lookup); bit 23 of X: some
+//       element other than A has ts M (k_inv_resolve);
+//   F = round 0's word: P, offered by raising elements of keys in state WRITE (k_lookup);
+//   Y = 1 + B when B != A (k_inv_resolve), or for keys without a raise.
+// k_lookup finishes the elements below ts_0; k_inv_resolve writes the other opcodes; in
+// k_inv_commit A (or, without a raise, B) applies the key's meta and clears X and Y. Most keys of a
+// launch have one element: it is A and B, and never touches Y.
+enum : uint8_t { kIvRaise = 1, kIvEq = 2, kIvWrite = 4, kIvCand = 8, kIvApply = 16 };
+constexpr int64_t kInvDirectMax = 1 << 23;
+constexpr unsigned long long kXHasB = 1ull << 23;
+
+__device__ __forceinline__ uint8_t inv_opcode(uint8_t in, bool oog)
+{
+    return oog ? kInvOutOfGroup : (in == kOpInvAbort || in == kInvOutOfGroup) ? in : kInvSuccess;
 }
 
 __device__ __forceinline__ Ctx make_ctx(const BatchArgs &a)
@@ -355,6 +384,7 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
         if (gi[k] >= i_end) continue;
         uint8_t *x = a.elems + gi[k] * a.esz;
         uint32_t e = kNone;
+        uint8_t ifl = 0;
         if (ok[k] && ekey[k] == key[k]) {
             e = (uint32_t)(phys[k] / a.g.entry_unit);
             uint8_t *entry = a.log + phys[k];
@@ -362,6 +392,20 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                 const uint64_t its = pack_ts((uint32_t)(hdr[k] >> 32), (uint8_t)(hdr[k] >> 24));
                 if (its == pack_ts(m0[k].ver, m_cid(m0[k])) && m_state(m0[k]) != kValid) entry[kEntryMetaOff] = kValid;
                 x[8] = kValSuccess;
+            } else if (a.inv_direct) {
+                const uint64_t its = pack_ts((uint32_t)(hdr[k] >> 32), (uint8_t)(hdr[k] >> 24));
+                const uint64_t cur = pack_ts(m0[k].ver, m_cid(m0[k]));
+                if (its < cur) {
+                    x[8] = inv_opcode((uint8_t)hdr[k], false);
+                } else if (its == cur) {
+                    ifl = kIvEq | (m_state(m0[k]) == kWrite ? kIvWrite : 0);
+                } else {
+                    ifl = kIvRaise;
+                    const uint32_t w = fw_index(a, phys[k]);
+                    const unsigned long long xv = (its << 24) | (0x7FFFFFull - (uint64_t)gi[k]);
+                    if (xv > __hip_atomic_load(a.fx + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(a.fx + w, xv);
+                    if (m_state(m0[k]) == kWrite) offer(a.fw + w, a.rtag0, (uint32_t)gi[k]);
+                }
             } else {
                 uint64_t h2[2] = {0, hdr[k]};
                 Ctx c = make_ctx(a);
@@ -378,7 +422,153 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
         }
         if (probe[k] && e == kNone) x[9] = kMiss;
         a.ent[gi[k]] = e;
+        if (a.inv_direct) a.st[gi[k]] = ifl;
     }
+}
+
+// INV direct path: opcodes of the elements at or above ts_0, A marks itself, the other elements
+// with ts M (or, without a raise, all of them) set Y. Launched twice, the last kLookupHead
+// elements first: they set Y (and the has-B bit) of every hot key near its final value, so the
+// bulk launch's candidates read a larger Y and issue no atomic (atomics on one address serialise,
+// and some 10^5 elements run at once).
+__global__ __launch_bounds__(256) void k_inv_resolve(BatchArgs a, int64_t i_begin, int64_t i_end)
+{
+    const int64_t i = i_begin + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= i_end) return;
+    const uint8_t fl = a.st[i];
+    if (fl == 0) return;
+    const uint32_t w = fw_index(a, phys_of(a, a.ent[i]));
+    uint8_t *x = a.elems + i * a.esz;
+    const uint64_t hdr = *reinterpret_cast<const uint64_t *>(x + 8);
+    const uint64_t its = pack_ts((uint32_t)(hdr >> 32), (uint8_t)(hdr >> 24));
+    const unsigned long long X = a.fx[w];  // M and A are final (k_lookup)
+    bool oog = false, y = false;
+    if (X != 0) {  // some element raises the key's ts
+        // in state WRITE, an element at ts_0 is out of group until the first raise P (offered by
+        // every raising element of a key in state WRITE, so it exists)
+        if (fl & kIvWrite) oog = (uint32_t)i < first_cand(a.fw[w], a.rtag0);
+        if ((uint32_t)i == 0x7FFFFFu - (uint32_t)(X & 0x7FFFFFu)) {
+            a.st[i] = kIvApply;
+        } else if (its == (uint64_t)(X >> 24)) {
+            y = true;
+            if (!(__hip_atomic_load(a.fx + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kXHasB)) atomicOr(a.fx + w, kXHasB);
+        }
+    } else {       // no raise: every flagged element of the key is at ts_0, B applies
+        oog = (fl & kIvWrite) != 0;
+        y = true;
+        a.st[i] = kIvCand;
+    }
+    x[8] = inv_opcode((uint8_t)hdr, oog);
+    if (y) {
+        const unsigned long long yv = (unsigned long long)i + 1;
+        if (yv > __hip_atomic_load(a.fy + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(a.fy + w, yv);
+    }
+}
+
+// A of a raising key applies the key's meta to a 64-B entry (31-B values): entry bytes 16..63
+// (meta, value) and the element's bytes 16..63 (flags, value) move as three 16-B words each, the
+// new entry image is put together in registers.
+__device__ __forceinline__ void inv_apply64(const BatchArgs &a, int64_t i, uint32_t w, uint8_t *entry)
+{
+    union Img {
+        U64x2 q[3];
+        uint64_t d[6];
+    };
+    Img en, el;
+    const U64x2 *pe = reinterpret_cast<const U64x2 *>(entry + 16);
+    const U64x2 *px = reinterpret_cast<const U64x2 *>(a.elems + i * a.esz + 16);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) en.q[k] = pe[k];
+    el.q[0] = px[0];  // the 56-B element ends at image byte 40: bytes 16..55 only
+    el.q[1] = px[1];
+    el.d[4] = *reinterpret_cast<const uint64_t *>(px + 2);
+    el.d[5] = 0;
+    const unsigned long long X = a.fx[w];
+    int64_t b = i;
+    if (X & kXHasB) {
+        b = (int64_t)a.fy[w] - 1;
+        a.fy[w] = 0;
+    }
+    const uint8_t lw = b == i ? (uint8_t)(a.elems[i * a.esz + 9]) : a.elems[b * a.esz + 9];
+    Meta m;
+    m.w4 = (uint32_t)en.d[0];
+    m.w5 = (uint32_t)(en.d[0] >> 32);
+    m.ver = (uint32_t)en.d[1];
+    m.llw_cid = (uint8_t)(en.d[1] >> 32);
+    m.llw_ver = (uint32_t)(en.d[1] >> 40) | ((uint32_t)(en.d[2] & 0xFFu) << 24);
+    const uint64_t M = X >> 24;
+    const uint8_t st = m_state(m);
+    if (st == kValid) m_set_state(m, kInvalid);
+    else if (st == kWrite || st == kReplay) m_set_state(m, kInvalidWrite);
+    m_set_val_len(m, (uint8_t)a.g.kvs_value);
+    m_set_rmw(m, (uint8_t)(el.d[0] & 1u));  // element byte 16: RMW_flag
+    m_set_lwid(m, lw);
+    m.ver = (uint32_t)(M >> 8);
+    m_set_cid(m, (uint8_t)M);
+    // value: element bytes 18..48 -> entry bytes 33..63, i.e. image byte 2 + k -> 17 + k: the
+    // element image shifted up by 15 bytes = 120 bits (one word and 56 bits)
+    uint64_t v[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const uint64_t lo = k >= 2 ? el.d[k - 2] : 0, hi = k >= 1 ? el.d[k - 1] : 0;
+        v[k] = (hi << 56) | (lo >> 8);
+    }
+    // bytes 0..15 of the image: meta (seqlock byte free), byte 16: llw_ver's top byte, 17..47: value
+    Img out;
+    out.d[0] = (uint64_t)m.w4 | ((uint64_t)(m.w5 & 0xFF00FFFFu) << 32);
+    out.d[1] = (uint64_t)m.ver | ((uint64_t)m.llw_cid << 32) | ((uint64_t)m.llw_ver << 40);
+    out.d[2] = (uint64_t)(uint8_t)(m.llw_ver >> 24) | (v[2] & ~0xFFull);
+    out.d[3] = v[3];
+    out.d[4] = v[4];
+    out.d[5] = v[5];
+    U64x2 *po = reinterpret_cast<U64x2 *>(entry + 16);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) po[k] = out.q[k];
+    a.fx[w] = 0;
+}
+
+// INV direct path: A (or, without a raise, B) applies its key's meta and clears X and Y.
+template <int SV>
+__global__ __launch_bounds__(256) void k_inv_commit(BatchArgs a)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    const uint8_t fl = a.st[i];
+    if (fl != kIvApply && fl != kIvCand) return;
+    const uint32_t e = a.ent[i];
+    const uint32_t w = fw_index(a, phys_of(a, e));
+    int64_t b = i;  // B
+    if (fl == kIvCand) {
+        if (a.fy[w] != (unsigned long long)i + 1) return;
+        a.fy[w] = 0;
+    }
+    uint8_t *entry = entry_of(a, e);
+    if (SV == 31 && fl == kIvApply) {  // 64-B entries: bytes 16..63 in and out as three 16-B words
+        inv_apply64(a, i, w, entry);
+        return;
+    }
+    Meta m;
+    meta_load(entry, m);
+    if (fl == kIvApply) {
+        const unsigned long long X = a.fx[w];
+        if (X & kXHasB) {
+            b = (int64_t)a.fy[w] - 1;
+            a.fy[w] = 0;
+        }
+        const uint8_t *xa = a.elems + i * a.esz;
+        const uint64_t M = X >> 24;
+        const uint8_t st = m_state(m);
+        if (st == kValid) m_set_state(m, kInvalid);
+        else if (st == kWrite || st == kReplay) m_set_state(m, kInvalidWrite);
+        m_set_val_len(m, (uint8_t)a.g.kvs_value);
+        m_set_rmw(m, e_rmw(xa));
+        copy_value<SV>(entry + kEntryValueOff, xa + kOpValueOff, a.g.st_value);
+        m.ver = (uint32_t)(M >> 8);
+        m_set_cid(m, (uint8_t)M);
+        a.fx[w] = 0;
+    }
+    m_set_lwid(m, a.elems[b * a.esz + 9]);
+    meta_store(entry, m);
 }
 
 // ------------------------------------------------------------------ rounds (passes over all elements)
@@ -813,6 +1003,9 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.rtag0 = bl.epoch << 3;
     a.ltag = (uint8_t)(bl.epoch % 255u + 1u);
     a.rounds = rounds_for(bl.type, bl.g.rmw_enabled != 0);
+    a.fx = bl.fx;
+    a.fy = bl.fy;
+    a.inv_direct = bl.type == kInvs && !bl.g.rmw_enabled && n < kInvDirectMax;
     a.g_membership = bl.g_membership;
     a.w_ack_init = bl.w_ack_init;
     static const uint32_t var = getenv("HKV_VAR") ? (uint32_t)atoi(getenv("HKV_VAR")) : 0u;
@@ -831,6 +1024,14 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     hipLaunchKernelGGL(k_lookup, dim3((unsigned)((head + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, head);
     if (n > head)
         hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n - head + kPer - 1) / kPer)), dim3(256), 0, s, a, head, n);
+    if (a.inv_direct) {
+        const int64_t tail = n > kLookupHead ? n - kLookupHead : 0;
+        hipLaunchKernelGGL(k_inv_resolve, dim3((unsigned)((n - tail + 255) / 256)), dim3(256), 0, s, a, tail, n);
+        if (tail > 0) hipLaunchKernelGGL(k_inv_resolve, dim3((unsigned)((tail + 255) / 256)), dim3(256), 0, s, a, (int64_t)0, tail);
+        if (bl.g.st_value == 31) hipLaunchKernelGGL((k_inv_commit<31>), dim3(grid), dim3(256), 0, s, a);
+        else if (bl.g.st_value == 287) hipLaunchKernelGGL((k_inv_commit<287>), dim3(grid), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_inv_commit<0>), dim3(grid), dim3(256), 0, s, a);
+    } else {
 #define HKV_ROUNDS(T, V)                                                                          \
     do {                                                                                          \
         if (big) hipLaunchKernelGGL((k_resolve0<T, V, 128>), dim3(rgrid), dim3(128), rlds, s, a); \
@@ -857,6 +1058,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     }
 #undef HKV_ROUNDS_SV
 #undef HKV_ROUNDS
+    }
     if (hipGetLastError() != hipSuccess) return -3;
     static const bool stats = getenv("HKV_STATS") != nullptr;
     if (stats) {  // debug: what reached the fallback (synchronises the stream)

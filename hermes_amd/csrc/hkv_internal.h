@@ -21,6 +21,7 @@ struct BatchLaunch {
     // round state (see hkv_batch.hip): F words per log line (table-wide, all-ones when
     // allocated) and per-launch scratch carved by batch_carve
     unsigned long long *fw;
+    unsigned long long *fx, *fy;              // INV words per log line (zero between launches)
     unsigned long long *mem;
     uint32_t *ent, *fbl, *pf, *ctr;
     uint8_t *st, *shadow;

@@ -360,3 +360,62 @@ def test_hash_ids_matches_oracle():
     from oracle.oracle import cityhash128
     for k, i in enumerate(ids[5000:]):
         assert got[5000 + k] == cityhash128(int(i).to_bytes(4, "little"))[1]
+
+
+def test_inv_direct_path_edge_cases():
+    """The INV direct path (non-RMW INV launches: X/F/Y words, k_inv_resolve, k_inv_commit) against
+    the oracle: timestamps below, equal to and above each key's (so OUT_OF_GROUP holds exactly up
+    to the first raise while the key is in WRITE), repeated maxima from several senders (the last
+    one's sender is the last writer), INV_ABORT / OUT_OF_GROUP / MEMBERSHIP_CHANGE input opcodes,
+    hot and missing keys, ragged counts, and launches past the 8192-element lookup head."""
+    g, o, sizes = make_pair(2000, 1024, 1 << 17)
+    keys = gen_keys(2000)
+    rng = np.random.default_rng(424242)
+    tsp = gen.TsPool(rng)
+    mb = L.membership(5, 0)
+    e = sizes.entry
+    W, M = 14, 900
+    for rnd in range(6):
+        pool = gen.key_pool(rng, keys, hot=12 if rnd % 2 else 150)
+        loc = gen.local_ops(rng, pool, 8 * 250, sizes, False, tsp)   # leaves keys in WRITE / REPLAY
+        loc_o = gen.bytecopy(loc)
+        _run_both(g, o, L.BatchType.local_ops, loc, loc_o, mb, 8, 250, None)
+        assert_elems_equal(loc, loc_o, f"round {rnd} local")
+        inv = np.zeros(W * M, dtype=L.op_dtype(sizes))
+        inv["key"] = gen.draw_keys(rng, pool, W * M)
+        log = o.log_bytes()
+        cur_v = np.zeros(W * M, np.uint32)
+        cur_c = np.zeros(W * M, np.uint8)
+        for i, k in enumerate(inv["key"]):
+            off = o.lookup(int(k))
+            if off is not None:
+                cur_v[i] = log[off + 24:off + 28].view(np.uint32)[0]
+                cur_c[i] = log[off + 23]
+        kind = rng.choice(4, size=W * M, p=[0.2, 0.35, 0.3, 0.15])   # below, equal, +2, +4
+        ver = cur_v.astype(np.int64) + np.select([kind == 0, kind == 2, kind == 3], [-2, 2, 4], 0)
+        ver = np.maximum(ver, 0).astype(np.uint32)
+        cid = np.where(kind == 1, cur_c, rng.integers(0, 3, size=W * M)).astype(np.uint8)
+        inv["ts_ver"] = ver
+        inv["ts_cid"] = cid
+        inv["state"] = rng.integers(0, 5, size=W * M)                    # sender
+        inv["opcode"] = rng.choice([int(L.Op.INV), int(L.Resp.OP_INV_ABORT), L.INV_OUT_OF_GROUP,
+                                    int(L.Op.MEMBERSHIP_CHANGE)], size=W * M, p=[0.8, 0.08, 0.07, 0.05])
+        inv["val_len"] = sizes.st_value >> sizes.shift
+        inv["flags"] = rng.integers(0, 2, size=W * M)
+        inv["value"] = rng.integers(0, 256, size=(W * M, sizes.st_value))
+        counts = rng.integers(M // 2, M + 1, size=W).astype(np.int32)
+        ns_g = np.full(W, -1, np.int32)
+        ns_o = ns_g.copy()
+        inv_o = gen.bytecopy(inv)
+        _run_both(g, o, L.BatchType.invs, inv, inv_o, mb, W, M, counts, ns_g=ns_g, ns_o=ns_o)
+        assert_elems_equal(inv, inv_o, f"round {rnd} invs")
+        np.testing.assert_array_equal(ns_g, ns_o)
+        assert_tables_equal(g, o, f"round {rnd} invs")
+        out = inv["opcode"][inv["state"] != int(L.Resp.MISS)]
+        assert (out == L.INV_OUT_OF_GROUP).any() and (out == int(L.Resp.INV_SUCCESS)).any()
+        # VALs for some of the INVs bring keys back to VALID for the next round
+        val = gen.vals(rng, pool, 8 * 250, sizes, False, tsp)
+        val_o = gen.bytecopy(val)
+        _run_both(g, o, L.BatchType.vals, val, val_o, mb, 8, 250, None)
+        assert_elems_equal(val, val_o, f"round {rnd} vals")
+    del e

@@ -185,6 +185,16 @@ __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, ui
     for (int k = i; k < words; k += 256) gslab[k] = slab[k];
 }
 
+// 16 bytes at an 8-byte aligned address: one dwordx4 access (op headers, 16-B messages)
+struct __attribute__((aligned(8))) W16 {
+    uint64_t a, b;
+};
+// header word (bytes 8..15) with opcode (byte 8) and state/sender (byte 9) replaced
+__device__ __forceinline__ uint64_t with_op_state(uint64_t h, uint8_t op, uint8_t st)
+{
+    return (h & ~0xFFFFull) | op | ((uint64_t)st << 8);
+}
+
 // wings_issue_pkts(inv) with the INV callbacks of hermes_worker.c:12-65. At most out_stride
 // INVs per worker go out per round (the send credits); the rest keep their state and are
 // sent by a later round, as with the reference's credit-limited wings sends.
@@ -205,11 +215,12 @@ __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stri
     }
     if (!send || rank >= out_stride) return;
     uint8_t *dst = out + ((int64_t)w * out_stride + rank) * op_size;
-    const uint64_t *s64 = reinterpret_cast<const uint64_t *>(op);
-    uint64_t *d64 = reinterpret_cast<uint64_t *>(dst);
-    for (uint32_t k = 0; k < op_size / 8; ++k) d64[k] = s64[k];
-    dst[9] = (uint8_t)machine_id;
-    dst[8] = kOpInv;
+    // 16-B words; the header word is rewritten in registers
+    const W16 h = *reinterpret_cast<const W16 *>(op);
+    *reinterpret_cast<W16 *>(dst) = W16{h.a, with_op_state(h.b, kOpInv, (uint8_t)machine_id)};
+    uint32_t k = 16;
+    for (; k + 16 <= op_size; k += 16) *reinterpret_cast<W16 *>(dst + k) = *reinterpret_cast<const W16 *>(op + k);
+    if (k < op_size) *reinterpret_cast<uint64_t *>(dst + k) = *reinterpret_cast<const uint64_t *>(op + k);
     op[9] = st == kPutSuccess ? kInProgressPut : st == kRmwSuccess ? kInProgressRmw
           : st == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
 }
@@ -310,10 +321,8 @@ __global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32
     if (j >= n) return;
     const uint64_t *src = reinterpret_cast<const uint64_t *>(invs + ((int64_t)w * inv_stride + j) * op_size);
     uint64_t *dst = reinterpret_cast<uint64_t *>(acks + ((int64_t)w * out_stride + rem) * kOpMetaSize);
-    uint64_t h1 = src[1];
-    h1 = (h1 & ~0xFFFFull) | kOpAck | ((uint64_t)peers[r] << 8);  // ack_copy_and_modify_elem
-    dst[0] = src[0];
-    dst[1] = h1;
+    const W16 h = *reinterpret_cast<const W16 *>(src);
+    *reinterpret_cast<W16 *>(dst) = W16{h.a, with_op_state(h.b, kOpAck, peers[r])};  // ack_copy_and_modify_elem
 }
 
 // ack_skip_or_get_sender_id + ack_copy_and_modify_elem + ack_modify_elem_after_send
@@ -324,13 +333,14 @@ __global__ void k_marshal_acks(uint8_t *invs, int64_t n, uint32_t op_size, uint8
     if (i >= n) return;
     uint8_t *x = invs + i * op_size;
     uint8_t *y = out + i * ack_size;
-    uint8_t oc = x[8];
+    const W16 h = *reinterpret_cast<const W16 *>(x);
+    const uint8_t oc = (uint8_t)h.b;
     if (oc == kInvSuccess || (oc == kOpInvAbort && ack_size >= op_size)) {
-        uint32_t words = (oc == kInvSuccess ? kOpMetaSize : op_size) / 8;
-        for (uint32_t k = 0; k < words; ++k)
-            reinterpret_cast<uint64_t *>(y)[k] = reinterpret_cast<const uint64_t *>(x)[k];
-        y[9] = (uint8_t)machine_id;
-        y[8] = oc == kInvSuccess ? kOpAck : kOpInvAbort;
+        *reinterpret_cast<W16 *>(y) =
+            W16{h.a, with_op_state(h.b, oc == kInvSuccess ? kOpAck : kOpInvAbort, (uint8_t)machine_id)};
+        if (oc != kInvSuccess)
+            for (uint32_t k = 16; k < op_size; k += 8)
+                *reinterpret_cast<uint64_t *>(y + k) = *reinterpret_cast<const uint64_t *>(x + k);
     } else {
         y[8] = kEmpty;
     }
@@ -344,15 +354,10 @@ __global__ void k_marshal_vals(uint8_t *acks, int64_t n, uint32_t ack_size, uint
     if (i >= n) return;
     uint8_t *x = acks + i * ack_size;
     uint8_t *y = out + i * kOpMetaSize;
-    uint8_t oc = x[8];
-    if (oc == kLastAckSuccess) {
-        reinterpret_cast<uint64_t *>(y)[0] = reinterpret_cast<const uint64_t *>(x)[0];
-        reinterpret_cast<uint64_t *>(y)[1] = reinterpret_cast<const uint64_t *>(x)[1];
-        y[8] = kOpVal;
-        y[9] = (uint8_t)machine_id;
-    } else {
-        y[8] = kEmpty;
-    }
+    const W16 h = *reinterpret_cast<const W16 *>(x);
+    const uint8_t oc = (uint8_t)h.b;
+    if (oc == kLastAckSuccess) *reinterpret_cast<W16 *>(y) = W16{h.a, with_op_state(h.b, kOpVal, (uint8_t)machine_id)};
+    else y[8] = kEmpty;
     if (oc == kLastAckSuccess || oc == kAckSuccess || oc == kOpMembChange) x[8] = kEmpty;
 }
 

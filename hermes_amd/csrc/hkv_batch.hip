@@ -57,6 +57,7 @@ struct BatchArgs {
     int32_t *ns_idx;
     unsigned long long *fw;      // [log_cap / 64] F word per 64-B log line (table-wide), see fw_index
     unsigned long long *fx, *fy; // [log_cap / 64] INV words X, Y (INV direct path; zero between launches)
+    uint32_t *ft;                // [log_cap / 64][8] ACK words T (ACK direct path; zero between launches)
     uint32_t fw_mask;
     uint32_t *ent;               // [n] entry id of every element (kNone: skipped or missing)
     uint8_t *st;                 // [n] stage (kSt*)
@@ -76,6 +77,7 @@ struct BatchArgs {
     uint8_t ltag;                // launch tag (1..255) in the seqlock byte of keys with a round-0 candidate
     int32_t rounds;              // rounds after round 0 before the fallback
     int32_t inv_direct;          // INV launch on the direct path (k_inv_resolve)
+    int32_t ack_direct;          // ACK launch on the direct path (k_ack_resolve)
     uint8_t g_membership;
     uint8_t w_ack_init;
     uint32_t var;                // experiment switches (HKV_VAR)
@@ -125,6 +127,24 @@ __device__ __forceinline__ uint8_t absorbing_state()
 enum : uint8_t { kIvRaise = 1, kIvEq = 2, kIvWrite = 4, kIvCand = 8, kIvApply = 16 };
 constexpr int64_t kInvDirectMax = 1 << 23;
 constexpr unsigned long long kXHasB = 1ull << 23;
+
+// ACK direct path (ACK launches without RMWs). Without RMWs, hermes_exec_ack (hermesKV.c:591-674)
+// changes a key only through ACKs that match its pending write (ts = last local write's ts, op
+// buffer index set): each ORs its sender's bit into ack_bv, and the first one after which ack_bv
+// covers the group membership G completes the write (op buffer index := EMPTY, INVALID_WRITE ->
+// INVALID, WRITE/REPLAY -> VALID, the read_write_op slot completes; LAST_ACK_SUCCESS from WRITE or
+// REPLAY). The ACKs never change the timestamp they match against, so with T[s] = the first
+// matching element of sender s and N = G minus the bits already set, that element is
+//   j* = max over s in N of T[s] (none if some T[s] is missing), or the first matching element
+//        of any sender (F) when N is empty.
+// ack_bv ends as ack_bv | the bits of the senders whose T[s] <= j* (every T[s] without a
+// completion). Opcodes: ACK_SUCCESS (a LAST_ACK_SUCCESS input stays), LAST_ACK_SUCCESS for j*
+// from WRITE or REPLAY. k_lookup finishes the non-matching elements, sets T (as max of ~i) and F
+// and caches each matching element's ack_bv / state / op buffer index in pf; in k_ack_resolve
+// j* (or, without a completion, F) applies the key's meta; k_ack_clear zeroes T.
+enum : uint8_t { kAkMatch = 1, kAkApply = 2 };
+
+__device__ __forceinline__ uint8_t ack_opcode(uint8_t in) { return in == kLastAckSuccess ? in : kAckSuccess; }
 
 __device__ __forceinline__ uint8_t inv_opcode(uint8_t in, bool oog)
 {
@@ -392,6 +412,22 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                 const uint64_t its = pack_ts((uint32_t)(hdr[k] >> 32), (uint8_t)(hdr[k] >> 24));
                 if (its == pack_ts(m0[k].ver, m_cid(m0[k])) && m_state(m0[k]) != kValid) entry[kEntryMetaOff] = kValid;
                 x[8] = kValSuccess;
+            } else if (a.ack_direct) {
+                const uint64_t ats = pack_ts((uint32_t)(hdr[k] >> 32), (uint8_t)(hdr[k] >> 24));
+                if (ats != pack_ts(m0[k].llw_ver, m0[k].llw_cid) || m_obi(m0[k]) == kObiEmpty) {
+                    x[8] = ack_opcode((uint8_t)hdr[k]);
+                } else {
+                    ifl = kAkMatch;
+                    const uint32_t w = fw_index(a, phys[k]);
+                    offer(a.fw + w, a.rtag0, (uint32_t)gi[k]);
+                    const uint8_t snd = (uint8_t)(hdr[k] >> 8);
+                    if (snd < 8) {
+                        uint32_t *t = a.ft + (size_t)w * 8 + snd;
+                        const uint32_t tv = 0xFFFFFFFFu - (uint32_t)gi[k];
+                        if (tv > __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(t, tv);
+                    }
+                    a.pf[gi[k]] = (uint32_t)m_ack_bv(m0[k]) | ((uint32_t)m_state(m0[k]) << 8) | ((uint32_t)m_obi(m0[k]) << 16);
+                }
             } else if (a.inv_direct) {
                 const uint64_t its = pack_ts((uint32_t)(hdr[k] >> 32), (uint8_t)(hdr[k] >> 24));
                 const uint64_t cur = pack_ts(m0[k].ver, m_cid(m0[k]));
@@ -422,7 +458,7 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
         }
         if (probe[k] && e == kNone) x[9] = kMiss;
         a.ent[gi[k]] = e;
-        if (a.inv_direct) a.st[gi[k]] = ifl;
+        if (a.inv_direct || a.ack_direct) a.st[gi[k]] = ifl;
     }
 }
 
@@ -569,6 +605,78 @@ __global__ __launch_bounds__(256) void k_inv_commit(BatchArgs a)
     }
     m_set_lwid(m, a.elems[b * a.esz + 9]);
     meta_store(entry, m);
+}
+
+// ACK direct path: each matching element finds j*; j* (or, without a completion, F) applies the
+// key's meta and completes the read_write_op slot. Nothing else reads the entry in this pass (the
+// others use the cached S_0 fields), so the applier writes it here.
+__global__ __launch_bounds__(256) void k_ack_resolve(BatchArgs a)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n || a.st[i] != kAkMatch) return;
+    const uint32_t e = a.ent[i];
+    const uint32_t w = fw_index(a, phys_of(a, e));
+    const uint32_t c0 = a.pf[i];
+    const uint8_t bv0 = (uint8_t)c0, st0 = (uint8_t)(c0 >> 8), obi0 = (uint8_t)(c0 >> 16);
+    const uint4 *tp = reinterpret_cast<const uint4 *>(a.ft + (size_t)w * 8);
+    const uint4 t0 = tp[0], t1 = tp[1];
+    const uint32_t tv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+    const uint8_t need = (uint8_t)(a.g_membership & ~bv0);
+    const uint32_t f = first_cand(a.fw[w], a.rtag0);
+    uint32_t js = kNone;  // j*
+    if (need == 0) {
+        js = f;
+    } else {
+        uint32_t mx = 0;
+        bool all = true;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            if (!((need >> s) & 1u)) continue;
+            if (tv[s] == 0) all = false;
+            else mx = max(mx, 0xFFFFFFFFu - tv[s]);
+        }
+        if (all) js = mx;
+    }
+    uint8_t *x = a.elems + i * a.esz;
+    const bool done = (uint32_t)i == js;
+    const bool wr = st0 == kWrite || st0 == kReplay;
+    x[8] = done && wr ? kLastAckSuccess : ack_opcode(x[8]);
+    if (!(done || (js == kNone && (uint32_t)i == f))) return;
+    // the applier: ack_bv, and with a completion the state, op buffer index and read_write_op
+    uint8_t bv = bv0;
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+        if (tv[s] != 0 && (js == kNone || 0xFFFFFFFFu - tv[s] <= js)) bv |= (uint8_t)(1u << s);
+    uint8_t *entry = entry_of(a, e);
+    Meta m;
+    meta_load(entry, m);
+    m_set_ack_bv(m, bv);
+    if (done) {
+        if (st0 == kInvalidWrite) m_set_state(m, kInvalid);
+        else if (wr) m_set_state(m, kValid);
+        else if (st0 != kValid && st0 != kInvalid && a.error_flags) atomicOr(a.error_flags, 2u);
+        m_set_obi(m, kObiEmpty);
+        if (a.rw) {
+            const int64_t b = i / a.stride;
+            uint8_t *rw = a.rw + b * a.rw_stride + (size_t)obi0 * a.g.op_size;
+            const uint8_t oc = rw[8];
+            if (oc == kOpGet) rw[9] = kNew;
+            else if (oc == kOpPut) rw[9] = kPutComplete;
+            else if (oc == kOpRmw) rw[9] = kRmwComplete;
+        }
+    }
+    meta_store(entry, m);
+    a.st[i] = kAkApply;
+}
+
+// ACK direct path: the appliers zero their keys' T words.
+__global__ __launch_bounds__(256) void k_ack_clear(BatchArgs a)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n || a.st[i] != kAkApply) return;
+    uint4 *tp = reinterpret_cast<uint4 *>(a.ft + (size_t)fw_index(a, phys_of(a, a.ent[i])) * 8);
+    tp[0] = make_uint4(0u, 0u, 0u, 0u);
+    tp[1] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // ------------------------------------------------------------------ rounds (passes over all elements)
@@ -1006,6 +1114,8 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.fx = bl.fx;
     a.fy = bl.fy;
     a.inv_direct = bl.type == kInvs && !bl.g.rmw_enabled && n < kInvDirectMax;
+    a.ft = bl.ft;
+    a.ack_direct = bl.type == kAcks && !bl.g.rmw_enabled && n < (int64_t)kNone;
     a.g_membership = bl.g_membership;
     a.w_ack_init = bl.w_ack_init;
     static const uint32_t var = getenv("HKV_VAR") ? (uint32_t)atoi(getenv("HKV_VAR")) : 0u;
@@ -1024,7 +1134,10 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     hipLaunchKernelGGL(k_lookup, dim3((unsigned)((head + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, head);
     if (n > head)
         hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n - head + kPer - 1) / kPer)), dim3(256), 0, s, a, head, n);
-    if (a.inv_direct) {
+    if (a.ack_direct) {
+        hipLaunchKernelGGL(k_ack_resolve, dim3(grid), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_ack_clear, dim3(grid), dim3(256), 0, s, a);
+    } else if (a.inv_direct) {
         const int64_t tail = n > kLookupHead ? n - kLookupHead : 0;
         hipLaunchKernelGGL(k_inv_resolve, dim3((unsigned)((n - tail + 255) / 256)), dim3(256), 0, s, a, tail, n);
         if (tail > 0) hipLaunchKernelGGL(k_inv_resolve, dim3((unsigned)((tail + 255) / 256)), dim3(256), 0, s, a, (int64_t)0, tail);

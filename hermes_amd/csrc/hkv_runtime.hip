@@ -32,7 +32,7 @@ struct hkv_table {
     // batch scratch (batch_carve)
     uint8_t *d_batch = nullptr;
     int64_t batch_cap = 0;
-    unsigned long long *d_fw = nullptr;  // F words, one per 64-B log line (+ the INV words X, Y)
+    unsigned long long *d_fw = nullptr;  // F words, one per 64-B log line (+ INV words X, Y, ACK words T)
     uint32_t epoch = 0;                // batch launches since d_fw was all-ones
     unsigned int *d_error_flags = nullptr;
     int32_t *d_ns_idx = nullptr;
@@ -131,14 +131,15 @@ static int bit_width(uint64_t x)
 static int ensure_batch_scratch(hkv_table *t, int64_t n)
 {
     if (!t->d_fw) {
-        // F words, then the INV words X and Y (batch_fw_words each, see hkv_batch.hip)
+        // F words, the INV words X and Y (batch_fw_words each), then the ACK words T (eight u32
+        // per line), see hkv_batch.hip
         const size_t bytes = 8 * batch_fw_words(t->cfg.log_cap);
-        HIP_TRY(hipMalloc(&t->d_fw, 3 * bytes));
-        // F all-ones: every F word reads as stale for every epoch; X and Y zero (they are cleared
-        // by the launch that sets them). hipMemset runs on the null stream, which does not order
-        // the table's non-blocking streams: wait for it here.
+        HIP_TRY(hipMalloc(&t->d_fw, 7 * bytes));
+        // F all-ones: every F word reads as stale for every epoch; X, Y and T zero (they are
+        // cleared by the launch that sets them). hipMemset runs on the null stream, which does
+        // not order the table's non-blocking streams: wait for it here.
         HIP_TRY(hipMemset(t->d_fw, 0xFF, bytes));
-        HIP_TRY(hipMemset(reinterpret_cast<uint8_t *>(t->d_fw) + bytes, 0, 2 * bytes));
+        HIP_TRY(hipMemset(reinterpret_cast<uint8_t *>(t->d_fw) + bytes, 0, 6 * bytes));
         HIP_TRY(hipDeviceSynchronize());
         t->epoch = 0;
     }
@@ -349,6 +350,7 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.fw = t->d_fw;
     bl.fx = t->d_fw + batch_fw_words(t->cfg.log_cap);
     bl.fy = bl.fx + batch_fw_words(t->cfg.log_cap);
+    bl.ft = reinterpret_cast<uint32_t *>(bl.fy + batch_fw_words(t->cfg.log_cap));
     if (++t->epoch > batch_max_epoch()) {  // round tags would wrap: start the F words over
         HIP_TRY(hipMemsetAsync(t->d_fw, 0xFF, 8 * batch_fw_words(t->cfg.log_cap), s));
         t->epoch = 1;

@@ -134,12 +134,13 @@ constexpr unsigned long long kXHasB = 1ull << 23;
 // covers the group membership G completes the write (op buffer index := EMPTY, INVALID_WRITE ->
 // INVALID, WRITE/REPLAY -> VALID, the read_write_op slot completes; LAST_ACK_SUCCESS from WRITE or
 // REPLAY). The ACKs never change the timestamp they match against, so with T[s] = the first
-// matching element of sender s and N = G minus the bits already set, that element is
+// matching element of sender s (s < 8) and N = G minus the bits already set, that element is
 //   j* = max over s in N of T[s] (none if some T[s] is missing), or the first matching element
-//        of any sender (F) when N is empty.
+//        of any sender when N is empty (min of the T[s] and F, the first match from a sender >= 8).
+// Without a completion the applier is the first match of a sender < 8 (only those set bits).
 // ack_bv ends as ack_bv | the bits of the senders whose T[s] <= j* (every T[s] without a
-// completion). Opcodes: ACK_SUCCESS (a LAST_ACK_SUCCESS input stays), LAST_ACK_SUCCESS for j*
-// from WRITE or REPLAY. k_lookup finishes the non-matching elements, sets T (as max of ~i) and F
+// completion). Opcodes: ACK_SUCCESS (a LAST_ACK_SUCCESS input stays, except at j*),
+// LAST_ACK_SUCCESS for j* from WRITE or REPLAY. k_lookup finishes the non-matching elements, sets T (as max of ~i) and F
 // and caches each matching element's ack_bv / state / op buffer index in pf; in k_ack_resolve
 // j* (or, without a completion, F) applies the key's meta; k_ack_clear zeroes T.
 enum : uint8_t { kAkMatch = 1, kAkApply = 2 };
@@ -419,8 +420,11 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                 } else {
                     ifl = kAkMatch;
                     const uint32_t w = fw_index(a, phys[k]);
-                    offer(a.fw + w, a.rtag0, (uint32_t)gi[k]);
                     const uint8_t snd = (uint8_t)(hdr[k] >> 8);
+                    // F: the first match of a sender without a T word, or of any sender when the
+                    // quorum is complete already (the first match then completes)
+                    if (snd >= 8 || (uint8_t)(a.g_membership & ~m_ack_bv(m0[k])) == 0)
+                        offer(a.fw + w, a.rtag0, (uint32_t)gi[k]);
                     if (snd < 8) {
                         uint32_t *t = a.ft + (size_t)w * 8 + snd;
                         const uint32_t tv = 0xFFFFFFFFu - (uint32_t)gi[k];
@@ -622,10 +626,16 @@ __global__ __launch_bounds__(256) void k_ack_resolve(BatchArgs a)
     const uint4 t0 = tp[0], t1 = tp[1];
     const uint32_t tv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
     const uint8_t need = (uint8_t)(a.g_membership & ~bv0);
-    const uint32_t f = first_cand(a.fw[w], a.rtag0);
+    // the first match of senders 0..7 (min T), and of any sender (with F; F is offered only by
+    // matches from senders >= 8, or by every match when need is empty)
+    uint32_t f = kNone;
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+        if (tv[s] != 0) f = min(f, 0xFFFFFFFFu - tv[s]);
+    const uint32_t f_any = min(f, first_cand(a.fw[w], a.rtag0));
     uint32_t js = kNone;  // j*
     if (need == 0) {
-        js = f;
+        js = f_any;
     } else {
         uint32_t mx = 0;
         bool all = true;
@@ -640,7 +650,9 @@ __global__ __launch_bounds__(256) void k_ack_resolve(BatchArgs a)
     uint8_t *x = a.elems + i * a.esz;
     const bool done = (uint32_t)i == js;
     const bool wr = st0 == kWrite || st0 == kReplay;
-    x[8] = done && wr ? kLastAckSuccess : ack_opcode(x[8]);
+    // j* overwrites the opcode (LAST_ACK_SUCCESS, or LAST_ACK_NO_BCAST -> ACK_SUCCESS), even a
+    // LAST_ACK_SUCCESS input; the others keep a LAST_ACK_SUCCESS input
+    x[8] = done ? (wr ? kLastAckSuccess : kAckSuccess) : ack_opcode(x[8]);
     if (!(done || (js == kNone && (uint32_t)i == f))) return;
     // the applier: ack_bv, and with a completion the state, op buffer index and read_write_op
     uint8_t bv = bv0;

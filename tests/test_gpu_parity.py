@@ -419,3 +419,52 @@ def test_inv_direct_path_edge_cases():
         _run_both(g, o, L.BatchType.vals, val, val_o, mb, 8, 250, None)
         assert_elems_equal(val, val_o, f"round {rnd} vals")
     del e
+
+
+def test_ack_direct_path_edge_cases():
+    """The ACK direct path (non-RMW ACK launches: T/F words, k_ack_resolve, k_ack_clear) against the
+    oracle: ACKs matching each key's pending write or not, duplicate and out-of-range (>= 8)
+    senders, quorums reached at different elements or never, LAST_ACK_* input opcodes, a
+    membership with a dropped node, ragged counts and read_write_ops completions."""
+    g, o, sizes = make_pair(2000, 1024, 1 << 17)
+    keys = gen_keys(2000)
+    rng = np.random.default_rng(515151)
+    tsp = gen.TsPool(rng)
+    W, S, M = 10, 250, 400
+    for rnd in range(6):
+        mb = L.membership(5, 0) if rnd < 4 else L.membership(5, 0, alive=0b10111)
+        pool = gen.key_pool(rng, keys, hot=16 if rnd % 2 else 300)
+        loc = gen.local_ops(rng, pool, W * S, sizes, False, tsp)     # pending writes / replays
+        loc_o = gen.bytecopy(loc)
+        _run_both(g, o, L.BatchType.local_ops, loc, loc_o, mb, W, S, None)
+        assert_elems_equal(loc, loc_o, f"round {rnd} local")
+        rw_g, rw_o = gen.bytecopy(loc), gen.bytecopy(loc)
+        ack = np.zeros(W * M, dtype=L.msg_dtype())
+        ack["key"] = gen.draw_keys(rng, pool, W * M)
+        log = o.log_bytes()
+        lv = np.zeros(W * M, np.uint32)
+        lc = np.zeros(W * M, np.uint8)
+        for i, k in enumerate(ack["key"]):
+            off = o.lookup(int(k))
+            if off is not None:
+                lc[i] = log[off + 28]
+                lv[i] = int.from_bytes(bytes(log[off + 29:off + 33]), "little")
+        match = rng.random(W * M) < 0.7
+        ack["ts_ver"] = np.where(match, lv, lv + 2)
+        ack["ts_cid"] = np.where(match, lc, rng.integers(0, 5, size=W * M))
+        ack["sender"] = rng.choice(10, size=W * M, p=[0.22, 0.22, 0.22, 0.12, 0.1, 0.04, 0.02, 0.02, 0.02, 0.02])
+        ack["opcode"] = rng.choice([int(L.Op.ACK), int(L.Resp.LAST_ACK_SUCCESS),
+                                    int(L.Resp.LAST_ACK_NO_BCAST_SUCCESS), int(L.Resp.ACK_SUCCESS)],
+                                   size=W * M, p=[0.8, 0.1, 0.05, 0.05])
+        counts = rng.integers(M // 3, M + 1, size=W).astype(np.int32)
+        ack_o = gen.bytecopy(ack)
+        _run_both(g, o, L.BatchType.acks, ack, ack_o, mb, W, M, counts, rw_g, rw_o, rw_stride=S)
+        assert_elems_equal(ack, ack_o, f"round {rnd} acks")
+        assert_elems_equal(rw_g, rw_o, f"round {rnd} acks rw")
+        assert_tables_equal(g, o, f"round {rnd} acks")
+        live = np.concatenate([np.arange(b * M, b * M + counts[b]) for b in range(W)])
+        assert (ack["opcode"][live] == int(L.Resp.LAST_ACK_SUCCESS)).sum() > 0
+        val = gen.vals(rng, pool, W * S, sizes, False, tsp)
+        val_o = gen.bytecopy(val)
+        _run_both(g, o, L.BatchType.vals, val, val_o, mb, W, S, None)
+        assert_elems_equal(val, val_o, f"round {rnd} vals")

@@ -361,6 +361,99 @@ __global__ void k_marshal_vals(uint8_t *acks, int64_t n, uint32_t ack_size, uint
     if (oc == kLastAckSuccess || oc == kAckSuccess || oc == kOpMembChange) x[8] = kEmpty;
 }
 
+// ---- packed slabs (replica groups): one contiguous slab per rank instead of [W][C] rows
+// exclusive prefix of counts[0..n) into off[0..n], off[n] = the total (one workgroup)
+__global__ __launch_bounds__(1024) void k_scan_counts(const int32_t *counts, int32_t n, int32_t *off)
+{
+    __shared__ int32_t part[1024];
+    const int t = threadIdx.x;
+    const int per = (n + 1023) / 1024;
+    const int lo = t * per, hi = min(n, lo + per);
+    int32_t sum = 0;
+    for (int k = lo; k < hi; ++k) sum += counts[k];
+    part[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan of the per-thread sums
+        const int32_t v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int32_t run = part[t] - sum;
+    for (int k = lo; k < hi; ++k) {
+        off[k] = run;
+        run += counts[k];
+    }
+    if (t == 1023) off[n] = part[1023];
+}
+
+// rows [W][C] x esz with counts[W] -> packed[off[w] ..], one workgroup per row
+__global__ __launch_bounds__(256) void k_pack_rows(const uint8_t *rows, const int32_t *counts, const int32_t *off,
+                                                   int32_t C, uint32_t esz, uint8_t *packed)
+{
+    const int w = blockIdx.x;
+    const int words = (int)((uint32_t)counts[w] * esz / 8u);
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(rows + (int64_t)w * C * esz);
+    uint64_t *dst = reinterpret_cast<uint64_t *>(packed + (int64_t)off[w] * esz);
+    for (int k = threadIdx.x; k < words; k += 256) dst[k] = src[k];
+}
+
+// ACKs in the positions of the received INVs ([rows][width], counts[rows]): an ACK (or, with
+// RMWs, an INV-abort) where the INV applied, ST_EMPTY elsewhere (also past the row's count),
+// so row r of the output lines up with the packed INV slab its coordinator sent
+__global__ void k_marshal_acks_aligned(uint8_t *invs, const int32_t *counts, int32_t width, int64_t n,
+                                       uint32_t op_size, uint8_t *out, uint32_t ack_size, uint32_t machine_id)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint8_t *y = out + i * ack_size;
+    if ((int32_t)(i % width) >= counts[i / width]) {
+        y[8] = kEmpty;
+        return;
+    }
+    uint8_t *x = invs + i * op_size;
+    const W16 h = *reinterpret_cast<const W16 *>(x);
+    const uint8_t oc = (uint8_t)h.b;
+    if (oc == kInvSuccess || (oc == kOpInvAbort && ack_size >= op_size)) {
+        *reinterpret_cast<W16 *>(y) =
+            W16{h.a, with_op_state(h.b, oc == kInvSuccess ? kOpAck : kOpInvAbort, (uint8_t)machine_id)};
+        if (oc != kInvSuccess)
+            for (uint32_t k = 16; k < op_size; k += 8)
+                *reinterpret_cast<uint64_t *>(y + k) = *reinterpret_cast<const uint64_t *>(x + k);
+    } else {
+        y[8] = kEmpty;
+    }
+    if (oc == kInvSuccess || oc == kOpInvAbort || oc == kOpMembChange) x[8] = kEmpty;
+}
+
+// The ACKs returned to this coordinator ([n_peers][width], row p from peer p, lined up with the
+// packed INV slab it sent: worker w's INVs at off[w] .. off[w] + count[w]) -> per-worker ACK
+// batches [W][out_stride]: the peers' ACKs back to back in peer order, ST_EMPTY slots dropped
+__global__ __launch_bounds__(256) void k_regroup_aligned(const uint8_t *in, int32_t n_peers, int32_t width,
+                                                         const int32_t *off, const int32_t *count, uint32_t esz,
+                                                         uint8_t *out, int32_t out_stride, int32_t *out_count)
+{
+    const int w = blockIdx.x;
+    const int n = count[w];
+    int base = 0;
+    for (int p = 0; p < n_peers; ++p) {
+        for (int j0 = 0; j0 < n; j0 += 256) {
+            const int j = j0 + (int)threadIdx.x;
+            const uint8_t *x = in + ((int64_t)p * width + off[w] + j) * esz;
+            const bool keep = j < n && x[8] != kEmpty;
+            int total;
+            const int rank = block_rank(keep, total);
+            if (keep && base + rank < out_stride) {
+                uint8_t *y = out + ((int64_t)w * out_stride + base + rank) * esz;
+                for (uint32_t k = 0; k < esz; k += 8)
+                    *reinterpret_cast<uint64_t *>(y + k) = *reinterpret_cast<const uint64_t *>(x + k);
+            }
+            base += total;
+        }
+    }
+    if (threadIdx.x == 0) out_count[w] = base < out_stride ? base : out_stride;
+}
+
 __global__ void k_gen_remote(uint8_t *invs, uint8_t *vals, int32_t per_peer, const uint8_t *peers, int32_t n_peers,
                              uint32_t op_size, uint32_t st_value, uint32_t shift, hkv_zipf z, uint32_t clock,
                              uint64_t seed, int64_t total)
@@ -509,6 +602,39 @@ int hkv_wl_collect_vals(uint8_t *acks, const int32_t *count, int32_t n_workers, 
     if (C <= 0 || ack_size % 8) return -1;
     hipLaunchKernelGGL(k_collect_vals, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, acks, count, stride,
                        ack_size, out, C, out_count, machine_id, held);
+    return ok();
+}
+
+int hkv_wl_pack_rows(const uint8_t *rows, const int32_t *counts, int32_t n_rows, int32_t C, uint32_t elem_size,
+                     uint8_t *packed, int32_t *offsets, void *stream)
+{
+    if (n_rows <= 0) return 0;
+    if (C <= 0 || elem_size % 8) return -1;
+    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, (hipStream_t)stream, counts, n_rows, offsets);
+    hipLaunchKernelGGL(k_pack_rows, dim3(n_rows), dim3(256), 0, (hipStream_t)stream, rows, counts, offsets, C,
+                       elem_size, packed);
+    return ok();
+}
+
+int hkv_wl_marshal_acks_aligned(uint8_t *invs, const int32_t *counts, int32_t rows, int32_t width, uint32_t op_size,
+                                uint8_t *out, uint32_t ack_size, uint32_t machine_id, void *stream)
+{
+    const int64_t n = (int64_t)rows * width;
+    if (n <= 0) return 0;
+    if (op_size % 8 || ack_size % 8) return -1;
+    hipLaunchKernelGGL(k_marshal_acks_aligned, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, invs, counts,
+                       width, n, op_size, out, ack_size, machine_id);
+    return ok();
+}
+
+int hkv_wl_regroup_aligned(const uint8_t *in, int32_t n_peers, int32_t width, const int32_t *offsets,
+                           const int32_t *counts, int32_t n_workers, uint32_t elem_size, uint8_t *out,
+                           int32_t out_stride, int32_t *out_count, void *stream)
+{
+    if (n_workers <= 0) return 0;
+    if (n_peers <= 0 || width <= 0 || elem_size % 8) return -1;
+    hipLaunchKernelGGL(k_regroup_aligned, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, in, n_peers, width,
+                       offsets, counts, elem_size, out, out_stride, out_count);
     return ok();
 }
 

@@ -2,22 +2,28 @@
 
 Hermes replicates every key on every node, so N GPUs form an N-replica group (N <= 8: the
 membership bit vectors are 8 bits wide, spacetime.h:188-195). The wings RDMA layer
-(wings.h:770-916) becomes three collectives per protocol round, on torch's current stream so
-they order with the batch kernels without host synchronisation:
+(wings.h:770-916) becomes three data collectives per protocol round, on torch's current stream:
 
-  1. all-gather of fixed-capacity INV slabs: worker w of every replica sends at most C INVs
-     per round (C = the send credits, sized so a round's writes fit); [N][W][C] x op_size
-  2. every replica applies its peers' INVs as one INV batch launch (n_batches = N*W, its own
-     row masked out by a zero count), then ACKs (INV-aborts with RMWs) go back to the
-     coordinators with an all-to-all: row p of the ACK slab holds rank p's ACKs
-  3. coordinators regroup the ACKs per worker (one receive poll over all peers), apply them as
-     an ACK batch against the worker's op buffer (read_write_ops), and all-gather the VALs of
-     the writes that completed; every replica applies its peers' VALs as one VAL batch.
+  1. every replica packs the round's INVs (at most C per worker: the send credits) into one
+     contiguous slab, worker after worker; the totals are all-gathered and the host reads the
+     largest, the round's width (the one host synchronisation of a round). The INV slabs are
+     all-gathered as [N][width] x op_size
+  2. every replica applies its peers' INVs as one INV batch launch of N batches (one per peer,
+     its own masked out by a zero count); the ACKs (INV-aborts with RMWs) are written in the
+     positions of the INVs they answer and go back to the coordinators with an all-to-all:
+     row p of the ACK slab holds rank p's ACKs, lined up with the slab rank p sent
+  3. coordinators regroup the ACKs per worker through their own packing offsets (one receive
+     poll over all peers), apply them as an ACK batch against the worker's op buffer
+     (read_write_ops), pack the VALs of the writes that completed and all-gather them at the
+     same width (a round completes at most the writes it INV'd); every replica applies its
+     peers' VALs as one VAL batch.
 
-Per-worker counts travel with each slab in a second (small) collective. `ReplicaRound` holds
-one replica's buffers and phases; `ReplicaGroupRound` drives one replica per process over
-torch.distributed (RCCL); `LoopbackGroup` drives N replicas in one process (tests: the same
-phases and kernels, with the collectives done by tensor copies).
+Packed slabs carry what a round sends, not the credits' worst case: at 20 % writes about 24 INVs
+per worker go out, against C = 104 slots, so the collectives and the INV/VAL launches are about
+4x smaller than with [N][W][C] rows. `ReplicaRound` holds one replica's buffers and phases;
+`ReplicaGroupRound` drives one replica per process over torch.distributed (RCCL);
+`LoopbackGroup` drives N replicas in one process (tests: the same phases and kernels, with the
+collectives done by tensor copies).
 """
 from __future__ import annotations
 
@@ -38,6 +44,11 @@ _L.hkv_wl_regroup.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_i
                               ctypes.c_int32, _P, _P]
 _L.hkv_wl_collect_vals.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
                                    _P, ctypes.c_uint32, _P, _P]
+_L.hkv_wl_pack_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, _P]
+_L.hkv_wl_marshal_acks_aligned.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P,
+                                           ctypes.c_uint32, ctypes.c_uint32, _P]
+_L.hkv_wl_regroup_aligned.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_uint32,
+                                      _P, ctypes.c_int32, _P, _P]
 
 MAX_REPLICAS = 8
 LOCAL = 250  # MAX_BATCH_KVS_OPS_SIZE, config.h:42
@@ -65,20 +76,24 @@ class ReplicaRound:
         u8 = dict(dtype=torch.uint8, device=dev)
         i32 = dict(dtype=torch.int32, device=dev)
         self.ops = torch.zeros(W * LOCAL * self.op, **u8)
+        # outgoing INVs: [W][C] rows, then packed (worker w at inv_off[w]; inv_off[W] = total)
         self.inv_slab = torch.zeros(W * C * self.op, **u8)
         self.inv_count = torch.zeros(W, **i32)
+        self.inv_off = torch.zeros(W + 1, **i32)
+        self.inv_pack = torch.zeros(W * C * self.op, **u8)
+        self.inv_totals = torch.zeros(N, **i32)          # all ranks' INV totals (this round's width: max)
+        # receive buffers at the largest width (W * C); a round uses [N][width] of them
         self.inv_recv = torch.zeros(N * W * C * self.op, **u8)
-        self.inv_recv_count = torch.zeros(N * W, **i32)
         self.ack_slab = torch.zeros(N * W * C * self.ack_size, **u8)
-        self.ack_slab_count = torch.zeros(N * W, **i32)
         self.ack_recv = torch.zeros(N * W * C * self.ack_size, **u8)
-        self.ack_recv_count = torch.zeros(N * W, **i32)
         self.ack_batch = torch.zeros(W * N * C * self.ack_size, **u8)
         self.ack_batch_count = torch.zeros(W, **i32)
         self.val_slab = torch.zeros(W * C * L.OP_META_SIZE, **u8)
         self.val_count = torch.zeros(W, **i32)
+        self.val_off = torch.zeros(W + 1, **i32)
+        self.val_pack = torch.zeros(W * C * L.OP_META_SIZE, **u8)
+        self.val_totals = torch.zeros(N, **i32)
         self.val_recv = torch.zeros(N * W * C * L.OP_META_SIZE, **u8)
-        self.val_recv_count = torch.zeros(N * W, **i32)
         self.held = torch.zeros(2, dtype=torch.int64, device=dev)    # INVs held back, VALs dropped
         self.cursor = torch.zeros(W, **i32)
         self.counters = torch.zeros(4096, dtype=torch.int64, device=dev)  # HKV_WL_COUNTER_WORDS
@@ -100,34 +115,51 @@ class ReplicaRound:
                                self.rank, int(first), int(not self.retry), _ptr(self.counters), _s()), "refill")
 
     def local(self):
-        """Local batch, then this round's INVs into the outgoing slab (inv_slab, inv_count)."""
+        """Local batch, then this round's INVs, packed (inv_pack; worker w at inv_off[w])."""
         self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, LOCAL, self.op, self.mb)
         check(_L.hkv_wl_marshal_invs_cap(_ptr(self.ops), self.W, LOCAL, self.op, _ptr(self.inv_slab), self.C,
                                          _ptr(self.inv_count), self.rank, _ptr(self.held), _s()), "marshal_invs")
+        check(_L.hkv_wl_pack_rows(_ptr(self.inv_slab), _ptr(self.inv_count), self.W, self.C, self.op,
+                                  _ptr(self.inv_pack), _ptr(self.inv_off), _s()), "pack invs")
         if self.count_elems:
-            self.inv_total += self.inv_count.sum()
+            self.inv_total += self.inv_off[self.W]
 
-    def _own_row(self, counts: torch.Tensor) -> torch.Tensor:
-        return counts[self.rank * self.W:(self.rank + 1) * self.W]
+    # -- the slabs each collective moves: (receive, send) views at the round's width
+    def inv_total_io(self):
+        return self.inv_totals, self.inv_off[self.W:]
 
-    def invs(self):
-        """Apply the gathered INVs of the peers (inv_recv [N][W][C], inv_recv_count [N][W]);
-        their ACKs go to ack_slab row p (for rank p), counts in ack_slab_count."""
-        self._own_row(self.inv_recv_count).zero_()
+    def inv_io(self, width: int):
+        n = width * self.op
+        return self.inv_recv[:self.N * n], self.inv_pack[:n]
+
+    def ack_io(self, width: int):
+        n = self.N * width * self.ack_size
+        return self.ack_recv[:n], self.ack_slab[:n]
+
+    def val_total_io(self):
+        return self.val_totals, self.val_off[self.W:]
+
+    def val_io(self, width: int):
+        n = width * L.OP_META_SIZE
+        return self.val_recv[:self.N * n], self.val_pack[:n]
+
+    def invs(self, width: int):
+        """Apply the gathered INVs of the peers ([N][width], row p: inv_totals[p] INVs) as N
+        batches; their ACKs go into ack_slab in the positions of the INVs they answer."""
+        self.inv_totals[self.rank] = 0
         if self.count_elems:
-            self.elem_totals[0] += self.inv_recv_count.sum()
-        self.kvs.batch(L.BatchType.invs, self.inv_recv, self.N * self.W, self.C, self.op, self.mb,
-                       counts=self.inv_recv_count)
-        check(_L.hkv_wl_marshal_acks_rows(_ptr(self.inv_recv), _ptr(self.inv_recv_count), self.N * self.W, self.C,
-                                          self.op, _ptr(self.ack_slab), self.ack_size, _ptr(self.ack_slab_count),
-                                          self.rank, _s()), "marshal_acks")
+            self.elem_totals[0] += self.inv_totals.sum()
+        self.kvs.batch(L.BatchType.invs, self.inv_recv, self.N, width, self.op, self.mb, counts=self.inv_totals)
+        check(_L.hkv_wl_marshal_acks_aligned(_ptr(self.inv_recv), _ptr(self.inv_totals), self.N, width, self.op,
+                                             _ptr(self.ack_slab), self.ack_size, self.rank, _s()), "marshal_acks")
 
-    def acks(self):
-        """Apply the ACKs returned by the peers (ack_recv [N][W][C] from rank p in row p),
-        regrouped per worker; VALs of completed writes into val_slab / val_count."""
+    def acks(self, width: int):
+        """Apply the ACKs returned by the peers (ack_recv [N][width], row p from rank p, lined up
+        with inv_pack), regrouped per worker; the VALs of completed writes, packed (val_pack)."""
         N, W, C = self.N, self.W, self.C
-        check(_L.hkv_wl_regroup(_ptr(self.ack_recv), _ptr(self.ack_recv_count), N, W, C, self.ack_size,
-                                _ptr(self.ack_batch), N * C, _ptr(self.ack_batch_count), _s()), "regroup")
+        check(_L.hkv_wl_regroup_aligned(_ptr(self.ack_recv), N, width, _ptr(self.inv_off), _ptr(self.inv_count), W,
+                                        self.ack_size, _ptr(self.ack_batch), N * C, _ptr(self.ack_batch_count),
+                                        _s()), "regroup")
         if self.count_elems:
             self.elem_totals[1] += self.ack_batch_count.sum()
         self.kvs.batch(L.BatchType.acks, self.ack_batch, W, N * C, self.ack_size, self.mb,
@@ -135,14 +167,16 @@ class ReplicaRound:
         check(_L.hkv_wl_collect_vals(_ptr(self.ack_batch), _ptr(self.ack_batch_count), W, N * C, self.ack_size,
                                      _ptr(self.val_slab), C, _ptr(self.val_count), self.rank,
                                      _ptr(self.held[1:]), _s()), "collect_vals")
+        check(_L.hkv_wl_pack_rows(_ptr(self.val_slab), _ptr(self.val_count), W, C, L.OP_META_SIZE,
+                                  _ptr(self.val_pack), _ptr(self.val_off), _s()), "pack vals")
 
-    def vals(self):
-        """Apply the gathered VALs of the peers (val_recv [N][W][C], val_recv_count [N][W])."""
-        self._own_row(self.val_recv_count).zero_()
+    def vals(self, width: int):
+        """Apply the gathered VALs of the peers ([N][width], row p: val_totals[p] VALs)."""
+        self.val_totals[self.rank] = 0
         if self.count_elems:
-            self.elem_totals[2] += self.val_recv_count.sum()
-        self.kvs.batch(L.BatchType.vals, self.val_recv, self.N * self.W, self.C, L.OP_META_SIZE, self.mb,
-                       counts=self.val_recv_count)
+            self.elem_totals[2] += self.val_totals.sum()
+        self.kvs.batch(L.BatchType.vals, self.val_recv, self.N, width, L.OP_META_SIZE, self.mb,
+                       counts=self.val_totals)
 
     def stats(self) -> dict:
         c = self.counters[:3].cpu().tolist()
@@ -198,15 +232,15 @@ class ReplicaGroupRound:
     def step(self, events: dict | None = None, timed_batches=None):
         r = self.r
         _timed(events, "local", r.local, timed_batches)
-        self._gather(r.inv_recv, r.inv_slab)
-        self._gather(r.inv_recv_count, r.inv_count)
-        _timed(events, "invs", r.invs, timed_batches)
-        self._a2a(r.ack_recv, r.ack_slab)
-        self._a2a(r.ack_recv_count, r.ack_slab_count)
-        _timed(events, "acks", r.acks, timed_batches)
-        self._gather(r.val_recv, r.val_slab)
-        self._gather(r.val_recv_count, r.val_count)
-        _timed(events, "vals", r.vals, timed_batches)
+        self._gather(*r.inv_total_io())
+        width = max(1, int(r.inv_total_io()[0].max().item()))  # the round's one host synchronisation
+        self._gather(*r.inv_io(width))
+        _timed(events, "invs", lambda: r.invs(width), timed_batches)
+        self._a2a(*r.ack_io(width))
+        _timed(events, "acks", lambda: r.acks(width), timed_batches)
+        self._gather(*r.val_total_io())
+        self._gather(*r.val_io(width))
+        _timed(events, "vals", lambda: r.vals(width), timed_batches)
         r.refill()
 
     def stats(self) -> dict:
@@ -234,21 +268,27 @@ class LoopbackGroup:
             for p, x in enumerate(ins):
                 ov[p].copy_(x.view(N, -1)[q])
 
+    def _gather_io(self, ios):
+        self._gather([o for o, _ in ios], [i for _, i in ios])
+
+    def _a2a_io(self, ios):
+        self._a2a([o for o, _ in ios], [i for _, i in ios])
+
     def step(self):
         rs = self.rounds
         for r in rs:
             r.local()
-        self._gather([r.inv_recv for r in rs], [r.inv_slab for r in rs])
-        self._gather([r.inv_recv_count for r in rs], [r.inv_count for r in rs])
+        self._gather_io([r.inv_total_io() for r in rs])
+        width = max(1, max(int(r.inv_total_io()[0].max().item()) for r in rs))
+        self._gather_io([r.inv_io(width) for r in rs])
         for r in rs:
-            r.invs()
-        self._a2a([r.ack_recv for r in rs], [r.ack_slab for r in rs])
-        self._a2a([r.ack_recv_count for r in rs], [r.ack_slab_count for r in rs])
+            r.invs(width)
+        self._a2a_io([r.ack_io(width) for r in rs])
         for r in rs:
-            r.acks()
-        self._gather([r.val_recv for r in rs], [r.val_slab for r in rs])
-        self._gather([r.val_recv_count for r in rs], [r.val_count for r in rs])
+            r.acks(width)
+        self._gather_io([r.val_total_io() for r in rs])
+        self._gather_io([r.val_io(width) for r in rs])
         for r in rs:
-            r.vals()
+            r.vals(width)
         for r in rs:
             r.refill()

@@ -115,6 +115,26 @@ int hkv_wl_collect_vals(uint8_t *d_acks, const int32_t *d_count, int32_t n_worke
                         uint32_t ack_size, uint8_t *d_val_out, int32_t C, int32_t *d_val_count,
                         uint32_t machine_id, unsigned long long *d_held, void *stream);
 
+/* Packed slabs of a replica group (one contiguous slab per rank instead of [W][C] rows):
+ * rows [n_rows][C] x elem_size with d_counts[n_rows] -> d_packed, row w at d_offsets[w];
+ * d_offsets[n_rows] = the total (d_offsets has n_rows + 1 entries) */
+int hkv_wl_pack_rows(const uint8_t *d_rows, const int32_t *d_counts, int32_t n_rows, int32_t C,
+                     uint32_t elem_size, uint8_t *d_packed, int32_t *d_offsets, void *stream);
+
+/* ACKs for received packed INV slabs ([rows][width], d_counts[rows] live per row), element i of
+ * the output in the position of INV i: an ACK (with RMWs an INV-abort) where it applied,
+ * ST_EMPTY elsewhere; the INVs become ST_EMPTY as in hkv_wl_marshal_acks */
+int hkv_wl_marshal_acks_aligned(uint8_t *d_invs, const int32_t *d_counts, int32_t rows, int32_t width,
+                                uint32_t op_size, uint8_t *d_ack_out, uint32_t ack_size, uint32_t machine_id,
+                                void *stream);
+
+/* ACK rows returned by the peers ([n_peers][width], lined up with the packed INV slab this
+ * coordinator sent: worker w's INVs at d_offsets[w], d_counts[w] of them) -> per-worker ACK
+ * batches [n_workers][out_stride], ST_EMPTY elements dropped, counts in d_out_count */
+int hkv_wl_regroup_aligned(const uint8_t *d_in, int32_t n_peers, int32_t width, const int32_t *d_offsets,
+                           const int32_t *d_counts, int32_t n_workers, uint32_t elem_size, uint8_t *d_out,
+                           int32_t out_stride, int32_t *d_out_count, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,8 +1,9 @@
 """The replica-group exchange choreography over torch.distributed, on CPU with gloo
 (world_size 2 and 3): ReplicaGroupRound.step() and LoopbackGroup.step() drive a stand-in
-replica whose phases tag every slab element with (origin rank, worker, slot) and check, in the
-next phase, that each element arrived in the row and slot the kernels assume
-(all-gather: row p = rank p's slab; all-to-all: row p = what rank p addressed to this rank).
+replica whose phases tag every packed-slab element with (origin rank, worker, slot) and check, in
+the next phase, that each element arrived in the row and position the kernels assume
+(all-gather at the round's width: row p = rank p's packed slab; all-to-all: row p = what rank p
+addressed to this rank, in the positions of the INVs it answers).
 The HIP phases themselves run in tests/test_replica_group_gpu.py."""
 import os
 import socket
@@ -20,79 +21,97 @@ def _tag(kind, a, b, w, j):
 
 
 class TagReplica:
-    """Stand-in for ReplicaRound with the same tensors (int64 tags for bytes)."""
+    """Stand-in for ReplicaRound with the same exchange interface (int64 tags for elements)."""
 
     def __init__(self, world, rank, W=5, C=7):
         self.N, self.rank, self.W, self.C = world, rank, W, C
         N = world
         z = lambda *s: torch.zeros(*s, dtype=torch.int64)  # noqa: E731
         zi = lambda *s: torch.zeros(*s, dtype=torch.int32)  # noqa: E731
-        self.inv_slab, self.inv_count = z(W * C), zi(W)
-        self.inv_recv, self.inv_recv_count = z(N * W * C), zi(N * W)
-        self.ack_slab, self.ack_slab_count = z(N * W * C), zi(N * W)
-        self.ack_recv, self.ack_recv_count = z(N * W * C), zi(N * W)
-        self.val_slab, self.val_count = z(W * C), zi(W)
-        self.val_recv, self.val_recv_count = z(N * W * C), zi(N * W)
+        self.inv_pack, self.inv_off, self.inv_totals = z(W * C), zi(W + 1), zi(N)
+        self.inv_recv = z(N * W * C)
+        self.ack_slab, self.ack_recv = z(N * W * C), z(N * W * C)
+        self.val_pack, self.val_off, self.val_totals = z(W * C), zi(W + 1), zi(N)
+        self.val_recv = z(N * W * C)
         self.counters = z(4)
         self.inv_total = z(1)
         self.elem_totals = z(3)
+        self.count_elems = True
         self.checked = 0
         self.round = 0
 
     def count(self, origin, w):
         return (origin + w + self.round) % self.C
 
-    def local(self):
-        v = self.inv_slab.view(self.W, self.C)
-        v.fill_(-1)
+    def _pack(self, slab, off, kind):
+        k = 0
         for w in range(self.W):
-            n = self.count(self.rank, w)
-            self.inv_count[w] = n
-            for j in range(n):
-                v[w, j] = _tag(1, self.rank, 0, w, j)
+            off[w] = k
+            for j in range(self.count(self.rank, w)):
+                slab[k] = _tag(kind, self.rank, 0, w, j)
+                k += 1
+        off[self.W] = k
 
-    def invs(self):
-        N, W, C = self.N, self.W, self.C
-        rv, rc = self.inv_recv.view(N, W, C), self.inv_recv_count.view(N, W)
-        av, ac = self.ack_slab.view(N, W, C), self.ack_slab_count.view(N, W)
-        rc[self.rank].zero_()
-        for p in range(N):
-            for w in range(W):
-                n = int(rc[p, w])
-                assert n == (0 if p == self.rank else self.count(p, w))
-                for j in range(n):
-                    assert int(rv[p, w, j]) == _tag(1, p, 0, w, j)
-                    av[p, w, j] = _tag(2, self.rank, p, w, j)   # ACK from me to coordinator p
-                    self.checked += 1
-                ac[p, w] = n
+    def _rows(self, origin):
+        """(w, j) of origin's packed slab, in order"""
+        return [(w, j) for w in range(self.W) for j in range(self.count(origin, w))]
 
-    def acks(self):
-        N, W, C = self.N, self.W, self.C
-        rv, rc = self.ack_recv.view(N, W, C), self.ack_recv_count.view(N, W)
-        vv = self.val_slab.view(W, C)
-        for p in range(N):
-            for w in range(W):
-                n = int(rc[p, w])
-                assert n == (0 if p == self.rank else self.count(self.rank, w))
-                for j in range(n):
-                    assert int(rv[p, w, j]) == _tag(2, p, self.rank, w, j)
-                    self.checked += 1
-        for w in range(W):
-            n = self.count(self.rank, w)
-            self.val_count[w] = n
-            for j in range(n):
-                vv[w, j] = _tag(3, self.rank, 0, w, j)
+    def local(self):
+        self._pack(self.inv_pack, self.inv_off, 1)
 
-    def vals(self):
-        N, W, C = self.N, self.W, self.C
-        rv, rc = self.val_recv.view(N, W, C), self.val_recv_count.view(N, W)
-        rc[self.rank].zero_()
-        for p in range(N):
-            for w in range(W):
-                n = int(rc[p, w])
-                for j in range(n):
-                    assert int(rv[p, w, j]) == _tag(3, p, 0, w, j)
+    def inv_total_io(self):
+        return self.inv_totals, self.inv_off[self.W:]
+
+    def inv_io(self, width):
+        return self.inv_recv[:self.N * width], self.inv_pack[:width]
+
+    def ack_io(self, width):
+        return self.ack_recv[:self.N * width], self.ack_slab[:self.N * width]
+
+    def val_total_io(self):
+        return self.val_totals, self.val_off[self.W:]
+
+    def val_io(self, width):
+        return self.val_recv[:self.N * width], self.val_pack[:width]
+
+    def invs(self, width):
+        self.inv_totals[self.rank] = 0
+        rv, av = self.inv_recv[:self.N * width].view(self.N, width), self.ack_slab[:self.N * width].view(self.N, width)
+        av.fill_(-1)                                     # ST_EMPTY where no ACK
+        for p in range(self.N):
+            n = int(self.inv_totals[p])
+            rows = self._rows(p)
+            assert n == (0 if p == self.rank else len(rows)) and len(rows) <= width
+            for k in range(n):
+                w, j = rows[k]
+                assert int(rv[p, k]) == _tag(1, p, 0, w, j)
+                av[p, k] = _tag(2, self.rank, p, w, j)   # ACK from me to coordinator p, INV's position
+                self.checked += 1
+
+    def acks(self, width):
+        rv = self.ack_recv[:self.N * width].view(self.N, width)
+        mine = self._rows(self.rank)
+        for p in range(self.N):
+            for k in range(width):
+                if p != self.rank and k < len(mine):
+                    w, j = mine[k]
+                    assert int(rv[p, k]) == _tag(2, p, self.rank, w, j)
                     self.checked += 1
+                else:
+                    assert int(rv[p, k]) == -1
+        self._pack(self.val_pack, self.val_off, 3)
+
+    def vals(self, width):
+        self.val_totals[self.rank] = 0
+        rv = self.val_recv[:self.N * width].view(self.N, width)
+        for p in range(self.N):
+            n = int(self.val_totals[p])
+            rows = self._rows(p)
+            assert n == (0 if p == self.rank else len(rows))
+            for k in range(n):
+                w, j = rows[k]
+                assert int(rv[p, k]) == _tag(3, p, 0, w, j)
+                self.checked += 1
 
     def refill(self):
         self.round += 1
@@ -136,7 +155,6 @@ def test_rccl_choreography_gloo(world):
     for rank, checked, err in res:
         assert err is None, f"rank {rank}: {err}"
         assert checked > 0
-
 
 
 def test_loopback_matches_choreography():

@@ -82,6 +82,7 @@ class ReplicaRound:
         self.inv_off = torch.zeros(W + 1, **i32)
         self.inv_pack = torch.zeros(W * C * self.op, **u8)
         self.inv_totals = torch.zeros(N, **i32)          # all ranks' INV totals (this round's width: max)
+        self.inv_maxc = torch.zeros(1, **i32)            # this rank's largest per-worker INV count
         # receive buffers at the largest width (W * C); a round uses [N][width] of them
         self.inv_recv = torch.zeros(N * W * C * self.op, **u8)
         self.ack_slab = torch.zeros(N * W * C * self.ack_size, **u8)
@@ -121,12 +122,20 @@ class ReplicaRound:
                                          _ptr(self.inv_count), self.rank, _ptr(self.held), _s()), "marshal_invs")
         check(_L.hkv_wl_pack_rows(_ptr(self.inv_slab), _ptr(self.inv_count), self.W, self.C, self.op,
                                   _ptr(self.inv_pack), _ptr(self.inv_off), _s()), "pack invs")
+        torch.amax(self.inv_count, dim=0, keepdim=True, out=self.inv_maxc)
         if self.count_elems:
             self.inv_total += self.inv_off[self.W]
 
     # -- the slabs each collective moves: (receive, send) views at the round's width
     def inv_total_io(self):
         return self.inv_totals, self.inv_off[self.W:]
+
+    def round_shape(self) -> tuple[int, int]:
+        """After the totals are gathered (host synchronisation): the round's width (the largest
+        INV total of any rank) and this rank's ACK batch stride ((N-1) x its largest per-worker
+        INV count: a worker gets at most one ACK per INV from every peer)."""
+        v = torch.cat([self.inv_totals.max().view(1), self.inv_maxc]).cpu().tolist()
+        return max(1, int(v[0])), max(1, (self.N - 1) * int(v[1]))
 
     def inv_io(self, width: int):
         n = width * self.op
@@ -153,18 +162,19 @@ class ReplicaRound:
         check(_L.hkv_wl_marshal_acks_aligned(_ptr(self.inv_recv), _ptr(self.inv_totals), self.N, width, self.op,
                                              _ptr(self.ack_slab), self.ack_size, self.rank, _s()), "marshal_acks")
 
-    def acks(self, width: int):
+    def acks(self, width: int, stride: int):
         """Apply the ACKs returned by the peers (ack_recv [N][width], row p from rank p, lined up
-        with inv_pack), regrouped per worker; the VALs of completed writes, packed (val_pack)."""
+        with inv_pack), regrouped per worker ([W][stride]); the VALs of completed writes, packed
+        (val_pack)."""
         N, W, C = self.N, self.W, self.C
         check(_L.hkv_wl_regroup_aligned(_ptr(self.ack_recv), N, width, _ptr(self.inv_off), _ptr(self.inv_count), W,
-                                        self.ack_size, _ptr(self.ack_batch), N * C, _ptr(self.ack_batch_count),
+                                        self.ack_size, _ptr(self.ack_batch), stride, _ptr(self.ack_batch_count),
                                         _s()), "regroup")
         if self.count_elems:
             self.elem_totals[1] += self.ack_batch_count.sum()
-        self.kvs.batch(L.BatchType.acks, self.ack_batch, W, N * C, self.ack_size, self.mb,
+        self.kvs.batch(L.BatchType.acks, self.ack_batch, W, stride, self.ack_size, self.mb,
                        counts=self.ack_batch_count, rw=self.ops, rw_stride_bytes=LOCAL * self.op)
-        check(_L.hkv_wl_collect_vals(_ptr(self.ack_batch), _ptr(self.ack_batch_count), W, N * C, self.ack_size,
+        check(_L.hkv_wl_collect_vals(_ptr(self.ack_batch), _ptr(self.ack_batch_count), W, stride, self.ack_size,
                                      _ptr(self.val_slab), C, _ptr(self.val_count), self.rank,
                                      _ptr(self.held[1:]), _s()), "collect_vals")
         check(_L.hkv_wl_pack_rows(_ptr(self.val_slab), _ptr(self.val_count), W, C, L.OP_META_SIZE,
@@ -233,11 +243,11 @@ class ReplicaGroupRound:
         r = self.r
         _timed(events, "local", r.local, timed_batches)
         self._gather(*r.inv_total_io())
-        width = max(1, int(r.inv_total_io()[0].max().item()))  # the round's one host synchronisation
+        width, stride = r.round_shape()  # the round's one host synchronisation
         self._gather(*r.inv_io(width))
         _timed(events, "invs", lambda: r.invs(width), timed_batches)
         self._a2a(*r.ack_io(width))
-        _timed(events, "acks", lambda: r.acks(width), timed_batches)
+        _timed(events, "acks", lambda: r.acks(width, stride), timed_batches)
         self._gather(*r.val_total_io())
         self._gather(*r.val_io(width))
         _timed(events, "vals", lambda: r.vals(width), timed_batches)
@@ -279,13 +289,14 @@ class LoopbackGroup:
         for r in rs:
             r.local()
         self._gather_io([r.inv_total_io() for r in rs])
-        width = max(1, max(int(r.inv_total_io()[0].max().item()) for r in rs))
+        shapes = [r.round_shape() for r in rs]
+        width = shapes[0][0]                 # the same on every replica (max of the same totals)
         self._gather_io([r.inv_io(width) for r in rs])
         for r in rs:
             r.invs(width)
         self._a2a_io([r.ack_io(width) for r in rs])
-        for r in rs:
-            r.acks(width)
+        for r, (_, stride) in zip(rs, shapes):
+            r.acks(width, stride)
         self._gather_io([r.val_total_io() for r in rs])
         self._gather_io([r.val_io(width) for r in rs])
         for r in rs:

@@ -65,6 +65,9 @@ class TagReplica:
     def inv_io(self, width):
         return self.inv_recv[:self.N * width], self.inv_pack[:width]
 
+    def round_shape(self):
+        return max(1, int(self.inv_totals.max())), (self.N - 1) * self.C
+
     def ack_io(self, width):
         return self.ack_recv[:self.N * width], self.ack_slab[:self.N * width]
 
@@ -88,7 +91,7 @@ class TagReplica:
                 av[p, k] = _tag(2, self.rank, p, w, j)   # ACK from me to coordinator p, INV's position
                 self.checked += 1
 
-    def acks(self, width):
+    def acks(self, width, stride):
         rv = self.ack_recv[:self.N * width].view(self.N, width)
         mine = self._rows(self.rank)
         for p in range(self.N):

@@ -174,9 +174,19 @@ def main():
         "acks": n_ack * BYTES["ack"],
         "vals": n_val * BYTES["val"],
     }
-    dom = max(ms, key=ms.get) if ms else "local"
+    # the roofline is quoted on the local batch launch (configs[1]'s metric unit); the other
+    # launches are in batch_ms
+    dom = "local" if "local" in ms else (max(ms, key=ms.get) if ms else "local")
     ach = per_launch_bytes[dom] / (ms[dom] / 1e3) / 1e9 if ms else 0.0
     value = committed_all / elapsed_max
+    # HBM traffic of the local launch: rocprofv3 PMC passes of this bench (tools/pmc.sh,
+    # tools/pmc_local.py) are committed under profiles/; counters cannot be read in this run
+    traffic, traffic_src = None, None
+    pmc = os.path.join(ROOT, "profiles", "pmc_local_batch.json")
+    if world == 1 and dom == "local" and a.workers == 8192 and a.keys == 100_000_000 and os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f)["traffic_bytes"]
+        traffic_src = "profiles/pmc_local_batch.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, separate runs)"
     out = {
         "metric": "replicated KVS ops/s (reads+writes committed)",
         "value": value,
@@ -202,7 +212,8 @@ def main():
         "roofline": {
             "bound": "hbm", "kernel": f"{dom} batch launch (k_lookup + element-order rounds, hkv_batch.hip)",
             "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-            "traffic": None, "launch_ms": ms.get(dom), "algorithmic_bytes_per_launch": per_launch_bytes[dom],
+            "traffic": traffic, "traffic_source": traffic_src, "launch_ms": ms.get(dom),
+            "algorithmic_bytes_per_launch": per_launch_bytes[dom],
             "batch_ms": ms,
         },
         "detail": {

@@ -80,7 +80,6 @@ struct BatchArgs {
     int32_t ack_direct;          // ACK launch on the direct path (k_ack_resolve)
     uint8_t g_membership;
     uint8_t w_ack_init;
-    uint32_t var;                // experiment switches (HKV_VAR)
 };
 
 // Rounds after round 0 per batch type: how often a hot key usually mutates in one launch beyond
@@ -826,7 +825,7 @@ __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
     // one out instead of the exec functions' byte-wise global accesses. (A 56-B op costs more to
     // write back whole than the one or two bytes an INV changes.)
     extern __shared__ uint64_t sx[];
-    const bool kStage = SV == 31 && (a.esz <= 16 || (a.var & 1));
+    const bool kStage = SV == 31 && a.esz <= 16;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     bool left = false;
     if (i < a.n && a.st[i] == kStPend) {
@@ -1130,8 +1129,6 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.ack_direct = bl.type == kAcks && !bl.g.rmw_enabled && n < (int64_t)kNone;
     a.g_membership = bl.g_membership;
     a.w_ack_init = bl.w_ack_init;
-    static const uint32_t var = getenv("HKV_VAR") ? (uint32_t)atoi(getenv("HKV_VAR")) : 0u;
-    a.var = var;
     const unsigned grid = (unsigned)((n + 255) / 256);
     const unsigned cgrid = (unsigned)((n + 256 * kCandPer - 1) / (256 * kCandPer));
     const bool big = bl.esz > 64;

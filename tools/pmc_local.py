@@ -1,0 +1,53 @@
+"""HBM bytes per local batch launch from a tools/pmc.sh run (FETCH_SIZE and WRITE_SIZE passes):
+    python tools/pmc_local.py TAG OUT.json
+
+A local launch is the two k_lookup dispatches before a k_resolve0<0, ...> dispatch, that dispatch
+and the k_commit after it. Counters are KB per dispatch; FETCH_SIZE is doubled (on gfx950 it
+reports half the bytes of wide reads, MI355X_MICROARCH.md, HBM section). The median over the
+launches of the run is written to OUT.json, which bench.py reports as roofline.traffic."""
+import csv
+import json
+import statistics
+import sys
+
+
+def dispatches(path):
+    rows = {}
+    for r in csv.DictReader(open(path)):
+        rows[int(r["Dispatch_Id"])] = (r["Kernel_Name"], float(r["Counter_Value"]) * 1024.0)
+    return rows
+
+
+def local_launches(rows):
+    ids = sorted(rows)
+    out = []
+    for k, d in enumerate(ids):
+        if "k_resolve0<0," not in rows[d][0]:
+            continue
+        grp = [ids[k - 2], ids[k - 1], d, ids[k + 1]]
+        names = [rows[g][0] for g in grp]
+        if "k_lookup" in names[0] and "k_lookup" in names[1] and "k_commit" in names[3]:
+            out.append(grp)
+    return out
+
+
+def main():
+    tag, dst = sys.argv[1], sys.argv[2]
+    f = dispatches(f"gpurun_out/{tag}/pmc/FETCH_SIZE/run_counter_collection.csv")
+    w = dispatches(f"gpurun_out/{tag}/pmc/WRITE_SIZE/run_counter_collection.csv")
+    fl = [sum(2.0 * f[g][1] for g in grp) for grp in local_launches(f)]
+    wl = [sum(w[g][1] for g in grp) for grp in local_launches(w)]
+    res = {
+        "what": "HBM bytes per local batch launch (k_lookup x2, k_resolve0, k_commit), rocprofv3 --pmc "
+                "FETCH_SIZE (x2, gfx950) and WRITE_SIZE in separate passes of bench.py",
+        "launches": len(fl),
+        "fetch_bytes": statistics.median(fl),
+        "write_bytes": statistics.median(wl),
+    }
+    res["traffic_bytes"] = res["fetch_bytes"] + res["write_bytes"]
+    json.dump(res, open(dst, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -29,5 +29,7 @@ for (k, g), v in sorted(res.items(), key=key):
         m = sum(x) / len(x) if x else float("nan")
         if c in ("FETCH_SIZE", "WRITE_SIZE"):
             m /= 1024.0  # KB -> MB
+        if c == "FETCH_SIZE":
+            m *= 2.0     # gfx950: half the bytes of wide reads (128-B requests tallied at 64 B)
         vals.append(f"{m:14.1f}")
     print(f"{k[:40]:40s} {g:>9s} " + " ".join(vals))

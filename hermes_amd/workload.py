@@ -37,6 +37,8 @@ _L.hkv_wl_marshal_invs_cap.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctype
                                        ctypes.c_uint32, _P, _P]
 _L.hkv_wl_marshal_acks.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_vals.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
+_L.hkv_wl_collect_vals.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
+                                   _P, ctypes.c_uint32, _P, _P]
 _L.hkv_wl_peer_acks.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
                                 _P, ctypes.c_int32, _P]
 _L.hkv_wl_gen_remote.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_uint32,
@@ -112,6 +114,7 @@ class Round:
         self.acks = torch.zeros(W * self.ack_stride * self.ack_size, **u8)
         self.ack_count = torch.zeros(W, dtype=torch.int32, device=dev)
         self.val_out = torch.zeros(W * self.ack_stride * L.OP_META_SIZE, **u8)
+        self.val_count = torch.zeros(W, dtype=torch.int32, device=dev)
         self.rstride = self.rpp * max(self.R, 1)
         self.ack_out = torch.zeros(W * self.rstride * self.ack_size, **u8)
         self.cursor = torch.zeros(W, dtype=torch.int32, device=dev)
@@ -179,6 +182,13 @@ class Round:
         check(_L.hkv_wl_marshal_vals(_ptr(acks), n, self.ack_size, _ptr(out), self.machine_id, _s()),
               "marshal_vals")
 
+    def collect_vals(self):
+        """VALs of the writes this round's ACK batch completed, compacted per worker (val_out
+        [W][ack_stride], val_count): only the ACK slab's live elements are read."""
+        check(_L.hkv_wl_collect_vals(_ptr(self.acks), _ptr(self.ack_count), self.W, self.ack_stride, self.ack_size,
+                                     _ptr(self.val_out), self.ack_stride, _ptr(self.val_count), self.machine_id,
+                                     None, _s()), "collect_vals")
+
     def val_batch(self, vals: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None):
         self.kvs.batch(L.BatchType.vals, vals, n_batches, stride, L.OP_META_SIZE, self.mb, counts=counts)
 
@@ -210,7 +220,7 @@ class Round:
             timed("acks", self.ack_batch)
             if self.count_elems:
                 self.elem_totals[1] += self.ack_count.sum()
-            self.marshal_vals(self.acks, self.W * self.ack_stride, self.val_out)
+            self.collect_vals()
             timed("vals", lambda: self.val_batch(rv, self.W, self.rstride))
         self.refill()
         if self.R and self.count_elems:

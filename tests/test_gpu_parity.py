@@ -149,6 +149,7 @@ def test_known_answers_reference_entry_points():
 # ------------------------------------------------------------------ randomized protocol rounds
 CONFIGS = [
     pytest.param(dict(rmw=False, big=False), id="default"),
+    pytest.param(dict(rmw=False, big=True), id="big"),
     pytest.param(dict(rmw=True, big=False), id="rmw"),
     pytest.param(dict(rmw=True, big=True), id="big_rmw"),
 ]
@@ -362,13 +363,14 @@ def test_hash_ids_matches_oracle():
         assert got[5000 + k] == cityhash128(int(i).to_bytes(4, "little"))[1]
 
 
-def test_inv_direct_path_edge_cases():
+@pytest.mark.parametrize("big", [False, True])
+def test_inv_direct_path_edge_cases(big):
     """The INV direct path (non-RMW INV launches: X/F/Y words, k_inv_resolve, k_inv_commit) against
     the oracle: timestamps below, equal to and above each key's (so OUT_OF_GROUP holds exactly up
     to the first raise while the key is in WRITE), repeated maxima from several senders (the last
     one's sender is the last writer), INV_ABORT / OUT_OF_GROUP / MEMBERSHIP_CHANGE input opcodes,
     hot and missing keys, ragged counts, and launches past the 8192-element lookup head."""
-    g, o, sizes = make_pair(2000, 1024, 1 << 17)
+    g, o, sizes = make_pair(2000, 1024, 1 << 20 if big else 1 << 17, big=big)
     keys = gen_keys(2000)
     rng = np.random.default_rng(424242)
     tsp = gen.TsPool(rng)
@@ -421,12 +423,13 @@ def test_inv_direct_path_edge_cases():
     del e
 
 
-def test_ack_direct_path_edge_cases():
+@pytest.mark.parametrize("big", [False, True])
+def test_ack_direct_path_edge_cases(big):
     """The ACK direct path (non-RMW ACK launches: T/F words, k_ack_resolve, k_ack_clear) against the
     oracle: ACKs matching each key's pending write or not, duplicate and out-of-range (>= 8)
     senders, quorums reached at different elements or never, LAST_ACK_* input opcodes, a
     membership with a dropped node, ragged counts and read_write_ops completions."""
-    g, o, sizes = make_pair(2000, 1024, 1 << 17)
+    g, o, sizes = make_pair(2000, 1024, 1 << 20 if big else 1 << 17, big=big)
     keys = gen_keys(2000)
     rng = np.random.default_rng(515151)
     tsp = gen.TsPool(rng)

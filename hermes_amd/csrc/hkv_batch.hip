@@ -116,16 +116,16 @@ __device__ __forceinline__ uint8_t absorbing_state()
 // Every element's opcode is INV_SUCCESS (an INV_ABORT / OUT_OF_GROUP input stays), except
 // OUT_OF_GROUP for an element with ts = ts_0 in state WRITE, which holds until the first element
 // with a larger ts (P). Per key (log line) three words:
-//   X = max over raising elements of (ts << 24 | ~i) -> M and A (k_lookup); bit 23 of X: some
-//       element other than A has ts M (k_inv_resolve);
+//   X = max over raising elements of (ts << 24 | ~i) -> M and A (k_lookup);
 //   F = round 0's word: P, offered by raising elements of keys in state WRITE (k_lookup);
 //   Y = 1 + B when B != A (k_inv_resolve), or for keys without a raise.
-// k_lookup finishes the elements below ts_0; k_inv_resolve writes the other opcodes; in
-// k_inv_commit A (or, without a raise, B) applies the key's meta and clears X and Y. Most keys of a
-// launch have one element: it is A and B, and never touches Y.
+// k_lookup finishes the elements below ts_0; k_inv_resolve writes the other opcodes, A keeps X in
+// its own scratch slot (mem[A]) and the other elements with ts M flag A's slot pf[A] ("B is not
+// A") and raise Y; in k_inv_commit A (or, without a raise, B) applies the key's meta and clears X
+// and Y. Most keys of a launch have one element: it is A and B, never touches Y, and commits from
+// its own slots without reading X again.
 enum : uint8_t { kIvRaise = 1, kIvEq = 2, kIvWrite = 4, kIvCand = 8, kIvApply = 16 };
 constexpr int64_t kInvDirectMax = 1 << 23;
-constexpr unsigned long long kXHasB = 1ull << 23;
 
 // ACK direct path (ACK launches without RMWs). Without RMWs, hermes_exec_ack (hermesKV.c:591-674)
 // changes a key only through ACKs that match its pending write (ts = last local write's ts, op
@@ -440,6 +440,7 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                     ifl = kIvEq | (m_state(m0[k]) == kWrite ? kIvWrite : 0);
                 } else {
                     ifl = kIvRaise;
+                    a.pf[gi[k]] = 0;  // "B is not A" flag, should this element be A
                     const uint32_t w = fw_index(a, phys[k]);
                     const unsigned long long xv = (its << 24) | (0x7FFFFFull - (uint64_t)gi[k]);
                     if (xv > __hip_atomic_load(a.fx + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(a.fx + w, xv);
@@ -486,11 +487,13 @@ __global__ __launch_bounds__(256) void k_inv_resolve(BatchArgs a, int64_t i_begi
         // in state WRITE, an element at ts_0 is out of group until the first raise P (offered by
         // every raising element of a key in state WRITE, so it exists)
         if (fl & kIvWrite) oog = (uint32_t)i < first_cand(a.fw[w], a.rtag0);
-        if ((uint32_t)i == 0x7FFFFFu - (uint32_t)(X & 0x7FFFFFu)) {
+        const uint32_t ia = 0x7FFFFFu - (uint32_t)(X & 0x7FFFFFu);
+        if ((uint32_t)i == ia) {
             a.st[i] = kIvApply;
+            a.mem[i] = X;
         } else if (its == (uint64_t)(X >> 24)) {
             y = true;
-            if (!(__hip_atomic_load(a.fx + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kXHasB)) atomicOr(a.fx + w, kXHasB);
+            if (a.pf[ia] == 0) a.pf[ia] = 1;  // every writer stores the same value
         }
     } else {       // no raise: every flagged element of the key is at ts_0, B applies
         oog = (fl & kIvWrite) != 0;
@@ -507,7 +510,8 @@ __global__ __launch_bounds__(256) void k_inv_resolve(BatchArgs a, int64_t i_begi
 // A of a raising key applies the key's meta to a 64-B entry (31-B values): entry bytes 16..63
 // (meta, value) and the element's bytes 16..63 (flags, value) move as three 16-B words each, the
 // new entry image is put together in registers.
-__device__ __forceinline__ void inv_apply64(const BatchArgs &a, int64_t i, uint32_t w, uint8_t *entry)
+__device__ __forceinline__ void inv_apply64(const BatchArgs &a, int64_t i, uint32_t w, uint8_t *entry,
+                                            unsigned long long X)
 {
     union Img {
         U64x2 q[3];
@@ -522,13 +526,12 @@ __device__ __forceinline__ void inv_apply64(const BatchArgs &a, int64_t i, uint3
     el.q[1] = px[1];
     el.d[4] = *reinterpret_cast<const uint64_t *>(px + 2);
     el.d[5] = 0;
-    const unsigned long long X = a.fx[w];
     int64_t b = i;
-    if (X & kXHasB) {
+    if (a.pf[i]) {  // B is not A
         b = (int64_t)a.fy[w] - 1;
         a.fy[w] = 0;
     }
-    const uint8_t lw = b == i ? (uint8_t)(a.elems[i * a.esz + 9]) : a.elems[b * a.esz + 9];
+    const uint8_t lw = a.elems[b * a.esz + 9];
     Meta m;
     m.w4 = (uint32_t)en.d[0];
     m.w5 = (uint32_t)(en.d[0] >> 32);
@@ -583,14 +586,14 @@ __global__ __launch_bounds__(256) void k_inv_commit(BatchArgs a)
     }
     uint8_t *entry = entry_of(a, e);
     if (SV == 31 && fl == kIvApply) {  // 64-B entries: bytes 16..63 in and out as three 16-B words
-        inv_apply64(a, i, w, entry);
+        inv_apply64(a, i, w, entry, a.mem[i]);
         return;
     }
     Meta m;
     meta_load(entry, m);
     if (fl == kIvApply) {
-        const unsigned long long X = a.fx[w];
-        if (X & kXHasB) {
+        const unsigned long long X = a.mem[i];
+        if (a.pf[i]) {
             b = (int64_t)a.fy[w] - 1;
             a.fy[w] = 0;
         }
@@ -631,10 +634,9 @@ __global__ __launch_bounds__(256) void k_ack_resolve(BatchArgs a)
 #pragma unroll
     for (int s = 0; s < 8; ++s)
         if (tv[s] != 0) f = min(f, 0xFFFFFFFFu - tv[s]);
-    const uint32_t f_any = min(f, first_cand(a.fw[w], a.rtag0));
     uint32_t js = kNone;  // j*
     if (need == 0) {
-        js = f_any;
+        js = min(f, first_cand(a.fw[w], a.rtag0));  // F is read only here
     } else {
         uint32_t mx = 0;
         bool all = true;

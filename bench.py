@@ -23,21 +23,28 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# algorithmic bytes per element, SURVEY.md 8(d): S_op=56, bucket=64, entry=64, S_msg=16
-BYTES = {"get": 56 + 64 + 64 + 56, "put": 56 + 64 + 2 * 64 + 56, "inv": 56 + 64 + 2 * 64 + 56,
-         "ack": 16 + 64 + 2 * 64 + 16, "val": 16 + 64 + 2 * 64 + 16}
+# algorithmic bytes per element, SURVEY.md 8(d): S_op (56, or 312 big), bucket 64, entry (64, or
+# 320 big), S_msg 16 (ACKs carry S_op with RMWs)
+def elem_bytes(op: int, entry: int, ack: int) -> dict:
+    return {"get": op + 64 + entry + op, "put": op + 64 + 2 * entry + op, "inv": op + 64 + 2 * entry + op,
+            "ack": ack + 64 + 2 * entry + ack, "val": 16 + 64 + 2 * entry + 16}
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--config", choices=["cfg2", "cfg3"], default="cfg2",
+                   help="cfg2: BASELINE configs[1] (the metric's config); cfg3: configs[2], RMW-heavy "
+                        "(RMWs on, 287-B values, 25%% PUT + 25%% RMW; one replica, virtual peers)")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--keys", type=int, default=None,
                    help="keys per replica (default: 100M at N=1, configs[1]; 1B at N>1, configs[3])")
     p.add_argument("--workers", type=int, default=8192, help="virtual workers (250-op buffers) per GPU")
     p.add_argument("--zipf", type=float, default=0.99)
-    p.add_argument("--write-permille", type=int, default=200)
+    p.add_argument("--write-permille", type=int, default=None, help="default 200 (cfg2), 500 (cfg3)")
+    p.add_argument("--rmw-permille", type=int, default=None,
+                   help="RMWs among the writes, permille (default 0 (cfg2), 500 (cfg3))")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (0 = skip)")
     p.add_argument("--cpu-workers", type=int, default=64)
     p.add_argument("--seed", type=int, default=0x5EED)
@@ -96,11 +103,23 @@ def main():
     from hermes_amd.kvs import HermesKV, sized_geometry
     from hermes_amd.workload import Round, zipf_params
 
-    if a.keys is None:
-        a.keys = 100_000_000 if world == 1 else 1_000_000_000
+    cfg3 = a.config == "cfg3"
+    if a.keys is None:  # cfg3: 320-B entries; 10M keys keep log offsets within 32-bit entry ids
+        a.keys = 10_000_000 if cfg3 else 100_000_000 if world == 1 else 1_000_000_000
+    if cfg3 and world > 1:
+        raise SystemExit("--config cfg3 is a one-replica configuration (configs[2])")
+    if a.write_permille is None:
+        a.write_permille = 500 if cfg3 else 200
+    if a.rmw_permille is None:
+        a.rmw_permille = 500 if cfg3 else 0
+    if cfg3:
+        a.cpu_seconds = 0.0       # the CPU restatement's bench driver runs the default build only
     t0 = time.time()
-    bkts, cap = sized_geometry(a.keys)
-    kvs = HermesKV(a.keys, bkts, cap, machine_id=rank if world > 1 else 0, device=local_rank)
+    sizes = L.Sizes(True, 4) if cfg3 else L.DEFAULT
+    bkts, cap = sized_geometry(a.keys, sizes)
+    kvs = HermesKV(a.keys, bkts, cap, machine_id=rank if world > 1 else 0, device=local_rank, rmw=cfg3,
+                   big_objects=cfg3, extra_cache_lines=4 if cfg3 else 0)
+    BYTES = elem_bytes(kvs.sizes.op, kvs.sizes.entry, kvs.sizes.op if cfg3 else 16)
     torch.cuda.synchronize()
     t_pop = time.time() - t0
     z = zipf_params(a.keys, a.zipf)
@@ -117,7 +136,7 @@ def main():
         rnd = ReplicaGroupRound(kvs, a.workers, z, a.write_permille, seed=a.seed, world=world, rank=rank,
                                 retry_stalled=a.retry)
     else:
-        rnd = Round(kvs, a.workers, L.membership(3, 0), [1, 2], z, a.write_permille, seed=a.seed,
+        rnd = Round(kvs, a.workers, L.membership(3, 0), [1, 2], z, a.write_permille, a.rmw_permille, seed=a.seed,
                     max_steps=total_steps + 2, retry_stalled=a.retry)
     torch.cuda.synchronize()
 
@@ -183,7 +202,8 @@ def main():
     # tools/pmc_local.py) are committed under profiles/; counters cannot be read in this run
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_local_batch.json")
-    if world == 1 and dom == "local" and a.workers == 8192 and a.keys == 100_000_000 and os.path.exists(pmc):
+    if (world == 1 and not cfg3 and dom == "local" and a.workers == 8192 and a.keys == 100_000_000
+            and os.path.exists(pmc)):
         with open(pmc) as f:
             traffic = json.load(f)["traffic_bytes"]
         traffic_src = "profiles/pmc_local_batch.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, separate runs)"
@@ -201,11 +221,14 @@ def main():
         "dtype": "u8",
         "data": "synthetic (seeded Zipf traces, CityHash keys, virtual or RCCL peers)",
         "config": {
-            "workload": ("cfg2: 1xMI355X, 100M keys, 31 B values, Zipf 0.99, 20% writes, "
+            "workload": (f"cfg3: 1xMI355X RMW-heavy, {a.keys} keys, RMWs on, 287 B values, Zipf 0.99, 25% PUT + 25% RMW, "
+                         "INV/ACK/VAL from 2 virtual replicas" if cfg3 else
+                         "cfg2: 1xMI355X, 100M keys, 31 B values, Zipf 0.99, 20% writes, "
                          "INV/ACK/VAL from 2 virtual replicas" if world == 1 else
                          f"cfg4: {world}-replica Hermes group over RCCL, {a.keys} keys/replica"),
             "keys": a.keys, "buckets": bkts, "log_cap": cap, "workers_per_gpu": W,
             "local_batch": S, "zipf": a.zipf, "write_permille": a.write_permille,
+            "rmw_permille_of_writes": a.rmw_permille,
             "remote_invs_per_worker": rnd.rstride, "parallelism": f"replicas{world}",
             "elements_per_step": {"inv": n_inv, "ack": n_ack, "val": n_val},
         },

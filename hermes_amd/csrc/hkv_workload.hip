@@ -307,8 +307,8 @@ __global__ __launch_bounds__(256) void k_collect_vals(uint8_t *acks, const int32
 }
 
 __global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32_t inv_stride, uint32_t op_size,
-                            uint8_t *acks, int32_t out_stride, int32_t *ack_count, const uint8_t *peers,
-                            int32_t n_peers, int64_t total)
+                            uint8_t *acks, uint32_t ack_size, int32_t out_stride, int32_t *ack_count,
+                            const uint8_t *peers, int32_t n_peers, int64_t total)
 {
     int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= total) return;
@@ -320,7 +320,8 @@ __global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32
     if (rem == 0) ack_count[w] = n * n_peers;
     if (j >= n) return;
     const uint64_t *src = reinterpret_cast<const uint64_t *>(invs + ((int64_t)w * inv_stride + j) * op_size);
-    uint64_t *dst = reinterpret_cast<uint64_t *>(acks + ((int64_t)w * out_stride + rem) * kOpMetaSize);
+    // an ACK is the INV's 16-B op_meta (the rest of an op-sized ACK of an RMW build is not read)
+    uint64_t *dst = reinterpret_cast<uint64_t *>(acks + ((int64_t)w * out_stride + rem) * ack_size);
     const W16 h = *reinterpret_cast<const W16 *>(src);
     *reinterpret_cast<W16 *>(dst) = W16{h.a, with_op_state(h.b, kOpAck, peers[r])};  // ack_copy_and_modify_elem
 }
@@ -542,14 +543,14 @@ int hkv_wl_marshal_vals(uint8_t *acks, int64_t n, uint32_t ack_size, uint8_t *ou
 }
 
 int hkv_wl_peer_acks(const uint8_t *inv_out, const int32_t *inv_count, int32_t n_workers, int32_t inv_stride,
-                     uint32_t op_size, uint8_t *acks, int32_t out_stride, int32_t *ack_count, const uint8_t *peer_ids,
-                     int32_t n_peers, void *stream)
+                     uint32_t op_size, uint8_t *acks, uint32_t ack_size, int32_t out_stride, int32_t *ack_count,
+                     const uint8_t *peer_ids, int32_t n_peers, void *stream)
 {
-    if (n_peers <= 0 || n_workers <= 0) return -1;
+    if (n_peers <= 0 || n_workers <= 0 || ack_size < kOpMetaSize || ack_size % 8) return -1;
     if (out_stride != inv_stride * n_peers) return -1;
     int64_t total = (int64_t)n_workers * inv_stride * n_peers;
     hipLaunchKernelGGL(k_peer_acks, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, inv_out, inv_count,
-                       inv_stride, op_size, acks, out_stride, ack_count, peer_ids, n_peers, total);
+                       inv_stride, op_size, acks, ack_size, out_stride, ack_count, peer_ids, n_peers, total);
     return ok();
 }
 

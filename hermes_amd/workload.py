@@ -39,8 +39,8 @@ _L.hkv_wl_marshal_acks.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctyp
 _L.hkv_wl_marshal_vals.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_collect_vals.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
                                    _P, ctypes.c_uint32, _P, _P]
-_L.hkv_wl_peer_acks.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
-                                _P, ctypes.c_int32, _P]
+_L.hkv_wl_peer_acks.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_uint32,
+                                ctypes.c_int32, _P, _P, ctypes.c_int32, _P]
 _L.hkv_wl_gen_remote.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_uint32,
                                  ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(HkvZipf), ctypes.c_uint32,
                                  ctypes.c_uint64, _P]
@@ -161,8 +161,8 @@ class Round:
 
     def virtual_peer_acks(self):
         check(_L.hkv_wl_peer_acks(_ptr(self.inv_out), _ptr(self.inv_count), self.W, self.C, self.op,
-                                  _ptr(self.acks), self.ack_stride, _ptr(self.ack_count), _ptr(self.peer_t),
-                                  self.R, _s()), "peer_acks")
+                                  _ptr(self.acks), self.ack_size, self.ack_stride, _ptr(self.ack_count),
+                                  _ptr(self.peer_t), self.R, _s()), "peer_acks")
 
     def inv_batch(self, invs: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None):
         self.kvs.batch(L.BatchType.invs, invs, n_batches, stride, self.op, self.mb, counts=counts)

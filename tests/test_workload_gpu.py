@@ -20,18 +20,22 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("theta,workers", [(0.99, 40), (0.0, 40), (0.99, 160)])
-def test_bench_round_mirrored(theta, workers):
+@pytest.mark.parametrize("theta,workers,cfg3", [(0.99, 40, False), (0.0, 40, False), (0.99, 160, False),
+                                                (0.99, 40, True)])
+def test_bench_round_mirrored(theta, workers, cfg3):
+    """cfg3: bench.py --config cfg3 (RMWs on, big objects, 25 % PUT + 25 % RMW): the rounds engine,
+    op-sized ACKs from the virtual peers, RMW completions."""
     from hermes_amd.kvs import HermesKV
     from hermes_amd.workload import Round, zipf_params
-    n_keys, bkts, cap = 60_000, 1 << 16, 1 << 23
+    n_keys, bkts = 60_000, 1 << 16
+    cap = 1 << 25 if cfg3 else 1 << 23
     steps = 3                         # 10,000 / 40,000 local elements per launch
-    g = HermesKV(n_keys, bkts, cap, machine_id=0)
-    o = OracleKVS(bkts, cap, 0)
-    o.populate(n_keys, L.DEFAULT.kvs_value)
+    g = HermesKV(n_keys, bkts, cap, machine_id=0, rmw=cfg3, big_objects=cfg3, extra_cache_lines=4 if cfg3 else 0)
+    o = OracleKVS(bkts, cap, 0, cfg3, cfg3, 4 if cfg3 else 0)
+    o.populate(n_keys, g.sizes.kvs_value)
     m = Mirror(g, o, "bench round")
-    r = Round(g, workers, L.membership(3, 0), [1, 2], zipf_params(n_keys, theta), 200, seed=0x5EED,
-              max_steps=8, trace_len=1024)
+    r = Round(g, workers, L.membership(3, 0), [1, 2], zipf_params(n_keys, theta), 500 if cfg3 else 200,
+              500 if cfg3 else 0, seed=0x5EED, max_steps=8, trace_len=1024)
     for _ in range(steps):
         r.step()
     torch.cuda.synchronize()

@@ -234,11 +234,15 @@ __device__ __forceinline__ uint8_t *shadow_of(const BatchArgs &a, uint32_t i)
     return a.shadow + (size_t)i * a.g.entry_size;
 }
 
-// entries and shadows are 8-byte aligned and a multiple of 8 long
+// entries and shadows are 8-byte aligned and a multiple of 8 long: 16-B words, then one 8-B word
 __device__ __forceinline__ void copy_entry(uint8_t *dst, const uint8_t *src, uint32_t bytes)
 {
-    for (uint32_t w = 0; w < bytes / 8; ++w)
-        reinterpret_cast<uint64_t *>(dst)[w] = reinterpret_cast<const uint64_t *>(src)[w];
+    struct __attribute__((aligned(8))) W16 {
+        uint64_t a, b;
+    };
+    uint32_t o = 0;
+    for (; o + 16 <= bytes; o += 16) *reinterpret_cast<W16 *>(dst + o) = *reinterpret_cast<const W16 *>(src + o);
+    if (o < bytes) *reinterpret_cast<uint64_t *>(dst + o) = *reinterpret_cast<const uint64_t *>(src + o);
 }
 
 // The round's first candidate of a key: S_r (read from src: the entry in round 0, the previous
@@ -769,10 +773,24 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
     // what the non-mutating elements read the entry value from (bytes below 16 are never read)
     uint8_t *rentry = kStage ? reinterpret_cast<uint8_t *>(&sent[3 * threadIdx.x]) - 16 : entry_of(a, e);
     const uint32_t bytes = (uint32_t)cnt * (uint32_t)a.esz;  // a multiple of 8
-    const uint4 *src = reinterpret_cast<const uint4 *>(a.elems + i0 * a.esz);
-    for (uint32_t w = threadIdx.x; w < bytes / 16; w += BP) sops[w] = src[w];
-    if ((bytes & 8) && threadIdx.x == 0)
-        reinterpret_cast<uint64_t *>(sops)[bytes / 8 - 1] = reinterpret_cast<const uint64_t *>(src)[bytes / 8 - 1];
+    // big ops (312 B): only the elements that hit move through LDS (message slabs are mostly
+    // padding); 8-B words, each inside one element
+    constexpr bool kLive = BP == 128;
+    __shared__ uint8_t live[kLive ? BP : 1];
+    const uint32_t ew = (uint32_t)a.esz / 8u;
+    if (kLive) {
+        live[threadIdx.x] = e != kNone;
+        __syncthreads();
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(a.elems + i0 * a.esz);
+        uint64_t *s8 = reinterpret_cast<uint64_t *>(sops);
+        for (uint32_t w = threadIdx.x; w < bytes / 8; w += BP)
+            if (live[w / ew]) s8[w] = src[w];
+    } else {
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.elems + i0 * a.esz);
+        for (uint32_t w = threadIdx.x; w < bytes / 16; w += BP) sops[w] = src[w];
+        if ((bytes & 8) && threadIdx.x == 0)
+            reinterpret_cast<uint64_t *>(sops)[bytes / 8 - 1] = reinterpret_cast<const uint64_t *>(src)[bytes / 8 - 1];
+    }
     __syncthreads();
     const int t = threadIdx.x;
     if (t < cnt) {
@@ -811,6 +829,13 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
         a.st[i] = st;
     }
     __syncthreads();
+    if (kLive) {
+        uint64_t *dst = reinterpret_cast<uint64_t *>(a.elems + i0 * a.esz);
+        const uint64_t *s8 = reinterpret_cast<const uint64_t *>(sops);
+        for (uint32_t w = threadIdx.x; w < bytes / 8; w += BP)
+            if (live[w / ew]) dst[w] = s8[w];
+        return;
+    }
     uint4 *dst = reinterpret_cast<uint4 *>(a.elems + i0 * a.esz);
     for (uint32_t w = threadIdx.x; w < bytes / 16; w += BP) dst[w] = sops[w];
     if ((bytes & 8) && threadIdx.x == 0)

@@ -23,6 +23,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+EVENT_EVERY = 4                # timed steps per sampled local-launch duration
 # algorithmic bytes per element, SURVEY.md 8(d): S_op (56, or 312 big), bucket 64, entry (64, or
 # 320 big), S_msg 16 (ACKs carry S_op with RMWs)
 def elem_bytes(op: int, entry: int, ack: int) -> dict:
@@ -153,8 +154,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t = time.perf_counter()
-    for _ in range(a.steps):
-        rnd.step(events, timed_batches=("local",))  # the roofline's launch; the rest: probe step
+    for k in range(a.steps):
+        # HIP events around the local launch (the roofline's) on every EVENT_EVERY-th step: each
+        # record costs ~5 us of GPU time between kernels; the other launches: probe step below
+        rnd.step(events if k % EVENT_EVERY == 0 else None, timed_batches=("local",))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -236,6 +239,7 @@ def main():
             "bound": "hbm", "kernel": f"{dom} batch launch (k_lookup + element-order rounds, hkv_batch.hip)",
             "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
             "traffic": traffic, "traffic_source": traffic_src, "launch_ms": ms.get(dom),
+            "launch_samples": len(events.get(dom, [])),
             "algorithmic_bytes_per_launch": per_launch_bytes[dom],
             "batch_ms": ms,
         },

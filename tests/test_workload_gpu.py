@@ -43,3 +43,36 @@ def test_bench_round_mirrored(theta, workers, cfg3):
     st = r.stats()
     assert st["committed"] > 0 and st["writes_completed"] > 0, st
     assert g.take_error_flags() == 0
+
+
+class _DeviceBytes:
+    """A device byte range as a torch tensor, without a copy (__cuda_array_interface__)."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False), "version": 3}
+
+
+def test_full_size_round_invariants():
+    """BASELINE configs[1] at full size (100M keys, 8192 virtual workers, the bench's round):
+    properties that hold at any size. After every round each key is VALID again (every local write
+    was ACKed by both virtual peers and completed, every INV's VAL applied, no membership change),
+    no INV was held back, writes completed, and the engine's consistency flags are clear."""
+    from hermes_amd.kvs import HermesKV, sized_geometry
+    from hermes_amd.workload import Round, zipf_params
+    n_keys = 100_000_000
+    bkts, cap = sized_geometry(n_keys)
+    g = HermesKV(n_keys, bkts, cap, machine_id=0)
+    r = Round(g, 8192, L.membership(3, 0), [1, 2], zipf_params(n_keys, 0.99), 200, seed=0x5EED, max_steps=4)
+    entry = g.sizes.entry
+    assert g.log_head == n_keys * entry       # populate wrote entries 0..n-1 back to back
+    log = torch.as_tensor(_DeviceBytes(g.device_log(), n_keys * entry), device="cuda")
+    state = log.view(n_keys, entry)[:, 18]    # object meta byte 0: state
+    assert int((state != int(L.State.VALID)).sum()) == 0
+    for step in range(3):
+        r.step()
+        torch.cuda.synchronize()
+        bad = int((state != int(L.State.VALID)).sum())
+        assert bad == 0, f"round {step}: {bad} keys not VALID"
+    st = r.stats()
+    assert st["invs_held"] == 0 and st["committed"] > 2_000_000 and st["writes_completed"] > 300_000, st
+    assert g.take_error_flags() == 0

@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--seed", type=int, default=0x5EED)
     p.add_argument("--host-api-seconds", type=float, default=1.0,
                    help="time the host-pointer entry point for this long (0 = skip; N=1 only)")
+    p.add_argument("--no-fit-acks", action="store_true",
+                   help="N=1: keep the ACK slab at its capacity stride (2C) instead of the round's largest count")
     p.add_argument("--retry", action="store_true",
                    help="refill_ops semantics: stalled ops keep their slot (default: fresh batch per step)")
     return p.parse_args()
@@ -138,7 +140,7 @@ def main():
                                 retry_stalled=a.retry)
     else:
         rnd = Round(kvs, a.workers, L.membership(3, 0), [1, 2], z, a.write_permille, a.rmw_permille, seed=a.seed,
-                    max_steps=total_steps + 2, retry_stalled=a.retry)
+                    max_steps=total_steps + 2, retry_stalled=a.retry, fit_ack_stride=not a.no_fit_acks)
     torch.cuda.synchronize()
 
     for _ in range(a.warmup):

@@ -312,7 +312,7 @@ __global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32
 {
     int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= total) return;
-    int64_t per_w = (int64_t)inv_stride * n_peers;
+    int64_t per_w = out_stride;     // slots x n_peers ACK positions per worker (host checks)
     int32_t w = (int32_t)(g / per_w);
     int32_t rem = (int32_t)(g - (int64_t)w * per_w);
     int32_t j = rem / n_peers, r = rem - j * n_peers;
@@ -547,8 +547,8 @@ int hkv_wl_peer_acks(const uint8_t *inv_out, const int32_t *inv_count, int32_t n
                      const uint8_t *peer_ids, int32_t n_peers, void *stream)
 {
     if (n_peers <= 0 || n_workers <= 0 || ack_size < kOpMetaSize || ack_size % 8) return -1;
-    if (out_stride != inv_stride * n_peers) return -1;
-    int64_t total = (int64_t)n_workers * inv_stride * n_peers;
+    if (out_stride % n_peers || out_stride > inv_stride * n_peers || out_stride <= 0) return -1;
+    int64_t total = (int64_t)n_workers * out_stride;
     hipLaunchKernelGGL(k_peer_acks, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, inv_out, inv_count,
                        inv_stride, op_size, acks, ack_size, out_stride, ack_count, peer_ids, n_peers, total);
     return ok();

@@ -88,7 +88,8 @@ class Round:
     def __init__(self, kvs: HermesKV, n_workers: int, membership: bytes, peer_ids: list[int],
                  zipf: HkvZipf, write_permille: int = 200, rmw_permille: int = 0,
                  remote_per_peer: int = 50, trace_len: int = 8192, seed: int = 0x5EED,
-                 virtual_peers: bool = True, max_steps: int = 64, retry_stalled: bool = False):
+                 virtual_peers: bool = True, max_steps: int = 64, retry_stalled: bool = False,
+                 fit_ack_stride: bool = True):
         self.kvs = kvs
         self.W = n_workers
         self.mb = membership
@@ -110,7 +111,13 @@ class Round:
         self.inv_out = torch.zeros(W * self.C * self.op, **u8)
         self.inv_count = torch.zeros(W, dtype=torch.int32, device=dev)
         self.held = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.ack_stride = self.C * max(self.R, 1)
+        self.ack_stride = self.C * max(self.R, 1)   # capacity; the round uses self.ack_width
+        self.ack_width = self.ack_stride
+        # fit_ack_stride: each round's ACK slab is laid out at R x (largest per-worker INV count),
+        # read back while the remote INV batch runs (about 20 ACKs per worker against 2C slots)
+        self.fit = fit_ack_stride and virtual_peers and self.R > 0
+        self.maxc_h = torch.zeros(1, dtype=torch.int32, pin_memory=True) if self.fit else None
+        self.maxc_ev = torch.cuda.Event() if self.fit else None
         self.acks = torch.zeros(W * self.ack_stride * self.ack_size, **u8)
         self.ack_count = torch.zeros(W, dtype=torch.int32, device=dev)
         self.val_out = torch.zeros(W * self.ack_stride * L.OP_META_SIZE, **u8)
@@ -161,7 +168,7 @@ class Round:
 
     def virtual_peer_acks(self):
         check(_L.hkv_wl_peer_acks(_ptr(self.inv_out), _ptr(self.inv_count), self.W, self.C, self.op,
-                                  _ptr(self.acks), self.ack_size, self.ack_stride, _ptr(self.ack_count),
+                                  _ptr(self.acks), self.ack_size, self.ack_width, _ptr(self.ack_count),
                                   _ptr(self.peer_t), self.R, _s()), "peer_acks")
 
     def inv_batch(self, invs: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None):
@@ -174,7 +181,7 @@ class Round:
     def ack_batch(self, acks: torch.Tensor | None = None, n_batches: int | None = None, stride: int | None = None,
                   counts: torch.Tensor | None = None):
         acks = self.acks if acks is None else acks
-        self.kvs.batch(L.BatchType.acks, acks, n_batches or self.W, stride or self.ack_stride, self.ack_size,
+        self.kvs.batch(L.BatchType.acks, acks, n_batches or self.W, stride or self.ack_width, self.ack_size,
                        self.mb, counts=self.ack_count if counts is None else counts, rw=self.ops,
                        rw_stride_bytes=self.LOCAL * self.op)
 
@@ -185,8 +192,8 @@ class Round:
     def collect_vals(self):
         """VALs of the writes this round's ACK batch completed, compacted per worker (val_out
         [W][ack_stride], val_count): only the ACK slab's live elements are read."""
-        check(_L.hkv_wl_collect_vals(_ptr(self.acks), _ptr(self.ack_count), self.W, self.ack_stride, self.ack_size,
-                                     _ptr(self.val_out), self.ack_stride, _ptr(self.val_count), self.machine_id,
+        check(_L.hkv_wl_collect_vals(_ptr(self.acks), _ptr(self.ack_count), self.W, self.ack_width, self.ack_size,
+                                     _ptr(self.val_out), self.ack_width, _ptr(self.val_count), self.machine_id,
                                      None, _s()), "collect_vals")
 
     def val_batch(self, vals: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None):
@@ -212,11 +219,17 @@ class Round:
         self.marshal_invs()
         if self.count_elems:
             self.inv_total += self.inv_count.sum()
+        if self.fit:
+            self.maxc_h.copy_(self.inv_count.max().view(1), non_blocking=True)
+            self.maxc_ev.record()
         if self.R:
-            self.virtual_peer_acks()
             ri, rv = self.remote_inv[k], self.remote_val[k]
             timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride))
             self.marshal_acks(ri, self.W * self.rstride, self.ack_out)
+            if self.fit:   # the GPU is still on the INV batch: this wait leaves no gap on the stream
+                self.maxc_ev.synchronize()
+                self.ack_width = max(1, min(int(self.maxc_h[0]), self.C)) * self.R
+            self.virtual_peer_acks()
             timed("acks", self.ack_batch)
             if self.count_elems:
                 self.elem_totals[1] += self.ack_count.sum()

@@ -76,7 +76,9 @@ int hkv_wl_marshal_vals(uint8_t *d_acks, int64_t n, uint32_t ack_size, uint8_t *
 /* ACK batch answering a slab of INVs from n_peers replicas: for INV j of worker w, the
  * ack_size-byte element d_acks[w*out_stride + j*n_peers + r] gets the op_meta {key, ST_OP_ACK,
  * sender = peer_ids[r], ts = inv ts} (ack_size: 16, or the op size in an RMW build);
- * d_ack_count[w] = n_peers * d_inv_count[w] */
+ * d_ack_count[w] = n_peers * d_inv_count[w]. out_stride is a multiple of n_peers, at most
+ * inv_stride * n_peers, and the caller keeps every d_inv_count[w] <= out_stride / n_peers (the N=1
+ * round fits it to the round's largest count) */
 int hkv_wl_peer_acks(const uint8_t *d_inv_out, const int32_t *d_inv_count, int32_t n_workers, int32_t inv_stride,
                      uint32_t op_size, uint8_t *d_acks, uint32_t ack_size, int32_t out_stride,
                      int32_t *d_ack_count, const uint8_t *peer_ids, int32_t n_peers, void *stream);

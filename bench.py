@@ -34,9 +34,11 @@ def elem_bytes(op: int, entry: int, ack: int) -> dict:
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--config", choices=["cfg2", "cfg3"], default="cfg2",
+    p.add_argument("--config", choices=["cfg2", "cfg3", "cfg5"], default="cfg2",
                    help="cfg2: BASELINE configs[1] (the metric's config); cfg3: configs[2], RMW-heavy "
-                        "(RMWs on, 287-B values, 25%% PUT + 25%% RMW; one replica, virtual peers)")
+                        "(RMWs on, 287-B values, 25%% PUT + 25%% RMW; one replica, virtual peers); "
+                        "cfg5: configs[4] on one GPU, an 8-replica group of 7 virtual peers, the last "
+                        "one dropped in the middle of the timed steps")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--keys", type=int, default=None,
@@ -107,16 +109,17 @@ def main():
     from hermes_amd.workload import Round, zipf_params
 
     cfg3 = a.config == "cfg3"
+    cfg5 = a.config == "cfg5"
     if a.keys is None:  # cfg3: 320-B entries; 10M keys keep log offsets within 32-bit entry ids
-        a.keys = 10_000_000 if cfg3 else 100_000_000 if world == 1 else 1_000_000_000
-    if cfg3 and world > 1:
-        raise SystemExit("--config cfg3 is a one-replica configuration (configs[2])")
+        a.keys = 10_000_000 if cfg3 else 100_000_000 if world == 1 and not cfg5 else 1_000_000_000
+    if (cfg3 or cfg5) and world > 1:
+        raise SystemExit(f"--config {a.config} runs on one GPU with virtual peers")
     if a.write_permille is None:
         a.write_permille = 500 if cfg3 else 200
     if a.rmw_permille is None:
         a.rmw_permille = 500 if cfg3 else 0
-    if cfg3:
-        a.cpu_seconds = 0.0       # the CPU restatement's bench driver runs the default build only
+    if cfg3 or cfg5:
+        a.cpu_seconds = 0.0       # the CPU restatement's bench driver runs configs[1]'s round only
     t0 = time.time()
     sizes = L.Sizes(True, 4) if cfg3 else L.DEFAULT
     bkts, cap = sized_geometry(a.keys, sizes)
@@ -139,7 +142,9 @@ def main():
         rnd = ReplicaGroupRound(kvs, a.workers, z, a.write_permille, seed=a.seed, world=world, rank=rank,
                                 retry_stalled=a.retry)
     else:
-        rnd = Round(kvs, a.workers, L.membership(3, 0), [1, 2], z, a.write_permille, a.rmw_permille, seed=a.seed,
+        machines = 8 if cfg5 else 3
+        rnd = Round(kvs, a.workers, L.membership(machines, 0), list(range(1, machines)), z, a.write_permille,
+                    a.rmw_permille, seed=a.seed,
                     max_steps=total_steps + 2, retry_stalled=a.retry, fit_ack_stride=not a.no_fit_acks)
     torch.cuda.synchronize()
 
@@ -155,11 +160,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    drop_at = a.steps // 2 if cfg5 else -1   # cfg5: the last peer fails in this timed step
     t = time.perf_counter()
     for k in range(a.steps):
         # HIP events around the local launch (the roofline's) on every EVENT_EVERY-th step: each
         # record costs ~5 us of GPU time between kernels; the other launches: probe step below
-        rnd.step(events if k % EVENT_EVERY == 0 else None, timed_batches=("local",))
+        rnd.step(events if k % EVENT_EVERY == 0 else None, timed_batches=("local",),
+                 drop=rnd.peers[-1] if k == drop_at else None)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -207,7 +214,7 @@ def main():
     # tools/pmc_local.py) are committed under profiles/; counters cannot be read in this run
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_local_batch.json")
-    if (world == 1 and not cfg3 and dom == "local" and a.workers == 8192 and a.keys == 100_000_000
+    if (world == 1 and not cfg3 and not cfg5 and dom == "local" and a.workers == 8192 and a.keys == 100_000_000
             and os.path.exists(pmc)):
         with open(pmc) as f:
             traffic = json.load(f)["traffic_bytes"]
@@ -226,7 +233,9 @@ def main():
         "dtype": "u8",
         "data": "synthetic (seeded Zipf traces, CityHash keys, virtual or RCCL peers)",
         "config": {
-            "workload": (f"cfg3: 1xMI355X RMW-heavy, {a.keys} keys, RMWs on, 287 B values, Zipf 0.99, 25% PUT + 25% RMW, "
+            "workload": (f"cfg5: 1xMI355X, 8-replica group (7 virtual peers), {a.keys} keys, 20% writes, "
+                         f"peer 7 fails in timed step {drop_at} (membership change, write replays)" if cfg5 else
+                         f"cfg3: 1xMI355X RMW-heavy, {a.keys} keys, RMWs on, 287 B values, Zipf 0.99, 25% PUT + 25% RMW, "
                          "INV/ACK/VAL from 2 virtual replicas" if cfg3 else
                          "cfg2: 1xMI355X, 100M keys, 31 B values, Zipf 0.99, 20% writes, "
                          "INV/ACK/VAL from 2 virtual replicas" if world == 1 else
@@ -252,6 +261,9 @@ def main():
             "round_stats_rank0": rnd.stats(),
         },
     }
+    if cfg5:
+        out["detail"]["membership"] = {"machines": 8, "dropped": rnd.drops, "at_timed_step": drop_at,
+                                       "g_membership_after": rnd.mb[1]}
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0 and world == 1 and a.host_api_seconds > 0:

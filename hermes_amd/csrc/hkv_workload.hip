@@ -225,6 +225,32 @@ __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stri
           : st == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
 }
 
+// VALs of the writes and replays a membership change completed: wings_issue_pkts(val) over the
+// ops with memb_change_skip_or_get_sender_id / memb_change_copy_and_modify_elem /
+// memb_change_modify_elem_after_send (hermes_worker.c:163-203). The callback sets opcode, sender
+// and ts of the message; the key is the op's (the 16-B op_meta with opcode and sender replaced).
+// *_COMPLETE_SEND_VALS -> PUT_COMPLETE / RMW_COMPLETE / NEW (a replayed GET is issued again).
+__global__ __launch_bounds__(256) void k_marshal_memb_vals(uint8_t *ops, int32_t stride, uint32_t op_size,
+                                                           uint8_t *out, int32_t out_stride, int32_t *count,
+                                                           uint32_t machine_id)
+{
+    const int w = blockIdx.x, i = threadIdx.x;
+    const bool live = i < stride;
+    uint8_t *op = ops + ((int64_t)w * stride + i) * op_size;
+    const uint8_t st = live ? op[9] : 0;
+    const bool send = live && (st == kPutCompleteSendVals || st == kRmwCompleteSendVals || st == kReplayCompleteSendVals);
+    int total;
+    const int rank = block_rank(send, total);
+    if (i == 0) count[w] = total < out_stride ? total : out_stride;
+    if (!send) return;
+    if (rank < out_stride) {
+        const W16 h = *reinterpret_cast<const W16 *>(op);
+        *reinterpret_cast<W16 *>(out + ((int64_t)w * out_stride + rank) * kOpMetaSize) =
+            W16{h.a, with_op_state(h.b, kOpVal, (uint8_t)machine_id)};
+    }
+    op[9] = st == kPutCompleteSendVals ? kPutComplete : st == kRmwCompleteSendVals ? kRmwComplete : kNew;
+}
+
 // ACKs for received INV rows: row r holds in_count[r] INVs (row stride C); its ACKs are
 // compacted to the front of output row r (ack_skip_or_get_sender_id + ack_copy_and_modify_elem
 // + ack_modify_elem_after_send, hermes_worker.c:67-110)
@@ -572,6 +598,15 @@ int hkv_wl_marshal_invs_cap(uint8_t *ops, int32_t n_workers, int32_t stride, uin
     if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
     hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
                        out_stride, count, machine_id, held);
+    return ok();
+}
+
+int hkv_wl_marshal_memb_vals(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint8_t *out,
+                             int32_t out_stride, int32_t *count, uint32_t machine_id, void *stream)
+{
+    if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
+    hipLaunchKernelGGL(k_marshal_memb_vals, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
+                       out, out_stride, count, machine_id);
     return ok();
 }
 

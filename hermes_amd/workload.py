@@ -36,6 +36,8 @@ _L.hkv_wl_marshal_invs.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_
 _L.hkv_wl_marshal_invs_cap.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
                                        ctypes.c_uint32, _P, _P]
 _L.hkv_wl_marshal_acks.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, _P]
+_L.hkv_wl_marshal_memb_vals.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
+                                        ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_vals.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_collect_vals.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
                                    _P, ctypes.c_uint32, _P, _P]
@@ -131,25 +133,36 @@ class Round:
         self.count_elems = True        # keep inv_total / elem_totals (small torch ops per step)
         self.peer_t = torch.tensor(self.peers or [0], dtype=torch.uint8, device=dev)
         self.trace_len = trace_len
+        self.seed = seed
         self.trace_key = torch.empty(W * trace_len, dtype=torch.int64, device=dev)
         self.trace_op = torch.empty(W * trace_len, dtype=torch.uint8, device=dev)
         check(_L.hkv_wl_gen_trace(_ptr(self.trace_key), _ptr(self.trace_op), None, W, trace_len,
                                   ctypes.byref(zipf), write_permille, rmw_permille,
                                   ctypes.c_uint64(seed ^ (self.machine_id << 48)), _s()), "gen_trace")
-        self.seed = seed
         self.clock = 0
+        self.max_steps = max_steps
         self.remote_inv = []
         self.remote_val = []
-        if virtual_peers and self.R:
-            for k in range(max_steps):
-                ri = torch.empty(W * self.rstride * self.op, **u8)
-                rv = torch.empty(W * self.rstride * L.OP_META_SIZE, **u8)
-                check(_L.hkv_wl_gen_remote(_ptr(ri), _ptr(rv), W, self.rpp, _ptr(self.peer_t), self.R, self.op,
-                                           self.sizes.st_value, self.sizes.shift, ctypes.byref(zipf), k,
-                                           ctypes.c_uint64(seed * 7919 + self.machine_id), _s()), "gen_remote")
-                self.remote_inv.append(ri)
-                self.remote_val.append(rv)
+        self.drops = []                # peers dropped from the membership (membership_change)
+        self.alive = self.R            # live peers: the first `alive` slots of the remote slabs
+        self._counts = {}
+        self._gen_remote()
         self.refill(first=True)
+
+    def _gen_remote(self):
+        """INV + VAL slabs [W][R][rpp] of the virtual peers, one per round index"""
+        if not (self.virtual and self.R):
+            return
+        W, dev = self.W, torch.device("cuda", self.kvs.device)
+        u8 = dict(dtype=torch.uint8, device=dev)
+        for k in range(self.max_steps):
+            ri = torch.empty(W * self.rstride * self.op, **u8)
+            rv = torch.empty(W * self.rstride * L.OP_META_SIZE, **u8)
+            check(_L.hkv_wl_gen_remote(_ptr(ri), _ptr(rv), W, self.rpp, _ptr(self.peer_t), self.R, self.op,
+                                       self.sizes.st_value, self.sizes.shift, ctypes.byref(self.zipf), k,
+                                       ctypes.c_uint64(self.seed * 7919 + self.machine_id), _s()), "gen_remote")
+            self.remote_inv.append(ri)
+            self.remote_val.append(rv)
 
     # -- pieces of one round
     def refill(self, first: bool = False):
@@ -166,10 +179,11 @@ class Round:
                                          _ptr(self.inv_count), self.machine_id, _ptr(self.held), _s()),
               "marshal_invs")
 
-    def virtual_peer_acks(self):
+    def virtual_peer_acks(self, n_peers: int | None = None):
+        """ACKs of the first n_peers virtual peers (default all) to this round's INVs"""
         check(_L.hkv_wl_peer_acks(_ptr(self.inv_out), _ptr(self.inv_count), self.W, self.C, self.op,
                                   _ptr(self.acks), self.ack_size, self.ack_width, _ptr(self.ack_count),
-                                  _ptr(self.peer_t), self.R, _s()), "peer_acks")
+                                  _ptr(self.peer_t), self.R if n_peers is None else n_peers, _s()), "peer_acks")
 
     def inv_batch(self, invs: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None):
         self.kvs.batch(L.BatchType.invs, invs, n_batches, stride, self.op, self.mb, counts=counts)
@@ -200,8 +214,10 @@ class Round:
         self.kvs.batch(L.BatchType.vals, vals, n_batches, stride, L.OP_META_SIZE, self.mb, counts=counts)
 
     # -- a whole round with virtual peers
-    def step(self, events: dict | None = None, timed_batches=("local", "invs", "acks", "vals")):
-        """One round of every virtual worker. `events` (name -> list) collects (start, end)
+    def step(self, events: dict | None = None, timed_batches=("local", "invs", "acks", "vals"),
+             drop: int | None = None):
+        """One round of every virtual worker. `drop`: the last virtual peer fails in this round
+        after sending its INVs (no ACKs, no VALs from it); the round ends with membership_change. `events` (name -> list) collects (start, end)
         torch.cuda.Event pairs for the batches named in `timed_batches` (each event record costs
         a few microseconds of GPU time, so a timed region records only what it reports)."""
         def timed(name, fn):
@@ -215,6 +231,10 @@ class Round:
             events.setdefault(name, []).append((a, b))
 
         k = self.clock % max(len(self.remote_inv), 1)
+        if drop is not None:
+            assert self.virtual and self.alive and drop == self.peers[self.alive - 1], "drop the last live peer"
+        sent = self.alive                          # peers whose INVs this round applies
+        alive = self.alive - (drop is not None)    # peers that answer them (ACKs) and send VALs
         timed("local", self.local_batch)
         self.marshal_invs()
         if self.count_elems:
@@ -224,22 +244,56 @@ class Round:
             self.maxc_ev.record()
         if self.R:
             ri, rv = self.remote_inv[k], self.remote_val[k]
-            timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride))
+            ic = self._slot_counts(sent)
+            timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride, counts=ic))
             self.marshal_acks(ri, self.W * self.rstride, self.ack_out)
+            m = self.C
             if self.fit:   # the GPU is still on the INV batch: this wait leaves no gap on the stream
                 self.maxc_ev.synchronize()
-                self.ack_width = max(1, min(int(self.maxc_h[0]), self.C)) * self.R
-            self.virtual_peer_acks()
-            timed("acks", self.ack_batch)
+                m = min(int(self.maxc_h[0]), self.C)
+            if alive:
+                self.ack_width = max(1, m) * alive
+                self.virtual_peer_acks(alive)
+                timed("acks", self.ack_batch)
+                if self.count_elems:
+                    self.elem_totals[1] += self.ack_count.sum()
+                self.collect_vals()
+            # a dropped peer sent its INVs but fails before its VALs
+            vc = self._slot_counts(alive)
+            timed("vals", lambda: self.val_batch(rv, self.W, self.rstride, counts=vc))
             if self.count_elems:
-                self.elem_totals[1] += self.ack_count.sum()
-            self.collect_vals()
-            timed("vals", lambda: self.val_batch(rv, self.W, self.rstride))
+                self.elem_totals[0] += self.W * sent * self.rpp
+                self.elem_totals[2] += self.W * alive * self.rpp
+        if drop is not None:
+            self.membership_change(drop)
         self.refill()
-        if self.R and self.count_elems:
-            self.elem_totals[0] += self.W * self.rstride
-            self.elem_totals[2] += self.W * self.rstride
         self.clock += 1
+
+    def _slot_counts(self, n_peers: int):
+        """Per-worker counts applying the first n_peers slots of the [W][R][rpp] remote slabs
+        (None: all of them)"""
+        if n_peers == self.R:
+            return None
+        if n_peers not in self._counts:
+            self._counts[n_peers] = torch.full((self.W,), n_peers * self.rpp, dtype=torch.int32,
+                                               device=self.inv_count.device)
+        return self._counts[n_peers]
+
+    def membership_change(self, peer: int):
+        """The group drops `peer` (group_membership_update, inline-util.h:26-43) and every worker
+        runs the after-membership-change batch on its ops (hermes_worker.c:526-542): writes and
+        replays that waited only for the dropped peer's ACK complete, and their VALs go out
+        (hkv_wl_marshal_memb_vals). From now on the peer's slot of the remote slabs is not applied;
+        reads of keys it left INVALID replay the write (early value propagation)."""
+        g = self.mb[1] & ~(1 << peer) & 0xFF
+        self.mb = L.membership(0, self.machine_id, alive=g)
+        self.kvs.batch(L.BatchType.local_ops_after_membership_change, self.ops, self.W, self.LOCAL, self.op, self.mb)
+        check(_L.hkv_wl_marshal_memb_vals(_ptr(self.ops), self.W, self.LOCAL, self.op, _ptr(self.val_out),
+                                          self.ack_stride, _ptr(self.val_count), self.machine_id, _s()),
+              "marshal_memb_vals")
+        self.drops.append(peer)
+        self.alive -= 1
+        self.fit = self.fit and self.alive > 0
 
     def committed(self) -> int:
         return int(self.counters[0].item())

@@ -10,6 +10,7 @@
  *                         inv_copy_and_modify_elem, hermes_worker.c:12-65
  *   hkv_wl_marshal_acks   ack_skip_or_get_sender_id / ack_copy_and_modify_elem, :69-118
  *   hkv_wl_marshal_vals   val_skip_or_get_sender_id / val_copy_and_modify_elem, :122-157
+ *   hkv_wl_marshal_memb_vals  memb_change_* callbacks, :163-203
  *   hkv_wl_peer_acks      the ACKs `n_peers` replicas answer to a slab of INVs (the remote
  *                         side of hermes_worker.c:467-473 for INVs they accept)
  *   hkv_wl_gen_remote     INVs + VALs written by virtual peer replicas (a coordinator's
@@ -91,6 +92,15 @@ int hkv_wl_gen_remote(uint8_t *d_invs, uint8_t *d_vals, int32_t n_workers, int32
                       uint32_t shift, const hkv_zipf *zipf, uint32_t clock, uint64_t seed, void *stream);
 
 /* ---- replica groups (one replica per GPU, slabs exchanged over RCCL) ------------------ */
+
+/* VALs of the writes/replays a membership change completed (memb_change_* callbacks,
+ * hermes_worker.c:163-203): per worker w, ops in state PUT/RMW/REPLAY_COMPLETE_SEND_VALS are
+ * compacted in op order into d_val_out[w*out_stride ...] (16-B VALs: the op's key and ts,
+ * ST_OP_VAL, sender machine_id), d_count[w] = how many (at most out_stride); the ops become
+ * PUT_COMPLETE / RMW_COMPLETE / ST_NEW. stride <= 256. */
+int hkv_wl_marshal_memb_vals(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size,
+                             uint8_t *d_val_out, int32_t out_stride, int32_t *d_count, uint32_t machine_id,
+                             void *stream);
 
 /* hkv_wl_marshal_invs with at most out_stride INVs per worker per round (d_inv_out rows of
  * out_stride); further sendable ops keep their state for a later round and are counted in

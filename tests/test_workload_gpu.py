@@ -76,3 +76,38 @@ def test_full_size_round_invariants():
     st = r.stats()
     assert st["invs_held"] == 0 and st["committed"] > 2_000_000 and st["writes_completed"] > 300_000, st
     assert g.take_error_flags() == 0
+
+
+@pytest.mark.parametrize("machines", [3, 8])
+def test_membership_change_round_mirrored(machines):
+    """BASELINE configs[4] on one GPU: the last virtual peer fails in round 2 after sending its
+    INVs (no ACKs, no VALs from it), the group drops it and every worker runs the
+    after-membership-change batch (hermes_worker.c:526-542); later rounds replay the writes it
+    left INVALID. Every launch, including the after-change batch, is mirrored into the oracle."""
+    from hermes_amd.kvs import HermesKV
+    from hermes_amd.workload import Round, zipf_params
+    n_keys, bkts, cap = 60_000, 1 << 16, 1 << 23
+    g = HermesKV(n_keys, bkts, cap, machine_id=0)
+    o = OracleKVS(bkts, cap, 0)
+    o.populate(n_keys, g.sizes.kvs_value)
+    m = Mirror(g, o, "membership round")
+    peers = list(range(1, machines))
+    r = Round(g, 40, L.membership(machines, 0), peers, zipf_params(n_keys, 0.99), 200, seed=0x5EED,
+              max_steps=8, trace_len=1024, remote_per_peer=20)
+    op = g.sizes.op
+    replays = []
+    marshal = r.marshal_invs
+
+    def counting_marshal():
+        replays.append(int((r.ops.view(-1, op)[:, 9] == int(L.Resp.REPLAY_SUCCESS)).sum()))
+        marshal()
+    r.marshal_invs = counting_marshal
+    for step in range(6):
+        r.step(drop=peers[-1] if step == 2 else None)
+    torch.cuda.synchronize()
+    assert m.launches == 6 * 4 + 1
+    assert r.mb[1] == ((1 << machines) - 1) & ~(1 << peers[-1]) and r.alive == machines - 2
+    st = r.stats()
+    assert st["committed"] > 0 and st["writes_completed"] > 0, st
+    assert sum(replays[3:]) > 0, replays
+    assert g.take_error_flags() == 0

@@ -112,8 +112,8 @@ def main():
     cfg5 = a.config == "cfg5"
     if a.keys is None:  # cfg3: 320-B entries; 10M keys keep log offsets within 32-bit entry ids
         a.keys = 10_000_000 if cfg3 else 100_000_000 if world == 1 and not cfg5 else 1_000_000_000
-    if (cfg3 or cfg5) and world > 1:
-        raise SystemExit(f"--config {a.config} runs on one GPU with virtual peers")
+    if cfg3 and world > 1:
+        raise SystemExit("--config cfg3 runs on one GPU with virtual peers")
     if a.write_permille is None:
         a.write_permille = 500 if cfg3 else 200
     if a.rmw_permille is None:
@@ -160,13 +160,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    drop_at = a.steps // 2 if cfg5 else -1   # cfg5: the last peer fails in this timed step
+    drop_at = a.steps // 2 if cfg5 else -1   # cfg5: the last replica fails in this timed step
+    drop_id = world - 1 if world > 1 else 7
     t = time.perf_counter()
     for k in range(a.steps):
         # HIP events around the local launch (the roofline's) on every EVENT_EVERY-th step: each
         # record costs ~5 us of GPU time between kernels; the other launches: probe step below
         rnd.step(events if k % EVENT_EVERY == 0 else None, timed_batches=("local",),
-                 drop=rnd.peers[-1] if k == drop_at else None)
+                 drop=drop_id if k == drop_at else None)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -233,8 +234,10 @@ def main():
         "dtype": "u8",
         "data": "synthetic (seeded Zipf traces, CityHash keys, virtual or RCCL peers)",
         "config": {
-            "workload": (f"cfg5: 1xMI355X, 8-replica group (7 virtual peers), {a.keys} keys, 20% writes, "
-                         f"peer 7 fails in timed step {drop_at} (membership change, write replays)" if cfg5 else
+            "workload": (f"cfg5: {world}x MI355X, {8 if world == 1 else world}-replica group "
+                         f"({'7 virtual peers' if world == 1 else 'RCCL'}), {a.keys} keys/replica, 20% writes, "
+                         f"replica {drop_id} fails in timed step {drop_at} (membership change, write replays)"
+                         if cfg5 else
                          f"cfg3: 1xMI355X RMW-heavy, {a.keys} keys, RMWs on, 287 B values, Zipf 0.99, 25% PUT + 25% RMW, "
                          "INV/ACK/VAL from 2 virtual replicas" if cfg3 else
                          "cfg2: 1xMI355X, 100M keys, 31 B values, Zipf 0.99, 20% writes, "
@@ -262,8 +265,9 @@ def main():
         },
     }
     if cfg5:
-        out["detail"]["membership"] = {"machines": 8, "dropped": rnd.drops, "at_timed_step": drop_at,
-                                       "g_membership_after": rnd.mb[1]}
+        mb = rnd.mb if world == 1 else rnd.r.mb
+        out["detail"]["membership"] = {"machines": 8 if world == 1 else world, "dropped": drop_id,
+                                       "at_timed_step": drop_at, "g_membership_after": mb[1]}
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0 and world == 1 and a.host_api_seconds > 0:

@@ -47,6 +47,8 @@ _L.hkv_wl_collect_vals.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctype
 _L.hkv_wl_pack_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_marshal_acks_aligned.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P,
                                            ctypes.c_uint32, ctypes.c_uint32, _P]
+_L.hkv_wl_marshal_memb_vals.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
+                                        ctypes.c_uint32, _P]
 _L.hkv_wl_regroup_aligned.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_uint32,
                                       _P, ctypes.c_int32, _P, _P]
 
@@ -107,16 +109,29 @@ class ReplicaRound:
         check(_L.hkv_wl_gen_trace(_ptr(self.trace_key), _ptr(self.trace_op), None, W, trace_len,
                                   ctypes.byref(zipf), write_permille, rmw_permille,
                                   ctypes.c_uint64(seed ^ (rank << 48)), _s()), "gen_trace")
+        self.failed = False            # this replica has failed (fail()): it sends nothing more
         self.refill(first=True)
 
     # -- phases (all asynchronous on torch's current stream)
+    def fail(self):
+        """This replica fails after its INVs of the current round went out: from now on it sends
+        no ACKs, VALs or INVs (it still joins the collectives, with empty slabs)."""
+        self.failed = True
+
     def refill(self, first: bool = False):
+        if self.failed:
+            return
         check(_L.hkv_wl_refill(_ptr(self.ops), self.W, LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
                                _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
                                self.rank, int(first), int(not self.retry), _ptr(self.counters), _s()), "refill")
 
     def local(self):
         """Local batch, then this round's INVs, packed (inv_pack; worker w at inv_off[w])."""
+        if self.failed:
+            self.inv_count.zero_()
+            self.inv_off.zero_()
+            self.inv_maxc.zero_()
+            return
         self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, LOCAL, self.op, self.mb)
         check(_L.hkv_wl_marshal_invs_cap(_ptr(self.ops), self.W, LOCAL, self.op, _ptr(self.inv_slab), self.C,
                                          _ptr(self.inv_count), self.rank, _ptr(self.held), _s()), "marshal_invs")
@@ -156,6 +171,9 @@ class ReplicaRound:
         """Apply the gathered INVs of the peers ([N][width], row p: inv_totals[p] INVs) as N
         batches; their ACKs go into ack_slab in the positions of the INVs they answer."""
         self.inv_totals[self.rank] = 0
+        if self.failed:   # no ACKs from a failed replica
+            self.ack_slab[:self.N * width * self.ack_size].view(-1, self.ack_size)[:, 8] = int(L.Bucket.EMPTY)
+            return
         if self.count_elems:
             self.elem_totals[0] += self.inv_totals.sum()
         self.kvs.batch(L.BatchType.invs, self.inv_recv, self.N, width, self.op, self.mb, counts=self.inv_totals)
@@ -167,6 +185,9 @@ class ReplicaRound:
         with inv_pack), regrouped per worker ([W][stride]); the VALs of completed writes, packed
         (val_pack)."""
         N, W, C = self.N, self.W, self.C
+        if self.failed:
+            self.val_off[W:].zero_()
+            return
         check(_L.hkv_wl_regroup_aligned(_ptr(self.ack_recv), N, width, _ptr(self.inv_off), _ptr(self.inv_count), W,
                                         self.ack_size, _ptr(self.ack_batch), stride, _ptr(self.ack_batch_count),
                                         _s()), "regroup")
@@ -182,11 +203,34 @@ class ReplicaRound:
 
     def vals(self, width: int):
         """Apply the gathered VALs of the peers ([N][width], row p: val_totals[p] VALs)."""
+        if self.failed:
+            return
         self.val_totals[self.rank] = 0
         if self.count_elems:
             self.elem_totals[2] += self.val_totals.sum()
         self.kvs.batch(L.BatchType.vals, self.val_recv, self.N, width, L.OP_META_SIZE, self.mb,
                        counts=self.val_totals)
+
+    def membership_change(self, peer: int):
+        """The group drops `peer` (group_membership_update, inline-util.h:26-43). Every worker runs
+        the after-membership-change batch over its ops (hermes_worker.c:526-542); the VALs of the
+        writes and replays it completed are packed into val_pack for one more VAL exchange
+        (memb_change_* callbacks, hermes_worker.c:163-203). A failed replica sends none."""
+        W, C = self.W, self.C
+        if self.failed:
+            self.val_off[W:].zero_()
+            return
+        g = self.mb[1] & ~(1 << peer) & 0xFF
+        self.mb = L.membership(0, self.rank, alive=g)
+        self.kvs.batch(L.BatchType.local_ops_after_membership_change, self.ops, W, LOCAL, self.op, self.mb)
+        check(_L.hkv_wl_marshal_memb_vals(_ptr(self.ops), W, LOCAL, self.op, _ptr(self.val_slab), C,
+                                          _ptr(self.val_count), self.rank, _s()), "marshal_memb_vals")
+        check(_L.hkv_wl_pack_rows(_ptr(self.val_slab), _ptr(self.val_count), W, C, L.OP_META_SIZE,
+                                  _ptr(self.val_pack), _ptr(self.val_off), _s()), "pack memb vals")
+
+    def val_width(self) -> int:
+        """After the VAL totals are gathered (host synchronisation): the largest of them"""
+        return max(1, int(self.val_totals.max().item()))
 
     def stats(self) -> dict:
         c = self.counters[:3].cpu().tolist()
@@ -239,18 +283,29 @@ class ReplicaGroupRound:
     def _a2a(self, out, inp):
         self.dist.all_to_all_single(out, inp, group=self.group)
 
-    def step(self, events: dict | None = None, timed_batches=None):
+    def step(self, events: dict | None = None, timed_batches=None, drop: int | None = None):
+        """One protocol round. `drop`: that rank fails once its INVs of this round are out (no
+        ACKs or VALs from it); the round ends with a membership change and one more VAL
+        exchange for the writes it completes."""
         r = self.r
         _timed(events, "local", r.local, timed_batches)
         self._gather(*r.inv_total_io())
         width, stride = r.round_shape()  # the round's one host synchronisation
         self._gather(*r.inv_io(width))
+        if drop is not None and drop == r.rank:
+            r.fail()
         _timed(events, "invs", lambda: r.invs(width), timed_batches)
         self._a2a(*r.ack_io(width))
         _timed(events, "acks", lambda: r.acks(width, stride), timed_batches)
         self._gather(*r.val_total_io())
         self._gather(*r.val_io(width))
         _timed(events, "vals", lambda: r.vals(width), timed_batches)
+        if drop is not None:
+            r.membership_change(drop)
+            self._gather(*r.val_total_io())
+            w2 = r.val_width()
+            self._gather(*r.val_io(w2))
+            r.vals(w2)
         r.refill()
 
     def stats(self) -> dict:
@@ -284,7 +339,7 @@ class LoopbackGroup:
     def _a2a_io(self, ios):
         self._a2a([o for o, _ in ios], [i for _, i in ios])
 
-    def step(self):
+    def step(self, drop: int | None = None):
         rs = self.rounds
         for r in rs:
             r.local()
@@ -292,6 +347,8 @@ class LoopbackGroup:
         shapes = [r.round_shape() for r in rs]
         width = shapes[0][0]                 # the same on every replica (max of the same totals)
         self._gather_io([r.inv_io(width) for r in rs])
+        if drop is not None:
+            rs[drop].fail()
         for r in rs:
             r.invs(width)
         self._a2a_io([r.ack_io(width) for r in rs])
@@ -301,5 +358,13 @@ class LoopbackGroup:
         self._gather_io([r.val_io(width) for r in rs])
         for r in rs:
             r.vals(width)
+        if drop is not None:
+            for r in rs:
+                r.membership_change(drop)
+            self._gather_io([r.val_total_io() for r in rs])
+            w2 = rs[0].val_width()
+            self._gather_io([r.val_io(w2) for r in rs])
+            for r in rs:
+                r.vals(w2)
         for r in rs:
             r.refill()

@@ -23,8 +23,11 @@ def _tag(kind, a, b, w, j):
 class TagReplica:
     """Stand-in for ReplicaRound with the same exchange interface (int64 tags for elements)."""
 
-    def __init__(self, world, rank, W=5, C=7):
+    def __init__(self, world, rank, W=5, C=7, drop=None):
         self.N, self.rank, self.W, self.C = world, rank, W, C
+        self.drop = drop        # (rank, round): that rank fails in that round after its INVs (checks only)
+        self.failed = False
+        self.in_memb = False
         N = world
         z = lambda *s: torch.zeros(*s, dtype=torch.int64)  # noqa: E731
         zi = lambda *s: torch.zeros(*s, dtype=torch.int32)  # noqa: E731
@@ -40,8 +43,14 @@ class TagReplica:
         self.checked = 0
         self.round = 0
 
+    def dead(self, p, after=False):
+        """p has failed by this round (after=True: before this round's INVs)"""
+        return self.drop is not None and p == self.drop[0] and self.round >= self.drop[1] + int(after)
+
     def count(self, origin, w):
-        return (origin + w + self.round) % self.C
+        if self.in_memb:
+            return 0 if self.dead(origin) else (origin + w) % 3
+        return 0 if self.dead(origin, after=True) else (origin + w + self.round) % self.C
 
     def _pack(self, slab, off, kind):
         k = 0
@@ -58,6 +67,21 @@ class TagReplica:
 
     def local(self):
         self._pack(self.inv_pack, self.inv_off, 1)
+
+    def fail(self):
+        assert self.drop == (self.rank, self.round)
+        self.failed = True
+
+    def membership_change(self, peer):
+        assert self.drop == (peer, self.round)
+        self.in_memb = True
+        if self.failed:
+            self.val_off.zero_()
+            return
+        self._pack(self.val_pack, self.val_off, 4)
+
+    def val_width(self):
+        return max(1, int(self.val_totals.max()))
 
     def inv_total_io(self):
         return self.inv_totals, self.inv_off[self.W:]
@@ -81,6 +105,8 @@ class TagReplica:
         self.inv_totals[self.rank] = 0
         rv, av = self.inv_recv[:self.N * width].view(self.N, width), self.ack_slab[:self.N * width].view(self.N, width)
         av.fill_(-1)                                     # ST_EMPTY where no ACK
+        if self.failed:
+            return
         for p in range(self.N):
             n = int(self.inv_totals[p])
             rows = self._rows(p)
@@ -93,10 +119,13 @@ class TagReplica:
 
     def acks(self, width, stride):
         rv = self.ack_recv[:self.N * width].view(self.N, width)
+        if self.failed:
+            self.val_off.zero_()
+            return
         mine = self._rows(self.rank)
         for p in range(self.N):
             for k in range(width):
-                if p != self.rank and k < len(mine):
+                if p != self.rank and k < len(mine) and not self.dead(p):
                     w, j = mine[k]
                     assert int(rv[p, k]) == _tag(2, p, self.rank, w, j)
                     self.checked += 1
@@ -105,29 +134,32 @@ class TagReplica:
         self._pack(self.val_pack, self.val_off, 3)
 
     def vals(self, width):
+        if self.failed:
+            return
         self.val_totals[self.rank] = 0
         rv = self.val_recv[:self.N * width].view(self.N, width)
         for p in range(self.N):
             n = int(self.val_totals[p])
             rows = self._rows(p)
-            assert n == (0 if p == self.rank else len(rows))
+            assert n == (0 if p == self.rank or self.dead(p) else len(rows))
             for k in range(n):
                 w, j = rows[k]
-                assert int(rv[p, k]) == _tag(3, p, 0, w, j)
+                assert int(rv[p, k]) == _tag(4 if self.in_memb else 3, p, 0, w, j)
                 self.checked += 1
 
     def refill(self):
         self.round += 1
+        self.in_memb = False
 
 
-def _worker(rank, world, port, rounds, q):
+def _worker(rank, world, port, rounds, q, drop=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        rep = TagReplica(world, rank)
+        rep = TagReplica(world, rank, drop=drop)
         drv = ReplicaGroupRound(None, rep.W, None, world=world, rank=rank, replica=rep)
-        for _ in range(rounds):
-            drv.step()
+        for k in range(rounds):
+            drv.step(drop=drop[0] if drop is not None and k == drop[1] else None)
         q.put((rank, rep.checked, None))
     except Exception as e:  # surfaced by the parent
         q.put((rank, 0, repr(e)))
@@ -143,13 +175,15 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_rccl_choreography_gloo(world):
+@pytest.mark.parametrize("world,drop", [(2, None), (3, None), (3, (2, 1)), (4, (1, 1))])
+def test_rccl_choreography_gloo(world, drop):
+    """drop = (rank, round): that rank fails in that round once its INVs are out; the others
+    see no ACKs or VALs from it, the membership-change VAL exchange, and no INVs from it later."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    rounds = 3
+    rounds = 4 if drop else 3
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, rounds, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, rounds, q, drop)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
@@ -160,12 +194,13 @@ def test_rccl_choreography_gloo(world):
         assert checked > 0
 
 
-def test_loopback_matches_choreography():
+@pytest.mark.parametrize("drop", [None, (2, 1)])
+def test_loopback_matches_choreography(drop):
     world = 3
-    reps = [TagReplica(world, r) for r in range(world)]
+    reps = [TagReplica(world, r, drop=drop) for r in range(world)]
     grp = LoopbackGroup(reps)
-    for _ in range(3):
-        grp.step()
+    for k in range(4):
+        grp.step(drop=drop[0] if drop is not None and k == drop[1] else None)
     assert all(r.checked > 0 for r in reps)
 
 

@@ -82,7 +82,59 @@ def test_loopback_group_parity_and_convergence(n_rep, workers, write_pm, rounds)
     assert inv_applied == inv_sent * (n_rep - 1)
 
 
-def _dist_child(rank, world, port, q):
+@pytest.mark.parametrize("n_rep", [3, 4])
+def test_loopback_group_membership_change(n_rep):
+    """BASELINE configs[4] in the replica group: the last replica fails in round 1 after its INVs
+    are out (no ACKs, no VALs from it). The others drop it from the membership, run the
+    after-membership-change batch and exchange the VALs of the writes it completes; later rounds
+    replay the writes the failed replica left INVALID. Every launch is mirrored into the oracle;
+    after every round the live replicas agree on every key (state, timestamp, value), and a key
+    is either VALID or INVALID with the failed replica's write."""
+    from hermes_amd.kvs import HermesKV
+    from hermes_amd.replica_group import LoopbackGroup, ReplicaRound
+    from hermes_amd.workload import zipf_params
+
+    n_keys, bkts, cap = 4000, 8192, 1 << 20
+    z = zipf_params(n_keys, 0.99)
+    reps, mirrors = [], []
+    for r in range(n_rep):
+        g = HermesKV(n_keys, bkts, cap, machine_id=r)
+        o = OracleKVS(bkts, cap, r)
+        o.populate(n_keys, L.DEFAULT.kvs_value)
+        mirrors.append(Mirror(g, o, f"replica {r}"))
+        reps.append(ReplicaRound(g, 16, n_rep, r, z, 400, seed=55 + r, trace_len=512))
+    grp = LoopbackGroup(reps)
+    keys = gen_keys(n_keys)
+    dead = n_rep - 1
+    invalid_after = []
+    for step in range(5):
+        grp.step(drop=dead if step == 1 else None)
+        torch.cuda.synchronize()
+        imgs = [_key_images(m.g, m.o, keys) for m in mirrors[:dead]]
+        n_inv = 0
+        for i in range(len(keys)):
+            base = imgs[0][i]
+            for r in range(1, dead):
+                assert imgs[r][i] == base, f"round {step}: key #{i} differs between replica 0 and {r}"
+            if base is None:
+                continue
+            if step < 1:
+                assert base[0] == L.State.VALID
+            else:
+                assert base[0] in (L.State.VALID, L.State.INVALID), f"round {step}: key #{i} state {base[0]}"
+                if base[0] == L.State.INVALID:
+                    assert base[1] == dead, f"round {step}: key #{i} INVALID by {base[1]}"
+                    n_inv += 1
+        invalid_after.append(n_inv)
+    assert invalid_after[1] > 0, invalid_after            # the failed replica's last writes
+    assert invalid_after[-1] < invalid_after[1], invalid_after   # reads replayed some of them
+    for rep in reps[:dead]:
+        assert rep.mb[1] == ((1 << n_rep) - 1) & ~(1 << dead)
+        st = rep.stats()
+        assert st["invs_held"] == 0 and st["vals_dropped"] == 0 and st["writes_completed"] > 0, st
+
+
+def _dist_child(rank, world, port, q, drop=None):
     import os
 
     import torch.distributed as dist
@@ -97,8 +149,8 @@ def _dist_child(rank, world, port, q):
         g = HermesKV(n_keys, 8192, 1 << 20, machine_id=rank)
         drv = ReplicaGroupRound(g, 16, zipf_params(n_keys, 0.99), 400, seed=99, world=world, rank=rank,
                                 trace_len=512)
-        for _ in range(3):
-            drv.step()
+        for k in range(4 if drop is not None else 3):
+            drv.step(drop=drop if k == 1 else None)
         torch.cuda.synchronize()
         log = g.log_bytes()
         imgs = []
@@ -115,8 +167,8 @@ def _dist_child(rank, world, port, q):
         q.put((rank, None, None, 0, repr(e)))
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_dist_group_driver_one_gpu(world):
+@pytest.mark.parametrize("world,drop", [(2, None), (3, None), (3, 2)])
+def test_dist_group_driver_one_gpu(world, drop):
     """ReplicaGroupRound itself (the driver bench.py runs over RCCL), with `world` processes
     sharing one GPU over gloo (which takes CUDA tensors): every key converges across ranks."""
     import socket
@@ -128,7 +180,7 @@ def test_dist_group_driver_one_gpu(world):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dist_child, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_dist_child, args=(r, world, port, q, drop)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in procs], key=lambda x: x[0])
@@ -138,10 +190,14 @@ def test_dist_group_driver_one_gpu(world):
         assert err is None, f"rank {rank}: {err}"
         assert flags == 0
         assert st["invs_held"] == 0 and st["vals_dropped"] == 0 and st["writes_completed"] > 0, st
-    base = res[0][1]
+    live = [x for x in res if x[0] != drop]     # a failed rank's table no longer follows the group
+    base = live[0][1]
     for i, b in enumerate(base):
         if b is None:
             continue
-        assert b[0] == L.State.VALID, f"key #{i} state {b[0]}"
-        for rank, imgs, *_ in res[1:]:
-            assert imgs[i] == b, f"key #{i} differs between rank 0 and rank {rank}"
+        if drop is None:
+            assert b[0] == L.State.VALID, f"key #{i} state {b[0]}"
+        else:   # INVALID only where the failed rank's last write was never validated
+            assert b[0] == L.State.VALID or (b[0] == L.State.INVALID and b[1] == drop), f"key #{i} {b[:3]}"
+        for rank, imgs, *_ in live[1:]:
+            assert imgs[i] == b, f"key #{i} differs between rank {live[0][0]} and rank {rank}"

@@ -251,6 +251,25 @@ __global__ __launch_bounds__(256) void k_marshal_memb_vals(uint8_t *ops, int32_t
     op[9] = st == kPutCompleteSendVals ? kPutComplete : st == kRmwCompleteSendVals ? kRmwComplete : kNew;
 }
 
+// The largest of n counts, stored straight into pinned host memory (one workgroup): the host
+// reads a round's ACK width without a reduction kernel and a copy.
+__global__ __launch_bounds__(1024) void k_max_to_host(const int32_t *counts, int32_t n, int32_t *out)
+{
+    __shared__ int32_t part[16];
+    int32_t m = 0;
+    for (int32_t i = threadIdx.x; i < n; i += 1024) m = counts[i] > m ? counts[i] : m;
+    for (int o = 32; o > 0; o >>= 1) {
+        const int32_t u = __shfl_down(m, o, 64);
+        m = u > m ? u : m;
+    }
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < 16; ++k) m = part[k] > m ? part[k] : m;
+        *out = m;
+    }
+}
+
 // ACKs for received INV rows: row r holds in_count[r] INVs (row stride C); its ACKs are
 // compacted to the front of output row r (ack_skip_or_get_sender_id + ack_copy_and_modify_elem
 // + ack_modify_elem_after_send, hermes_worker.c:67-110)
@@ -607,6 +626,15 @@ int hkv_wl_marshal_memb_vals(uint8_t *ops, int32_t n_workers, int32_t stride, ui
     if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
     hipLaunchKernelGGL(k_marshal_memb_vals, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
                        out, out_stride, count, machine_id);
+    return ok();
+}
+
+int hkv_wl_max_to_host(const int32_t *counts, int32_t n, int32_t *h_out, void *stream)
+{
+    if (n <= 0) return -1;
+    int32_t *d_out = nullptr;
+    if (hipHostGetDevicePointer(reinterpret_cast<void **>(&d_out), h_out, 0) != hipSuccess || !d_out) return -1;
+    hipLaunchKernelGGL(k_max_to_host, dim3(1), dim3(1024), 0, (hipStream_t)stream, counts, n, d_out);
     return ok();
 }
 

@@ -38,6 +38,7 @@ _L.hkv_wl_marshal_invs_cap.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctype
 _L.hkv_wl_marshal_acks.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_memb_vals.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
                                         ctypes.c_uint32, _P]
+_L.hkv_wl_max_to_host.argtypes = [_P, ctypes.c_int32, _P, _P]
 _L.hkv_wl_marshal_vals.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_collect_vals.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
                                    _P, ctypes.c_uint32, _P, _P]
@@ -240,7 +241,7 @@ class Round:
         if self.count_elems:
             self.inv_total += self.inv_count.sum()
         if self.fit:
-            self.maxc_h.copy_(self.inv_count.max().view(1), non_blocking=True)
+            check(_L.hkv_wl_max_to_host(_ptr(self.inv_count), self.W, _ptr(self.maxc_h), _s()), "max_to_host")
             self.maxc_ev.record()
         if self.R:
             ri, rv = self.remote_inv[k], self.remote_val[k]

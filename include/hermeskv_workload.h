@@ -102,6 +102,10 @@ int hkv_wl_marshal_memb_vals(uint8_t *d_ops, int32_t n_workers, int32_t stride, 
                              uint8_t *d_val_out, int32_t out_stride, int32_t *d_count, uint32_t machine_id,
                              void *stream);
 
+/* *h_out = max(d_counts[0..n)), written by the kernel into pinned host memory (hipHostMalloc /
+ * hipHostRegister; valid once the stream passes this call): a round's width without a copy. */
+int hkv_wl_max_to_host(const int32_t *d_counts, int32_t n, int32_t *h_out, void *stream);
+
 /* hkv_wl_marshal_invs with at most out_stride INVs per worker per round (d_inv_out rows of
  * out_stride); further sendable ops keep their state for a later round and are counted in
  * *d_held (may be NULL). */

@@ -230,9 +230,7 @@ int hkv_table_destroy(hkv_table *t)
     hipFree(t->d_fw);
     hipFree(t->d_error_flags);
     hipFree(t->d_ns_idx);
-    hipFree(t->d_stage_ops);
-    hipFree(t->d_stage_rw);
-    hipFree(t->d_stage_ns);
+    hipFree(t->d_stage_ops);  // rw and node_suspected staging live in the same region
     hipHostFree(t->h_stage);
     if (t->stream) hipStreamDestroy(t->stream);
     delete t;
@@ -496,30 +494,34 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
     if (ops_bytes > t->stage_ops_cap || (with_rw && rw_bytes > t->stage_rw_cap) || !t->d_stage_ns) {
         size_t oc = ops_bytes > t->stage_ops_cap ? ops_bytes : t->stage_ops_cap;
         size_t rc = rw_bytes > t->stage_rw_cap ? rw_bytes : t->stage_rw_cap;
+        oc = (oc + 255) & ~(size_t)255;
+        rc = (rc + 255) & ~(size_t)255;
         hipFree(t->d_stage_ops);
-        hipFree(t->d_stage_rw);
-        hipFree(t->d_stage_ns);
         hipHostFree(t->h_stage);
         t->d_stage_ops = t->d_stage_rw = nullptr;
         t->d_stage_ns = nullptr;
         t->h_stage = nullptr;
         t->stage_ops_cap = t->stage_rw_cap = 0;
-        if (hipMalloc(&t->d_stage_ops, oc) != hipSuccess || hipMalloc(&t->d_stage_rw, rc) != hipSuccess ||
-            hipMalloc(&t->d_stage_ns, 64) != hipSuccess ||
+        // one device region laid out like the pinned mirror (ops | rw | node_suspected), so each
+        // call moves one contiguous range each way
+        if (hipMalloc(&t->d_stage_ops, oc + rc + 64) != hipSuccess ||
             hipHostMalloc((void **)&t->h_stage, oc + rc + 64, hipHostMallocDefault) != hipSuccess)
             die("staging alloc");
+        t->d_stage_rw = t->d_stage_ops + oc;
+        t->d_stage_ns = reinterpret_cast<int32_t *>(t->d_stage_ops + oc + rc);
         t->stage_ops_cap = oc;
         t->stage_rw_cap = rc;
     }
     uint8_t *h_ops = t->h_stage, *h_rw = t->h_stage + t->stage_ops_cap;
     int32_t *h_ns = reinterpret_cast<int32_t *>(t->h_stage + t->stage_ops_cap + t->stage_rw_cap);
     hipStream_t s = t->stream;
+    const bool with_ns = type == invs && node_suspected != nullptr;
     memcpy(h_ops, op_array, ops_bytes);
     if (with_rw) memcpy(h_rw, read_write_ops, rw_bytes);
-    *h_ns = node_suspected ? *node_suspected : -1;
-    if (hipMemcpyAsync(t->d_stage_ops, h_ops, ops_bytes, hipMemcpyHostToDevice, s) != hipSuccess) die("copy in");
-    if (with_rw && hipMemcpyAsync(t->d_stage_rw, h_rw, rw_bytes, hipMemcpyHostToDevice, s) != hipSuccess) die("copy in");
-    if (hipMemcpyAsync(t->d_stage_ns, h_ns, 4, hipMemcpyHostToDevice, s) != hipSuccess) die("copy in");
+    if (with_ns) *h_ns = *node_suspected;
+    const size_t span = with_ns ? t->stage_ops_cap + t->stage_rw_cap + 4
+                      : with_rw ? t->stage_ops_cap + rw_bytes : ops_bytes;
+    if (hipMemcpyAsync(t->d_stage_ops, h_ops, span, hipMemcpyHostToDevice, s) != hipSuccess) die("copy in");
     hkv_batch_desc d;
     memset(&d, 0, sizeof d);
     d.type = (int32_t)type;
@@ -528,14 +530,12 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
     d.elem_size = sizeof_op_elem;
     d.d_elems = t->d_stage_ops;
     d.d_rw = with_rw ? t->d_stage_rw : nullptr;
-    d.d_node_suspected = (type == invs && node_suspected) ? t->d_stage_ns : nullptr;
+    d.d_node_suspected = with_ns ? t->d_stage_ns : nullptr;
     memcpy(d.membership, &curr_membership, 8);
     TRACE("staged in; launching");
     if (hkv_batch_async(t, &d, s)) die("hermes_batch_ops_to_KVS");
     TRACE("launched");
-    if (hipMemcpyAsync(h_ops, t->d_stage_ops, ops_bytes, hipMemcpyDeviceToHost, s) != hipSuccess) die("copy out");
-    if (with_rw && hipMemcpyAsync(h_rw, t->d_stage_rw, rw_bytes, hipMemcpyDeviceToHost, s) != hipSuccess) die("copy out");
-    if (d.d_node_suspected && hipMemcpyAsync(h_ns, t->d_stage_ns, 4, hipMemcpyDeviceToHost, s) != hipSuccess) die("copy out");
+    if (hipMemcpyAsync(h_ops, t->d_stage_ops, span, hipMemcpyDeviceToHost, s) != hipSuccess) die("copy out");
     if (hipStreamSynchronize(s) != hipSuccess) die("sync");
     memcpy(op_array, h_ops, ops_bytes);
     if (with_rw) memcpy(read_write_ops, h_rw, rw_bytes);

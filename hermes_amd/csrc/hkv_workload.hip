@@ -185,6 +185,59 @@ __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, ui
     for (int k = i; k < words; k += 256) gslab[k] = slab[k];
 }
 
+// k_refill for big ops (312 B): staging a 78-KB slab per workgroup caps occupancy at two
+// workgroups per CU, so each thread edits its own op in place instead -- the same bytes as
+// k_refill (key, opcode, state, val_len, flags, and the value of a write), 8-B stores.
+__global__ __launch_bounds__(256) void k_refill_direct(uint8_t *ops, int32_t stride, uint32_t op_size,
+                                                       uint32_t st_value, uint32_t shift, const uint64_t *tkey,
+                                                       const uint8_t *top, int32_t tlen, uint32_t *cursor,
+                                                       uint32_t machine_id, int32_t first_iter, int32_t refill_all,
+                                                       unsigned long long *counters)
+{
+    const int w = blockIdx.x, i = threadIdx.x;
+    const bool live = i < stride;
+    uint8_t *op = ops + ((int64_t)w * stride + (live ? i : 0)) * op_size;
+    const uint8_t st = live ? op[9] : 0;
+    const bool complete = st == kMiss || st == kPutComplete || st == kRmwAbort || st == kRmwComplete ||
+                          st == kOpMembComplete || st == kGetComplete;
+    const bool done = live && (first_iter || refill_all || complete);
+    const int commits = (live && complete && !first_iter && st != kMiss && st != kRmwAbort) ? 1 : 0;
+    const int misses = (live && !first_iter && st == kMiss) ? 1 : 0;
+    const int writes = (live && !first_iter && st == kPutComplete) ? 1 : 0;
+    int total;
+    const int rank = block_rank(done, total);
+    const uint32_t base = cursor[w];
+    const int c = block_sum(commits), m = block_sum(misses), wr = block_sum(writes);
+    if (i == 0) {
+        cursor[w] = (uint32_t)((base + (uint32_t)total) % (uint32_t)tlen);
+        unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + (w % kStripes) * 16;
+        if (c) atomicAdd(&stripe[0], (unsigned long long)c);
+        if (m) atomicAdd(&stripe[1], (unsigned long long)m);
+        if (wr) atomicAdd(&stripe[2], (unsigned long long)wr);
+    }
+    if (!done) return;
+    const int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)rank) % (uint32_t)tlen);
+    const uint8_t oc = top[t];
+    *reinterpret_cast<uint64_t *>(op) = tkey[t];
+    // bytes 8..10 (opcode, state, val_len) of the second header word; 11..15 keep their bytes
+    uint64_t *h1 = reinterpret_cast<uint64_t *>(op + 8);
+    const uint64_t vl = oc == kOpGet ? 0 : (uint8_t)(st_value >> shift);
+    *h1 = (*h1 & ~0xFFFFFFull) | oc | ((uint64_t)kNew << 8) | (vl << 16);
+    const uint16_t flags = (uint16_t)((oc == kOpRmw ? 1u : 0u) | (first_iter ? 0u : 2u));  // RMW_flag, no_coales
+    if (oc == kOpGet) {
+        *reinterpret_cast<uint16_t *>(op + 16) = flags;
+        return;
+    }
+    // value bytes 18 .. 18 + st_value: 8-B words from byte 16 (the first carries the flags), then
+    // the tail bytes
+    const uint64_t vv = 0x0101010101010101ull * (uint8_t)('a' + machine_id);
+    const uint32_t end = kOpValueOff + st_value;
+    *reinterpret_cast<uint64_t *>(op + 16) = (uint64_t)flags | (vv << 16);
+    uint32_t k = 24;
+    for (; k + 8 <= end; k += 8) *reinterpret_cast<uint64_t *>(op + k) = vv;
+    for (; k < end; ++k) op[k] = (uint8_t)vv;
+}
+
 // 16 bytes at an 8-byte aligned address: one dwordx4 access (op headers, 16-B messages)
 struct __attribute__((aligned(8))) W16 {
     uint64_t a, b;
@@ -550,6 +603,12 @@ int hkv_wl_refill(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_s
                   int32_t first_iter, int32_t refill_all, unsigned long long *counters, void *stream)
 {
     if (stride > 256 || n_workers <= 0 || op_size % 8) return -1;
+    if (op_size > 64 && st_value >= 6) {  // big ops: in place (see k_refill_direct)
+        hipLaunchKernelGGL(k_refill_direct, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
+                           st_value, shift, tkey, top, tlen, cursor, machine_id, first_iter, refill_all, counters);
+        hipLaunchKernelGGL(k_fold_counters, dim3(1), dim3(256), 0, (hipStream_t)stream, counters);
+        return ok();
+    }
     const size_t lds = (size_t)stride * op_size;
     if (lds > 160 * 1024 - 64) return -1;
     if (lds > 64 * 1024 &&

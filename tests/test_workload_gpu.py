@@ -3,6 +3,7 @@ of a Round over more than kLookupHead (8192) local elements -- so the split look
 absorbing-state shortcut, the INV/ACK rounds and the fallback all run as in bench.py -- is
 mirrored into an oracle table and must be bit-exact (elements, read_write_ops, index, log).
 """
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -111,3 +112,68 @@ def test_membership_change_round_mirrored(machines):
     assert st["committed"] > 0 and st["writes_completed"] > 0, st
     assert sum(replays[3:]) > 0, replays
     assert g.take_error_flags() == 0
+
+
+def _refill_ref(ops, W, S, osz, st_value, shift, tkey, top, tlen, cursor, mid, first, refill_all):
+    """refill_ops (inline-util.h:149-303) as hkv_wl_refill applies it, in numpy: per worker, the
+    completed ops (every op with refill_all / first) take the next trace entries in op order."""
+    ops = ops.copy().reshape(W, S, osz)
+    cursor = cursor.copy()
+    cnt = np.zeros(3, dtype=np.int64)
+    done_states = (130, 128, 138, 137, 119, 121)
+    for w in range(W):
+        rank = 0
+        for i in range(S):
+            o = ops[w, i]
+            st = int(o[9])
+            complete = st in done_states
+            if not first and complete:
+                cnt[0] += st not in (130, 138)
+                cnt[1] += st == 130
+                cnt[2] += st == 128
+            if not (first or refill_all or complete):
+                continue
+            t = w * tlen + (int(cursor[w]) + rank) % tlen
+            rank += 1
+            oc = int(top[t])
+            o[0:8] = np.frombuffer(np.uint64(tkey[t]).tobytes(), dtype=np.uint8)
+            o[8], o[9] = oc, 141
+            o[10] = 0 if oc == 111 else (st_value >> shift) & 0xFF
+            flags = (1 if oc == 113 else 0) | (0 if first else 2)
+            o[16], o[17] = flags & 0xFF, flags >> 8
+            if oc != 111:
+                o[18:18 + st_value] = ord("a") + mid
+        cursor[w] = (int(cursor[w]) + rank) % tlen
+    return ops.reshape(-1), cursor, cnt
+
+
+@pytest.mark.parametrize("big", [False, True])
+@pytest.mark.parametrize("refill_all", [0, 1])
+def test_refill_kernel_matches_numpy(big, refill_all):
+    """hkv_wl_refill (LDS-staged for 56-B ops, in place for 312-B ops) against a numpy restatement:
+    slab bytes, trace cursors and the committed / miss / PUT_COMPLETE counters."""
+    from hermes_amd import workload as WL
+    sz = L.BIG if big else L.DEFAULT
+    W, S, osz, tlen, mid = 37, 250, sz.op, 300, 2
+    rng = np.random.default_rng(11 + big + 2 * refill_all)
+    states = np.array([130, 128, 138, 137, 119, 121, 131, 132, 143, 144, 141], dtype=np.uint8)
+    ops = rng.integers(0, 256, size=W * S * osz, dtype=np.uint8)
+    ops.reshape(W, S, osz)[:, :, 9] = rng.choice(states, size=(W, S))
+    tkey = rng.integers(0, 2**63, size=W * tlen, dtype=np.int64)
+    top = rng.choice(np.array([111, 112, 113], dtype=np.uint8), size=W * tlen)
+    cursor = rng.integers(0, tlen, size=W, dtype=np.int32)
+    exp_ops, exp_cur, exp_cnt = _refill_ref(ops, W, S, osz, sz.st_value, sz.shift, tkey.view(np.uint64), top, tlen,
+                                            cursor, mid, False, refill_all)
+    d_ops = torch.from_numpy(ops.copy()).cuda()
+    d_tkey, d_top = torch.from_numpy(tkey).cuda(), torch.from_numpy(top).cuda()
+    d_cur = torch.from_numpy(cursor.copy()).cuda()
+    d_cnt = torch.zeros(4096, dtype=torch.int64, device="cuda")
+    WL.check(WL._L.hkv_wl_refill(WL._ptr(d_ops), W, S, osz, sz.st_value, sz.shift, WL._ptr(d_tkey), WL._ptr(d_top),
+                                 tlen, WL._ptr(d_cur), mid, 0, refill_all, WL._ptr(d_cnt), None), "refill")
+    torch.cuda.synchronize()
+    got = d_ops.cpu().numpy()
+    if not np.array_equal(got, exp_ops):
+        bad = np.nonzero(got != exp_ops)[0]
+        pytest.fail(f"slab differs at {len(bad)} bytes: ops {np.unique(bad // osz)[:8]}, offsets {np.unique(bad % osz)[:16]}")
+    assert np.array_equal(d_cur.cpu().numpy(), exp_cur)
+    assert d_cnt[:3].cpu().tolist() == exp_cnt.tolist()

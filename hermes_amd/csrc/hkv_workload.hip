@@ -215,27 +215,35 @@ __global__ __launch_bounds__(256) void k_refill_direct(uint8_t *ops, int32_t str
         if (m) atomicAdd(&stripe[1], (unsigned long long)m);
         if (wr) atomicAdd(&stripe[2], (unsigned long long)wr);
     }
-    if (!done) return;
     const int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)rank) % (uint32_t)tlen);
-    const uint8_t oc = top[t];
-    *reinterpret_cast<uint64_t *>(op) = tkey[t];
-    // bytes 8..10 (opcode, state, val_len) of the second header word; 11..15 keep their bytes
-    uint64_t *h1 = reinterpret_cast<uint64_t *>(op + 8);
-    const uint64_t vl = oc == kOpGet ? 0 : (uint8_t)(st_value >> shift);
-    *h1 = (*h1 & ~0xFFFFFFull) | oc | ((uint64_t)kNew << 8) | (vl << 16);
+    const uint8_t oc = done ? top[t] : (uint8_t)kOpGet;
     const uint16_t flags = (uint16_t)((oc == kOpRmw ? 1u : 0u) | (first_iter ? 0u : 2u));  // RMW_flag, no_coales
-    if (oc == kOpGet) {
-        *reinterpret_cast<uint16_t *>(op + 16) = flags;
-        return;
+    if (done) {
+        *reinterpret_cast<uint64_t *>(op) = tkey[t];
+        // bytes 8..10 (opcode, state, val_len) of the second header word; 11..15 keep their bytes
+        uint64_t *h1 = reinterpret_cast<uint64_t *>(op + 8);
+        const uint64_t vl = oc == kOpGet ? 0 : (uint8_t)(st_value >> shift);
+        *h1 = (*h1 & ~0xFFFFFFull) | oc | ((uint64_t)kNew << 8) | (vl << 16);
+        if (oc == kOpGet) *reinterpret_cast<uint16_t *>(op + 16) = flags;
     }
-    // value bytes 18 .. 18 + st_value: 8-B words from byte 16 (the first carries the flags), then
-    // the tail bytes
+    // the values of the writes, one op at a time per wave: lane k stores 8-B word k of bytes
+    // 16 .. 18 + st_value (word 0 carries the flags), the tail bytes go to the lanes after them
     const uint64_t vv = 0x0101010101010101ull * (uint8_t)('a' + machine_id);
-    const uint32_t end = kOpValueOff + st_value;
-    *reinterpret_cast<uint64_t *>(op + 16) = (uint64_t)flags | (vv << 16);
-    uint32_t k = 24;
-    for (; k + 8 <= end; k += 8) *reinterpret_cast<uint64_t *>(op + k) = vv;
-    for (; k < end; ++k) op[k] = (uint8_t)vv;
+    const uint32_t span = kOpValueOff - 16 + st_value;
+    const int nfull = (int)(span / 8), tail = (int)(span % 8);
+    const int lane = threadIdx.x & 63;
+    uint8_t *wave_ops = ops + ((int64_t)w * stride + (threadIdx.x & ~63)) * op_size;
+    unsigned long long todo = __ballot(done && oc != kOpGet);
+    while (todo) {
+        const int j = __ffsll((long long)todo) - 1;
+        todo &= todo - 1;
+        const uint16_t fj = (uint16_t)__shfl((int)flags, j, 64);
+        uint8_t *oj = wave_ops + (int64_t)j * op_size + 16;
+        if (lane < nfull)
+            *reinterpret_cast<uint64_t *>(oj + 8 * lane) = lane == 0 ? ((uint64_t)fj | (vv << 16)) : vv;
+        else if (lane < nfull + tail)
+            oj[8 * nfull + (lane - nfull)] = (uint8_t)vv;
+    }
 }
 
 // 16 bytes at an 8-byte aligned address: one dwordx4 access (op headers, 16-B messages)
@@ -603,7 +611,7 @@ int hkv_wl_refill(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_s
                   int32_t first_iter, int32_t refill_all, unsigned long long *counters, void *stream)
 {
     if (stride > 256 || n_workers <= 0 || op_size % 8) return -1;
-    if (op_size > 64 && st_value >= 6) {  // big ops: in place (see k_refill_direct)
+    if (op_size > 64 && st_value >= 6 && (kOpValueOff - 16 + st_value) / 8 + 7 <= 64) {  // big ops: in place
         hipLaunchKernelGGL(k_refill_direct, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
                            st_value, shift, tkey, top, tlen, cursor, machine_id, first_iter, refill_all, counters);
         hipLaunchKernelGGL(k_fold_counters, dim3(1), dim3(256), 0, (hipStream_t)stream, counters);

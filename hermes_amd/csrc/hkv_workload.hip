@@ -274,6 +274,27 @@ __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stri
         count[w] = total < out_stride ? total : out_stride;
         if (total > out_stride && held) atomicAdd(held, (unsigned long long)(total - out_stride));
     }
+    if (op_size > 64) {  // big ops: one op at a time per wave, 8-B word k by lane k
+        const int lane = i & 63;
+        const int words = (int)(op_size / 8);
+        uint8_t *wave_ops = ops + ((int64_t)w * stride + (i & ~63)) * op_size;
+        unsigned long long todo = __ballot(send && rank < out_stride);
+        while (todo) {
+            const int j = __ffsll((long long)todo) - 1;
+            todo &= todo - 1;
+            const int rj = __shfl(rank, j, 64);
+            const uint64_t *src = reinterpret_cast<const uint64_t *>(wave_ops + (int64_t)j * op_size);
+            uint64_t *dst = reinterpret_cast<uint64_t *>(out + ((int64_t)w * out_stride + rj) * op_size);
+            for (int k = lane; k < words; k += 64) {
+                const uint64_t v = src[k];
+                dst[k] = k == 1 ? with_op_state(v, kOpInv, (uint8_t)machine_id) : v;
+            }
+        }
+        if (send && rank < out_stride)
+            op[9] = st == kPutSuccess ? kInProgressPut : st == kRmwSuccess ? kInProgressRmw
+                  : st == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
+        return;
+    }
     if (!send || rank >= out_stride) return;
     uint8_t *dst = out + ((int64_t)w * out_stride + rank) * op_size;
     // 16-B words; the header word is rewritten in registers

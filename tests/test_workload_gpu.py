@@ -177,3 +177,49 @@ def test_refill_kernel_matches_numpy(big, refill_all):
         pytest.fail(f"slab differs at {len(bad)} bytes: ops {np.unique(bad // osz)[:8]}, offsets {np.unique(bad % osz)[:16]}")
     assert np.array_equal(d_cur.cpu().numpy(), exp_cur)
     assert d_cnt[:3].cpu().tolist() == exp_cnt.tolist()
+
+
+@pytest.mark.parametrize("big", [False, True])
+def test_marshal_invs_kernel_matches_numpy(big):
+    """hkv_wl_marshal_invs_cap (per-thread 16-B copies for 56-B ops, one wave-wide copy per op for
+    312-B ops) against a numpy restatement of inv_skip_or_get_sender_id /
+    inv_copy_and_modify_elem / inv_modify_elem_after_send (hermes_worker.c:12-65) with C credits."""
+    from hermes_amd import workload as WL
+    sz = L.BIG if big else L.DEFAULT
+    W, S, osz, C, mid = 29, 250, sz.op, 40, 3
+    rng = np.random.default_rng(5 + big)
+    states = np.array([122, 135, 123, 118, 121, 131, 130, 143], dtype=np.uint8)
+    ops = rng.integers(0, 256, size=W * S * osz, dtype=np.uint8)
+    ops.reshape(W, S, osz)[:, :, 9] = rng.choice(states, size=(W, S), p=[.3, .05, .05, .02, .3, .1, .1, .08])
+    exp_ops = ops.copy().reshape(W, S, osz)
+    exp_out = np.zeros((W, C, osz), dtype=np.uint8)
+    exp_cnt = np.zeros(W, dtype=np.int32)
+    held = 0
+    after = {122: 143, 135: 148, 123: 144, 118: 119}
+    for w in range(W):
+        r = 0
+        for i in range(S):
+            st = int(exp_ops[w, i, 9])
+            if st not in after:
+                continue
+            if r < C:
+                exp_out[w, r] = exp_ops[w, i]
+                exp_out[w, r, 8], exp_out[w, r, 9] = 114, mid
+                exp_ops[w, i, 9] = after[st]
+            r += 1
+        exp_cnt[w] = min(r, C)
+        held += max(0, r - C)
+    d_ops = torch.from_numpy(ops.copy()).cuda()
+    d_out = torch.zeros(W * C * osz, dtype=torch.uint8, device="cuda")
+    d_cnt = torch.zeros(W, dtype=torch.int32, device="cuda")
+    d_held = torch.zeros(1, dtype=torch.int64, device="cuda")
+    WL.check(WL._L.hkv_wl_marshal_invs_cap(WL._ptr(d_ops), W, S, osz, WL._ptr(d_out), C, WL._ptr(d_cnt), mid,
+                                           WL._ptr(d_held), None), "marshal_invs")
+    torch.cuda.synchronize()
+    cnt = d_cnt.cpu().numpy()
+    assert np.array_equal(cnt, exp_cnt)
+    out = d_out.cpu().numpy().reshape(W, C, osz)
+    for w in range(W):
+        assert np.array_equal(out[w, :cnt[w]], exp_out[w, :cnt[w]]), f"worker {w}: INV rows differ"
+    assert np.array_equal(d_ops.cpu().numpy(), exp_ops.reshape(-1)), "op states differ"
+    assert int(d_held.item()) == held

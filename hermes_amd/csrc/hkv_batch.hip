@@ -6,23 +6,25 @@
 //
 //   k_lookup    one element per 4 lanes, in element order: skip test (hermesKV.c:709-769),
 //               bucket probe over the 64-B bucket (hermesKV.c:952-975), wrap test, 8-B key
-//               compare (hermesKV.c:977-993; a miss writes ST_MISS into byte 9). A hit claims its
-//               key's slot g in the launch's group table, reads the key's object meta S_0 from
-//               the same log line, and offers itself as round 0's first candidate if
-//               would_mutate(elem, S_0) (hkv_exec.h).
+//               compare (hermesKV.c:977-993; a miss writes ST_MISS into byte 9). A hit reads
+//               the key's object meta S_0 from the same log line and offers itself as round
+//               0's first candidate if would_mutate(elem, S_0) (hkv_exec.h).
 //   round r     every key keeps F_r, the smallest element index among its candidates (one
-//               atomicMin on the slot's F word). Then
+//               atomicMin on the F word of the key's log line). Then
 //                 k_resolve: an element before F_r (or of a key without a candidate) sees S_r in
 //                   the sequential order and S_r does not change under it: it runs the
 //                   reference's exec function on a private copy of S_r against the live entry,
 //                   in parallel with everything else. F_r itself runs the exec function on a
 //                   shadow image of the entry (S_r -> S_{r+1}), so the entry still holds S_r for
 //                   every concurrent reader; later elements stay pending.
-//                 k_cand (r+1): commits the shadows to the entries, and every pending element
-//                   tests would_mutate against S_{r+1}.
+//                 k_cand (r+1): every pending element tests would_mutate against S_{r+1}, read
+//                   from the shadow of round r's first candidate; k_commit copies each key's
+//                   last shadow into its entry once, after the last round.
 //   fallback    elements still pending after the last round (keys mutated in every round) are
-//               gathered per key, sorted by element index, and finished by one workgroup per
-//               key with first-candidate passes over chunks (k_fb_exec).
+//               gathered per key into workgroup-owned lists (key -> workgroup by its last first
+//               candidate), sorted by element index in LDS, and finished in element order: runs
+//               of up to 32 by one thread, longer runs by the whole workgroup with block-wide
+//               first-candidate passes over chunks (k_fb_exec).
 //
 // Exactness rests on one property: would_mutate() is sound (false => the exec function leaves
 // the meta unchanged). Every resolved element checks it: a private copy that did change raises
@@ -1200,6 +1202,10 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     } else {
 #define HKV_ROUNDS(T, V)                                                                          \
     do {                                                                                          \
+        if (big && rlds > 64 * 1024 &&                                                            \
+            hipFuncSetAttribute((const void *)k_resolve0<T, V, 128>,                              \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds) != hipSuccess) \
+            return -3;                                                                            \
         if (big) hipLaunchKernelGGL((k_resolve0<T, V, 128>), dim3(rgrid), dim3(128), rlds, s, a); \
         else hipLaunchKernelGGL((k_resolve0<T, V, 256>), dim3(rgrid), dim3(256), rlds, s, a);     \
         for (int r = 1; r <= a.rounds; ++r) {                                                     \

@@ -1,13 +1,16 @@
 // hkv_exec.h -- per-entry state machine of the HermesKV protocol, device side.
 //
-// A segment (all elements of one launch that hit one log entry, in concatenation order) is
-// applied by ONE owner lane: it loads the entry's object meta into registers, runs every
-// element of the segment through the Hermes transitions below, and stores the meta once.
-// Because exactly one lane owns an entry during the launch, the reference's per-key seqlock
+// Each function applies ONE element to a register copy of its key's object meta (Meta), the
+// way the reference's exec function applies it to the entry. The batch engine (hkv_batch.hip)
+// decides which meta an element sees: elements that cannot change the meta (would_mutate
+// false) run in parallel against one snapshot, and a key's mutating elements run one per
+// round, each on its own shadow image of the entry, in element order. Within one exec call
+// no other thread touches the key's meta, so the reference's per-key seqlock
 // (concur_ctrl.h:144-224) has no work to do; only its NET effect on the version survives a
 // batch boundary, so the lock/unlock pair is folded into the version arithmetic:
 //   lock+unlock_dec -> +0, lock+unlock_inc -> +2, lock+unlock_inc_by_three -> +4,
 //   lock+unlock_custom(v) -> v, and "locked version - 1" reads are the plain version.
+// tests/test_oracle.py pins these net effects against the reference's own cctrl_* functions.
 // Each function cites the reference function whose observable behaviour it reproduces.
 #pragma once
 #include <hip/hip_runtime.h>

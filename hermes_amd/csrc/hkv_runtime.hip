@@ -186,6 +186,10 @@ int hkv_table_create(const hkv_config *cfg, hkv_table **out)
     if (!is_pow2(cfg->num_bkts) || cfg->num_bkts > (1ull << 31)) return fail(-1, "num_bkts must be a power of two <= 2^31");
     if (!is_pow2(cfg->log_cap) || cfg->log_cap < 4096) return fail(-1, "log_cap must be a power of two >= 4096");
     if (cfg->machine_id > 127) return fail(-1, "machine_id must be < 128");
+    // 287 + 64 k value bytes in (k + 1) cache lines: val_len >> SHIFT_BITS must fit its byte and
+    // the batch engine stages 128 entries of a launch in one workgroup's LDS
+    if (cfg->big_objects && (cfg->extra_cache_lines < 1 || cfg->extra_cache_lines > 16))
+        return fail(-1, "extra_cache_lines must be 1..16 with big objects");
     hkv_table *t = new hkv_table();
     t->cfg = *cfg;
     if (t->cfg.rw_len == 0) t->cfg.rw_len = 250;
@@ -309,7 +313,11 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     if (d->type < 0 || d->type > 4) return fail(-1, "bad batch type %d", d->type);
     if (d->n_batches < 0 || d->stride <= 0) return fail(-1, "bad batch geometry");
     if (d->elem_size < kOpMetaSize || (d->elem_size & 7)) return fail(-1, "elem_size %u must be >= 16 and a multiple of 8", d->elem_size);
-    const bool needs_value = d->type == kLocal || d->type == kLocalAfterMemb || d->type == kInvs;
+    // ACK batches of an RMW table carry INV-aborts, which hermes_exec_inv applies with their value
+    // (hermesKV.c:877-890): they need op-sized elements, as the reference worker sends them
+    // (hermes_worker.c:332)
+    const bool needs_value = d->type == kLocal || d->type == kLocalAfterMemb || d->type == kInvs ||
+                             (d->type == kAcks && t->geo.rmw_enabled);
     if (needs_value && d->elem_size < kOpValueOff + t->geo.st_value)
         return fail(-1, "elem_size %u too small for %u-byte values", d->elem_size, t->geo.st_value);
     if (d->type == kLocal && d->stride > 255)

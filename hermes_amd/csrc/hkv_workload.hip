@@ -110,28 +110,46 @@ __global__ void k_gen_trace(uint64_t *tkey, uint8_t *top, uint32_t *tid, int32_t
 
 // refill_ops, inline-util.h:149-303 (hot-key coalescing and latency probes off)
 constexpr int kStripes = (HKV_WL_COUNTER_WORDS - HKV_WL_STRIPE_BASE) / 16;
+constexpr int kCounters = 4;  // committed, misses, completed writes, dropped (refill_all)
 
-// folds the refill stripes into counters[0..2] and clears them
+// Ops a fresh-batch refill (refill_all) must keep: writes and replays between their local
+// success and their completion (waiting for INV credits, ACKs or the VALs of a membership
+// change), and membership-change ops. Overwriting one would leave its key in WRITE/REPLAY with
+// an op buffer index that points at an unrelated op.
+__device__ __forceinline__ bool in_flight(uint8_t st)
+{
+    return st == kPutSuccess || st == kRmwSuccess || st == kReplaySuccess || st == kInProgressPut ||
+           st == kInProgressRmw || st == kInProgressReplay || st == kPutCompleteSendVals ||
+           st == kRmwCompleteSendVals || st == kReplayCompleteSendVals || st == kOpMembChange;
+}
+
+__device__ __forceinline__ bool is_complete(uint8_t st)  // refill_ops, inline-util.h:189-195
+{
+    return st == kMiss || st == kPutComplete || st == kRmwAbort || st == kRmwComplete || st == kOpMembComplete ||
+           st == kGetComplete;
+}
+
+// folds the refill stripes into counters[0..3] and clears them
 __global__ __launch_bounds__(256) void k_fold_counters(unsigned long long *counters)
 {
-    __shared__ unsigned long long part[4][3];
-    unsigned long long v[3] = {0, 0, 0};
+    __shared__ unsigned long long part[4][kCounters];
+    unsigned long long v[kCounters] = {0, 0, 0, 0};
     for (int s = threadIdx.x; s < kStripes; s += 256) {
         unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + s * 16;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < kCounters; ++k) {
             v[k] += stripe[k];
             stripe[k] = 0;
         }
     }
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < kCounters; ++k) {
         for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_down(v[k], o, 64);
         if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6][k] = v[k];
     }
     __syncthreads();
-    if (threadIdx.x < 3) counters[threadIdx.x] += part[0][threadIdx.x] + part[1][threadIdx.x] +
-                                                 part[2][threadIdx.x] + part[3][threadIdx.x];
+    if (threadIdx.x < kCounters) counters[threadIdx.x] += part[0][threadIdx.x] + part[1][threadIdx.x] +
+                                                         part[2][threadIdx.x] + part[3][threadIdx.x];
 }
 
 // The worker's op slab (stride * op_size contiguous bytes) is staged through LDS so HBM sees
@@ -150,22 +168,24 @@ __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, ui
     __syncthreads();
     uint8_t *op = reinterpret_cast<uint8_t *>(slab) + (uint32_t)i * op_size;
     uint8_t st = live ? op[9] : 0;
-    const bool complete = st == kMiss || st == kPutComplete || st == kRmwAbort || st == kRmwComplete ||
-                          st == kOpMembComplete || st == kGetComplete;
-    bool done = live && (first_iter || refill_all || complete);
+    const bool complete = is_complete(st);
+    // refill_all: stalled ops are dropped (and counted), ops in flight keep their slot
+    const bool drop = live && !first_iter && refill_all && !complete && !in_flight(st);
+    bool done = live && (first_iter || complete || drop);
     int commits = (live && complete && !first_iter && st != kMiss && st != kRmwAbort) ? 1 : 0;
     int misses = (live && !first_iter && st == kMiss) ? 1 : 0;
     int writes = (live && !first_iter && st == kPutComplete) ? 1 : 0;
     int total;
     int rank = block_rank(done, total);
     uint32_t base = cursor[w];
-    int c = block_sum(commits), m = block_sum(misses), wr = block_sum(writes);
+    int c = block_sum(commits), m = block_sum(misses), wr = block_sum(writes), dr = block_sum(drop ? 1 : 0);
     if (i == 0) {
         cursor[w] = (uint32_t)((base + (uint32_t)total) % (uint32_t)tlen);
         unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + (w % kStripes) * 16;
         if (c) atomicAdd(&stripe[0], (unsigned long long)c);
         if (m) atomicAdd(&stripe[1], (unsigned long long)m);
         if (wr) atomicAdd(&stripe[2], (unsigned long long)wr);
+        if (dr) atomicAdd(&stripe[3], (unsigned long long)dr);
     }
     if (done) {
         int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)rank) % (uint32_t)tlen);
@@ -198,22 +218,23 @@ __global__ __launch_bounds__(256) void k_refill_direct(uint8_t *ops, int32_t str
     const bool live = i < stride;
     uint8_t *op = ops + ((int64_t)w * stride + (live ? i : 0)) * op_size;
     const uint8_t st = live ? op[9] : 0;
-    const bool complete = st == kMiss || st == kPutComplete || st == kRmwAbort || st == kRmwComplete ||
-                          st == kOpMembComplete || st == kGetComplete;
-    const bool done = live && (first_iter || refill_all || complete);
+    const bool complete = is_complete(st);
+    const bool drop = live && !first_iter && refill_all && !complete && !in_flight(st);
+    const bool done = live && (first_iter || complete || drop);
     const int commits = (live && complete && !first_iter && st != kMiss && st != kRmwAbort) ? 1 : 0;
     const int misses = (live && !first_iter && st == kMiss) ? 1 : 0;
     const int writes = (live && !first_iter && st == kPutComplete) ? 1 : 0;
     int total;
     const int rank = block_rank(done, total);
     const uint32_t base = cursor[w];
-    const int c = block_sum(commits), m = block_sum(misses), wr = block_sum(writes);
+    const int c = block_sum(commits), m = block_sum(misses), wr = block_sum(writes), dr = block_sum(drop ? 1 : 0);
     if (i == 0) {
         cursor[w] = (uint32_t)((base + (uint32_t)total) % (uint32_t)tlen);
         unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + (w % kStripes) * 16;
         if (c) atomicAdd(&stripe[0], (unsigned long long)c);
         if (m) atomicAdd(&stripe[1], (unsigned long long)m);
         if (wr) atomicAdd(&stripe[2], (unsigned long long)wr);
+        if (dr) atomicAdd(&stripe[3], (unsigned long long)dr);
     }
     const int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)rank) % (uint32_t)tlen);
     const uint8_t oc = done ? top[t] : (uint8_t)kOpGet;

@@ -127,7 +127,8 @@ int  hkv_table_populate(hkv_table *t, int64_t n, int val_len);
 int  hkv_table_config(const hkv_table *t, hkv_config *out);
 
 /* device-resident batch path, asynchronous on `stream` (NULL = the HIP null stream). One
- * stream at a time per table: launches share the table's sort scratch. */
+ * stream at a time per table: launches share the table's round scratch (entry ids, stages,
+ * shadow images) and its per-log-line F/X/Y/T words. */
 int  hkv_batch_async(hkv_table *t, const hkv_batch_desc *desc, void *stream);
 int  hkv_sync(hkv_table *t, void *stream);
 

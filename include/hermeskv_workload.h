@@ -43,12 +43,15 @@ int hkv_wl_gen_trace(uint64_t *d_trace_key, uint8_t *d_trace_op, uint32_t *d_tra
                      uint64_t seed, void *stream);
 
 /* refill_ops over n_workers buffers of `stride` ops (op_size bytes each). Slots that are
- * complete take the next trace command of their worker (all slots when first_iter, or when
- * refill_all: then stalled ops are dropped instead of retried -- one fresh batch per round).
+ * complete take the next trace command of their worker (all slots when first_iter). With
+ * refill_all, stalled ops (GET/PUT/RMW stalls, ST_EMPTY, ST_NEW) are dropped instead of
+ * retried and take a fresh command too; ops in flight (PUT/RMW/REPLAY_SUCCESS, IN_PROGRESS_*,
+ * *_COMPLETE_SEND_VALS, membership change) always keep their slot.
  * Adds completed-and-committed ops (everything complete except ST_MISS and ST_RMW_ABORT)
- * to d_counters[0], misses to d_counters[1], completed writes to d_counters[2].
+ * to d_counters[0], misses to d_counters[1], completed writes to d_counters[2], dropped
+ * stalled ops to d_counters[3].
  * d_counters holds HKV_WL_COUNTER_WORDS words, zeroed by the caller once: words from
- * HKV_WL_STRIPE_BASE on are per-worker-group partial sums the call folds back into [0..2]
+ * HKV_WL_STRIPE_BASE on are per-worker-group partial sums the call folds back into [0..3]
  * (one counter address hit by every worker serialises in L2). */
 #define HKV_WL_COUNTER_WORDS 4096
 #define HKV_WL_STRIPE_BASE 64

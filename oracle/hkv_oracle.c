@@ -3,8 +3,9 @@
  *
  * A straight sequential restatement of the reference batch path. Every function cites the
  * reference function (file:line) whose behaviour it restates. The product (libhermeskv.so)
- * is written independently (sort-by-entry + segmented device kernels); this file is the
- * single-threaded definition of "what the reference would have produced".
+ * is written independently (element-order rounds with per-key first-candidate words and
+ * shadow images, hkv_batch.hip); this file is the single-threaded definition of "what the
+ * reference would have produced".
  *
  * The reference seqlock (include/utils/concur_ctrl.h:144-224) is modelled exactly: lock sets
  * the lock byte and bumps the version by one, and each unlock variant applies its own version
@@ -680,3 +681,31 @@ int64_t hko_num_index_evictions(hko_kvs *kv) { return kv->num_index_evictions; }
 
 /* lets the CPU baseline start from a table image copied out of HBM */
 void hko_set_log_head(hko_kvs *kv, uint64_t head) { kv->log_head = head; }
+
+/* ---------------------------------------------------------------- test hooks
+ * The seqlock / timestamp / ack-quorum restatements above, exported so tests/test_oracle.py can
+ * compare them with the reference's own concur_ctrl.h / bit_vector.h (oracle/ref_prims.c).
+ * cc: 6 bytes {lock, tie_breaker_id, version} as conc_ctrl_t; variant 0 dec, 1 inc,
+ * 2 inc_by_three, 3 custom. Returns the version an inc variant reports, else 0. */
+uint32_t hko_test_cctrl_lock_unlock(uint8_t *cc, int variant, uint8_t cid, uint32_t version)
+{
+    uint8_t m[OBJ_META_SIZE];
+    uint32_t resp = 0;
+    memset(m, 0, sizeof m);
+    memcpy(m + 4, cc, 6);
+    cc_lock(m);
+    switch (variant) {
+    case 0: cc_unlock_dec(m); break;
+    case 1: resp = cc_unlock_inc(m, cid, 1u); break;
+    case 2: resp = cc_unlock_inc(m, cid, 3u); break;
+    default: cc_unlock_custom(m, cid, version); break;
+    }
+    memcpy(cc, m + 4, 6);
+    return resp;
+}
+
+int hko_test_ts_less(uint32_t v1, uint8_t c1, uint32_t v2, uint8_t c2) { return ts_less(v1, c1, v2, c2); }
+int hko_test_ts_equal(uint32_t v1, uint8_t c1, uint32_t v2, uint8_t c2) { return ts_equal(v1, c1, v2, c2); }
+
+int hko_test_is_last_ack(uint8_t ack_bv, const uint8_t membership[8]) { return memb_is_last_ack(ack_bv, membership); }
+int hko_test_has_node(const uint8_t membership[8], uint8_t node) { return memb_has_node(membership, node); }

@@ -116,8 +116,12 @@ int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, doub
                 uint8_t *o = ow + (size_t)i * osz;
                 uint8_t st = o[9];
                 int complete = st == 130 || st == 128 || st == 138 || st == 137 || st == 119 || st == 121;
+                /* in flight: PUT/RMW/REPLAY_SUCCESS, IN_PROGRESS_*, *_COMPLETE_SEND_VALS, membership change */
+                int in_flight = st == 122 || st == 135 || st == 123 || st == 143 || st == 148 || st == 144 ||
+                                st == 133 || st == 149 || st == 147 || st == 118;
                 if (!first && complete && st != 130 && st != 138) committed++;
-                if (!(first || refill_all || complete)) continue;  /* stalled ops retry unless refill_all */
+                /* stalled ops retry unless refill_all; ops in flight always keep their slot */
+                if (!(first || complete || (refill_all && !in_flight))) continue;
                 int64_t ti = (int64_t)w * T + cursor[w];
                 cursor[w] = (cursor[w] + 1) % T;
                 memcpy(o, &tkey[ti], 8);

@@ -114,12 +114,17 @@ def test_membership_change_round_mirrored(machines):
     assert g.take_error_flags() == 0
 
 
+# PUT/RMW/REPLAY_SUCCESS, IN_PROGRESS_PUT/RMW/REPLAY, PUT/RMW/REPLAY_COMPLETE_SEND_VALS, membership
+# change: a fresh-batch refill keeps these (their keys point at the slot through op_buffer_index)
+IN_FLIGHT = (122, 135, 123, 143, 148, 144, 133, 149, 147, 118)
+
+
 def _refill_ref(ops, W, S, osz, st_value, shift, tkey, top, tlen, cursor, mid, first, refill_all):
     """refill_ops (inline-util.h:149-303) as hkv_wl_refill applies it, in numpy: per worker, the
     completed ops (every op with refill_all / first) take the next trace entries in op order."""
     ops = ops.copy().reshape(W, S, osz)
     cursor = cursor.copy()
-    cnt = np.zeros(3, dtype=np.int64)
+    cnt = np.zeros(4, dtype=np.int64)
     done_states = (130, 128, 138, 137, 119, 121)
     for w in range(W):
         rank = 0
@@ -127,11 +132,13 @@ def _refill_ref(ops, W, S, osz, st_value, shift, tkey, top, tlen, cursor, mid, f
             o = ops[w, i]
             st = int(o[9])
             complete = st in done_states
+            drop = bool(refill_all) and not first and not complete and st not in IN_FLIGHT
             if not first and complete:
                 cnt[0] += st not in (130, 138)
                 cnt[1] += st == 130
                 cnt[2] += st == 128
-            if not (first or refill_all or complete):
+            cnt[3] += drop
+            if not (first or complete or drop):
                 continue
             t = w * tlen + (int(cursor[w]) + rank) % tlen
             rank += 1
@@ -151,12 +158,13 @@ def _refill_ref(ops, W, S, osz, st_value, shift, tkey, top, tlen, cursor, mid, f
 @pytest.mark.parametrize("refill_all", [0, 1])
 def test_refill_kernel_matches_numpy(big, refill_all):
     """hkv_wl_refill (LDS-staged for 56-B ops, in place for 312-B ops) against a numpy restatement:
-    slab bytes, trace cursors and the committed / miss / PUT_COMPLETE counters."""
+    slab bytes, trace cursors and the committed / miss / PUT_COMPLETE / dropped counters; with
+    refill_all, ops in flight keep their slots."""
     from hermes_amd import workload as WL
     sz = L.BIG if big else L.DEFAULT
     W, S, osz, tlen, mid = 37, 250, sz.op, 300, 2
     rng = np.random.default_rng(11 + big + 2 * refill_all)
-    states = np.array([130, 128, 138, 137, 119, 121, 131, 132, 143, 144, 141], dtype=np.uint8)
+    states = np.array([130, 128, 138, 137, 119, 121, 131, 132, 136, 140, 141, *IN_FLIGHT], dtype=np.uint8)
     ops = rng.integers(0, 256, size=W * S * osz, dtype=np.uint8)
     ops.reshape(W, S, osz)[:, :, 9] = rng.choice(states, size=(W, S))
     tkey = rng.integers(0, 2**63, size=W * tlen, dtype=np.int64)
@@ -176,7 +184,7 @@ def test_refill_kernel_matches_numpy(big, refill_all):
         bad = np.nonzero(got != exp_ops)[0]
         pytest.fail(f"slab differs at {len(bad)} bytes: ops {np.unique(bad // osz)[:8]}, offsets {np.unique(bad % osz)[:16]}")
     assert np.array_equal(d_cur.cpu().numpy(), exp_cur)
-    assert d_cnt[:3].cpu().tolist() == exp_cnt.tolist()
+    assert d_cnt[:4].cpu().tolist() == exp_cnt.tolist()
 
 
 @pytest.mark.parametrize("big", [False, True])

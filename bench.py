@@ -24,6 +24,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 EVENT_EVERY = 4                # timed steps per sampled local-launch duration
+PROBE_STEPS = 3                # untimed steps with every batch launch timed
 # algorithmic bytes per element, SURVEY.md 8(d): S_op (56, or 312 big), bucket 64, entry (64, or
 # 320 big), S_msg 16 (ACKs carry S_op with RMWs)
 def elem_bytes(op: int, entry: int, ack: int) -> dict:
@@ -57,6 +58,12 @@ def parse():
                    help="N=1: keep the ACK slab at its capacity stride (2C) instead of the round's largest count")
     p.add_argument("--retry", action="store_true",
                    help="refill_ops semantics: stalled ops keep their slot (default: fresh batch per step)")
+    p.add_argument("--retry-steps", type=int, default=10,
+                   help="N=1, default (fresh) policy: also time this many steps of a second round with "
+                        "refill_ops' retry policy and report it under detail.retry (0 = skip)")
+    p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                   help="torch.distributed backend for N>1 (nccl = RCCL; gloo lets several ranks share one "
+                        "GPU in tests)")
     return p.parse_args()
 
 
@@ -100,9 +107,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
+    dev = local_rank % max(1, torch.cuda.device_count())   # gloo tests: several ranks on one GPU
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
 
     from hermes_amd import layout as L
     from hermes_amd.kvs import HermesKV, sized_geometry
@@ -123,7 +134,7 @@ def main():
     t0 = time.time()
     sizes = L.Sizes(True, 4) if cfg3 else L.DEFAULT
     bkts, cap = sized_geometry(a.keys, sizes)
-    kvs = HermesKV(a.keys, bkts, cap, machine_id=rank if world > 1 else 0, device=local_rank, rmw=cfg3,
+    kvs = HermesKV(a.keys, bkts, cap, machine_id=rank if world > 1 else 0, device=dev, rmw=cfg3,
                    big_objects=cfg3, extra_cache_lines=4 if cfg3 else 0)
     BYTES = elem_bytes(kvs.sizes.op, kvs.sizes.entry, kvs.sizes.op if cfg3 else 16)
     torch.cuda.synchronize()
@@ -154,7 +165,7 @@ def main():
     if world > 1:
         dist.barrier()
     c0 = rnd.counters[:4].clone()
-    rnd.count_elems = False  # element bookkeeping runs in one probe step after the timed region
+    rnd.count_elems = False  # element bookkeeping runs in probe steps after the timed region
     events: dict = {}
     torch.cuda.synchronize()
     if world > 1:
@@ -165,7 +176,7 @@ def main():
     t = time.perf_counter()
     for k in range(a.steps):
         # HIP events around the local launch (the roofline's) on every EVENT_EVERY-th step: each
-        # record costs ~5 us of GPU time between kernels; the other launches: probe step below
+        # record costs ~5 us of GPU time between kernels; the other launches: probe steps below
         rnd.step(events if k % EVENT_EVERY == 0 else None, timed_batches=("local",),
                  drop=drop_id if k == drop_at else None)
     torch.cuda.synchronize()
@@ -176,41 +187,57 @@ def main():
     c1 = rnd.counters[:4].clone()
     committed = int((c1[0] - c0[0]).item())
     writes = int((c1[2] - c0[2]).item())
-    # probe step (untimed): elements each batch launch applies, for the roofline's bytes
+    dropped = int((c1[3] - c0[3]).item())
+    # probe steps (untimed): elements each batch launch applies and every launch's duration
     rnd.count_elems = True
     e0, inv0 = rnd.elem_totals.clone(), rnd.inv_total.clone()
     probe_events: dict = {}
-    rnd.step(probe_events)
+    for _ in range(PROBE_STEPS):
+        rnd.step(probe_events)
     torch.cuda.synchronize()
-    n_inv, n_ack, n_val = (rnd.elem_totals - e0).double().tolist()
-    puts_per_step = float((rnd.inv_total - inv0).item())
-    puts_ok = puts_per_step * a.steps
+    n_inv, n_ack, n_val = ((rnd.elem_totals - e0).double() / PROBE_STEPS).tolist()
+    puts_per_step = float((rnd.inv_total - inv0).item()) / PROBE_STEPS
+    flags = kvs.take_error_flags()
 
     if world > 1:
-        tt = torch.tensor([committed, elapsed * 1e9], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([committed, elapsed * 1e9, flags], dtype=torch.float64, device="cuda")
         allc = [torch.zeros_like(tt) for _ in range(world)]
         dist.all_gather(allc, tt)
         committed_all = int(sum(x[0].item() for x in allc))
         elapsed_max = max(x[1].item() for x in allc) / 1e9
+        flags_any = int(max(x[2].item() for x in allc))
     else:
-        committed_all, elapsed_max = committed, elapsed
+        committed_all, elapsed_max, flags_any = committed, elapsed, flags
 
     # live kernel time of the local batch launch over the timed region (HIP events on the stream
-    # the batches run on); the other batch launches from the untimed probe step (one sample each)
-    ms = {k: sum(s.elapsed_time(e) for s, e in v) / len(v) for k, v in probe_events.items()}
-    ms.update({k: sum(s.elapsed_time(e) for s, e in v) / len(v) for k, v in events.items()})
+    # the batches run on); every launch over the untimed probe steps
+    def avg(v):
+        return sum(s.elapsed_time(e) for s, e in v) / len(v)
+    probe_ms = {k: avg(v) for k, v in probe_events.items()}
+    ms = dict(probe_ms)
+    ms.update({k: avg(v) for k, v in events.items()})
     W, S = a.workers, Round.LOCAL
     per_launch_bytes = {
-        "local": W * S * BYTES["get"] + (puts_ok / a.steps) * (BYTES["put"] - BYTES["get"]),
+        "local": W * S * BYTES["get"] + puts_per_step * (BYTES["put"] - BYTES["get"]),
         "invs": n_inv * BYTES["inv"],
         "acks": n_ack * BYTES["ack"],
         "vals": n_val * BYTES["val"],
     }
-    # the roofline is quoted on the local batch launch (configs[1]'s metric unit); the other
-    # launches are in batch_ms
+    units = {"local": W * S, "invs": n_inv, "acks": n_ack, "vals": n_val}
+    launches = {}
+    for k, b in per_launch_bytes.items():
+        if k not in ms or ms[k] <= 0:
+            continue
+        gbs = b / (ms[k] / 1e3) / 1e9
+        launches[k] = {"elements": units[k], "algorithmic_bytes": b, "ms": ms[k], "achieved": gbs,
+                       "frac": gbs / HBM_PEAK_GBS}
+    # the roofline is quoted on the local batch launch (configs[1]'s metric unit); every launch
+    # and the whole step are in `launches` / `step`
     dom = "local" if "local" in ms else (max(ms, key=ms.get) if ms else "local")
     ach = per_launch_bytes[dom] / (ms[dom] / 1e3) / 1e9 if ms else 0.0
     value = committed_all / elapsed_max
+    step_ms = elapsed_max * 1e3 / a.steps
+    step_bytes = sum(per_launch_bytes.values())
     # HBM traffic of the local launch: rocprofv3 PMC passes of this bench (tools/pmc.sh,
     # tools/pmc_local.py) are committed under profiles/; counters cannot be read in this run
     traffic, traffic_src = None, None
@@ -220,6 +247,7 @@ def main():
         with open(pmc) as f:
             traffic = json.load(f)["traffic_bytes"]
         traffic_src = "profiles/pmc_local_batch.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, separate runs)"
+    refill = "retry" if a.retry else "fresh"
     out = {
         "metric": "replicated KVS ops/s (reads+writes committed)",
         "value": value,
@@ -227,7 +255,7 @@ def main():
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": elapsed_max * 1e3 / a.steps,
+        "ms_per_step": step_ms,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -242,10 +270,16 @@ def main():
                          "INV/ACK/VAL from 2 virtual replicas" if cfg3 else
                          "cfg2: 1xMI355X, 100M keys, 31 B values, Zipf 0.99, 20% writes, "
                          "INV/ACK/VAL from 2 virtual replicas" if world == 1 else
-                         f"cfg4: {world}-replica Hermes group over RCCL, {a.keys} keys/replica"),
+                         f"cfg4: {world}-replica Hermes group over {'RCCL' if a.dist_backend == 'nccl' else 'gloo'}, "
+                         f"{a.keys} keys/replica"),
             "keys": a.keys, "buckets": bkts, "log_cap": cap, "workers_per_gpu": W,
             "local_batch": S, "zipf": a.zipf, "write_permille": a.write_permille,
             "rmw_permille_of_writes": a.rmw_permille,
+            # fresh: every worker gets a fresh 250-op batch each round; ops that stalled (e.g. a GET
+            # on a key being written) are dropped and counted in detail.dropped_per_step, never
+            # committed; writes in flight keep their slots. retry: refill_ops (inline-util.h:149-303),
+            # stalled ops keep their slots (detail.retry reports that policy's rate at N=1)
+            "refill": refill,
             "remote_invs_per_worker": rnd.rstride, "parallelism": f"replicas{world}",
             "elements_per_step": {"inv": n_inv, "ack": n_ack, "val": n_val},
         },
@@ -255,27 +289,61 @@ def main():
             "traffic": traffic, "traffic_source": traffic_src, "launch_ms": ms.get(dom),
             "launch_samples": len(events.get(dom, [])),
             "algorithmic_bytes_per_launch": per_launch_bytes[dom],
-            "batch_ms": ms,
+            "launches": launches,
+            # all four batch launches' algorithmic bytes over the whole step's wall time (refill,
+            # marshalling and host synchronisation included)
+            "step": {"algorithmic_bytes": step_bytes, "ms": step_ms,
+                     "achieved": step_bytes / (step_ms / 1e3) / 1e9,
+                     "frac": step_bytes / (step_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
         },
         "detail": {
             "committed_per_step_rank0": committed / a.steps, "writes_completed_rank0": writes,
-            "puts_succeeded_rank0": puts_ok, "populate_s": t_pop,
+            "dropped_per_step_rank0": dropped / a.steps,
+            "issued_per_step_rank0": W * S,
+            "puts_succeeded_per_step_rank0": puts_per_step, "populate_s": t_pop,
             "step_bytes_per_committed_op_model": 554,
+            "error_flags": flags_any,
             "round_stats_rank0": rnd.stats(),
         },
     }
+    if flags_any:
+        print(json.dumps({"error": f"device consistency flags {flags_any:#x} raised", "partial": out}), flush=True)
+        raise SystemExit(3)
     if cfg5:
         mb = rnd.mb if world == 1 else rnd.r.mb
         out["detail"]["membership"] = {"machines": 8 if world == 1 else world, "dropped": drop_id,
                                        "at_timed_step": drop_at, "g_membership_after": mb[1]}
     if cpu is not None:
         out["cpu_baseline"] = cpu
+    if world == 1 and not a.retry and a.retry_steps > 0 and not cfg5:
+        out["detail"]["retry"] = retry_rate(a, kvs, z, L, Round)
     if rank == 0 and world == 1 and a.host_api_seconds > 0:
         out["detail"]["host_api"] = host_api_rate(a.host_api_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def retry_rate(a, kvs, z, L, Round) -> dict:
+    """The same round with refill_ops' retry policy (stalled ops keep their slots), on the same
+    table, after the headline run: W warmup steps, then a.retry_steps timed steps."""
+    import torch
+    r = Round(kvs, a.workers, L.membership(3, 0), [1, 2], z, a.write_permille, a.rmw_permille,
+              seed=a.seed + 1, max_steps=a.warmup + a.retry_steps + 2, retry_stalled=True)
+    for _ in range(a.warmup):
+        r.step()
+    torch.cuda.synchronize()
+    c0 = r.counters[:4].clone()
+    t = time.perf_counter()
+    for _ in range(a.retry_steps):
+        r.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    c = (r.counters[:4] - c0).tolist()
+    return {"value": c[0] / dt, "unit": "ops/s", "steps": a.retry_steps, "ms_per_step": dt * 1e3 / a.retry_steps,
+            "committed_per_step": c[0] / a.retry_steps, "writes_completed_per_step": c[2] / a.retry_steps,
+            "what": "refill_ops retry policy (stalled ops keep their slots), same workload and table"}
 
 
 if __name__ == "__main__":

@@ -6,6 +6,8 @@
 
 #include "hkv_codes.h"
 
+struct hkv_table;
+
 namespace hkv {
 
 struct BatchLaunch {
@@ -54,6 +56,15 @@ struct PopulateLaunch {
     int32_t key_bits;
     uint8_t val_len_byte;
 };
+
+// A table's HBM image and geometry, for the workload kernels that read it (virtual peers take
+// each key's current timestamp when they write it, hkv_workload.hip)
+struct TableView {
+    Geometry g;
+    const uint8_t *index;
+    const uint8_t *log;
+};
+int table_view(const hkv_table *t, TableView *out);
 
 int launch_batch(const BatchLaunch &bl, hipStream_t s);
 int launch_populate(const PopulateLaunch &pl, hipStream_t s);

@@ -173,6 +173,17 @@ static void plan_log(uint64_t h0, uint64_t cap, uint32_t e, uint32_t maxv, uint6
     final_head = (n < k) ? h0 + n * e : hw + (n - k) * e;
 }
 
+namespace hkv {
+int table_view(const hkv_table *t, TableView *out)
+{
+    if (!t || !out) return -1;
+    out->g = t->geo;
+    out->index = t->d_index;
+    out->log = t->d_log;
+    return 0;
+}
+}  // namespace hkv
+
 extern "C" {
 
 int hkv_abi_version(void) { return HKV_ABI_VERSION; }

@@ -7,6 +7,7 @@
 
 #include "../../include/hermeskv_workload.h"
 #include "hkv_codes.h"
+#include "hkv_internal.h"
 
 namespace hkv {
 
@@ -110,7 +111,7 @@ __global__ void k_gen_trace(uint64_t *tkey, uint8_t *top, uint32_t *tid, int32_t
 
 // refill_ops, inline-util.h:149-303 (hot-key coalescing and latency probes off)
 constexpr int kStripes = (HKV_WL_COUNTER_WORDS - HKV_WL_STRIPE_BASE) / 16;
-constexpr int kCounters = 4;  // committed, misses, completed writes, dropped (refill_all)
+constexpr int kCounters = 5;  // committed, misses, completed writes, dropped (refill_all), RMW aborts
 
 // Ops a fresh-batch refill (refill_all) must keep: writes and replays between their local
 // success and their completion (waiting for INV credits, ACKs or the VALs of a membership
@@ -129,11 +130,11 @@ __device__ __forceinline__ bool is_complete(uint8_t st)  // refill_ops, inline-u
            st == kGetComplete;
 }
 
-// folds the refill stripes into counters[0..3] and clears them
+// folds the refill stripes into counters[0..4] and clears them
 __global__ __launch_bounds__(256) void k_fold_counters(unsigned long long *counters)
 {
     __shared__ unsigned long long part[4][kCounters];
-    unsigned long long v[kCounters] = {0, 0, 0, 0};
+    unsigned long long v[kCounters] = {0, 0, 0, 0, 0};
     for (int s = threadIdx.x; s < kStripes; s += 256) {
         unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + s * 16;
 #pragma unroll
@@ -179,6 +180,7 @@ __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, ui
     int rank = block_rank(done, total);
     uint32_t base = cursor[w];
     int c = block_sum(commits), m = block_sum(misses), wr = block_sum(writes), dr = block_sum(drop ? 1 : 0);
+    int ab = block_sum((live && !first_iter && st == kRmwAbort) ? 1 : 0);
     if (i == 0) {
         cursor[w] = (uint32_t)((base + (uint32_t)total) % (uint32_t)tlen);
         unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + (w % kStripes) * 16;
@@ -186,6 +188,7 @@ __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, ui
         if (m) atomicAdd(&stripe[1], (unsigned long long)m);
         if (wr) atomicAdd(&stripe[2], (unsigned long long)wr);
         if (dr) atomicAdd(&stripe[3], (unsigned long long)dr);
+        if (ab) atomicAdd(&stripe[4], (unsigned long long)ab);
     }
     if (done) {
         int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)rank) % (uint32_t)tlen);
@@ -228,6 +231,7 @@ __global__ __launch_bounds__(256) void k_refill_direct(uint8_t *ops, int32_t str
     const int rank = block_rank(done, total);
     const uint32_t base = cursor[w];
     const int c = block_sum(commits), m = block_sum(misses), wr = block_sum(writes), dr = block_sum(drop ? 1 : 0);
+    const int ab = block_sum((live && !first_iter && st == kRmwAbort) ? 1 : 0);
     if (i == 0) {
         cursor[w] = (uint32_t)((base + (uint32_t)total) % (uint32_t)tlen);
         unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + (w % kStripes) * 16;
@@ -235,6 +239,7 @@ __global__ __launch_bounds__(256) void k_refill_direct(uint8_t *ops, int32_t str
         if (m) atomicAdd(&stripe[1], (unsigned long long)m);
         if (wr) atomicAdd(&stripe[2], (unsigned long long)wr);
         if (dr) atomicAdd(&stripe[3], (unsigned long long)dr);
+        if (ab) atomicAdd(&stripe[4], (unsigned long long)ab);
     }
     const int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)rank) % (uint32_t)tlen);
     const uint8_t oc = done ? top[t] : (uint8_t)kOpGet;
@@ -454,26 +459,6 @@ __global__ __launch_bounds__(256) void k_collect_vals(uint8_t *acks, const int32
     }
 }
 
-__global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32_t inv_stride, uint32_t op_size,
-                            uint8_t *acks, uint32_t ack_size, int32_t out_stride, int32_t *ack_count,
-                            const uint8_t *peers, int32_t n_peers, int64_t total)
-{
-    int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= total) return;
-    int64_t per_w = out_stride;     // slots x n_peers ACK positions per worker (host checks)
-    int32_t w = (int32_t)(g / per_w);
-    int32_t rem = (int32_t)(g - (int64_t)w * per_w);
-    int32_t j = rem / n_peers, r = rem - j * n_peers;
-    int32_t n = inv_count[w];
-    if (rem == 0) ack_count[w] = n * n_peers;
-    if (j >= n) return;
-    const uint64_t *src = reinterpret_cast<const uint64_t *>(invs + ((int64_t)w * inv_stride + j) * op_size);
-    // an ACK is the INV's 16-B op_meta (the rest of an op-sized ACK of an RMW build is not read)
-    uint64_t *dst = reinterpret_cast<uint64_t *>(acks + ((int64_t)w * out_stride + rem) * ack_size);
-    const W16 h = *reinterpret_cast<const W16 *>(src);
-    *reinterpret_cast<W16 *>(dst) = W16{h.a, with_op_state(h.b, kOpAck, peers[r])};  // ack_copy_and_modify_elem
-}
-
 // ack_skip_or_get_sender_id + ack_copy_and_modify_elem + ack_modify_elem_after_send
 __global__ void k_marshal_acks(uint8_t *invs, int64_t n, uint32_t op_size, uint8_t *out, uint32_t ack_size,
                                uint32_t machine_id)
@@ -603,30 +588,203 @@ __global__ __launch_bounds__(256) void k_regroup_aligned(const uint8_t *in, int3
     if (threadIdx.x == 0) out_count[w] = base < out_stride ? base : out_stride;
 }
 
-__global__ void k_gen_remote(uint8_t *invs, uint8_t *vals, int32_t per_peer, const uint8_t *peers, int32_t n_peers,
-                             uint32_t op_size, uint32_t st_value, uint32_t shift, hkv_zipf z, uint32_t clock,
-                             uint64_t seed, int64_t total)
+// ---- virtual peer replicas
+// A virtual peer stands for a replica that runs the same workload as this one. Its INVs of a
+// round are its successful writes: at most one per key and round (a second local write of the
+// key stalls on op_buffer_index, hermesKV.c:314-356), each with the timestamp its
+// update_actions_n_unlock gives (hermesKV.c:100-141): the key's current version + 2 (+4 for a
+// plain write in an RMW build) and the peer's id as cid. Keys, values and the dedup are drawn
+// once per round index (hkv_wl_gen_peer_round); the timestamps are taken from the table at the
+// start of each round (hkv_wl_peer_ts), when every replica holds the same converged state.
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x)
+{
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ULL;
+    return x ^ (x >> 33);
+}
+
+// open-addressed (peer, id) -> smallest order index, for the first-occurrence dedup
+__device__ __forceinline__ uint32_t dedup_slot(const unsigned long long *hk, uint64_t key, uint32_t mask, bool insert)
+{
+    uint32_t h = (uint32_t)mix64(key) & mask;
+    for (;;) {
+        unsigned long long cur = hk[h];
+        if (cur == key) return h;
+        if (cur == 0ull) {
+            if (!insert) return 0xFFFFFFFFu;
+            cur = atomicCAS(const_cast<unsigned long long *>(hk) + h, 0ull, (unsigned long long)key);
+            if (cur == 0ull || cur == key) return h;
+        }
+        h = (h + 1) & mask;
+    }
+}
+
+__global__ void k_peer_draw(uint32_t *ids, uint8_t *rmw, unsigned long long *hk, uint32_t *hmin, uint32_t mask,
+                            int32_t per_peer, int32_t n_peers, hkv_zipf z, uint32_t rmw_pm, uint32_t round,
+                            uint64_t seed, int64_t total)
+{
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= total) return;
+    const int64_t row = (int64_t)per_peer * n_peers;
+    const int32_t w = (int32_t)(g / row);
+    const int32_t rem = (int32_t)(g - (int64_t)w * row);
+    const int32_t r = rem / per_peer, j = rem - r * per_peer;
+    const uint64_t r1 = splitmix64(seed ^ ((uint64_t)round << 40) ^ (0x9E37ull * (uint64_t)g));
+    const uint32_t id = (uint32_t)zipf_draw(z, unit_double(r1));
+    ids[g] = id;
+    rmw[g] = rmw_pm && (uint32_t)((r1 >> 3) % 1000u) < rmw_pm;
+    const uint64_t key = (((uint64_t)r << 32) | id) + 1;
+    const uint32_t h = dedup_slot(hk, key, mask, true);
+    atomicMin(&hmin[h], (uint32_t)w * (uint32_t)per_peer + (uint32_t)j);  // the peer's own op order
+}
+
+// one workgroup per worker: each peer's first occurrences, compacted in peer order
+__global__ __launch_bounds__(256) void k_peer_compact(const uint32_t *ids, const uint8_t *rmw,
+                                                      const unsigned long long *hk, const uint32_t *hmin, uint32_t mask,
+                                                      uint8_t *invs, uint8_t *vals, int32_t *peer_counts,
+                                                      int32_t per_peer, const uint8_t *peers, int32_t n_peers,
+                                                      uint32_t op_size, uint32_t st_value, uint32_t shift)
+{
+    const int w = blockIdx.x;
+    const int32_t row = per_peer * n_peers;
+    int base = 0;
+    for (int r = 0; r < n_peers; ++r) {
+        const uint8_t peer = peers[r];
+        int cnt = 0;
+        for (int j0 = 0; j0 < per_peer; j0 += 256) {
+            const int j = j0 + (int)threadIdx.x;
+            const int64_t g = (int64_t)w * row + (int64_t)r * per_peer + j;
+            bool keep = false;
+            uint32_t id = 0;
+            if (j < per_peer) {
+                id = ids[g];
+                const uint32_t h = dedup_slot(hk, (((uint64_t)r << 32) | id) + 1, mask, false);
+                keep = h != 0xFFFFFFFFu && hmin[h] == (uint32_t)w * (uint32_t)per_peer + (uint32_t)j;
+            }
+            int total;
+            const int rank = block_rank(keep, total);
+            if (keep) {
+                const int64_t o = (int64_t)w * row + base + cnt + rank;
+                const uint64_t key = key_of_id(id);
+                const uint8_t f = rmw[g];
+                // inv_copy_and_modify_elem of the peer's op: version filled in per round
+                const uint64_t h1 = (uint64_t)kOpInv | ((uint64_t)peer << 8) | ((uint64_t)(st_value >> shift) << 16) |
+                                    ((uint64_t)peer << 24);
+                uint64_t *x = reinterpret_cast<uint64_t *>(invs + o * op_size);
+                x[0] = key;
+                x[1] = h1;
+                const uint64_t vv = 0x0101010101010101ULL * (uint8_t)('a' + peer);
+                x[2] = (vv << 16) | f;  // bytes 16..17: RMW_flag, no_coales 0; value from byte 18
+                for (uint32_t k = 3; k < op_size / 8; ++k) x[k] = vv;
+                uint64_t *v = reinterpret_cast<uint64_t *>(vals + o * kOpMetaSize);
+                v[0] = key;
+                v[1] = (h1 & ~0xFFull) | kOpVal;
+            }
+            cnt += total;
+        }
+        if (threadIdx.x == 0) peer_counts[(int64_t)w * n_peers + r] = cnt;
+        base += cnt;
+    }
+}
+
+// the MICA lookup of hermesKV.c:952-993 (first tag match, wrap test, 8-B key compare): the
+// entry's physical offset, or ~0 for a miss
+__device__ __forceinline__ uint64_t find_entry(const TableView &t, uint64_t key)
+{
+    const uint64_t *b = reinterpret_cast<const uint64_t *>(t.index + ((key & 0xFFFFFFFFFFFFULL) & t.g.bkt_mask) * 64u);
+    const uint32_t tag = (uint32_t)(key >> 48);
+    for (int s = 0; s < 8; ++s) {
+        const uint64_t slot = b[s];
+        if ((slot & 1u) && ((uint32_t)(slot >> 1) & 0x7FFFFFu) == tag) {
+            const uint64_t off = slot >> 24;
+            if (t.g.log_head - off >= t.g.log_cap) return ~0ull;
+            const uint64_t phys = off & t.g.log_mask;
+            return *reinterpret_cast<const uint64_t *>(t.log + phys + 8) == key ? phys : ~0ull;
+        }
+    }
+    return ~0ull;
+}
+
+// peer_ts words: round tag (23 bits) << 41 | the write's RMW flag << 40 | its 40-bit timestamp
+__device__ __forceinline__ uint32_t peer_round_tag(uint32_t round) { return (round + 1u) & 0x7FFFFFu; }
+
+// per round: every live peer INV (and its VAL) takes its key's current timestamp + the write's
+// step, cid = the peer; peer_ts (RMW builds) records the peer's write per [entry][peer id]
+__global__ void k_peer_ts(TableView t, uint8_t *invs, uint8_t *vals, const int32_t *counts, int32_t stride,
+                          uint32_t op_size, unsigned long long *peer_ts, uint32_t round, int64_t total)
+{
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= total) return;
+    const int32_t w = (int32_t)(g / stride);
+    if ((int32_t)(g - (int64_t)w * stride) >= counts[w]) return;
+    uint8_t *x = invs + g * op_size;
+    const uint64_t key = *reinterpret_cast<const uint64_t *>(x);
+    const uint64_t phys = find_entry(t, key);
+    const uint8_t peer = x[9];
+    uint32_t ver = 2;
+    if (phys != ~0ull) {
+        const uint8_t *e = t.log + phys;
+        const uint32_t step = (!t.g.rmw_enabled || (x[16] & 1u)) ? 2u : 4u;
+        ver = *reinterpret_cast<const uint32_t *>(e + kEntryMetaOff + 6) + step;
+        if (peer_ts && peer < 8)
+            atomicMax(peer_ts + (phys / t.g.entry_unit) * 8 + peer,
+                      ((unsigned long long)peer_round_tag(round) << 41) | ((unsigned long long)(x[16] & 1u) << 40) |
+                          ((unsigned long long)ver << 8) | peer);
+    }
+    // a fresh message each round: the batches of a previous use of the slab rewrote the opcodes
+    x[8] = kOpInv;
+    *reinterpret_cast<uint32_t *>(x + 12) = ver;
+    uint8_t *v = vals + g * kOpMetaSize;
+    v[8] = kOpVal;
+    *reinterpret_cast<uint32_t *>(v + 12) = ver;
+}
+
+// The virtual peers' answers to this round's INVs: an ACK (ack_copy_and_modify_elem,
+// hermes_worker.c:100-118) -- or, for an RMW INV whose timestamp is below the peer's own write of
+// the key this round (peer_ts, RMW builds), the INV-abort hermes_exec_inv makes at the peer
+// (hermesKV.c:566-576): the peer's local state (local_state_to_op, hermesKV.c:143-153: its RMW
+// flag, timestamp, val_len and value 'a' + peer) with opcode ST_OP_INV_ABORT and sender = peer.
+__global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32_t inv_stride, uint32_t op_size,
+                            uint8_t *acks, uint32_t ack_size, int32_t out_stride, int32_t *ack_count,
+                            const uint8_t *peers, int32_t n_peers, int64_t total, TableView t,
+                            const unsigned long long *peer_ts, uint32_t round)
 {
     int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= total) return;
-    int32_t r = (int32_t)((g / per_peer) % n_peers);
-    uint64_t r1 = splitmix64(seed ^ ((uint64_t)clock << 40) ^ (0x9E37ull * (uint64_t)g));
-    uint32_t id = (uint32_t)zipf_draw(z, unit_double(r1));
-    uint32_t ver = 2u * (clock + 1u + (uint32_t)((r1 >> 7) & 1u));
-    uint8_t peer = peers[r];
-    uint64_t key = key_of_id(id);
-    uint64_t h1 = (uint64_t)kOpInv | ((uint64_t)peer << 8) | ((uint64_t)(st_value >> shift) << 16) |
-                  ((uint64_t)peer << 24) | ((uint64_t)ver << 32);
-    uint64_t *x = reinterpret_cast<uint64_t *>(invs + g * op_size);
-    x[0] = key;
-    x[1] = h1;
-    uint64_t vv = 0x0101010101010101ULL * (uint8_t)('a' + peer);
-    // bytes 16..17: RMW_flag 0, no_coales 0; value from byte 18
-    x[2] = vv << 16;
-    for (uint32_t k = 3; k < op_size / 8; ++k) x[k] = vv;
-    uint64_t *v = reinterpret_cast<uint64_t *>(vals + g * kOpMetaSize);
-    v[0] = key;
-    v[1] = (h1 & ~0xFFull) | kOpVal;
+    int64_t per_w = out_stride;     // slots x n_peers ACK positions per worker (host checks)
+    int32_t w = (int32_t)(g / per_w);
+    int32_t rem = (int32_t)(g - (int64_t)w * per_w);
+    int32_t j = rem / n_peers, r = rem - j * n_peers;
+    int32_t n = inv_count[w];
+    if (rem == 0) ack_count[w] = n * n_peers;
+    if (j >= n) return;
+    const uint8_t *x = invs + ((int64_t)w * inv_stride + j) * op_size;
+    uint8_t *y = acks + ((int64_t)w * out_stride + rem) * ack_size;
+    const W16 h = *reinterpret_cast<const W16 *>(x);
+    const uint8_t peer = peers[r];
+    if (peer_ts && (x[16] & 1u) && peer < 8 && ack_size >= op_size) {
+        const uint64_t phys = find_entry(t, h.a);
+        if (phys != ~0ull) {
+            const unsigned long long pw = peer_ts[(phys / t.g.entry_unit) * 8 + peer];
+            const uint64_t ours = ((uint64_t)(uint32_t)(h.b >> 32) << 8) | (uint8_t)(h.b >> 24);
+            if ((uint32_t)(pw >> 41) == peer_round_tag(round) && (pw & 0xFFFFFFFFFFull) > ours) {
+                const uint64_t pts = pw & 0xFFFFFFFFFFull;
+                uint64_t *d = reinterpret_cast<uint64_t *>(y);
+                d[0] = h.a;
+                d[1] = (uint64_t)kOpInvAbort | ((uint64_t)peer << 8) | ((uint64_t)(uint8_t)x[10] << 16) |
+                       ((pts & 0xFFull) << 24) | ((pts >> 8) << 32);
+                // the peer key's RMW flag is its write's (update_actions, hermesKV.c:100-141)
+                const uint64_t vv = 0x0101010101010101ULL * (uint8_t)('a' + peer);
+                d[2] = (vv << 16) | ((uint64_t)x[17] << 8) | ((pw >> 40) & 1u);
+                for (uint32_t k = 3; k < op_size / 8; ++k) d[k] = vv;
+                return;
+            }
+        }
+    }
+    *reinterpret_cast<W16 *>(y) = W16{h.a, with_op_state(h.b, kOpAck, peer)};  // ack_copy_and_modify_elem
 }
 
 }  // namespace hkv
@@ -696,27 +854,81 @@ int hkv_wl_marshal_vals(uint8_t *acks, int64_t n, uint32_t ack_size, uint8_t *ou
     return ok();
 }
 
-int hkv_wl_peer_acks(const uint8_t *inv_out, const int32_t *inv_count, int32_t n_workers, int32_t inv_stride,
-                     uint32_t op_size, uint8_t *acks, uint32_t ack_size, int32_t out_stride, int32_t *ack_count,
-                     const uint8_t *peer_ids, int32_t n_peers, void *stream)
+int hkv_wl_peer_acks(hkv_table *t, const uint8_t *inv_out, const int32_t *inv_count, int32_t n_workers,
+                     int32_t inv_stride, uint32_t op_size, uint8_t *acks, uint32_t ack_size, int32_t out_stride,
+                     int32_t *ack_count, const uint8_t *peer_ids, int32_t n_peers,
+                     const unsigned long long *peer_ts, uint32_t round, void *stream)
 {
     if (n_peers <= 0 || n_workers <= 0 || ack_size < kOpMetaSize || ack_size % 8) return -1;
     if (out_stride % n_peers || out_stride > inv_stride * n_peers || out_stride <= 0) return -1;
+    TableView tv{};
+    if (peer_ts && table_view(t, &tv)) return -1;
     int64_t total = (int64_t)n_workers * out_stride;
     hipLaunchKernelGGL(k_peer_acks, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, inv_out, inv_count,
-                       inv_stride, op_size, acks, ack_size, out_stride, ack_count, peer_ids, n_peers, total);
+                       inv_stride, op_size, acks, ack_size, out_stride, ack_count, peer_ids, n_peers, total, tv,
+                       peer_ts, round);
     return ok();
 }
 
-int hkv_wl_gen_remote(uint8_t *invs, uint8_t *vals, int32_t n_workers, int32_t per_peer, const uint8_t *peer_ids,
-                      int32_t n_peers, uint32_t op_size, uint32_t st_value, uint32_t shift, const hkv_zipf *z,
-                      uint32_t clock, uint64_t seed, void *stream)
+static size_t peer_slots(int64_t total)
 {
-    int64_t total = (int64_t)n_workers * per_peer * n_peers;
+    size_t s = 1024;
+    while (s < 2 * (size_t)total) s <<= 1;
+    return s;
+}
+
+static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+size_t hkv_wl_peer_round_scratch(int32_t n_workers, int32_t per_peer, int32_t n_peers)
+{
+    const int64_t total = (int64_t)n_workers * per_peer * n_peers;
+    const size_t slots = peer_slots(total);
+    return align_up(8 * slots) + align_up(4 * slots) + align_up(4 * (size_t)total) + align_up((size_t)total);
+}
+
+int hkv_wl_gen_peer_round(uint8_t *invs, uint8_t *vals, int32_t *peer_counts, int32_t n_workers, int32_t per_peer,
+                          const uint8_t *peer_ids, int32_t n_peers, uint32_t op_size, uint32_t st_value,
+                          uint32_t shift, const hkv_zipf *z, uint32_t rmw_pm, uint32_t round, uint64_t seed,
+                          void *scratch, void *stream)
+{
+    const int64_t total = (int64_t)n_workers * per_peer * n_peers;
     if (total <= 0) return 0;
-    hipLaunchKernelGGL(k_gen_remote, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, invs, vals, per_peer,
-                       peer_ids, n_peers, op_size, st_value, shift, *z, clock, seed, total);
+    if (op_size % 8 || op_size < kOpValueOff + st_value || total > 0x7FFFFFFFll) return -1;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t slots = peer_slots(total);
+    uint8_t *p = static_cast<uint8_t *>(scratch);
+    unsigned long long *hk = reinterpret_cast<unsigned long long *>(p);
+    p += align_up(8 * slots);
+    uint32_t *hmin = reinterpret_cast<uint32_t *>(p);
+    p += align_up(4 * slots);
+    uint32_t *ids = reinterpret_cast<uint32_t *>(p);
+    p += align_up(4 * (size_t)total);
+    uint8_t *rmw = p;
+    if (hipMemsetAsync(hk, 0, 8 * slots, s) != hipSuccess || hipMemsetAsync(hmin, 0xFF, 4 * slots, s) != hipSuccess)
+        return -5;
+    hipLaunchKernelGGL(k_peer_draw, dim3(blocks_for(total)), dim3(256), 0, s, ids, rmw, hk, hmin,
+                       (uint32_t)(slots - 1), per_peer, n_peers, *z, rmw_pm, round, seed, total);
+    hipLaunchKernelGGL(k_peer_compact, dim3(n_workers), dim3(256), 0, s, ids, rmw, hk, hmin, (uint32_t)(slots - 1), invs,
+                       vals, peer_counts, per_peer, peer_ids, n_peers, op_size, st_value, shift);
     return ok();
+}
+
+int hkv_wl_peer_ts(hkv_table *t, uint8_t *invs, uint8_t *vals, const int32_t *counts, int32_t n_workers,
+                   int32_t stride, uint32_t op_size, unsigned long long *peer_ts, uint32_t round, void *stream)
+{
+    TableView tv;
+    if (table_view(t, &tv) || n_workers <= 0 || stride <= 0 || op_size % 8) return -1;
+    const int64_t total = (int64_t)n_workers * stride;
+    hipLaunchKernelGGL(k_peer_ts, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, tv, invs, vals, counts,
+                       stride, op_size, peer_ts, round, total);
+    return ok();
+}
+
+uint64_t hkv_wl_peer_ts_words(const hkv_table *t)
+{
+    TableView tv;
+    if (table_view(t, &tv)) return 0;
+    return (tv.g.log_cap / tv.g.entry_unit + 1) * 8;
 }
 
 int hkv_wl_marshal_invs_cap(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint8_t *out,

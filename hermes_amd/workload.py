@@ -42,11 +42,17 @@ _L.hkv_wl_max_to_host.argtypes = [_P, ctypes.c_int32, _P, _P]
 _L.hkv_wl_marshal_vals.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_collect_vals.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
                                    _P, ctypes.c_uint32, _P, _P]
-_L.hkv_wl_peer_acks.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_uint32,
-                                ctypes.c_int32, _P, _P, ctypes.c_int32, _P]
-_L.hkv_wl_gen_remote.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32, ctypes.c_uint32,
-                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(HkvZipf), ctypes.c_uint32,
-                                 ctypes.c_uint64, _P]
+_L.hkv_wl_peer_acks.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_uint32,
+                                ctypes.c_int32, _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, _P]
+_L.hkv_wl_peer_round_scratch.restype = ctypes.c_size_t
+_L.hkv_wl_peer_round_scratch.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
+_L.hkv_wl_gen_peer_round.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32,
+                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(HkvZipf),
+                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, _P, _P]
+_L.hkv_wl_peer_ts.argtypes = [_P, _P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P,
+                              ctypes.c_uint32, _P]
+_L.hkv_wl_peer_ts_words.restype = ctypes.c_uint64
+_L.hkv_wl_peer_ts_words.argtypes = [_P]
 
 
 def slots_per_worker(write_permille: int, rmw_permille: int = 0, batch: int = 250) -> int:
@@ -142,8 +148,14 @@ class Round:
                                   ctypes.c_uint64(seed ^ (self.machine_id << 48)), _s()), "gen_trace")
         self.clock = 0
         self.max_steps = max_steps
+        self.rmw_pm = rmw_permille
         self.remote_inv = []
         self.remote_val = []
+        self.remote_counts = []        # per round index: [n live peers] -> per-worker counts
+        # RMW builds: each virtual peer's write of the round per [entry][peer], for its INV-aborts
+        self.peer_ts = None
+        if virtual_peers and self.R and kvs.rmw:
+            self.peer_ts = torch.zeros(int(_L.hkv_wl_peer_ts_words(kvs.h)), dtype=torch.int64, device=dev)
         self.drops = []                # peers dropped from the membership (membership_change)
         self.alive = self.R            # live peers: the first `alive` slots of the remote slabs
         self._counts = {}
@@ -151,19 +163,27 @@ class Round:
         self.refill(first=True)
 
     def _gen_remote(self):
-        """INV + VAL slabs [W][R][rpp] of the virtual peers, one per round index"""
+        """INV + VAL slabs [W][R * rpp] of the virtual peers, one per round index: each peer's
+        first write of a key in the round, compacted per worker in peer order
+        (hkv_wl_gen_peer_round); the timestamps are taken at the start of each round"""
         if not (self.virtual and self.R):
             return
-        W, dev = self.W, torch.device("cuda", self.kvs.device)
+        W, R, dev = self.W, self.R, torch.device("cuda", self.kvs.device)
         u8 = dict(dtype=torch.uint8, device=dev)
+        scratch = torch.empty(int(_L.hkv_wl_peer_round_scratch(W, self.rpp, R)), **u8)
+        pc = torch.empty(W * R, dtype=torch.int32, device=dev)
         for k in range(self.max_steps):
-            ri = torch.empty(W * self.rstride * self.op, **u8)
-            rv = torch.empty(W * self.rstride * L.OP_META_SIZE, **u8)
-            check(_L.hkv_wl_gen_remote(_ptr(ri), _ptr(rv), W, self.rpp, _ptr(self.peer_t), self.R, self.op,
-                                       self.sizes.st_value, self.sizes.shift, ctypes.byref(self.zipf), k,
-                                       ctypes.c_uint64(self.seed * 7919 + self.machine_id), _s()), "gen_remote")
+            ri = torch.zeros(W * self.rstride * self.op, **u8)
+            rv = torch.zeros(W * self.rstride * L.OP_META_SIZE, **u8)
+            check(_L.hkv_wl_gen_peer_round(_ptr(ri), _ptr(rv), _ptr(pc), W, self.rpp, _ptr(self.peer_t), R, self.op,
+                                           self.sizes.st_value, self.sizes.shift, ctypes.byref(self.zipf),
+                                           self.rmw_pm, k, ctypes.c_uint64(self.seed * 7919 + self.machine_id),
+                                           _ptr(scratch), _s()), "gen_peer_round")
+            cum = torch.cumsum(pc.view(W, R), dim=1, dtype=torch.int32)
+            self.remote_counts.append([None] + [cum[:, n - 1].contiguous() for n in range(1, R + 1)])
             self.remote_inv.append(ri)
             self.remote_val.append(rv)
+        del scratch
 
     # -- pieces of one round
     def refill(self, first: bool = False):
@@ -181,10 +201,18 @@ class Round:
               "marshal_invs")
 
     def virtual_peer_acks(self, n_peers: int | None = None):
-        """ACKs of the first n_peers virtual peers (default all) to this round's INVs"""
-        check(_L.hkv_wl_peer_acks(_ptr(self.inv_out), _ptr(self.inv_count), self.W, self.C, self.op,
+        """ACKs (INV-aborts for RMWs a peer's own write beats) of the first n_peers virtual peers
+        (default all) to this round's INVs"""
+        check(_L.hkv_wl_peer_acks(self.kvs.h, _ptr(self.inv_out), _ptr(self.inv_count), self.W, self.C, self.op,
                                   _ptr(self.acks), self.ack_size, self.ack_width, _ptr(self.ack_count),
-                                  _ptr(self.peer_t), self.R if n_peers is None else n_peers, _s()), "peer_acks")
+                                  _ptr(self.peer_t), self.R if n_peers is None else n_peers, _ptr(self.peer_ts),
+                                  self.clock, _s()), "peer_acks")
+
+    def peer_timestamps(self, k: int, n_peers: int):
+        """Round start: the live peers' INVs and VALs of round index k take their timestamps"""
+        check(_L.hkv_wl_peer_ts(self.kvs.h, _ptr(self.remote_inv[k]), _ptr(self.remote_val[k]),
+                                _ptr(self.remote_counts[k][n_peers]), self.W, self.rstride, self.op,
+                                _ptr(self.peer_ts), self.clock, _s()), "peer_ts")
 
     def inv_batch(self, invs: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None):
         self.kvs.batch(L.BatchType.invs, invs, n_batches, stride, self.op, self.mb, counts=counts)
@@ -236,6 +264,8 @@ class Round:
             assert self.virtual and self.alive and drop == self.peers[self.alive - 1], "drop the last live peer"
         sent = self.alive                          # peers whose INVs this round applies
         alive = self.alive - (drop is not None)    # peers that answer them (ACKs) and send VALs
+        if self.R and sent:
+            self.peer_timestamps(k, sent)
         timed("local", self.local_batch)
         self.marshal_invs()
         if self.count_elems:
@@ -245,7 +275,7 @@ class Round:
             self.maxc_ev.record()
         if self.R:
             ri, rv = self.remote_inv[k], self.remote_val[k]
-            ic = self._slot_counts(sent)
+            ic = self._slot_counts(k, sent)
             timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride, counts=ic))
             self.marshal_acks(ri, self.W * self.rstride, self.ack_out)
             m = self.C
@@ -260,25 +290,25 @@ class Round:
                     self.elem_totals[1] += self.ack_count.sum()
                 self.collect_vals()
             # a dropped peer sent its INVs but fails before its VALs
-            vc = self._slot_counts(alive)
+            vc = self._slot_counts(k, alive)
             timed("vals", lambda: self.val_batch(rv, self.W, self.rstride, counts=vc))
             if self.count_elems:
-                self.elem_totals[0] += self.W * sent * self.rpp
-                self.elem_totals[2] += self.W * alive * self.rpp
+                self.elem_totals[0] += ic.sum()
+                if alive:
+                    self.elem_totals[2] += vc.sum()
         if drop is not None:
             self.membership_change(drop)
         self.refill()
         self.clock += 1
 
-    def _slot_counts(self, n_peers: int):
-        """Per-worker counts applying the first n_peers slots of the [W][R][rpp] remote slabs
-        (None: all of them)"""
-        if n_peers == self.R:
-            return None
-        if n_peers not in self._counts:
-            self._counts[n_peers] = torch.full((self.W,), n_peers * self.rpp, dtype=torch.int32,
-                                               device=self.inv_count.device)
-        return self._counts[n_peers]
+    def _slot_counts(self, k: int, n_peers: int):
+        """Per-worker counts applying the first n_peers peers' elements of round index k's
+        remote slabs (peer order within each worker's row)"""
+        if n_peers == 0:
+            if 0 not in self._counts:
+                self._counts[0] = torch.zeros(self.W, dtype=torch.int32, device=self.inv_count.device)
+            return self._counts[0]
+        return self.remote_counts[k][n_peers]
 
     def membership_change(self, peer: int):
         """The group drops `peer` (group_membership_update, inline-util.h:26-43) and every worker
@@ -300,5 +330,6 @@ class Round:
         return int(self.counters[0].item())
 
     def stats(self) -> dict:
-        c = self.counters[:3].cpu().tolist()
-        return {"committed": c[0], "misses": c[1], "writes_completed": c[2], "invs_held": int(self.held.item())}
+        c = self.counters[:5].cpu().tolist()
+        return {"committed": c[0], "misses": c[1], "writes_completed": c[2], "dropped": c[3], "rmw_aborts": c[4],
+                "invs_held": int(self.held.item())}

@@ -11,20 +11,24 @@
  *   hkv_wl_marshal_acks   ack_skip_or_get_sender_id / ack_copy_and_modify_elem, :69-118
  *   hkv_wl_marshal_vals   val_skip_or_get_sender_id / val_copy_and_modify_elem, :122-157
  *   hkv_wl_marshal_memb_vals  memb_change_* callbacks, :163-203
- *   hkv_wl_peer_acks      the ACKs `n_peers` replicas answer to a slab of INVs (the remote
- *                         side of hermes_worker.c:467-473 for INVs they accept)
- *   hkv_wl_gen_remote     INVs + VALs written by virtual peer replicas (a coordinator's
+ *   hkv_wl_peer_acks      the ACKs / INV-aborts `n_peers` replicas answer to a slab of INVs
+ *                         (the remote side of hermes_worker.c:467-473)
+ *   hkv_wl_gen_peer_round, hkv_wl_peer_ts
+ *                         INVs + VALs written by virtual peer replicas (a coordinator's
  *                         inv_copy_and_modify_elem + val_copy_and_modify_elem)
  * All device pointers; stream = hipStream_t or NULL.
  */
 #ifndef HERMESKV_WORKLOAD_H
 #define HERMESKV_WORKLOAD_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+typedef struct hkv_table hkv_table;
 
 typedef struct hkv_zipf {
     double theta;      /* 0 = uniform */
@@ -49,9 +53,9 @@ int hkv_wl_gen_trace(uint64_t *d_trace_key, uint8_t *d_trace_op, uint32_t *d_tra
  * *_COMPLETE_SEND_VALS, membership change) always keep their slot.
  * Adds completed-and-committed ops (everything complete except ST_MISS and ST_RMW_ABORT)
  * to d_counters[0], misses to d_counters[1], completed writes to d_counters[2], dropped
- * stalled ops to d_counters[3].
+ * stalled ops to d_counters[3], RMW aborts (ST_RMW_ABORT) to d_counters[4].
  * d_counters holds HKV_WL_COUNTER_WORDS words, zeroed by the caller once: words from
- * HKV_WL_STRIPE_BASE on are per-worker-group partial sums the call folds back into [0..3]
+ * HKV_WL_STRIPE_BASE on are per-worker-group partial sums the call folds back into [0..4]
  * (one counter address hit by every worker serialises in L2). */
 #define HKV_WL_COUNTER_WORDS 4096
 #define HKV_WL_STRIPE_BASE 64
@@ -77,22 +81,45 @@ int hkv_wl_marshal_acks(uint8_t *d_invs, int64_t n, uint32_t op_size, uint8_t *d
 int hkv_wl_marshal_vals(uint8_t *d_acks, int64_t n, uint32_t ack_size, uint8_t *d_val_out,
                         uint32_t machine_id, void *stream);
 
-/* ACK batch answering a slab of INVs from n_peers replicas: for INV j of worker w, the
- * ack_size-byte element d_acks[w*out_stride + j*n_peers + r] gets the op_meta {key, ST_OP_ACK,
- * sender = peer_ids[r], ts = inv ts} (ack_size: 16, or the op size in an RMW build);
- * d_ack_count[w] = n_peers * d_inv_count[w]. out_stride is a multiple of n_peers, at most
- * inv_stride * n_peers, and the caller keeps every d_inv_count[w] <= out_stride / n_peers (the N=1
- * round fits it to the round's largest count) */
-int hkv_wl_peer_acks(const uint8_t *d_inv_out, const int32_t *d_inv_count, int32_t n_workers, int32_t inv_stride,
-                     uint32_t op_size, uint8_t *d_acks, uint32_t ack_size, int32_t out_stride,
-                     int32_t *d_ack_count, const uint8_t *peer_ids, int32_t n_peers, void *stream);
+/* ---- virtual peer replicas (one-GPU rounds) ------------------------------------------
+ * A virtual peer stands for a replica running the same workload. Per round it sends its
+ * successful writes: at most one per key (a second local write of a key stalls on
+ * op_buffer_index, hermesKV.c:314-356), timestamped by update_actions_n_unlock
+ * (hermesKV.c:100-141) from the key's state at round start: version + 2 (+4 for a plain write
+ * in an RMW build), cid = the peer. */
 
-/* INVs (op_size bytes) and matching VALs (16 bytes) written by n_peers virtual replicas:
- * per worker w and peer r, `per_peer` INVs on keys drawn from zipf, timestamp
- * (2*(clock + 1 + coin), peer_ids[r]), value bytes 'a' + peer id. */
-int hkv_wl_gen_remote(uint8_t *d_invs, uint8_t *d_vals, int32_t n_workers, int32_t per_peer,
-                      const uint8_t *peer_ids, int32_t n_peers, uint32_t op_size, uint32_t st_value,
-                      uint32_t shift, const hkv_zipf *zipf, uint32_t clock, uint64_t seed, void *stream);
+/* Draws `per_peer` Zipf keys per worker and peer for round index `round`, keeps each peer's
+ * first occurrence of every key (in the peer's worker-major op order), and writes the kept
+ * ones compacted per worker in peer order: d_invs / d_vals [n_workers][n_peers * per_peer]
+ * (op_size-byte INVs with value 'a' + peer and RMW_flag drawn with rmw_permille; 16-B VALs),
+ * d_peer_counts[w * n_peers + r] = how many of peer r's. The timestamps are filled in per
+ * round by hkv_wl_peer_ts. d_scratch: hkv_wl_peer_round_scratch() bytes. */
+size_t hkv_wl_peer_round_scratch(int32_t n_workers, int32_t per_peer, int32_t n_peers);
+int hkv_wl_gen_peer_round(uint8_t *d_invs, uint8_t *d_vals, int32_t *d_peer_counts, int32_t n_workers,
+                          int32_t per_peer, const uint8_t *d_peer_ids, int32_t n_peers, uint32_t op_size,
+                          uint32_t st_value, uint32_t shift, const hkv_zipf *zipf, uint32_t rmw_permille,
+                          uint32_t round, uint64_t seed, void *d_scratch, void *stream);
+
+/* At the start of a round: the first d_counts[w] INVs of each worker's row (and their VALs) take
+ * the timestamp the peer's write gives, read from table t. d_peer_ts (RMW builds, may be NULL;
+ * hkv_wl_peer_ts_words() zeroed words) records each peer's write per [entry][peer id] for
+ * hkv_wl_peer_acks. */
+int hkv_wl_peer_ts(hkv_table *t, uint8_t *d_invs, uint8_t *d_vals, const int32_t *d_counts, int32_t n_workers,
+                   int32_t stride, uint32_t op_size, unsigned long long *d_peer_ts, uint32_t round, void *stream);
+uint64_t hkv_wl_peer_ts_words(const hkv_table *t);
+
+/* The virtual peers' answers to this round's INVs: for INV j of worker w, the ack_size-byte
+ * element d_acks[w*out_stride + j*n_peers + r] from peer_ids[r] is an ACK {key, ST_OP_ACK,
+ * sender, ts = inv ts} (ack_copy_and_modify_elem, hermes_worker.c:100-118) -- or, with d_peer_ts
+ * and an RMW INV below the peer's own write of the key this round, the INV-abort the peer's
+ * hermes_exec_inv returns (hermesKV.c:566-576: the peer's RMW flag, timestamp and value). ack_size:
+ * 16, or the op size in an RMW build; d_ack_count[w] = n_peers * d_inv_count[w]. out_stride is a
+ * multiple of n_peers, at most inv_stride * n_peers, and the caller keeps every d_inv_count[w] <=
+ * out_stride / n_peers (the N=1 round fits it to the round's largest count) */
+int hkv_wl_peer_acks(hkv_table *t, const uint8_t *d_inv_out, const int32_t *d_inv_count, int32_t n_workers,
+                     int32_t inv_stride, uint32_t op_size, uint8_t *d_acks, uint32_t ack_size, int32_t out_stride,
+                     int32_t *d_ack_count, const uint8_t *peer_ids, int32_t n_peers,
+                     const unsigned long long *d_peer_ts, uint32_t round, void *stream);
 
 /* ---- replica groups (one replica per GPU, slabs exchanged over RCCL) ------------------ */
 

@@ -87,23 +87,55 @@ int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, doub
         tkey[g] = key_of(id);
         top[g] = (uint32_t)(r2 % 1000u) < write_pm ? OPC_PUT : OPC_GET;
     }
-    /* peer INVs + VALs, P rounds deep; the version field holds the coin until use, when it
-     * becomes 2*(round + 1 + coin) -- the same peer clock as the GPU run */
-    for (int64_t g = 0; g < (int64_t)n_workers * P * rstride; g++) {
-        int64_t k = g / ((int64_t)n_workers * rstride);
-        int r = (int)((g / per_peer) % n_peers);
-        uint64_t r1 = sm64(seed ^ ((uint64_t)k << 40) ^ (0x9E37ull * (uint64_t)g));
-        uint32_t id = (uint32_t)zipf_draw(z, (double)(r1 >> 11) * (1.0 / 9007199254740992.0));
-        uint32_t ver = (uint32_t)((r1 >> 7) & 1u);
-        uint8_t peer = (uint8_t)(1 + r);
-        uint8_t *x = rinv_pool + g * osz, *v = rval_pool + g * 16;
-        uint64_t key = key_of(id);
-        memcpy(x, &key, 8);
-        x[8] = OPC_INV; x[9] = peer; x[10] = (uint8_t)sv; x[11] = peer;
-        memcpy(x + 12, &ver, 4);
-        memset(x + 18, 'a' + peer, sv);
-        memcpy(v, x, 16);
-        v[8] = OPC_VAL;
+    /* peer INVs + VALs, P round indices deep: per round, each virtual peer's first write of a key
+     * (in its worker-major op order), compacted per worker in peer order -- the GPU run's
+     * hkv_wl_gen_peer_round. The timestamps are taken from the table when a round uses them. */
+    int32_t *rcount = calloc((size_t)n_workers * P, sizeof(int32_t));
+    {
+        const int64_t per_round = (int64_t)n_workers * rstride;
+        size_t hs = 1024;
+        while (hs < 2 * (size_t)(per_round ? per_round : 1)) hs <<= 1;
+        uint64_t *hk = malloc(hs * sizeof(uint64_t));
+        uint32_t *ids = malloc(sizeof(uint32_t) * (size_t)(per_round ? per_round : 1));
+        uint8_t *keep = malloc((size_t)(per_round ? per_round : 1));
+        for (int k = 0; k < P && rstride; k++) {
+            memset(hk, 0, hs * sizeof(uint64_t));
+            for (int64_t g = 0; g < per_round; g++) {
+                uint64_t r1 = sm64(seed ^ ((uint64_t)k << 40) ^ (0x9E37ull * (uint64_t)g));
+                ids[g] = (uint32_t)zipf_draw(z, (double)(r1 >> 11) * (1.0 / 9007199254740992.0));
+            }
+            /* peer-major over the worker-major draws: a (peer, id) pair's first occurrence wins */
+            for (int r = 0; r < n_peers; r++)
+                for (int w = 0; w < n_workers; w++)
+                    for (int j = 0; j < per_peer; j++) {
+                        int64_t g = (int64_t)w * rstride + (int64_t)r * per_peer + j;
+                        uint64_t key = (((uint64_t)r << 32) | ids[g]) + 1;
+                        size_t h = (size_t)(sm64(key) & (hs - 1));
+                        while (hk[h] != 0 && hk[h] != key) h = (h + 1) & (hs - 1);
+                        keep[g] = hk[h] == 0;
+                        hk[h] = key;
+                    }
+            for (int w = 0; w < n_workers; w++) {
+                int cnt = 0;
+                for (int r = 0; r < n_peers; r++)
+                    for (int j = 0; j < per_peer; j++) {
+                        int64_t g = (int64_t)w * rstride + (int64_t)r * per_peer + j;
+                        if (!keep[g]) continue;
+                        uint8_t peer = (uint8_t)(1 + r);
+                        size_t o = ((size_t)k * n_workers + w) * rstride + cnt++;
+                        uint8_t *x = rinv_pool + o * osz, *v = rval_pool + o * 16;
+                        uint64_t key = key_of(ids[g]);
+                        memcpy(x, &key, 8);
+                        x[8] = OPC_INV; x[9] = peer; x[10] = (uint8_t)sv; x[11] = peer;
+                        memset(x + 12, 0, 6);
+                        memset(x + 18, 'a' + peer, sv);
+                        memcpy(v, x, 16);
+                        v[8] = OPC_VAL;
+                    }
+                rcount[(size_t)k * n_workers + w] = cnt;
+            }
+        }
+        free(hk); free(ids); free(keep);
     }
     int64_t committed = 0, rounds = 0;
     int first = 1;
@@ -153,18 +185,22 @@ int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, doub
             }
             if (rstride) {
                 size_t k = (size_t)(rounds % P) * n_workers + w;
-                memcpy(rinv, rinv_pool + k * rstride * osz, (size_t)rstride * osz);
-                memcpy(rval, rval_pool + k * rstride * 16, (size_t)rstride * 16);
-                for (int i = 0; i < rstride; i++) {
-                    uint32_t coin, ver;
-                    memcpy(&coin, rinv + (size_t)i * osz + 12, 4);
-                    ver = 2u * ((uint32_t)rounds + 1u + coin);
+                const int rn = rcount[k];
+                memcpy(rinv, rinv_pool + k * rstride * osz, (size_t)rn * osz);
+                memcpy(rval, rval_pool + k * rstride * 16, (size_t)rn * 16);
+                /* the peer's write: the key's current version + 2, cid = the peer (hermesKV.c:100-141) */
+                for (int i = 0; i < rn; i++) {
+                    uint64_t key;
+                    memcpy(&key, rinv + (size_t)i * osz, 8);
+                    const uint8_t *e = hko_lookup(kv, key);
+                    uint32_t ver = 2;
+                    if (e) { memcpy(&ver, e + 24, 4); ver += 2; }
                     memcpy(rinv + (size_t)i * osz + 12, &ver, 4);
                     memcpy(rval + (size_t)i * 16 + 12, &ver, 4);
                 }
                 int ns = -1;
-                hko_batch(kv, 2, rinv, rstride, (uint16_t)osz, membership, &ns, NULL);
-                for (int i = 0; i < rstride; i++) { /* ACKs back to the peers */
+                hko_batch(kv, 2, rinv, rn, (uint16_t)osz, membership, &ns, NULL);
+                for (int i = 0; i < rn; i++) { /* ACKs back to the peers */
                     uint8_t *x = rinv + (size_t)i * osz, *a = ack_out + (size_t)i * 16;
                     if (x[8] == 124) { memcpy(a, x, 16); a[8] = OPC_ACK; a[9] = mid; }
                     x[8] = 140;
@@ -175,7 +211,7 @@ int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, doub
                     if (a[8] == 126) { memcpy(v, a, 16); v[8] = OPC_VAL; v[9] = mid; }
                     a[8] = 140;
                 }
-                hko_batch(kv, 4, rval, rstride, 16, membership, NULL, NULL);
+                hko_batch(kv, 4, rval, rn, 16, membership, NULL, NULL);
             }
         }
         rounds++;
@@ -190,6 +226,6 @@ int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, doub
     *out_rounds = rounds;
     *out_secs = t - t0;
     free(ops); free(inv_out); free(acks); free(ack_out); free(val_out); free(rinv_pool); free(rval_pool);
-    free(rinv); free(rval); free(tkey); free(top); free(cursor);
+    free(rinv); free(rval); free(tkey); free(top); free(cursor); free(rcount);
     return committed;
 }

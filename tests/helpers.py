@@ -1,6 +1,7 @@
 """Shared test helpers: build op/message arrays and drive the known-answer scenario."""
 from __future__ import annotations
 
+import collections
 import json
 import os
 
@@ -80,8 +81,17 @@ class Mirror:
     def __init__(self, g, o, name):
         self.g, self.o, self.name = g, o, name
         self.launches = 0
+        self.codes = collections.Counter()   # (batch type, "in8"/"out8"/"out9", code) over live elements
         self._orig = g.batch
         g.batch = self.batch
+
+    def _count(self, btype, tag, col, arr, n_batches, stride, elem_size, counts):
+        v = arr.reshape(n_batches, stride, elem_size)[:, :, col]
+        if counts is not None:
+            v = v[np.arange(stride)[None, :] < counts[:, None]]
+        vals, cnt = np.unique(v, return_counts=True)
+        for x, c in zip(vals.tolist(), cnt.tolist()):
+            self.codes[(int(btype), tag, x)] += c
 
     def batch(self, btype, elems, n_batches, stride, elem_size, membership, counts=None, rw=None,
               rw_stride_bytes=0, node_suspected=None, stream=None):
@@ -91,6 +101,7 @@ class Mirror:
         vt = np.dtype((np.void, elem_size))
         e_in = elems[:n].cpu().numpy().copy().view(vt)
         c_in = counts[:n_batches].cpu().numpy().copy() if counts is not None else None
+        self._count(btype, "in8", 8, np.frombuffer(e_in.tobytes(), np.uint8), n_batches, stride, elem_size, c_in)
         rw_in = rw_op = None
         if rw is not None:
             rw_in = rw.cpu().numpy().copy().view(np.dtype((np.void, self.g.sizes.op)))
@@ -101,6 +112,8 @@ class Mirror:
                            rw_stride_bytes // self.g.sizes.op if rw is not None else 0)
         what = f"{self.name} launch {self.launches} type {int(btype)}"
         got = elems[:n].cpu().numpy()
+        self._count(btype, "out8", 8, got, n_batches, stride, elem_size, c_in)
+        self._count(btype, "out9", 9, got, n_batches, stride, elem_size, c_in)
         if not np.array_equal(got, e_in.view(np.uint8)):
             bad = np.nonzero(got != e_in.view(np.uint8))[0]
             pytest.fail(f"{what}: elements differ at {len(bad)} bytes, first elems {np.unique(bad // elem_size)[:8]}")

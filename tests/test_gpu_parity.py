@@ -471,3 +471,31 @@ def test_ack_direct_path_edge_cases(big):
         val_o = gen.bytecopy(val)
         _run_both(g, o, L.BatchType.vals, val, val_o, mb, W, S, None)
         assert_elems_equal(val, val_o, f"round {rnd} vals")
+
+
+@pytest.mark.parametrize("cfg", CONFIGS)
+def test_scripted_rare_outcomes(cfg):
+    """tests/scripted.py through the device path and the oracle side by side: every step's
+    elements, read_write_ops, node_suspected and table image bit-exact, the scripted outcomes
+    (OUT_OF_GROUP, INV-aborts both ways, RMW_ABORT, ST_EMPTY reads, LAST_ACK completions of PUTs,
+    RMWs and GET replays, write replays, *_COMPLETE_SEND_VALS after membership changes) all
+    produced, covering every outcome code the batch function can emit in the build."""
+    from tests.scripted import required_outcomes, run_scripted
+    rmw, big = cfg["rmw"], cfg["big"]
+    g, o, sizes = make_pair(1000, 4096, 1 << 22, rmw=rmw, big=big)
+
+    def runner(btype, elems, mb, rw=None, node_suspected=None):
+        eo, rwo = gen.bytecopy(elems), (gen.bytecopy(rw) if rw is not None else None)
+        ns_o = node_suspected.copy() if node_suspected is not None else None
+        g.batch_host(btype, elems, mb, rw=rw, node_suspected=node_suspected)
+        o.batch_multi(btype, eo, 1, len(eo), None, mb, rw=rwo, node_suspected=ns_o)
+        assert_elems_equal(elems, eo, f"scripted type {int(btype)}")
+        if rw is not None:
+            assert_elems_equal(rw, rwo, f"scripted type {int(btype)} rw")
+        if node_suspected is not None:
+            np.testing.assert_array_equal(node_suspected, ns_o)
+        assert_tables_equal(g, o, f"scripted type {int(btype)}")
+
+    seen = run_scripted(runner, gen_keys(1000), sizes, rmw)
+    missing = required_outcomes(rmw) - seen
+    assert not missing, f"not produced: {sorted(missing, key=str)}"

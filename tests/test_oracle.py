@@ -100,3 +100,23 @@ def test_big_object_val_len_quirks():
     kv.batch(L.BatchType.local_ops, ops, L.membership(3, 0))
     assert (ops["state"] == int(L.Resp.GET_COMPLETE)).all()
     assert (ops["val_len"] == 244).all()
+
+
+@pytest.mark.parametrize("rmw,big", [(False, False), (True, False), (True, True)])
+def test_scripted_rare_outcomes_oracle(rmw, big):
+    """tests/scripted.py on the oracle alone: every branch outcome it expects (written out from
+    hermesKV.c) happens, and together they cover every code the batch function can emit."""
+    from tests.scripted import required_outcomes, run_scripted
+    sz = L.BIG if big else L.DEFAULT
+    kv = O.OracleKVS(1 << 12, 1 << 22, machine_id=0, rmw=rmw, big_objects=big, extra_cache_lines=4 if big else 0)
+    kv.populate(1000, sz.kvs_value)
+
+    def runner(btype, elems, mb, rw=None, node_suspected=None):
+        if node_suspected is not None:
+            node_suspected[0] = kv.batch(btype, elems, mb, rw=rw)
+        else:
+            kv.batch(btype, elems, mb, rw=rw)
+
+    seen = run_scripted(runner, O.gen_keys(1000), sz, rmw)
+    missing = required_outcomes(rmw) - seen
+    assert not missing, f"not produced: {sorted(missing, key=str)}"

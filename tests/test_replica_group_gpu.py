@@ -43,8 +43,12 @@ def _key_images(g, o, keys):
     return rows
 
 
-@pytest.mark.parametrize("n_rep,workers,write_pm,rounds", [(2, 24, 300, 4), (3, 16, 400, 4), (4, 8, 500, 3)])
+@pytest.mark.parametrize("n_rep,workers,write_pm,rounds", [(2, 24, 300, 4), (3, 16, 400, 4), (4, 8, 500, 3),
+                                                           (8, 16, 200, 3)])
 def test_loopback_group_parity_and_convergence(n_rep, workers, write_pm, rounds):
+    """(8, 16, 200, 3) is BASELINE configs[3]'s group on one GPU: 8 replicas (the width of the
+    membership vectors), 20 % writes, Zipf 0.99 -- every phase, kernel and slab layout of the RCCL
+    run, with every launch of every replica mirrored into its oracle twin."""
     from hermes_amd.kvs import HermesKV
     from hermes_amd.replica_group import LoopbackGroup, ReplicaRound
     from hermes_amd.workload import zipf_params
@@ -201,3 +205,40 @@ def test_dist_group_driver_one_gpu(world, drop):
             assert b[0] == L.State.VALID or (b[0] == L.State.INVALID and b[1] == drop), f"key #{i} {b[:3]}"
         for rank, imgs, *_ in live[1:]:
             assert imgs[i] == b, f"key #{i} differs between rank {live[0][0]} and rank {rank}"
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("world,config", [(2, "cfg2"), (3, "cfg5")])
+def test_bench_multi_rank_over_gloo(world, config):
+    """bench.py's N > 1 branch end to end (what the driver runs on 8 GPUs over RCCL): torchrun with
+    `world` ranks sharing this GPU over gloo, small tables. cfg5 drops the last rank in the middle
+    of the timed steps. The JSON line must report every rank's committed ops, no consistency flags,
+    and (cfg5) the shrunken membership."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", str(world), "--steps", "4", "--warmup", "1", "--keys", "30000", "--workers", "48",
+           "--config", config, "--dist-backend", "gloo", "--cpu-seconds", "0", "--host-api-seconds", "0"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == world and d["value"] > 0 and d["detail"]["error_flags"] == 0, d
+    assert d["config"]["parallelism"] == f"replicas{world}"
+    assert d["roofline"]["launches"]["invs"]["elements"] > 0
+    if config == "cfg5":
+        g = d["detail"]["membership"]["g_membership_after"]
+        assert g == ((1 << world) - 1) & ~(1 << (world - 1)), d["detail"]["membership"]

@@ -44,6 +44,17 @@ def test_bench_round_mirrored(theta, workers, cfg3):
     st = r.stats()
     assert st["committed"] > 0 and st["writes_completed"] > 0, st
     assert g.take_error_flags() == 0
+    # the virtual peers write with the keys' live timestamps: some of their INVs beat local writes
+    # in flight on the cid tie-break (WRITE -> INVALID_WRITE / INVALID), and the ACK completes them
+    assert m.codes[(int(L.BatchType.invs), "out8", int(L.Resp.INV_SUCCESS))] > 0
+    if cfg3:
+        # configs[2]'s conflicts: peers INV-abort local RMWs their own write beats (received in the
+        # ACK batch), the local replica INV-aborts peer RMWs below its key's timestamp, and the
+        # aborted RMWs end as RMW_ABORT in the next local batch (hermesKV.c:372-394)
+        assert m.codes[(int(L.BatchType.acks), "in8", int(L.Resp.OP_INV_ABORT))] > 0, m.codes
+        assert m.codes[(int(L.BatchType.invs), "out8", int(L.Resp.OP_INV_ABORT))] > 0, m.codes
+        assert m.codes[(int(L.BatchType.local_ops), "out9", int(L.Resp.RMW_ABORT))] > 0, m.codes
+        assert st["rmw_aborts"] > 0, st
 
 
 class _DeviceBytes:
@@ -124,7 +135,7 @@ def _refill_ref(ops, W, S, osz, st_value, shift, tkey, top, tlen, cursor, mid, f
     completed ops (every op with refill_all / first) take the next trace entries in op order."""
     ops = ops.copy().reshape(W, S, osz)
     cursor = cursor.copy()
-    cnt = np.zeros(4, dtype=np.int64)
+    cnt = np.zeros(5, dtype=np.int64)
     done_states = (130, 128, 138, 137, 119, 121)
     for w in range(W):
         rank = 0
@@ -138,6 +149,7 @@ def _refill_ref(ops, W, S, osz, st_value, shift, tkey, top, tlen, cursor, mid, f
                 cnt[1] += st == 130
                 cnt[2] += st == 128
             cnt[3] += drop
+            cnt[4] += (not first) and st == 138
             if not (first or complete or drop):
                 continue
             t = w * tlen + (int(cursor[w]) + rank) % tlen
@@ -184,7 +196,7 @@ def test_refill_kernel_matches_numpy(big, refill_all):
         bad = np.nonzero(got != exp_ops)[0]
         pytest.fail(f"slab differs at {len(bad)} bytes: ops {np.unique(bad // osz)[:8]}, offsets {np.unique(bad % osz)[:16]}")
     assert np.array_equal(d_cur.cpu().numpy(), exp_cur)
-    assert d_cnt[:4].cpu().tolist() == exp_cnt.tolist()
+    assert d_cnt[:5].cpu().tolist() == exp_cnt.tolist()
 
 
 @pytest.mark.parametrize("big", [False, True])

@@ -473,10 +473,8 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
 }
 
 // INV direct path: opcodes of the elements at or above ts_0, A marks itself, the other elements
-// with ts M (or, without a raise, all of them) set Y. Launched twice, the last kLookupHead
-// elements first: they set Y (and the has-B bit) of every hot key near its final value, so the
-// bulk launch's candidates read a larger Y and issue no atomic (atomics on one address serialise,
-// and some 10^5 elements run at once).
+// with ts M (or, without a raise, all of them) set Y. The load before each atomicMax filters the
+// offers of a key with many INVs (Y only rises).
 __global__ __launch_bounds__(256) void k_inv_resolve(BatchArgs a, int64_t i_begin, int64_t i_end)
 {
     const int64_t i = i_begin + (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1185,7 +1183,11 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
         hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, n);
         return hipGetLastError() == hipSuccess ? 0 : -3;
     }
-    const int64_t head = n < kLookupHead ? n : kLookupHead;
+    // The head split pays off where one launch piles many candidates onto a few keys: local
+    // batches under Zipf. A replica's INVs and ACKs carry at most one write per key and peer per
+    // round, so those launches take one pass (their launch-sized head took ~9 us at cfg2).
+    const bool split = bl.type == kLocal || bl.type == kLocalAfterMemb;
+    const int64_t head = split && n > kLookupHead ? kLookupHead : n;
     hipLaunchKernelGGL(k_lookup, dim3((unsigned)((head + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, head);
     if (n > head)
         hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n - head + kPer - 1) / kPer)), dim3(256), 0, s, a, head, n);
@@ -1193,9 +1195,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
         hipLaunchKernelGGL(k_ack_resolve, dim3(grid), dim3(256), 0, s, a);
         hipLaunchKernelGGL(k_ack_clear, dim3(grid), dim3(256), 0, s, a);
     } else if (a.inv_direct) {
-        const int64_t tail = n > kLookupHead ? n - kLookupHead : 0;
-        hipLaunchKernelGGL(k_inv_resolve, dim3((unsigned)((n - tail + 255) / 256)), dim3(256), 0, s, a, tail, n);
-        if (tail > 0) hipLaunchKernelGGL(k_inv_resolve, dim3((unsigned)((tail + 255) / 256)), dim3(256), 0, s, a, (int64_t)0, tail);
+        hipLaunchKernelGGL(k_inv_resolve, dim3(grid), dim3(256), 0, s, a, (int64_t)0, n);
         if (bl.g.st_value == 31) hipLaunchKernelGGL((k_inv_commit<31>), dim3(grid), dim3(256), 0, s, a);
         else if (bl.g.st_value == 287) hipLaunchKernelGGL((k_inv_commit<287>), dim3(grid), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((k_inv_commit<0>), dim3(grid), dim3(256), 0, s, a);

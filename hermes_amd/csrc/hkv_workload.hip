@@ -712,34 +712,70 @@ __device__ __forceinline__ uint64_t find_entry(const TableView &t, uint64_t key)
 __device__ __forceinline__ uint32_t peer_round_tag(uint32_t round) { return (round + 1u) & 0x7FFFFFu; }
 
 // per round: every live peer INV (and its VAL) takes its key's current timestamp + the write's
-// step, cid = the peer; peer_ts (RMW builds) records the peer's write per [entry][peer id]
-__global__ void k_peer_ts(TableView t, uint8_t *invs, uint8_t *vals, const int32_t *counts, int32_t stride,
-                          uint32_t op_size, unsigned long long *peer_ts, uint32_t round, int64_t total)
+// step, cid = the peer; peer_ts (RMW builds) records the peer's write per [entry][peer id].
+// Four lanes per INV, as in the batch lookup (hkv_batch.hip k_lookup): each lane reads 16 B of
+// the bucket, so one load instruction covers the 64-B bucket line, then lanes 0 and 1 read the
+// entry's key and timestamp.
+struct __attribute__((aligned(8))) U64x2w {
+    uint64_t a, b;
+};
+__global__ __launch_bounds__(256) void k_peer_ts(TableView t, uint8_t *invs, uint8_t *vals, const int32_t *counts,
+                                                 int32_t stride, uint32_t op_size, unsigned long long *peer_ts,
+                                                 uint32_t round, int64_t total)
 {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= total) return;
-    const int32_t w = (int32_t)(g / stride);
-    if ((int32_t)(g - (int64_t)w * stride) >= counts[w]) return;
+    const int q = threadIdx.x & 3;
+    const int gbase = (threadIdx.x & 63) & ~3;
+    const int64_t g = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 2;
+    int live = 0;
+    uint64_t key = 0, flags = 0;
+    if (g < total && q == 0) {
+        const int32_t w = (int32_t)(g / stride);
+        if ((int32_t)(g - (int64_t)w * stride) < counts[w]) {
+            live = 1;
+            const uint8_t *x = invs + g * op_size;
+            key = *reinterpret_cast<const uint64_t *>(x);
+            flags = *reinterpret_cast<const uint64_t *>(x + 8) >> 8 & 0xFFu;   // byte 9: the peer
+            flags |= (uint64_t)(x[16] & 1u) << 8;                               // RMW_flag
+        }
+    }
+    live = __shfl(live, 0, 4);
+    key = __shfl(key, 0, 4);
+    const uint4 v = live ? reinterpret_cast<const uint4 *>(t.index + ((key & 0xFFFFFFFFFFFFULL) & t.g.bkt_mask) * 64u)[q]
+                         : make_uint4(0u, 0u, 0u, 0u);
+    const uint64_t s0 = (uint64_t)v.x | ((uint64_t)v.y << 32), s1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    const uint32_t tag = (uint32_t)(key >> 48);
+    const bool mt0 = live && (s0 & 1u) && ((uint32_t)(s0 >> 1) & 0x7FFFFFu) == tag;
+    const bool mt1 = live && (s1 & 1u) && ((uint32_t)(s1 >> 1) & 0x7FFFFFu) == tag;
+    const uint32_t g0 = (uint32_t)(__ballot(mt0) >> gbase) & 0xFu, g1 = (uint32_t)(__ballot(mt1) >> gbase) & 0xFu;
+    uint32_t o = 0;  // bit 2*l + j: slot 2*l + j matches (the reference's slot order)
+#pragma unroll
+    for (int l = 0; l < 4; ++l) o |= ((g0 >> l) & 1u) << (2 * l) | ((g1 >> l) & 1u) << (2 * l + 1);
+    const int first = o ? __ffs(o) - 1 : 0;
+    const uint64_t off = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
+    const bool ok = live && o && t.g.log_head - off < t.g.log_cap;
+    const uint64_t phys = off & t.g.log_mask;
+    // lane 0: entry bytes 0..15 (key at 8), lane 1: bytes 16..31 (version at 24)
+    const U64x2w ln = ok && q < 2 ? reinterpret_cast<const U64x2w *>(t.log + phys)[q] : U64x2w{0, 0};
+    const uint64_t ekey = __shfl(ln.b, 0, 4);
+    const uint32_t cur = (uint32_t)__shfl(ln.b, 1, 4);
+    if (q != 0 || !live) return;
     uint8_t *x = invs + g * op_size;
-    const uint64_t key = *reinterpret_cast<const uint64_t *>(x);
-    const uint64_t phys = find_entry(t, key);
-    const uint8_t peer = x[9];
+    const uint8_t peer = (uint8_t)flags;
+    const bool rmw = (flags >> 8) & 1u;
     uint32_t ver = 2;
-    if (phys != ~0ull) {
-        const uint8_t *e = t.log + phys;
-        const uint32_t step = (!t.g.rmw_enabled || (x[16] & 1u)) ? 2u : 4u;
-        ver = *reinterpret_cast<const uint32_t *>(e + kEntryMetaOff + 6) + step;
+    if (ok && ekey == key) {
+        ver = cur + ((!t.g.rmw_enabled || rmw) ? 2u : 4u);
         if (peer_ts && peer < 8)
             atomicMax(peer_ts + (phys / t.g.entry_unit) * 8 + peer,
-                      ((unsigned long long)peer_round_tag(round) << 41) | ((unsigned long long)(x[16] & 1u) << 40) |
+                      ((unsigned long long)peer_round_tag(round) << 41) | ((unsigned long long)rmw << 40) |
                           ((unsigned long long)ver << 8) | peer);
     }
     // a fresh message each round: the batches of a previous use of the slab rewrote the opcodes
     x[8] = kOpInv;
     *reinterpret_cast<uint32_t *>(x + 12) = ver;
-    uint8_t *v = vals + g * kOpMetaSize;
-    v[8] = kOpVal;
-    *reinterpret_cast<uint32_t *>(v + 12) = ver;
+    uint8_t *vv = vals + g * kOpMetaSize;
+    vv[8] = kOpVal;
+    *reinterpret_cast<uint32_t *>(vv + 12) = ver;
 }
 
 // The virtual peers' answers to this round's INVs: an ACK (ack_copy_and_modify_elem,
@@ -919,8 +955,8 @@ int hkv_wl_peer_ts(hkv_table *t, uint8_t *invs, uint8_t *vals, const int32_t *co
     TableView tv;
     if (table_view(t, &tv) || n_workers <= 0 || stride <= 0 || op_size % 8) return -1;
     const int64_t total = (int64_t)n_workers * stride;
-    hipLaunchKernelGGL(k_peer_ts, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, tv, invs, vals, counts,
-                       stride, op_size, peer_ts, round, total);
+    hipLaunchKernelGGL(k_peer_ts, dim3(blocks_for(4 * total)), dim3(256), 0, (hipStream_t)stream, tv, invs, vals,
+                       counts, stride, op_size, peer_ts, round, total);
     return ok();
 }
 

@@ -50,7 +50,10 @@ def parse():
     p.add_argument("--rmw-permille", type=int, default=None,
                    help="RMWs among the writes, permille (default 0 (cfg2), 500 (cfg3))")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample length (0 = skip)")
-    p.add_argument("--cpu-workers", type=int, default=64)
+    p.add_argument("--cpu-workers", type=int, default=0,
+                   help="CPU baseline 250-op buffers (0 = one per thread, as the reference's workers)")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="CPU baseline worker threads (0 = one per usable core, at most 16)")
     p.add_argument("--seed", type=int, default=0x5EED)
     p.add_argument("--host-api-seconds", type=float, default=1.0,
                    help="time the host-pointer entry point for this long (0 = skip; N=1 only)")
@@ -146,7 +149,7 @@ def main():
         # CPU baseline first, on the freshly populated table image (copied out of HBM)
         from oracle.cpu_baseline import run_cpu_baseline
         cpu = run_cpu_baseline(kvs, z, a.write_permille, a.cpu_workers, a.cpu_seconds, a.seed,
-                               refill_all=not a.retry)
+                               refill_all=not a.retry, threads=a.cpu_threads)
 
     if world > 1:
         from hermes_amd.replica_group import ReplicaGroupRound

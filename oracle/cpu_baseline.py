@@ -1,13 +1,14 @@
 """bench.py's cpu_baseline leg -- TEST INFRASTRUCTURE ONLY.
 
 Times the oracle (the CPU restatement of the reference batch path, hkv_oracle.c) on the GPU
-host's own cores, single-threaded, on a bounded sample of the same workload (see
-hkv_oracle_bench.c). The table image is copied out of HBM so the CPU starts from the same
+host's own cores -- one worker thread per core over one shared table, as the reference runs --
+on a bounded sample of the same workload (see hkv_oracle_bench.c). The table image is copied out of HBM so the CPU starts from the same
 state the device produced (the two populates are bit-identical, tests/test_gpu_parity.py).
 """
 from __future__ import annotations
 
 import ctypes
+import os
 
 from .oracle import Config, build, lib
 
@@ -17,14 +18,28 @@ class HkoZipf(ctypes.Structure):
                 ("eta", ctypes.c_double), ("half_pow", ctypes.c_double), ("n", ctypes.c_uint64)]
 
 
+def host_threads(cap: int = 16) -> int:
+    """Cores this process may use: its affinity set, capped by OMP_NUM_THREADS (16 on the GPU
+    box, which shows the whole machine's CPUs) and `cap`."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp > 0:
+        n = min(n, omp)
+    return max(1, min(n, cap))
+
+
 def run_cpu_baseline(kvs, zipf, write_permille: int, workers: int, seconds: float, seed: int,
-                     n_peers: int = 2, per_peer: int = 50, refill_all: bool = True) -> dict:
+                     n_peers: int = 2, per_peer: int = 50, refill_all: bool = True, threads: int = 0) -> dict:
+    """threads = 0: one per usable core (host_threads()); workers = 0: one 250-op buffer per thread,
+    as the reference's workers (main.c:193-210)."""
     build()
     L = lib()
+    threads = threads or host_threads()
+    workers = workers or threads
     L.hko_bench_rounds.restype = ctypes.c_int64
-    L.hko_bench_rounds.argtypes = [ctypes.c_void_p, ctypes.POINTER(Config), ctypes.c_int, ctypes.c_double,
-                                   ctypes.POINTER(HkoZipf), ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
-                                   ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
+    L.hko_bench_rounds.argtypes = [ctypes.c_void_p, ctypes.POINTER(Config), ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_double, ctypes.POINTER(HkoZipf), ctypes.c_uint32, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
                                    ctypes.POINTER(ctypes.c_double)]
     L.hko_set_log_head.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
     c = kvs.cfg
@@ -41,13 +56,14 @@ def run_cpu_baseline(kvs, zipf, write_permille: int, workers: int, seconds: floa
         L.hko_set_log_head(h, kvs.log_head)
         hz = HkoZipf(zipf.theta, zipf.zetan, zipf.alpha, zipf.eta, zipf.half_pow, zipf.n)
         rounds, secs = ctypes.c_int64(0), ctypes.c_double(0.0)
-        committed = L.hko_bench_rounds(h, ctypes.byref(cfg), workers, seconds, ctypes.byref(hz), write_permille,
-                                       n_peers, per_peer, seed, int(refill_all), ctypes.byref(rounds),
+        committed = L.hko_bench_rounds(h, ctypes.byref(cfg), workers, threads, seconds, ctypes.byref(hz),
+                                       write_permille, n_peers, per_peer, seed, int(refill_all), ctypes.byref(rounds),
                                        ctypes.byref(secs))
     finally:
         L.hko_destroy(h)
-    return {"value": committed / secs.value, "unit": "ops/s", "cores": 1, "kind": "port",
-            "sample": (f"{rounds.value} rounds x {workers} workers x 250-op {'fresh' if refill_all else 'refilled'} "
-                       f"local batches (+{n_peers} virtual "
-                       f"peers x {per_peer} INV/VAL per worker-round, 2 ACKs per write) in {secs.value:.1f} s, "
-                       f"same table ({c.num_bkts} buckets) and Zipf/write mix as the GPU run")}
+    return {"value": committed / secs.value, "unit": "ops/s", "cores": threads, "kind": "port",
+            "sample": (f"{threads} worker threads sharing one table (per-key seqlocks, concur_ctrl.h:144-224), "
+                       f"{workers} x 250-op {'fresh' if refill_all else 'refilled'} local batches per round, "
+                       f">= {rounds.value} rounds each in {secs.value:.1f} s; +{n_peers} virtual peers (one write per "
+                       f"key and round each, live timestamps, up to {per_peer} per worker-round), 2 ACKs per write; "
+                       f"same table ({c.num_bkts} buckets, copied from HBM) and Zipf/write mix as the GPU run")}

@@ -170,29 +170,74 @@ void hko_gen_keys(uint64_t *out_second, int64_t n) /* mica.c:149-165 (only .seco
     }
 }
 
-/* ---------------------------------------------------------------- seqlock (concur_ctrl.h:144-213) */
+/* ---------------------------------------------------------------- seqlock (concur_ctrl.h:144-213)
+ * With the reference's CAS and ordering, so that worker threads can share one table as the
+ * reference's workers do (main.c:193-210; the multi-core CPU baseline, hkv_oracle_bench.c). One
+ * thread runs exactly the sequential semantics: the CAS always succeeds and every lock-free
+ * snapshot validates on its first pass. The version word sits at entry byte 24 (4-aligned). */
+static inline void cpu_relax(void)
+{
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#endif
+}
+static inline uint32_t ver_load(const uint8_t *m) { return __atomic_load_n((const uint32_t *)(m + 6), __ATOMIC_ACQUIRE); }
+static inline void ver_store(uint8_t *m, uint32_t v) { __atomic_store_n((uint32_t *)(m + 6), v, __ATOMIC_RELEASE); }
+static inline void lock_release(uint8_t *m) { __atomic_store_n(m + 4, (uint8_t)0, __ATOMIC_RELEASE); }
+
 static void cc_lock(uint8_t *m)
 {
-    M_LOCK(m) = 1;
-    M_SET_TSVER(m, M_TSVER(m) + 1);
+    for (;;) {
+        while (__atomic_load_n(m + 4, __ATOMIC_RELAXED) == 1) cpu_relax();
+        uint8_t expect = 0;
+        if (__atomic_compare_exchange_n(m + 4, &expect, (uint8_t)1, 0, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED)) break;
+    }
+    ver_store(m, M_TSVER(m) + 1);   /* odd while locked: lock-free readers retry */
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
 }
 static void cc_unlock_dec(uint8_t *m)
 {
-    M_SET_TSVER(m, M_TSVER(m) - 1);
-    M_LOCK(m) = 0;
+    ver_store(m, M_TSVER(m) - 1);
+    lock_release(m);
 }
 static void cc_unlock_custom(uint8_t *m, uint8_t cid, uint32_t version)
 {
-    M_TSCID(m) = cid;
-    M_SET_TSVER(m, version);
-    M_LOCK(m) = 0;
+    __atomic_store_n(m + 5, cid, __ATOMIC_RELAXED);
+    ver_store(m, version);
+    lock_release(m);
 }
 static uint32_t cc_unlock_inc(uint8_t *m, uint8_t cid, uint32_t by)
 {
-    M_TSCID(m) = cid;
-    M_SET_TSVER(m, M_TSVER(m) + by);
-    M_LOCK(m) = 0;
-    return M_TSVER(m);
+    __atomic_store_n(m + 5, cid, __ATOMIC_RELAXED);
+    const uint32_t v = M_TSVER(m) + by;
+    ver_store(m, v);
+    lock_release(m);
+    return v;
+}
+
+/* byte copy of bytes another thread may be writing (validated by the version afterwards) */
+static inline void racy_copy(uint8_t *dst, const uint8_t *src, size_t n)
+{
+    const volatile uint8_t *s = src;
+    for (size_t i = 0; i < n; i++) dst[i] = s[i];
+}
+
+/* cctrl_timestamp_is_same_and_valid (concur_ctrl.h:217-224) of a snapshot against the live meta */
+static inline int snap_valid(const uint8_t *snap, const uint8_t *m)
+{
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    const uint32_t v = M_TSVER(snap);
+    return (v & 1u) == 0 && v == ver_load(m) && snap[5] == __atomic_load_n(m + 5, __ATOMIC_RELAXED);
+}
+
+/* hermes_lock_free_read_obj_meta, hermesKV.c:81-96 */
+static void snapshot(uint8_t *snap, const uint8_t *m)
+{
+    for (;;) {
+        racy_copy(snap, m, OBJ_META_SIZE);
+        if (snap_valid(snap, m)) return;
+        cpu_relax();
+    }
 }
 
 static int ts_less(uint32_t v1, uint8_t c1, uint32_t v2, uint8_t c2) /* concur_ctrl.h:70-75 */
@@ -270,31 +315,38 @@ static void membership_check_replay(hko_kvs *kv, uint8_t *op, uint8_t idx, uint8
 /* hermes_read_actions, hermesKV.c:240-246 */
 static void read_into_op(hko_kvs *kv, uint8_t *op, uint8_t *entry)
 {
-    memcpy(O_VALUE(op), entry + ENTRY_META_OFF + OBJ_META_SIZE, kv->st_value);
+    racy_copy(O_VALUE(op), entry + ENTRY_META_OFF + OBJ_META_SIZE, kv->st_value);
     O_STATE(op) = R_GET_COMPLETE;
     O_VALLEN(op) = get_val_len(kv, entry);
 }
 
 /* ---------------------------------------------------------------- exec functions */
-/* hermes_exec_read, hermesKV.c:251-311 */
+/* hermes_exec_read, hermesKV.c:251-311: a lock-free pass (copy the meta, act on the live state,
+ * validate the copy's timestamp afterwards), or a locked one for INVALID keys */
 static void ex_read(hko_kvs *kv, uint8_t *op, uint8_t *entry, uint8_t idx, const uint8_t *mb)
 {
     uint8_t *m = entry + ENTRY_META_OFF;
+    uint8_t prev[OBJ_META_SIZE];
+    int locked = 0;
     O_STATE(op) = B_EMPTY;
-    switch (M_STATE(m)) {
-    case S_VALID: read_into_op(kv, op, entry); break;
-    case S_INVALID_WRITE: case S_WRITE: case S_REPLAY: O_STATE(op) = R_GET_STALL; break;
-    default:
-        cc_lock(m);
-        switch (M_STATE(m)) {
+    do {
+        racy_copy(prev, m, OBJ_META_SIZE);
+        switch (__atomic_load_n(m, __ATOMIC_ACQUIRE)) {
         case S_VALID: read_into_op(kv, op, entry); break;
         case S_INVALID_WRITE: case S_WRITE: case S_REPLAY: O_STATE(op) = R_GET_STALL; break;
-        case S_INVALID: membership_check_replay(kv, op, idx, m, mb); break;
-        default: break;
+        default:
+            locked = 1;
+            cc_lock(m);
+            switch (M_STATE(m)) {
+            case S_VALID: read_into_op(kv, op, entry); break;
+            case S_INVALID_WRITE: case S_WRITE: case S_REPLAY: O_STATE(op) = R_GET_STALL; break;
+            case S_INVALID: membership_check_replay(kv, op, idx, m, mb); break;
+            default: break;
+            }
+            cc_unlock_dec(m);
+            break;
         }
-        cc_unlock_dec(m);
-        break;
-    }
+    } while (!snap_valid(prev, m) && !locked);
 }
 
 /* hermes_exec_write, hermesKV.c:314-356 (write coalescing disabled, config.h:80) */
@@ -322,7 +374,7 @@ static void ex_rmw(hko_kvs *kv, uint8_t *op, uint8_t *entry, uint8_t idx, const 
     uint8_t *m = entry + ENTRY_META_OFF;
     if (O_STATE(op) == B_IN_PROGRESS_RMW) {
         uint8_t snap[OBJ_META_SIZE];
-        memcpy(snap, m, OBJ_META_SIZE);
+        snapshot(snap, m);
         if (ts_less(O_TSVER(op), O_TSCID(op), M_TSVER(snap), M_TSCID(snap))) {
             O_STATE(op) = R_RMW_ABORT;
             cc_lock(m);
@@ -355,7 +407,9 @@ static void ex_update_completion(hko_kvs *kv, uint8_t *op, uint8_t *entry, const
 {
     (void)kv;
     uint8_t *m = entry + ENTRY_META_OFF;
-    if (!memb_is_last_ack(M_ACKBV(m), mb)) return;
+    uint8_t snap[OBJ_META_SIZE];
+    snapshot(snap, m);
+    if (!memb_is_last_ack(M_ACKBV(snap), mb)) return;
     cc_lock(m);
     if (memb_is_last_ack(M_ACKBV(m), mb)) {
         M_OBI(m) = OBI_EMPTY;
@@ -388,7 +442,9 @@ static void ex_inv(hko_kvs *kv, uint8_t *inv, uint8_t *entry)
     const int rmw_on = kv->cfg.rmw_enabled != 0;
     uint32_t iv = O_TSVER(inv);
     uint8_t ic = O_TSCID(inv);
-    if (!ts_less(iv, ic, M_TSVER(m), M_TSCID(m)) || (rmw_on && O_RMW(inv) == 1)) {
+    uint8_t snap[OBJ_META_SIZE];
+    snapshot(snap, m);
+    if (!ts_less(iv, ic, M_TSVER(snap), M_TSCID(snap)) || (rmw_on && O_RMW(inv) == 1)) {
         cc_lock(m);
         if (ts_less(M_TSVER(m) - 1, M_TSCID(m), iv, ic)) {
             switch (M_STATE(m)) {
@@ -429,7 +485,9 @@ static void ex_ack(hko_kvs *kv, uint8_t *ack, uint8_t *entry, const uint8_t *mb,
     int done_idx = OBI_EMPTY;
     uint32_t av = O_TSVER(ack);
     uint8_t ac = O_TSCID(ack);
-    if (ts_equal(av, ac, M_LLWVER(m), M_LLWCID(m))) {
+    uint8_t snap[OBJ_META_SIZE];
+    snapshot(snap, m);
+    if (ts_equal(av, ac, M_LLWVER(snap), M_LLWCID(snap))) {
         cc_lock(m);
         if (M_OBI(m) != OBI_EMPTY && ts_equal(av, ac, M_LLWVER(m), M_LLWCID(m))) {
             uint8_t sender = O_STATE(ack);
@@ -474,7 +532,9 @@ static void ex_ack(hko_kvs *kv, uint8_t *ack, uint8_t *entry, const uint8_t *mb,
 static void ex_val(uint8_t *val, uint8_t *entry)
 {
     uint8_t *m = entry + ENTRY_META_OFF;
-    if (ts_equal(M_TSVER(m), M_TSCID(m), O_TSVER(val), O_TSCID(val))) {
+    uint8_t snap[OBJ_META_SIZE];
+    snapshot(snap, m);
+    if (ts_equal(M_TSVER(snap), M_TSCID(snap), O_TSVER(val), O_TSCID(val))) {
         cc_lock(m);
         if (ts_equal(M_TSVER(m) - 1, M_TSCID(m), O_TSVER(val), O_TSCID(val))) M_STATE(m) = S_VALID;
         cc_unlock_dec(m);
@@ -689,9 +749,10 @@ void hko_set_log_head(hko_kvs *kv, uint64_t head) { kv->log_head = head; }
  * 2 inc_by_three, 3 custom. Returns the version an inc variant reports, else 0. */
 uint32_t hko_test_cctrl_lock_unlock(uint8_t *cc, int variant, uint8_t cid, uint32_t version)
 {
-    uint8_t m[OBJ_META_SIZE];
+    uint8_t buf[32] __attribute__((aligned(8)));
+    uint8_t *m = buf + 2;   /* the version word 4-aligned, as at entry byte 24 */
     uint32_t resp = 0;
-    memset(m, 0, sizeof m);
+    memset(buf, 0, sizeof buf);
     memcpy(m + 4, cc, 6);
     cc_lock(m);
     switch (variant) {
@@ -709,3 +770,13 @@ int hko_test_ts_equal(uint32_t v1, uint8_t c1, uint32_t v2, uint8_t c2) { return
 
 int hko_test_is_last_ack(uint8_t ack_bv, const uint8_t membership[8]) { return memb_is_last_ack(ack_bv, membership); }
 int hko_test_has_node(const uint8_t membership[8], uint8_t node) { return memb_has_node(membership, node); }
+
+/* the key's current version through a lock-free read (the CPU baseline's virtual peers) */
+uint32_t hko_key_version(hko_kvs *kv, uint64_t key)
+{
+    uint8_t *e = hko_lookup(kv, key);
+    if (!e) return 0;
+    uint8_t snap[OBJ_META_SIZE];
+    snapshot(snap, e + ENTRY_META_OFF);
+    return M_TSVER(snap);
+}

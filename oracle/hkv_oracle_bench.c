@@ -1,8 +1,9 @@
 /*
  * hkv_oracle_bench.c -- TEST INFRASTRUCTURE ONLY: bench.py's cpu_baseline leg.
  *
- * Times the CPU restatement (hkv_oracle.c) on the same workload shape as the GPU step: each
- * virtual worker runs the reference worker loop (hermes_worker.c:438-546) on one core:
+ * Times the CPU restatement (hkv_oracle.c) on the same workload shape as the GPU step, one worker
+ * thread per core over one shared table as the reference runs (main.c:193-210): each thread runs
+ * the reference worker loop (hermes_worker.c:438-546) over its workers' 250-op buffers:
  * refill (inline-util.h:149-303) -> local batch -> INV marshal (hermes_worker.c:12-65) ->
  * ACKs from the virtual peers -> incoming INV batch -> ACK batch (rw = the worker's ops) ->
  * VAL marshal -> incoming VAL batch. Traces and peer INV/VAL slabs are generated before the
@@ -11,6 +12,7 @@
  * stalled ops in their slots as refill_ops does.
  */
 #include <math.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -57,28 +59,155 @@ static double now_s(void)
 }
 
 void hko_set_log_head(hko_kvs *kv, uint64_t head);
+uint32_t hko_key_version(hko_kvs *kv, uint64_t key);
 
-/* returns committed ops; rounds and seconds through out-params */
-int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, double seconds, const hko_zipf *z,
-                         uint32_t write_pm, int n_peers, int per_peer, uint64_t seed, int refill_all, int64_t *out_rounds,
-                         double *out_secs)
+enum { BS = 250, BT = 8192, BP = 16 };   /* local batch, trace length, peer round indices */
+
+typedef struct {
+    hko_kvs *kv;
+    uint32_t osz, sv;
+    int n_peers, per_peer, rstride, refill_all;
+    uint8_t mid;
+    uint8_t *ops;
+    const uint64_t *tkey;
+    const uint8_t *top;
+    uint32_t *cursor;
+    const uint8_t *rinv_pool, *rval_pool;
+    const int32_t *rcount;
+    int n_workers, w0, w1;
+    double seconds;
+    pthread_barrier_t *start;
+    double *t0;
+    int64_t committed, rounds;
+    double t_end;
+} bench_thread;
+
+/* One worker thread of the reference (hermes_worker.c:438-546) per core, each over its own
+ * workers' 250-op buffers; all threads share the table (concurrency control: hkv_oracle.c's
+ * seqlock, concur_ctrl.h:144-224). */
+static void *bench_worker(void *arg)
 {
-    const int S = 250, T = 8192, P = 16;
-    const uint32_t osz = hko_op_size(cfg), sv = hko_st_value_size(cfg);
-    const int rstride = n_peers * per_peer;
-    uint8_t *ops = calloc((size_t)n_workers * S, osz);
+    bench_thread *b = (bench_thread *)arg;
+    const uint32_t osz = b->osz, sv = b->sv;
+    const int n_peers = b->n_peers, rstride = b->rstride, S = BS;
     uint8_t *inv_out = calloc(S, osz);
     uint8_t *acks = calloc((size_t)S * (n_peers ? n_peers : 1), 16);
     uint8_t *ack_out = calloc(rstride ? rstride : 1, 16);
     uint8_t *val_out = calloc((size_t)S * (n_peers ? n_peers : 1), 16);
-    uint8_t *rinv_pool = calloc((size_t)n_workers * P * (rstride ? rstride : 1), osz);
-    uint8_t *rval_pool = calloc((size_t)n_workers * P * (rstride ? rstride : 1), 16);
     uint8_t *rinv = calloc(rstride ? rstride : 1, osz);
     uint8_t *rval = calloc(rstride ? rstride : 1, 16);
+    uint8_t membership[8] = {2, 0x07, 0xF9, 0, 0, 0, 0, 0};
+    const uint8_t mid = b->mid;
+    int64_t committed = 0, rounds = 0;
+    int first = 1;
+    pthread_barrier_wait(b->start);
+    const double t0 = *b->t0;
+    double t = now_s();
+    while (first || t - t0 < b->seconds) {
+        for (int w = b->w0; w < b->w1; w++) {
+            uint8_t *ow = b->ops + (size_t)w * S * osz;
+            /* refill_ops (inline-util.h:149-303) */
+            for (int i = 0; i < S; i++) {
+                uint8_t *o = ow + (size_t)i * osz;
+                uint8_t st = o[9];
+                int complete = st == 130 || st == 128 || st == 138 || st == 137 || st == 119 || st == 121;
+                /* in flight: PUT/RMW/REPLAY_SUCCESS, IN_PROGRESS_*, *_COMPLETE_SEND_VALS, membership change */
+                int in_flight = st == 122 || st == 135 || st == 123 || st == 143 || st == 148 || st == 144 ||
+                                st == 133 || st == 149 || st == 147 || st == 118;
+                if (!first && complete && st != 130 && st != 138) committed++;
+                /* stalled ops retry unless refill_all; ops in flight always keep their slot */
+                if (!(first || complete || (b->refill_all && !in_flight))) continue;
+                int64_t ti = (int64_t)w * BT + b->cursor[w];
+                b->cursor[w] = (b->cursor[w] + 1) % BT;
+                memcpy(o, &b->tkey[ti], 8);
+                o[8] = b->top[ti];
+                o[9] = 141;
+                o[10] = b->top[ti] == OPC_GET ? 0 : (uint8_t)sv;
+                o[16] = 0;
+                o[17] = 0;
+                if (b->top[ti] != OPC_GET) memset(o + 18, 'a' + mid, sv);
+            }
+            hko_batch(b->kv, 0, ow, S, (uint16_t)osz, membership, NULL, NULL);
+            /* INV marshalling (hermes_worker.c:12-65) + peers' ACKs */
+            int ninv = 0;
+            for (int i = 0; i < S; i++) {
+                uint8_t *o = ow + (size_t)i * osz;
+                if (o[9] != 122) continue;
+                uint8_t *x = inv_out + (size_t)ninv * osz;
+                memcpy(x, o, osz);
+                x[9] = mid;
+                x[8] = OPC_INV;
+                o[9] = 143;
+                for (int r = 0; r < n_peers; r++) {
+                    uint8_t *a = acks + ((size_t)ninv * n_peers + r) * 16;
+                    memcpy(a, x, 16);
+                    a[8] = OPC_ACK;
+                    a[9] = (uint8_t)(1 + r);
+                }
+                ninv++;
+            }
+            if (rstride) {
+                size_t k = (size_t)(rounds % BP) * b->n_workers + w;
+                const int rn = b->rcount[k];
+                memcpy(rinv, b->rinv_pool + k * rstride * osz, (size_t)rn * osz);
+                memcpy(rval, b->rval_pool + k * rstride * 16, (size_t)rn * 16);
+                /* the peer's write: the key's current version + 2, cid = the peer (hermesKV.c:100-141) */
+                for (int i = 0; i < rn; i++) {
+                    uint64_t key;
+                    memcpy(&key, rinv + (size_t)i * osz, 8);
+                    const uint32_t ver = hko_key_version(b->kv, key) + 2;
+                    memcpy(rinv + (size_t)i * osz + 12, &ver, 4);
+                    memcpy(rval + (size_t)i * 16 + 12, &ver, 4);
+                }
+                int ns = -1;
+                hko_batch(b->kv, 2, rinv, rn, (uint16_t)osz, membership, &ns, NULL);
+                for (int i = 0; i < rn; i++) { /* ACKs back to the peers */
+                    uint8_t *x = rinv + (size_t)i * osz, *a = ack_out + (size_t)i * 16;
+                    if (x[8] == 124) { memcpy(a, x, 16); a[8] = OPC_ACK; a[9] = mid; }
+                    x[8] = 140;
+                }
+                hko_batch(b->kv, 3, acks, ninv * n_peers, 16, membership, NULL, ow);
+                for (int i = 0; i < ninv * n_peers; i++) { /* VALs for completed writes */
+                    uint8_t *a = acks + (size_t)i * 16, *v = val_out + (size_t)i * 16;
+                    if (a[8] == 126) { memcpy(v, a, 16); v[8] = OPC_VAL; v[9] = mid; }
+                    a[8] = 140;
+                }
+                hko_batch(b->kv, 4, rval, rn, 16, membership, NULL, NULL);
+            }
+        }
+        rounds++;
+        first = 0;
+        t = now_s();
+    }
+    /* harvest the last round's completions (counted by the next refill in the reference) */
+    for (int64_t i = (int64_t)b->w0 * S; i < (int64_t)b->w1 * S; i++) {
+        uint8_t st = b->ops[i * osz + 9];
+        if (st == 128 || st == 121 || st == 137) committed++;
+    }
+    b->committed = committed;
+    b->rounds = rounds;
+    b->t_end = t;
+    free(inv_out); free(acks); free(ack_out); free(val_out); free(rinv); free(rval);
+    return NULL;
+}
+
+/* returns committed ops of all threads; rounds (per thread, the smallest) and seconds (the
+ * slowest thread's) through out-params */
+int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, int n_threads, double seconds,
+                         const hko_zipf *z, uint32_t write_pm, int n_peers, int per_peer, uint64_t seed,
+                         int refill_all, int64_t *out_rounds, double *out_secs)
+{
+    const int T = BT, P = BP;
+    const uint32_t osz = hko_op_size(cfg), sv = hko_st_value_size(cfg);
+    const int rstride = n_peers * per_peer;
+    if (n_threads < 1) n_threads = 1;
+    if (n_workers < n_threads) n_workers = n_threads;
+    uint8_t *ops = calloc((size_t)n_workers * BS, osz);
+    uint8_t *rinv_pool = calloc((size_t)n_workers * P * (rstride ? rstride : 1), osz);
+    uint8_t *rval_pool = calloc((size_t)n_workers * P * (rstride ? rstride : 1), 16);
     uint64_t *tkey = malloc(sizeof(uint64_t) * (size_t)n_workers * T);
     uint8_t *top = malloc((size_t)n_workers * T);
     uint32_t *cursor = calloc(n_workers, 4);
-    uint8_t membership[8] = {2, 0x07, 0xF9, 0, 0, 0, 0, 0};
     const uint8_t mid = (uint8_t)cfg->machine_id;
     /* traces (create_uni_trace / parse_trace shape) */
     for (int64_t g = 0; g < (int64_t)n_workers * T; g++) {
@@ -137,95 +266,35 @@ int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, doub
         }
         free(hk); free(ids); free(keep);
     }
-    int64_t committed = 0, rounds = 0;
-    int first = 1;
-    double t0 = now_s(), t = t0;
-    while (first || t - t0 < seconds) {
-        for (int w = 0; w < n_workers; w++) {
-            uint8_t *ow = ops + (size_t)w * S * osz;
-            /* refill_ops (inline-util.h:149-303) */
-            for (int i = 0; i < S; i++) {
-                uint8_t *o = ow + (size_t)i * osz;
-                uint8_t st = o[9];
-                int complete = st == 130 || st == 128 || st == 138 || st == 137 || st == 119 || st == 121;
-                /* in flight: PUT/RMW/REPLAY_SUCCESS, IN_PROGRESS_*, *_COMPLETE_SEND_VALS, membership change */
-                int in_flight = st == 122 || st == 135 || st == 123 || st == 143 || st == 148 || st == 144 ||
-                                st == 133 || st == 149 || st == 147 || st == 118;
-                if (!first && complete && st != 130 && st != 138) committed++;
-                /* stalled ops retry unless refill_all; ops in flight always keep their slot */
-                if (!(first || complete || (refill_all && !in_flight))) continue;
-                int64_t ti = (int64_t)w * T + cursor[w];
-                cursor[w] = (cursor[w] + 1) % T;
-                memcpy(o, &tkey[ti], 8);
-                o[8] = top[ti];
-                o[9] = 141;
-                o[10] = top[ti] == OPC_GET ? 0 : (uint8_t)sv;
-                o[16] = 0;
-                o[17] = 0;
-                if (top[ti] != OPC_GET) memset(o + 18, 'a' + mid, sv);
-            }
-            hko_batch(kv, 0, ow, S, (uint16_t)osz, membership, NULL, NULL);
-            /* INV marshalling (hermes_worker.c:12-65) + peers' ACKs */
-            int ninv = 0;
-            for (int i = 0; i < S; i++) {
-                uint8_t *o = ow + (size_t)i * osz;
-                if (o[9] != 122) continue;
-                uint8_t *x = inv_out + (size_t)ninv * osz;
-                memcpy(x, o, osz);
-                x[9] = mid;
-                x[8] = OPC_INV;
-                o[9] = 143;
-                for (int r = 0; r < n_peers; r++) {
-                    uint8_t *a = acks + ((size_t)ninv * n_peers + r) * 16;
-                    memcpy(a, x, 16);
-                    a[8] = OPC_ACK;
-                    a[9] = (uint8_t)(1 + r);
-                }
-                ninv++;
-            }
-            if (rstride) {
-                size_t k = (size_t)(rounds % P) * n_workers + w;
-                const int rn = rcount[k];
-                memcpy(rinv, rinv_pool + k * rstride * osz, (size_t)rn * osz);
-                memcpy(rval, rval_pool + k * rstride * 16, (size_t)rn * 16);
-                /* the peer's write: the key's current version + 2, cid = the peer (hermesKV.c:100-141) */
-                for (int i = 0; i < rn; i++) {
-                    uint64_t key;
-                    memcpy(&key, rinv + (size_t)i * osz, 8);
-                    const uint8_t *e = hko_lookup(kv, key);
-                    uint32_t ver = 2;
-                    if (e) { memcpy(&ver, e + 24, 4); ver += 2; }
-                    memcpy(rinv + (size_t)i * osz + 12, &ver, 4);
-                    memcpy(rval + (size_t)i * 16 + 12, &ver, 4);
-                }
-                int ns = -1;
-                hko_batch(kv, 2, rinv, rn, (uint16_t)osz, membership, &ns, NULL);
-                for (int i = 0; i < rn; i++) { /* ACKs back to the peers */
-                    uint8_t *x = rinv + (size_t)i * osz, *a = ack_out + (size_t)i * 16;
-                    if (x[8] == 124) { memcpy(a, x, 16); a[8] = OPC_ACK; a[9] = mid; }
-                    x[8] = 140;
-                }
-                hko_batch(kv, 3, acks, ninv * n_peers, 16, membership, NULL, ow);
-                for (int i = 0; i < ninv * n_peers; i++) { /* VALs for completed writes */
-                    uint8_t *a = acks + (size_t)i * 16, *v = val_out + (size_t)i * 16;
-                    if (a[8] == 126) { memcpy(v, a, 16); v[8] = OPC_VAL; v[9] = mid; }
-                    a[8] = 140;
-                }
-                hko_batch(kv, 4, rval, rn, 16, membership, NULL, NULL);
-            }
-        }
-        rounds++;
-        first = 0;
-        t = now_s();
+    pthread_barrier_t start;
+    pthread_barrier_init(&start, NULL, (unsigned)n_threads + 1);
+    bench_thread *th = calloc((size_t)n_threads, sizeof(bench_thread));
+    pthread_t *tid = calloc((size_t)n_threads, sizeof(pthread_t));
+    double t0 = 0;
+    for (int k = 0; k < n_threads; k++) {
+        bench_thread *b = &th[k];
+        b->kv = kv; b->osz = osz; b->sv = sv; b->n_peers = n_peers; b->per_peer = per_peer; b->rstride = rstride;
+        b->refill_all = refill_all; b->mid = mid; b->ops = ops; b->tkey = tkey; b->top = top; b->cursor = cursor;
+        b->rinv_pool = rinv_pool; b->rval_pool = rval_pool; b->rcount = rcount; b->n_workers = n_workers;
+        b->w0 = (int)((int64_t)n_workers * k / n_threads);
+        b->w1 = (int)((int64_t)n_workers * (k + 1) / n_threads);
+        b->seconds = seconds; b->start = &start; b->t0 = &t0;
+        pthread_create(&tid[k], NULL, bench_worker, b);
     }
-    /* harvest the last round's completions (counted by the next refill in the reference) */
-    for (int64_t i = 0; i < (int64_t)n_workers * S; i++) {
-        uint8_t st = ops[i * osz + 9];
-        if (st == 128 || st == 121 || st == 137) committed++;
+    t0 = now_s();
+    pthread_barrier_wait(&start);
+    int64_t committed = 0, rounds = -1;
+    double t_end = t0;
+    for (int k = 0; k < n_threads; k++) {
+        pthread_join(tid[k], NULL);
+        committed += th[k].committed;
+        if (rounds < 0 || th[k].rounds < rounds) rounds = th[k].rounds;
+        if (th[k].t_end > t_end) t_end = th[k].t_end;
     }
+    pthread_barrier_destroy(&start);
     *out_rounds = rounds;
-    *out_secs = t - t0;
-    free(ops); free(inv_out); free(acks); free(ack_out); free(val_out); free(rinv_pool); free(rval_pool);
-    free(rinv); free(rval); free(tkey); free(top); free(cursor); free(rcount);
+    *out_secs = t_end - t0;
+    free(th); free(tid);
+    free(ops); free(rinv_pool); free(rval_pool); free(tkey); free(top); free(cursor); free(rcount);
     return committed;
 }

@@ -70,36 +70,25 @@ def parse():
     return p.parse_args()
 
 
-def host_api_rate(seconds: float) -> dict:
-    """The drop-in entry point hermes_batch_ops_to_KVS on host buffers (configs[0] shape: the
-    reference's default 1M-key table, uniform keys, 5 % PUTs, 250-op local batches): every call
-    copies its batch over PCIe, runs it and copies it back. Reported beside `value`, never as it."""
-    import numpy as np
-    import torch
-    from hermes_amd import kvs as K, layout as L
-    K.spacetime_init(0)
-    g = torch.Generator(device="cpu").manual_seed(7)
-    pool = 256
-    ids = torch.randint(0, 1_000_000, (pool * 250,), generator=g, dtype=torch.int32).cuda()
-    keys = K.hash_ids(ids).cpu().numpy().view(np.uint64)
-    puts = (torch.rand(pool * 250, generator=g) < 0.05).numpy()
-    ops = np.zeros(250, dtype=L.op_dtype())
-    mb = L.membership(3, 0)
-    n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        j = (n % pool) * 250
-        ops[:] = 0
-        ops["key"] = keys[j:j + 250]
-        ops["state"] = int(L.Bucket.NEW)
-        p = puts[j:j + 250]
-        ops["opcode"] = np.where(p, int(L.Op.PUT), int(L.Op.GET))
-        ops["value"][p] = ord("x")
-        ops["val_len"][p] = L.DEFAULT.st_value
-        K.hermes_batch_ops_to_KVS(L.BatchType.local_ops, ops, 250, ops.dtype.itemsize, mb, None, None)
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": n * 250 / dt, "unit": "elements/s", "calls": n, "us_per_call": dt / n * 1e6,
-            "what": "hermes_batch_ops_to_KVS on host buffers (PCIe round trip per call), 1M keys, 5% PUT"}
+def host_api_rate(seconds: float, threads=(1, 8)) -> dict:
+    """The drop-in entry point hermes_batch_ops_to_KVS on host buffers, as the reference's worker
+    threads call it (configs[0] shape: the default 1M-key table, uniform keys, 5 % PUTs, 250-op
+    local batches, then the ACKs of each batch's writes): tools/capi_threads, a gcc-built caller,
+    with 1 and 8 threads whose batches the library combines into shared launches. Every call
+    copies its batch over PCIe and back. Reported beside `value`, never as it."""
+    import subprocess
+    tool = os.path.join(ROOT, "tools", "capi_threads")
+    out = {"unit": "local ops/s", "what": "hermes_batch_ops_to_KVS from T gcc-built worker threads (PCIe round "
+           "trip per call, concurrent callers combined), 1M keys, uniform, 5% PUT, + ACK batches"}
+    for t in threads:
+        p = subprocess.run([tool, "throughput", str(t), str(seconds), "50"], capture_output=True, text=True,
+                           timeout=120)
+        if p.returncode != 0:
+            raise RuntimeError(f"capi_threads failed: {p.stderr[-500:]}")
+        d = json.loads(p.stdout.strip().splitlines()[-1])
+        out[f"threads_{t}"] = d["local_ops_per_s"]
+    out["value"] = out[f"threads_{max(threads)}"]
+    return out
 
 
 def main():

@@ -10,7 +10,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
+#include <vector>
 #include <string>
 
 #define HKV_IMPLEMENTATION 1
@@ -18,6 +21,43 @@
 #include "hkv_internal.h"
 
 using namespace hkv;
+
+// ---- combining submit for the host-pointer entry point
+// The reference's worker threads call hermes_batch_ops_to_KVS concurrently on one table; its
+// per-key seqlocks make the result some serial order of their batches (concur_ctrl.h:144-224,
+// main.c:193-210). Here every caller queues its batch; whichever caller finds no combiner active
+// becomes one: it takes the compatible batches at the head of the queue (same type, element size
+// and membership), stages them into one of kHostSets pinned/device buffer sets, and enqueues the
+// copy in, ONE multi-batch launch (hkv_batch_async, concatenation order) and the copy out on the
+// table's stream. Each caller then waits for its set's event and copies its own results out.
+// Launches on one stream run in order, so the combined result is the serial order of the sets'
+// concatenations -- an order the reference could have produced. With several sets, the next
+// combiner stages while the GPU runs the previous launch.
+constexpr int kHostSets = 3;
+constexpr int kHostMaxBatches = 64;
+constexpr int64_t kHostMaxElems = 32768;
+
+struct HostSet {
+    uint8_t *h = nullptr;    // pinned: counts | node_suspected | ops | rw
+    uint8_t *d = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    int refs = 0;            // callers still to copy their results out
+    bool busy = false;
+};
+
+struct HostReq {
+    int type;
+    uint8_t *ops;
+    int n;
+    uint16_t esz;
+    uint64_t mb;
+    int *ns;
+    uint8_t *rw;
+    HostSet *set = nullptr;
+    size_t ops_off = 0, rw_off = 0, ns_off = 0, rw_bytes = 0;
+    bool launched = false;
+};
 
 struct hkv_table {
     hkv_config cfg;
@@ -37,13 +77,13 @@ struct hkv_table {
     unsigned int *d_error_flags = nullptr;
     int32_t *d_ns_idx = nullptr;
     int32_t ns_cap = 0;
-    // staging for the host-pointer reference API
-    uint8_t *d_stage_ops = nullptr;
-    size_t stage_ops_cap = 0;
-    uint8_t *d_stage_rw = nullptr;
-    size_t stage_rw_cap = 0;
-    int32_t *d_stage_ns = nullptr;
-    uint8_t *h_stage = nullptr;  // pinned: ops | rw | node_suspected
+    // the host-pointer reference API: concurrent callers' batches are combined into one launch
+    // (see "combining submit" below)
+    std::mutex hmu;
+    std::condition_variable hcv;
+    std::deque<HostReq *> hq;
+    bool combining = false;
+    HostSet sets[kHostSets];
     std::mutex mu;
 };
 
@@ -245,8 +285,11 @@ int hkv_table_destroy(hkv_table *t)
     hipFree(t->d_fw);
     hipFree(t->d_error_flags);
     hipFree(t->d_ns_idx);
-    hipFree(t->d_stage_ops);  // rw and node_suspected staging live in the same region
-    hipHostFree(t->h_stage);
+    for (HostSet &hs : t->sets) {
+        hipFree(hs.d);
+        hipHostFree(hs.h);
+        if (hs.ev) hipEventDestroy(hs.ev);
+    }
     if (t->stream) hipStreamDestroy(t->stream);
     delete t;
     return 0;
@@ -485,6 +528,101 @@ void spacetime_populate_fixed_len(struct spacetime_kv *, int n, int val_len)
     if (hkv_table_populate(t, n, val_len)) die("spacetime_populate_fixed_len");
 }
 
+static bool host_compatible(const HostReq *a, const HostReq *b)
+{
+    return a->type == b->type && a->esz == b->esz && a->mb == b->mb && (a->rw != nullptr) == (b->rw != nullptr) &&
+           (a->ns != nullptr) == (b->ns != nullptr);
+}
+
+// Called with t->hmu held by a caller that found no combiner active: launches the compatible
+// batches at the head of the queue as one multi-batch launch (see "combining submit" above).
+static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
+{
+    t->combining = true;
+    HostSet *set = nullptr;
+    for (;;) {
+        for (HostSet &hs : t->sets)
+            if (!hs.busy) {
+                set = &hs;
+                break;
+            }
+        if (set) break;
+        t->hcv.wait(lk);
+    }
+    std::vector<HostReq *> take;
+    int stride = 0;
+    const HostReq *head = t->hq.front();
+    for (auto it = t->hq.begin(); it != t->hq.end() && (int)take.size() < kHostMaxBatches;) {
+        HostReq *r = *it;
+        if (!host_compatible(head, r)) break;  // keep the callers' queue order
+        const int st = std::max(stride, r->n);
+        if (!take.empty() && (int64_t)st * (int64_t)(take.size() + 1) > kHostMaxElems) break;
+        stride = st;
+        take.push_back(r);
+        it = t->hq.erase(it);
+    }
+    lk.unlock();
+    const int nb = (int)take.size();
+    const HostReq *r0 = take[0];
+    const bool with_rw = r0->type == acks && r0->rw != nullptr;
+    const bool with_ns = r0->type == invs && r0->ns != nullptr;
+    const size_t rw_bytes = with_rw ? (size_t)t->cfg.rw_len * t->geo.op_size : 0;
+    const size_t ops_off = ((size_t)8 * nb + 255) & ~(size_t)255;
+    const size_t ops_bytes = (size_t)nb * stride * r0->esz;
+    const size_t rw_off = (ops_off + ops_bytes + 255) & ~(size_t)255;
+    const size_t total = rw_off + (size_t)nb * rw_bytes;
+    if (total > set->cap) {
+        hipFree(set->d);
+        hipHostFree(set->h);
+        set->d = set->h = nullptr;
+        const size_t cap = std::max(total + total / 2, (size_t)1 << 20);
+        if (hipMalloc(&set->d, cap) != hipSuccess || hipHostMalloc((void **)&set->h, cap, hipHostMallocDefault) != hipSuccess)
+            die("staging alloc");
+        set->cap = cap;
+    }
+    if (!set->ev && hipEventCreateWithFlags(&set->ev, hipEventDisableTiming) != hipSuccess) die("event");
+    int32_t *h_counts = reinterpret_cast<int32_t *>(set->h);
+    int32_t *h_ns = h_counts + nb;
+    for (int b = 0; b < nb; ++b) {
+        HostReq *r = take[b];
+        h_counts[b] = r->n;
+        h_ns[b] = with_ns ? *r->ns : -1;
+        r->ops_off = ops_off + (size_t)b * stride * r->esz;
+        r->ns_off = (size_t)4 * (nb + b);
+        r->rw_off = rw_off + (size_t)b * rw_bytes;
+        r->rw_bytes = rw_bytes;
+        memcpy(set->h + r->ops_off, r->ops, (size_t)r->n * r->esz);
+        if (with_rw) memcpy(set->h + r->rw_off, r->rw, rw_bytes);
+    }
+    hipStream_t s = t->stream;
+    if (hipMemcpyAsync(set->d, set->h, total, hipMemcpyHostToDevice, s) != hipSuccess) die("copy in");
+    hkv_batch_desc d;
+    memset(&d, 0, sizeof d);
+    d.type = r0->type;
+    d.n_batches = nb;
+    d.stride = stride;
+    d.elem_size = r0->esz;
+    d.d_elems = set->d + ops_off;
+    d.d_counts = reinterpret_cast<const int32_t *>(set->d);
+    d.d_rw = with_rw ? set->d + rw_off : nullptr;
+    d.rw_stride_bytes = (int64_t)rw_bytes;
+    d.d_node_suspected = with_ns ? reinterpret_cast<int32_t *>(set->d) + nb : nullptr;
+    memcpy(d.membership, &r0->mb, 8);
+    TRACE("combined launch type=%d batches=%d stride=%d", d.type, nb, stride);
+    if (hkv_batch_async(t, &d, s)) die("hermes_batch_ops_to_KVS");
+    if (hipMemcpyAsync(set->h, set->d, total, hipMemcpyDeviceToHost, s) != hipSuccess) die("copy out");
+    if (hipEventRecord(set->ev, s) != hipSuccess) die("event record");
+    lk.lock();
+    set->busy = true;
+    set->refs = nb;
+    for (HostReq *r : take) {
+        r->set = set;
+        r->launched = true;
+    }
+    t->combining = false;
+    t->hcv.notify_all();
+}
+
 // see the ABI note in hermeskv.h: curr_membership arrives as gcc passes the reference struct
 void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, int op_num,
                              uint16_t sizeof_op_elem, uint64_t curr_membership,
@@ -504,61 +642,36 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
         g_err = "spacetime_init was not called";
         die("hermes_batch_ops_to_KVS");
     }
-    std::lock_guard<std::mutex> lk(t->mu);
-    if (hipSetDevice(t->cfg.device) != hipSuccess) die("hipSetDevice");
-    const size_t ops_bytes = (size_t)op_num * sizeof_op_elem;
-    const bool with_rw = type == acks && read_write_ops != nullptr;
-    const size_t rw_bytes = (size_t)t->cfg.rw_len * t->geo.op_size;
-    // device buffers + pinned host mirrors (pageable async copies are avoided on purpose)
-    if (ops_bytes > t->stage_ops_cap || (with_rw && rw_bytes > t->stage_rw_cap) || !t->d_stage_ns) {
-        size_t oc = ops_bytes > t->stage_ops_cap ? ops_bytes : t->stage_ops_cap;
-        size_t rc = rw_bytes > t->stage_rw_cap ? rw_bytes : t->stage_rw_cap;
-        oc = (oc + 255) & ~(size_t)255;
-        rc = (rc + 255) & ~(size_t)255;
-        hipFree(t->d_stage_ops);
-        hipHostFree(t->h_stage);
-        t->d_stage_ops = t->d_stage_rw = nullptr;
-        t->d_stage_ns = nullptr;
-        t->h_stage = nullptr;
-        t->stage_ops_cap = t->stage_rw_cap = 0;
-        // one device region laid out like the pinned mirror (ops | rw | node_suspected), so each
-        // call moves one contiguous range each way
-        if (hipMalloc(&t->d_stage_ops, oc + rc + 64) != hipSuccess ||
-            hipHostMalloc((void **)&t->h_stage, oc + rc + 64, hipHostMallocDefault) != hipSuccess)
-            die("staging alloc");
-        t->d_stage_rw = t->d_stage_ops + oc;
-        t->d_stage_ns = reinterpret_cast<int32_t *>(t->d_stage_ops + oc + rc);
-        t->stage_ops_cap = oc;
-        t->stage_rw_cap = rc;
+    if ((int)type < 0 || (int)type > 4 || (type == local_ops && op_num > 255) || (int64_t)op_num > kHostMaxElems) {
+        g_err = "bad batch (type, or more ops than a launch holds)";
+        die("hermes_batch_ops_to_KVS");
     }
-    uint8_t *h_ops = t->h_stage, *h_rw = t->h_stage + t->stage_ops_cap;
-    int32_t *h_ns = reinterpret_cast<int32_t *>(t->h_stage + t->stage_ops_cap + t->stage_rw_cap);
-    hipStream_t s = t->stream;
-    const bool with_ns = type == invs && node_suspected != nullptr;
-    memcpy(h_ops, op_array, ops_bytes);
-    if (with_rw) memcpy(h_rw, read_write_ops, rw_bytes);
-    if (with_ns) *h_ns = *node_suspected;
-    const size_t span = with_ns ? t->stage_ops_cap + t->stage_rw_cap + 4
-                      : with_rw ? t->stage_ops_cap + rw_bytes : ops_bytes;
-    if (hipMemcpyAsync(t->d_stage_ops, h_ops, span, hipMemcpyHostToDevice, s) != hipSuccess) die("copy in");
-    hkv_batch_desc d;
-    memset(&d, 0, sizeof d);
-    d.type = (int32_t)type;
-    d.n_batches = 1;
-    d.stride = op_num;
-    d.elem_size = sizeof_op_elem;
-    d.d_elems = t->d_stage_ops;
-    d.d_rw = with_rw ? t->d_stage_rw : nullptr;
-    d.d_node_suspected = with_ns ? t->d_stage_ns : nullptr;
-    memcpy(d.membership, &curr_membership, 8);
-    TRACE("staged in; launching");
-    if (hkv_batch_async(t, &d, s)) die("hermes_batch_ops_to_KVS");
-    TRACE("launched");
-    if (hipMemcpyAsync(h_ops, t->d_stage_ops, span, hipMemcpyDeviceToHost, s) != hipSuccess) die("copy out");
-    if (hipStreamSynchronize(s) != hipSuccess) die("sync");
-    memcpy(op_array, h_ops, ops_bytes);
-    if (with_rw) memcpy(read_write_ops, h_rw, rw_bytes);
-    if (d.d_node_suspected) *node_suspected = *h_ns;
+    if (hipSetDevice(t->cfg.device) != hipSuccess) die("hipSetDevice");
+    HostReq r;
+    r.type = (int)type;
+    r.ops = op_array;
+    r.n = op_num;
+    r.esz = sizeof_op_elem;
+    r.mb = curr_membership;
+    r.ns = type == invs ? node_suspected : nullptr;
+    r.rw = type == acks ? reinterpret_cast<uint8_t *>(read_write_ops) : nullptr;
+    std::unique_lock<std::mutex> lk(t->hmu);
+    t->hq.push_back(&r);
+    while (!r.launched) {
+        if (!t->combining) host_combine(t, lk);
+        else t->hcv.wait(lk);
+    }
+    HostSet *set = r.set;
+    lk.unlock();
+    if (hipEventSynchronize(set->ev) != hipSuccess) die("sync");
+    memcpy(op_array, set->h + r.ops_off, (size_t)op_num * sizeof_op_elem);
+    if (r.rw) memcpy(r.rw, set->h + r.rw_off, r.rw_bytes);
+    if (r.ns) memcpy(r.ns, set->h + r.ns_off, 4);
+    lk.lock();
+    if (--set->refs == 0) {
+        set->busy = false;
+        t->hcv.notify_all();
+    }
     TRACE("done");
 }
 

@@ -21,7 +21,8 @@ for line in open(sys.argv[1]):
     if "retry" in det:
         print(f"  retry {det['retry']['value'] / 1e6:.1f} M/s")
     if "host_api" in det:
-        print(f"  host_api {det['host_api']['value'] / 1e6:.2f} M/s ({det['host_api']['us_per_call']:.1f} us/call)")
+        h = det["host_api"]
+        print("  host_api", {k: round(v / 1e6, 2) for k, v in h.items() if k.startswith("threads_")}, "M local ops/s")
     if "cpu_baseline" in d:
         c = d["cpu_baseline"]
         print(f"  cpu {c['value'] / 1e6:.2f} M/s cores {c['cores']} kind {c['kind']}")

@@ -82,6 +82,16 @@ struct BatchArgs {
     int32_t ack_direct;          // ACK launch on the direct path (k_ack_resolve)
     uint8_t g_membership;
     uint8_t w_ack_init;
+    int32_t *node_suspected;     // small launches write it themselves
+    int32_t n_batches;
+    const uint8_t *host_src;     // small launches staged in host memory (BatchLaunch)
+    uint8_t *host_dst;
+    uint8_t *dev_region;
+    uint64_t region_bytes;
+    uint32_t *done_flag;
+    uint32_t done_value;
+    unsigned long long *prof;    // HKV_SMALL_PROF: phase timestamps of k_small (debug)
+    const SmallBatch *hdr;       // mixed small launches: the batch headers (in dev_region)
 };
 
 // Rounds after round 0 per batch type: how often a hot key usually mutates in one launch beyond
@@ -1096,6 +1106,333 @@ __global__ __launch_bounds__(kFbThreads) void k_fb_exec(BatchArgs a)
     }
 }
 
+// ------------------------------------------------------------------ small launches
+// Launches of at most kSmallMax elements (the drop-in entry point's combined host batches, a
+// few hundred to a few thousand elements) run in ONE workgroup and ONE kernel: the launch-wide
+// latency of the multi-kernel engine (lookup, resolve, commit passes) is what bounds them, not
+// bandwidth. The same rounds, with the workgroup's barriers instead of kernel boundaries:
+//   lookup     every element (four per thread) as hermesKV.c:938-993; entry ids in LDS
+//   round r    pending elements test would_mutate against their key's entry as it stands
+//              (S_r); candidates lower their key's F in an LDS hash table (entry id -> F);
+//              barrier; elements before F (or of keys without one) resolve on private copies of
+//              S_r; barrier; F applies to the entry itself (S_r -> S_{r+1}); barrier.
+//   after kSmallRounds rounds, keys still mutating are finished serially: the smallest pending
+//   element of each key walks its key's pending elements in element order.
+// Exactness is the engine's (would_mutate sound, checked through *error_flags).
+constexpr int kSmallMax = (int)kSmallMaxElems;
+constexpr int kSmallThreads = 1024;
+constexpr int kSmallPer = kSmallMax / kSmallThreads;
+constexpr int kSmallSlots = 2 * kSmallMax;
+constexpr int kSmallRounds = 8;
+
+__device__ __forceinline__ uint32_t small_slot(uint32_t *hkey, uint32_t e)
+{
+    uint32_t h = (e * 0x9E3779B1u) >> (32 - 13);  // kSmallSlots = 2^13
+    for (;;) {
+        const uint32_t old = atomicCAS(&hkey[h], kNone, e);
+        if (old == kNone || old == e) return h;
+        h = (h + 1) & (kSmallSlots - 1);
+    }
+}
+
+// Where element i of a small launch lives. Uniform launches: n_batches batches of one type at
+// `stride` elements each (hkv_batch_async). Mixed launches (the combining submit of the host entry
+// point): batches of any type back to back, each described by a SmallBatch header, element i in
+// the batch b with bstart[b] <= i < bstart[b + 1].
+struct SmallView {
+    uint8_t *x;
+    uint8_t idx;
+    int type;
+    int b;
+    bool live;
+};
+
+template <bool MIXED>
+__device__ __forceinline__ SmallView small_at(const BatchArgs &a, const int32_t *bstart, const SmallBatch *bh,
+                                              int i, Ctx &c)
+{
+    SmallView v;
+    if (!MIXED) {
+        const int32_t b = i / a.stride, idx = i - b * a.stride;
+        v.x = a.elems + (int64_t)i * a.esz;
+        v.idx = (uint8_t)idx;
+        v.type = a.type;
+        v.b = b;
+        v.live = a.counts == nullptr || idx < a.counts[b];
+        c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
+        return v;
+    }
+    int lo = 0, hi = a.n_batches;  // the last b with bstart[b] <= i
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (bstart[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    const SmallBatch &h = bh[lo];
+    const int idx = i - bstart[lo];
+    v.x = a.dev_region + h.elem_off + (int64_t)idx * h.esz;
+    v.idx = (uint8_t)idx;
+    v.type = h.type;
+    v.b = lo;
+    v.live = true;
+    c.g_membership = h.g_membership;
+    c.w_ack_init = h.w_ack_init;
+    c.rw = h.rw_off >= 0 ? a.dev_region + h.rw_off : nullptr;
+    return v;
+}
+
+template <int SV, bool MIXED>
+__global__ __launch_bounds__(kSmallThreads) void k_small(BatchArgs a)
+{
+    extern __shared__ uint32_t lds[];
+    uint32_t *eid = lds;                          // [kSmallMax] entry id, kNone: skipped / missing / done
+    uint32_t *hkey = eid + kSmallMax;             // [kSmallSlots] entry id of the slot
+    uint32_t *hf = hkey + kSmallSlots;            // [kSmallSlots] the key's first candidate this round
+    int32_t *ns = reinterpret_cast<int32_t *>(hf + kSmallSlots);      // [kSmallMax] per batch: last membership change
+    uint16_t *slot = reinterpret_cast<uint16_t *>(ns + kSmallMax);    // [kSmallMax]
+    __shared__ int32_t bstart[kSmallMaxBatches + 1];
+    __shared__ SmallBatch bh[MIXED ? kSmallMaxBatches : 1];
+    const int tid = threadIdx.x;
+    const int n = (int)a.n;
+    if (a.prof && tid == 0) a.prof[0] = wall_clock64();
+    if (a.region_bytes) {  // staged in host memory: bring the launch's region into HBM (the
+                           // dispatch's system-scope acquire drops any line an earlier launch left)
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.host_src);
+        uint4 *dst = reinterpret_cast<uint4 *>(a.dev_region);
+        for (uint64_t w = tid; w < a.region_bytes / 16; w += kSmallThreads) dst[w] = src[w];
+        __threadfence_block();
+    }
+    for (int j = tid; j < kSmallSlots; j += kSmallThreads) {
+        hkey[j] = kNone;
+        hf[j] = kNone;
+    }
+    for (int j = tid; j < a.n_batches && j < kSmallMax; j += kSmallThreads) ns[j] = -1;
+    if (MIXED) {
+        __syncthreads();  // the copied-in headers
+        const SmallBatch *g = reinterpret_cast<const SmallBatch *>(a.dev_region);
+        for (int j = tid; j < a.n_batches; j += kSmallThreads) bh[j] = g[j];
+        if (tid == 0) {
+            int32_t acc = 0;
+            for (int j = 0; j < a.n_batches; ++j) {
+                bstart[j] = acc;
+                acc += g[j].count;
+            }
+            bstart[a.n_batches] = acc;
+        }
+    }
+    __syncthreads();
+    if (a.prof && tid == 0) a.prof[1] = wall_clock64();
+    Ctx c = make_ctx(a);
+    // lookup (hermesKV.c:938-993); a hit reads the key and its meta S_0 from the log line at once
+    Meta m0[kSmallPer];
+    uint32_t pend = 0;  // bit k: element tid + k * kSmallThreads is pending
+#pragma unroll
+    for (int k = 0; k < kSmallPer; ++k) {
+        const int i = tid + k * kSmallThreads;
+        if (i >= n) continue;
+        uint32_t e = kNone;
+        const SmallView v = small_at<MIXED>(a, bstart, bh, i, c);
+        if (v.live) {
+            const U64x2 h = *reinterpret_cast<const U64x2 *>(v.x);
+            if (skip_elem_os(v.type, (uint8_t)h.b, (uint8_t)(h.b >> 8))) {
+                if (v.type == kInvs) atomicMax(&ns[v.b], (int)v.idx);   // hermes_skip_inv: the last one wins
+            } else {
+                const uint64_t key = h.a;
+                const uint4 *bk = reinterpret_cast<const uint4 *>(a.index + ((key & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u);
+                const uint4 q0 = bk[0], q1 = bk[1], q2 = bk[2], q3 = bk[3];
+                const uint64_t sl[8] = {(uint64_t)q0.x | ((uint64_t)q0.y << 32), (uint64_t)q0.z | ((uint64_t)q0.w << 32),
+                                        (uint64_t)q1.x | ((uint64_t)q1.y << 32), (uint64_t)q1.z | ((uint64_t)q1.w << 32),
+                                        (uint64_t)q2.x | ((uint64_t)q2.y << 32), (uint64_t)q2.z | ((uint64_t)q2.w << 32),
+                                        (uint64_t)q3.x | ((uint64_t)q3.y << 32), (uint64_t)q3.z | ((uint64_t)q3.w << 32)};
+                const uint32_t tag = (uint32_t)(key >> 48);
+                int hit = -1;
+#pragma unroll
+                for (int q = 7; q >= 0; --q)
+                    if ((sl[q] & 1u) && ((uint32_t)(sl[q] >> 1) & 0x7FFFFFu) == tag) hit = q;
+                if (hit >= 0) {
+                    const uint64_t off = sl[hit] >> 24;
+                    if (a.g.log_head - off < a.g.log_cap) {
+                        const uint64_t phys = off & a.g.log_mask;
+                        const U64x2 *ln = reinterpret_cast<const U64x2 *>(a.log + phys);
+                        const U64x2 l0 = ln[0], l1 = ln[1], l2 = ln[2];  // key at 8, meta at 16..32
+                        if (l0.b == key) {
+                            e = (uint32_t)(phys / a.g.entry_unit);
+                            m0[k].w4 = (uint32_t)l1.a;
+                            m0[k].w5 = (uint32_t)(l1.a >> 32);
+                            m0[k].ver = (uint32_t)l1.b;
+                            m0[k].llw_cid = (uint8_t)(l1.b >> 32);
+                            m0[k].llw_ver = (uint32_t)(l1.b >> 40) | ((uint32_t)(l2.a & 0xFFu) << 24);
+                        }
+                    }
+                }
+                if (e == kNone) v.x[9] = kMiss;
+            }
+        }
+        eid[i] = e;
+        if (e != kNone) {
+            slot[i] = (uint16_t)small_slot(hkey, e);
+            pend |= 1u << k;
+        }
+    }
+    __syncthreads();
+    if (a.prof && tid == 0) a.prof[2] = wall_clock64();
+    bool any = true;
+    for (int r = 0;; ++r) {
+        any = __syncthreads_or(pend != 0);
+        if (!any || r == kSmallRounds) break;
+        // round 0 tests S_0 from the lookup's registers, later rounds the entry as it now stands
+#pragma unroll
+        for (int k = 0; k < kSmallPer; ++k) {  // candidates of round r
+            if (!(pend >> k & 1u)) continue;
+            const int i = tid + k * kSmallThreads;
+            const SmallView v = small_at<MIXED>(a, bstart, bh, i, c);
+            if (r > 0) meta_load(entry_of(a, eid[i]), m0[k]);
+            if (would_mutate(v.type, v.x, m0[k], c)) atomicMin(&hf[slot[i]], (uint32_t)i);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kSmallPer; ++k) {  // before the key's candidate: S_r, unchanged
+            if (!(pend >> k & 1u)) continue;
+            const int i = tid + k * kSmallThreads;
+            if (hf[slot[i]] <= (uint32_t)i) continue;
+            const SmallView v = small_at<MIXED>(a, bstart, bh, i, c);
+            Meta t = m0[k];
+            dispatch<SV>(v.type, v.x, entry_of(a, eid[i]), v.idx, t, c);
+            if (a.error_flags && !meta_equal(t, m0[k])) atomicOr(a.error_flags, 1u);
+            pend &= ~(1u << k);
+        }
+        __threadfence_block();
+        __syncthreads();  // every read of S_r precedes the mutation
+#pragma unroll
+        for (int k = 0; k < kSmallPer; ++k) {  // the candidate: S_r -> S_{r+1}
+            if (!(pend >> k & 1u)) continue;
+            const int i = tid + k * kSmallThreads;
+            if (hf[slot[i]] != (uint32_t)i) continue;
+            const SmallView v = small_at<MIXED>(a, bstart, bh, i, c);
+            uint8_t *entry = entry_of(a, eid[i]);
+            Meta m = m0[k];
+            dispatch<SV>(v.type, v.x, entry, v.idx, m, c);
+            meta_store(entry, m);
+            hf[slot[i]] = kNone;
+            pend &= ~(1u << k);
+        }
+        __threadfence_block();
+    }
+    if (a.prof && tid == 0) a.prof[3] = wall_clock64();
+    if (any) {  // keys that kept mutating: the first pending element of each key finishes it in order
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kSmallPer; ++k) {
+            const int i = tid + k * kSmallThreads;
+            if (i < n && !(pend >> k & 1u)) eid[i] = kNone;   // done: no longer part of any key's walk
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kSmallPer; ++k)
+            if (pend >> k & 1u) atomicMin(&hf[slot[tid + k * kSmallThreads]], (uint32_t)(tid + k * kSmallThreads));
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kSmallPer; ++k) {
+            const int i = tid + k * kSmallThreads;
+            if (!(pend >> k & 1u) || hf[slot[i]] != (uint32_t)i) continue;
+            const uint32_t e = eid[i];
+            uint8_t *entry = entry_of(a, e);
+            Meta m;
+            meta_load(entry, m);
+            for (int j = i; j < n; ++j) {
+                if (eid[j] != e) continue;
+                const SmallView v = small_at<MIXED>(a, bstart, bh, j, c);
+                dispatch<SV>(v.type, v.x, entry, v.idx, m, c);
+            }
+            meta_store(entry, m);
+        }
+    }
+    // hermes_skip_dispatcher's *node_suspected = value[0] of each INV batch's last membership change
+    if (MIXED) {
+        __syncthreads();
+        for (int b = tid; b < a.n_batches; b += kSmallThreads) {
+            const SmallBatch &h = bh[b];
+            if (h.type == kInvs && h.ns_off >= 0 && ns[b] >= 0)
+                *reinterpret_cast<int32_t *>(a.dev_region + h.ns_off) =
+                    a.dev_region[h.elem_off + (int64_t)ns[b] * h.esz + kOpValueOff];
+        }
+    } else if (a.type == kInvs && a.node_suspected) {
+        __syncthreads();
+        for (int b = tid; b < a.n_batches; b += kSmallThreads)
+            if (ns[b] >= 0) a.node_suspected[b] = a.elems[((int64_t)b * a.stride + ns[b]) * a.esz + kOpValueOff];
+    }
+    if (a.prof && tid == 0) a.prof[4] = wall_clock64();
+    if (a.region_bytes) {  // results back to the host staging, then the completion flag
+        __threadfence_block();  // one workgroup wrote the region: its CU's caches see it
+        __syncthreads();
+        // System-scope stores (sc0 sc1) write through L2 to the host, and a thread's vmcnt counts
+        // them done once they are visible there: each thread waits for its own, then the flag
+        // follows the barrier. A __threadfence_system() instead writes back all of L2, every entry
+        // this launch dirtied included (~10 us); plain stores would sit in L2 and reach the host
+        // later, over the set's next use.
+        const unsigned long long *src = reinterpret_cast<const unsigned long long *>(a.dev_region);
+        unsigned long long *dst = reinterpret_cast<unsigned long long *>(a.host_dst);
+        for (uint64_t w = tid; w < a.region_bytes / 8; w += kSmallThreads)
+            __hip_atomic_store(dst + w, src[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(a.done_flag, a.done_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (a.prof && tid == 0) a.prof[5] = wall_clock64();
+}
+
+int launch_small(const BatchArgs &a0, hipStream_t s)
+{
+    // HKV_SMALL_PROF=N: every N-th launch records its phase timestamps and prints the running
+    // average (debug; synchronises the stream)
+    static const int prof_every = getenv("HKV_SMALL_PROF") ? atoi(getenv("HKV_SMALL_PROF")) : 0;
+    static unsigned long long *prof = nullptr;
+    static long prof_n = 0;
+    static double prof_sum[5] = {0, 0, 0, 0, 0};
+    BatchArgs a = a0;
+    a.prof = nullptr;
+    const bool sample = prof_every > 0 && (++prof_n % prof_every) == 0;
+    if (sample) {
+        if (!prof && hipHostMalloc((void **)&prof, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return -3;
+        a.prof = prof;
+    }
+    const size_t lds = (size_t)4 * (2 * kSmallMax + 2 * kSmallSlots) + (size_t)2 * kSmallMax;
+    auto setup = [&](const void *f, int k) {
+        static bool done[6] = {false, false, false, false, false, false};
+        if (!done[k]) {
+            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return false;
+            done[k] = true;
+        }
+        return true;
+    };
+#define HKV_SMALL(V, M)                                                                   \
+    do {                                                                                  \
+        if (!setup((const void *)k_small<V, M>, (V == 31 ? 0 : V == 287 ? 1 : 2) + (M ? 3 : 0))) return -3; \
+        hipLaunchKernelGGL((k_small<V, M>), dim3(1), dim3(kSmallThreads), lds, s, a);        \
+    } while (0)
+    const bool mixed = a.hdr != nullptr;
+    if (a.g.st_value == 31) {
+        if (mixed) HKV_SMALL(31, true);
+        else HKV_SMALL(31, false);
+    } else if (a.g.st_value == 287) {
+        if (mixed) HKV_SMALL(287, true);
+        else HKV_SMALL(287, false);
+    } else {
+        if (mixed) HKV_SMALL(0, true);
+        else HKV_SMALL(0, false);
+    }
+#undef HKV_SMALL
+    if (sample) {
+        hipStreamSynchronize(s);
+        static long k = 0;
+        ++k;
+        for (int p = 0; p < 5; ++p) prof_sum[p] += (double)(prof[p + 1] - prof[p]) * 10.0 / 1000.0;  // 100 MHz ticks -> us
+        fprintf(stderr, "[hkv] k_small phases (us, avg of %ld): copy-in+init %.2f lookup %.2f rounds %.2f fallback %.2f copy-out %.2f\n", k,
+                prof_sum[0] / k, prof_sum[1] / k, prof_sum[2] / k, prof_sum[3] / k, prof_sum[4] / k);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 __global__ void k_node_suspected(const uint8_t *elems, const int32_t *ns_idx, int32_t *out, int32_t n_batches,
                                  int32_t stride, int32_t esz)
 {
@@ -1173,16 +1510,30 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.ack_direct = bl.type == kAcks && !bl.g.rmw_enabled && n < (int64_t)kNone;
     a.g_membership = bl.g_membership;
     a.w_ack_init = bl.w_ack_init;
+    a.node_suspected = bl.node_suspected;
+    a.n_batches = bl.n_batches;
+    a.host_src = bl.host_src;
+    a.host_dst = bl.host_dst;
+    a.dev_region = bl.dev_region;
+    a.region_bytes = bl.region_bytes;
+    a.done_flag = bl.done_flag;
+    a.done_value = bl.done_value;
+    a.hdr = bl.hdr;
     const unsigned grid = (unsigned)((n + 255) / 256);
     const unsigned cgrid = (unsigned)((n + 256 * kCandPer - 1) / (256 * kCandPer));
     const bool big = bl.esz > 64;
     const unsigned rgrid = (unsigned)(big ? (n + 127) / 128 : grid);
     const size_t rlds = (size_t)(big ? 128 : 256) * (size_t)bl.esz;
     constexpr int64_t kPer = 64 * kLookupPair;  // elements per k_lookup block
-    if (bl.type == kVals) {                    // one pass (see k_lookup)
+    const bool small = (bl.path == kPathSmall || (bl.path == kPathAuto && n <= kSmallMax)) && n <= kSmallMax;
+    if (bl.region_bytes && !small) return -1;  // host-staged launches are small ones
+    if (small) {
+        if (launch_small(a, s)) return -3;
+        return 0;                              // node_suspected written by the kernel
+    } else if (bl.type == kVals) {             // one pass (see k_lookup)
         hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, n);
         return hipGetLastError() == hipSuccess ? 0 : -3;
-    }
+    } else {
     // The head split pays off where one launch piles many candidates onto a few keys: local
     // batches under Zipf. A replica's INVs and ACKs carry at most one write per key and peer per
     // round, so those launches take one pass (their launch-sized head took ~9 us at cfg2).
@@ -1230,6 +1581,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     }
 #undef HKV_ROUNDS_SV
 #undef HKV_ROUNDS
+    }
     }
     if (hipGetLastError() != hipSuccess) return -3;
     static const bool stats = getenv("HKV_STATS") != nullptr;

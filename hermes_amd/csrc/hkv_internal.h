@@ -38,7 +38,32 @@ struct BatchLaunch {
     int32_t type;
     uint8_t g_membership;
     uint8_t w_ack_init;
+    int32_t path;                             // kPath*: which engine runs the launch
+    // small launches staged in host memory (the combining submit of hermes_batch_ops_to_KVS): the
+    // kernel first copies region_bytes from host_src to dev_region (where elems, counts, rw and
+    // node_suspected point), at the end copies them back to host_dst, then stores done_value into
+    // *done_flag at system scope. region_bytes = 0: everything already in device memory.
+    const uint8_t *host_src;
+    uint8_t *host_dst;
+    uint8_t *dev_region;
+    uint64_t region_bytes;
+    uint32_t *done_flag;
+    uint32_t done_value;
+    // mixed small launches (host-staged): n_batches headers at dev_region, batches of any type and
+    // element size back to back; elems/counts/stride/esz/type/rw/node_suspected unused
+    const struct SmallBatch *hdr;
 };
+
+// One batch of a mixed small launch; offsets are bytes from the launch's device region.
+struct SmallBatch {
+    int32_t type, count, esz, elem_off;
+    int32_t rw_off, ns_off;   // -1: none (rw: ACK batches' read_write_ops; ns: INV batches' node_suspected)
+    uint8_t g_membership, w_ack_init, pad0, pad1;
+    int32_t pad2;
+};
+constexpr int kSmallMaxBatches = 64;
+
+enum : int32_t { kPathAuto = 0, kPathEngine = 1, kPathSmall = 2 };
 
 struct PopulateLaunch {
     uint64_t *first, *second;
@@ -67,6 +92,7 @@ struct TableView {
 int table_view(const hkv_table *t, TableView *out);
 
 int launch_batch(const BatchLaunch &bl, hipStream_t s);
+constexpr int64_t kSmallMaxElems = 4096;   // launches the single-workgroup kernel can take
 int launch_populate(const PopulateLaunch &pl, hipStream_t s);
 int launch_hash_ids(const uint32_t *ids, uint64_t *out, int64_t n, hipStream_t s);
 size_t sort_temp_bytes(int64_t n, int key_bits);

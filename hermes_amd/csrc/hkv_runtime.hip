@@ -10,6 +10,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <sched.h>
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -33,15 +35,20 @@ using namespace hkv;
 // Launches on one stream run in order, so the combined result is the serial order of the sets'
 // concatenations -- an order the reference could have produced. With several sets, the next
 // combiner stages while the GPU runs the previous launch.
-constexpr int kHostSets = 3;
+constexpr int kHostSets = 2;
 constexpr int kHostMaxBatches = 64;
 constexpr int64_t kHostMaxElems = 32768;
 
 struct HostSet {
-    uint8_t *h = nullptr;    // pinned: counts | node_suspected | ops | rw
+    uint8_t *h = nullptr;    // pinned, coherent: counts | node_suspected | ops | rw
+    uint8_t *hd = nullptr;   // the same bytes as the device sees them
     uint8_t *d = nullptr;
     size_t cap = 0;
     hipEvent_t ev = nullptr;
+    uint32_t *flag = nullptr;   // pinned: the launch's kernel stores `seq` when its results are in h
+    uint32_t *flag_d = nullptr;
+    uint32_t seq = 0;
+    bool small = false;      // this launch signals through flag (else through ev)
     int refs = 0;            // callers still to copy their results out
     bool busy = false;
 };
@@ -288,6 +295,7 @@ int hkv_table_destroy(hkv_table *t)
     for (HostSet &hs : t->sets) {
         hipFree(hs.d);
         hipHostFree(hs.h);
+        hipHostFree(hs.flag);
         if (hs.ev) hipEventDestroy(hs.ev);
     }
     if (t->stream) hipStreamDestroy(t->stream);
@@ -424,6 +432,7 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.type = d->type;
     bl.g_membership = d->membership[1];
     bl.w_ack_init = d->membership[2];
+    bl.path = (d->flags & HKV_BATCH_ENGINE) ? kPathEngine : (d->flags & HKV_BATCH_SMALL) ? kPathSmall : kPathAuto;
     TRACE("batch_async type=%d n=%lld", d->type, (long long)n);
     rc = launch_batch(bl, s);
     if (rc) return fail(rc, "batch launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));
@@ -528,10 +537,143 @@ void spacetime_populate_fixed_len(struct spacetime_kv *, int n, int val_len)
     if (hkv_table_populate(t, n, val_len)) die("spacetime_populate_fixed_len");
 }
 
+// HKV_HOST_STATS=1: launches and batches per launch of the combining submit, printed at exit
+static const bool g_host_stats = getenv("HKV_HOST_STATS") != nullptr;
+static std::atomic<long> g_hs_launches{0}, g_hs_batches{0};
+static void host_stats_print()
+{
+    const long l = g_hs_launches.load(), b = g_hs_batches.load();
+    fprintf(stderr, "[hkv] host submit: %ld launches, %ld batches, %.2f batches/launch\n", l, b, l ? (double)b / l : 0.0);
+}
+static void host_stats_note(int nb)
+{
+    static std::once_flag once;
+    std::call_once(once, [] { atexit(host_stats_print); });
+    g_hs_launches++;
+    g_hs_batches += nb;
+}
+
+static const bool g_staging_nc = getenv("HKV_STAGING_NC") != nullptr;  // experiment: non-coherent staging
+
 static bool host_compatible(const HostReq *a, const HostReq *b)
 {
     return a->type == b->type && a->esz == b->esz && a->mb == b->mb && (a->rw != nullptr) == (b->rw != nullptr) &&
            (a->ns != nullptr) == (b->ns != nullptr);
+}
+
+static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// (re)allocates a staging set for `total` bytes: pinned coherent host memory the kernel reads and
+// writes directly, and the device region it works in
+static void host_set_reserve(HostSet *set, size_t total)
+{
+    if (total > set->cap) {
+        hipFree(set->d);
+        hipHostFree(set->h);
+        set->d = set->h = set->hd = nullptr;
+        const size_t cap = std::max(total + total / 2, (size_t)1 << 20);
+        if (hipMalloc(&set->d, cap) != hipSuccess ||
+            hipHostMalloc((void **)&set->h, cap, hipHostMallocMapped | (g_staging_nc ? hipHostMallocNonCoherent : hipHostMallocCoherent)) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&set->hd, set->h, 0) != hipSuccess)
+            die("staging alloc");
+        set->cap = cap;
+    }
+    if (!set->ev && hipEventCreateWithFlags(&set->ev, hipEventDisableTiming) != hipSuccess) die("event");
+    if (!set->flag) {
+        if (hipHostMalloc((void **)&set->flag, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&set->flag_d, set->flag, 0) != hipSuccess)
+            die("flag alloc");
+        __atomic_store_n(set->flag, 0u, __ATOMIC_RELEASE);
+    }
+}
+
+// The queued batches (any type, in queue order, as many as fit kSmallMaxElems elements and
+// kSmallMaxBatches batches) as ONE mixed launch of the single-workgroup kernel: the region holds
+// the batch headers, each batch's elements, each ACK batch's read_write_ops and each INV batch's
+// node_suspected; the kernel copies it in, applies the batches in order, copies it back and
+// stores the set's sequence number into set->flag. Called with t->hmu held.
+static void host_launch_mixed(hkv_table *t, HostSet *set, std::unique_lock<std::mutex> &lk)
+{
+    std::vector<HostReq *> take;
+    int64_t elems = 0;
+    for (auto it = t->hq.begin(); it != t->hq.end() && (int)take.size() < kSmallMaxBatches;) {
+        HostReq *r = *it;
+        if (elems + r->n > kSmallMaxElems) {
+            ++it;
+            continue;
+        }
+        elems += r->n;
+        take.push_back(r);
+        it = t->hq.erase(it);
+    }
+    lk.unlock();
+    const int nb = (int)take.size();
+    const size_t rw_bytes = (size_t)t->cfg.rw_len * t->geo.op_size;
+    size_t off = align16(sizeof(SmallBatch) * (size_t)nb);
+    for (HostReq *r : take) {
+        r->ops_off = off;
+        off = align16(off + (size_t)r->n * r->esz);
+    }
+    for (HostReq *r : take) {
+        r->rw_bytes = r->type == acks && r->rw ? rw_bytes : 0;
+        r->rw_off = off;
+        off = align16(off + r->rw_bytes);
+        r->ns_off = off;
+        if (r->type == invs && r->ns) off += 4;
+    }
+    const size_t total = align16(off);
+    host_set_reserve(set, total);
+    SmallBatch *hdr = reinterpret_cast<SmallBatch *>(set->h);
+    for (int b = 0; b < nb; ++b) {
+        HostReq *r = take[b];
+        SmallBatch &h = hdr[b];
+        memset(&h, 0, sizeof h);
+        h.type = r->type;
+        h.count = r->n;
+        h.esz = r->esz;
+        h.elem_off = (int32_t)r->ops_off;
+        h.rw_off = r->rw_bytes ? (int32_t)r->rw_off : -1;
+        h.ns_off = r->type == invs && r->ns ? (int32_t)r->ns_off : -1;
+        h.g_membership = (uint8_t)(r->mb >> 8);
+        h.w_ack_init = (uint8_t)(r->mb >> 16);
+        memcpy(set->h + r->ops_off, r->ops, (size_t)r->n * r->esz);
+        if (r->rw_bytes) memcpy(set->h + r->rw_off, r->rw, r->rw_bytes);
+        if (h.ns_off >= 0) memcpy(set->h + r->ns_off, r->ns, 4);
+    }
+    BatchLaunch bl;
+    memset(&bl, 0, sizeof bl);
+    bl.g = t->geo;
+    bl.index = t->d_index;
+    bl.log = t->d_log;
+    bl.error_flags = t->d_error_flags;
+    bl.n = elems;
+    bl.n_batches = nb;
+    bl.stride = 1;
+    bl.esz = 16;
+    bl.type = take[0]->type;
+    bl.g_membership = hdr[0].g_membership;
+    bl.w_ack_init = hdr[0].w_ack_init;
+    bl.path = kPathSmall;
+    bl.host_src = set->hd;
+    bl.host_dst = set->hd;
+    bl.dev_region = set->d;
+    bl.region_bytes = total;
+    bl.done_flag = set->flag_d;
+    bl.done_value = ++set->seq;
+    bl.hdr = reinterpret_cast<const SmallBatch *>(set->d);
+    set->small = true;
+    if (g_host_stats) host_stats_note(nb);
+    TRACE("mixed launch batches=%d elements=%lld", nb, (long long)elems);
+    if (launch_batch(bl, t->stream)) die("hermes_batch_ops_to_KVS (small launch)");
+    lk.lock();
+    set->busy = true;
+    set->refs = nb;
+    for (HostReq *r : take) {
+        r->set = set;
+        r->launched = true;
+    }
+    t->combining = false;
+    t->hcv.notify_all();
 }
 
 // Called with t->hmu held by a caller that found no combiner active: launches the compatible
@@ -552,11 +694,20 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
     std::vector<HostReq *> take;
     int stride = 0;
     const HostReq *head = t->hq.front();
+    if (head->n <= kSmallMaxElems) {  // batches of any type, one single-workgroup kernel
+        host_launch_mixed(t, set, lk);
+        return;
+    }
+    // a batch larger than the single-workgroup kernel takes: every queued batch of its kind on the
+    // multi-kernel engine. Each caller has one batch queued at a time, so taking them out of queue
+    // order still keeps every caller's own calls in program order.
     for (auto it = t->hq.begin(); it != t->hq.end() && (int)take.size() < kHostMaxBatches;) {
         HostReq *r = *it;
-        if (!host_compatible(head, r)) break;  // keep the callers' queue order
         const int st = std::max(stride, r->n);
-        if (!take.empty() && (int64_t)st * (int64_t)(take.size() + 1) > kHostMaxElems) break;
+        if (!host_compatible(head, r) || (!take.empty() && (int64_t)st * (int64_t)(take.size() + 1) > kHostMaxElems)) {
+            ++it;
+            continue;
+        }
         stride = st;
         take.push_back(r);
         it = t->hq.erase(it);
@@ -570,17 +721,8 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
     const size_t ops_off = ((size_t)8 * nb + 255) & ~(size_t)255;
     const size_t ops_bytes = (size_t)nb * stride * r0->esz;
     const size_t rw_off = (ops_off + ops_bytes + 255) & ~(size_t)255;
-    const size_t total = rw_off + (size_t)nb * rw_bytes;
-    if (total > set->cap) {
-        hipFree(set->d);
-        hipHostFree(set->h);
-        set->d = set->h = nullptr;
-        const size_t cap = std::max(total + total / 2, (size_t)1 << 20);
-        if (hipMalloc(&set->d, cap) != hipSuccess || hipHostMalloc((void **)&set->h, cap, hipHostMallocDefault) != hipSuccess)
-            die("staging alloc");
-        set->cap = cap;
-    }
-    if (!set->ev && hipEventCreateWithFlags(&set->ev, hipEventDisableTiming) != hipSuccess) die("event");
+    const size_t total = (rw_off + (size_t)nb * rw_bytes + 15) & ~(size_t)15;
+    host_set_reserve(set, total);
     int32_t *h_counts = reinterpret_cast<int32_t *>(set->h);
     int32_t *h_ns = h_counts + nb;
     for (int b = 0; b < nb; ++b) {
@@ -595,6 +737,7 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
         if (with_rw) memcpy(set->h + r->rw_off, r->rw, rw_bytes);
     }
     hipStream_t s = t->stream;
+    set->small = false;
     if (hipMemcpyAsync(set->d, set->h, total, hipMemcpyHostToDevice, s) != hipSuccess) die("copy in");
     hkv_batch_desc d;
     memset(&d, 0, sizeof d);
@@ -609,6 +752,7 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
     d.d_node_suspected = with_ns ? reinterpret_cast<int32_t *>(set->d) + nb : nullptr;
     memcpy(d.membership, &r0->mb, 8);
     TRACE("combined launch type=%d batches=%d stride=%d", d.type, nb, stride);
+    if (g_host_stats) host_stats_note(nb);
     if (hkv_batch_async(t, &d, s)) die("hermes_batch_ops_to_KVS");
     if (hipMemcpyAsync(set->h, set->d, total, hipMemcpyDeviceToHost, s) != hipSuccess) die("copy out");
     if (hipEventRecord(set->ev, s) != hipSuccess) die("event record");
@@ -662,10 +806,20 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
         else t->hcv.wait(lk);
     }
     HostSet *set = r.set;
+    const uint32_t seq = set->seq;
+    const bool small = set->small;
     lk.unlock();
-    if (hipEventSynchronize(set->ev) != hipSuccess) die("sync");
+    if (small) {  // the kernel's completion flag in pinned memory; yield now and then, so callers
+                  // that outnumber the cores leave the next combiner CPU time
+        for (uint32_t spins = 0; __atomic_load_n(set->flag, __ATOMIC_ACQUIRE) != seq; ++spins) {
+            __builtin_ia32_pause();
+            if ((spins & 1023u) == 1023u) sched_yield();
+        }
+    } else if (hipEventSynchronize(set->ev) != hipSuccess) {
+        die("sync");
+    }
     memcpy(op_array, set->h + r.ops_off, (size_t)op_num * sizeof_op_elem);
-    if (r.rw) memcpy(r.rw, set->h + r.rw_off, r.rw_bytes);
+    if (r.rw && r.rw_bytes) memcpy(r.rw, set->h + r.rw_off, r.rw_bytes);
     if (r.ns) memcpy(r.ns, set->h + r.ns_off, 4);
     lk.lock();
     if (--set->refs == 0) {

@@ -77,8 +77,14 @@ def sized_geometry(num_keys: int, sizes: L.Sizes = L.DEFAULT) -> tuple[int, int]
     return min(bkts, 1 << (27 if num_keys <= 1 << 28 else 29)), cap
 
 
+BATCH_ENGINE = 1   # hkv_batch_desc.flags (include/hermeskv.h): the multi-kernel engine
+BATCH_SMALL = 2    # the single-workgroup kernel (launches of at most 4096 elements)
+
+
 class HermesKV:
     """One HermesKV replica: a MICA-herd table in HBM plus the batch path on it."""
+
+    default_flags = 0   # hkv_batch_desc.flags for every launch (tests pin one engine or the other)
 
     def __init__(self, num_keys: int | None = 1_000_000, num_bkts: int | None = None,
                  log_cap: int | None = None, machine_id: int = 0, rmw: bool = False,
@@ -156,6 +162,7 @@ class HermesKV:
         d.n_batches = int(n_batches)
         d.stride = int(stride)
         d.elem_size = int(elem_size)
+        d.flags = self.default_flags
         d.d_elems = elems.data_ptr()
         if counts is not None:
             assert counts.is_cuda and counts.dtype == torch.int32 and counts.numel() >= n_batches

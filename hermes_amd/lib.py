@@ -34,7 +34,7 @@ class HkvConfig(ctypes.Structure):
 
 class HkvBatchDesc(ctypes.Structure):
     _fields_ = [("type", ctypes.c_int32), ("n_batches", ctypes.c_int32), ("stride", ctypes.c_int32),
-                ("elem_size", ctypes.c_uint16), ("reserved", ctypes.c_uint16),
+                ("elem_size", ctypes.c_uint16), ("flags", ctypes.c_uint16),
                 ("d_elems", ctypes.c_void_p), ("d_counts", ctypes.c_void_p), ("d_rw", ctypes.c_void_p),
                 ("rw_stride_bytes", ctypes.c_int64), ("d_node_suspected", ctypes.c_void_p),
                 ("membership", ctypes.c_uint8 * 8)]

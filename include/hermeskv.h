@@ -108,7 +108,7 @@ typedef struct hkv_batch_desc {
     int32_t  n_batches;
     int32_t  stride;            /* elements reserved per batch */
     uint16_t elem_size;         /* sizeof_op_elem */
-    uint16_t reserved;
+    uint16_t flags;             /* HKV_BATCH_*: which engine runs the launch (0 = by size) */
     uint8_t *d_elems;           /* device */
     const int32_t *d_counts;    /* device, n_batches entries; NULL = stride each */
     uint8_t *d_rw;              /* device base of batch 0's read_write_ops (ACK batches) */
@@ -116,6 +116,11 @@ typedef struct hkv_batch_desc {
     int32_t *d_node_suspected;  /* device, n_batches entries (INV batches); NULL = ignore */
     uint8_t  membership[8];     /* spacetime_group_membership by value */
 } hkv_batch_desc;
+
+/* hkv_batch_desc.flags. By default launches of at most 4096 elements run as one single-workgroup
+ * kernel and larger ones on the multi-kernel engine; both give the same bytes. */
+#define HKV_BATCH_ENGINE 1u     /* always the multi-kernel engine */
+#define HKV_BATCH_SMALL  2u     /* the single-workgroup kernel (launches of at most 4096 elements) */
 
 int  hkv_abi_version(void);
 const char *hkv_last_error(void);

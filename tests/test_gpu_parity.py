@@ -23,6 +23,16 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
+@pytest.fixture(params=["engine", "small"], autouse=True)
+def engine_path(request):
+    """Every parity test runs on both device engines: the multi-kernel engine and the
+    single-workgroup kernel that launches of at most 4096 elements take by default."""
+    from hermes_amd import kvs
+    kvs.HermesKV.default_flags = kvs.BATCH_ENGINE if request.param == "engine" else kvs.BATCH_SMALL
+    yield request.param
+    kvs.HermesKV.default_flags = 0
+
+
 def _kvs():
     from hermes_amd.kvs import HermesKV
     return HermesKV

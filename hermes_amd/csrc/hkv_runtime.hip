@@ -90,6 +90,7 @@ struct hkv_table {
     std::condition_variable hcv;
     std::deque<HostReq *> hq;
     bool combining = false;
+    int inside = 0;   // callers inside hermes_batch_ops_to_KVS (queued, or waiting for results)
     HostSet sets[kHostSets];
     std::mutex mu;
 };
@@ -682,14 +683,33 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
 {
     t->combining = true;
     HostSet *set = nullptr;
+    static const int n_sets = getenv("HKV_HOST_SETS") ? std::max(1, std::min(kHostSets, atoi(getenv("HKV_HOST_SETS")))) : kHostSets;
     for (;;) {
-        for (HostSet &hs : t->sets)
+        for (int k = 0; k < n_sets; ++k) {
+            HostSet &hs = t->sets[k];
             if (!hs.busy) {
                 set = &hs;
                 break;
             }
+        }
         if (set) break;
         t->hcv.wait(lk);
+    }
+    // While another launch is in flight the GPU has work: wait for the callers that are not
+    // waiting on it to queue their batches (or for it to finish), so one launch carries them all.
+    for (;;) {
+        int other = 0;
+        const HostSet *busy = nullptr;
+        for (const HostSet &hs : t->sets)
+            if (hs.busy) {
+                other += hs.refs;
+                busy = &hs;
+            }
+        if (!busy || (int)t->hq.size() >= t->inside - other || (int)t->hq.size() >= kSmallMaxBatches) break;
+        if (busy->small && __atomic_load_n(busy->flag, __ATOMIC_ACQUIRE) == busy->seq) break;
+        lk.unlock();
+        for (int k = 0; k < 64; ++k) __builtin_ia32_pause();
+        lk.lock();
     }
     std::vector<HostReq *> take;
     int stride = 0;
@@ -801,6 +821,7 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
     r.rw = type == acks ? reinterpret_cast<uint8_t *>(read_write_ops) : nullptr;
     std::unique_lock<std::mutex> lk(t->hmu);
     t->hq.push_back(&r);
+    ++t->inside;
     while (!r.launched) {
         if (!t->combining) host_combine(t, lk);
         else t->hcv.wait(lk);
@@ -822,6 +843,7 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
     if (r.rw && r.rw_bytes) memcpy(r.rw, set->h + r.rw_off, r.rw_bytes);
     if (r.ns) memcpy(r.ns, set->h + r.ns_off, 4);
     lk.lock();
+    --t->inside;
     if (--set->refs == 0) {
         set->busy = false;
         t->hcv.notify_all();

@@ -59,6 +59,10 @@ def parse():
                    help="time the host-pointer entry point for this long (0 = skip; N=1 only)")
     p.add_argument("--no-fit-acks", action="store_true",
                    help="N=1: keep the ACK slab at its capacity stride (2C) instead of the round's largest count")
+    p.add_argument("--val-credits", type=int, default=None,
+                   help="N=1: VAL messages per worker and round (the VAL credits; 225 = the reference's 15 "
+                        "credits x 15 coalesced messages); workers with VALs outstanding do not poll ACKs. "
+                        "Default: credits that never bind (every ACK applied and every VAL sent each round)")
     p.add_argument("--retry", action="store_true",
                    help="refill_ops semantics: stalled ops keep their slot (default: fresh batch per step)")
     p.add_argument("--retry-steps", type=int, default=10,
@@ -148,7 +152,8 @@ def main():
         machines = 8 if cfg5 else 3
         rnd = Round(kvs, a.workers, L.membership(machines, 0), list(range(1, machines)), z, a.write_permille,
                     a.rmw_permille, seed=a.seed,
-                    max_steps=total_steps + 2, retry_stalled=a.retry, fit_ack_stride=not a.no_fit_acks)
+                    max_steps=total_steps + 2, retry_stalled=a.retry, fit_ack_stride=not a.no_fit_acks,
+                    val_credits=a.val_credits)
     torch.cuda.synchronize()
 
     for _ in range(a.warmup):
@@ -272,6 +277,8 @@ def main():
             # committed; writes in flight keep their slots. retry: refill_ops (inline-util.h:149-303),
             # stalled ops keep their slots (detail.retry reports that policy's rate at N=1)
             "refill": refill,
+            # VAL credits per worker and round (null: never binding, hermes_worker.c:479's gate idle)
+            "val_credits": getattr(rnd, "V", None),
             "remote_invs_per_worker": rnd.rstride, "parallelism": f"replicas{world}",
             "elements_per_step": {"inv": n_inv, "ack": n_ack, "val": n_val},
         },

@@ -287,7 +287,7 @@ __device__ __forceinline__ uint64_t with_op_state(uint64_t h, uint8_t op, uint8_
 // sent by a later round, as with the reference's credit-limited wings sends.
 __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stride, uint32_t op_size, uint8_t *out,
                                                       int32_t out_stride, int32_t *count, uint32_t machine_id,
-                                                      unsigned long long *held)
+                                                      unsigned long long *held, const int32_t *aq_n, int32_t r_alive)
 {
     const int w = blockIdx.x, i = threadIdx.x;
     const bool live = i < stride;
@@ -296,15 +296,20 @@ __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stri
     bool send = live && (st == kPutSuccess || st == kRmwSuccess || st == kReplaySuccess || st == kOpMembChange);
     int total;
     int rank = block_rank(send, total);
+    // INV credits: ACK packets return them (wings.h:426-540), so INVs whose ACKs this worker has not
+    // applied yet (aq_n / r_alive of them: held while VALs were outstanding) still hold theirs
+    const int cap = aq_n ? max(0, out_stride - aq_n[w] / max(1, r_alive)) : out_stride;
     if (i == 0) {
-        count[w] = total < out_stride ? total : out_stride;
-        if (total > out_stride && held) atomicAdd(held, (unsigned long long)(total - out_stride));
+        count[w] = total < cap ? total : cap;
+        if (total > cap && held) atomicAdd(held, (unsigned long long)(total - cap));
     }
+    out_stride = cap > 0 ? out_stride : 0;  // row stride unchanged; rank < cap below
+    const int send_cap = cap;
     if (op_size > 64) {  // big ops: one op at a time per wave, 8-B word k by lane k
         const int lane = i & 63;
         const int words = (int)(op_size / 8);
         uint8_t *wave_ops = ops + ((int64_t)w * stride + (i & ~63)) * op_size;
-        unsigned long long todo = __ballot(send && rank < out_stride);
+        unsigned long long todo = __ballot(send && rank < send_cap);
         while (todo) {
             const int j = __ffsll((long long)todo) - 1;
             todo &= todo - 1;
@@ -316,12 +321,12 @@ __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stri
                 dst[k] = k == 1 ? with_op_state(v, kOpInv, (uint8_t)machine_id) : v;
             }
         }
-        if (send && rank < out_stride)
+        if (send && rank < send_cap)
             op[9] = st == kPutSuccess ? kInProgressPut : st == kRmwSuccess ? kInProgressRmw
                   : st == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
         return;
     }
-    if (!send || rank >= out_stride) return;
+    if (!send || rank >= send_cap) return;
     uint8_t *dst = out + ((int64_t)w * out_stride + rank) * op_size;
     // 16-B words; the header word is rewritten in registers
     const W16 h = *reinterpret_cast<const W16 *>(op);
@@ -823,6 +828,106 @@ __global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32
     *reinterpret_cast<W16 *>(y) = W16{h.a, with_op_state(h.b, kOpAck, peer)};  // ack_copy_and_modify_elem
 }
 
+// The virtual peers' answers appended to each worker's ACK queue (aq: [W][q_stride] elements of
+// ack_size bytes, aq_n[w] queued): one workgroup per worker. A worker with outstanding VALs
+// (vq_n[w] > 0) does not poll its ACKs this round (hermes_worker.c:479): acnt[w] = 0 and the
+// queue keeps growing; otherwise acnt[w] = the whole queue, applied by this round's ACK batch.
+__global__ __launch_bounds__(256) void k_peer_acks_q(const uint8_t *invs, const int32_t *inv_count, int32_t inv_stride,
+                                                     uint32_t op_size, uint8_t *aq, uint32_t ack_size, int32_t q_stride,
+                                                     int32_t *aq_n, const int32_t *vq_n, int32_t *acnt,
+                                                     const uint8_t *peers, int32_t n_peers, TableView t,
+                                                     const unsigned long long *peer_ts, uint32_t round)
+{
+    const int w = blockIdx.x;
+    const int n = inv_count[w], base = aq_n[w];
+    const int total = n * n_peers;
+    for (int g = threadIdx.x; g < total; g += 256) {
+        const int j = g / n_peers, r = g - j * n_peers;
+        if (base + g >= q_stride) break;  // the host sizes q_stride for C INVs x n_peers
+        const uint8_t *x = invs + ((int64_t)w * inv_stride + j) * op_size;
+        uint8_t *y = aq + ((int64_t)w * q_stride + base + g) * ack_size;
+        const W16 h = *reinterpret_cast<const W16 *>(x);
+        const uint8_t peer = peers[r];
+        bool abort = false;
+        if (peer_ts && (x[16] & 1u) && peer < 8 && ack_size >= op_size) {
+            const uint64_t phys = find_entry(t, h.a);
+            if (phys != ~0ull) {
+                const unsigned long long pw = peer_ts[(phys / t.g.entry_unit) * 8 + peer];
+                const uint64_t ours = ((uint64_t)(uint32_t)(h.b >> 32) << 8) | (uint8_t)(h.b >> 24);
+                if ((uint32_t)(pw >> 41) == peer_round_tag(round) && (pw & 0xFFFFFFFFFFull) > ours) {
+                    const uint64_t pts = pw & 0xFFFFFFFFFFull;
+                    uint64_t *d = reinterpret_cast<uint64_t *>(y);
+                    d[0] = h.a;
+                    d[1] = (uint64_t)kOpInvAbort | ((uint64_t)peer << 8) | ((uint64_t)(uint8_t)x[10] << 16) |
+                           ((pts & 0xFFull) << 24) | ((pts >> 8) << 32);
+                    const uint64_t vv = 0x0101010101010101ULL * (uint8_t)('a' + peer);
+                    d[2] = (vv << 16) | ((uint64_t)x[17] << 8) | ((pw >> 40) & 1u);
+                    for (uint32_t k = 3; k < op_size / 8; ++k) d[k] = vv;
+                    abort = true;
+                }
+            }
+        }
+        if (!abort) *reinterpret_cast<W16 *>(y) = W16{h.a, with_op_state(h.b, kOpAck, peer)};
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int q = min(base + total, q_stride);
+        aq_n[w] = q;
+        acnt[w] = vq_n[w] > 0 ? 0 : q;
+    }
+}
+
+// VALs under credits: the worker's carried VALs (vq, from rounds whose VALs did not all fit) and
+// then the VALs of the writes this round's ACK batch completed (ST_LAST_ACK_SUCCESS in its ACK
+// queue, when it applied one: acnt[w] > 0) go out in that order, at most v_credits per round
+// (the VAL channel's credits, returned by the peers' CRD messages once they apply them:
+// hermes_worker.c:513, wings.h:862-916); the rest is carried to the next round, when the worker
+// sends them before polling ACKs again (has_outstanding_vals, hermes_worker.c:479, 500-503). An
+// applied queue empties (val_skip_or_get_sender_id / val_modify_elem_after_send set its elements
+// ST_EMPTY). One workgroup per worker.
+constexpr int kMaxVq = 1024;
+__global__ __launch_bounds__(256) void k_vals_credit(uint8_t *aq, int32_t *aq_n, const int32_t *acnt, int32_t q_stride,
+                                                     uint32_t ack_size, uint8_t *vq, int32_t *vq_n, int32_t vq_stride,
+                                                     uint8_t *out, int32_t *out_count, int32_t out_stride,
+                                                     int32_t v_credits, uint32_t machine_id,
+                                                     unsigned long long *overflow)
+{
+    __shared__ W16 buf[kMaxVq];
+    const int w = blockIdx.x;
+    const int carried = vq_n[w], applied = acnt[w];
+    W16 *vrow = reinterpret_cast<W16 *>(vq + (int64_t)w * vq_stride * kOpMetaSize);
+    for (int j = threadIdx.x; j < carried && j < kMaxVq; j += 256) buf[j] = vrow[j];
+    int total = min(carried, kMaxVq);
+    for (int j0 = 0; j0 < applied; j0 += 256) {
+        const int j = j0 + (int)threadIdx.x;
+        uint8_t *x = aq + ((int64_t)w * q_stride + j) * ack_size;
+        const uint8_t oc = j < applied ? x[8] : 0;
+        const bool send = j < applied && oc == kLastAckSuccess;
+        int cnt;
+        const int rank = block_rank(send, cnt);
+        if (send && total + rank < kMaxVq) {
+            const W16 h = *reinterpret_cast<const W16 *>(x);
+            buf[total + rank] = W16{h.a, (h.b & ~0xFFFFull) | kOpVal | ((uint64_t)(machine_id & 0xFF) << 8)};
+        } else if (send && overflow) {
+            atomicAdd(overflow, 1ull);
+        }
+        if (j < applied && (oc == kLastAckSuccess || oc == kAckSuccess || oc == kOpMembChange)) x[8] = kEmpty;
+        total = min(total + cnt, kMaxVq);
+    }
+    __syncthreads();
+    const int send = min(total, min(v_credits, out_stride));
+    W16 *orow = reinterpret_cast<W16 *>(out + (int64_t)w * out_stride * kOpMetaSize);
+    for (int j = threadIdx.x; j < send; j += 256) orow[j] = buf[j];
+    const int keep = min(total - send, vq_stride);
+    for (int j = threadIdx.x; j < keep; j += 256) vrow[j] = buf[send + j];
+    if (threadIdx.x == 0) {
+        out_count[w] = send;
+        vq_n[w] = keep;
+        if (applied) aq_n[w] = 0;
+        if (total - send > keep && overflow) atomicAdd(overflow, (unsigned long long)(total - send - keep));
+    }
+}
+
 }  // namespace hkv
 
 using namespace hkv;
@@ -869,7 +974,7 @@ int hkv_wl_marshal_invs(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_
 {
     if (stride > 256 || n_workers <= 0) return -1;
     hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
-                       stride, count, machine_id, (unsigned long long *)nullptr);
+                       stride, count, machine_id, (unsigned long long *)nullptr, (const int32_t *)nullptr, 1);
     return ok();
 }
 
@@ -973,7 +1078,17 @@ int hkv_wl_marshal_invs_cap(uint8_t *ops, int32_t n_workers, int32_t stride, uin
 {
     if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
     hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
-                       out_stride, count, machine_id, held);
+                       out_stride, count, machine_id, held, (const int32_t *)nullptr, 1);
+    return ok();
+}
+
+int hkv_wl_marshal_invs_credits(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint8_t *out,
+                                int32_t out_stride, int32_t *count, uint32_t machine_id, unsigned long long *held,
+                                const int32_t *aq_n, int32_t r_alive, void *stream)
+{
+    if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
+    hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
+                       out_stride, count, machine_id, held, aq_n, r_alive);
     return ok();
 }
 
@@ -1056,6 +1171,34 @@ int hkv_wl_regroup_aligned(const uint8_t *in, int32_t n_peers, int32_t width, co
     if (n_peers <= 0 || width <= 0 || elem_size % 8) return -1;
     hipLaunchKernelGGL(k_regroup_aligned, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, in, n_peers, width,
                        offsets, counts, elem_size, out, out_stride, out_count);
+    return ok();
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int hkv_wl_peer_acks_queue(hkv_table *t, const uint8_t *inv_out, const int32_t *inv_count, int32_t n_workers,
+                           int32_t inv_stride, uint32_t op_size, uint8_t *aq, uint32_t ack_size, int32_t q_stride,
+                           int32_t *aq_n, const int32_t *vq_n, int32_t *acnt, const uint8_t *peer_ids, int32_t n_peers,
+                           const unsigned long long *peer_ts, uint32_t round, void *stream)
+{
+    if (n_peers <= 0 || n_workers <= 0 || ack_size < kOpMetaSize || ack_size % 8 || q_stride <= 0) return -1;
+    TableView tv{};
+    if (peer_ts && table_view(t, &tv)) return -1;
+    hipLaunchKernelGGL(k_peer_acks_q, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, inv_out, inv_count, inv_stride,
+                       op_size, aq, ack_size, q_stride, aq_n, vq_n, acnt, peer_ids, n_peers, tv, peer_ts, round);
+    return ok();
+}
+
+int hkv_wl_vals_credit(uint8_t *aq, int32_t *aq_n, const int32_t *acnt, int32_t n_workers, int32_t q_stride,
+                       uint32_t ack_size, uint8_t *vq, int32_t *vq_n, int32_t vq_stride, uint8_t *out,
+                       int32_t *out_count, int32_t out_stride, int32_t v_credits, uint32_t machine_id,
+                       unsigned long long *overflow, void *stream)
+{
+    if (n_workers <= 0 || ack_size % 8 || vq_stride <= 0 || out_stride <= 0 || v_credits < 0) return -1;
+    hipLaunchKernelGGL(k_vals_credit, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, aq, aq_n, acnt, q_stride,
+                       ack_size, vq, vq_n, vq_stride, out, out_count, out_stride, v_credits, machine_id, overflow);
     return ok();
 }
 

@@ -51,6 +51,12 @@ _L.hkv_wl_gen_peer_round.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32,
                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, _P, _P]
 _L.hkv_wl_peer_ts.argtypes = [_P, _P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P,
                               ctypes.c_uint32, _P]
+_L.hkv_wl_marshal_invs_credits.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
+                                           _P, ctypes.c_uint32, _P, _P, ctypes.c_int32, _P]
+_L.hkv_wl_peer_acks_queue.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_uint32,
+                                      ctypes.c_int32, _P, _P, _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, _P]
+_L.hkv_wl_vals_credit.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_int32,
+                                  _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P]
 _L.hkv_wl_peer_ts_words.restype = ctypes.c_uint64
 _L.hkv_wl_peer_ts_words.argtypes = [_P]
 
@@ -98,7 +104,7 @@ class Round:
                  zipf: HkvZipf, write_permille: int = 200, rmw_permille: int = 0,
                  remote_per_peer: int = 50, trace_len: int = 8192, seed: int = 0x5EED,
                  virtual_peers: bool = True, max_steps: int = 64, retry_stalled: bool = False,
-                 fit_ack_stride: bool = True):
+                 fit_ack_stride: bool = True, val_credits: int | None = None):
         self.kvs = kvs
         self.W = n_workers
         self.mb = membership
@@ -124,7 +130,21 @@ class Round:
         self.ack_width = self.ack_stride
         # fit_ack_stride: each round's ACK slab is laid out at R x (largest per-worker INV count),
         # read back while the remote INV batch runs (about 20 ACKs per worker against 2C slots)
-        self.fit = fit_ack_stride and virtual_peers and self.R > 0
+        self.fit = fit_ack_stride and virtual_peers and self.R > 0 and val_credits is None
+        # val_credits: VAL messages each worker may send per round (the VAL channel's credits, which
+        # the virtual peers return every round). Then a worker's ACKs queue up in its row of `acks`
+        # (aq_n of them) and are polled only while it has no VALs outstanding (hermes_worker.c:479);
+        # VALs beyond the credits are carried (vq) and sent first next round; INVs whose ACKs wait
+        # in the queue keep their INV credits. None: every round applies every ACK and sends every
+        # VAL (credits that never bind).
+        self.V = val_credits
+        if val_credits is not None:
+            assert virtual_peers and val_credits >= 0
+            self.aq_n = torch.zeros(W, dtype=torch.int32, device=dev)
+            self.vq = torch.zeros(W * self.C * L.OP_META_SIZE, **u8)
+            self.vq_n = torch.zeros(W, dtype=torch.int32, device=dev)
+            self.val_overflow = torch.zeros(1, dtype=torch.int64, device=dev)
+            self.val_totals = torch.zeros(2, dtype=torch.int64, device=dev)  # VALs sent, gated worker-rounds
         self.maxc_h = torch.zeros(1, dtype=torch.int32, pin_memory=True) if self.fit else None
         self.maxc_ev = torch.cuda.Event() if self.fit else None
         self.acks = torch.zeros(W * self.ack_stride * self.ack_size, **u8)
@@ -196,6 +216,11 @@ class Round:
         self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb)
 
     def marshal_invs(self):
+        if self.V is not None:
+            check(_L.hkv_wl_marshal_invs_credits(_ptr(self.ops), self.W, self.LOCAL, self.op, _ptr(self.inv_out),
+                                                 self.C, _ptr(self.inv_count), self.machine_id, _ptr(self.held),
+                                                 _ptr(self.aq_n), max(self.alive, 1), _s()), "marshal_invs")
+            return
         check(_L.hkv_wl_marshal_invs_cap(_ptr(self.ops), self.W, self.LOCAL, self.op, _ptr(self.inv_out), self.C,
                                          _ptr(self.inv_count), self.machine_id, _ptr(self.held), _s()),
               "marshal_invs")
@@ -238,6 +263,26 @@ class Round:
         check(_L.hkv_wl_collect_vals(_ptr(self.acks), _ptr(self.ack_count), self.W, self.ack_width, self.ack_size,
                                      _ptr(self.val_out), self.ack_width, _ptr(self.val_count), self.machine_id,
                                      None, _s()), "collect_vals")
+
+    def peer_acks_queued(self, n_peers: int):
+        """The first n_peers virtual peers' ACKs to this round's INVs appended to each worker's ACK
+        queue; ack_count = the queue for workers without outstanding VALs, 0 for the others"""
+        if self.count_elems:
+            self.val_totals[1] += (self.vq_n > 0).sum()
+        check(_L.hkv_wl_peer_acks_queue(self.kvs.h, _ptr(self.inv_out), _ptr(self.inv_count), self.W, self.C, self.op,
+                                        _ptr(self.acks), self.ack_size, self.ack_stride, _ptr(self.aq_n),
+                                        _ptr(self.vq_n), _ptr(self.ack_count), _ptr(self.peer_t), n_peers,
+                                        _ptr(self.peer_ts), self.clock, _s()), "peer_acks_queue")
+
+    def vals_under_credits(self):
+        """Carried VALs first, then those of the writes this round's ACK batch completed, at most
+        val_credits per worker (val_out / val_count); the rest carried to the next round"""
+        check(_L.hkv_wl_vals_credit(_ptr(self.acks), _ptr(self.aq_n), _ptr(self.ack_count), self.W, self.ack_stride,
+                                    self.ack_size, _ptr(self.vq), _ptr(self.vq_n), self.C, _ptr(self.val_out),
+                                    _ptr(self.val_count), self.ack_stride, self.V, self.machine_id,
+                                    _ptr(self.val_overflow), _s()), "vals_credit")
+        if self.count_elems:
+            self.val_totals[0] += self.val_count.sum()
 
     def val_batch(self, vals: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None):
         self.kvs.batch(L.BatchType.vals, vals, n_batches, stride, L.OP_META_SIZE, self.mb, counts=counts)
@@ -282,7 +327,13 @@ class Round:
             if self.fit:   # the GPU is still on the INV batch: this wait leaves no gap on the stream
                 self.maxc_ev.synchronize()
                 m = min(int(self.maxc_h[0]), self.C)
-            if alive:
+            if alive and self.V is not None:
+                self.peer_acks_queued(alive)
+                timed("acks", lambda: self.ack_batch(stride=self.ack_stride))
+                if self.count_elems:
+                    self.elem_totals[1] += self.ack_count.sum()
+                self.vals_under_credits()
+            elif alive:
                 self.ack_width = max(1, m) * alive
                 self.virtual_peer_acks(alive)
                 timed("acks", self.ack_batch)
@@ -331,5 +382,10 @@ class Round:
 
     def stats(self) -> dict:
         c = self.counters[:5].cpu().tolist()
-        return {"committed": c[0], "misses": c[1], "writes_completed": c[2], "dropped": c[3], "rmw_aborts": c[4],
-                "invs_held": int(self.held.item())}
+        d = {"committed": c[0], "misses": c[1], "writes_completed": c[2], "dropped": c[3], "rmw_aborts": c[4],
+             "invs_held": int(self.held.item())}
+        if self.V is not None:
+            v = self.val_totals.cpu().tolist()
+            d.update(vals_sent=v[0], gated_worker_rounds=v[1], vals_carried=int(self.vq_n.sum().item()),
+                     acks_queued=int(self.aq_n.sum().item()), val_overflow=int(self.val_overflow.item()))
+        return d

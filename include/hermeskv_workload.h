@@ -162,6 +162,35 @@ int hkv_wl_collect_vals(uint8_t *d_acks, const int32_t *d_count, int32_t n_worke
                         uint32_t ack_size, uint8_t *d_val_out, int32_t C, int32_t *d_val_count,
                         uint32_t machine_id, unsigned long long *d_held, void *stream);
 
+/* ---- VAL credits and the outstanding-VAL gate (hermes_worker.c:479-503, wings.h:424-540, 862-916)
+ * Per worker: an ACK queue (d_aq rows of q_stride elements of ack_size bytes, d_aq_n queued) and a
+ * carried-VAL queue (d_vq rows of vq_stride 16-B VALs, d_vq_n carried).
+ *
+ * hkv_wl_marshal_invs_cap under INV credits: worker w may send at most
+ * out_stride - d_aq_n[w] / r_alive INVs (INVs whose ACKs still wait in its queue hold theirs). */
+int hkv_wl_marshal_invs_credits(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size,
+                                uint8_t *d_inv_out, int32_t out_stride, int32_t *d_inv_count, uint32_t machine_id,
+                                unsigned long long *d_held, const int32_t *d_aq_n, int32_t r_alive, void *stream);
+
+/* The virtual peers' ACKs (INV-aborts as in hkv_wl_peer_acks) appended to each worker's ACK queue;
+ * d_ack_count[w] = the whole queue when d_vq_n[w] == 0, else 0 (the worker does not poll ACKs
+ * while it has VALs outstanding). */
+int hkv_wl_peer_acks_queue(hkv_table *t, const uint8_t *d_inv_out, const int32_t *d_inv_count, int32_t n_workers,
+                           int32_t inv_stride, uint32_t op_size, uint8_t *d_aq, uint32_t ack_size, int32_t q_stride,
+                           int32_t *d_aq_n, const int32_t *d_vq_n, int32_t *d_ack_count, const uint8_t *d_peer_ids,
+                           int32_t n_peers, const unsigned long long *d_peer_ts, uint32_t round, void *stream);
+
+/* After the ACK batch over the queues (counts d_ack_count): per worker, the carried VALs and then
+ * the VALs of the queue's ST_LAST_ACK_SUCCESS elements (when it was applied), in that order; the
+ * first min(v_credits, out_stride) go to d_val_out row w (d_val_count), the rest are carried in
+ * d_vq. An applied queue's ACK/LAST_ACK/membership-change elements become ST_EMPTY and
+ * d_aq_n[w] = 0. VALs that fit nowhere are counted in *d_overflow (may be NULL; 0 when
+ * vq_stride >= the INV credits). */
+int hkv_wl_vals_credit(uint8_t *d_aq, int32_t *d_aq_n, const int32_t *d_ack_count, int32_t n_workers,
+                       int32_t q_stride, uint32_t ack_size, uint8_t *d_vq, int32_t *d_vq_n, int32_t vq_stride,
+                       uint8_t *d_val_out, int32_t *d_val_count, int32_t out_stride, int32_t v_credits,
+                       uint32_t machine_id, unsigned long long *d_overflow, void *stream);
+
 /* Packed slabs of a replica group (one contiguous slab per rank instead of [W][C] rows):
  * rows [n_rows][C] x elem_size with d_counts[n_rows] -> d_packed, row w at d_offsets[w];
  * d_offsets[n_rows] = the total (d_offsets has n_rows + 1 entries) */

@@ -125,6 +125,76 @@ def test_membership_change_round_mirrored(machines):
     assert g.take_error_flags() == 0
 
 
+@pytest.mark.parametrize("credits,cfg3", [(3, False), (6, True)])
+def test_val_credits_round_mirrored(credits, cfg3):
+    """VALs under credits and the outstanding-VAL gate (hermes_worker.c:479-503).
+    With a few VAL credits per round, workers carry VALs, stop polling their ACKs while they do
+    (the ACKs wait in their queue, holding INV credits) and send the carried VALs first. Every
+    batch launch is mirrored into the oracle; every round's VALs are checked against a model of
+    the queues (carried first, then the applied queue's LAST_ACK_SUCCESS elements in queue order,
+    at most `credits` sent), and every VAL produced is sent exactly once or still carried."""
+    from hermes_amd.kvs import HermesKV
+    from hermes_amd.workload import Round, zipf_params
+    n_keys, bkts = 60_000, 1 << 16
+    cap = 1 << 25 if cfg3 else 1 << 23
+    g = HermesKV(n_keys, bkts, cap, machine_id=0, rmw=cfg3, big_objects=cfg3, extra_cache_lines=4 if cfg3 else 0)
+    o = OracleKVS(bkts, cap, 0, cfg3, cfg3, 4 if cfg3 else 0)
+    o.populate(n_keys, g.sizes.kvs_value)
+    m = Mirror(g, o, "val credits round")
+    W = 40
+    r = Round(g, W, L.membership(3, 0), [1, 2], zipf_params(n_keys, 0.99), 500 if cfg3 else 200,
+              500 if cfg3 else 0, seed=0x5EED, max_steps=8, trace_len=1024, val_credits=credits)
+    asz, q = r.ack_size, r.ack_stride
+    seen = {"gated": 0, "carried_rounds": 0, "produced": 0}
+    vals_credit = r.vals_under_credits
+
+    def checked_vals():
+        torch.cuda.synchronize()
+        carried = r.vq.view(W, r.C, 16).cpu().numpy().copy()
+        vq_n = r.vq_n.cpu().numpy().copy()
+        acnt = r.ack_count.cpu().numpy().copy()
+        aq = r.acks.view(W, q, asz).cpu().numpy().copy()
+        vals_credit()
+        torch.cuda.synchronize()
+        out = r.val_out.view(W, -1, 16).cpu().numpy()
+        vc, vq_n2 = r.val_count.cpu().numpy(), r.vq_n.cpu().numpy()
+        vq2, aq_n2 = r.vq.view(W, r.C, 16).cpu().numpy(), r.aq_n.cpu().numpy()
+        for w in range(W):
+            src = [carried[w, j] for j in range(vq_n[w])]
+            assert acnt[w] == 0 or vq_n[w] == 0, "ACKs applied while VALs were outstanding"
+            new = [j for j in range(acnt[w]) if aq[w, j, 8] == int(L.Resp.LAST_ACK_SUCCESS)]
+            seen["produced"] += len(new)
+            for j in new:
+                v = aq[w, j, :16].copy()
+                v[8], v[9] = int(L.Op.VAL), 0
+                src.append(v)
+            send = min(len(src), credits)
+            assert vc[w] == send and vq_n2[w] == len(src) - send, (w, vc[w], vq_n2[w], len(src))
+            for j in range(send):
+                assert np.array_equal(out[w, j], src[j]), (w, j)
+            for j in range(len(src) - send):
+                assert np.array_equal(vq2[w, j], src[send + j]), (w, j)
+            if acnt[w]:
+                assert aq_n2[w] == 0
+            seen["gated"] += int(vq_n[w] > 0)
+        seen["carried_rounds"] += int((vq_n2 > 0).any())
+    r.vals_under_credits = checked_vals
+    steps = 6
+    for _ in range(steps):
+        r.step()
+    torch.cuda.synchronize()
+    assert m.launches == steps * 4
+    st = r.stats()
+    assert g.take_error_flags() == 0
+    assert seen["gated"] > 0 and seen["carried_rounds"] > 0, seen
+    assert st["gated_worker_rounds"] == seen["gated"], (st, seen)
+    assert st["vals_sent"] + st["vals_carried"] == seen["produced"], (st, seen)
+    assert st["val_overflow"] == 0 and st["writes_completed"] > 0, st
+    if not cfg3:   # queued ACKs held INV credits back (cfg3's slots rarely bind: most ops stall on RMW conflicts)
+        assert st["invs_held"] > 0, st
+    assert m.codes[(int(L.BatchType.acks), "out8", int(L.Resp.LAST_ACK_SUCCESS))] == seen["produced"]
+
+
 # PUT/RMW/REPLAY_SUCCESS, IN_PROGRESS_PUT/RMW/REPLAY, PUT/RMW/REPLAY_COMPLETE_SEND_VALS, membership
 # change: a fresh-batch refill keeps these (their keys point at the slot through op_buffer_index)
 IN_FLIGHT = (122, 135, 123, 143, 148, 144, 133, 149, 147, 118)

@@ -53,6 +53,7 @@ enum { kCtrFbM = 1, kCtrFbL = 2 };  // fallback: mem cursor, list length
 struct BatchArgs {
     uint8_t *elems;
     const int32_t *counts;
+    const int32_t *offsets;      // packed INV/VAL launches (counts NULL, stride = n): batch offsets
     const uint8_t *index;
     uint8_t *log;
     uint8_t *rw;
@@ -349,7 +350,18 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                 kk = h.a;
                 hh = h.b;
                 if (skip_elem_os(a.type, (uint8_t)hh, (uint8_t)(hh >> 8))) {
-                    if (a.type == kInvs && a.ns_idx) atomicMax(&a.ns_idx[b], idx);
+                    if (a.type == kInvs && a.ns_idx) {
+                        if (a.offsets) {  // packed: the batch holding gi (rare: membership-change INVs)
+                            int lo = 0, hi = a.n_batches - 1;
+                            while (lo < hi) {
+                                const int mid = (lo + hi + 1) >> 1;
+                                if (a.offsets[mid] <= gi[k]) lo = mid; else hi = mid - 1;
+                            }
+                            atomicMax(&a.ns_idx[lo], (int32_t)(gi[k] - a.offsets[lo]));
+                        } else {
+                            atomicMax(&a.ns_idx[b], idx);
+                        }
+                    }
                 } else {
                     p = 1;
                 }
@@ -1434,12 +1446,13 @@ int launch_small(const BatchArgs &a0, hipStream_t s)
 }
 
 __global__ void k_node_suspected(const uint8_t *elems, const int32_t *ns_idx, int32_t *out, int32_t n_batches,
-                                 int32_t stride, int32_t esz)
+                                 int32_t stride, int32_t esz, const int32_t *offsets)
 {
     const int32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= n_batches) return;
     const int32_t i = ns_idx[b];
-    if (i >= 0) out[b] = elems[((int64_t)b * stride + i) * esz + kOpValueOff];
+    const int64_t base = offsets ? (int64_t)offsets[b] : (int64_t)b * stride;
+    if (i >= 0) out[b] = elems[(base + i) * esz + kOpValueOff];
 }
 
 // ------------------------------------------------------------------ host side
@@ -1480,6 +1493,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     BatchArgs a;
     a.elems = bl.elems;
     a.counts = bl.counts;
+    a.offsets = bl.offsets;
     a.index = bl.index;
     a.log = bl.log;
     a.rw = bl.rw;
@@ -1593,7 +1607,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     }
     if (bl.type == kInvs && bl.ns_idx && bl.node_suspected) {
         hipLaunchKernelGGL(k_node_suspected, dim3((bl.n_batches + 255) / 256), dim3(256), 0, s, bl.elems, bl.ns_idx,
-                           bl.node_suspected, bl.n_batches, bl.stride, bl.esz);
+                           bl.node_suspected, bl.n_batches, bl.stride, bl.esz, bl.offsets);
         if (hipGetLastError() != hipSuccess) return -4;
     }
     return 0;

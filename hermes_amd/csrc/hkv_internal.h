@@ -14,6 +14,7 @@ struct BatchLaunch {
     Geometry g;
     uint8_t *elems;
     const int32_t *counts;
+    const int32_t *offsets;      // packed INV/VAL launches: n_batches + 1 batch offsets (counts NULL)
     const uint8_t *index;
     uint8_t *log;
     uint8_t *rw;

@@ -374,7 +374,8 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
 {
     if (!t || !d) return fail(-1, "null argument");
     if (d->type < 0 || d->type > 4) return fail(-1, "bad batch type %d", d->type);
-    if (d->n_batches < 0 || d->stride <= 0) return fail(-1, "bad batch geometry");
+    const bool packed = (d->flags & HKV_BATCH_PACKED) != 0;
+    if (d->n_batches < 0 || d->stride < 0 || (d->stride == 0 && !packed)) return fail(-1, "bad batch geometry");
     if (d->elem_size < kOpMetaSize || (d->elem_size & 7)) return fail(-1, "elem_size %u must be >= 16 and a multiple of 8", d->elem_size);
     // ACK batches of an RMW table carry INV-aborts, which hermes_exec_inv applies with their value
     // (hermesKV.c:877-890): they need op-sized elements, as the reference worker sends them
@@ -385,8 +386,12 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
         return fail(-1, "elem_size %u too small for %u-byte values", d->elem_size, t->geo.st_value);
     if (d->type == kLocal && d->stride > 255)
         return fail(-1, "local batches hold at most 255 ops (uint8 op_buffer_index)");
-    int64_t n = (int64_t)d->n_batches * d->stride;
-    if (n == 0) return 0;
+    // HKV_BATCH_PACKED: d_counts holds n_batches + 1 element offsets and stride the total
+    if (packed && d->type != kInvs && d->type != kVals)
+        return fail(-1, "HKV_BATCH_PACKED applies to INV and VAL batches");
+    if (packed && !d->d_counts) return fail(-1, "HKV_BATCH_PACKED needs the batch offsets in d_counts");
+    int64_t n = packed ? (int64_t)d->stride : (int64_t)d->n_batches * d->stride;
+    if (n == 0 || d->n_batches == 0) return 0;
     if ((uintptr_t)d->d_elems & 15) return fail(-1, "d_elems must be 16-byte aligned");
     if (n > 0x7FFFFFFFll) return fail(-1, "too many elements in one launch");
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream, as in every HIP API
@@ -408,7 +413,8 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     memset(&bl, 0, sizeof bl);
     bl.g = t->geo;
     bl.elems = d->d_elems;
-    bl.counts = d->d_counts;
+    bl.counts = packed ? nullptr : d->d_counts;
+    bl.offsets = packed ? d->d_counts : nullptr;
     bl.index = t->d_index;
     bl.log = t->d_log;
     bl.rw = d->type == kAcks ? d->d_rw : nullptr;
@@ -433,7 +439,8 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.type = d->type;
     bl.g_membership = d->membership[1];
     bl.w_ack_init = d->membership[2];
-    bl.path = (d->flags & HKV_BATCH_ENGINE) ? kPathEngine : (d->flags & HKV_BATCH_SMALL) ? kPathSmall : kPathAuto;
+    bl.path = (d->flags & HKV_BATCH_ENGINE) || packed ? kPathEngine
+            : (d->flags & HKV_BATCH_SMALL) ? kPathSmall : kPathAuto;
     TRACE("batch_async type=%d n=%lld", d->type, (long long)n);
     rc = launch_batch(bl, s);
     if (rc) return fail(rc, "batch launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));

@@ -79,6 +79,7 @@ def sized_geometry(num_keys: int, sizes: L.Sizes = L.DEFAULT) -> tuple[int, int]
 
 BATCH_ENGINE = 1   # hkv_batch_desc.flags (include/hermeskv.h): the multi-kernel engine
 BATCH_SMALL = 2    # the single-workgroup kernel (launches of at most 4096 elements)
+BATCH_PACKED = 4   # INV / VAL batches back to back, d_counts = n_batches + 1 offsets
 
 
 class HermesKV:
@@ -152,11 +153,14 @@ class HermesKV:
     def batch(self, btype: int, elems: torch.Tensor, n_batches: int, stride: int, elem_size: int,
               membership: bytes, counts: torch.Tensor | None = None, rw: torch.Tensor | None = None,
               rw_stride_bytes: int = 0, node_suspected: torch.Tensor | None = None,
-              stream: torch.cuda.Stream | None = None) -> None:
+              stream: torch.cuda.Stream | None = None, offsets: torch.Tensor | None = None) -> None:
         """Apply n_batches batches of one type, concatenated in `elems` (uint8, on the GPU),
-        in concatenation order, asynchronously on `stream` (default: torch's current)."""
+        in concatenation order, asynchronously on `stream` (default: torch's current).
+        offsets (INV / VAL batches): the batches stored back to back, batch b at elements
+        [offsets[b], offsets[b+1]); `stride` is then the total (HKV_BATCH_PACKED)."""
         assert elems.is_cuda and elems.dtype == torch.uint8
-        assert elems.numel() >= n_batches * stride * elem_size
+        total = stride if offsets is not None else n_batches * stride
+        assert elems.numel() >= total * elem_size
         d = HkvBatchDesc()
         d.type = int(btype)
         d.n_batches = int(n_batches)
@@ -164,6 +168,11 @@ class HermesKV:
         d.elem_size = int(elem_size)
         d.flags = self.default_flags
         d.d_elems = elems.data_ptr()
+        if offsets is not None:
+            assert counts is None and offsets.is_cuda and offsets.dtype == torch.int32
+            assert offsets.numel() >= n_batches + 1
+            d.flags |= BATCH_PACKED
+            d.d_counts = offsets.data_ptr()
         if counts is not None:
             assert counts.is_cuda and counts.dtype == torch.int32 and counts.numel() >= n_batches
             d.d_counts = counts.data_ptr()
@@ -181,9 +190,23 @@ class HermesKV:
 
     def batch_host(self, btype: int, elems: np.ndarray, membership: bytes, rw: np.ndarray | None = None,
                    n_batches: int = 1, stride: int | None = None, counts: np.ndarray | None = None,
-                   rw_stride_elems: int = 0, node_suspected: np.ndarray | None = None) -> None:
-        """Round-trip numpy arrays through the device path (parity tests)."""
+                   rw_stride_elems: int = 0, node_suspected: np.ndarray | None = None,
+                   offsets: np.ndarray | None = None) -> None:
+        """Round-trip numpy arrays through the device path (parity tests). offsets: packed INV /
+        VAL batches (HKV_BATCH_PACKED), batch b = elems[offsets[b]:offsets[b+1]]."""
         dev = torch.device("cuda", self.device)
+        if offsets is not None:
+            t = torch.from_numpy(elems.view(np.uint8).reshape(-1).copy()).to(dev)
+            to = torch.from_numpy(np.ascontiguousarray(offsets, dtype=np.int32)).to(dev)
+            tn = torch.from_numpy(np.ascontiguousarray(node_suspected, dtype=np.int32)).to(dev) \
+                if node_suspected is not None else None
+            self.batch(btype, t, n_batches, len(elems), elems.dtype.itemsize, membership, node_suspected=tn,
+                       offsets=to)
+            torch.cuda.synchronize(dev)
+            elems.view(np.uint8).reshape(-1)[:] = t.cpu().numpy()
+            if node_suspected is not None:
+                node_suspected[:] = tn.cpu().numpy()
+            return
         stride = len(elems) // n_batches if stride is None else stride
         esz = elems.dtype.itemsize
         t = torch.from_numpy(elems.view(np.uint8).reshape(-1).copy()).to(dev)

@@ -57,6 +57,7 @@ _L.hkv_wl_peer_acks_queue.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32
                                       ctypes.c_int32, _P, _P, _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_vals_credit.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_int32,
                                   _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P]
+_L.hkv_wl_pack_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_peer_ts_words.restype = ctypes.c_uint64
 _L.hkv_wl_peer_ts_words.argtypes = [_P]
 
@@ -104,7 +105,7 @@ class Round:
                  zipf: HkvZipf, write_permille: int = 200, rmw_permille: int = 0,
                  remote_per_peer: int = 50, trace_len: int = 8192, seed: int = 0x5EED,
                  virtual_peers: bool = True, max_steps: int = 64, retry_stalled: bool = False,
-                 fit_ack_stride: bool = True, val_credits: int | None = None):
+                 fit_ack_stride: bool = True, val_credits: int | None = None, pack_remote: bool = True):
         self.kvs = kvs
         self.W = n_workers
         self.mb = membership
@@ -176,6 +177,8 @@ class Round:
         self.peer_ts = None
         if virtual_peers and self.R and kvs.rmw:
             self.peer_ts = torch.zeros(int(_L.hkv_wl_peer_ts_words(kvs.h)), dtype=torch.int64, device=dev)
+        self.pack_remote = virtual_peers and self.R > 0 and pack_remote
+        self.remote_packed = []        # per round index: (INVs, VALs, batch offsets, total, [total])
         self.drops = []                # peers dropped from the membership (membership_change)
         self.alive = self.R            # live peers: the first `alive` slots of the remote slabs
         self._counts = {}
@@ -203,6 +206,21 @@ class Round:
             self.remote_counts.append([None] + [cum[:, n - 1].contiguous() for n in range(1, R + 1)])
             self.remote_inv.append(ri)
             self.remote_val.append(rv)
+            if self.pack_remote:
+                # the same elements back to back (HKV_BATCH_PACKED): rounds where every peer is live
+                # launch over the live INVs / VALs only, not the slabs' empty slots
+                full = self.remote_counts[-1][R]
+                off = torch.zeros(W + 1, dtype=torch.int32, device=dev)
+                torch.cumsum(full, 0, dtype=torch.int32, out=off[1:])
+                total = int(off[W].item())
+                pi = torch.empty(max(total, 1) * self.op, **u8)
+                pv = torch.empty(max(total, 1) * L.OP_META_SIZE, **u8)
+                check(_L.hkv_wl_pack_rows(_ptr(ri), _ptr(full), W, self.rstride, self.op, _ptr(pi), _ptr(off), _s()),
+                      "pack remote invs")
+                check(_L.hkv_wl_pack_rows(_ptr(rv), _ptr(full), W, self.rstride, L.OP_META_SIZE, _ptr(pv), _ptr(off),
+                                          _s()), "pack remote vals")
+                one = torch.full((1,), total, dtype=torch.int32, device=dev)
+                self.remote_packed.append((pi, pv, off, total, one))
         del scratch
 
     # -- pieces of one round
@@ -239,8 +257,14 @@ class Round:
                                 _ptr(self.remote_counts[k][n_peers]), self.W, self.rstride, self.op,
                                 _ptr(self.peer_ts), self.clock, _s()), "peer_ts")
 
-    def inv_batch(self, invs: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None):
-        self.kvs.batch(L.BatchType.invs, invs, n_batches, stride, self.op, self.mb, counts=counts)
+    def peer_timestamps_packed(self, k: int):
+        pi, pv, _, total, one = self.remote_packed[k]
+        check(_L.hkv_wl_peer_ts(self.kvs.h, _ptr(pi), _ptr(pv), _ptr(one), 1, total, self.op, _ptr(self.peer_ts),
+                                self.clock, _s()), "peer_ts")
+
+    def inv_batch(self, invs: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None,
+                  offsets: torch.Tensor | None = None):
+        self.kvs.batch(L.BatchType.invs, invs, n_batches, stride, self.op, self.mb, counts=counts, offsets=offsets)
 
     def marshal_acks(self, invs: torch.Tensor, n: int, out: torch.Tensor):
         check(_L.hkv_wl_marshal_acks(_ptr(invs), n, self.op, _ptr(out), self.ack_size, self.machine_id, _s()),
@@ -284,8 +308,10 @@ class Round:
         if self.count_elems:
             self.val_totals[0] += self.val_count.sum()
 
-    def val_batch(self, vals: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None):
-        self.kvs.batch(L.BatchType.vals, vals, n_batches, stride, L.OP_META_SIZE, self.mb, counts=counts)
+    def val_batch(self, vals: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None,
+                  offsets: torch.Tensor | None = None):
+        self.kvs.batch(L.BatchType.vals, vals, n_batches, stride, L.OP_META_SIZE, self.mb, counts=counts,
+                       offsets=offsets)
 
     # -- a whole round with virtual peers
     def step(self, events: dict | None = None, timed_batches=("local", "invs", "acks", "vals"),
@@ -309,8 +335,13 @@ class Round:
             assert self.virtual and self.alive and drop == self.peers[self.alive - 1], "drop the last live peer"
         sent = self.alive                          # peers whose INVs this round applies
         alive = self.alive - (drop is not None)    # peers that answer them (ACKs) and send VALs
+        # every peer live and none failing this round: the packed slabs (same elements, same order)
+        packed = self.pack_remote and sent == self.R and alive == self.R
         if self.R and sent:
-            self.peer_timestamps(k, sent)
+            if packed:
+                self.peer_timestamps_packed(k)
+            else:
+                self.peer_timestamps(k, sent)
         timed("local", self.local_batch)
         self.marshal_invs()
         if self.count_elems:
@@ -321,8 +352,13 @@ class Round:
         if self.R:
             ri, rv = self.remote_inv[k], self.remote_val[k]
             ic = self._slot_counts(k, sent)
-            timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride, counts=ic))
-            self.marshal_acks(ri, self.W * self.rstride, self.ack_out)
+            if packed:
+                pi, pv, off, total, _ = self.remote_packed[k]
+                timed("invs", lambda: self.inv_batch(pi, self.W, total, offsets=off))
+                self.marshal_acks(pi, total, self.ack_out)
+            else:
+                timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride, counts=ic))
+                self.marshal_acks(ri, self.W * self.rstride, self.ack_out)
             m = self.C
             if self.fit:   # the GPU is still on the INV batch: this wait leaves no gap on the stream
                 self.maxc_ev.synchronize()
@@ -342,7 +378,10 @@ class Round:
                 self.collect_vals()
             # a dropped peer sent its INVs but fails before its VALs
             vc = self._slot_counts(k, alive)
-            timed("vals", lambda: self.val_batch(rv, self.W, self.rstride, counts=vc))
+            if packed:
+                timed("vals", lambda: self.val_batch(pv, self.W, total, offsets=off))
+            else:
+                timed("vals", lambda: self.val_batch(rv, self.W, self.rstride, counts=vc))
             if self.count_elems:
                 self.elem_totals[0] += ic.sum()
                 if alive:

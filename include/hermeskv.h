@@ -102,7 +102,8 @@ typedef struct hkv_config {
 typedef struct hkv_table hkv_table;
 
 /* One batch launch: n_batches batches of the same type, batch b owning elements
- * [b*stride, b*stride + counts[b]) of d_elems, applied in concatenation order. */
+ * [b*stride, b*stride + counts[b]) of d_elems (HKV_BATCH_PACKED: see below), applied in
+ * concatenation order. */
 typedef struct hkv_batch_desc {
     int32_t  type;              /* enum hermes_batch_type_t */
     int32_t  n_batches;
@@ -121,6 +122,10 @@ typedef struct hkv_batch_desc {
  * kernel and larger ones on the multi-kernel engine; both give the same bytes. */
 #define HKV_BATCH_ENGINE 1u     /* always the multi-kernel engine */
 #define HKV_BATCH_SMALL  2u     /* the single-workgroup kernel (launches of at most 4096 elements) */
+/* INV and VAL batches stored back to back: d_counts holds n_batches + 1 element offsets (batch b is
+ * elements [d_counts[b], d_counts[b+1]) of d_elems) and stride is the total, d_counts[n_batches].
+ * Same results as the row layout; no empty slots to launch over. */
+#define HKV_BATCH_PACKED 4u
 
 int  hkv_abi_version(void);
 const char *hkv_last_error(void);

@@ -94,8 +94,10 @@ class Mirror:
             self.codes[(int(btype), tag, x)] += c
 
     def batch(self, btype, elems, n_batches, stride, elem_size, membership, counts=None, rw=None,
-              rw_stride_bytes=0, node_suspected=None, stream=None):
+              rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None):
         import torch
+        if offsets is not None:
+            return self._packed(btype, elems, n_batches, stride, elem_size, membership, offsets, stream)
         torch.cuda.synchronize()
         n = n_batches * stride * elem_size
         vt = np.dtype((np.void, elem_size))
@@ -126,6 +128,42 @@ class Mirror:
             e = self.g.sizes.entry
             pytest.fail(f"{what}: log differs in entries {np.unique(bad // e)[:8]}, "
                         f"bytes-in-entry {np.unique(bad % e)[:16]}")
+        assert np.array_equal(self.g.index_bytes(), self.o.index_bytes()), f"{what}: index differs"
+        assert self.g.take_error_flags() == 0, f"{what}: device consistency flags"
+        self.launches += 1
+
+    def _packed(self, btype, elems, n_batches, total, elem_size, membership, offsets, stream):
+        """A packed (HKV_BATCH_PACKED) INV / VAL launch: the oracle applies the same batches laid
+        out in rows; the device's packed output must equal the oracle's rows packed again."""
+        import torch
+        torch.cuda.synchronize()
+        off = offsets[: n_batches + 1].cpu().numpy().astype(np.int64)
+        cnt = np.diff(off).astype(np.int32)
+        assert off[0] == 0 and off[-1] == total and (cnt >= 0).all()
+        width = max(int(cnt.max()), 1) if n_batches else 1
+        flat = elems[: total * elem_size].cpu().numpy().copy().reshape(total, elem_size)
+        rows = np.zeros((n_batches, width, elem_size), np.uint8)
+        pos = np.arange(width)[None, :] < cnt[:, None]
+        rows[pos] = flat
+        self._count(btype, "in8", 8, rows.reshape(-1), n_batches, width, elem_size, cnt)
+        self._orig(btype, elems, n_batches, total, elem_size, membership, stream=stream, offsets=offsets)
+        torch.cuda.synchronize()
+        e_in = rows.reshape(-1).view(np.dtype((np.void, elem_size))).copy()
+        self.o.batch_multi(int(btype), e_in, n_batches, width, cnt, membership, None, 0)
+        want = e_in.view(np.uint8).reshape(n_batches, width, elem_size)[pos]
+        got = elems[: total * elem_size].cpu().numpy().reshape(total, elem_size)
+        what = f"{self.name} launch {self.launches} type {int(btype)} (packed)"
+        grow = np.zeros_like(rows)
+        grow[pos] = got
+        self._count(btype, "out8", 8, grow.reshape(-1), n_batches, width, elem_size, cnt)
+        self._count(btype, "out9", 9, grow.reshape(-1), n_batches, width, elem_size, cnt)
+        if not np.array_equal(got, want):
+            bad = np.nonzero((got != want).any(axis=1))[0]
+            pytest.fail(f"{what}: elements differ at {len(bad)} elements, first {bad[:8]}")
+        gl, ol = self.g.log_bytes(), self.o.log_bytes()[: self.g.cfg.log_cap]
+        if not np.array_equal(gl, ol):
+            bad = np.nonzero(gl != ol)[0]
+            pytest.fail(f"{what}: log differs in entries {np.unique(bad // self.g.sizes.entry)[:8]}")
         assert np.array_equal(self.g.index_bytes(), self.o.index_bytes()), f"{what}: index differs"
         assert self.g.take_error_flags() == 0, f"{what}: device consistency flags"
         self.launches += 1

@@ -166,9 +166,19 @@ CONFIGS = [
 
 
 def _run_both(g, o, btype, elems_g, elems_o, mb, n_batches, stride, counts, rw_g=None, rw_o=None,
-              rw_stride=0, ns_g=None, ns_o=None):
-    g.batch_host(btype, elems_g, mb, rw=rw_g, n_batches=n_batches, stride=stride, counts=counts,
-                 rw_stride_elems=rw_stride, node_suspected=ns_g)
+              rw_stride=0, ns_g=None, ns_o=None, packed=False):
+    """packed: the device gets the batches back to back (HKV_BATCH_PACKED), the oracle in rows;
+    elems_g then holds the rows again afterwards (empty slots untouched)"""
+    if packed:
+        cnt = np.full(n_batches, stride, np.int32) if counts is None else counts
+        live = (np.arange(stride)[None, :] < cnt[:, None]).reshape(-1)
+        off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int32)
+        flat = elems_g[live].copy()
+        g.batch_host(btype, flat, mb, n_batches=n_batches, node_suspected=ns_g, offsets=off)
+        elems_g[live] = flat
+    else:
+        g.batch_host(btype, elems_g, mb, rw=rw_g, n_batches=n_batches, stride=stride, counts=counts,
+                     rw_stride_elems=rw_stride, node_suspected=ns_g)
     o.batch_multi(btype, elems_o, n_batches, stride, counts, mb, rw=rw_o, rw_stride_elems=rw_stride,
                   node_suspected=ns_o)
 
@@ -205,7 +215,7 @@ def test_random_protocol_rounds(cfg):
         ns_g = np.full(W, -1, np.int32)
         ns_o = ns_g.copy()
         inv_o = gen.bytecopy(inv)
-        _run_both(g, o, L.BatchType.invs, inv, inv_o, mb, W, M, counts, ns_g=ns_g, ns_o=ns_o)
+        _run_both(g, o, L.BatchType.invs, inv, inv_o, mb, W, M, counts, ns_g=ns_g, ns_o=ns_o, packed=rnd % 2 == 1)
         assert_elems_equal(inv, inv_o, f"round {rnd} invs")
         np.testing.assert_array_equal(ns_g, ns_o)
         assert_tables_equal(g, o, f"round {rnd} invs")
@@ -220,7 +230,7 @@ def test_random_protocol_rounds(cfg):
         # vals
         val = gen.vals(rng, pool, W * M, sizes, rmw, tsp)
         val_o = gen.bytecopy(val)
-        _run_both(g, o, L.BatchType.vals, val, val_o, mb, W, M, None)
+        _run_both(g, o, L.BatchType.vals, val, val_o, mb, W, M, None, packed=rnd % 3 == 1)
         assert_elems_equal(val, val_o, f"round {rnd} vals")
         assert_tables_equal(g, o, f"round {rnd} vals")
         # completion after a membership change
@@ -419,7 +429,7 @@ def test_inv_direct_path_edge_cases(big):
         ns_g = np.full(W, -1, np.int32)
         ns_o = ns_g.copy()
         inv_o = gen.bytecopy(inv)
-        _run_both(g, o, L.BatchType.invs, inv, inv_o, mb, W, M, counts, ns_g=ns_g, ns_o=ns_o)
+        _run_both(g, o, L.BatchType.invs, inv, inv_o, mb, W, M, counts, ns_g=ns_g, ns_o=ns_o, packed=rnd % 2 == 1)
         assert_elems_equal(inv, inv_o, f"round {rnd} invs")
         np.testing.assert_array_equal(ns_g, ns_o)
         assert_tables_equal(g, o, f"round {rnd} invs")

@@ -174,11 +174,34 @@ __device__ __forceinline__ Ctx make_ctx(const BatchArgs &a)
     return c;
 }
 
+// The batch holding element i and its first element: i / stride, or for a packed launch the last
+// batch whose offset is <= i (empty batches share their successor's offset)
+__device__ __forceinline__ int32_t batch_of(const BatchArgs &a, int64_t i, int64_t &start)
+{
+    if (!a.offsets) {
+        const int32_t b = (int32_t)(i / a.stride);
+        start = (int64_t)b * a.stride;
+        return b;
+    }
+    int lo = 0, hi = a.n_batches - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.offsets[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    start = a.offsets[lo];
+    return lo;
+}
+
 __device__ __forceinline__ void elem_at(const BatchArgs &a, uint32_t i, uint8_t *&x, uint8_t &idx, Ctx &c)
 {
-    const uint32_t b = i / (uint32_t)a.stride;
-    idx = (uint8_t)(i - b * (uint32_t)a.stride);
-    c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
+    c.rw = nullptr;
+    idx = 0;
+    if (a.rw || !a.offsets) {  // packed INV / VAL elements need neither (exec_inv / exec_val)
+        int64_t start;
+        const int32_t b = batch_of(a, i, start);
+        idx = (uint8_t)(i - start);
+        c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
+    }
     x = a.elems + (int64_t)i * a.esz;
 }
 
@@ -351,16 +374,9 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                 hh = h.b;
                 if (skip_elem_os(a.type, (uint8_t)hh, (uint8_t)(hh >> 8))) {
                     if (a.type == kInvs && a.ns_idx) {
-                        if (a.offsets) {  // packed: the batch holding gi (rare: membership-change INVs)
-                            int lo = 0, hi = a.n_batches - 1;
-                            while (lo < hi) {
-                                const int mid = (lo + hi + 1) >> 1;
-                                if (a.offsets[mid] <= gi[k]) lo = mid; else hi = mid - 1;
-                            }
-                            atomicMax(&a.ns_idx[lo], (int32_t)(gi[k] - a.offsets[lo]));
-                        } else {
-                            atomicMax(&a.ns_idx[b], idx);
-                        }
+                        int64_t start;  // packed: a search, for the rare membership-change INVs only
+                        const int32_t bb = a.offsets ? batch_of(a, gi[k], start) : b;
+                        atomicMax(&a.ns_idx[bb], a.offsets ? (int32_t)(gi[k] - start) : idx);
                     }
                 } else {
                     p = 1;
@@ -696,7 +712,8 @@ __global__ __launch_bounds__(256) void k_ack_resolve(BatchArgs a)
         else if (st0 != kValid && st0 != kInvalid && a.error_flags) atomicOr(a.error_flags, 2u);
         m_set_obi(m, kObiEmpty);
         if (a.rw) {
-            const int64_t b = i / a.stride;
+            int64_t start;
+            const int64_t b = batch_of(a, i, start);
             uint8_t *rw = a.rw + b * a.rw_stride + (size_t)obi0 * a.g.op_size;
             const uint8_t oc = rw[8];
             if (oc == kOpGet) rw[9] = kNew;

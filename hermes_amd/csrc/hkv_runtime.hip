@@ -387,8 +387,8 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     if (d->type == kLocal && d->stride > 255)
         return fail(-1, "local batches hold at most 255 ops (uint8 op_buffer_index)");
     // HKV_BATCH_PACKED: d_counts holds n_batches + 1 element offsets and stride the total
-    if (packed && d->type != kInvs && d->type != kVals)
-        return fail(-1, "HKV_BATCH_PACKED applies to INV and VAL batches");
+    if (packed && d->type != kInvs && d->type != kVals && d->type != kAcks)
+        return fail(-1, "HKV_BATCH_PACKED applies to INV, ACK and VAL batches");
     if (packed && !d->d_counts) return fail(-1, "HKV_BATCH_PACKED needs the batch offsets in d_counts");
     int64_t n = packed ? (int64_t)d->stride : (int64_t)d->n_batches * d->stride;
     if (n == 0 || d->n_batches == 0) return 0;

@@ -437,14 +437,17 @@ __global__ __launch_bounds__(256) void k_regroup(const uint8_t *in, const int32_
 // [W][C]; the ACK elements become ST_EMPTY (hermes_worker.c:112-160)
 __global__ __launch_bounds__(256) void k_collect_vals(uint8_t *acks, const int32_t *count, int32_t stride,
                                                       uint32_t ack_size, uint8_t *out, int32_t C, int32_t *out_count,
-                                                      uint32_t machine_id, unsigned long long *held)
+                                                      uint32_t machine_id, unsigned long long *held,
+                                                      const int32_t *offsets)
 {
     const int64_t w = blockIdx.x;
-    const int n = count[w];
+    // rows: worker w's ACKs at w * stride, count[w] of them; packed: [offsets[w], offsets[w+1])
+    const int n = offsets ? offsets[w + 1] - offsets[w] : count[w];
+    const int64_t row = offsets ? (int64_t)offsets[w] : w * stride;
     int base = 0;
     for (int j0 = 0; j0 < n; j0 += 256) {
         const int j = j0 + (int)threadIdx.x;
-        uint8_t *x = acks + (w * stride + j) * (int64_t)ack_size;
+        uint8_t *x = acks + (row + j) * (int64_t)ack_size;
         const uint8_t oc = j < n ? x[8] : 0;
         const bool send = j < n && oc == kLastAckSuccess;
         int total;
@@ -788,24 +791,11 @@ __global__ __launch_bounds__(256) void k_peer_ts(TableView t, uint8_t *invs, uin
 // the key this round (peer_ts, RMW builds), the INV-abort hermes_exec_inv makes at the peer
 // (hermesKV.c:566-576): the peer's local state (local_state_to_op, hermesKV.c:143-153: its RMW
 // flag, timestamp, val_len and value 'a' + peer) with opcode ST_OP_INV_ABORT and sender = peer.
-__global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32_t inv_stride, uint32_t op_size,
-                            uint8_t *acks, uint32_t ack_size, int32_t out_stride, int32_t *ack_count,
-                            const uint8_t *peers, int32_t n_peers, int64_t total, TableView t,
-                            const unsigned long long *peer_ts, uint32_t round)
+__device__ __forceinline__ void peer_answer(const uint8_t *x, uint8_t *y, uint32_t op_size, uint32_t ack_size,
+                                            uint8_t peer, const TableView &t, const unsigned long long *peer_ts,
+                                            uint32_t round)
 {
-    int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= total) return;
-    int64_t per_w = out_stride;     // slots x n_peers ACK positions per worker (host checks)
-    int32_t w = (int32_t)(g / per_w);
-    int32_t rem = (int32_t)(g - (int64_t)w * per_w);
-    int32_t j = rem / n_peers, r = rem - j * n_peers;
-    int32_t n = inv_count[w];
-    if (rem == 0) ack_count[w] = n * n_peers;
-    if (j >= n) return;
-    const uint8_t *x = invs + ((int64_t)w * inv_stride + j) * op_size;
-    uint8_t *y = acks + ((int64_t)w * out_stride + rem) * ack_size;
     const W16 h = *reinterpret_cast<const W16 *>(x);
-    const uint8_t peer = peers[r];
     if (peer_ts && (x[16] & 1u) && peer < 8 && ack_size >= op_size) {
         const uint64_t phys = find_entry(t, h.a);
         if (phys != ~0ull) {
@@ -828,6 +818,68 @@ __global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32
     *reinterpret_cast<W16 *>(y) = W16{h.a, with_op_state(h.b, kOpAck, peer)};  // ack_copy_and_modify_elem
 }
 
+// rows: worker w's answers at w * out_stride; out_off (packed ACK batches): at out_off[w]
+__global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32_t inv_stride, uint32_t op_size,
+                            uint8_t *acks, uint32_t ack_size, int32_t out_stride, int32_t *ack_count,
+                            const uint8_t *peers, int32_t n_peers, int64_t total, TableView t,
+                            const unsigned long long *peer_ts, uint32_t round, const int32_t *out_off)
+{
+    int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= total) return;
+    int64_t per_w = out_stride;     // slots x n_peers ACK positions per worker (host checks)
+    int32_t w = (int32_t)(g / per_w);
+    int32_t rem = (int32_t)(g - (int64_t)w * per_w);
+    int32_t j = rem / n_peers, r = rem - j * n_peers;
+    int32_t n = inv_count[w];
+    if (rem == 0 && ack_count) ack_count[w] = n * n_peers;
+    if (j >= n) return;
+    const uint8_t *x = invs + ((int64_t)w * inv_stride + j) * op_size;
+    const int64_t pos = out_off ? (int64_t)out_off[w] + rem : (int64_t)w * out_stride + rem;
+    peer_answer(x, acks + pos * ack_size, op_size, ack_size, peers[r], t, peer_ts, round);
+}
+
+// Packed ACK batches: off[w] = n_peers x (INVs of workers before w), off[n] = the total; the total
+// and the largest per-worker INV count land in pinned host memory (h[0], h[1]) for the host to size
+// the round's launches while the GPU runs the INV batch
+__global__ __launch_bounds__(1024) void k_ack_offsets(const int32_t *counts, int32_t n, int32_t n_peers, int32_t *off,
+                                                      int32_t *h)
+{
+    __shared__ int32_t part[16], pmax[16];
+    __shared__ int32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    int32_t mx = 0;
+    for (int32_t i0 = 0; i0 < n; i0 += 1024) {
+        __syncthreads();
+        const int32_t i = i0 + (int32_t)threadIdx.x;
+        const int32_t c = i < n ? counts[i] : 0;
+        mx = c > mx ? c : mx;
+        int32_t v = c * n_peers;  // inclusive scan within the wave, then across waves
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t u = __shfl_up(v, o, 64);
+            if ((threadIdx.x & 63) >= (unsigned)o) v += u;
+        }
+        if ((threadIdx.x & 63) == 63) part[threadIdx.x >> 6] = v;
+        __syncthreads();
+        int32_t before = carry;
+        for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) before += part[k];
+        if (i < n) off[i] = before + v - c * n_peers;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry = before + v;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const int32_t u = __shfl_down(mx, o, 64);
+        mx = u > mx ? u : mx;
+    }
+    if ((threadIdx.x & 63) == 0) pmax[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < 16; ++k) mx = pmax[k] > mx ? pmax[k] : mx;
+        off[n] = carry;
+        h[0] = carry;
+        h[1] = mx;
+    }
+}
+
 // The virtual peers' answers appended to each worker's ACK queue (aq: [W][q_stride] elements of
 // ack_size bytes, aq_n[w] queued): one workgroup per worker. A worker with outstanding VALs
 // (vq_n[w] > 0) does not poll its ACKs this round (hermes_worker.c:479): acnt[w] = 0 and the
@@ -845,29 +897,8 @@ __global__ __launch_bounds__(256) void k_peer_acks_q(const uint8_t *invs, const 
         const int j = g / n_peers, r = g - j * n_peers;
         if (base + g >= q_stride) break;  // the host sizes q_stride for C INVs x n_peers
         const uint8_t *x = invs + ((int64_t)w * inv_stride + j) * op_size;
-        uint8_t *y = aq + ((int64_t)w * q_stride + base + g) * ack_size;
-        const W16 h = *reinterpret_cast<const W16 *>(x);
-        const uint8_t peer = peers[r];
-        bool abort = false;
-        if (peer_ts && (x[16] & 1u) && peer < 8 && ack_size >= op_size) {
-            const uint64_t phys = find_entry(t, h.a);
-            if (phys != ~0ull) {
-                const unsigned long long pw = peer_ts[(phys / t.g.entry_unit) * 8 + peer];
-                const uint64_t ours = ((uint64_t)(uint32_t)(h.b >> 32) << 8) | (uint8_t)(h.b >> 24);
-                if ((uint32_t)(pw >> 41) == peer_round_tag(round) && (pw & 0xFFFFFFFFFFull) > ours) {
-                    const uint64_t pts = pw & 0xFFFFFFFFFFull;
-                    uint64_t *d = reinterpret_cast<uint64_t *>(y);
-                    d[0] = h.a;
-                    d[1] = (uint64_t)kOpInvAbort | ((uint64_t)peer << 8) | ((uint64_t)(uint8_t)x[10] << 16) |
-                           ((pts & 0xFFull) << 24) | ((pts >> 8) << 32);
-                    const uint64_t vv = 0x0101010101010101ULL * (uint8_t)('a' + peer);
-                    d[2] = (vv << 16) | ((uint64_t)x[17] << 8) | ((pw >> 40) & 1u);
-                    for (uint32_t k = 3; k < op_size / 8; ++k) d[k] = vv;
-                    abort = true;
-                }
-            }
-        }
-        if (!abort) *reinterpret_cast<W16 *>(y) = W16{h.a, with_op_state(h.b, kOpAck, peer)};
+        peer_answer(x, aq + ((int64_t)w * q_stride + base + g) * ack_size, op_size, ack_size, peers[r], t, peer_ts,
+                    round);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -998,7 +1029,7 @@ int hkv_wl_marshal_vals(uint8_t *acks, int64_t n, uint32_t ack_size, uint8_t *ou
 int hkv_wl_peer_acks(hkv_table *t, const uint8_t *inv_out, const int32_t *inv_count, int32_t n_workers,
                      int32_t inv_stride, uint32_t op_size, uint8_t *acks, uint32_t ack_size, int32_t out_stride,
                      int32_t *ack_count, const uint8_t *peer_ids, int32_t n_peers,
-                     const unsigned long long *peer_ts, uint32_t round, void *stream)
+                     const unsigned long long *peer_ts, uint32_t round, const int32_t *out_off, void *stream)
 {
     if (n_peers <= 0 || n_workers <= 0 || ack_size < kOpMetaSize || ack_size % 8) return -1;
     if (out_stride % n_peers || out_stride > inv_stride * n_peers || out_stride <= 0) return -1;
@@ -1007,7 +1038,7 @@ int hkv_wl_peer_acks(hkv_table *t, const uint8_t *inv_out, const int32_t *inv_co
     int64_t total = (int64_t)n_workers * out_stride;
     hipLaunchKernelGGL(k_peer_acks, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, inv_out, inv_count,
                        inv_stride, op_size, acks, ack_size, out_stride, ack_count, peer_ids, n_peers, total, tv,
-                       peer_ts, round);
+                       peer_ts, round, out_off);
     return ok();
 }
 
@@ -1132,12 +1163,23 @@ int hkv_wl_regroup(const uint8_t *in, const int32_t *counts, int32_t n_peers, in
 
 int hkv_wl_collect_vals(uint8_t *acks, const int32_t *count, int32_t n_workers, int32_t stride, uint32_t ack_size,
                         uint8_t *out, int32_t C, int32_t *out_count, uint32_t machine_id, unsigned long long *held,
-                        void *stream)
+                        const int32_t *offsets, void *stream)
 {
     if (n_workers <= 0) return 0;
     if (C <= 0 || ack_size % 8) return -1;
     hipLaunchKernelGGL(k_collect_vals, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, acks, count, stride,
-                       ack_size, out, C, out_count, machine_id, held);
+                       ack_size, out, C, out_count, machine_id, held, offsets);
+    return ok();
+}
+
+int hkv_wl_ack_offsets(const int32_t *inv_count, int32_t n_workers, int32_t n_peers, int32_t *offsets, int32_t *h_out,
+                       void *stream)
+{
+    if (n_workers <= 0 || n_peers <= 0) return -1;
+    int32_t *d_out = nullptr;
+    if (hipHostGetDevicePointer(reinterpret_cast<void **>(&d_out), h_out, 0) != hipSuccess || !d_out) return -1;
+    hipLaunchKernelGGL(k_ack_offsets, dim3(1), dim3(1024), 0, (hipStream_t)stream, inv_count, n_workers, n_peers,
+                       offsets, d_out);
     return ok();
 }
 

@@ -156,7 +156,7 @@ class HermesKV:
               stream: torch.cuda.Stream | None = None, offsets: torch.Tensor | None = None) -> None:
         """Apply n_batches batches of one type, concatenated in `elems` (uint8, on the GPU),
         in concatenation order, asynchronously on `stream` (default: torch's current).
-        offsets (INV / VAL batches): the batches stored back to back, batch b at elements
+        offsets (INV / ACK / VAL batches): the batches stored back to back, batch b at elements
         [offsets[b], offsets[b+1]); `stride` is then the total (HKV_BATCH_PACKED)."""
         assert elems.is_cuda and elems.dtype == torch.uint8
         total = stride if offsets is not None else n_batches * stride
@@ -200,10 +200,14 @@ class HermesKV:
             to = torch.from_numpy(np.ascontiguousarray(offsets, dtype=np.int32)).to(dev)
             tn = torch.from_numpy(np.ascontiguousarray(node_suspected, dtype=np.int32)).to(dev) \
                 if node_suspected is not None else None
-            self.batch(btype, t, n_batches, len(elems), elems.dtype.itemsize, membership, node_suspected=tn,
-                       offsets=to)
+            tr = torch.from_numpy(rw.view(np.uint8).reshape(-1).copy()).to(dev) if rw is not None else None
+            self.batch(btype, t, n_batches, len(elems), elems.dtype.itemsize, membership, rw=tr,
+                       rw_stride_bytes=rw_stride_elems * (rw.dtype.itemsize if rw is not None else 0),
+                       node_suspected=tn, offsets=to)
             torch.cuda.synchronize(dev)
             elems.view(np.uint8).reshape(-1)[:] = t.cpu().numpy()
+            if rw is not None:
+                rw.view(np.uint8).reshape(-1)[:] = tr.cpu().numpy()
             if node_suspected is not None:
                 node_suspected[:] = tn.cpu().numpy()
             return

@@ -43,7 +43,7 @@ _L.hkv_wl_marshal_acks_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, 
 _L.hkv_wl_regroup.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P,
                               ctypes.c_int32, _P, _P]
 _L.hkv_wl_collect_vals.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
-                                   _P, ctypes.c_uint32, _P, _P]
+                                   _P, ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_pack_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_marshal_acks_aligned.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P,
                                            ctypes.c_uint32, ctypes.c_uint32, _P]
@@ -197,7 +197,7 @@ class ReplicaRound:
                        counts=self.ack_batch_count, rw=self.ops, rw_stride_bytes=LOCAL * self.op)
         check(_L.hkv_wl_collect_vals(_ptr(self.ack_batch), _ptr(self.ack_batch_count), W, stride, self.ack_size,
                                      _ptr(self.val_slab), C, _ptr(self.val_count), self.rank,
-                                     _ptr(self.held[1:]), _s()), "collect_vals")
+                                     _ptr(self.held[1:]), None, _s()), "collect_vals")
         check(_L.hkv_wl_pack_rows(_ptr(self.val_slab), _ptr(self.val_count), W, C, L.OP_META_SIZE,
                                   _ptr(self.val_pack), _ptr(self.val_off), _s()), "pack vals")
 

@@ -41,9 +41,9 @@ _L.hkv_wl_marshal_memb_vals.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctyp
 _L.hkv_wl_max_to_host.argtypes = [_P, ctypes.c_int32, _P, _P]
 _L.hkv_wl_marshal_vals.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_collect_vals.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
-                                   _P, ctypes.c_uint32, _P, _P]
+                                   _P, ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_peer_acks.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_uint32,
-                                ctypes.c_int32, _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, _P]
+                                ctypes.c_int32, _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, _P, _P]
 _L.hkv_wl_peer_round_scratch.restype = ctypes.c_size_t
 _L.hkv_wl_peer_round_scratch.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
 _L.hkv_wl_gen_peer_round.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, _P, ctypes.c_int32,
@@ -57,6 +57,7 @@ _L.hkv_wl_peer_acks_queue.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32
                                       ctypes.c_int32, _P, _P, _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_vals_credit.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_int32,
                                   _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P]
+_L.hkv_wl_ack_offsets.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, _P]
 _L.hkv_wl_pack_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_peer_ts_words.restype = ctypes.c_uint64
 _L.hkv_wl_peer_ts_words.argtypes = [_P]
@@ -129,8 +130,9 @@ class Round:
         self.held = torch.zeros(1, dtype=torch.int64, device=dev)
         self.ack_stride = self.C * max(self.R, 1)   # capacity; the round uses self.ack_width
         self.ack_width = self.ack_stride
-        # fit_ack_stride: each round's ACK slab is laid out at R x (largest per-worker INV count),
-        # read back while the remote INV batch runs (about 20 ACKs per worker against 2C slots)
+        # fit_ack_stride: each round's ACK batch is packed (HKV_BATCH_PACKED, about 20 ACKs per
+        # worker instead of R x C slots); its offsets, total and the largest INV count are computed
+        # on the GPU and read back while the remote INV batch runs
         self.fit = fit_ack_stride and virtual_peers and self.R > 0 and val_credits is None
         # val_credits: VAL messages each worker may send per round (the VAL channel's credits, which
         # the virtual peers return every round). Then a worker's ACKs queue up in its row of `acks`
@@ -146,7 +148,9 @@ class Round:
             self.vq_n = torch.zeros(W, dtype=torch.int32, device=dev)
             self.val_overflow = torch.zeros(1, dtype=torch.int64, device=dev)
             self.val_totals = torch.zeros(2, dtype=torch.int64, device=dev)  # VALs sent, gated worker-rounds
-        self.maxc_h = torch.zeros(1, dtype=torch.int32, pin_memory=True) if self.fit else None
+        self.maxc_h = torch.zeros(2, dtype=torch.int32, pin_memory=True) if self.fit else None
+        self.ack_off = torch.zeros(W + 1, dtype=torch.int32, device=dev) if self.fit else None
+        self.ack_total = 0
         self.maxc_ev = torch.cuda.Event() if self.fit else None
         self.acks = torch.zeros(W * self.ack_stride * self.ack_size, **u8)
         self.ack_count = torch.zeros(W, dtype=torch.int32, device=dev)
@@ -249,7 +253,7 @@ class Round:
         check(_L.hkv_wl_peer_acks(self.kvs.h, _ptr(self.inv_out), _ptr(self.inv_count), self.W, self.C, self.op,
                                   _ptr(self.acks), self.ack_size, self.ack_width, _ptr(self.ack_count),
                                   _ptr(self.peer_t), self.R if n_peers is None else n_peers, _ptr(self.peer_ts),
-                                  self.clock, _s()), "peer_acks")
+                                  self.clock, _ptr(self.ack_off) if self.fit else None, _s()), "peer_acks")
 
     def peer_timestamps(self, k: int, n_peers: int):
         """Round start: the live peers' INVs and VALs of round index k take their timestamps"""
@@ -273,6 +277,10 @@ class Round:
     def ack_batch(self, acks: torch.Tensor | None = None, n_batches: int | None = None, stride: int | None = None,
                   counts: torch.Tensor | None = None):
         acks = self.acks if acks is None else acks
+        if self.fit and stride is None:   # this round's packed ACKs
+            self.kvs.batch(L.BatchType.acks, acks, self.W, self.ack_total, self.ack_size, self.mb,
+                           rw=self.ops, rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off)
+            return
         self.kvs.batch(L.BatchType.acks, acks, n_batches or self.W, stride or self.ack_width, self.ack_size,
                        self.mb, counts=self.ack_count if counts is None else counts, rw=self.ops,
                        rw_stride_bytes=self.LOCAL * self.op)
@@ -285,8 +293,8 @@ class Round:
         """VALs of the writes this round's ACK batch completed, compacted per worker (val_out
         [W][ack_stride], val_count): only the ACK slab's live elements are read."""
         check(_L.hkv_wl_collect_vals(_ptr(self.acks), _ptr(self.ack_count), self.W, self.ack_width, self.ack_size,
-                                     _ptr(self.val_out), self.ack_width, _ptr(self.val_count), self.machine_id,
-                                     None, _s()), "collect_vals")
+                                     _ptr(self.val_out), self.C, _ptr(self.val_count), self.machine_id,
+                                     None, _ptr(self.ack_off) if self.fit else None, _s()), "collect_vals")
 
     def peer_acks_queued(self, n_peers: int):
         """The first n_peers virtual peers' ACKs to this round's INVs appended to each worker's ACK
@@ -346,8 +354,9 @@ class Round:
         self.marshal_invs()
         if self.count_elems:
             self.inv_total += self.inv_count.sum()
-        if self.fit:
-            check(_L.hkv_wl_max_to_host(_ptr(self.inv_count), self.W, _ptr(self.maxc_h), _s()), "max_to_host")
+        if self.fit and alive:
+            check(_L.hkv_wl_ack_offsets(_ptr(self.inv_count), self.W, alive, _ptr(self.ack_off), _ptr(self.maxc_h),
+                                        _s()), "ack_offsets")
             self.maxc_ev.record()
         if self.R:
             ri, rv = self.remote_inv[k], self.remote_val[k]
@@ -360,9 +369,10 @@ class Round:
                 timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride, counts=ic))
                 self.marshal_acks(ri, self.W * self.rstride, self.ack_out)
             m = self.C
-            if self.fit:   # the GPU is still on the INV batch: this wait leaves no gap on the stream
+            if self.fit and alive:   # the GPU is still on the INV batch: this wait leaves no gap
                 self.maxc_ev.synchronize()
-                m = min(int(self.maxc_h[0]), self.C)
+                self.ack_total = int(self.maxc_h[0])
+                m = min(int(self.maxc_h[1]), self.C)
             if alive and self.V is not None:
                 self.peer_acks_queued(alive)
                 timed("acks", lambda: self.ack_batch(stride=self.ack_stride))

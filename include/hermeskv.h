@@ -122,9 +122,10 @@ typedef struct hkv_batch_desc {
  * kernel and larger ones on the multi-kernel engine; both give the same bytes. */
 #define HKV_BATCH_ENGINE 1u     /* always the multi-kernel engine */
 #define HKV_BATCH_SMALL  2u     /* the single-workgroup kernel (launches of at most 4096 elements) */
-/* INV and VAL batches stored back to back: d_counts holds n_batches + 1 element offsets (batch b is
- * elements [d_counts[b], d_counts[b+1]) of d_elems) and stride is the total, d_counts[n_batches].
- * Same results as the row layout; no empty slots to launch over. */
+/* INV, ACK and VAL batches stored back to back: d_counts holds n_batches + 1 element offsets (batch
+ * b is elements [d_counts[b], d_counts[b+1]) of d_elems) and stride is the total, d_counts[n_batches];
+ * an ACK batch b still completes into d_rw + b * rw_stride_bytes. Same results as the row layout;
+ * no empty slots to launch over. */
 #define HKV_BATCH_PACKED 4u
 
 int  hkv_abi_version(void);

@@ -115,11 +115,20 @@ uint64_t hkv_wl_peer_ts_words(const hkv_table *t);
  * hermes_exec_inv returns (hermesKV.c:566-576: the peer's RMW flag, timestamp and value). ack_size:
  * 16, or the op size in an RMW build; d_ack_count[w] = n_peers * d_inv_count[w]. out_stride is a
  * multiple of n_peers, at most inv_stride * n_peers, and the caller keeps every d_inv_count[w] <=
- * out_stride / n_peers (the N=1 round fits it to the round's largest count) */
+ * out_stride / n_peers (the N=1 round fits it to the round's largest count). d_out_off (may be
+ * NULL): worker w's answers start at element d_out_off[w] instead (a packed ACK batch, offsets from
+ * hkv_wl_ack_offsets); d_ack_count may then be NULL. */
 int hkv_wl_peer_acks(hkv_table *t, const uint8_t *d_inv_out, const int32_t *d_inv_count, int32_t n_workers,
                      int32_t inv_stride, uint32_t op_size, uint8_t *d_acks, uint32_t ack_size, int32_t out_stride,
                      int32_t *d_ack_count, const uint8_t *peer_ids, int32_t n_peers,
-                     const unsigned long long *d_peer_ts, uint32_t round, void *stream);
+                     const unsigned long long *d_peer_ts, uint32_t round, const int32_t *d_out_off, void *stream);
+
+/* Offsets of a packed ACK batch answering d_inv_count[0..n_workers) INVs from n_peers peers:
+ * d_offsets[w] = n_peers * (INVs of workers before w), d_offsets[n_workers] = the total. h_out
+ * (pinned host memory, 2 ints) receives the total and the largest d_inv_count once the stream
+ * passes this call. */
+int hkv_wl_ack_offsets(const int32_t *d_inv_count, int32_t n_workers, int32_t n_peers, int32_t *d_offsets,
+                       int32_t *h_out, void *stream);
 
 /* ---- replica groups (one replica per GPU, slabs exchanged over RCCL) ------------------ */
 
@@ -155,12 +164,14 @@ int hkv_wl_marshal_acks_rows(uint8_t *d_invs, const int32_t *d_in_count, int32_t
 int hkv_wl_regroup(const uint8_t *d_in, const int32_t *d_counts, int32_t n_peers, int32_t n_workers, int32_t C,
                    uint32_t elem_size, uint8_t *d_out, int32_t out_stride, int32_t *d_out_count, void *stream);
 
-/* VALs (16 B) for the ACK elements of per-worker ACK batches ([n_workers][stride], counts)
- * that completed a write, compacted into [n_workers][C]; the ACK elements become ST_EMPTY as
- * in hkv_wl_marshal_vals. VALs beyond C are dropped and counted in *d_held (may be NULL). */
+/* VALs (16 B) for the ACK elements of per-worker ACK batches ([n_workers][stride], counts; or
+ * packed, worker w at [d_offsets[w], d_offsets[w+1]) when d_offsets is not NULL) that completed a
+ * write, compacted into [n_workers][C]; the ACK elements become ST_EMPTY as in
+ * hkv_wl_marshal_vals. C must cover a worker's VALs (the N=1 round: its INV credits); any beyond
+ * are counted in *d_held (may be NULL) -- the VAL-credit path (hkv_wl_vals_credit) carries them. */
 int hkv_wl_collect_vals(uint8_t *d_acks, const int32_t *d_count, int32_t n_workers, int32_t stride,
                         uint32_t ack_size, uint8_t *d_val_out, int32_t C, int32_t *d_val_count,
-                        uint32_t machine_id, unsigned long long *d_held, void *stream);
+                        uint32_t machine_id, unsigned long long *d_held, const int32_t *d_offsets, void *stream);
 
 /* ---- VAL credits and the outstanding-VAL gate (hermes_worker.c:479-503, wings.h:424-540, 862-916)
  * Per worker: an ACK queue (d_aq rows of q_stride elements of ack_size bytes, d_aq_n queued) and a

@@ -97,7 +97,8 @@ class Mirror:
               rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None):
         import torch
         if offsets is not None:
-            return self._packed(btype, elems, n_batches, stride, elem_size, membership, offsets, stream)
+            return self._packed(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
+                                rw_stride_bytes)
         torch.cuda.synchronize()
         n = n_batches * stride * elem_size
         vt = np.dtype((np.void, elem_size))
@@ -132,9 +133,10 @@ class Mirror:
         assert self.g.take_error_flags() == 0, f"{what}: device consistency flags"
         self.launches += 1
 
-    def _packed(self, btype, elems, n_batches, total, elem_size, membership, offsets, stream):
-        """A packed (HKV_BATCH_PACKED) INV / VAL launch: the oracle applies the same batches laid
-        out in rows; the device's packed output must equal the oracle's rows packed again."""
+    def _packed(self, btype, elems, n_batches, total, elem_size, membership, offsets, stream, rw=None,
+                rw_stride_bytes=0):
+        """A packed (HKV_BATCH_PACKED) INV / ACK / VAL launch: the oracle applies the same batches
+        laid out in rows; the device's packed output must equal the oracle's rows packed again."""
         import torch
         torch.cuda.synchronize()
         off = offsets[: n_batches + 1].cpu().numpy().astype(np.int64)
@@ -146,10 +148,13 @@ class Mirror:
         pos = np.arange(width)[None, :] < cnt[:, None]
         rows[pos] = flat
         self._count(btype, "in8", 8, rows.reshape(-1), n_batches, width, elem_size, cnt)
-        self._orig(btype, elems, n_batches, total, elem_size, membership, stream=stream, offsets=offsets)
+        rw_in = rw.cpu().numpy().copy().view(np.dtype((np.void, self.g.sizes.op))) if rw is not None else None
+        self._orig(btype, elems, n_batches, total, elem_size, membership, rw=rw, rw_stride_bytes=rw_stride_bytes,
+                   stream=stream, offsets=offsets)
         torch.cuda.synchronize()
         e_in = rows.reshape(-1).view(np.dtype((np.void, elem_size))).copy()
-        self.o.batch_multi(int(btype), e_in, n_batches, width, cnt, membership, None, 0)
+        self.o.batch_multi(int(btype), e_in, n_batches, width, cnt, membership, rw_in,
+                           rw_stride_bytes // self.g.sizes.op if rw is not None else 0)
         want = e_in.view(np.uint8).reshape(n_batches, width, elem_size)[pos]
         got = elems[: total * elem_size].cpu().numpy().reshape(total, elem_size)
         what = f"{self.name} launch {self.launches} type {int(btype)} (packed)"
@@ -160,6 +165,8 @@ class Mirror:
         if not np.array_equal(got, want):
             bad = np.nonzero((got != want).any(axis=1))[0]
             pytest.fail(f"{what}: elements differ at {len(bad)} elements, first {bad[:8]}")
+        if rw is not None:
+            assert np.array_equal(rw.cpu().numpy(), rw_in.view(np.uint8)), f"{what}: read_write_ops differ"
         gl, ol = self.g.log_bytes(), self.o.log_bytes()[: self.g.cfg.log_cap]
         if not np.array_equal(gl, ol):
             bad = np.nonzero(gl != ol)[0]

@@ -174,7 +174,8 @@ def _run_both(g, o, btype, elems_g, elems_o, mb, n_batches, stride, counts, rw_g
         live = (np.arange(stride)[None, :] < cnt[:, None]).reshape(-1)
         off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int32)
         flat = elems_g[live].copy()
-        g.batch_host(btype, flat, mb, n_batches=n_batches, node_suspected=ns_g, offsets=off)
+        g.batch_host(btype, flat, mb, rw=rw_g, n_batches=n_batches, node_suspected=ns_g, offsets=off,
+                     rw_stride_elems=rw_stride)
         elems_g[live] = flat
     else:
         g.batch_host(btype, elems_g, mb, rw=rw_g, n_batches=n_batches, stride=stride, counts=counts,
@@ -223,7 +224,7 @@ def test_random_protocol_rounds(cfg):
         ack = gen.acks(rng, pool, W * M, sizes, rmw, tsp)
         counts = rng.integers(M // 2, M + 1, size=W).astype(np.int32)
         ack_o = gen.bytecopy(ack)
-        _run_both(g, o, L.BatchType.acks, ack, ack_o, mb, W, M, counts, rw_g, rw_o, rw_stride=S)
+        _run_both(g, o, L.BatchType.acks, ack, ack_o, mb, W, M, counts, rw_g, rw_o, rw_stride=S, packed=rnd % 2 == 0)
         assert_elems_equal(ack, ack_o, f"round {rnd} acks")
         assert_elems_equal(rw_g, rw_o, f"round {rnd} acks rw")
         assert_tables_equal(g, o, f"round {rnd} acks")
@@ -481,7 +482,7 @@ def test_ack_direct_path_edge_cases(big):
                                    size=W * M, p=[0.8, 0.1, 0.05, 0.05])
         counts = rng.integers(M // 3, M + 1, size=W).astype(np.int32)
         ack_o = gen.bytecopy(ack)
-        _run_both(g, o, L.BatchType.acks, ack, ack_o, mb, W, M, counts, rw_g, rw_o, rw_stride=S)
+        _run_both(g, o, L.BatchType.acks, ack, ack_o, mb, W, M, counts, rw_g, rw_o, rw_stride=S, packed=rnd % 2 == 0)
         assert_elems_equal(ack, ack_o, f"round {rnd} acks")
         assert_elems_equal(rw_g, rw_o, f"round {rnd} acks rw")
         assert_tables_equal(g, o, f"round {rnd} acks")

@@ -161,7 +161,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    c0 = rnd.counters[:4].clone()
+    c0 = rnd.fold_counters()[:4].clone()
     rnd.count_elems = False  # element bookkeeping runs in probe steps after the timed region
     events: dict = {}
     torch.cuda.synchronize()
@@ -181,7 +181,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t
-    c1 = rnd.counters[:4].clone()
+    c1 = rnd.fold_counters()[:4].clone()
     committed = int((c1[0] - c0[0]).item())
     writes = int((c1[2] - c0[2]).item())
     dropped = int((c1[3] - c0[3]).item())
@@ -333,13 +333,13 @@ def retry_rate(a, kvs, z, L, Round) -> dict:
     for _ in range(a.warmup):
         r.step()
     torch.cuda.synchronize()
-    c0 = r.counters[:4].clone()
+    c0 = r.fold_counters()[:4].clone()
     t = time.perf_counter()
     for _ in range(a.retry_steps):
         r.step()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t
-    c = (r.counters[:4] - c0).tolist()
+    c = (r.fold_counters()[:4] - c0).tolist()
     return {"value": c[0] / dt, "unit": "ops/s", "steps": a.retry_steps, "ms_per_step": dt * 1e3 / a.retry_steps,
             "committed_per_step": c[0] / a.retry_steps, "writes_completed_per_step": c[2] / a.retry_steps,
             "what": "refill_ops retry policy (stalled ops keep their slots), same workload and table"}

@@ -435,23 +435,25 @@ __global__ __launch_bounds__(256) void k_regroup(const uint8_t *in, const int32_
 
 // VALs of the writes an ACK batch completed (ST_LAST_ACK_SUCCESS), compacted per worker into
 // [W][C]; the ACK elements become ST_EMPTY (hermes_worker.c:112-160)
-__global__ __launch_bounds__(256) void k_collect_vals(uint8_t *acks, const int32_t *count, int32_t stride,
-                                                      uint32_t ack_size, uint8_t *out, int32_t C, int32_t *out_count,
-                                                      uint32_t machine_id, unsigned long long *held,
-                                                      const int32_t *offsets)
+__global__ __launch_bounds__(64) void k_collect_vals(uint8_t *acks, const int32_t *count, int32_t stride,
+                                                     uint32_t ack_size, uint8_t *out, int32_t C, int32_t *out_count,
+                                                     uint32_t machine_id, unsigned long long *held,
+                                                     const int32_t *offsets)
 {
+    // one wave per worker (a worker's round has a few dozen ACKs)
     const int64_t w = blockIdx.x;
+    const int lane = (int)threadIdx.x;
     // rows: worker w's ACKs at w * stride, count[w] of them; packed: [offsets[w], offsets[w+1])
     const int n = offsets ? offsets[w + 1] - offsets[w] : count[w];
     const int64_t row = offsets ? (int64_t)offsets[w] : w * stride;
     int base = 0;
-    for (int j0 = 0; j0 < n; j0 += 256) {
-        const int j = j0 + (int)threadIdx.x;
+    for (int j0 = 0; j0 < n; j0 += 64) {
+        const int j = j0 + lane;
         uint8_t *x = acks + (row + j) * (int64_t)ack_size;
         const uint8_t oc = j < n ? x[8] : 0;
         const bool send = j < n && oc == kLastAckSuccess;
-        int total;
-        const int rank = block_rank(send, total);
+        const unsigned long long m = __ballot(send);
+        const int rank = __popcll(m & ((1ull << lane) - 1ull));
         if (send && base + rank < C) {
             uint64_t *y = reinterpret_cast<uint64_t *>(out + (w * C + base + rank) * (int64_t)kOpMetaSize);
             y[0] = reinterpret_cast<const uint64_t *>(x)[0];
@@ -459,9 +461,9 @@ __global__ __launch_bounds__(256) void k_collect_vals(uint8_t *acks, const int32
             y[1] = (h & ~0xFFFFull) | kOpVal | ((uint64_t)(machine_id & 0xFF) << 8);
         }
         if (j < n && (oc == kLastAckSuccess || oc == kAckSuccess || oc == kOpMembChange)) x[8] = kEmpty;
-        base += total;
+        base += __popcll(m);
     }
-    if (threadIdx.x == 0) {
+    if (lane == 0) {
         out_count[w] = base < C ? base : C;
         if (base > C && held) atomicAdd(held, (unsigned long long)(base - C));
     }
@@ -727,63 +729,83 @@ __device__ __forceinline__ uint32_t peer_round_tag(uint32_t round) { return (rou
 struct __attribute__((aligned(8))) U64x2w {
     uint64_t a, b;
 };
+constexpr int kPeerTsPair = 2;  // elements in flight per 4-lane group
 __global__ __launch_bounds__(256) void k_peer_ts(TableView t, uint8_t *invs, uint8_t *vals, const int32_t *counts,
                                                  int32_t stride, uint32_t op_size, unsigned long long *peer_ts,
                                                  uint32_t round, int64_t total)
 {
     const int q = threadIdx.x & 3;
     const int gbase = (threadIdx.x & 63) & ~3;
-    const int64_t g = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 2;
-    int live = 0;
-    uint64_t key = 0, flags = 0;
-    if (g < total && q == 0) {
-        const int32_t w = (int32_t)(g / stride);
-        if ((int32_t)(g - (int64_t)w * stride) < counts[w]) {
-            live = 1;
-            const uint8_t *x = invs + g * op_size;
-            key = *reinterpret_cast<const uint64_t *>(x);
-            flags = *reinterpret_cast<const uint64_t *>(x + 8) >> 8 & 0xFFu;   // byte 9: the peer
-            flags |= (uint64_t)(x[16] & 1u) << 8;                               // RMW_flag
+    int64_t g[kPeerTsPair];
+    int live[kPeerTsPair];
+    uint64_t key[kPeerTsPair], flags[kPeerTsPair];
+#pragma unroll
+    for (int k = 0; k < kPeerTsPair; ++k) {
+        g[k] = ((int64_t)blockIdx.x * kPeerTsPair + k) * 64 + (threadIdx.x >> 2);
+        live[k] = 0;
+        key[k] = flags[k] = 0;
+        if (g[k] < total && q == 0) {
+            const int32_t w = (int32_t)(g[k] / stride);
+            if ((int32_t)(g[k] - (int64_t)w * stride) < counts[w]) {
+                live[k] = 1;
+                const uint8_t *x = invs + g[k] * op_size;
+                key[k] = *reinterpret_cast<const uint64_t *>(x);
+                flags[k] = *reinterpret_cast<const uint64_t *>(x + 8) >> 8 & 0xFFu;  // byte 9: the peer
+                flags[k] |= (uint64_t)(x[16] & 1u) << 8;                               // RMW_flag
+            }
         }
     }
-    live = __shfl(live, 0, 4);
-    key = __shfl(key, 0, 4);
-    const uint4 v = live ? reinterpret_cast<const uint4 *>(t.index + ((key & 0xFFFFFFFFFFFFULL) & t.g.bkt_mask) * 64u)[q]
-                         : make_uint4(0u, 0u, 0u, 0u);
-    const uint64_t s0 = (uint64_t)v.x | ((uint64_t)v.y << 32), s1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
-    const uint32_t tag = (uint32_t)(key >> 48);
-    const bool mt0 = live && (s0 & 1u) && ((uint32_t)(s0 >> 1) & 0x7FFFFFu) == tag;
-    const bool mt1 = live && (s1 & 1u) && ((uint32_t)(s1 >> 1) & 0x7FFFFFu) == tag;
-    const uint32_t g0 = (uint32_t)(__ballot(mt0) >> gbase) & 0xFu, g1 = (uint32_t)(__ballot(mt1) >> gbase) & 0xFu;
-    uint32_t o = 0;  // bit 2*l + j: slot 2*l + j matches (the reference's slot order)
+    uint4 v[kPeerTsPair];
 #pragma unroll
-    for (int l = 0; l < 4; ++l) o |= ((g0 >> l) & 1u) << (2 * l) | ((g1 >> l) & 1u) << (2 * l + 1);
-    const int first = o ? __ffs(o) - 1 : 0;
-    const uint64_t off = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
-    const bool ok = live && o && t.g.log_head - off < t.g.log_cap;
-    const uint64_t phys = off & t.g.log_mask;
-    // lane 0: entry bytes 0..15 (key at 8), lane 1: bytes 16..31 (version at 24)
-    const U64x2w ln = ok && q < 2 ? reinterpret_cast<const U64x2w *>(t.log + phys)[q] : U64x2w{0, 0};
-    const uint64_t ekey = __shfl(ln.b, 0, 4);
-    const uint32_t cur = (uint32_t)__shfl(ln.b, 1, 4);
-    if (q != 0 || !live) return;
-    uint8_t *x = invs + g * op_size;
-    const uint8_t peer = (uint8_t)flags;
-    const bool rmw = (flags >> 8) & 1u;
-    uint32_t ver = 2;
-    if (ok && ekey == key) {
-        ver = cur + ((!t.g.rmw_enabled || rmw) ? 2u : 4u);
-        if (peer_ts && peer < 8)
-            atomicMax(peer_ts + (phys / t.g.entry_unit) * 8 + peer,
-                      ((unsigned long long)peer_round_tag(round) << 41) | ((unsigned long long)rmw << 40) |
-                          ((unsigned long long)ver << 8) | peer);
+    for (int k = 0; k < kPeerTsPair; ++k) {
+        live[k] = __shfl(live[k], 0, 4);
+        key[k] = __shfl(key[k], 0, 4);
+        v[k] = live[k] ? reinterpret_cast<const uint4 *>(t.index + ((key[k] & 0xFFFFFFFFFFFFULL) & t.g.bkt_mask) * 64u)[q]
+                       : make_uint4(0u, 0u, 0u, 0u);
     }
-    // a fresh message each round: the batches of a previous use of the slab rewrote the opcodes
-    x[8] = kOpInv;
-    *reinterpret_cast<uint32_t *>(x + 12) = ver;
-    uint8_t *vv = vals + g * kOpMetaSize;
-    vv[8] = kOpVal;
-    *reinterpret_cast<uint32_t *>(vv + 12) = ver;
+    bool ok[kPeerTsPair];
+    uint64_t phys[kPeerTsPair];
+    U64x2w ln[kPeerTsPair];
+#pragma unroll
+    for (int k = 0; k < kPeerTsPair; ++k) {
+        const uint64_t s0 = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32), s1 = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
+        const uint32_t tag = (uint32_t)(key[k] >> 48);
+        const bool mt0 = live[k] && (s0 & 1u) && ((uint32_t)(s0 >> 1) & 0x7FFFFFu) == tag;
+        const bool mt1 = live[k] && (s1 & 1u) && ((uint32_t)(s1 >> 1) & 0x7FFFFFu) == tag;
+        const uint32_t g0 = (uint32_t)(__ballot(mt0) >> gbase) & 0xFu, g1 = (uint32_t)(__ballot(mt1) >> gbase) & 0xFu;
+        uint32_t o = 0;  // bit 2*l + j: slot 2*l + j matches (the reference's slot order)
+#pragma unroll
+        for (int l = 0; l < 4; ++l) o |= ((g0 >> l) & 1u) << (2 * l) | ((g1 >> l) & 1u) << (2 * l + 1);
+        const int first = o ? __ffs(o) - 1 : 0;
+        const uint64_t off = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
+        ok[k] = live[k] && o && t.g.log_head - off < t.g.log_cap;
+        phys[k] = off & t.g.log_mask;
+        // lane 0: entry bytes 0..15 (key at 8), lane 1: bytes 16..31 (version at 24)
+        ln[k] = ok[k] && q < 2 ? reinterpret_cast<const U64x2w *>(t.log + phys[k])[q] : U64x2w{0, 0};
+    }
+#pragma unroll
+    for (int k = 0; k < kPeerTsPair; ++k) {
+        const uint64_t ekey = __shfl(ln[k].b, 0, 4);
+        const uint32_t cur = (uint32_t)__shfl(ln[k].b, 1, 4);
+        if (q != 0 || !live[k]) continue;
+        uint8_t *x = invs + g[k] * op_size;
+        const uint8_t peer = (uint8_t)flags[k];
+        const bool rmw = (flags[k] >> 8) & 1u;
+        uint32_t ver = 2;
+        if (ok[k] && ekey == key[k]) {
+            ver = cur + ((!t.g.rmw_enabled || rmw) ? 2u : 4u);
+            if (peer_ts && peer < 8)
+                atomicMax(peer_ts + (phys[k] / t.g.entry_unit) * 8 + peer,
+                          ((unsigned long long)peer_round_tag(round) << 41) | ((unsigned long long)rmw << 40) |
+                              ((unsigned long long)ver << 8) | peer);
+        }
+        // a fresh message each round: the batches of a previous use of the slab rewrote the opcodes
+        x[8] = kOpInv;
+        *reinterpret_cast<uint32_t *>(x + 12) = ver;
+        uint8_t *vv = vals + g[k] * kOpMetaSize;
+        vv[8] = kOpVal;
+        *reinterpret_cast<uint32_t *>(vv + 12) = ver;
+    }
 }
 
 // The virtual peers' answers to this round's INVs: an ACK (ack_copy_and_modify_elem,
@@ -844,27 +866,39 @@ __global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32
 __global__ __launch_bounds__(1024) void k_ack_offsets(const int32_t *counts, int32_t n, int32_t n_peers, int32_t *off,
                                                       int32_t *h)
 {
+    // each thread owns 8 consecutive counts (one pass up to 8192 workers, loads issued together)
     __shared__ int32_t part[16], pmax[16];
     __shared__ int32_t carry;
     if (threadIdx.x == 0) carry = 0;
     int32_t mx = 0;
-    for (int32_t i0 = 0; i0 < n; i0 += 1024) {
+    for (int32_t i0 = 0; i0 < n; i0 += 8192) {
         __syncthreads();
-        const int32_t i = i0 + (int32_t)threadIdx.x;
-        const int32_t c = i < n ? counts[i] : 0;
-        mx = c > mx ? c : mx;
-        int32_t v = c * n_peers;  // inclusive scan within the wave, then across waves
+        const int32_t b = i0 + (int32_t)threadIdx.x * 8;
+        int32_t c[8], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c[k] = b + k < n ? counts[b + k] : 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            mx = c[k] > mx ? c[k] : mx;
+            sum += c[k] * n_peers;
+        }
+        int32_t v = sum;  // inclusive scan of the thread sums within the wave, then across waves
         for (int o = 1; o < 64; o <<= 1) {
             const int32_t u = __shfl_up(v, o, 64);
             if ((threadIdx.x & 63) >= (unsigned)o) v += u;
         }
         if ((threadIdx.x & 63) == 63) part[threadIdx.x >> 6] = v;
         __syncthreads();
-        int32_t before = carry;
-        for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) before += part[k];
-        if (i < n) off[i] = before + v - c * n_peers;
+        int32_t run = carry;
+        for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) run += part[k];
+        run += v - sum;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (b + k < n) off[b + k] = run;
+            run += c[k] * n_peers;
+        }
         __syncthreads();
-        if (threadIdx.x == 1023) carry = before + v;
+        if (threadIdx.x == 1023) carry = run;
     }
     for (int o = 32; o > 0; o >>= 1) {
         const int32_t u = __shfl_down(mx, o, 64);
@@ -986,7 +1020,6 @@ int hkv_wl_refill(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_s
     if (op_size > 64 && st_value >= 6 && (kOpValueOff - 16 + st_value) / 8 + 7 <= 64) {  // big ops: in place
         hipLaunchKernelGGL(k_refill_direct, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
                            st_value, shift, tkey, top, tlen, cursor, machine_id, first_iter, refill_all, counters);
-        hipLaunchKernelGGL(k_fold_counters, dim3(1), dim3(256), 0, (hipStream_t)stream, counters);
         return ok();
     }
     const size_t lds = (size_t)stride * op_size;
@@ -996,6 +1029,11 @@ int hkv_wl_refill(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_s
         return -1;
     hipLaunchKernelGGL(k_refill, dim3(n_workers), dim3(256), lds, (hipStream_t)stream, ops, stride, op_size, st_value,
                        shift, tkey, top, tlen, cursor, machine_id, first_iter, refill_all, counters);
+    return ok();
+}
+
+int hkv_wl_fold_counters(unsigned long long *counters, void *stream)
+{
     hipLaunchKernelGGL(k_fold_counters, dim3(1), dim3(256), 0, (hipStream_t)stream, counters);
     return ok();
 }
@@ -1091,8 +1129,9 @@ int hkv_wl_peer_ts(hkv_table *t, uint8_t *invs, uint8_t *vals, const int32_t *co
     TableView tv;
     if (table_view(t, &tv) || n_workers <= 0 || stride <= 0 || op_size % 8) return -1;
     const int64_t total = (int64_t)n_workers * stride;
-    hipLaunchKernelGGL(k_peer_ts, dim3(blocks_for(4 * total)), dim3(256), 0, (hipStream_t)stream, tv, invs, vals,
-                       counts, stride, op_size, peer_ts, round, total);
+    const int64_t per_block = 64 * kPeerTsPair;  // 4 lanes per element, kPeerTsPair elements per group
+    hipLaunchKernelGGL(k_peer_ts, dim3((unsigned)((total + per_block - 1) / per_block)), dim3(256), 0,
+                       (hipStream_t)stream, tv, invs, vals, counts, stride, op_size, peer_ts, round, total);
     return ok();
 }
 
@@ -1167,7 +1206,7 @@ int hkv_wl_collect_vals(uint8_t *acks, const int32_t *count, int32_t n_workers, 
 {
     if (n_workers <= 0) return 0;
     if (C <= 0 || ack_size % 8) return -1;
-    hipLaunchKernelGGL(k_collect_vals, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, acks, count, stride,
+    hipLaunchKernelGGL(k_collect_vals, dim3(n_workers), dim3(64), 0, (hipStream_t)stream, acks, count, stride,
                        ack_size, out, C, out_count, machine_id, held, offsets);
     return ok();
 }

@@ -44,6 +44,7 @@ _L.hkv_wl_regroup.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_i
                               ctypes.c_int32, _P, _P]
 _L.hkv_wl_collect_vals.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
                                    _P, ctypes.c_uint32, _P, _P, _P]
+_L.hkv_wl_fold_counters.argtypes = [_P, _P]
 _L.hkv_wl_pack_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_marshal_acks_aligned.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P,
                                            ctypes.c_uint32, ctypes.c_uint32, _P]
@@ -232,8 +233,13 @@ class ReplicaRound:
         """After the VAL totals are gathered (host synchronisation): the largest of them"""
         return max(1, int(self.val_totals.max().item()))
 
+    def fold_counters(self) -> torch.Tensor:
+        """counters[0..4] brought up to date (refill leaves per-worker-group partial sums)"""
+        check(_L.hkv_wl_fold_counters(_ptr(self.counters), _s()), "fold_counters")
+        return self.counters
+
     def stats(self) -> dict:
-        c = self.counters[:3].cpu().tolist()
+        c = self.fold_counters()[:3].cpu().tolist()
         h = self.held.cpu().tolist()
         return {"committed": c[0], "misses": c[1], "writes_completed": c[2], "invs_held": h[0], "vals_dropped": h[1]}
 
@@ -266,6 +272,7 @@ class ReplicaGroupRound:
         self.R = world - 1
         self.rstride = self.r.C * self.R
         self.counters = self.r.counters
+        self.fold_counters = self.r.fold_counters
         self.inv_total = self.r.inv_total
         self.elem_totals = self.r.elem_totals
 

@@ -32,6 +32,7 @@ _L.hkv_wl_gen_trace.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctyp
                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, _P]
 _L.hkv_wl_refill.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                              _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, _P, _P]
+_L.hkv_wl_fold_counters.argtypes = [_P, _P]
 _L.hkv_wl_marshal_invs.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_invs_cap.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
                                        ctypes.c_uint32, _P, _P]
@@ -426,11 +427,16 @@ class Round:
         self.alive -= 1
         self.fit = self.fit and self.alive > 0
 
+    def fold_counters(self) -> torch.Tensor:
+        """counters[0..4] brought up to date (refill leaves per-worker-group partial sums)"""
+        check(_L.hkv_wl_fold_counters(_ptr(self.counters), _s()), "fold_counters")
+        return self.counters
+
     def committed(self) -> int:
-        return int(self.counters[0].item())
+        return int(self.fold_counters()[0].item())
 
     def stats(self) -> dict:
-        c = self.counters[:5].cpu().tolist()
+        c = self.fold_counters()[:5].cpu().tolist()
         d = {"committed": c[0], "misses": c[1], "writes_completed": c[2], "dropped": c[3], "rmw_aborts": c[4],
              "invs_held": int(self.held.item())}
         if self.V is not None:

@@ -51,18 +51,20 @@ int hkv_wl_gen_trace(uint64_t *d_trace_key, uint8_t *d_trace_op, uint32_t *d_tra
  * refill_all, stalled ops (GET/PUT/RMW stalls, ST_EMPTY, ST_NEW) are dropped instead of
  * retried and take a fresh command too; ops in flight (PUT/RMW/REPLAY_SUCCESS, IN_PROGRESS_*,
  * *_COMPLETE_SEND_VALS, membership change) always keep their slot.
- * Adds completed-and-committed ops (everything complete except ST_MISS and ST_RMW_ABORT)
- * to d_counters[0], misses to d_counters[1], completed writes to d_counters[2], dropped
- * stalled ops to d_counters[3], RMW aborts (ST_RMW_ABORT) to d_counters[4].
- * d_counters holds HKV_WL_COUNTER_WORDS words, zeroed by the caller once: words from
- * HKV_WL_STRIPE_BASE on are per-worker-group partial sums the call folds back into [0..4]
- * (one counter address hit by every worker serialises in L2). */
+ * Counts completed-and-committed ops (everything complete except ST_MISS and ST_RMW_ABORT),
+ * misses, completed writes, dropped stalled ops and RMW aborts (ST_RMW_ABORT) into
+ * d_counters: HKV_WL_COUNTER_WORDS words, zeroed by the caller once, of which the words from
+ * HKV_WL_STRIPE_BASE on are per-worker-group partial sums (one counter address hit by every
+ * worker serialises in L2); hkv_wl_fold_counters adds them into d_counters[0..4] when the
+ * caller reads the totals. */
 #define HKV_WL_COUNTER_WORDS 4096
 #define HKV_WL_STRIPE_BASE 64
 int hkv_wl_refill(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint32_t st_value,
                   uint32_t shift, const uint64_t *d_trace_key, const uint8_t *d_trace_op, int32_t trace_len,
                   uint32_t *d_cursor, uint32_t machine_id, int32_t first_iter, int32_t refill_all,
                   unsigned long long *d_counters, void *stream);
+/* d_counters[0..4] += the refill stripes (which are cleared) */
+int hkv_wl_fold_counters(unsigned long long *d_counters, void *stream);
 
 /* INVs for this round's successful writes/RMWs/replays: per worker, compacted into
  * d_inv_out[w*stride ..] (op_size-byte spacetime_inv_t, sender = machine_id), count in

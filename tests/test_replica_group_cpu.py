@@ -37,6 +37,7 @@ class TagReplica:
         self.val_pack, self.val_off, self.val_totals = z(W * C), zi(W + 1), zi(N)
         self.val_recv = z(N * W * C)
         self.counters = z(4)
+        self.fold_counters = lambda: self.counters
         self.inv_total = z(1)
         self.elem_totals = z(3)
         self.count_elems = True

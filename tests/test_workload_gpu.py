@@ -260,6 +260,7 @@ def test_refill_kernel_matches_numpy(big, refill_all):
     d_cnt = torch.zeros(4096, dtype=torch.int64, device="cuda")
     WL.check(WL._L.hkv_wl_refill(WL._ptr(d_ops), W, S, osz, sz.st_value, sz.shift, WL._ptr(d_tkey), WL._ptr(d_top),
                                  tlen, WL._ptr(d_cur), mid, 0, refill_all, WL._ptr(d_cnt), None), "refill")
+    WL.check(WL._L.hkv_wl_fold_counters(WL._ptr(d_cnt), None), "fold")
     torch.cuda.synchronize()
     got = d_ops.cpu().numpy()
     if not np.array_equal(got, exp_ops):

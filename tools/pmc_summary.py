@@ -17,7 +17,8 @@ for f in glob.glob(f"gpurun_out/{tag}/pmc/*/run_counter_collection.csv"):
             short = "rocprim:" + ("onesweep" if "onesweep" in name else "scan" if "scan" in name else "other")
         res[(short, r.get("Grid_Size", ""))][r["Counter_Name"]].append(float(r["Counter_Value"]))
 cols = sorted({c for v in res.values() for c in v})
-hdr = f"{'kernel':40s} {'grid':>9s} " + " ".join(f"{c[:14]:>14s}" for c in cols)
+short = lambda c: c.replace("TCC_EA0_", "").replace("_sum", "")[:14]  # noqa: E731
+hdr = f"{'kernel':40s} {'grid':>9s} " + " ".join(f"{short(c):>14s}" for c in cols)
 print(hdr)
 def key(kv):
     v = kv[1].get(cols[0], [0])

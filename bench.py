@@ -146,8 +146,10 @@ def main():
 
     if world > 1:
         from hermes_amd.replica_group import ReplicaGroupRound
+        # cfg5: the membership comes from Hades agreement over per-round heartbeats (SURVEY 8(f)
+        # row 4): the failed rank stops heartbeating and the survivors expel it when they agree
         rnd = ReplicaGroupRound(kvs, a.workers, z, a.write_permille, seed=a.seed, world=world, rank=rank,
-                                retry_stalled=a.retry)
+                                retry_stalled=a.retry, hades=cfg5)
     else:
         machines = 8 if cfg5 else 3
         rnd = Round(kvs, a.workers, L.membership(machines, 0), list(range(1, machines)), z, a.write_permille,
@@ -261,7 +263,8 @@ def main():
         "config": {
             "workload": (f"cfg5: {world}x MI355X, {8 if world == 1 else world}-replica group "
                          f"({'7 virtual peers' if world == 1 else 'RCCL'}), {a.keys} keys/replica, 20% writes, "
-                         f"replica {drop_id} fails in timed step {drop_at} (membership change, write replays)"
+                         f"replica {drop_id} fails in timed step {drop_at} (membership change"
+                         f"{' agreed by Hades heartbeats' if world > 1 else ''}, write replays)"
                          if cfg5 else
                          f"cfg3: 1xMI355X RMW-heavy, {a.keys} keys, RMWs on, 287 B values, Zipf 0.99, 25% PUT + 25% RMW, "
                          "INV/ACK/VAL from 2 virtual replicas" if cfg3 else
@@ -312,6 +315,9 @@ def main():
         mb = rnd.mb if world == 1 else rnd.r.mb
         out["detail"]["membership"] = {"machines": 8 if world == 1 else world, "dropped": drop_id,
                                        "at_timed_step": drop_at, "g_membership_after": mb[1]}
+        if world > 1:
+            g, epoch = rnd.r.hades.state() if not rnd.r.failed else (None, None)
+            out["detail"]["membership"].update(agreement="hades", epoch=epoch)
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if world == 1 and not a.retry and a.retry_steps > 0 and not cfg5:

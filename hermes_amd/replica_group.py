@@ -34,6 +34,7 @@ import torch
 from . import layout as L
 from .kvs import HermesKV
 from .lib import check, raw
+from .hades import NO_VIEW, Hades, MajorityLost, exchange_views
 from .workload import HkvZipf, _ptr, _s, slots_per_worker  # noqa: F401 (re-exported)
 
 _L = raw()
@@ -112,6 +113,19 @@ class ReplicaRound:
                                   ctypes.c_uint64(seed ^ (rank << 48)), _s()), "gen_trace")
         self.failed = False            # this replica has failed (fail()): it sends nothing more
         self.refill(first=True)
+
+    # -- Hades: one view-update period per round when enabled
+    def hades_start(self):
+        self.hades = Hades(self.N, self.rank)
+
+    def hades_row(self, changed: bool) -> bytes:
+        """this replica's heartbeats (one 4-byte view per destination) and a 4-byte trailer:
+        [membership changed this period, membership is the whole group]; a failed replica sends
+        nothing"""
+        if self.failed:
+            return bytes([NO_VIEW, 0, 0, 0]) * self.N + bytes(4)
+        g, _ = self.hades.state()
+        return self.hades.views_row() + bytes([int(changed), int(g == (1 << self.N) - 1), 0, 0])
 
     # -- phases (all asynchronous on torch's current stream)
     def fail(self):
@@ -212,17 +226,25 @@ class ReplicaRound:
         self.kvs.batch(L.BatchType.vals, self.val_recv, self.N, width, L.OP_META_SIZE, self.mb,
                        counts=self.val_totals)
 
-    def membership_change(self, peer: int):
-        """The group drops `peer` (group_membership_update, inline-util.h:26-43). Every worker runs
-        the after-membership-change batch over its ops (hermes_worker.c:526-542); the VALs of the
+    def membership_change(self, peer: int | None = None, membership: bytes | None = None):
+        """The group drops `peer` (group_membership_update, inline-util.h:26-43), or takes the
+        spacetime_group_membership Hades agreed on (`membership`). Every worker runs the
+        after-membership-change batch over its ops (hermes_worker.c:526-542); the VALs of the
         writes and replays it completed are packed into val_pack for one more VAL exchange
-        (memb_change_* callbacks, hermes_worker.c:163-203). A failed replica sends none."""
+        (memb_change_* callbacks, hermes_worker.c:163-203). A failed replica, or one whose
+        membership did not change (both None), sends none."""
         W, C = self.W, self.C
-        if self.failed:
+        if self.failed or (peer is None and membership is None):
             self.val_off[W:].zero_()
             return
-        g = self.mb[1] & ~(1 << peer) & 0xFF
-        self.mb = L.membership(0, self.rank, alive=g)
+        if membership is not None:
+            g = membership[1]
+            if bin(g).count("1") < self.N // 2:   # inline-util.h:39-42: "Majority is down!"
+                raise MajorityLost(f"replica {self.rank}: membership {g:#04x} of {self.N}")
+            self.mb = bytes(membership[:3]) + bytes(5)
+        else:
+            g = self.mb[1] & ~(1 << peer) & 0xFF
+            self.mb = L.membership(0, self.rank, alive=g)
         self.kvs.batch(L.BatchType.local_ops_after_membership_change, self.ops, W, LOCAL, self.op, self.mb)
         check(_L.hkv_wl_marshal_memb_vals(_ptr(self.ops), W, LOCAL, self.op, _ptr(self.val_slab), C,
                                           _ptr(self.val_count), self.rank, _s()), "marshal_memb_vals")
@@ -262,13 +284,20 @@ class ReplicaGroupRound:
     LOCAL = LOCAL
 
     def __init__(self, kvs: HermesKV | None, n_workers: int, zipf: HkvZipf | None, write_permille: int = 200, *,
-                 seed: int = 0x5EED, world: int, rank: int, group=None, replica=None, **kw):
-        """`replica`: drive an existing ReplicaRound-shaped object instead of building one."""
+                 seed: int = 0x5EED, world: int, rank: int, group=None, replica=None, hades: bool = False, **kw):
+        """`replica`: drive an existing ReplicaRound-shaped object instead of building one.
+        `hades`: the membership comes from Hades agreement over heartbeats exchanged every round
+        (a failed rank is expelled when the survivors agree), instead of a host-driven drop."""
         import torch.distributed as dist
         self.dist = dist
         self.group = group
         self.r = replica if replica is not None else ReplicaRound(kvs, n_workers, world, rank, zipf,
                                                                   write_permille, seed=seed, **kw)
+        self.hades = hades
+        self.world = world
+        if hades:
+            self.r.hades_start()
+            self._hades_bootstrap()
         self.R = world - 1
         self.rstride = self.r.C * self.R
         self.counters = self.r.counters
@@ -290,10 +319,53 @@ class ReplicaGroupRound:
     def _a2a(self, out, inp):
         self.dist.all_to_all_single(out, inp, group=self.group)
 
+    def _views(self, changed: bool) -> bytes:
+        """one heartbeat exchange: all ranks' rows gathered (row = sender), this rank polls its
+        column. Returns the gathered table."""
+        r, n = self.r, self.world
+        row = torch.tensor(list(r.hades_row(changed)), dtype=torch.uint8, device=r.ops.device)
+        out = torch.empty(n * row.numel(), dtype=torch.uint8, device=r.ops.device)
+        self._gather(out, row)
+        table = bytes(out.cpu().tolist())
+        if not r.failed:
+            w = 4 * n + 4
+            r.hades.receive_column(b"".join(table[s * w:s * w + 4 * n] for s in range(n)))
+        return table
+
+    def _trailers(self, table: bytes) -> list[bytes]:
+        w = 4 * self.world + 4
+        return [table[s * w + 4 * self.world:(s + 1) * w] for s in range(self.world)]
+
+    def _hades_bootstrap(self, max_periods: int = 16):
+        """spin_until_all_nodes_are_in_membership (hermes_worker.c:245-259): heartbeat periods
+        until every rank's membership is the whole group"""
+        for _ in range(max_periods):
+            self.r.hades.update()
+            if all(t[1] for t in self._trailers(self._views(False))):
+                return
+        raise RuntimeError("Hades bootstrap did not reach the full membership")
+
+    def _hades_period(self):
+        """update_view_and_issue_hbs + group_membership_update + poll_for_remote_views
+        (hermes_worker.c:262-291); when any rank's membership changed, the ranks whose membership
+        changed run the after-membership-change batch and every rank joins one VAL exchange"""
+        r = self.r
+        changed, mb = False, None
+        if not r.failed:
+            changed, mb, _ = r.hades.update()
+        table = self._views(changed)
+        if any(t[0] for t in self._trailers(table)):
+            r.membership_change(membership=mb if changed else None)
+            self._gather(*r.val_total_io())
+            w2 = r.val_width()
+            self._gather(*r.val_io(w2))
+            r.vals(w2)
+
     def step(self, events: dict | None = None, timed_batches=None, drop: int | None = None):
         """One protocol round. `drop`: that rank fails once its INVs of this round are out (no
         ACKs or VALs from it); the round ends with a membership change and one more VAL
-        exchange for the writes it completes."""
+        exchange for the writes it completes -- or, with Hades, the failed rank stops
+        heartbeating and the survivors expel it when they agree (two periods later)."""
         r = self.r
         _timed(events, "local", r.local, timed_batches)
         self._gather(*r.inv_total_io())
@@ -307,7 +379,9 @@ class ReplicaGroupRound:
         self._gather(*r.val_total_io())
         self._gather(*r.val_io(width))
         _timed(events, "vals", lambda: r.vals(width), timed_batches)
-        if drop is not None:
+        if self.hades:
+            self._hades_period()
+        elif drop is not None:
             r.membership_change(drop)
             self._gather(*r.val_total_io())
             w2 = r.val_width()
@@ -324,9 +398,43 @@ class LoopbackGroup:
     exactly the layouts the RCCL driver produces (all-gather: row p = rank p's slab;
     all-to-all: row p of the output = row `rank` of rank p's input)."""
 
-    def __init__(self, rounds: list[ReplicaRound]):
+    def __init__(self, rounds: list[ReplicaRound], hades: bool = False):
         self.rounds = rounds
         self.N = len(rounds)
+        self.hades = hades
+        self.hades_changes = []        # (round, rank, membership) of every agreed change
+        self.clock = 0
+        if hades:
+            for r in rounds:
+                r.hades_start()
+            full = (1 << self.N) - 1
+            for _ in range(16):        # spin_until_all_nodes_are_in_membership
+                for r in rounds:
+                    r.hades.update()
+                exchange_views([r.hades for r in rounds])
+                if all(r.hades.state()[0] == full for r in rounds):
+                    break
+            else:
+                raise RuntimeError("Hades bootstrap did not reach the full membership")
+
+    def _hades_period(self):
+        rs = self.rounds
+        res = {}
+        for r in rs:
+            if not r.failed:
+                res[r.rank] = r.hades.update()
+        exchange_views([None if r.failed else r.hades for r in rs])
+        if any(ch for ch, _, _ in res.values()):
+            for r in rs:
+                ch, mb, _ = res.get(r.rank, (False, None, False))
+                if ch:
+                    self.hades_changes.append((self.clock, r.rank, mb))
+                r.membership_change(membership=mb if ch else None)
+            self._gather_io([r.val_total_io() for r in rs])
+            w2 = max(r.val_width() for r in rs)
+            self._gather_io([r.val_io(w2) for r in rs])
+            for r in rs:
+                r.vals(w2)
 
     @staticmethod
     def _gather(outs, ins):
@@ -365,7 +473,9 @@ class LoopbackGroup:
         self._gather_io([r.val_io(width) for r in rs])
         for r in rs:
             r.vals(width)
-        if drop is not None:
+        if self.hades:
+            self._hades_period()
+        elif drop is not None:
             for r in rs:
                 r.membership_change(drop)
             self._gather_io([r.val_total_io() for r in rs])
@@ -375,3 +485,4 @@ class LoopbackGroup:
                 r.vals(w2)
         for r in rs:
             r.refill()
+        self.clock += 1

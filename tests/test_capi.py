@@ -4,7 +4,7 @@ import re
 import subprocess
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("hermeskv.h", "hermeskv_workload.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("hermeskv.h", "hermeskv_workload.h", "hermeskv_hades.h")]
 LIB = os.path.join(ROOT, "hermes_amd", "libhermeskv.so")
 
 

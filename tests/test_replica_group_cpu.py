@@ -210,3 +210,91 @@ def test_slots_per_worker():
     assert slots_per_worker(0) == 8
     assert slots_per_worker(1000) == 250
     assert 125 < slots_per_worker(500) <= 250
+
+
+class HadesReplica:
+    """Stand-in for ReplicaRound in Hades mode: only heartbeats, membership changes and the
+    VAL exchange that follows one (every rank joins it; ranks without a change send nothing)."""
+
+    from hermes_amd.replica_group import ReplicaRound as _RR
+    hades_start = _RR.hades_start
+    hades_row = _RR.hades_row
+
+    def __init__(self, world, rank, W=3):
+        self.N, self.rank, self.W, self.C = world, rank, W, 1
+        self.failed = False
+        z = torch.zeros
+        self.counters, self.inv_total, self.elem_totals = z(4), z(1), z(3)
+        self.fold_counters = lambda: self.counters
+        self.ops = torch.zeros(1, dtype=torch.uint8)
+        self.val_off = torch.zeros(W + 1, dtype=torch.int32)
+        self.val_totals = torch.zeros(world, dtype=torch.int32)
+        self.val_pack = torch.zeros(16, dtype=torch.int64)
+        self.val_recv = torch.zeros(world * 16, dtype=torch.int64)
+        self.changes = []       # (period, g) of this rank's membership changes
+        self.memb_exchanges = 0
+        self.period = 0
+
+    def membership_change(self, peer=None, membership=None):
+        if self.failed or membership is None:
+            self.val_off.zero_()
+            return
+        self.changes.append((self.period, membership[1]))
+        self.val_off[self.W] = 1 + self.rank
+        self.val_pack[:1 + self.rank] = 100 + self.rank
+
+    def val_total_io(self):
+        return self.val_totals, self.val_off[self.W:]
+
+    def val_width(self):
+        return max(1, int(self.val_totals.max()))
+
+    def val_io(self, width):
+        return self.val_recv[:self.N * width], self.val_pack[:width]
+
+    def vals(self, width):
+        self.memb_exchanges += 1
+
+
+def _hades_worker(rank, world, port, periods, dead, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rep = HadesReplica(world, rank)
+        drv = ReplicaGroupRound(None, rep.W, None, world=world, rank=rank, replica=rep, hades=True)
+        assert rep.hades.state()[0] == (1 << world) - 1       # bootstrap: the whole group
+        for p in range(periods):
+            rep.period = p
+            if rank == dead[0] and p == dead[1]:
+                rep.failed = True
+            drv._hades_period()
+        q.put((rank, rep.changes, rep.memb_exchanges, rep.hades.state(), None))
+    except Exception as e:  # surfaced by the parent
+        q.put((rank, None, 0, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,dead", [(3, (2, 2)), (4, (1, 3))])
+def test_hades_membership_over_gloo(world, dead):
+    """ReplicaGroupRound(hades=True): heartbeats all-gathered every round, a failed rank stops
+    sending them, and the survivors agree on its expulsion in the same period with a new epoch;
+    every rank (the failed one with nothing to send) joins the one VAL exchange that follows"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    periods = 8
+    procs = [ctx.Process(target=_hades_worker, args=(r, world, port, periods, dead, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for rank, changes, exch, state, err in res:
+        assert err is None, f"rank {rank}: {err}"
+    want = ((1 << world) - 1) & ~(1 << dead[0])
+    live = [x for x in res if x[0] != dead[0]]
+    assert all(len(x[1]) == 1 and x[1][0][1] == want for x in live), res
+    assert len({x[1][0][0] for x in live}) == 1 and live[0][1][0][0] <= dead[1] + 2, res
+    assert len({x[3] for x in live}) == 1                      # same membership and epoch
+    assert all(x[2] == 1 for x in res), res                     # one VAL exchange, joined by all

@@ -138,6 +138,57 @@ def test_loopback_group_membership_change(n_rep):
         assert st["invs_held"] == 0 and st["vals_dropped"] == 0 and st["writes_completed"] > 0, st
 
 
+def test_loopback_group_hades_membership():
+    """SURVEY 8(f) row 4 on the GPU: the membership comes from Hades agreement (hkv_hades_*) over
+    heartbeats exchanged every round. Replica 3 of 4 fails in round 1 after its INVs; the others
+    keep issuing writes that wait for its ACK until they agree to expel it (the same round on every
+    survivor, within two periods, with a new epoch), run the after-membership-change batch under
+    the agreed membership and exchange the VALs of the writes it completes. Every launch is
+    mirrored into the oracle; once the change is in, the survivors agree on every key, and a key
+    is either VALID or INVALID with the failed replica's write."""
+    from hermes_amd.kvs import HermesKV
+    from hermes_amd.replica_group import LoopbackGroup, ReplicaRound
+    from hermes_amd.workload import zipf_params
+
+    n_rep, n_keys, bkts, cap = 4, 4000, 8192, 1 << 20
+    z = zipf_params(n_keys, 0.99)
+    reps, mirrors = [], []
+    for r in range(n_rep):
+        g = HermesKV(n_keys, bkts, cap, machine_id=r)
+        o = OracleKVS(bkts, cap, r)
+        o.populate(n_keys, L.DEFAULT.kvs_value)
+        mirrors.append(Mirror(g, o, f"replica {r}"))
+        reps.append(ReplicaRound(g, 16, n_rep, r, z, 400, seed=77 + r, trace_len=512))
+    grp = LoopbackGroup(reps, hades=True)
+    e0 = reps[0].hades.state()[1]
+    keys = gen_keys(n_keys)
+    dead = n_rep - 1
+    for step in range(6):
+        grp.step(drop=dead if step == 1 else None)
+        torch.cuda.synchronize()
+        changed = [c for c in grp.hades_changes]
+        if not changed or changed[0][0] == step:
+            continue            # writes may still wait for the failed replica's ACKs
+        imgs = [_key_images(m.g, m.o, keys) for m in mirrors[:dead]]
+        for i in range(len(keys)):
+            base = imgs[0][i]
+            for r in range(1, dead):
+                assert imgs[r][i] == base, f"round {step}: key #{i} differs between replica 0 and {r}"
+            if base is not None:
+                assert base[0] in (L.State.VALID, L.State.INVALID), f"round {step}: key #{i} state {base[0]}"
+                if base[0] == L.State.INVALID:
+                    assert base[1] == dead, f"round {step}: key #{i} INVALID by {base[1]}"
+    want = ((1 << n_rep) - 1) & ~(1 << dead)
+    ch = grp.hades_changes
+    assert sorted(c[1] for c in ch) == list(range(dead)), ch          # every survivor, once
+    assert len({c[0] for c in ch}) == 1 and 1 <= ch[0][0] <= 3, ch     # together, within two periods
+    for rep in reps[:dead]:
+        g, e = rep.hades.state()
+        assert g == want and e == e0 + 1 and rep.mb[1] == want and rep.mb[2] == ((~want | (1 << rep.rank)) & 0xFF)
+        st = rep.stats()
+        assert st["invs_held"] == 0 and st["vals_dropped"] == 0 and st["writes_completed"] > 0, st
+
+
 def _dist_child(rank, world, port, q, drop=None):
     import os
 

@@ -155,7 +155,7 @@ def main():
         rnd = Round(kvs, a.workers, L.membership(machines, 0), list(range(1, machines)), z, a.write_permille,
                     a.rmw_permille, seed=a.seed,
                     max_steps=total_steps + 2, retry_stalled=a.retry, fit_ack_stride=not a.no_fit_acks,
-                    val_credits=a.val_credits)
+                    val_credits=a.val_credits, hades=cfg5)
     torch.cuda.synchronize()
 
     for _ in range(a.warmup):
@@ -264,7 +264,7 @@ def main():
             "workload": (f"cfg5: {world}x MI355X, {8 if world == 1 else world}-replica group "
                          f"({'7 virtual peers' if world == 1 else 'RCCL'}), {a.keys} keys/replica, 20% writes, "
                          f"replica {drop_id} fails in timed step {drop_at} (membership change"
-                         f"{' agreed by Hades heartbeats' if world > 1 else ''}, write replays)"
+                         " agreed by Hades heartbeats, write replays)"
                          if cfg5 else
                          f"cfg3: 1xMI355X RMW-heavy, {a.keys} keys, RMWs on, 287 B values, Zipf 0.99, 25% PUT + 25% RMW, "
                          "INV/ACK/VAL from 2 virtual replicas" if cfg3 else
@@ -315,9 +315,10 @@ def main():
         mb = rnd.mb if world == 1 else rnd.r.mb
         out["detail"]["membership"] = {"machines": 8 if world == 1 else world, "dropped": drop_id,
                                        "at_timed_step": drop_at, "g_membership_after": mb[1]}
-        if world > 1:
-            g, epoch = rnd.r.hades.state() if not rnd.r.failed else (None, None)
-            out["detail"]["membership"].update(agreement="hades", epoch=epoch)
+        hz = rnd.hades[0] if world == 1 else (rnd.r.hades if not rnd.r.failed else None)
+        out["detail"]["membership"].update(agreement="hades", epoch=hz.state()[1] if hz else None)
+        if world == 1:
+            out["detail"]["membership"]["agreed_at_round"] = [c[0] for c in rnd.hades_changes]
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if world == 1 and not a.retry and a.retry_steps > 0 and not cfg5:

@@ -107,7 +107,8 @@ class Round:
                  zipf: HkvZipf, write_permille: int = 200, rmw_permille: int = 0,
                  remote_per_peer: int = 50, trace_len: int = 8192, seed: int = 0x5EED,
                  virtual_peers: bool = True, max_steps: int = 64, retry_stalled: bool = False,
-                 fit_ack_stride: bool = True, val_credits: int | None = None, pack_remote: bool = True):
+                 fit_ack_stride: bool = True, val_credits: int | None = None, pack_remote: bool = True,
+                 hades: bool = False):
         self.kvs = kvs
         self.W = n_workers
         self.mb = membership
@@ -187,6 +188,9 @@ class Round:
         self.drops = []                # peers dropped from the membership (membership_change)
         self.alive = self.R            # live peers: the first `alive` slots of the remote slabs
         self._counts = {}
+        self.hades = None
+        if hades:
+            self._hades_start()
         self._gen_remote()
         self.refill(first=True)
 
@@ -397,7 +401,11 @@ class Round:
                 self.elem_totals[0] += ic.sum()
                 if alive:
                     self.elem_totals[2] += vc.sum()
-        if drop is not None:
+        if self.hades is not None:
+            if drop is not None:         # the peer is gone; the membership follows the agreement
+                self._peer_gone(drop)
+            self._hades_period()
+        elif drop is not None:
             self.membership_change(drop)
         self.refill()
         self.clock += 1
@@ -418,14 +426,53 @@ class Round:
         (hkv_wl_marshal_memb_vals). From now on the peer's slot of the remote slabs is not applied;
         reads of keys it left INVALID replay the write (early value propagation)."""
         g = self.mb[1] & ~(1 << peer) & 0xFF
-        self.mb = L.membership(0, self.machine_id, alive=g)
+        self._after_membership_change(L.membership(0, self.machine_id, alive=g))
+        self._peer_gone(peer)
+
+    def _peer_gone(self, peer: int):
+        self.drops.append(peer)
+        self.alive -= 1
+        self.fit = self.fit and self.alive > 0
+
+    def _after_membership_change(self, mb: bytes):
+        self.mb = mb
         self.kvs.batch(L.BatchType.local_ops_after_membership_change, self.ops, self.W, self.LOCAL, self.op, self.mb)
         check(_L.hkv_wl_marshal_memb_vals(_ptr(self.ops), self.W, self.LOCAL, self.op, _ptr(self.val_out),
                                           self.ack_stride, _ptr(self.val_count), self.machine_id, _s()),
               "marshal_memb_vals")
-        self.drops.append(peer)
-        self.alive -= 1
-        self.fit = self.fit and self.alive > 0
+
+    # -- Hades (SURVEY 8(f) row 4): this replica and every virtual peer run the agreement
+    def _hades_start(self):
+        from .hades import Hades, exchange_views
+        ids = [self.machine_id] + self.peers
+        self.hades_n = max(ids) + 1
+        self.hades = {i: Hades(self.hades_n, i) for i in ids}
+        self.hades_changes = []         # (round, agreed g_membership) of this replica's changes
+        self._exchange = exchange_views
+        full = sum(1 << i for i in ids)
+        for _ in range(16):             # spin_until_all_nodes_are_in_membership
+            for h in self.hades.values():
+                h.update()
+            self._exchange([self.hades.get(i) for i in range(self.hades_n)])
+            if all(h.state()[0] == full for h in self.hades.values()):
+                return
+        raise RuntimeError("Hades bootstrap did not reach the full membership")
+
+    def _hades_period(self):
+        """update_view_and_issue_hbs + group_membership_update + poll_for_remote_views
+        (hermes_worker.c:262-291) for this replica and its live virtual peers; a failed peer no
+        longer heartbeats. When this replica's agreed membership changes, every worker runs the
+        after-membership-change batch under it."""
+        from .hades import MajorityLost
+        live = {i: h for i, h in self.hades.items() if i not in self.drops}
+        res = {i: h.update() for i, h in live.items()}
+        self._exchange([live.get(i) for i in range(self.hades_n)])
+        changed, mb, _ = res[self.machine_id]
+        if changed:
+            if bin(mb[1]).count("1") < self.hades_n // 2:   # inline-util.h:39-42
+                raise MajorityLost(f"membership {mb[1]:#04x} of {self.hades_n}")
+            self.hades_changes.append((self.clock, mb[1]))
+            self._after_membership_change(bytes(mb[:3]) + bytes(5))
 
     def fold_counters(self) -> torch.Tensor:
         """counters[0..4] brought up to date (refill leaves per-worker-group partial sums)"""

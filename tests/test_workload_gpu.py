@@ -125,6 +125,52 @@ def test_membership_change_round_mirrored(machines):
     assert g.take_error_flags() == 0
 
 
+@pytest.mark.parametrize("machines", [3, 8])
+def test_hades_membership_round_mirrored(machines):
+    """SURVEY 8(f) row 4 on one GPU: this replica and its virtual peers run the Hades agreement
+    (hkv_hades_*) over heartbeats every round. The last peer fails in round 2 after its INVs; the
+    writes waiting for its ACK stay in flight until the survivors agree to expel it (every live
+    node in the same period, within two periods, with a new epoch); then the after-membership-change
+    batch runs under the agreed membership and later reads replay what it left INVALID. Every
+    launch is mirrored into the oracle."""
+    from hermes_amd.kvs import HermesKV
+    from hermes_amd.workload import Round, zipf_params
+    n_keys, bkts, cap = 60_000, 1 << 16, 1 << 23
+    g = HermesKV(n_keys, bkts, cap, machine_id=0)
+    o = OracleKVS(bkts, cap, 0)
+    o.populate(n_keys, g.sizes.kvs_value)
+    m = Mirror(g, o, "hades round")
+    peers = list(range(1, machines))
+    r = Round(g, 40, L.membership(machines, 0), peers, zipf_params(n_keys, 0.99), 200, seed=0x5EED,
+              max_steps=10, trace_len=1024, remote_per_peer=20, hades=True)
+    e0 = r.hades[0].state()[1]
+    op = g.sizes.op
+    replays = []
+    marshal = r.marshal_invs
+
+    def counting_marshal():
+        replays.append(int((r.ops.view(-1, op)[:, 9] == int(L.Resp.REPLAY_SUCCESS)).sum()))
+        marshal()
+    r.marshal_invs = counting_marshal
+    steps = 8
+    for step in range(steps):
+        r.step(drop=peers[-1] if step == 2 else None)
+    torch.cuda.synchronize()
+    want = ((1 << machines) - 1) & ~(1 << peers[-1])
+    assert len(r.hades_changes) == 1 and r.hades_changes[0][1] == want, r.hades_changes
+    at = r.hades_changes[0][0]
+    assert 2 <= at <= 4, r.hades_changes
+    assert m.launches == steps * 4 + 1
+    assert r.mb[1] == want and r.mb[2] == (~want | 1) & 0xFF
+    for i, h in r.hades.items():
+        if i != peers[-1]:
+            assert h.state() == (want, e0 + 1), (i, h.state())
+    st = r.stats()
+    assert st["committed"] > 0 and st["writes_completed"] > 0, st
+    assert sum(replays[at + 1:]) > 0, replays
+    assert g.take_error_flags() == 0
+
+
 @pytest.mark.parametrize("credits,cfg3", [(3, False), (6, True)])
 def test_val_credits_round_mirrored(credits, cfg3):
     """VALs under credits and the outstanding-VAL gate (hermes_worker.c:479-503).

@@ -28,8 +28,12 @@ PROBE_STEPS = 3                # untimed steps with every batch launch timed
 # algorithmic bytes per element, SURVEY.md 8(d): S_op (56, or 312 big), bucket 64, entry (64, or
 # 320 big), S_msg 16 (ACKs carry S_op with RMWs)
 def elem_bytes(op: int, entry: int, ack: int) -> dict:
+    """Algorithmic HBM bytes per element: the element read and written, the bucket,
+    the entry read (and written when it changes). ACKs and VALs touch only the entry's first
+    64-B line (key and meta); GETs, PUTs and INVs the whole entry (value)."""
+    meta = min(entry, 64)
     return {"get": op + 64 + entry + op, "put": op + 64 + 2 * entry + op, "inv": op + 64 + 2 * entry + op,
-            "ack": ack + 64 + 2 * entry + ack, "val": 16 + 64 + 2 * entry + 16}
+            "ack": ack + 64 + 2 * meta + ack, "val": 16 + 64 + 2 * meta + 16}
 
 
 def parse():

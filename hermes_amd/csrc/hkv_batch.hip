@@ -93,6 +93,7 @@ struct BatchArgs {
     uint32_t done_value;
     unsigned long long *prof;    // HKV_SMALL_PROF: phase timestamps of k_small (debug)
     const SmallBatch *hdr;       // mixed small launches: the batch headers (in dev_region)
+    uint8_t *state_out;          // local launches: each element's final state byte (may be NULL)
 };
 
 // Rounds after round 0 per batch type: how often a hot key usually mutates in one launch beyond
@@ -203,6 +204,12 @@ __device__ __forceinline__ void elem_at(const BatchArgs &a, uint32_t i, uint8_t 
         c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
     }
     x = a.elems + (int64_t)i * a.esz;
+}
+
+// the state mirror of a local launch: written by whichever pass finishes the element
+__device__ __forceinline__ void note_state(const BatchArgs &a, int64_t i, const uint8_t *x)
+{
+    if (a.state_out) a.state_out[i] = x[9];
 }
 
 __device__ __forceinline__ uint64_t phys_of(const BatchArgs &a, uint32_t e) { return (uint64_t)e * a.g.entry_unit; }
@@ -866,6 +873,9 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
             }
         }
         a.st[i] = st;
+        // big ops move through LDS only when they hit (kLive); the others are in memory unchanged
+        note_state(a, i, kLive && e == kNone ? a.elems + i * a.esz
+                                              : reinterpret_cast<const uint8_t *>(sops) + (uint32_t)t * a.esz);
     }
     __syncthreads();
     if (kLive) {
@@ -912,6 +922,7 @@ __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
                 a.st[i] = kStCommit;
             }
             if (kStage) copy_elem(xg, xl, a.esz);
+            note_state(a, i, kStage ? xl : xg);
         } else {
             a.pf[i] = f;  // after the last round: identifies the key's run in k_fb_exec
             left = r == a.rounds;
@@ -1063,6 +1074,7 @@ __global__ __launch_bounds__(kFbThreads) void k_fb_exec(BatchArgs a)
             uint8_t idx;
             elem_at(a, (uint32_t)ord[q], x, idx, c);
             dispatch<SV>(TYPE, x, entry, idx, m, c);
+            note_state(a, (uint32_t)ord[q], x);
         }
         meta_store(entry, m);
     }
@@ -1111,6 +1123,7 @@ __global__ __launch_bounds__(kFbThreads) void k_fb_exec(BatchArgs a)
                     Meta t = m;
                     dispatch<SV>(TYPE, x, entry, idx, t, c);
                     if (a.error_flags && !meta_equal(t, m)) atomicOr(a.error_flags, 1u);
+                    note_state(a, (uint32_t)ord[base + pos], x);
                     pending &= ~(1u << j);
                 }
                 __syncthreads();  // every read of the entry value precedes the mutation
@@ -1120,6 +1133,7 @@ __global__ __launch_bounds__(kFbThreads) void k_fb_exec(BatchArgs a)
                     elem_at(a, (uint32_t)ord[base + f], x, idx, c);
                     Meta mm = m;
                     dispatch<SV>(TYPE, x, entry, idx, mm, c);
+                    note_state(a, (uint32_t)ord[base + f], x);
                     pending &= ~(1u << (f / kFbThreads));
                     sm = mm;
                 }
@@ -1390,6 +1404,10 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(BatchArgs a)
         for (int b = tid; b < a.n_batches; b += kSmallThreads)
             if (ns[b] >= 0) a.node_suspected[b] = a.elems[((int64_t)b * a.stride + ns[b]) * a.esz + kOpValueOff];
     }
+    if (!MIXED && a.state_out) {
+        __syncthreads();
+        for (int i = tid; i < n; i += kSmallThreads) a.state_out[i] = a.elems[(int64_t)i * a.esz + 9];
+    }
     if (a.prof && tid == 0) a.prof[4] = wall_clock64();
     if (a.region_bytes) {  // results back to the host staging, then the completion flag
         __threadfence_block();  // one workgroup wrote the region: its CU's caches see it
@@ -1511,6 +1529,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.elems = bl.elems;
     a.counts = bl.counts;
     a.offsets = bl.offsets;
+    a.state_out = (bl.type == kLocal || bl.type == kLocalAfterMemb) ? bl.state_out : nullptr;
     a.index = bl.index;
     a.log = bl.log;
     a.rw = bl.rw;

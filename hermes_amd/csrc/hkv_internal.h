@@ -15,6 +15,7 @@ struct BatchLaunch {
     uint8_t *elems;
     const int32_t *counts;
     const int32_t *offsets;      // packed INV/VAL launches: n_batches + 1 batch offsets (counts NULL)
+    uint8_t *state_out;          // local launches: each element's final state byte (may be NULL)
     const uint8_t *index;
     uint8_t *log;
     uint8_t *rw;

@@ -414,6 +414,7 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.g = t->geo;
     bl.elems = d->d_elems;
     bl.counts = packed ? nullptr : d->d_counts;
+    bl.state_out = d->d_state_out;
     bl.offsets = packed ? d->d_counts : nullptr;
     bl.index = t->d_index;
     bl.log = t->d_log;

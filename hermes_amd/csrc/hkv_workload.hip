@@ -165,7 +165,15 @@ __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, ui
     const bool live = i < stride;
     uint64_t *gslab = reinterpret_cast<uint64_t *>(ops + (int64_t)w * stride * op_size);
     const int words = (int)((uint32_t)stride * op_size / 8u);
-    for (int k = i; k < words; k += 256) slab[k] = gslab[k];
+    // 16-B accesses when the slab allows (250 x 56 B does): half the memory instructions
+    const bool wide = (words & 1) == 0 && (reinterpret_cast<uintptr_t>(gslab) & 15) == 0;
+    if (wide) {
+        const uint4 *g4 = reinterpret_cast<const uint4 *>(gslab);
+        uint4 *s4 = reinterpret_cast<uint4 *>(slab);
+        for (int k = i; k < words / 2; k += 256) s4[k] = g4[k];
+    } else {
+        for (int k = i; k < words; k += 256) slab[k] = gslab[k];
+    }
     __syncthreads();
     uint8_t *op = reinterpret_cast<uint8_t *>(slab) + (uint32_t)i * op_size;
     uint8_t st = live ? op[9] : 0;
@@ -205,7 +213,13 @@ __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, ui
         }
     }
     __syncthreads();
-    for (int k = i; k < words; k += 256) gslab[k] = slab[k];
+    if (wide) {
+        uint4 *g4 = reinterpret_cast<uint4 *>(gslab);
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(slab);
+        for (int k = i; k < words / 2; k += 256) g4[k] = s4[k];
+    } else {
+        for (int k = i; k < words; k += 256) gslab[k] = slab[k];
+    }
 }
 
 // k_refill for big ops (312 B): staging a 78-KB slab per workgroup caps occupancy at two
@@ -287,12 +301,14 @@ __device__ __forceinline__ uint64_t with_op_state(uint64_t h, uint8_t op, uint8_
 // sent by a later round, as with the reference's credit-limited wings sends.
 __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stride, uint32_t op_size, uint8_t *out,
                                                       int32_t out_stride, int32_t *count, uint32_t machine_id,
-                                                      unsigned long long *held, const int32_t *aq_n, int32_t r_alive)
+                                                      unsigned long long *held, const int32_t *aq_n, int32_t r_alive,
+                                                      const uint8_t *states)
 {
     const int w = blockIdx.x, i = threadIdx.x;
     const bool live = i < stride;
     uint8_t *op = ops + ((int64_t)w * stride + i) * op_size;
-    uint8_t st = live ? op[9] : 0;
+    // the local batch's state mirror, when it kept one, instead of every op's line
+    uint8_t st = live ? (states ? states[(int64_t)w * stride + i] : op[9]) : 0;
     bool send = live && (st == kPutSuccess || st == kRmwSuccess || st == kReplaySuccess || st == kOpMembChange);
     int total;
     int rank = block_rank(send, total);
@@ -993,6 +1009,64 @@ __global__ __launch_bounds__(256) void k_vals_credit(uint8_t *aq, int32_t *aq_n,
     }
 }
 
+// The entry of every peer INV of a pre-drawn round index, located once when the index is drawn
+// (the index never changes under the rounds: writes update entries in place and nothing is
+// inserted), so the per-round timestamps need one entry line per INV instead of bucket + line.
+__global__ __launch_bounds__(256) void k_peer_locate(TableView t, const uint8_t *invs, uint32_t op_size,
+                                                     int64_t total, uint64_t *phys_out)
+{
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= total) return;
+    phys_out[g] = find_entry(t, *reinterpret_cast<const uint64_t *>(invs + g * op_size));
+}
+
+// k_peer_ts for located INVs (one thread each): the key is checked at the entry, and an INV
+// whose entry does not hold its key any more takes the full lookup
+__global__ __launch_bounds__(256) void k_peer_ts_at(TableView t, uint8_t *invs, uint8_t *vals, const uint64_t *phys_in,
+                                                    int64_t total, uint32_t op_size, unsigned long long *peer_ts,
+                                                    uint32_t round)
+{
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= total) return;
+    uint8_t *x = invs + g * op_size;
+    const uint64_t key = *reinterpret_cast<const uint64_t *>(x);
+    const uint64_t h8 = *reinterpret_cast<const uint64_t *>(x + 8);
+    const uint8_t peer = (uint8_t)(h8 >> 8);
+    const bool rmw = x[16] & 1u;
+    uint64_t phys = phys_in[g];
+    uint32_t cur = 0;
+    bool ok = false;
+    if (phys != ~0ull) {
+        const U64x2w *e = reinterpret_cast<const U64x2w *>(t.log + phys);
+        const U64x2w l0 = e[0], l1 = e[1];  // key at 8, timestamp version at 24
+        if (l0.b == key) {
+            ok = true;
+            cur = (uint32_t)l1.b;
+        }
+    }
+    if (!ok) {
+        phys = find_entry(t, key);
+        if (phys != ~0ull) {
+            ok = true;
+            cur = *reinterpret_cast<const uint32_t *>(t.log + phys + 24);
+        }
+    }
+    uint32_t ver = 2;
+    if (ok) {
+        ver = cur + ((!t.g.rmw_enabled || rmw) ? 2u : 4u);
+        if (peer_ts && peer < 8)
+            atomicMax(peer_ts + (phys / t.g.entry_unit) * 8 + peer,
+                      ((unsigned long long)peer_round_tag(round) << 41) | ((unsigned long long)rmw << 40) |
+                          ((unsigned long long)ver << 8) | peer);
+    }
+    // bytes 8..15 rewritten whole (opcode, sender, val_len, cid, version): one 8-B store
+    const uint64_t nh = (h8 & 0xFFFFFF00ull & 0xFFFFFFFFull) | kOpInv | ((uint64_t)ver << 32);
+    *reinterpret_cast<uint64_t *>(x + 8) = nh;
+    uint8_t *vv = vals + g * kOpMetaSize;
+    const uint64_t vh = *reinterpret_cast<const uint64_t *>(vv + 8);
+    *reinterpret_cast<uint64_t *>(vv + 8) = (vh & 0xFFFFFF00ull & 0xFFFFFFFFull) | kOpVal | ((uint64_t)ver << 32);
+}
+
 }  // namespace hkv
 
 using namespace hkv;
@@ -1043,7 +1117,8 @@ int hkv_wl_marshal_invs(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_
 {
     if (stride > 256 || n_workers <= 0) return -1;
     hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
-                       stride, count, machine_id, (unsigned long long *)nullptr, (const int32_t *)nullptr, 1);
+                       stride, count, machine_id, (unsigned long long *)nullptr, (const int32_t *)nullptr, 1,
+                       (const uint8_t *)nullptr);
     return ok();
 }
 
@@ -1144,11 +1219,11 @@ uint64_t hkv_wl_peer_ts_words(const hkv_table *t)
 
 int hkv_wl_marshal_invs_cap(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint8_t *out,
                             int32_t out_stride, int32_t *count, uint32_t machine_id, unsigned long long *held,
-                            void *stream)
+                            const uint8_t *states, void *stream)
 {
     if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
     hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
-                       out_stride, count, machine_id, held, (const int32_t *)nullptr, 1);
+                       out_stride, count, machine_id, held, (const int32_t *)nullptr, 1, states);
     return ok();
 }
 
@@ -1158,7 +1233,7 @@ int hkv_wl_marshal_invs_credits(uint8_t *ops, int32_t n_workers, int32_t stride,
 {
     if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
     hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
-                       out_stride, count, machine_id, held, aq_n, r_alive);
+                       out_stride, count, machine_id, held, aq_n, r_alive, (const uint8_t *)nullptr);
     return ok();
 }
 
@@ -1280,6 +1355,31 @@ int hkv_wl_vals_credit(uint8_t *aq, int32_t *aq_n, const int32_t *acnt, int32_t 
     if (n_workers <= 0 || ack_size % 8 || vq_stride <= 0 || out_stride <= 0 || v_credits < 0) return -1;
     hipLaunchKernelGGL(k_vals_credit, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, aq, aq_n, acnt, q_stride,
                        ack_size, vq, vq_n, vq_stride, out, out_count, out_stride, v_credits, machine_id, overflow);
+    return ok();
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int hkv_wl_peer_locate(hkv_table *t, const uint8_t *invs, int64_t n, uint32_t op_size, uint64_t *phys_out, void *stream)
+{
+    TableView tv;
+    if (table_view(t, &tv) || n < 0 || op_size % 8) return -1;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_peer_locate, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, tv, invs, op_size, n,
+                       phys_out);
+    return ok();
+}
+
+int hkv_wl_peer_ts_at(hkv_table *t, uint8_t *invs, uint8_t *vals, const uint64_t *phys, int64_t n, uint32_t op_size,
+                      unsigned long long *peer_ts, uint32_t round, void *stream)
+{
+    TableView tv;
+    if (table_view(t, &tv) || n < 0 || op_size % 8) return -1;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_peer_ts_at, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, tv, invs, vals, phys, n,
+                       op_size, peer_ts, round);
     return ok();
 }
 

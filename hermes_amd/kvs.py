@@ -16,7 +16,7 @@ import numpy as np
 import torch
 
 from . import layout as L
-from .lib import HkvBatchDesc, HkvConfig, Membership, check, raw
+from .lib import ABI_VERSION, HkvBatchDesc, HkvConfig, Membership, check, raw
 
 _L = raw()
 
@@ -63,7 +63,7 @@ def hermes_batch_ops_to_KVS(btype: int, op_array: np.ndarray, op_num: int, sizeo
 def make_config(num_keys: int = 1_000_000, num_bkts: int = 2 * 1024 * 1024, log_cap: int = 1 << 30,
                 machine_id: int = 0, rmw: bool = False, big_objects: bool = False,
                 extra_cache_lines: int = 0, device: int = 0, rw_len: int = 250) -> HkvConfig:
-    return HkvConfig(1, machine_id, int(rmw), int(big_objects), int(extra_cache_lines), device, rw_len, 0,
+    return HkvConfig(ABI_VERSION, machine_id, int(rmw), int(big_objects), int(extra_cache_lines), device, rw_len, 0,
                      num_keys, num_bkts, log_cap)
 
 
@@ -153,7 +153,8 @@ class HermesKV:
     def batch(self, btype: int, elems: torch.Tensor, n_batches: int, stride: int, elem_size: int,
               membership: bytes, counts: torch.Tensor | None = None, rw: torch.Tensor | None = None,
               rw_stride_bytes: int = 0, node_suspected: torch.Tensor | None = None,
-              stream: torch.cuda.Stream | None = None, offsets: torch.Tensor | None = None) -> None:
+              stream: torch.cuda.Stream | None = None, offsets: torch.Tensor | None = None,
+              state_out: torch.Tensor | None = None) -> None:
         """Apply n_batches batches of one type, concatenated in `elems` (uint8, on the GPU),
         in concatenation order, asynchronously on `stream` (default: torch's current).
         offsets (INV / ACK / VAL batches): the batches stored back to back, batch b at elements
@@ -168,6 +169,9 @@ class HermesKV:
         d.elem_size = int(elem_size)
         d.flags = self.default_flags
         d.d_elems = elems.data_ptr()
+        if state_out is not None:   # local batches: the mirror of each element's final state byte
+            assert state_out.is_cuda and state_out.dtype == torch.uint8 and state_out.numel() >= n_batches * stride
+            d.d_state_out = state_out.data_ptr()
         if offsets is not None:
             assert counts is None and offsets.is_cuda and offsets.dtype == torch.int32
             assert offsets.numel() >= n_batches + 1
@@ -214,13 +218,19 @@ class HermesKV:
         stride = len(elems) // n_batches if stride is None else stride
         esz = elems.dtype.itemsize
         t = torch.from_numpy(elems.view(np.uint8).reshape(-1).copy()).to(dev)
+        # local launches also keep the state mirror (d_state_out), checked against the elements
+        local = int(btype) in (int(L.BatchType.local_ops), int(L.BatchType.local_ops_after_membership_change))
+        st = torch.full((n_batches * stride,), 0xEE, dtype=torch.uint8, device=dev) if local else None
         tc = torch.from_numpy(np.ascontiguousarray(counts, dtype=np.int32)).to(dev) if counts is not None else None
         tr = torch.from_numpy(rw.view(np.uint8).reshape(-1).copy()).to(dev) if rw is not None else None
         tn = torch.from_numpy(np.ascontiguousarray(node_suspected, dtype=np.int32)).to(dev) if node_suspected is not None else None
         self.batch(btype, t, n_batches, stride, esz, membership, tc, tr,
-                   rw_stride_elems * (rw.dtype.itemsize if rw is not None else 0), tn)
+                   rw_stride_elems * (rw.dtype.itemsize if rw is not None else 0), tn, state_out=st)
         torch.cuda.synchronize(dev)
         elems.view(np.uint8).reshape(-1)[:] = t.cpu().numpy()
+        if st is not None and not np.array_equal(st.cpu().numpy(),
+                                                 elems.view(np.uint8).reshape(-1, esz)[: n_batches * stride, 9]):
+            raise AssertionError("state mirror (d_state_out) differs from the elements' state bytes")
         if rw is not None:
             rw.view(np.uint8).reshape(-1)[:] = tr.cpu().numpy()
         if node_suspected is not None:

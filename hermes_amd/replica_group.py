@@ -80,6 +80,7 @@ class ReplicaRound:
         u8 = dict(dtype=torch.uint8, device=dev)
         i32 = dict(dtype=torch.int32, device=dev)
         self.ops = torch.zeros(W * LOCAL * self.op, **u8)
+        self.states = torch.zeros(W * LOCAL, dtype=torch.uint8, device=dev)  # local batch state mirror
         # outgoing INVs: [W][C] rows, then packed (worker w at inv_off[w]; inv_off[W] = total)
         self.inv_slab = torch.zeros(W * C * self.op, **u8)
         self.inv_count = torch.zeros(W, **i32)
@@ -147,9 +148,10 @@ class ReplicaRound:
             self.inv_off.zero_()
             self.inv_maxc.zero_()
             return
-        self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, LOCAL, self.op, self.mb)
+        self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, LOCAL, self.op, self.mb, state_out=self.states)
         check(_L.hkv_wl_marshal_invs_cap(_ptr(self.ops), self.W, LOCAL, self.op, _ptr(self.inv_slab), self.C,
-                                         _ptr(self.inv_count), self.rank, _ptr(self.held), _s()), "marshal_invs")
+                                         _ptr(self.inv_count), self.rank, _ptr(self.held), _ptr(self.states), _s()),
+              "marshal_invs")
         check(_L.hkv_wl_pack_rows(_ptr(self.inv_slab), _ptr(self.inv_count), self.W, self.C, self.op,
                                   _ptr(self.inv_pack), _ptr(self.inv_off), _s()), "pack invs")
         torch.amax(self.inv_count, dim=0, keepdim=True, out=self.inv_maxc)

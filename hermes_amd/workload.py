@@ -35,7 +35,7 @@ _L.hkv_wl_refill.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32
 _L.hkv_wl_fold_counters.argtypes = [_P, _P]
 _L.hkv_wl_marshal_invs.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_invs_cap.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
-                                       ctypes.c_uint32, _P, _P]
+                                       ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_marshal_acks.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_memb_vals.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
                                         ctypes.c_uint32, _P]
@@ -60,6 +60,8 @@ _L.hkv_wl_vals_credit.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ct
                                   _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P]
 _L.hkv_wl_ack_offsets.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, _P]
 _L.hkv_wl_pack_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, _P]
+_L.hkv_wl_peer_locate.argtypes = [_P, _P, ctypes.c_int64, ctypes.c_uint32, _P, _P]
+_L.hkv_wl_peer_ts_at.argtypes = [_P, _P, _P, _P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_peer_ts_words.restype = ctypes.c_uint64
 _L.hkv_wl_peer_ts_words.argtypes = [_P]
 
@@ -126,6 +128,7 @@ class Round:
         W, S = n_workers, self.LOCAL
         u8 = dict(dtype=torch.uint8, device=dev)
         self.ops = torch.zeros(W * S * self.op, **u8)
+        self.states = torch.zeros(W * S, **u8)   # the local batch's mirror of every op's state byte
         self.C = slots_per_worker(write_permille, rmw_permille)   # INV send credits per worker
         self.inv_out = torch.zeros(W * self.C * self.op, **u8)
         self.inv_count = torch.zeros(W, dtype=torch.int32, device=dev)
@@ -184,7 +187,7 @@ class Round:
         if virtual_peers and self.R and kvs.rmw:
             self.peer_ts = torch.zeros(int(_L.hkv_wl_peer_ts_words(kvs.h)), dtype=torch.int64, device=dev)
         self.pack_remote = virtual_peers and self.R > 0 and pack_remote
-        self.remote_packed = []        # per round index: (INVs, VALs, batch offsets, total, [total])
+        self.remote_packed = []        # per round index: (INVs, VALs, batch offsets, total, entry offsets)
         self.drops = []                # peers dropped from the membership (membership_change)
         self.alive = self.R            # live peers: the first `alive` slots of the remote slabs
         self._counts = {}
@@ -228,8 +231,9 @@ class Round:
                       "pack remote invs")
                 check(_L.hkv_wl_pack_rows(_ptr(rv), _ptr(full), W, self.rstride, L.OP_META_SIZE, _ptr(pv), _ptr(off),
                                           _s()), "pack remote vals")
-                one = torch.full((1,), total, dtype=torch.int32, device=dev)
-                self.remote_packed.append((pi, pv, off, total, one))
+                phys = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+                check(_L.hkv_wl_peer_locate(self.kvs.h, _ptr(pi), total, self.op, _ptr(phys), _s()), "peer_locate")
+                self.remote_packed.append((pi, pv, off, total, phys))
         del scratch
 
     # -- pieces of one round
@@ -240,7 +244,7 @@ class Round:
               "refill")
 
     def local_batch(self):
-        self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb)
+        self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb, state_out=self.states)
 
     def marshal_invs(self):
         if self.V is not None:
@@ -249,8 +253,8 @@ class Round:
                                                  _ptr(self.aq_n), max(self.alive, 1), _s()), "marshal_invs")
             return
         check(_L.hkv_wl_marshal_invs_cap(_ptr(self.ops), self.W, self.LOCAL, self.op, _ptr(self.inv_out), self.C,
-                                         _ptr(self.inv_count), self.machine_id, _ptr(self.held), _s()),
-              "marshal_invs")
+                                         _ptr(self.inv_count), self.machine_id, _ptr(self.held), _ptr(self.states),
+                                         _s()), "marshal_invs")
 
     def virtual_peer_acks(self, n_peers: int | None = None):
         """ACKs (INV-aborts for RMWs a peer's own write beats) of the first n_peers virtual peers
@@ -267,9 +271,10 @@ class Round:
                                 _ptr(self.peer_ts), self.clock, _s()), "peer_ts")
 
     def peer_timestamps_packed(self, k: int):
-        pi, pv, _, total, one = self.remote_packed[k]
-        check(_L.hkv_wl_peer_ts(self.kvs.h, _ptr(pi), _ptr(pv), _ptr(one), 1, total, self.op, _ptr(self.peer_ts),
-                                self.clock, _s()), "peer_ts")
+        """the same for the packed slabs, whose INVs' entries were located when they were drawn"""
+        pi, pv, _, total, phys = self.remote_packed[k]
+        check(_L.hkv_wl_peer_ts_at(self.kvs.h, _ptr(pi), _ptr(pv), _ptr(phys), total, self.op, _ptr(self.peer_ts),
+                                   self.clock, _s()), "peer_ts_at")
 
     def inv_batch(self, invs: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None,
                   offsets: torch.Tensor | None = None):

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HKV_ABI_VERSION 1
+#define HKV_ABI_VERSION 2
 
 /* ------------------------------------------------------------------ reference types
  * Declared here only when the reference's own spacetime.h has not been included; the
@@ -116,6 +116,9 @@ typedef struct hkv_batch_desc {
     int64_t  rw_stride_bytes;   /* bytes between consecutive batches' read_write_ops */
     int32_t *d_node_suspected;  /* device, n_batches entries (INV batches); NULL = ignore */
     uint8_t  membership[8];     /* spacetime_group_membership by value */
+    uint8_t *d_state_out;       /* device, local batches: receives each element's final state byte
+                                   (op byte 9; n_batches * stride bytes), a mirror the worker loop's
+                                   next passes can read instead of the ops; NULL = none (ABI 2) */
 } hkv_batch_desc;
 
 /* hkv_batch_desc.flags. By default launches of at most 4096 elements run as one single-workgroup

@@ -110,6 +110,15 @@ int hkv_wl_peer_ts(hkv_table *t, uint8_t *d_invs, uint8_t *d_vals, const int32_t
                    int32_t stride, uint32_t op_size, unsigned long long *d_peer_ts, uint32_t round, void *stream);
 uint64_t hkv_wl_peer_ts_words(const hkv_table *t);
 
+/* The same for n INVs stored back to back (and their VALs), with each INV's entry located
+ * beforehand: hkv_wl_peer_locate writes the log offset of every INV's key (~0 when absent) into
+ * d_phys once per pre-drawn round index; hkv_wl_peer_ts_at reads one entry line per INV (an INV
+ * whose entry no longer holds its key takes the full lookup). */
+int hkv_wl_peer_locate(hkv_table *t, const uint8_t *d_invs, int64_t n, uint32_t op_size, uint64_t *d_phys,
+                       void *stream);
+int hkv_wl_peer_ts_at(hkv_table *t, uint8_t *d_invs, uint8_t *d_vals, const uint64_t *d_phys, int64_t n,
+                      uint32_t op_size, unsigned long long *d_peer_ts, uint32_t round, void *stream);
+
 /* The virtual peers' answers to this round's INVs: for INV j of worker w, the ack_size-byte
  * element d_acks[w*out_stride + j*n_peers + r] from peer_ids[r] is an ACK {key, ST_OP_ACK,
  * sender, ts = inv ts} (ack_copy_and_modify_elem, hermes_worker.c:100-118) -- or, with d_peer_ts
@@ -149,10 +158,11 @@ int hkv_wl_max_to_host(const int32_t *d_counts, int32_t n, int32_t *h_out, void 
 
 /* hkv_wl_marshal_invs with at most out_stride INVs per worker per round (d_inv_out rows of
  * out_stride); further sendable ops keep their state for a later round and are counted in
- * *d_held (may be NULL). */
+ * *d_held (may be NULL). d_states (may be NULL): the state mirror the local batch wrote
+ * (hkv_batch_desc.d_state_out), read instead of each op's state byte. */
 int hkv_wl_marshal_invs_cap(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size,
                             uint8_t *d_inv_out, int32_t out_stride, int32_t *d_inv_count, uint32_t machine_id,
-                            unsigned long long *d_held, void *stream);
+                            unsigned long long *d_held, const uint8_t *d_states, void *stream);
 
 /* ACKs for `rows` rows of received INVs (row r: d_in_count[r] INVs at d_invs + r*C*op_size),
  * compacted to the front of row r of d_ack_out (row stride C), d_out_count[r] ACKs; INV

@@ -94,7 +94,7 @@ class Mirror:
             self.codes[(int(btype), tag, x)] += c
 
     def batch(self, btype, elems, n_batches, stride, elem_size, membership, counts=None, rw=None,
-              rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None):
+              rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None, state_out=None):
         import torch
         if offsets is not None:
             return self._packed(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
@@ -109,7 +109,7 @@ class Mirror:
         if rw is not None:
             rw_in = rw.cpu().numpy().copy().view(np.dtype((np.void, self.g.sizes.op)))
         self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
-                   node_suspected, stream)
+                   node_suspected, stream, state_out=state_out)
         torch.cuda.synchronize()
         self.o.batch_multi(int(btype), e_in, n_batches, stride, c_in, membership, rw_in,
                            rw_stride_bytes // self.g.sizes.op if rw is not None else 0)
@@ -131,6 +131,9 @@ class Mirror:
                         f"bytes-in-entry {np.unique(bad % e)[:16]}")
         assert np.array_equal(self.g.index_bytes(), self.o.index_bytes()), f"{what}: index differs"
         assert self.g.take_error_flags() == 0, f"{what}: device consistency flags"
+        if state_out is not None:   # the local batch's state mirror: every element's state byte
+            mirror = state_out[: n_batches * stride].cpu().numpy()
+            assert np.array_equal(mirror, got.reshape(-1, elem_size)[:, 9]), f"{what}: state mirror differs"
         self.launches += 1
 
     def _packed(self, btype, elems, n_batches, total, elem_size, membership, offsets, stream, rw=None,

@@ -351,7 +351,7 @@ def test_marshal_invs_kernel_matches_numpy(big):
     d_cnt = torch.zeros(W, dtype=torch.int32, device="cuda")
     d_held = torch.zeros(1, dtype=torch.int64, device="cuda")
     WL.check(WL._L.hkv_wl_marshal_invs_cap(WL._ptr(d_ops), W, S, osz, WL._ptr(d_out), C, WL._ptr(d_cnt), mid,
-                                           WL._ptr(d_held), None), "marshal_invs")
+                                           WL._ptr(d_held), None, None), "marshal_invs")
     torch.cuda.synchronize()
     cnt = d_cnt.cpu().numpy()
     assert np.array_equal(cnt, exp_cnt)

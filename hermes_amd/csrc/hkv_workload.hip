@@ -117,6 +117,12 @@ constexpr int kCounters = 5;  // committed, misses, completed writes, dropped (r
 // success and their completion (waiting for INV credits, ACKs or the VALs of a membership
 // change), and membership-change ops. Overwriting one would leave its key in WRITE/REPLAY with
 // an op buffer index that points at an unrelated op.
+// val_skip_or_get_sender_id (hermes_worker.c:122-136, assertions off as configured, config.h:83):
+// an ACK element answers with a VAL unless it is ST_ACK_SUCCESS, a membership change or empty;
+// afterwards every one of them is empty (the skipped ones by the skip, the sent ones by
+// val_modify_elem_after_send)
+__device__ __forceinline__ bool val_sends(uint8_t oc) { return oc != kAckSuccess && oc != kOpMembChange && oc != kEmpty; }
+
 __device__ __forceinline__ bool in_flight(uint8_t st)
 {
     return st == kPutSuccess || st == kRmwSuccess || st == kReplaySuccess || st == kInProgressPut ||
@@ -467,7 +473,7 @@ __global__ __launch_bounds__(64) void k_collect_vals(uint8_t *acks, const int32_
         const int j = j0 + lane;
         uint8_t *x = acks + (row + j) * (int64_t)ack_size;
         const uint8_t oc = j < n ? x[8] : 0;
-        const bool send = j < n && oc == kLastAckSuccess;
+        const bool send = j < n && val_sends(oc);
         const unsigned long long m = __ballot(send);
         const int rank = __popcll(m & ((1ull << lane) - 1ull));
         if (send && base + rank < C) {
@@ -476,7 +482,7 @@ __global__ __launch_bounds__(64) void k_collect_vals(uint8_t *acks, const int32_
             uint64_t h = reinterpret_cast<const uint64_t *>(x)[1];
             y[1] = (h & ~0xFFFFull) | kOpVal | ((uint64_t)(machine_id & 0xFF) << 8);
         }
-        if (j < n && (oc == kLastAckSuccess || oc == kAckSuccess || oc == kOpMembChange)) x[8] = kEmpty;
+        if (j < n && oc != kEmpty) x[8] = kEmpty;
         base += __popcll(m);
     }
     if (lane == 0) {
@@ -516,9 +522,9 @@ __global__ void k_marshal_vals(uint8_t *acks, int64_t n, uint32_t ack_size, uint
     uint8_t *y = out + i * kOpMetaSize;
     const W16 h = *reinterpret_cast<const W16 *>(x);
     const uint8_t oc = (uint8_t)h.b;
-    if (oc == kLastAckSuccess) *reinterpret_cast<W16 *>(y) = W16{h.a, with_op_state(h.b, kOpVal, (uint8_t)machine_id)};
+    if (val_sends(oc)) *reinterpret_cast<W16 *>(y) = W16{h.a, with_op_state(h.b, kOpVal, (uint8_t)machine_id)};
     else y[8] = kEmpty;
-    if (oc == kLastAckSuccess || oc == kAckSuccess || oc == kOpMembChange) x[8] = kEmpty;
+    x[8] = kEmpty;
 }
 
 // ---- packed slabs (replica groups): one contiguous slab per rank instead of [W][C] rows
@@ -983,7 +989,7 @@ __global__ __launch_bounds__(256) void k_vals_credit(uint8_t *aq, int32_t *aq_n,
         const int j = j0 + (int)threadIdx.x;
         uint8_t *x = aq + ((int64_t)w * q_stride + j) * ack_size;
         const uint8_t oc = j < applied ? x[8] : 0;
-        const bool send = j < applied && oc == kLastAckSuccess;
+        const bool send = j < applied && val_sends(oc);
         int cnt;
         const int rank = block_rank(send, cnt);
         if (send && total + rank < kMaxVq) {
@@ -992,7 +998,7 @@ __global__ __launch_bounds__(256) void k_vals_credit(uint8_t *aq, int32_t *aq_n,
         } else if (send && overflow) {
             atomicAdd(overflow, 1ull);
         }
-        if (j < applied && (oc == kLastAckSuccess || oc == kAckSuccess || oc == kOpMembChange)) x[8] = kEmpty;
+        if (j < applied && oc != kEmpty) x[8] = kEmpty;
         total = min(total + cnt, kMaxVq);
     }
     __syncthreads();

@@ -78,8 +78,10 @@ int hkv_wl_marshal_invs(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint3
 int hkv_wl_marshal_acks(uint8_t *d_invs, int64_t n, uint32_t op_size, uint8_t *d_ack_out, uint32_t ack_size,
                         uint32_t machine_id, void *stream);
 
-/* VALs for ACK elements that completed a write (ST_LAST_ACK_SUCCESS): element i of d_val_out
- * (16 bytes), ST_EMPTY elsewhere; the ACK elements become ST_EMPTY */
+/* VALs for ACK elements that completed a write: element i of d_val_out (16 bytes), ST_EMPTY
+ * elsewhere; the ACK elements become ST_EMPTY. As val_skip_or_get_sender_id with the reference's
+ * assertions off (config.h:83), every element that is not ST_ACK_SUCCESS, a membership change or
+ * empty sends one (after an ACK batch: ST_LAST_ACK_SUCCESS, and ACKs of keys not in the table). */
 int hkv_wl_marshal_vals(uint8_t *d_acks, int64_t n, uint32_t ack_size, uint8_t *d_val_out,
                         uint32_t machine_id, void *stream);
 

@@ -208,7 +208,8 @@ def test_val_credits_round_mirrored(credits, cfg3):
         for w in range(W):
             src = [carried[w, j] for j in range(vq_n[w])]
             assert acnt[w] == 0 or vq_n[w] == 0, "ACKs applied while VALs were outstanding"
-            new = [j for j in range(acnt[w]) if aq[w, j, 8] == int(L.Resp.LAST_ACK_SUCCESS)]
+            skip = (int(L.Resp.ACK_SUCCESS), int(L.Op.MEMBERSHIP_CHANGE), int(L.Bucket.EMPTY))
+            new = [j for j in range(acnt[w]) if aq[w, j, 8] not in skip]   # val_skip_or_get_sender_id
             seen["produced"] += len(new)
             for j in new:
                 v = aq[w, j, :16].copy()

@@ -142,11 +142,12 @@ def main():
     z = zipf_params(a.keys, a.zipf)
     total_steps = a.warmup + a.steps
     cpu = None
+    snap = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
-        # CPU baseline first, on the freshly populated table image (copied out of HBM)
-        from oracle.cpu_baseline import run_cpu_baseline
-        cpu = run_cpu_baseline(kvs, z, a.write_permille, a.cpu_workers, a.cpu_seconds, a.seed,
-                               refill_all=not a.retry, threads=a.cpu_threads)
+        # the CPU baseline runs on the freshly populated table image (copied out of HBM now), after
+        # the GPU's timed region so that its threads never compete with the GPU run's host thread
+        from oracle.cpu_baseline import TableSnapshot
+        snap = TableSnapshot(kvs)
 
     if world > 1:
         from hermes_amd.replica_group import ReplicaGroupRound
@@ -323,6 +324,10 @@ def main():
         out["detail"]["membership"].update(agreement="hades", epoch=hz.state()[1] if hz else None)
         if world == 1:
             out["detail"]["membership"]["agreed_at_round"] = [c[0] for c in rnd.hades_changes]
+    if snap is not None:
+        from oracle.cpu_baseline import run_cpu_baseline
+        cpu = run_cpu_baseline(kvs, z, a.write_permille, a.cpu_workers, a.cpu_seconds, a.seed,
+                               refill_all=not a.retry, threads=a.cpu_threads, snapshot=snap)
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if world == 1 and not a.retry and a.retry_steps > 0 and not cfg5:

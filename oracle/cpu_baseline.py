@@ -28,12 +28,41 @@ def host_threads(cap: int = 16) -> int:
     return max(1, min(n, cap))
 
 
+class TableSnapshot:
+    """The device table's image (index and log) copied into an oracle table, taken before the GPU
+    rounds change it, so the CPU baseline can run after the GPU's timed region (nothing of it then
+    competes with the GPU run's host thread)."""
+
+    def __init__(self, kvs):
+        build()
+        self.L = L = lib()
+        L.hko_set_log_head.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        c = kvs.cfg
+        self.c = c
+        self.cfg = Config(c.big_objects, c.extra_cache_lines, c.rmw_enabled, c.machine_id, c.num_bkts, c.log_cap)
+        self.h = L.hko_create(ctypes.byref(self.cfg))
+        from hermes_amd.lib import check, raw
+        R = raw()
+        idx = ctypes.cast(L.hko_index(self.h), ctypes.c_void_p)
+        log = ctypes.cast(L.hko_log(self.h), ctypes.c_void_p)
+        check(R.hkv_copy_index(kvs.h, idx, 0, c.num_bkts * 64), "copy index")
+        check(R.hkv_copy_log(kvs.h, log, 0, min(kvs.log_head, c.log_cap)), "copy log")
+        L.hko_set_log_head(self.h, kvs.log_head)
+
+    def close(self):
+        if self.h:
+            self.L.hko_destroy(self.h)
+            self.h = None
+
+
 def run_cpu_baseline(kvs, zipf, write_permille: int, workers: int, seconds: float, seed: int,
-                     n_peers: int = 2, per_peer: int = 50, refill_all: bool = True, threads: int = 0) -> dict:
+                     n_peers: int = 2, per_peer: int = 50, refill_all: bool = True, threads: int = 0,
+                     snapshot: TableSnapshot | None = None) -> dict:
     """threads = 0: one per usable core (host_threads()); workers = 0: one 250-op buffer per thread,
-    as the reference's workers (main.c:193-210)."""
-    build()
-    L = lib()
+    as the reference's workers (main.c:193-210). snapshot: a TableSnapshot taken earlier (consumed);
+    default: the table as it is now."""
+    snap = snapshot if snapshot is not None else TableSnapshot(kvs)
+    L, h, cfg, c = snap.L, snap.h, snap.cfg, snap.c
     threads = threads or host_threads()
     workers = workers or threads
     L.hko_bench_rounds.restype = ctypes.c_int64
@@ -41,26 +70,14 @@ def run_cpu_baseline(kvs, zipf, write_permille: int, workers: int, seconds: floa
                                    ctypes.c_double, ctypes.POINTER(HkoZipf), ctypes.c_uint32, ctypes.c_int,
                                    ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
                                    ctypes.POINTER(ctypes.c_double)]
-    L.hko_set_log_head.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
-    c = kvs.cfg
-    cfg = Config(c.big_objects, c.extra_cache_lines, c.rmw_enabled, c.machine_id, c.num_bkts, c.log_cap)
-    h = L.hko_create(ctypes.byref(cfg))
     try:
-        from hermes_amd.lib import check, raw
-        R = raw()
-        idx = ctypes.cast(L.hko_index(h), ctypes.c_void_p)
-        log = ctypes.cast(L.hko_log(h), ctypes.c_void_p)
-        check(R.hkv_copy_index(kvs.h, idx, 0, c.num_bkts * 64), "copy index")
-        used = min(kvs.log_head, c.log_cap)
-        check(R.hkv_copy_log(kvs.h, log, 0, used), "copy log")
-        L.hko_set_log_head(h, kvs.log_head)
         hz = HkoZipf(zipf.theta, zipf.zetan, zipf.alpha, zipf.eta, zipf.half_pow, zipf.n)
         rounds, secs = ctypes.c_int64(0), ctypes.c_double(0.0)
         committed = L.hko_bench_rounds(h, ctypes.byref(cfg), workers, threads, seconds, ctypes.byref(hz),
                                        write_permille, n_peers, per_peer, seed, int(refill_all), ctypes.byref(rounds),
                                        ctypes.byref(secs))
     finally:
-        L.hko_destroy(h)
+        snap.close()
     return {"value": committed / secs.value, "unit": "ops/s", "cores": threads, "kind": "port",
             "sample": (f"{threads} worker threads sharing one table (per-key seqlocks, concur_ctrl.h:144-224), "
                        f"{workers} x 250-op {'fresh' if refill_all else 'refilled'} local batches per round, "

@@ -456,10 +456,15 @@ class LoopbackGroup:
     def _a2a_io(self, ios):
         self._a2a([o for o, _ in ios], [i for _, i in ios])
 
-    def step(self, drop: int | None = None):
+    def step(self, drop: int | None = None, observer=None):
+        """One round of every replica. observer(phase), when given, runs after each phase has
+        finished on every replica ("local", "invs", "acks", "vals", "end"): property checks of
+        the group's state between phases (tests)."""
         rs = self.rounds
+        seen = observer or (lambda phase: None)
         for r in rs:
             r.local()
+        seen("local")
         self._gather_io([r.inv_total_io() for r in rs])
         shapes = [r.round_shape() for r in rs]
         width = shapes[0][0]                 # the same on every replica (max of the same totals)
@@ -468,13 +473,16 @@ class LoopbackGroup:
             rs[drop].fail()
         for r in rs:
             r.invs(width)
+        seen("invs")
         self._a2a_io([r.ack_io(width) for r in rs])
         for r, (_, stride) in zip(rs, shapes):
             r.acks(width, stride)
+        seen("acks")
         self._gather_io([r.val_total_io() for r in rs])
         self._gather_io([r.val_io(width) for r in rs])
         for r in rs:
             r.vals(width)
+        seen("vals")
         if self.hades:
             self._hades_period()
         elif drop is not None:
@@ -487,4 +495,5 @@ class LoopbackGroup:
                 r.vals(w2)
         for r in rs:
             r.refill()
+        seen("end")
         self.clock += 1

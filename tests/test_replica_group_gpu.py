@@ -189,6 +189,70 @@ def test_loopback_group_hades_membership():
         assert st["invs_held"] == 0 and st["vals_dropped"] == 0 and st["writes_completed"] > 0, st
 
 
+class _HConsistent:
+    """HConsistent (tla/Hermes.tla:53-56), checked between phases: every two live replicas whose
+    copy of a key is VALID hold the same timestamp (version, cid) and value."""
+
+    def __init__(self, mirrors, keys):
+        o = mirrors[0].o
+        self.mirrors = mirrors
+        self.off = np.array([o.lookup(int(k)) for k in keys if o.lookup(int(k)) is not None], np.int64)
+        self.checks = 0
+        self.valid_pairs = 0
+
+    def __call__(self, live, phase):
+        import torch
+        torch.cuda.synchronize()
+        m0 = self.mirrors[0]
+        sv = m0.g.sizes.st_value
+        imgs = []
+        for r in live:
+            log = self.mirrors[r].g.log_bytes()
+            ent = log[self.off[:, None] + np.arange(33 + sv)[None, :]]
+            imgs.append((ent[:, 18], ent[:, 23], ent[:, 24:28].copy().view(np.uint32)[:, 0], ent[:, 33:33 + sv]))
+        valid = np.stack([im[0] == int(L.State.VALID) for im in imgs])
+        for a in range(len(live)):
+            for b in range(a + 1, len(live)):
+                both = valid[a] & valid[b]
+                self.valid_pairs += int(both.sum())
+                for f in range(3):
+                    x, y = imgs[a][f][both], imgs[b][f][both]
+                    assert np.array_equal(x, y), f"{phase}: replicas {live[a]} and {live[b]} VALID with different " \
+                                                 f"{('cid', 'version', 'value')[f]} on {int((x != y).reshape(len(x), -1).any(1).sum())} keys"
+        self.checks += 1
+
+
+@pytest.mark.parametrize("n_rep,hades", [(4, True), (8, False)])
+def test_loopback_group_hconsistent_between_phases(n_rep, hades):
+    """The TLA+ invariant HConsistent (tla/Hermes.tla:53-56, THEOREM :263) as a property of the
+    device replica group: after every phase of every round -- local batch, INVs, ACKs, VALs, round
+    end -- no two live replicas hold a key VALID with different timestamps or values. With Hades,
+    replica 3 fails in round 1 and the check also covers the rounds before its expulsion."""
+    from hermes_amd.kvs import HermesKV
+    from hermes_amd.replica_group import LoopbackGroup, ReplicaRound
+    from hermes_amd.workload import zipf_params
+
+    n_keys, bkts, cap = 4000, 8192, 1 << 20
+    z = zipf_params(n_keys, 0.99)
+    reps, mirrors = [], []
+    for r in range(n_rep):
+        g = HermesKV(n_keys, bkts, cap, machine_id=r)
+        o = OracleKVS(bkts, cap, r)
+        o.populate(n_keys, L.DEFAULT.kvs_value)
+        mirrors.append(Mirror(g, o, f"replica {r}"))
+        reps.append(ReplicaRound(g, 16, n_rep, r, z, 400, seed=91 + r, trace_len=512))
+    grp = LoopbackGroup(reps, hades=hades)
+    inv = _HConsistent(mirrors, gen_keys(n_keys))
+    dead = n_rep - 1 if hades else None
+    for step in range(5):
+        live = [r.rank for r in reps if not r.failed]
+        grp.step(drop=dead if hades and step == 1 else None,
+                 observer=lambda phase: inv([r.rank for r in reps if not r.failed], f"round {step} {phase}"))
+    assert inv.checks == 5 * 5 and inv.valid_pairs > 0
+    if hades:
+        assert grp.hades_changes and all(c[2][1] == ((1 << n_rep) - 1) & ~(1 << dead) for c in grp.hades_changes)
+
+
 def _dist_child(rank, world, port, q, drop=None):
     import os
 

@@ -171,6 +171,45 @@ def test_hades_membership_round_mirrored(machines):
     assert g.take_error_flags() == 0
 
 
+def test_rmw_semantics_invariant_cfg3():
+    """HRSemanticsRMW (tla/HermesRMWs.tla:31-37) on the RMW-heavy round: across every round, no
+    two RMWs committed on a key with the same version (and different tie-breakers), and no RMW
+    committed with the version of a committed write or the one just below it. Commits are read
+    from the op buffers before each refill (RMW_COMPLETE / PUT_COMPLETE with the op's timestamp)."""
+    from hermes_amd.kvs import HermesKV
+    from hermes_amd.workload import Round, zipf_params
+    n_keys, bkts, cap = 60_000, 1 << 16, 1 << 25
+    g = HermesKV(n_keys, bkts, cap, machine_id=0, rmw=True, big_objects=True, extra_cache_lines=4)
+    r = Round(g, 40, L.membership(3, 0), [1, 2], zipf_params(n_keys, 0.99), 500, 500, seed=0x5EED, max_steps=10,
+              trace_len=1024)
+    op = g.sizes.op
+    rmws, writes = {}, {}
+    refill = r.refill
+
+    def recording_refill(first=False):
+        ops = r.ops.view(-1, op).cpu().numpy()
+        st = ops[:, 9]
+        for kind, code in (("rmw", int(L.Resp.RMW_COMPLETE)), ("put", int(L.Resp.PUT_COMPLETE))):
+            for x in ops[st == code]:
+                key = int(x[:8].view(np.uint64)[0])
+                ver, cid = int(x[12:16].view(np.uint32)[0]), int(x[11])
+                (rmws if kind == "rmw" else writes).setdefault(key, []).append((ver, cid))
+        refill(first)
+    r.refill = recording_refill
+    for _ in range(8):
+        r.step()
+    torch.cuda.synchronize()
+    n_rmw = sum(len(v) for v in rmws.values())
+    assert n_rmw > 0 and sum(len(v) for v in writes.values()) > 0
+    for key, rv in rmws.items():
+        wv = {v for v, _ in writes.get(key, [])}
+        seen = {}
+        for ver, cid in rv:
+            assert ver not in wv and ver + 1 not in wv, (key, ver, sorted(wv))
+            assert seen.setdefault(ver, cid) == cid, (key, ver)
+    assert g.take_error_flags() == 0
+
+
 @pytest.mark.parametrize("credits,cfg3", [(3, False), (6, True)])
 def test_val_credits_round_mirrored(credits, cfg3):
     """VALs under credits and the outstanding-VAL gate (hermes_worker.c:479-503).

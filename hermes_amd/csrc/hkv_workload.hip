@@ -886,7 +886,7 @@ __global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32
 // and the largest per-worker INV count land in pinned host memory (h[0], h[1]) for the host to size
 // the round's launches while the GPU runs the INV batch
 __global__ __launch_bounds__(1024) void k_ack_offsets(const int32_t *counts, int32_t n, int32_t n_peers, int32_t *off,
-                                                      int32_t *h)
+                                                      int32_t *h, int32_t seq)
 {
     // each thread owns 8 consecutive counts (one pass up to 8192 workers, loads issued together)
     __shared__ int32_t part[16], pmax[16];
@@ -931,8 +931,18 @@ __global__ __launch_bounds__(1024) void k_ack_offsets(const int32_t *counts, int
     if (threadIdx.x == 0) {
         for (int k = 1; k < 16; ++k) mx = pmax[k] > mx ? pmax[k] : mx;
         off[n] = carry;
-        h[0] = carry;
-        h[1] = mx;
+        if (seq == 0) {  // the host waits on an event recorded after this kernel
+            h[0] = carry;
+            h[1] = mx;
+        } else {
+            // the host spins on h[2]: system-scope stores write through to host memory, the wait
+            // orders the flag after the values, and no release fence (an L2 write-back of
+            // everything dirty, ~6 us before the next kernel could start) is needed
+            __hip_atomic_store(h, carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(h + 1, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __builtin_amdgcn_s_waitcnt(0);
+            __hip_atomic_store(h + 2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -1293,13 +1303,13 @@ int hkv_wl_collect_vals(uint8_t *acks, const int32_t *count, int32_t n_workers, 
 }
 
 int hkv_wl_ack_offsets(const int32_t *inv_count, int32_t n_workers, int32_t n_peers, int32_t *offsets, int32_t *h_out,
-                       void *stream)
+                       int32_t seq, void *stream)
 {
-    if (n_workers <= 0 || n_peers <= 0) return -1;
+    if (n_workers <= 0 || n_peers <= 0 || seq < 0) return -1;
     int32_t *d_out = nullptr;
     if (hipHostGetDevicePointer(reinterpret_cast<void **>(&d_out), h_out, 0) != hipSuccess || !d_out) return -1;
     hipLaunchKernelGGL(k_ack_offsets, dim3(1), dim3(1024), 0, (hipStream_t)stream, inv_count, n_workers, n_peers,
-                       offsets, d_out);
+                       offsets, d_out, seq);
     return ok();
 }
 

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -58,7 +59,7 @@ _L.hkv_wl_peer_acks_queue.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32
                                       ctypes.c_int32, _P, _P, _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_vals_credit.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_int32,
                                   _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P]
-_L.hkv_wl_ack_offsets.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, _P]
+_L.hkv_wl_ack_offsets.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, _P]
 _L.hkv_wl_pack_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_peer_locate.argtypes = [_P, _P, ctypes.c_int64, ctypes.c_uint32, _P, _P]
 _L.hkv_wl_peer_ts_at.argtypes = [_P, _P, _P, _P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
@@ -153,7 +154,12 @@ class Round:
             self.vq_n = torch.zeros(W, dtype=torch.int32, device=dev)
             self.val_overflow = torch.zeros(1, dtype=torch.int64, device=dev)
             self.val_totals = torch.zeros(2, dtype=torch.int64, device=dev)  # VALs sent, gated worker-rounds
-        self.maxc_h = torch.zeros(2, dtype=torch.int32, pin_memory=True) if self.fit else None
+        self.maxc_h = torch.zeros(4, dtype=torch.int32, pin_memory=True) if self.fit else None
+        # the host spins on the flag word the kernel writes after the total (ack_spin), or waits on
+        # an event after the kernel
+        self.ack_spin = os.environ.get("HKV_ACK_EVENT", "0") != "1"
+        self._ack_seq = 0
+        self._ack_flag = ctypes.c_int32.from_address(self.maxc_h.data_ptr() + 8) if self.fit else None
         self.ack_off = torch.zeros(W + 1, dtype=torch.int32, device=dev) if self.fit else None
         self.ack_total = 0
         self.maxc_ev = torch.cuda.Event() if self.fit else None
@@ -365,9 +371,11 @@ class Round:
         if self.count_elems:
             self.inv_total += self.inv_count.sum()
         if self.fit and alive:
+            self._ack_seq = self._ack_seq % 0x7FFFFFFF + 1 if self.ack_spin else 0
             check(_L.hkv_wl_ack_offsets(_ptr(self.inv_count), self.W, alive, _ptr(self.ack_off), _ptr(self.maxc_h),
-                                        _s()), "ack_offsets")
-            self.maxc_ev.record()
+                                        self._ack_seq, _s()), "ack_offsets")
+            if not self.ack_spin:
+                self.maxc_ev.record()
         if self.R:
             ri, rv = self.remote_inv[k], self.remote_val[k]
             ic = self._slot_counts(k, sent)
@@ -380,7 +388,16 @@ class Round:
                 self.marshal_acks(ri, self.W * self.rstride, self.ack_out)
             m = self.C
             if self.fit and alive:   # the GPU is still on the INV batch: this wait leaves no gap
-                self.maxc_ev.synchronize()
+                if self.ack_spin:
+                    spins = 0
+                    while self._ack_flag.value != self._ack_seq:
+                        spins += 1
+                        if spins % 65536 == 0:   # a lost flag fails loudly instead of spinning on
+                            torch.cuda.synchronize()
+                            if self._ack_flag.value != self._ack_seq:
+                                raise RuntimeError("ACK layout flag never arrived")
+                else:
+                    self.maxc_ev.synchronize()
                 self.ack_total = int(self.maxc_h[0])
                 m = min(int(self.maxc_h[1]), self.C)
             if alive and self.V is not None:

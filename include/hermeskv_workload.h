@@ -138,10 +138,11 @@ int hkv_wl_peer_acks(hkv_table *t, const uint8_t *d_inv_out, const int32_t *d_in
 
 /* Offsets of a packed ACK batch answering d_inv_count[0..n_workers) INVs from n_peers peers:
  * d_offsets[w] = n_peers * (INVs of workers before w), d_offsets[n_workers] = the total. h_out
- * (pinned host memory, 2 ints) receives the total and the largest d_inv_count once the stream
- * passes this call. */
+ * (pinned host memory, 3 ints) receives the total and the largest d_inv_count: seq = 0, once
+ * the stream passes this call (wait on an event); seq > 0, with h_out[2] = seq written after
+ * them, for the host to spin on (no event, no fence on the stream). */
 int hkv_wl_ack_offsets(const int32_t *d_inv_count, int32_t n_workers, int32_t n_peers, int32_t *d_offsets,
-                       int32_t *h_out, void *stream);
+                       int32_t *h_out, int32_t seq, void *stream);
 
 /* ---- replica groups (one replica per GPU, slabs exchanged over RCCL) ------------------ */
 

@@ -891,6 +891,45 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
         reinterpret_cast<uint64_t *>(dst)[bytes / 8 - 1] = reinterpret_cast<const uint64_t *>(sops)[bytes / 8 - 1];
 }
 
+// k_resolve0 for big ops (312 B) in place: one thread per element on its global copy, no LDS, so
+// occupancy is bound by registers instead of by 312 B of LDS per element (local and ACK launches)
+template <int TYPE, int SV>
+__global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    const uint32_t e = a.ent[i];
+    uint8_t st = kStDone;
+    uint8_t *xg;
+    uint8_t idx;
+    Ctx c = make_ctx(a);
+    elem_at(a, (uint32_t)i, xg, idx, c);
+    if (e != kNone) {
+        Meta m;
+        meta_load(entry_of(a, e), m);
+        const uint32_t f = (uint8_t)(m.w5 >> 16) == a.ltag ? first_cand(*fw_of(a, e), a.rtag0) : kNone;
+        if (f == kNone || (uint32_t)i < f) {
+            Meta tm = m;
+            dispatch<SV>(TYPE, xg, entry_of(a, e), idx, tm, c);
+            if (a.error_flags && !meta_equal(tm, m)) atomicOr(a.error_flags, 1u);
+        } else if ((uint32_t)i == f) {
+            apply_to_shadow<TYPE, SV>(a, nullptr, (uint32_t)i, entry_of(a, e));
+            st = kStCommit;
+        } else if (a.rounds == 0) {
+            Meta m1 = m;
+            m_set_state(m1, absorbing_state<TYPE>());
+            Meta tm = m1;
+            dispatch<SV>(TYPE, xg, entry_of(a, e), idx, tm, c);
+            if (a.error_flags && !meta_equal(tm, m1)) atomicOr(a.error_flags, 1u);
+        } else {
+            a.pf[i] = f;
+            st = kStPend;
+        }
+    }
+    a.st[i] = st;
+    note_state(a, i, xg);
+}
+
 // Round r >= 1 resolve over the pending elements (sparse: direct global access), against S_r in
 // the shadow of round r-1's first candidate of the element's key.
 // After the last round, elements still pending go to the fallback list.
@@ -1572,6 +1611,11 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     const unsigned grid = (unsigned)((n + 255) / 256);
     const unsigned cgrid = (unsigned)((n + 256 * kCandPer - 1) / (256 * kCandPer));
     const bool big = bl.esz > 64;
+    // big ops: local and ACK launches resolve round 0 in place (measured at cfg3: local 1.26 ->
+    // 1.05 ms, ACK 0.69 -> 0.55 ms); INV launches keep the LDS slab (0.40 vs 0.52 ms in place).
+    // HKV_BIG_DIRECT=0/1 forces one or the other (experiments).
+    static const int big_env = getenv("HKV_BIG_DIRECT") ? atoi(getenv("HKV_BIG_DIRECT")) : -1;
+    const bool big_direct = big_env >= 0 ? big_env != 0 : bl.type != kInvs;
     const unsigned rgrid = (unsigned)(big ? (n + 127) / 128 : grid);
     const size_t rlds = (size_t)(big ? 128 : 256) * (size_t)bl.esz;
     constexpr int64_t kPer = 64 * kLookupPair;  // elements per k_lookup block
@@ -1607,7 +1651,8 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
             hipFuncSetAttribute((const void *)k_resolve0<T, V, 128>,                              \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds) != hipSuccess) \
             return -3;                                                                            \
-        if (big) hipLaunchKernelGGL((k_resolve0<T, V, 128>), dim3(rgrid), dim3(128), rlds, s, a); \
+        if (big && big_direct) hipLaunchKernelGGL((k_resolve0_direct<T, V>), dim3(grid), dim3(256), 0, s, a); \
+        else if (big) hipLaunchKernelGGL((k_resolve0<T, V, 128>), dim3(rgrid), dim3(128), rlds, s, a); \
         else hipLaunchKernelGGL((k_resolve0<T, V, 256>), dim3(rgrid), dim3(256), rlds, s, a);     \
         for (int r = 1; r <= a.rounds; ++r) {                                                     \
             hipLaunchKernelGGL((k_cand<T>), dim3(cgrid), dim3(256), 0, s, a, r);                  \

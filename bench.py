@@ -121,8 +121,8 @@ def main():
 
     cfg3 = a.config == "cfg3"
     cfg5 = a.config == "cfg5"
-    if a.keys is None:  # cfg3: 320-B entries; 10M keys keep log offsets within 32-bit entry ids
-        a.keys = 10_000_000 if cfg3 else 100_000_000 if world == 1 and not cfg5 else 1_000_000_000
+    if a.keys is None:  # cfg3: configs[1]'s 100M keys in 320-B entries (a 32 GiB log)
+        a.keys = 100_000_000 if world == 1 and not cfg5 else 1_000_000_000
     if cfg3 and world > 1:
         raise SystemExit("--config cfg3 runs on one GPU with virtual peers")
     if a.write_permille is None:

@@ -161,7 +161,11 @@ static void make_geometry(const hkv_config &c, Geometry &g)
     g.entry_size = (kEntryMetaOff + kvs_value + 7u) & ~7u;
     g.shift = c.big_objects ? 3u : 0u;
     g.op_size = (kOpMetaSize + 2u + g.st_value + 7u) & ~7u;
-    g.entry_unit = (c.log_cap % g.entry_size == 0) ? g.entry_size : 8u;
+    // entries start at multiples of entry_size from offset 0, modulo the power-of-two capacity: so
+    // every offset is a multiple of the largest power of two dividing entry_size (64 for 320-B
+    // entries), which keeps 32-bit entry ids valid up to 256 GiB of log
+    const uint32_t low = g.entry_size & (~g.entry_size + 1u);
+    g.entry_unit = (c.log_cap % g.entry_size == 0) ? g.entry_size : (low > 8u ? low : 8u);
     g.rmw_enabled = c.rmw_enabled ? 1u : 0u;
     g.machine_id = c.machine_id;
 }

@@ -740,6 +740,10 @@ __device__ __forceinline__ uint64_t find_entry(const TableView &t, uint64_t key)
     return ~0ull;
 }
 
+// The virtual peers' per-entry words: live entries never overlap and are entry_size long, so
+// phys / entry_size is distinct for every entry (one slot per possible entry, not per 8 bytes)
+__device__ __forceinline__ uint64_t peer_slot(const TableView &t, uint64_t phys) { return phys / t.g.entry_size; }
+
 // peer_ts words: round tag (23 bits) << 41 | the write's RMW flag << 40 | its 40-bit timestamp
 __device__ __forceinline__ uint32_t peer_round_tag(uint32_t round) { return (round + 1u) & 0x7FFFFFu; }
 
@@ -817,7 +821,7 @@ __global__ __launch_bounds__(256) void k_peer_ts(TableView t, uint8_t *invs, uin
         if (ok[k] && ekey == key[k]) {
             ver = cur + ((!t.g.rmw_enabled || rmw) ? 2u : 4u);
             if (peer_ts && peer < 8)
-                atomicMax(peer_ts + (phys[k] / t.g.entry_unit) * 8 + peer,
+                atomicMax(peer_ts + peer_slot(t, phys[k]) * 8 + peer,
                           ((unsigned long long)peer_round_tag(round) << 41) | ((unsigned long long)rmw << 40) |
                               ((unsigned long long)ver << 8) | peer);
         }
@@ -843,7 +847,7 @@ __device__ __forceinline__ void peer_answer(const uint8_t *x, uint8_t *y, uint32
     if (peer_ts && (x[16] & 1u) && peer < 8 && ack_size >= op_size) {
         const uint64_t phys = find_entry(t, h.a);
         if (phys != ~0ull) {
-            const unsigned long long pw = peer_ts[(phys / t.g.entry_unit) * 8 + peer];
+            const unsigned long long pw = peer_ts[peer_slot(t, phys) * 8 + peer];
             const uint64_t ours = ((uint64_t)(uint32_t)(h.b >> 32) << 8) | (uint8_t)(h.b >> 24);
             if ((uint32_t)(pw >> 41) == peer_round_tag(round) && (pw & 0xFFFFFFFFFFull) > ours) {
                 const uint64_t pts = pw & 0xFFFFFFFFFFull;
@@ -1071,7 +1075,7 @@ __global__ __launch_bounds__(256) void k_peer_ts_at(TableView t, uint8_t *invs, 
     if (ok) {
         ver = cur + ((!t.g.rmw_enabled || rmw) ? 2u : 4u);
         if (peer_ts && peer < 8)
-            atomicMax(peer_ts + (phys / t.g.entry_unit) * 8 + peer,
+            atomicMax(peer_ts + peer_slot(t, phys) * 8 + peer,
                       ((unsigned long long)peer_round_tag(round) << 41) | ((unsigned long long)rmw << 40) |
                           ((unsigned long long)ver << 8) | peer);
     }
@@ -1230,7 +1234,7 @@ uint64_t hkv_wl_peer_ts_words(const hkv_table *t)
 {
     TableView tv;
     if (table_view(t, &tv)) return 0;
-    return (tv.g.log_cap / tv.g.entry_unit + 1) * 8;
+    return (tv.g.log_cap / tv.g.entry_size + 1) * 8;
 }
 
 int hkv_wl_marshal_invs_cap(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint8_t *out,

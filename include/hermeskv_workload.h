@@ -106,8 +106,8 @@ int hkv_wl_gen_peer_round(uint8_t *d_invs, uint8_t *d_vals, int32_t *d_peer_coun
 
 /* At the start of a round: the first d_counts[w] INVs of each worker's row (and their VALs) take
  * the timestamp the peer's write gives, read from table t. d_peer_ts (RMW builds, may be NULL;
- * hkv_wl_peer_ts_words() zeroed words) records each peer's write per [entry][peer id] for
- * hkv_wl_peer_acks. */
+ * hkv_wl_peer_ts_words() zeroed words: 8 per possible entry, log_cap / entry size + 1 of them)
+ * records each peer's write per [entry][peer id] for hkv_wl_peer_acks. */
 int hkv_wl_peer_ts(hkv_table *t, uint8_t *d_invs, uint8_t *d_vals, const int32_t *d_counts, int32_t n_workers,
                    int32_t stride, uint32_t op_size, unsigned long long *d_peer_ts, uint32_t round, void *stream);
 uint64_t hkv_wl_peer_ts_words(const hkv_table *t);

@@ -60,7 +60,7 @@ struct BatchArgs {
     int32_t *ns_idx;
     unsigned long long *fw;      // [log_cap / 64] F word per 64-B log line (table-wide), see fw_index
     unsigned long long *fx, *fy; // [log_cap / 64] INV words X, Y (INV direct path; zero between launches)
-    uint32_t *ft;                // [log_cap / 64][8] ACK words T (ACK direct path; zero between launches)
+    unsigned long long *ft;      // [log_cap / 64][8] ACK words T (ACK direct path; epoch << 32 | ~i)
     uint32_t fw_mask;
     uint32_t *ent;               // [n] entry id of every element (kNone: skipped or missing)
     uint8_t *st;                 // [n] stage (kSt*)
@@ -155,8 +155,9 @@ constexpr int64_t kInvDirectMax = 1 << 23;
 // completion). Opcodes: ACK_SUCCESS (a LAST_ACK_SUCCESS input stays, except at j*),
 // LAST_ACK_SUCCESS for j* from WRITE or REPLAY. k_lookup finishes the non-matching elements, sets T (as max of ~i) and F
 // and caches each matching element's ack_bv / state / op buffer index in pf; in k_ack_resolve
-// j* (or, without a completion, F) applies the key's meta; k_ack_clear zeroes T.
-enum : uint8_t { kAkMatch = 1, kAkApply = 2 };
+// j* (or, without a completion, F) applies the key's meta. T words carry the launch's epoch in
+// their upper half, so a word of an earlier launch reads as empty and nothing is cleared.
+enum : uint8_t { kAkMatch = 1 };
 
 __device__ __forceinline__ uint8_t ack_opcode(uint8_t in) { return in == kLastAckSuccess ? in : kAckSuccess; }
 
@@ -475,9 +476,9 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                     // quorum is complete already (the first match then completes)
                     if (snd >= 8 || (uint8_t)(a.g_membership & ~m_ack_bv(m0[k])) == 0)
                         offer(a.fw + w, a.rtag0, (uint32_t)gi[k]);
-                    if (snd < 8) {
-                        uint32_t *t = a.ft + (size_t)w * 8 + snd;
-                        const uint32_t tv = 0xFFFFFFFFu - (uint32_t)gi[k];
+                    if (snd < 8) {  // tagged with the launch: no clearing between launches
+                        unsigned long long *t = a.ft + (size_t)w * 8 + snd;
+                        const unsigned long long tv = ((unsigned long long)(a.rtag0 >> 3) << 32) | (0xFFFFFFFFu - (uint32_t)gi[k]);
                         if (tv > __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(t, tv);
                     }
                     a.pf[gi[k]] = (uint32_t)m_ack_bv(m0[k]) | ((uint32_t)m_state(m0[k]) << 8) | ((uint32_t)m_obi(m0[k]) << 16);
@@ -673,9 +674,14 @@ __global__ __launch_bounds__(256) void k_ack_resolve(BatchArgs a)
     const uint32_t w = fw_index(a, phys_of(a, e));
     const uint32_t c0 = a.pf[i];
     const uint8_t bv0 = (uint8_t)c0, st0 = (uint8_t)(c0 >> 8), obi0 = (uint8_t)(c0 >> 16);
-    const uint4 *tp = reinterpret_cast<const uint4 *>(a.ft + (size_t)w * 8);
-    const uint4 t0 = tp[0], t1 = tp[1];
-    const uint32_t tv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+    const U64x2 *tp = reinterpret_cast<const U64x2 *>(a.ft + (size_t)w * 8);
+    uint32_t tv[8];  // 0: no match of that sender in this launch
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const U64x2 p = tp[h];
+        tv[2 * h] = (uint32_t)(p.a >> 32) == (a.rtag0 >> 3) ? (uint32_t)p.a : 0u;
+        tv[2 * h + 1] = (uint32_t)(p.b >> 32) == (a.rtag0 >> 3) ? (uint32_t)p.b : 0u;
+    }
     const uint8_t need = (uint8_t)(a.g_membership & ~bv0);
     // the first match of senders 0..7 (min T), and of any sender (with F; F is offered only by
     // matches from senders >= 8, or by every match when need is empty)
@@ -729,17 +735,6 @@ __global__ __launch_bounds__(256) void k_ack_resolve(BatchArgs a)
         }
     }
     meta_store(entry, m);
-    a.st[i] = kAkApply;
-}
-
-// ACK direct path: the appliers zero their keys' T words.
-__global__ __launch_bounds__(256) void k_ack_clear(BatchArgs a)
-{
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.n || a.st[i] != kAkApply) return;
-    uint4 *tp = reinterpret_cast<uint4 *>(a.ft + (size_t)fw_index(a, phys_of(a, a.ent[i])) * 8);
-    tp[0] = make_uint4(0u, 0u, 0u, 0u);
-    tp[1] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // ------------------------------------------------------------------ rounds (passes over all elements)
@@ -928,6 +923,365 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
     }
     a.st[i] = st;
     note_state(a, i, xg);
+}
+
+// ------------------------------------------------------------------ local launches: direct path
+// Local batches without RMWs, 56-B ops and 64-B entries (configs[1]). Under these, an element's
+// key can only be mutated by a PUT (hermes_exec_write) from VALID/INVALID, or by a GET replay
+// from INVALID (hermes_exec_read -> write replay), and its first mutation leaves the key in an
+// absorbing state (WRITE/REPLAY, see absorbing_state). So every element's result is fixed by S_0
+// and by F, its key's first mutating element:
+//   i < F (or no F): the exec function against S_0;  i = F: S_0 -> its shadow;  i > F: against WRITE.
+// Three passes instead of lookup + re-reading every op and entry line:
+//   k_local_pre    the PUTs only (one op header per element, then bucket + log line per PUT):
+//                  every PUT that mutates S_0 offers F and tags its entry's seqlock byte;
+//   k_local_fused  every element: op slab through LDS, bucket, log line (the whole 64-B entry, four
+//                  lanes) -- F is final for every key not INVALID at S_0, so each element resolves
+//                  right there, F applies itself to its shadow, and the slab is written back once;
+//                  elements of INVALID keys (where GET replays may mutate: they offer F here) wait;
+//   k_local_deferred  those waiting elements, against the final F.
+// k_commit then installs the shadows. Measured against k_lookup + k_resolve0: the entry line and
+// the op slab are read once instead of twice.
+constexpr int kPreElems = 512;           // elements per k_local_pre block
+constexpr int kPreHead = 1024;           // launch head whose PUT keys every block knows
+constexpr int kPreHash = 1024;           // LDS slots of the head's (key -> first PUT) table
+constexpr int kLfElems = 32;             // elements per k_local_fused block (one wave)
+enum { kCtrDefer = 3 };
+enum : uint8_t { kStDefer = 3 };
+
+// Four lanes (q = lane & 3) look up kLookupPair keys side by side: the 64-B bucket (16 B per
+// lane), the reference's slot order (first tag match, hermesKV.c:954-975), the log window
+// (:969-970), then each lane's 16 B of the 64-B log line (bytes 16q..16q+15). All four lanes of a
+// group call it with the same arguments.
+__device__ __forceinline__ void lookup_pair(const BatchArgs &a, const uint64_t *key, const bool *probe, int q,
+                                            int gbase, bool *ok, uint64_t *phys, uint4 *ln)
+{
+    uint4 v[kLookupPair];
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k)
+        v[k] = probe[k] ? reinterpret_cast<const uint4 *>(a.index + ((key[k] & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u)[q]
+                        : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        const uint64_t s0 = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
+        const uint64_t s1 = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
+        const uint32_t tag = (uint32_t)(key[k] >> 48);
+        const bool mt0 = probe[k] && (s0 & 1u) && ((uint32_t)(s0 >> 1) & 0x7FFFFFu) == tag;
+        const bool mt1 = probe[k] && (s1 & 1u) && ((uint32_t)(s1 >> 1) & 0x7FFFFFu) == tag;
+        const uint32_t g0 = (uint32_t)(__ballot(mt0) >> gbase) & 0xFu;
+        const uint32_t g1 = (uint32_t)(__ballot(mt1) >> gbase) & 0xFu;
+        uint32_t o = 0;  // bit 2*l + j: slot 2*l + j matches
+#pragma unroll
+        for (int l = 0; l < 4; ++l) o |= ((g0 >> l) & 1u) << (2 * l) | ((g1 >> l) & 1u) << (2 * l + 1);
+        const int first = o ? __ffs(o) - 1 : 0;
+        const uint64_t off = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
+        ok[k] = probe[k] && o && a.g.log_head - off < a.g.log_cap;
+        phys[k] = off & a.g.log_mask;
+    }
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k)
+        ln[k] = ok[k] ? reinterpret_cast<const uint4 *>(a.log + phys[k])[q] : make_uint4(0u, 0u, 0u, 0u);
+}
+
+// The key (bytes 8..15) and the meta (bytes 16..32) of a log line held 16 B per lane, in every lane
+__device__ __forceinline__ uint64_t line_key_meta(const uint4 &ln, Meta &m)
+{
+    const uint64_t ek = (uint64_t)(uint32_t)__shfl((int)ln.z, 0, 4) | ((uint64_t)(uint32_t)__shfl((int)ln.w, 0, 4) << 32);
+    m.w4 = (uint32_t)__shfl((int)ln.x, 1, 4);
+    m.w5 = (uint32_t)__shfl((int)ln.y, 1, 4);
+    m.ver = (uint32_t)__shfl((int)ln.z, 1, 4);
+    const uint32_t w7 = (uint32_t)__shfl((int)ln.w, 1, 4);
+    const uint32_t b32 = (uint32_t)__shfl((int)ln.x, 2, 4) & 0xFFu;
+    m.llw_cid = (uint8_t)w7;
+    m.llw_ver = (w7 >> 8) | (b32 << 24);
+    return ek;
+}
+
+// Wave-compacted append of (i, key) to an LDS list
+__device__ __forceinline__ void list_push(bool pred, uint32_t i, uint64_t key, uint32_t *li, uint64_t *lk,
+                                          uint32_t *cnt)
+{
+    const unsigned long long m = __ballot(pred);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, leader, 64);
+    if (pred) {
+        const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        li[pos] = i;
+        lk[pos] = key;
+    }
+}
+
+__device__ __forceinline__ uint32_t pre_slot(uint64_t key) { return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 54); }
+
+// The PUTs of kPreElems elements offer F. Whether a PUT mutates S_0 depends on S_0 alone
+// (hermes_exec_write: VALID or INVALID and no op buffer index), so either every PUT of a key is a
+// candidate or none is, and F is the key's first PUT or nothing. A Zipf-hot key's PUTs are spread
+// over every block, and all blocks of the launch are in flight together: every block first reads
+// the keys of the PUTs among the launch's first kPreHead elements (headers only, L2-resident after
+// the first block) and drops its PUTs whose key has a PUT there that comes first -- block 0 offers
+// that one. The rest look their key up and offer through the load-filtered atomicMin.
+__global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
+{
+    __shared__ uint32_t li[kPreElems];
+    __shared__ uint64_t lk[kPreElems];
+    __shared__ uint64_t hk[kPreHash];
+    __shared__ uint32_t hv[kPreHash];
+    __shared__ uint32_t nown;
+    const int tid = threadIdx.x, q = tid & 3, gbase = (tid & 63) & ~3;
+    if (tid == 0) {
+        nown = 0;
+        if (blockIdx.x == 0) a.ctr[kCtrDefer] = 0;
+    }
+    for (int j = tid; j < kPreHash; j += 256) {
+        hk[j] = ~0ull;
+        hv[j] = kNone;
+    }
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * kPreElems;
+    const bool use_head = blockIdx.x > 0;
+    // PUTs that are not skipped (hermes_skip_op, hermesKV.c:709-769): the head's go into the key
+    // table (key ~0 stays out: it is the empty mark), the block's own into the list. Every header
+    // load is issued before the first one is used.
+    constexpr int kOwnK = kPreElems / 256, kAllK = kPreElems / 256 + kPreHead / 256;
+    U64x2 h[kAllK];
+    bool in[kAllK];
+#pragma unroll
+    for (int k = 0; k < kAllK; ++k) {
+        const bool own = k < kOwnK;
+        const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
+        in[k] = own ? i < a.n : (use_head && i < i0 && i < a.n);  // the head: elements before the block's own
+        if (in[k]) {
+            const int32_t b = (int32_t)(i / a.stride);
+            in[k] = a.counts == nullptr || i - (int64_t)b * a.stride < a.counts[b];
+        }
+        h[k] = in[k] ? *reinterpret_cast<const U64x2 *>(a.elems + i * 56) : U64x2{0, 0};
+    }
+#pragma unroll
+    for (int k = 0; k < kAllK; ++k) {
+        const bool own = k < kOwnK;
+        const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
+        const uint64_t key = h[k].a;
+        const bool put = in[k] && (uint8_t)h[k].b == kOpPut && !skip_elem_os(kLocal, kOpPut, (uint8_t)(h[k].b >> 8));
+        if (own) {
+            list_push(put, (uint32_t)i, key, li, lk, &nown);
+        } else if (put && key != ~0ull) {
+            uint32_t sl = pre_slot(key);
+            for (;;) {
+                const unsigned long long old = atomicCAS((unsigned long long *)&hk[sl], ~0ull, key);
+                if (old == ~0ull || old == key) {
+                    atomicMin(&hv[sl], (uint32_t)i);
+                    break;
+                }
+                sl = (sl + 1) & (kPreHash - 1);
+            }
+        }
+    }
+    __syncthreads();
+    const Ctx c = make_ctx(a);
+    const uint64_t hput[2] = {0, (uint64_t)kOpPut};
+    const uint32_t cnt = nown;
+    for (uint32_t base = 0; base < cnt; base += 64 * kLookupPair) {
+        uint64_t key[kLookupPair];
+        bool probe[kLookupPair], ok[kLookupPair];
+        uint32_t idx[kLookupPair];
+        uint64_t phys[kLookupPair];
+        uint4 ln[kLookupPair];
+#pragma unroll
+        for (int k = 0; k < kLookupPair; ++k) {
+            const uint32_t j = base + k * 64 + (tid >> 2);
+            probe[k] = j < cnt;
+            key[k] = probe[k] ? lk[j] : 0;
+            idx[k] = probe[k] ? li[j] : kNone;
+            if (probe[k] && use_head && key[k] != ~0ull) {  // a head PUT of the same key comes first
+                uint32_t sl = pre_slot(key[k]);
+                for (;;) {
+                    const uint64_t hkk = hk[sl];
+                    if (hkk == ~0ull) break;
+                    if (hkk == key[k]) {
+                        probe[k] = hv[sl] > idx[k];
+                        break;
+                    }
+                    sl = (sl + 1) & (kPreHash - 1);
+                }
+            }
+        }
+        lookup_pair(a, key, probe, q, gbase, ok, phys, ln);
+#pragma unroll
+        for (int k = 0; k < kLookupPair; ++k) {
+            Meta m0;
+            const uint64_t ek = line_key_meta(ln[k], m0);
+            if (q != 0 || !ok[k] || ek != key[k]) continue;
+            if (!would_mutate(kLocal, reinterpret_cast<const uint8_t *>(hput), m0, c)) continue;
+            offer(a.fw + fw_index(a, phys[k]), a.rtag0, idx[k]);
+            if ((uint8_t)(m0.w5 >> 16) != a.ltag) a.log[phys[k] + kEntryMetaOff + 4] = a.ltag;
+        }
+    }
+}
+
+// Every element, F final (except on INVALID keys): see the section comment. One wave per block and
+// nothing shared beyond it. The lookup runs four lanes per element (each lane holds 16 B of the op
+// and of the log line); the wave-private LDS copies of op and entry are then resolved one element
+// per lane, so the exec code's branches are paid once per 32 elements; the ops go back whole.
+__global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
+{
+    __shared__ uint4 sops[kLfElems * 4];   // 64 B per op (56 used)
+    __shared__ uint4 sln[kLfElems * 4];
+    __shared__ unsigned long long sfw[kLfElems];
+    __shared__ uint32_t sent[kLfElems];     // entry id of a hit, kNone otherwise
+    __shared__ uint8_t sprb[kLfElems];      // probed (not skipped)
+    __shared__ uint32_t sdef[kLfElems];
+    __shared__ uint32_t ndef;
+    const int tid = threadIdx.x, q = tid & 3, gbase = tid & ~3;
+    const int64_t i0 = (int64_t)blockIdx.x * kLfElems;
+    if (tid == 0) ndef = 0;
+    uint64_t key[kLookupPair];
+    bool probe[kLookupPair], ok[kLookupPair], live[kLookupPair];
+    uint64_t phys[kLookupPair];
+    uint4 ln[kLookupPair], op[kLookupPair];
+    int te[kLookupPair];
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        te[k] = k * 16 + (tid >> 2);
+        const int64_t i = i0 + te[k];
+        live[k] = i < a.n;
+        op[k] = make_uint4(0u, 0u, 0u, 0u);
+        if (live[k]) {
+            const uint8_t *xg = a.elems + i * 56 + 16 * q;
+            if (q < 3) {
+                op[k] = *reinterpret_cast<const uint4 *>(xg);
+            } else {
+                const uint64_t t = *reinterpret_cast<const uint64_t *>(xg);
+                op[k].x = (uint32_t)t;
+                op[k].y = (uint32_t)(t >> 32);
+            }
+        }
+        sops[te[k] * 4 + q] = op[k];
+    }
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        // lane 0 of the group holds op bytes 0..15: the key and the header
+        key[k] = (uint64_t)(uint32_t)__shfl((int)op[k].x, 0, 4) | ((uint64_t)(uint32_t)__shfl((int)op[k].y, 0, 4) << 32);
+        const uint32_t h0 = (uint32_t)__shfl((int)op[k].z, 0, 4);
+        probe[k] = false;
+        if (live[k]) {
+            const int64_t i = i0 + te[k];
+            const int32_t b = (int32_t)(i / a.stride);
+            const int32_t idx = (int32_t)(i - (int64_t)b * a.stride);
+            probe[k] = (a.counts == nullptr || idx < a.counts[b]) && !skip_elem_os(kLocal, (uint8_t)h0, (uint8_t)(h0 >> 8));
+        }
+    }
+    lookup_pair(a, key, probe, q, gbase, ok, phys, ln);
+    // F of a key tagged by k_local_pre, loaded for both elements before either is resolved
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        Meta m;
+        const uint64_t ek = line_key_meta(ln[k], m);
+        const bool hit = ok[k] && ek == key[k];
+        const bool tagged = hit && m_state(m) != kInvalid && (uint8_t)(m.w5 >> 16) == a.ltag;
+        const unsigned long long f = tagged && q == 0 ? a.fw[fw_index(a, phys[k])] : ~0ull;
+        if (hit) sln[te[k] * 4 + q] = ln[k];
+        if (q == 0) {
+            sfw[te[k]] = f;
+            sent[te[k]] = hit ? (uint32_t)(phys[k] / a.g.entry_unit) : kNone;
+            sprb[te[k]] = probe[k];
+        }
+    }
+    __syncthreads();
+    if (tid < kLfElems && i0 + tid < a.n) {
+        const int64_t i = i0 + tid;
+        uint8_t *x = reinterpret_cast<uint8_t *>(&sops[tid * 4]);
+        uint8_t *ent = reinterpret_cast<uint8_t *>(&sln[tid * 4]);
+        const uint32_t e = sent[tid];
+        uint8_t st = kStDone;
+        if (e != kNone) {
+            Ctx c = make_ctx(a);
+            const uint8_t bidx = (uint8_t)(i - (i / a.stride) * a.stride);
+            Meta m;
+            meta_load(ent, m);
+            const bool wm = would_mutate(kLocal, x, m, c);
+            if (m_state(m) == kInvalid) {
+                // GET replays may mutate: they offer F now, and the key's elements resolve later
+                if (wm) {
+                    const uint64_t ph = phys_of(a, e);
+                    offer(a.fw + fw_index(a, ph), a.rtag0, (uint32_t)i);
+                    if ((uint8_t)(m.w5 >> 16) != a.ltag) a.log[ph + kEntryMetaOff + 4] = a.ltag;
+                }
+                st = kStDefer;
+                sdef[atomicAdd(&ndef, 1u)] = (uint32_t)i;
+            } else {
+                const uint32_t f = first_cand(sfw[tid], a.rtag0);
+                // a mutating element must have offered itself in k_local_pre
+                if (wm && (f == kNone || f > (uint32_t)i) && a.error_flags) atomicOr(a.error_flags, 4u);
+                Meta m0 = m;
+                if ((uint32_t)i == f) {
+                    apply_to_shadow<kLocal, 31>(a, x, (uint32_t)i, ent);
+                    st = kStCommit;
+                } else {
+                    if (f != kNone && (uint32_t)i > f) m_set_state(m0, absorbing_state<kLocal>());
+                    Meta tm = m0;
+                    dispatch<31>(kLocal, x, ent, bidx, tm, c);
+                    if (a.error_flags && !meta_equal(tm, m0)) atomicOr(a.error_flags, 1u);
+                }
+            }
+        } else if (sprb[tid]) {
+            x[9] = kMiss;
+        }
+        a.ent[i] = e;
+        a.st[i] = st;
+        if (st != kStDefer) note_state(a, i, x);
+    }
+    __syncthreads();
+    // the waiting elements (keys INVALID at S_0: rare), appended once per block
+    if (ndef && tid == 0) {
+        const uint32_t base = atomicAdd(&a.ctr[kCtrDefer], ndef);
+        for (uint32_t j = 0; j < ndef; ++j) a.fbl[base + j] = sdef[j];
+    }
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        if (!live[k]) continue;
+        uint8_t *xg = a.elems + (i0 + te[k]) * 56 + 16 * q;
+        const uint4 w = sops[te[k] * 4 + q];
+        if (q < 3) *reinterpret_cast<uint4 *>(xg) = w;
+        else *reinterpret_cast<uint64_t *>(xg) = (uint64_t)w.x | ((uint64_t)w.y << 32);
+    }
+}
+
+// Elements of keys that were INVALID at S_0, against their key's final F (k_resolve0_direct's rules)
+__global__ __launch_bounds__(256) void k_local_deferred(BatchArgs a)
+{
+    const uint32_t nd = a.ctr[kCtrDefer];
+    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < nd; j += gridDim.x * 256u) {
+        const uint32_t i = a.fbl[j];
+        const uint32_t e = a.ent[i];
+        uint8_t *xg;
+        uint8_t idx;
+        Ctx c = make_ctx(a);
+        elem_at(a, i, xg, idx, c);
+        Meta m;
+        meta_load(entry_of(a, e), m);
+        const uint32_t f = first_cand(*fw_of(a, e), a.rtag0);
+        uint8_t st = kStDone;
+        if (f == kNone || i < f) {
+            Meta tm = m;
+            dispatch<31>(kLocal, xg, entry_of(a, e), idx, tm, c);
+            if (a.error_flags && !meta_equal(tm, m)) atomicOr(a.error_flags, 1u);
+        } else if (i == f) {
+            apply_to_shadow<kLocal, 31>(a, nullptr, i, entry_of(a, e));
+            st = kStCommit;
+        } else {
+            Meta m1 = m;
+            m_set_state(m1, absorbing_state<kLocal>());
+            Meta tm = m1;
+            dispatch<31>(kLocal, xg, entry_of(a, e), idx, tm, c);
+            if (a.error_flags && !meta_equal(tm, m1)) atomicOr(a.error_flags, 1u);
+        }
+        a.st[i] = st;
+        note_state(a, i, xg);
+    }
 }
 
 // Round r >= 1 resolve over the pending elements (sparse: direct global access), against S_r in
@@ -1621,9 +1975,19 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     constexpr int64_t kPer = 64 * kLookupPair;  // elements per k_lookup block
     const bool small = (bl.path == kPathSmall || (bl.path == kPathAuto && n <= kSmallMax)) && n <= kSmallMax;
     if (bl.region_bytes && !small) return -1;  // host-staged launches are small ones
+    // local batches without RMWs in the default layout: the direct path (k_local_pre). HKV_LOCAL_DIRECT=0
+    // runs them on the rounds engine instead (experiments)
+    static const int ld_env = getenv("HKV_LOCAL_DIRECT") ? atoi(getenv("HKV_LOCAL_DIRECT")) : 1;
+    const bool local_direct = ld_env != 0 && bl.type == kLocal && !bl.g.rmw_enabled && bl.esz == 56 &&
+                              bl.g.st_value == 31 && bl.g.entry_size == 64 && !bl.offsets;
     if (small) {
         if (launch_small(a, s)) return -3;
         return 0;                              // node_suspected written by the kernel
+    } else if (local_direct) {
+        hipLaunchKernelGGL(k_local_pre, dim3((unsigned)((n + kPreElems - 1) / kPreElems)), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_local_fused, dim3((unsigned)((n + kLfElems - 1) / kLfElems)), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(k_local_deferred, dim3(64), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_commit<31>), dim3(grid), dim3(256), 0, s, a);
     } else if (bl.type == kVals) {             // one pass (see k_lookup)
         hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, n);
         return hipGetLastError() == hipSuccess ? 0 : -3;
@@ -1638,7 +2002,6 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
         hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n - head + kPer - 1) / kPer)), dim3(256), 0, s, a, head, n);
     if (a.ack_direct) {
         hipLaunchKernelGGL(k_ack_resolve, dim3(grid), dim3(256), 0, s, a);
-        hipLaunchKernelGGL(k_ack_clear, dim3(grid), dim3(256), 0, s, a);
     } else if (a.inv_direct) {
         hipLaunchKernelGGL(k_inv_resolve, dim3(grid), dim3(256), 0, s, a, (int64_t)0, n);
         if (bl.g.st_value == 31) hipLaunchKernelGGL((k_inv_commit<31>), dim3(grid), dim3(256), 0, s, a);

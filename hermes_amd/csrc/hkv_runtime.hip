@@ -183,15 +183,15 @@ static int bit_width(uint64_t x)
 static int ensure_batch_scratch(hkv_table *t, int64_t n)
 {
     if (!t->d_fw) {
-        // F words, the INV words X and Y (batch_fw_words each), then the ACK words T (eight u32
-        // per line), see hkv_batch.hip
+        // F words, the INV words X and Y (batch_fw_words each), then the ACK words T (eight
+        // epoch-tagged u64 per line), see hkv_batch.hip
         const size_t bytes = 8 * batch_fw_words(t->cfg.log_cap);
-        HIP_TRY(hipMalloc(&t->d_fw, 7 * bytes));
-        // F all-ones: every F word reads as stale for every epoch; X, Y and T zero (they are
-        // cleared by the launch that sets them). hipMemset runs on the null stream, which does
-        // not order the table's non-blocking streams: wait for it here.
+        HIP_TRY(hipMalloc(&t->d_fw, 11 * bytes));
+        // F all-ones: every F word reads as stale for every epoch; X and Y zero (they are cleared
+        // by the launch that sets them), T zero (older epochs read as empty). hipMemset runs on
+        // the null stream, which does not order the table's non-blocking streams: wait for it here.
         HIP_TRY(hipMemset(t->d_fw, 0xFF, bytes));
-        HIP_TRY(hipMemset(reinterpret_cast<uint8_t *>(t->d_fw) + bytes, 0, 6 * bytes));
+        HIP_TRY(hipMemset(reinterpret_cast<uint8_t *>(t->d_fw) + bytes, 0, 10 * bytes));
         HIP_TRY(hipDeviceSynchronize());
         t->epoch = 0;
     }
@@ -430,9 +430,10 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.fw = t->d_fw;
     bl.fx = t->d_fw + batch_fw_words(t->cfg.log_cap);
     bl.fy = bl.fx + batch_fw_words(t->cfg.log_cap);
-    bl.ft = reinterpret_cast<uint32_t *>(bl.fy + batch_fw_words(t->cfg.log_cap));
-    if (++t->epoch > batch_max_epoch()) {  // round tags would wrap: start the F words over
+    bl.ft = bl.fy + batch_fw_words(t->cfg.log_cap);
+    if (++t->epoch > batch_max_epoch()) {  // round tags would wrap: start the F and T words over
         HIP_TRY(hipMemsetAsync(t->d_fw, 0xFF, 8 * batch_fw_words(t->cfg.log_cap), s));
+        HIP_TRY(hipMemsetAsync(bl.ft, 0, 64 * batch_fw_words(t->cfg.log_cap), s));
         t->epoch = 1;
     }
     bl.epoch = t->epoch;

@@ -60,7 +60,7 @@ struct BatchArgs {
     int32_t *ns_idx;
     unsigned long long *fw;      // [log_cap / 64] F word per 64-B log line (table-wide), see fw_index
     unsigned long long *fx, *fy; // [log_cap / 64] INV words X, Y (INV direct path; zero between launches)
-    unsigned long long *ft;      // [log_cap / 64][8] ACK words T (ACK direct path; epoch << 32 | ~i)
+    uint32_t *ft;                // [log_cap / 64][8] ACK words T (ACK direct path; tag << 21 | ~i)
     uint32_t fw_mask;
     uint32_t *ent;               // [n] entry id of every element (kNone: skipped or missing)
     uint8_t *st;                 // [n] stage (kSt*)
@@ -81,6 +81,7 @@ struct BatchArgs {
     int32_t rounds;              // rounds after round 0 before the fallback
     int32_t inv_direct;          // INV launch on the direct path (k_inv_resolve)
     int32_t ack_direct;          // ACK launch on the direct path (k_ack_resolve)
+    uint32_t ack_tag;            // its T words' tag
     uint8_t g_membership;
     uint8_t w_ack_init;
     int32_t *node_suspected;     // small launches write it themselves
@@ -94,6 +95,8 @@ struct BatchArgs {
     unsigned long long *prof;    // HKV_SMALL_PROF: phase timestamps of k_small (debug)
     const SmallBatch *hdr;       // mixed small launches: the batch headers (in dev_region)
     uint8_t *state_out;          // local launches: each element's final state byte (may be NULL)
+    const uint8_t *opc;          // local launches: the caller's opcode mirror (may be NULL, see k_local_pre)
+    int32_t dbg;                 // HKV_DBG: timing experiments that skip work (results invalid)
 };
 
 // Rounds after round 0 per batch type: how often a hot key usually mutates in one launch beyond
@@ -155,9 +158,15 @@ constexpr int64_t kInvDirectMax = 1 << 23;
 // completion). Opcodes: ACK_SUCCESS (a LAST_ACK_SUCCESS input stays, except at j*),
 // LAST_ACK_SUCCESS for j* from WRITE or REPLAY. k_lookup finishes the non-matching elements, sets T (as max of ~i) and F
 // and caches each matching element's ack_bv / state / op buffer index in pf; in k_ack_resolve
-// j* (or, without a completion, F) applies the key's meta. T words carry the launch's epoch in
-// their upper half, so a word of an earlier launch reads as empty and nothing is cleared.
+// j* (or, without a completion, F) applies the key's meta. T words are u32: an 11-bit tag (the
+// table's direct-path ACK launch count mod 2048) over 21 bits of (2^21 - 1 - element), so a word
+// of an earlier launch reads as empty. Nothing clears the words a launch sets; instead every such
+// launch first zeroes 1/2048 of the T array (the slice of its tag), so each word is zeroed at least
+// once between two launches with the same tag. Launches of 2^21 - 1 elements or more take the rounds
+// engine.
 enum : uint8_t { kAkMatch = 1 };
+constexpr int kAckIdxBits = 21, kAckTags = 2048;
+constexpr uint32_t kAckIdxMask = (1u << kAckIdxBits) - 1;
 
 __device__ __forceinline__ uint8_t ack_opcode(uint8_t in) { return in == kLastAckSuccess ? in : kAckSuccess; }
 
@@ -476,10 +485,17 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                     // quorum is complete already (the first match then completes)
                     if (snd >= 8 || (uint8_t)(a.g_membership & ~m_ack_bv(m0[k])) == 0)
                         offer(a.fw + w, a.rtag0, (uint32_t)gi[k]);
-                    if (snd < 8) {  // tagged with the launch: no clearing between launches
-                        unsigned long long *t = a.ft + (size_t)w * 8 + snd;
-                        const unsigned long long tv = ((unsigned long long)(a.rtag0 >> 3) << 32) | (0xFFFFFFFFu - (uint32_t)gi[k]);
-                        if (tv > __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(t, tv);
+                    if (snd < 8) {  // tagged with the launch (see kAckTagBits)
+                        // tags wrap, so a stale word may compare larger: replace it by CAS, keep the
+                        // smallest element of this launch's tag
+                        uint32_t *t = a.ft + (size_t)w * 8 + snd;
+                        const uint32_t tv = (a.ack_tag << kAckIdxBits) | (kAckIdxMask - (uint32_t)gi[k]);
+                        uint32_t old = __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        while ((old >> kAckIdxBits) != a.ack_tag || old < tv) {
+                            const uint32_t seen = atomicCAS(t, old, tv);
+                            if (seen == old) break;
+                            old = seen;
+                        }
                     }
                     a.pf[gi[k]] = (uint32_t)m_ack_bv(m0[k]) | ((uint32_t)m_state(m0[k]) << 8) | ((uint32_t)m_obi(m0[k]) << 16);
                 }
@@ -674,14 +690,13 @@ __global__ __launch_bounds__(256) void k_ack_resolve(BatchArgs a)
     const uint32_t w = fw_index(a, phys_of(a, e));
     const uint32_t c0 = a.pf[i];
     const uint8_t bv0 = (uint8_t)c0, st0 = (uint8_t)(c0 >> 8), obi0 = (uint8_t)(c0 >> 16);
-    const U64x2 *tp = reinterpret_cast<const U64x2 *>(a.ft + (size_t)w * 8);
-    uint32_t tv[8];  // 0: no match of that sender in this launch
+    const uint4 *tp = reinterpret_cast<const uint4 *>(a.ft + (size_t)w * 8);
+    const uint4 t0 = tp[0], t1 = tp[1];
+    const uint32_t tr[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+    uint32_t tv[8];  // 0xFFFFFFFF - (first match of the sender), 0: none in this launch
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        const U64x2 p = tp[h];
-        tv[2 * h] = (uint32_t)(p.a >> 32) == (a.rtag0 >> 3) ? (uint32_t)p.a : 0u;
-        tv[2 * h + 1] = (uint32_t)(p.b >> 32) == (a.rtag0 >> 3) ? (uint32_t)p.b : 0u;
-    }
+    for (int s = 0; s < 8; ++s)
+        tv[s] = (tr[s] >> kAckIdxBits) == a.ack_tag && (tr[s] & kAckIdxMask) ? 0xFFFFFFFFu - (kAckIdxMask - (tr[s] & kAckIdxMask)) : 0u;
     const uint8_t need = (uint8_t)(a.g_membership & ~bv0);
     // the first match of senders 0..7 (min T), and of any sender (with F; F is offered only by
     // matches from senders >= 8, or by every match when need is empty)
@@ -942,9 +957,9 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
 //   k_local_deferred  those waiting elements, against the final F.
 // k_commit then installs the shadows. Measured against k_lookup + k_resolve0: the entry line and
 // the op slab are read once instead of twice.
-constexpr int kPreElems = 512;           // elements per k_local_pre block
+constexpr int kPreElems = 1024;          // elements per k_local_pre block
 constexpr int kPreHead = 1024;           // launch head whose PUT keys every block knows
-constexpr int kPreHash = 1024;           // LDS slots of the head's (key -> first PUT) table
+constexpr int kPreHash = 1024;           // LDS slots of a (key -> first PUT) table
 constexpr int kLfElems = 32;             // elements per k_local_fused block (one wave)
 enum { kCtrDefer = 3 };
 enum : uint8_t { kStDefer = 3 };
@@ -953,16 +968,17 @@ enum : uint8_t { kStDefer = 3 };
 // lane), the reference's slot order (first tag match, hermesKV.c:954-975), the log window
 // (:969-970), then each lane's 16 B of the 64-B log line (bytes 16q..16q+15). All four lanes of a
 // group call it with the same arguments.
+template <int P = kLookupPair>
 __device__ __forceinline__ void lookup_pair(const BatchArgs &a, const uint64_t *key, const bool *probe, int q,
                                             int gbase, bool *ok, uint64_t *phys, uint4 *ln)
 {
-    uint4 v[kLookupPair];
+    uint4 v[P];
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k)
+    for (int k = 0; k < P; ++k)
         v[k] = probe[k] ? reinterpret_cast<const uint4 *>(a.index + ((key[k] & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u)[q]
                         : make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         const uint64_t s0 = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
         const uint64_t s1 = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
         const uint32_t tag = (uint32_t)(key[k] >> 48);
@@ -979,7 +995,7 @@ __device__ __forceinline__ void lookup_pair(const BatchArgs &a, const uint64_t *
         phys[k] = off & a.g.log_mask;
     }
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k)
+    for (int k = 0; k < P; ++k)
         ln[k] = ok[k] ? reinterpret_cast<const uint4 *>(a.log + phys[k])[q] : make_uint4(0u, 0u, 0u, 0u);
 }
 
@@ -997,127 +1013,158 @@ __device__ __forceinline__ uint64_t line_key_meta(const uint4 &ln, Meta &m)
     return ek;
 }
 
-// Wave-compacted append of (i, key) to an LDS list
-__device__ __forceinline__ void list_push(bool pred, uint32_t i, uint64_t key, uint32_t *li, uint64_t *lk,
-                                          uint32_t *cnt)
+// element i lies inside its batch's count (launches are under 2^31 elements: 32-bit division,
+// and none at all without counts)
+__device__ __forceinline__ bool in_count(const BatchArgs &a, uint32_t i)
 {
-    const unsigned long long m = __ballot(pred);
-    if (!m) return;
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(cnt, (uint32_t)__popcll(m));
-    base = (uint32_t)__shfl((int)base, leader, 64);
-    if (pred) {
-        const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        li[pos] = i;
-        lk[pos] = key;
-    }
+    if (!a.counts) return true;
+    const uint32_t b = i / (uint32_t)a.stride;
+    return (int32_t)(i - b * (uint32_t)a.stride) < a.counts[b];
 }
 
-__device__ __forceinline__ uint32_t pre_slot(uint64_t key) { return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 54); }
+__device__ __forceinline__ uint32_t pre_slot(uint64_t key) { return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 54) & (kPreHash - 1); }
+
+// (key -> smallest element) in an LDS table of kPreHash slots, key ~0 the empty mark; false when the
+// key cannot go in (key ~0 itself, or a full table)
+__device__ __forceinline__ bool pre_insert(uint64_t *hk, uint32_t *hv, uint64_t key, uint32_t i, bool &created,
+                                           uint32_t &slot)
+{
+    created = false;
+    if (key == ~0ull) return false;
+    uint32_t sl = pre_slot(key);
+    for (int n = 0; n < kPreHash; ++n) {
+        const unsigned long long old = atomicCAS((unsigned long long *)&hk[sl], ~0ull, key);
+        if (old == ~0ull || old == key) {
+            created = old == ~0ull;
+            atomicMin(&hv[sl], i);
+            slot = sl;
+            return true;
+        }
+        sl = (sl + 1) & (kPreHash - 1);
+    }
+    return false;
+}
 
 // The PUTs of kPreElems elements offer F. Whether a PUT mutates S_0 depends on S_0 alone
 // (hermes_exec_write: VALID or INVALID and no op buffer index), so either every PUT of a key is a
-// candidate or none is, and F is the key's first PUT or nothing. A Zipf-hot key's PUTs are spread
-// over every block, and all blocks of the launch are in flight together: every block first reads
-// the keys of the PUTs among the launch's first kPreHead elements (headers only, L2-resident after
-// the first block) and drops its PUTs whose key has a PUT there that comes first -- block 0 offers
-// that one. The rest look their key up and offer through the load-filtered atomicMin.
+// candidate or none is, and F is the key's first PUT or nothing. So each block looks up each key
+// once, for its first PUT (an LDS table of the block's PUT keys). A Zipf-hot key's PUTs are spread
+// over every block, and all blocks of the launch are in flight together: every block also reads the
+// keys of the PUTs among the launch's first kPreHead elements (before its own; headers only,
+// L2-resident after the first block) and drops its keys that have a PUT there -- an earlier block
+// offers that one. Four keys per lane group are in flight; the offer is a plain atomicMin.
+constexpr int kPrePair = 4;
 __global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
 {
-    __shared__ uint32_t li[kPreElems];
-    __shared__ uint64_t lk[kPreElems];
-    __shared__ uint64_t hk[kPreHash];
-    __shared__ uint32_t hv[kPreHash];
-    __shared__ uint32_t nown;
+    __shared__ uint64_t hk[kPreHash], gk[kPreHash];  // the block's PUT keys, the head's
+    __shared__ uint32_t hv[kPreHash], gv[kPreHash];
+    __shared__ uint32_t dl[kPreElems];               // distinct keys: slots of hk, or ~index (no slot)
+    __shared__ uint32_t nd;
     const int tid = threadIdx.x, q = tid & 3, gbase = (tid & 63) & ~3;
     if (tid == 0) {
-        nown = 0;
+        nd = 0;
         if (blockIdx.x == 0) a.ctr[kCtrDefer] = 0;
     }
     for (int j = tid; j < kPreHash; j += 256) {
         hk[j] = ~0ull;
+        gk[j] = ~0ull;
         hv[j] = kNone;
+        gv[j] = kNone;
     }
-    __syncthreads();
+    if (a.dbg & 8) return;
     const int64_t i0 = (int64_t)blockIdx.x * kPreElems;
-    const bool use_head = blockIdx.x > 0;
-    // PUTs that are not skipped (hermes_skip_op, hermesKV.c:709-769): the head's go into the key
-    // table (key ~0 stays out: it is the empty mark), the block's own into the list. Every header
-    // load is issued before the first one is used.
+    const int64_t head_end = (a.dbg & 4) ? 0 : i0 < kPreHead ? i0 : kPreHead;  // the head: elements before the block's own
+    // PUTs that are not skipped (hermes_skip_op, hermesKV.c:709-769). Reading every op header is a
+    // pass over the whole op slab; with the caller's opcode mirror only the PUTs' headers are read
+    // (the others read element 0's, one cached line; k_local_fused checks the mirror against every
+    // element's opcode). Loads are unconditional and all issued before the first is used.
     constexpr int kOwnK = kPreElems / 256, kAllK = kPreElems / 256 + kPreHead / 256;
     U64x2 h[kAllK];
     bool in[kAllK];
+    uint8_t opm[kAllK];
 #pragma unroll
     for (int k = 0; k < kAllK; ++k) {
         const bool own = k < kOwnK;
         const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
-        in[k] = own ? i < a.n : (use_head && i < i0 && i < a.n);  // the head: elements before the block's own
-        if (in[k]) {
-            const int32_t b = (int32_t)(i / a.stride);
-            in[k] = a.counts == nullptr || i - (int64_t)b * a.stride < a.counts[b];
-        }
-        h[k] = in[k] ? *reinterpret_cast<const U64x2 *>(a.elems + i * 56) : U64x2{0, 0};
+        in[k] = i < a.n && (own || i < head_end);
+        opm[k] = a.opc ? a.opc[in[k] ? i : 0] : (uint8_t)kOpPut;
     }
 #pragma unroll
     for (int k = 0; k < kAllK; ++k) {
         const bool own = k < kOwnK;
         const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
+        h[k] = *reinterpret_cast<const U64x2 *>(a.elems + (in[k] && opm[k] == kOpPut ? i : 0) * 56);
+    }
+#pragma unroll
+    for (int k = 0; k < kAllK; ++k) {
+        const bool own = k < kOwnK;
+        const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
+        in[k] = in[k] && in_count(a, (uint32_t)i);
+    }
+    if (a.dbg & 16) {
+        uint64_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < kAllK; ++k) acc += h[k].a ^ h[k].b;
+        if (acc == 0x1234567ull) a.ctr[7] = 1;
+        return;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kAllK; ++k) {
+        const bool own = k < kOwnK;
+        const uint32_t i = (uint32_t)(own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid);
         const uint64_t key = h[k].a;
-        const bool put = in[k] && (uint8_t)h[k].b == kOpPut && !skip_elem_os(kLocal, kOpPut, (uint8_t)(h[k].b >> 8));
+        if (!(in[k] && (uint8_t)h[k].b == kOpPut && !skip_elem_os(kLocal, kOpPut, (uint8_t)(h[k].b >> 8)))) continue;
+        bool created;
+        uint32_t sl;
         if (own) {
-            list_push(put, (uint32_t)i, key, li, lk, &nown);
-        } else if (put && key != ~0ull) {
-            uint32_t sl = pre_slot(key);
-            for (;;) {
-                const unsigned long long old = atomicCAS((unsigned long long *)&hk[sl], ~0ull, key);
-                if (old == ~0ull || old == key) {
-                    atomicMin(&hv[sl], (uint32_t)i);
-                    break;
-                }
-                sl = (sl + 1) & (kPreHash - 1);
+            const bool in_table = pre_insert(hk, hv, key, i, created, sl);
+            if (!in_table || created) {  // a key's first arrival lists it (no slot: it offers for itself)
+                dl[atomicAdd(&nd, 1u)] = in_table ? sl : ~i;
             }
+        } else {
+            pre_insert(gk, gv, key, i, created, sl);
         }
     }
     __syncthreads();
     const Ctx c = make_ctx(a);
     const uint64_t hput[2] = {0, (uint64_t)kOpPut};
-    const uint32_t cnt = nown;
-    for (uint32_t base = 0; base < cnt; base += 64 * kLookupPair) {
-        uint64_t key[kLookupPair];
-        bool probe[kLookupPair], ok[kLookupPair];
-        uint32_t idx[kLookupPair];
-        uint64_t phys[kLookupPair];
-        uint4 ln[kLookupPair];
+    const uint32_t cnt = (a.dbg & 2) ? 0 : nd;
+    for (uint32_t base = 0; base < cnt; base += 64 * kPrePair) {
+        uint64_t key[kPrePair];
+        bool probe[kPrePair], ok[kPrePair];
+        uint32_t idx[kPrePair];
+        uint64_t phys[kPrePair];
+        uint4 ln[kPrePair];
 #pragma unroll
-        for (int k = 0; k < kLookupPair; ++k) {
+        for (int k = 0; k < kPrePair; ++k) {
             const uint32_t j = base + k * 64 + (tid >> 2);
             probe[k] = j < cnt;
-            key[k] = probe[k] ? lk[j] : 0;
-            idx[k] = probe[k] ? li[j] : kNone;
-            if (probe[k] && use_head && key[k] != ~0ull) {  // a head PUT of the same key comes first
+            const uint32_t d = probe[k] ? dl[j] : 0u;
+            idx[k] = !probe[k] ? kNone : d < (uint32_t)kPreHash ? hv[d] : ~d;
+            key[k] = !probe[k] ? 0 : d < (uint32_t)kPreHash ? hk[d] : *reinterpret_cast<const uint64_t *>(a.elems + (int64_t)idx[k] * 56);
+            if (probe[k] && head_end > 0 && key[k] != ~0ull) {  // a head PUT of the key comes first
                 uint32_t sl = pre_slot(key[k]);
-                for (;;) {
-                    const uint64_t hkk = hk[sl];
-                    if (hkk == ~0ull) break;
-                    if (hkk == key[k]) {
-                        probe[k] = hv[sl] > idx[k];
+                for (int n = 0; n < kPreHash; ++n) {
+                    const uint64_t g = gk[sl];
+                    if (g == ~0ull) break;
+                    if (g == key[k]) {
+                        probe[k] = false;
                         break;
                     }
                     sl = (sl + 1) & (kPreHash - 1);
                 }
             }
         }
-        lookup_pair(a, key, probe, q, gbase, ok, phys, ln);
+        lookup_pair<kPrePair>(a, key, probe, q, gbase, ok, phys, ln);
 #pragma unroll
-        for (int k = 0; k < kLookupPair; ++k) {
+        for (int k = 0; k < kPrePair; ++k) {
             Meta m0;
             const uint64_t ek = line_key_meta(ln[k], m0);
             if (q != 0 || !ok[k] || ek != key[k]) continue;
-            if (!would_mutate(kLocal, reinterpret_cast<const uint8_t *>(hput), m0, c)) continue;
-            offer(a.fw + fw_index(a, phys[k]), a.rtag0, idx[k]);
-            if ((uint8_t)(m0.w5 >> 16) != a.ltag) a.log[phys[k] + kEntryMetaOff + 4] = a.ltag;
+            if (!would_mutate(kLocal, reinterpret_cast<const uint8_t *>(hput), m0, c) || (a.dbg & 1)) continue;
+            atomicMin(a.fw + fw_index(a, phys[k]), ((unsigned long long)(~a.rtag0) << 32) | idx[k]);
+            if ((uint8_t)(m0.w5 >> 16) != a.ltag && !(a.dbg & 32)) a.log[phys[k] + kEntryMetaOff + 4] = a.ltag;
         }
     }
 }
@@ -1167,12 +1214,8 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         key[k] = (uint64_t)(uint32_t)__shfl((int)op[k].x, 0, 4) | ((uint64_t)(uint32_t)__shfl((int)op[k].y, 0, 4) << 32);
         const uint32_t h0 = (uint32_t)__shfl((int)op[k].z, 0, 4);
         probe[k] = false;
-        if (live[k]) {
-            const int64_t i = i0 + te[k];
-            const int32_t b = (int32_t)(i / a.stride);
-            const int32_t idx = (int32_t)(i - (int64_t)b * a.stride);
-            probe[k] = (a.counts == nullptr || idx < a.counts[b]) && !skip_elem_os(kLocal, (uint8_t)h0, (uint8_t)(h0 >> 8));
-        }
+        if (live[k])
+            probe[k] = in_count(a, (uint32_t)(i0 + te[k])) && !skip_elem_os(kLocal, (uint8_t)h0, (uint8_t)(h0 >> 8));
     }
     lookup_pair(a, key, probe, q, gbase, ok, phys, ln);
     // F of a key tagged by k_local_pre, loaded for both elements before either is resolved
@@ -1199,7 +1242,7 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         uint8_t st = kStDone;
         if (e != kNone) {
             Ctx c = make_ctx(a);
-            const uint8_t bidx = (uint8_t)(i - (i / a.stride) * a.stride);
+            const uint8_t bidx = (uint8_t)((uint32_t)i % (uint32_t)a.stride);
             Meta m;
             meta_load(ent, m);
             const bool wm = would_mutate(kLocal, x, m, c);
@@ -1230,6 +1273,8 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         } else if (sprb[tid]) {
             x[9] = kMiss;
         }
+        // k_local_pre read only the PUTs the caller's opcode mirror names
+        if (a.opc && sprb[tid] && x[8] == kOpPut && a.opc[i] != kOpPut && a.error_flags) atomicOr(a.error_flags, 8u);
         a.ent[i] = e;
         a.st[i] = st;
         if (st != kStDefer) note_state(a, i, x);
@@ -1923,6 +1968,10 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.counts = bl.counts;
     a.offsets = bl.offsets;
     a.state_out = (bl.type == kLocal || bl.type == kLocalAfterMemb) ? bl.state_out : nullptr;
+    a.opc = bl.type == kLocal ? bl.opcode_in : nullptr;
+    static const int dbg_env = getenv("HKV_DBG") ? atoi(getenv("HKV_DBG")) : 0;
+    a.dbg = dbg_env;
+    if (dbg_env) a.error_flags = nullptr;
     a.index = bl.index;
     a.log = bl.log;
     a.rw = bl.rw;
@@ -1950,7 +1999,8 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.fy = bl.fy;
     a.inv_direct = bl.type == kInvs && !bl.g.rmw_enabled && n < kInvDirectMax;
     a.ft = bl.ft;
-    a.ack_direct = bl.type == kAcks && !bl.g.rmw_enabled && n < (int64_t)kNone;
+    a.ack_direct = bl.type == kAcks && !bl.g.rmw_enabled && n < (int64_t)kAckIdxMask;
+    a.ack_tag = 0;
     a.g_membership = bl.g_membership;
     a.w_ack_init = bl.w_ack_init;
     a.node_suspected = bl.node_suspected;
@@ -1980,13 +2030,19 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     static const int ld_env = getenv("HKV_LOCAL_DIRECT") ? atoi(getenv("HKV_LOCAL_DIRECT")) : 1;
     const bool local_direct = ld_env != 0 && bl.type == kLocal && !bl.g.rmw_enabled && bl.esz == 56 &&
                               bl.g.st_value == 31 && bl.g.entry_size == 64 && !bl.offsets;
+    if (a.ack_direct && !small) {  // this launch's tag, and the T slice of that tag zeroed first
+        const uint32_t tag = ++*bl.ack_seq % kAckTags;
+        a.ack_tag = tag;
+        const size_t slice = bl.ft_words / kAckTags;
+        if (hipMemsetAsync(bl.ft + (size_t)tag * slice, 0, slice * 4, s) != hipSuccess) return -3;
+    }
     if (small) {
         if (launch_small(a, s)) return -3;
         return 0;                              // node_suspected written by the kernel
     } else if (local_direct) {
         hipLaunchKernelGGL(k_local_pre, dim3((unsigned)((n + kPreElems - 1) / kPreElems)), dim3(256), 0, s, a);
         hipLaunchKernelGGL(k_local_fused, dim3((unsigned)((n + kLfElems - 1) / kLfElems)), dim3(64), 0, s, a);
-        hipLaunchKernelGGL(k_local_deferred, dim3(64), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_local_deferred, dim3(8), dim3(256), 0, s, a);
         hipLaunchKernelGGL((k_commit<31>), dim3(grid), dim3(256), 0, s, a);
     } else if (bl.type == kVals) {             // one pass (see k_lookup)
         hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, n);

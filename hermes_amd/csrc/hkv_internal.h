@@ -16,6 +16,7 @@ struct BatchLaunch {
     const int32_t *counts;
     const int32_t *offsets;      // packed INV/VAL launches: n_batches + 1 batch offsets (counts NULL)
     uint8_t *state_out;          // local launches: each element's final state byte (may be NULL)
+    const uint8_t *opcode_in;    // local launches: the caller's mirror of each element's opcode (may be NULL)
     const uint8_t *index;
     uint8_t *log;
     uint8_t *rw;
@@ -26,7 +27,9 @@ struct BatchLaunch {
     // allocated) and per-launch scratch carved by batch_carve
     unsigned long long *fw;
     unsigned long long *fx, *fy;              // INV words per log line (zero between launches)
-    unsigned long long *ft;                   // ACK words, eight per log line (tagged with the epoch)
+    uint32_t *ft;                             // ACK words, eight per log line (tagged, see hkv_batch.hip)
+    size_t ft_words;                          // u32 words of ft
+    uint32_t *ack_seq;                        // the table's count of direct-path ACK launches
     unsigned long long *mem;
     uint32_t *ent, *fbl, *pf, *ctr;
     uint8_t *st, *shadow;

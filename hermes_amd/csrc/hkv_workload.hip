@@ -164,7 +164,8 @@ __global__ __launch_bounds__(256) void k_fold_counters(unsigned long long *count
 __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, uint32_t op_size, uint32_t st_value,
                                                 uint32_t shift, const uint64_t *tkey, const uint8_t *top,
                                                 int32_t tlen, uint32_t *cursor, uint32_t machine_id,
-                                                int32_t first_iter, int32_t refill_all, unsigned long long *counters)
+                                                int32_t first_iter, int32_t refill_all, unsigned long long *counters,
+                                                uint8_t *opc_out)
 {
     extern __shared__ uint64_t slab[];
     const int w = blockIdx.x, i = threadIdx.x;
@@ -218,6 +219,7 @@ __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, ui
             for (uint32_t k = 0; k < st_value; ++k) op[kOpValueOff + k] = v;
         }
     }
+    if (opc_out && live) opc_out[(int64_t)w * stride + i] = op[8];  // the opcode mirror
     __syncthreads();
     if (wide) {
         uint4 *g4 = reinterpret_cast<uint4 *>(gslab);
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(256) void k_refill_direct(uint8_t *ops, int32_t str
                                                        uint32_t st_value, uint32_t shift, const uint64_t *tkey,
                                                        const uint8_t *top, int32_t tlen, uint32_t *cursor,
                                                        uint32_t machine_id, int32_t first_iter, int32_t refill_all,
-                                                       unsigned long long *counters)
+                                                       unsigned long long *counters, uint8_t *opc_out)
 {
     const int w = blockIdx.x, i = threadIdx.x;
     const bool live = i < stride;
@@ -272,6 +274,7 @@ __global__ __launch_bounds__(256) void k_refill_direct(uint8_t *ops, int32_t str
         *h1 = (*h1 & ~0xFFFFFFull) | oc | ((uint64_t)kNew << 8) | (vl << 16);
         if (oc == kOpGet) *reinterpret_cast<uint16_t *>(op + 16) = flags;
     }
+    if (opc_out && live) opc_out[(int64_t)w * stride + i] = done ? oc : op[8];  // the opcode mirror
     // the values of the writes, one op at a time per wave: lane k stores 8-B word k of bytes
     // 16 .. 18 + st_value (word 0 carries the flags), the tail bytes go to the lanes after them
     const uint64_t vv = 0x0101010101010101ull * (uint8_t)('a' + machine_id);
@@ -1108,12 +1111,14 @@ int hkv_wl_gen_trace(uint64_t *tkey, uint8_t *top, uint32_t *tid, int32_t n_work
 
 int hkv_wl_refill(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint32_t st_value, uint32_t shift,
                   const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor, uint32_t machine_id,
-                  int32_t first_iter, int32_t refill_all, unsigned long long *counters, void *stream)
+                  int32_t first_iter, int32_t refill_all, unsigned long long *counters, uint8_t *opc_out,
+                  void *stream)
 {
     if (stride > 256 || n_workers <= 0 || op_size % 8) return -1;
     if (op_size > 64 && st_value >= 6 && (kOpValueOff - 16 + st_value) / 8 + 7 <= 64) {  // big ops: in place
         hipLaunchKernelGGL(k_refill_direct, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
-                           st_value, shift, tkey, top, tlen, cursor, machine_id, first_iter, refill_all, counters);
+                           st_value, shift, tkey, top, tlen, cursor, machine_id, first_iter, refill_all, counters,
+                           opc_out);
         return ok();
     }
     const size_t lds = (size_t)stride * op_size;
@@ -1122,7 +1127,7 @@ int hkv_wl_refill(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_s
         hipFuncSetAttribute((const void *)k_refill, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return -1;
     hipLaunchKernelGGL(k_refill, dim3(n_workers), dim3(256), lds, (hipStream_t)stream, ops, stride, op_size, st_value,
-                       shift, tkey, top, tlen, cursor, machine_id, first_iter, refill_all, counters);
+                       shift, tkey, top, tlen, cursor, machine_id, first_iter, refill_all, counters, opc_out);
     return ok();
 }
 

@@ -154,7 +154,7 @@ class HermesKV:
               membership: bytes, counts: torch.Tensor | None = None, rw: torch.Tensor | None = None,
               rw_stride_bytes: int = 0, node_suspected: torch.Tensor | None = None,
               stream: torch.cuda.Stream | None = None, offsets: torch.Tensor | None = None,
-              state_out: torch.Tensor | None = None) -> None:
+              state_out: torch.Tensor | None = None, opcode_in: torch.Tensor | None = None) -> None:
         """Apply n_batches batches of one type, concatenated in `elems` (uint8, on the GPU),
         in concatenation order, asynchronously on `stream` (default: torch's current).
         offsets (INV / ACK / VAL batches): the batches stored back to back, batch b at elements
@@ -172,6 +172,9 @@ class HermesKV:
         if state_out is not None:   # local batches: the mirror of each element's final state byte
             assert state_out.is_cuda and state_out.dtype == torch.uint8 and state_out.numel() >= n_batches * stride
             d.d_state_out = state_out.data_ptr()
+        if opcode_in is not None:   # local batches: the caller's mirror of each element's opcode byte
+            assert opcode_in.is_cuda and opcode_in.dtype == torch.uint8 and opcode_in.numel() >= n_batches * stride
+            d.d_opcode_in = opcode_in.data_ptr()
         if offsets is not None:
             assert counts is None and offsets.is_cuda and offsets.dtype == torch.int32
             assert offsets.numel() >= n_batches + 1

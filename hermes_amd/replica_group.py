@@ -81,6 +81,7 @@ class ReplicaRound:
         i32 = dict(dtype=torch.int32, device=dev)
         self.ops = torch.zeros(W * LOCAL * self.op, **u8)
         self.states = torch.zeros(W * LOCAL, dtype=torch.uint8, device=dev)  # local batch state mirror
+        self.opcodes = torch.zeros(W * LOCAL, dtype=torch.uint8, device=dev)  # the refill's opcode mirror
         # outgoing INVs: [W][C] rows, then packed (worker w at inv_off[w]; inv_off[W] = total)
         self.inv_slab = torch.zeros(W * C * self.op, **u8)
         self.inv_count = torch.zeros(W, **i32)
@@ -139,7 +140,8 @@ class ReplicaRound:
             return
         check(_L.hkv_wl_refill(_ptr(self.ops), self.W, LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
                                _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
-                               self.rank, int(first), int(not self.retry), _ptr(self.counters), _s()), "refill")
+                               self.rank, int(first), int(not self.retry), _ptr(self.counters), _ptr(self.opcodes),
+                               _s()), "refill")
 
     def local(self):
         """Local batch, then this round's INVs, packed (inv_pack; worker w at inv_off[w])."""
@@ -148,7 +150,8 @@ class ReplicaRound:
             self.inv_off.zero_()
             self.inv_maxc.zero_()
             return
-        self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, LOCAL, self.op, self.mb, state_out=self.states)
+        self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, LOCAL, self.op, self.mb, state_out=self.states,
+                       opcode_in=self.opcodes)
         check(_L.hkv_wl_marshal_invs_cap(_ptr(self.ops), self.W, LOCAL, self.op, _ptr(self.inv_slab), self.C,
                                          _ptr(self.inv_count), self.rank, _ptr(self.held), _ptr(self.states), _s()),
               "marshal_invs")

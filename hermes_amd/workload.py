@@ -32,7 +32,7 @@ class HkvZipf(ctypes.Structure):
 _L.hkv_wl_gen_trace.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(HkvZipf),
                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, _P]
 _L.hkv_wl_refill.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
-                             _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, _P, _P]
+                             _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P]
 _L.hkv_wl_fold_counters.argtypes = [_P, _P]
 _L.hkv_wl_marshal_invs.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_invs_cap.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
@@ -130,6 +130,7 @@ class Round:
         u8 = dict(dtype=torch.uint8, device=dev)
         self.ops = torch.zeros(W * S * self.op, **u8)
         self.states = torch.zeros(W * S, **u8)   # the local batch's mirror of every op's state byte
+        self.opcodes = torch.zeros(W * S, **u8)  # the refill's mirror of every op's opcode byte
         self.C = slots_per_worker(write_permille, rmw_permille)   # INV send credits per worker
         self.inv_out = torch.zeros(W * self.C * self.op, **u8)
         self.inv_count = torch.zeros(W, dtype=torch.int32, device=dev)
@@ -201,6 +202,14 @@ class Round:
         if hades:
             self._hades_start()
         self._gen_remote()
+        # the virtual peers take their timestamps on a side stream, beside the refill (which touches
+        # only the op slab): from the table as the previous round left it (tbl_ready, recorded
+        # before each refill) to the local batch, which waits for them (HKV_PEER_OVERLAP=0: in line)
+        self.overlap = os.environ.get("HKV_PEER_OVERLAP", "1") != "0" and self.pack_remote
+        if self.overlap:
+            self.side = torch.cuda.Stream(device=dev)
+            self.tbl_ready, self.pts_done = torch.cuda.Event(), torch.cuda.Event()
+            self.tbl_ready.record()
         self.refill(first=True)
 
     def _gen_remote(self):
@@ -246,11 +255,13 @@ class Round:
     def refill(self, first: bool = False):
         check(_L.hkv_wl_refill(_ptr(self.ops), self.W, self.LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
                                _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
-                               self.machine_id, int(first), int(not self.retry), _ptr(self.counters), _s()),
+                               self.machine_id, int(first), int(not self.retry), _ptr(self.counters),
+                               _ptr(self.opcodes), _s()),
               "refill")
 
     def local_batch(self):
-        self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb, state_out=self.states)
+        self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb, state_out=self.states,
+                       opcode_in=self.opcodes)
 
     def marshal_invs(self):
         if self.V is not None:
@@ -362,7 +373,13 @@ class Round:
         # every peer live and none failing this round: the packed slabs (same elements, same order)
         packed = self.pack_remote and sent == self.R and alive == self.R
         if self.R and sent:
-            if packed:
+            if packed and self.overlap:
+                self.side.wait_event(self.tbl_ready)
+                with torch.cuda.stream(self.side):
+                    self.peer_timestamps_packed(k)
+                self.pts_done.record(self.side)
+                torch.cuda.current_stream().wait_event(self.pts_done)
+            elif packed:
                 self.peer_timestamps_packed(k)
             else:
                 self.peer_timestamps(k, sent)
@@ -429,6 +446,8 @@ class Round:
             self._hades_period()
         elif drop is not None:
             self.membership_change(drop)
+        if self.overlap:
+            self.tbl_ready.record()
         self.refill()
         self.clock += 1
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HKV_ABI_VERSION 2
+#define HKV_ABI_VERSION 3
 
 /* ------------------------------------------------------------------ reference types
  * Declared here only when the reference's own spacetime.h has not been included; the
@@ -119,6 +119,11 @@ typedef struct hkv_batch_desc {
     uint8_t *d_state_out;       /* device, local batches: receives each element's final state byte
                                    (op byte 9; n_batches * stride bytes), a mirror the worker loop's
                                    next passes can read instead of the ops; NULL = none (ABI 2) */
+    const uint8_t *d_opcode_in; /* device, local batches: the caller's mirror of each element's opcode
+                                   (op byte 8; n_batches * stride bytes), e.g. written by its refill
+                                   (hkv_wl_refill); lets the launch find its PUTs without reading
+                                   every op. A PUT the mirror misses raises error flag bit 3.
+                                   NULL = read the ops (ABI 3) */
 } hkv_batch_desc;
 
 /* hkv_batch_desc.flags. By default launches of at most 4096 elements run as one single-workgroup
@@ -153,7 +158,10 @@ uint64_t hkv_log_head(const hkv_table *t);
 int64_t  hkv_num_index_evictions(const hkv_table *t);
 void *hkv_device_index(hkv_table *t);
 /* internal-consistency flags raised by the device path since the last call (0 = none);
- * bit 0: the hot-key engine saw a non-candidate element change the entry meta */
+ * bit 0: an element resolved in parallel (not a key's first mutating element) changed the meta;
+ * bit 1: the ACK direct path completed a write from an unexpected state;
+ * bit 2: a local launch's mutating element had not offered itself in its prepass;
+ * bit 3: d_opcode_in missed a PUT (the mirror disagrees with the op) */
 int  hkv_take_error_flags(hkv_table *t, uint32_t *out);
 void *hkv_device_log(hkv_table *t);
 

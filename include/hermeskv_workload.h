@@ -56,13 +56,14 @@ int hkv_wl_gen_trace(uint64_t *d_trace_key, uint8_t *d_trace_op, uint32_t *d_tra
  * d_counters: HKV_WL_COUNTER_WORDS words, zeroed by the caller once, of which the words from
  * HKV_WL_STRIPE_BASE on are per-worker-group partial sums (one counter address hit by every
  * worker serialises in L2); hkv_wl_fold_counters adds them into d_counters[0..4] when the
- * caller reads the totals. */
+ * caller reads the totals. d_opcode_out (NULL = none): every op's opcode byte after the refill,
+ * the mirror hkv_batch_desc.d_opcode_in takes. */
 #define HKV_WL_COUNTER_WORDS 4096
 #define HKV_WL_STRIPE_BASE 64
 int hkv_wl_refill(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint32_t st_value,
                   uint32_t shift, const uint64_t *d_trace_key, const uint8_t *d_trace_op, int32_t trace_len,
                   uint32_t *d_cursor, uint32_t machine_id, int32_t first_iter, int32_t refill_all,
-                  unsigned long long *d_counters, void *stream);
+                  unsigned long long *d_counters, uint8_t *d_opcode_out, void *stream);
 /* d_counters[0..4] += the refill stripes (which are cleared) */
 int hkv_wl_fold_counters(unsigned long long *d_counters, void *stream);
 

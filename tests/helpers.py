@@ -94,7 +94,7 @@ class Mirror:
             self.codes[(int(btype), tag, x)] += c
 
     def batch(self, btype, elems, n_batches, stride, elem_size, membership, counts=None, rw=None,
-              rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None, state_out=None):
+              rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None, state_out=None, opcode_in=None):
         import torch
         if offsets is not None:
             return self._packed(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
@@ -104,12 +104,15 @@ class Mirror:
         vt = np.dtype((np.void, elem_size))
         e_in = elems[:n].cpu().numpy().copy().view(vt)
         c_in = counts[:n_batches].cpu().numpy().copy() if counts is not None else None
+        if opcode_in is not None:   # the caller's opcode mirror must be every element's opcode byte
+            assert np.array_equal(opcode_in[: n_batches * stride].cpu().numpy(),
+                                  np.frombuffer(e_in.tobytes(), np.uint8).reshape(-1, elem_size)[:, 8])
         self._count(btype, "in8", 8, np.frombuffer(e_in.tobytes(), np.uint8), n_batches, stride, elem_size, c_in)
         rw_in = rw_op = None
         if rw is not None:
             rw_in = rw.cpu().numpy().copy().view(np.dtype((np.void, self.g.sizes.op)))
         self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
-                   node_suspected, stream, state_out=state_out)
+                   node_suspected, stream, state_out=state_out, opcode_in=opcode_in)
         torch.cuda.synchronize()
         self.o.batch_multi(int(btype), e_in, n_batches, stride, c_in, membership, rw_in,
                            rw_stride_bytes // self.g.sizes.op if rw is not None else 0)

@@ -520,3 +520,36 @@ def test_scripted_rare_outcomes(cfg):
     seen = run_scripted(runner, gen_keys(1000), sizes, rmw)
     missing = required_outcomes(rmw) - seen
     assert not missing, f"not produced: {sorted(missing, key=str)}"
+
+
+def test_local_opcode_mirror(engine_path):
+    """hkv_batch_desc.d_opcode_in: with a correct mirror the local launch gives the same bytes as
+    without one (k_local_pre then reads only the PUTs' headers); a mirror that hides a PUT is
+    reported as error flag bit 3."""
+    if engine_path != "engine":
+        pytest.skip("the mirror is read by the multi-kernel engine's direct local path")
+    rng = np.random.default_rng(31)
+    g, o, sizes = make_pair(3000, 512, 1 << 18)
+    keys = gen_keys(3000)
+    tsp = gen.TsPool(rng)
+    W, S = 40, 200   # 8000 elements: several prepass blocks, so the launch-head filter runs too
+    mb = L.membership(3, 0)
+    for rnd in range(3):
+        pool = gen.key_pool(rng, keys, hot=24 if rnd % 2 else 400)
+        loc = gen.local_ops(rng, pool, W * S, sizes, False, tsp)
+        loc_o = gen.bytecopy(loc)
+        d = torch.from_numpy(loc.view(np.uint8).copy()).cuda()
+        opc = torch.from_numpy(loc["opcode"].astype(np.uint8).copy()).cuda()
+        g.batch(L.BatchType.local_ops, d, W, S, sizes.op, mb, opcode_in=opc)
+        torch.cuda.synchronize()
+        o.batch_multi(L.BatchType.local_ops, loc_o, W, S, None, mb)
+        got = d.cpu().numpy()
+        assert np.array_equal(got, loc_o.view(np.uint8).reshape(-1)), f"round {rnd}: elements differ"
+        assert_tables_equal(g, o, f"round {rnd}")
+        assert g.take_error_flags() == 0
+    # hide every PUT from the mirror: the launch reports it
+    loc = gen.local_ops(rng, gen.key_pool(rng, keys, hot=400), W * S, sizes, False, tsp)
+    d = torch.from_numpy(loc.view(np.uint8).copy()).cuda()
+    opc = torch.full((W * S,), int(L.Op.GET), dtype=torch.uint8, device="cuda")
+    g.batch(L.BatchType.local_ops, d, W, S, sizes.op, mb, opcode_in=opc)
+    assert g.take_error_flags() & 8

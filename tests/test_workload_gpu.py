@@ -344,8 +344,10 @@ def test_refill_kernel_matches_numpy(big, refill_all):
     d_tkey, d_top = torch.from_numpy(tkey).cuda(), torch.from_numpy(top).cuda()
     d_cur = torch.from_numpy(cursor.copy()).cuda()
     d_cnt = torch.zeros(4096, dtype=torch.int64, device="cuda")
+    d_opc = torch.zeros(W * S, dtype=torch.uint8, device="cuda")
     WL.check(WL._L.hkv_wl_refill(WL._ptr(d_ops), W, S, osz, sz.st_value, sz.shift, WL._ptr(d_tkey), WL._ptr(d_top),
-                                 tlen, WL._ptr(d_cur), mid, 0, refill_all, WL._ptr(d_cnt), None), "refill")
+                                 tlen, WL._ptr(d_cur), mid, 0, refill_all, WL._ptr(d_cnt), WL._ptr(d_opc), None),
+             "refill")
     WL.check(WL._L.hkv_wl_fold_counters(WL._ptr(d_cnt), None), "fold")
     torch.cuda.synchronize()
     got = d_ops.cpu().numpy()
@@ -354,6 +356,8 @@ def test_refill_kernel_matches_numpy(big, refill_all):
         pytest.fail(f"slab differs at {len(bad)} bytes: ops {np.unique(bad // osz)[:8]}, offsets {np.unique(bad % osz)[:16]}")
     assert np.array_equal(d_cur.cpu().numpy(), exp_cur)
     assert d_cnt[:5].cpu().tolist() == exp_cnt.tolist()
+    # the opcode mirror (hkv_batch_desc.d_opcode_in) is every op's opcode byte after the refill
+    assert np.array_equal(d_opc.cpu().numpy(), exp_ops.reshape(W * S, osz)[:, 8])
 
 
 @pytest.mark.parametrize("big", [False, True])

@@ -291,7 +291,8 @@ def main():
             "elements_per_step": {"inv": n_inv, "ack": n_ack, "val": n_val},
         },
         "roofline": {
-            "bound": "hbm", "kernel": f"{dom} batch launch (k_lookup + element-order rounds, hkv_batch.hip)",
+            "bound": "hbm", "kernel": (f"{dom} batch launch (" + ("k_local_pre + k_local_fused + k_commit, the direct path" if dom == "local"
+                                                  and not cfg3 else "k_lookup + element-order rounds") + ", hkv_batch.hip)"),
             "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
             "traffic": traffic, "traffic_source": traffic_src, "launch_ms": ms.get(dom),
             "launch_samples": len(events.get(dom, [])),

@@ -164,6 +164,11 @@ class Round:
         self.ack_off = torch.zeros(W + 1, dtype=torch.int32, device=dev) if self.fit else None
         self.ack_total = 0
         self.maxc_ev = torch.cuda.Event() if self.fit else None
+        # HKV_ACKOFF_SIDE=1: the one-workgroup ACK-offsets scan runs on a side stream beside the INV batch
+        self.ackoff_side = self.fit and self.ack_spin and os.environ.get("HKV_ACKOFF_SIDE", "0") == "1"
+        if self.ackoff_side:
+            self.side2 = torch.cuda.Stream(device=dev)
+            self.ao_start, self.ao_done = torch.cuda.Event(), torch.cuda.Event()
         self.acks = torch.zeros(W * self.ack_stride * self.ack_size, **u8)
         self.ack_count = torch.zeros(W, dtype=torch.int32, device=dev)
         self.val_out = torch.zeros(W * self.ack_stride * L.OP_META_SIZE, **u8)
@@ -390,8 +395,16 @@ class Round:
             self.inv_total += self.inv_count.sum()
         if self.fit and alive:
             self._ack_seq = self._ack_seq % 0x7FFFFFFF + 1 if self.ack_spin else 0
-            check(_L.hkv_wl_ack_offsets(_ptr(self.inv_count), self.W, alive, _ptr(self.ack_off), _ptr(self.maxc_h),
-                                        self._ack_seq, _s()), "ack_offsets")
+            if self.ackoff_side:   # one workgroup: beside the INV batch, which does not need it
+                self.ao_start.record()
+                self.side2.wait_event(self.ao_start)
+                with torch.cuda.stream(self.side2):
+                    check(_L.hkv_wl_ack_offsets(_ptr(self.inv_count), self.W, alive, _ptr(self.ack_off),
+                                                _ptr(self.maxc_h), self._ack_seq, _s()), "ack_offsets")
+                self.ao_done.record(self.side2)
+            else:
+                check(_L.hkv_wl_ack_offsets(_ptr(self.inv_count), self.W, alive, _ptr(self.ack_off),
+                                            _ptr(self.maxc_h), self._ack_seq, _s()), "ack_offsets")
             if not self.ack_spin:
                 self.maxc_ev.record()
         if self.R:
@@ -416,6 +429,8 @@ class Round:
                                 raise RuntimeError("ACK layout flag never arrived")
                 else:
                     self.maxc_ev.synchronize()
+                if self.ackoff_side:
+                    torch.cuda.current_stream().wait_event(self.ao_done)
                 self.ack_total = int(self.maxc_h[0])
                 m = min(int(self.maxc_h[1]), self.C)
             if alive and self.V is not None:

@@ -60,7 +60,7 @@ struct BatchArgs {
     int32_t *ns_idx;
     unsigned long long *fw;      // [log_cap / 64] F word per 64-B log line (table-wide), see fw_index
     unsigned long long *fx, *fy; // [log_cap / 64] INV words X, Y (INV direct path; zero between launches)
-    uint32_t *ft;                // [log_cap / 64][8] ACK words T (ACK direct path; tag << 21 | ~i)
+    unsigned long long *ft;      // [log_cap / 64][8] ACK words T (ACK direct path; epoch << 32 | ~i)
     uint32_t fw_mask;
     uint32_t *ent;               // [n] entry id of every element (kNone: skipped or missing)
     uint8_t *st;                 // [n] stage (kSt*)
@@ -81,7 +81,6 @@ struct BatchArgs {
     int32_t rounds;              // rounds after round 0 before the fallback
     int32_t inv_direct;          // INV launch on the direct path (k_inv_resolve)
     int32_t ack_direct;          // ACK launch on the direct path (k_ack_resolve)
-    uint32_t ack_tag;            // its T words' tag
     uint8_t g_membership;
     uint8_t w_ack_init;
     int32_t *node_suspected;     // small launches write it themselves
@@ -158,15 +157,12 @@ constexpr int64_t kInvDirectMax = 1 << 23;
 // completion). Opcodes: ACK_SUCCESS (a LAST_ACK_SUCCESS input stays, except at j*),
 // LAST_ACK_SUCCESS for j* from WRITE or REPLAY. k_lookup finishes the non-matching elements, sets T (as max of ~i) and F
 // and caches each matching element's ack_bv / state / op buffer index in pf; in k_ack_resolve
-// j* (or, without a completion, F) applies the key's meta. T words are u32: an 11-bit tag (the
-// table's direct-path ACK launch count mod 2048) over 21 bits of (2^21 - 1 - element), so a word
-// of an earlier launch reads as empty. Nothing clears the words a launch sets; instead every such
-// launch first zeroes 1/2048 of the T array (the slice of its tag), so each word is zeroed at least
-// once between two launches with the same tag. Launches of 2^21 - 1 elements or more take the rounds
-// engine.
+// j* (or, without a completion, F) applies the key's meta. T words carry the launch's epoch in
+// their upper half, so a word of an earlier launch reads as empty and nothing is cleared (the
+// epoch only wraps after 2^29 launches, when the runtime zeroes T with the F words' reset).
+// Measured against u32 words with an 11-bit tag and a 1/2048 slice of T zeroed by every ACK
+// launch: the slice memset is a kernel of its own (4.6 us), as long as the clear pass it replaced.
 enum : uint8_t { kAkMatch = 1 };
-constexpr int kAckIdxBits = 21, kAckTags = 2048;
-constexpr uint32_t kAckIdxMask = (1u << kAckIdxBits) - 1;
 
 __device__ __forceinline__ uint8_t ack_opcode(uint8_t in) { return in == kLastAckSuccess ? in : kAckSuccess; }
 
@@ -485,17 +481,10 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                     // quorum is complete already (the first match then completes)
                     if (snd >= 8 || (uint8_t)(a.g_membership & ~m_ack_bv(m0[k])) == 0)
                         offer(a.fw + w, a.rtag0, (uint32_t)gi[k]);
-                    if (snd < 8) {  // tagged with the launch (see kAckTagBits)
-                        // tags wrap, so a stale word may compare larger: replace it by CAS, keep the
-                        // smallest element of this launch's tag
-                        uint32_t *t = a.ft + (size_t)w * 8 + snd;
-                        const uint32_t tv = (a.ack_tag << kAckIdxBits) | (kAckIdxMask - (uint32_t)gi[k]);
-                        uint32_t old = __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        while ((old >> kAckIdxBits) != a.ack_tag || old < tv) {
-                            const uint32_t seen = atomicCAS(t, old, tv);
-                            if (seen == old) break;
-                            old = seen;
-                        }
+                    if (snd < 8) {  // tagged with the launch: no clearing between launches
+                        unsigned long long *t = a.ft + (size_t)w * 8 + snd;
+                        const unsigned long long tv = ((unsigned long long)(a.rtag0 >> 3) << 32) | (0xFFFFFFFFu - (uint32_t)gi[k]);
+                        if (tv > __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(t, tv);
                     }
                     a.pf[gi[k]] = (uint32_t)m_ack_bv(m0[k]) | ((uint32_t)m_state(m0[k]) << 8) | ((uint32_t)m_obi(m0[k]) << 16);
                 }
@@ -690,13 +679,14 @@ __global__ __launch_bounds__(256) void k_ack_resolve(BatchArgs a)
     const uint32_t w = fw_index(a, phys_of(a, e));
     const uint32_t c0 = a.pf[i];
     const uint8_t bv0 = (uint8_t)c0, st0 = (uint8_t)(c0 >> 8), obi0 = (uint8_t)(c0 >> 16);
-    const uint4 *tp = reinterpret_cast<const uint4 *>(a.ft + (size_t)w * 8);
-    const uint4 t0 = tp[0], t1 = tp[1];
-    const uint32_t tr[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+    const U64x2 *tp = reinterpret_cast<const U64x2 *>(a.ft + (size_t)w * 8);
     uint32_t tv[8];  // 0xFFFFFFFF - (first match of the sender), 0: none in this launch
 #pragma unroll
-    for (int s = 0; s < 8; ++s)
-        tv[s] = (tr[s] >> kAckIdxBits) == a.ack_tag && (tr[s] & kAckIdxMask) ? 0xFFFFFFFFu - (kAckIdxMask - (tr[s] & kAckIdxMask)) : 0u;
+    for (int h = 0; h < 4; ++h) {
+        const U64x2 p = tp[h];
+        tv[2 * h] = (uint32_t)(p.a >> 32) == (a.rtag0 >> 3) ? (uint32_t)p.a : 0u;
+        tv[2 * h + 1] = (uint32_t)(p.b >> 32) == (a.rtag0 >> 3) ? (uint32_t)p.b : 0u;
+    }
     const uint8_t need = (uint8_t)(a.g_membership & ~bv0);
     // the first match of senders 0..7 (min T), and of any sender (with F; F is offered only by
     // matches from senders >= 8, or by every match when need is empty)
@@ -1999,8 +1989,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.fy = bl.fy;
     a.inv_direct = bl.type == kInvs && !bl.g.rmw_enabled && n < kInvDirectMax;
     a.ft = bl.ft;
-    a.ack_direct = bl.type == kAcks && !bl.g.rmw_enabled && n < (int64_t)kAckIdxMask;
-    a.ack_tag = 0;
+    a.ack_direct = bl.type == kAcks && !bl.g.rmw_enabled && n < (int64_t)kNone;
     a.g_membership = bl.g_membership;
     a.w_ack_init = bl.w_ack_init;
     a.node_suspected = bl.node_suspected;
@@ -2030,12 +2019,6 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     static const int ld_env = getenv("HKV_LOCAL_DIRECT") ? atoi(getenv("HKV_LOCAL_DIRECT")) : 1;
     const bool local_direct = ld_env != 0 && bl.type == kLocal && !bl.g.rmw_enabled && bl.esz == 56 &&
                               bl.g.st_value == 31 && bl.g.entry_size == 64 && !bl.offsets;
-    if (a.ack_direct && !small) {  // this launch's tag, and the T slice of that tag zeroed first
-        const uint32_t tag = ++*bl.ack_seq % kAckTags;
-        a.ack_tag = tag;
-        const size_t slice = bl.ft_words / kAckTags;
-        if (hipMemsetAsync(bl.ft + (size_t)tag * slice, 0, slice * 4, s) != hipSuccess) return -3;
-    }
     if (small) {
         if (launch_small(a, s)) return -3;
         return 0;                              // node_suspected written by the kernel

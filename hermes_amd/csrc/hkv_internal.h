@@ -27,9 +27,7 @@ struct BatchLaunch {
     // allocated) and per-launch scratch carved by batch_carve
     unsigned long long *fw;
     unsigned long long *fx, *fy;              // INV words per log line (zero between launches)
-    uint32_t *ft;                             // ACK words, eight per log line (tagged, see hkv_batch.hip)
-    size_t ft_words;                          // u32 words of ft
-    uint32_t *ack_seq;                        // the table's count of direct-path ACK launches
+    unsigned long long *ft;                   // ACK words, eight per log line (tagged with the epoch)
     unsigned long long *mem;
     uint32_t *ent, *fbl, *pf, *ctr;
     uint8_t *st, *shadow;

@@ -67,11 +67,21 @@ def parse():
                    help="N=1: VAL messages per worker and round (the VAL credits; 225 = the reference's 15 "
                         "credits x 15 coalesced messages); workers with VALs outstanding do not poll ACKs. "
                         "Default: credits that never bind (every ACK applied and every VAL sent each round)")
-    p.add_argument("--retry", action="store_true",
-                   help="refill_ops semantics: stalled ops keep their slot (default: fresh batch per step)")
-    p.add_argument("--retry-steps", type=int, default=10,
-                   help="N=1, default (fresh) policy: also time this many steps of a second round with "
-                        "refill_ops' retry policy and report it under detail.retry (0 = skip)")
+    p.add_argument("--refill", choices=["fresh", "retry"], default="retry",
+                   help="retry: refill_ops (inline-util.h:149-303), stalled ops keep their slot, as the "
+                        "reference; fresh: every worker gets a fresh batch per round, stalled ops dropped")
+    p.add_argument("--retry", action="store_true", help="same as --refill retry")
+    p.add_argument("--skew", type=int, default=3,
+                   help="the reference's opt-in skew optimisations (config.h:77-80), a bit mask: 1 completes a "
+                        "stalled GET once its key's version moved two on (READ_COMPLETE_AFTER_VAL_RECV_OF_HOT_REQS), "
+                        "2 coalesces a stalled PUT into the local write in flight (WRITE_COALESCE_TO_THE_SAME_KEY_IN_"
+                        "SAME_NODE); default 3, 0 = the reference's default build")
+    p.add_argument("--coalesce-hot", action="store_true",
+                   help="refill_ops' ENABLE_COALESCE_OF_HOT_REQS: requests on the 100 hottest ids join the worker's "
+                        "live op of that id (committed ops count them)")
+    p.add_argument("--policy-steps", "--retry-steps", type=int, default=10, dest="policy_steps",
+                   help="N=1: also time this many steps of each other refill policy on the same table and "
+                        "report them under detail.policies (0 = skip)")
     p.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                    help="torch.distributed backend for N>1 (nccl = RCCL; gloo lets several ranks share one "
                         "GPU in tests)")
@@ -121,6 +131,9 @@ def main():
 
     cfg3 = a.config == "cfg3"
     cfg5 = a.config == "cfg5"
+    if a.retry:
+        a.refill = "retry"
+    retry = a.refill == "retry"
     if a.keys is None:  # cfg3: configs[1]'s 100M keys in 320-B entries (a 32 GiB log)
         a.keys = 100_000_000 if world == 1 and not cfg5 else 1_000_000_000
     if cfg3 and world > 1:
@@ -135,7 +148,7 @@ def main():
     sizes = L.Sizes(True, 4) if cfg3 else L.DEFAULT
     bkts, cap = sized_geometry(a.keys, sizes)
     kvs = HermesKV(a.keys, bkts, cap, machine_id=rank if world > 1 else 0, device=dev, rmw=cfg3,
-                   big_objects=cfg3, extra_cache_lines=4 if cfg3 else 0)
+                   big_objects=cfg3, extra_cache_lines=4 if cfg3 else 0, skew=a.skew)
     BYTES = elem_bytes(kvs.sizes.op, kvs.sizes.entry, kvs.sizes.op if cfg3 else 16)
     torch.cuda.synchronize()
     t_pop = time.time() - t0
@@ -154,13 +167,13 @@ def main():
         # cfg5: the membership comes from Hades agreement over per-round heartbeats (SURVEY 8(f)
         # row 4): the failed rank stops heartbeating and the survivors expel it when they agree
         rnd = ReplicaGroupRound(kvs, a.workers, z, a.write_permille, seed=a.seed, world=world, rank=rank,
-                                retry_stalled=a.retry, hades=cfg5)
+                                retry_stalled=retry, hades=cfg5)
     else:
         machines = 8 if cfg5 else 3
         rnd = Round(kvs, a.workers, L.membership(machines, 0), list(range(1, machines)), z, a.write_permille,
                     a.rmw_permille, seed=a.seed,
-                    max_steps=total_steps + 2, retry_stalled=a.retry, fit_ack_stride=not a.no_fit_acks,
-                    val_credits=a.val_credits, hades=cfg5)
+                    max_steps=total_steps + 2, retry_stalled=retry, fit_ack_stride=not a.no_fit_acks,
+                    val_credits=a.val_credits, hades=cfg5, coalesce_hot=a.coalesce_hot)
     torch.cuda.synchronize()
 
     for _ in range(a.warmup):
@@ -251,7 +264,7 @@ def main():
         with open(pmc) as f:
             traffic = json.load(f)["traffic_bytes"]
         traffic_src = "profiles/pmc_local_batch.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, separate runs)"
-    refill = "retry" if a.retry else "fresh"
+    refill = a.refill
     out = {
         "metric": "replicated KVS ops/s (reads+writes committed)",
         "value": value,
@@ -280,11 +293,15 @@ def main():
             "keys": a.keys, "buckets": bkts, "log_cap": cap, "workers_per_gpu": W,
             "local_batch": S, "zipf": a.zipf, "write_permille": a.write_permille,
             "rmw_permille_of_writes": a.rmw_permille,
-            # fresh: every worker gets a fresh 250-op batch each round; ops that stalled (e.g. a GET
-            # on a key being written) are dropped and counted in detail.dropped_per_step, never
-            # committed; writes in flight keep their slots. retry: refill_ops (inline-util.h:149-303),
-            # stalled ops keep their slots (detail.retry reports that policy's rate at N=1)
+            # retry: refill_ops (inline-util.h:149-303), stalled ops keep their slots, as the reference;
+            # fresh: every worker gets a fresh 250-op batch each round, stalled ops (e.g. a GET on a
+            # key being written) are dropped and counted in detail.dropped_per_step, never committed;
+            # writes in flight keep their slots. detail.policies times the others at N=1.
             "refill": refill,
+            # the reference's opt-in skew optimisations (config.h:77-80): skew_flags bit 0 read
+            # completion, bit 1 write coalescing (hermesKV.c:196-238); coalesce_hot: refill_ops'
+            # hot-request coalescing (inline-util.h:237-257)
+            "skew_flags": a.skew, "coalesce_hot": a.coalesce_hot,
             # VAL credits per worker and round (null: never binding, hermes_worker.c:479's gate idle)
             "val_credits": getattr(rnd, "V", None),
             "remote_invs_per_worker": rnd.rstride, "parallelism": f"replicas{world}",
@@ -327,12 +344,14 @@ def main():
             out["detail"]["membership"]["agreed_at_round"] = [c[0] for c in rnd.hades_changes]
     if snap is not None:
         from oracle.cpu_baseline import run_cpu_baseline
+        from hermes_amd.workload import refill_flags
         cpu = run_cpu_baseline(kvs, z, a.write_permille, a.cpu_workers, a.cpu_seconds, a.seed,
-                               refill_all=not a.retry, threads=a.cpu_threads, snapshot=snap)
+                               refill_flags=refill_flags(kvs, retry, a.coalesce_hot), threads=a.cpu_threads,
+                               snapshot=snap)
     if cpu is not None:
         out["cpu_baseline"] = cpu
-    if world == 1 and not a.retry and a.retry_steps > 0 and not cfg5:
-        out["detail"]["retry"] = retry_rate(a, kvs, z, L, Round)
+    if world == 1 and a.policy_steps > 0 and not cfg5:
+        out["detail"]["policies"] = policy_rates(a, kvs, z, L, Round, (retry, a.skew, a.coalesce_hot))
     if rank == 0 and world == 1 and a.host_api_seconds > 0:
         out["detail"]["host_api"] = host_api_rate(a.host_api_seconds)
     if rank == 0:
@@ -341,25 +360,50 @@ def main():
         dist.destroy_process_group()
 
 
-def retry_rate(a, kvs, z, L, Round) -> dict:
-    """The same round with refill_ops' retry policy (stalled ops keep their slots), on the same
-    table, after the headline run: W warmup steps, then a.retry_steps timed steps."""
+# the refill policies bench.py can time: (name, retry, skew_flags, coalesce_hot, what)
+POLICIES = [
+    ("fresh", False, 0, False, "a fresh batch per worker and round, stalled ops dropped (not the reference)"),
+    ("retry", True, 0, False, "refill_ops (inline-util.h:149-303): stalled ops keep their slots; the reference's "
+                              "default configuration"),
+    ("retry_skew", True, 3, False, "refill_ops with the reference's skew optimisations: read completion and write "
+                                   "coalescing (config.h:79-80, hermesKV.c:196-238)"),
+    ("retry_skew_hot", True, 3, True, "retry_skew plus hot-request coalescing in refill_ops (config.h:77-78, "
+                                      "inline-util.h:237-257); committed ops count the coalesced requests"),
+]
+
+
+def policy_rates(a, kvs, z, L, Round, headline) -> dict:
+    """Every other refill policy of POLICIES on the same table, after the headline run (each round
+    leaves every write complete, so the table carries no state from one policy to the next): a
+    fresh Round, max(warmup, 10) untimed steps (retry's stalls build up over rounds), then
+    a.policy_steps timed steps."""
     import torch
-    r = Round(kvs, a.workers, L.membership(3, 0), [1, 2], z, a.write_permille, a.rmw_permille,
-              seed=a.seed + 1, max_steps=a.warmup + a.retry_steps + 2, retry_stalled=True)
-    for _ in range(a.warmup):
-        r.step()
-    torch.cuda.synchronize()
-    c0 = r.fold_counters()[:4].clone()
-    t = time.perf_counter()
-    for _ in range(a.retry_steps):
-        r.step()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t
-    c = (r.fold_counters()[:4] - c0).tolist()
-    return {"value": c[0] / dt, "unit": "ops/s", "steps": a.retry_steps, "ms_per_step": dt * 1e3 / a.retry_steps,
-            "committed_per_step": c[0] / a.retry_steps, "writes_completed_per_step": c[2] / a.retry_steps,
-            "what": "refill_ops retry policy (stalled ops keep their slots), same workload and table"}
+    out = {}
+    skew0 = kvs.skew
+    warm = max(a.warmup, 10)
+    for name, retry, skew, hot, what in POLICIES:
+        if (retry, skew, hot) == headline:
+            continue
+        kvs.set_skew(skew)
+        r = Round(kvs, a.workers, L.membership(3, 0), [1, 2], z, a.write_permille, a.rmw_permille,
+                  seed=a.seed + 1, max_steps=warm + a.policy_steps + 2, retry_stalled=retry, coalesce_hot=hot)
+        for _ in range(warm):
+            r.step()
+        torch.cuda.synchronize()
+        c0 = r.fold_counters()[:4].clone()
+        t = time.perf_counter()
+        for _ in range(a.policy_steps):
+            r.step()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        c = (r.fold_counters()[:4] - c0).tolist()
+        out[name] = {"value": c[0] / dt, "unit": "ops/s", "steps": a.policy_steps, "warmup": warm,
+                     "ms_per_step": dt * 1e3 / a.policy_steps, "committed_per_step": c[0] / a.policy_steps,
+                     "writes_completed_per_step": c[2] / a.policy_steps, "dropped_per_step": c[3] / a.policy_steps,
+                     "what": what}
+        del r
+    kvs.set_skew(skew0)
+    return out
 
 
 if __name__ == "__main__":

@@ -121,6 +121,27 @@ __device__ __forceinline__ uint8_t absorbing_state()
     return TYPE == kVals ? kValid : kWrite;
 }
 
+// The meta every element after F (its key's only mutation in the launch) runs against, from S_0.
+// Without the skew optimisations only the absorbing state matters. With them, a stalled GET or
+// PUT also reads the timestamp and tells WRITE from REPLAY (hermesKV.c:196-238), so the meta is
+// S_1 itself: after a PUT, update_actions' WRITE with version + 2 and this machine's cid
+// (hermesKV.c:100-141, RMWs off); after a GET replay, REPLAY with the timestamp unchanged
+// (:155-175). f_is_put: F is known to be a PUT (else its opcode is read).
+template <int TYPE>
+__device__ __forceinline__ Meta after_first(const BatchArgs &a, const Meta &m0, uint32_t f, int f_is_put)
+{
+    Meta m1 = m0;
+    m_set_state(m1, absorbing_state<TYPE>());
+    if (TYPE != kLocal || a.g.skew == 0) return m1;
+    if (f_is_put || a.elems[(int64_t)f * a.esz + 8] != kOpGet) {
+        m1.ver += 2;
+        m_set_cid(m1, (uint8_t)a.g.machine_id);
+    } else {
+        m_set_state(m1, kReplay);
+    }
+    return m1;
+}
+
 // INV direct path (INV launches without RMWs, fewer than 2^23 elements). Without RMWs,
 // hermes_exec_inv (hermesKV.c:489-588) on one key, element by element from S_0, comes to this:
 // let M be the largest INV timestamp of the key's elements.
@@ -862,8 +883,7 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
                 uint8_t *xg;
                 uint8_t idx;
                 elem_at(a, (uint32_t)i, xg, idx, c);
-                Meta m1 = m;
-                m_set_state(m1, absorbing_state<TYPE>());
+                const Meta m1 = after_first<TYPE>(a, m, f, 0);
                 Meta tm = m1;
                 dispatch<SV>(TYPE, reinterpret_cast<uint8_t *>(sops) + (uint32_t)t * a.esz, rentry, idx, tm, c);
                 if (a.error_flags && !meta_equal(tm, m1)) atomicOr(a.error_flags, 1u);
@@ -916,8 +936,7 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
             apply_to_shadow<TYPE, SV>(a, nullptr, (uint32_t)i, entry_of(a, e));
             st = kStCommit;
         } else if (a.rounds == 0) {
-            Meta m1 = m;
-            m_set_state(m1, absorbing_state<TYPE>());
+            const Meta m1 = after_first<TYPE>(a, m, f, 0);
             Meta tm = m1;
             dispatch<SV>(TYPE, xg, entry_of(a, e), idx, tm, c);
             if (a.error_flags && !meta_equal(tm, m1)) atomicOr(a.error_flags, 1u);
@@ -1249,12 +1268,12 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
                 const uint32_t f = first_cand(sfw[tid], a.rtag0);
                 // a mutating element must have offered itself in k_local_pre
                 if (wm && (f == kNone || f > (uint32_t)i) && a.error_flags) atomicOr(a.error_flags, 4u);
-                Meta m0 = m;
                 if ((uint32_t)i == f) {
                     apply_to_shadow<kLocal, 31>(a, x, (uint32_t)i, ent);
                     st = kStCommit;
                 } else {
-                    if (f != kNone && (uint32_t)i > f) m_set_state(m0, absorbing_state<kLocal>());
+                    // F of a key that is not INVALID is its first PUT (k_local_pre)
+                    const Meta m0 = f != kNone && (uint32_t)i > f ? after_first<kLocal>(a, m, f, 1) : m;
                     Meta tm = m0;
                     dispatch<31>(kLocal, x, ent, bidx, tm, c);
                     if (a.error_flags && !meta_equal(tm, m0)) atomicOr(a.error_flags, 1u);
@@ -1308,8 +1327,7 @@ __global__ __launch_bounds__(256) void k_local_deferred(BatchArgs a)
             apply_to_shadow<kLocal, 31>(a, nullptr, i, entry_of(a, e));
             st = kStCommit;
         } else {
-            Meta m1 = m;
-            m_set_state(m1, absorbing_state<kLocal>());
+            const Meta m1 = after_first<kLocal>(a, m, f, 0);
             Meta tm = m1;
             dispatch<31>(kLocal, xg, entry_of(a, e), idx, tm, c);
             if (a.error_flags && !meta_equal(tm, m1)) atomicOr(a.error_flags, 1u);

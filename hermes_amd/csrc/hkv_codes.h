@@ -51,6 +51,9 @@ struct Geometry {
     uint32_t entry_unit;    // divisor turning a physical log offset into a dense entry id
     uint32_t rmw_enabled;
     uint32_t machine_id;
+    uint32_t skew;          // HKV_SKEW_* (hkv_config.skew_flags)
 };
+constexpr uint32_t kSkewReadComplete = 1u;   // ENABLE_READ_COMPLETE_AFTER_VAL_RECV_OF_HOT_REQS
+constexpr uint32_t kSkewWriteCoalesce = 2u;  // ENABLE_WRITE_COALESCE_TO_THE_SAME_KEY_IN_SAME_NODE
 
 }  // namespace hkv

@@ -179,6 +179,18 @@ __device__ __forceinline__ void update_actions(uint8_t *op, uint8_t *entry, uint
     op[9] = rmw_flag ? kRmwSuccess : kPutSuccess;
 }
 
+// hermes_complete_hot_read_optimization, hermesKV.c:224-238 (HKV_SKEW_READ_COMPLETE): a stalled
+// GET records the key's timestamp when its own is (0, 0), and completes -- without a value, as
+// shipped ("TODO we also need to get the value here") -- once the key's version is two above it.
+// cur: the timestamp exec_read saw (the meta's; a write replay leaves it unchanged).
+__device__ __forceinline__ void hot_read_complete(uint8_t *op, uint32_t cur_ver, uint8_t cur_cid)
+{
+    if (op[9] != kGetStall) return;
+    const uint32_t over = ld32(op + 12);
+    if (over == 0 && op[11] == 0) e_set_ts(op, cur_ver, cur_cid);
+    else if (over + 1u < cur_ver) op[9] = kGetComplete;
+}
+
 // hermes_exec_read, hermesKV.c:251-311
 template <int SV>
 __device__ __forceinline__ void exec_read(uint8_t *op, uint8_t *entry, uint8_t idx, Meta &m, const Ctx &c)
@@ -194,15 +206,33 @@ __device__ __forceinline__ void exec_read(uint8_t *op, uint8_t *entry, uint8_t i
         op[9] = kEmpty;
         if (st == kInvalid) membership_replay<SV>(op, idx, m, entry, c);
     }
+    if (c.g.skew & kSkewReadComplete) hot_read_complete(op, m.ver, m_cid(m));
 }
 
-// hermes_exec_write, hermesKV.c:314-356 (write coalescing off, config.h:80)
+// hermes_exec_write, hermesKV.c:314-356, with hermes_marshal_write_coalesce_optimization and
+// hermes_complete_coalesced_write (:196-221) under HKV_SKEW_WRITE_COALESCE: a PUT that stalls in
+// VALID/INVALID (op buffer index set), WRITE or INVALID_WRITE -- not REPLAY -- records the key's
+// version as 16 bits when its own ts.version is 0; any stalled PUT completes once its
+// ts.version + 1 is below that 16-bit version. (The ts of a refilled PUT is whatever its slot
+// held: refill_ops resets only GETs', inline-util.h:268-272.)
 template <int SV>
 __device__ __forceinline__ void exec_write(uint8_t *op, uint8_t *entry, uint8_t idx, Meta &m, const Ctx &c)
 {
     uint8_t st = m_state(m);
-    if ((st == kValid || st == kInvalid) && m_obi(m) == kObiEmpty) update_actions<SV>(op, entry, idx, m, c, 0);
-    else op[9] = kPutStall;
+    if ((st == kValid || st == kInvalid) && m_obi(m) == kObiEmpty) {
+        update_actions<SV>(op, entry, idx, m, c, 0);
+        return;
+    }
+    op[9] = kPutStall;
+    if (c.g.skew & kSkewWriteCoalesce) {
+        const uint32_t cv = m.ver & 0xFFFFu;   // (uint16_t)(version - 1) under the lock
+        uint32_t over = ld32(op + 12);
+        if (st != kReplay && over == 0) {
+            st32(op + 12, cv);
+            over = cv;
+        }
+        if (over > 0 && over + 1u < cv) op[9] = kPutComplete;
+    }
 }
 
 // hermes_exec_rmw, hermesKV.c:358-428

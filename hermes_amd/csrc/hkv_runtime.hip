@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <sched.h>
+#include <unistd.h>
 #include <atomic>
 #include <condition_variable>
 #include <deque>
@@ -90,7 +91,6 @@ struct hkv_table {
     std::condition_variable hcv;
     std::deque<HostReq *> hq;
     bool combining = false;
-    int inside = 0;   // callers inside hermes_batch_ops_to_KVS (queued, or waiting for results)
     HostSet sets[kHostSets];
     std::mutex mu;
 };
@@ -168,6 +168,7 @@ static void make_geometry(const hkv_config &c, Geometry &g)
     g.entry_unit = (c.log_cap % g.entry_size == 0) ? g.entry_size : (low > 8u ? low : 8u);
     g.rmw_enabled = c.rmw_enabled ? 1u : 0u;
     g.machine_id = c.machine_id;
+    g.skew = c.skew_flags & (kSkewReadComplete | kSkewWriteCoalesce);
 }
 
 static int bit_width(uint64_t x)
@@ -249,6 +250,8 @@ int hkv_table_create(const hkv_config *cfg, hkv_table **out)
     if (!is_pow2(cfg->num_bkts) || cfg->num_bkts > (1ull << 31)) return fail(-1, "num_bkts must be a power of two <= 2^31");
     if (!is_pow2(cfg->log_cap) || cfg->log_cap < 4096) return fail(-1, "log_cap must be a power of two >= 4096");
     if (cfg->machine_id > 127) return fail(-1, "machine_id must be < 128");
+    if (cfg->skew_flags & ~(HKV_SKEW_READ_COMPLETE | HKV_SKEW_WRITE_COALESCE))
+        return fail(-1, "unknown skew_flags %#x", cfg->skew_flags);
     // 287 + 64 k value bytes in (k + 1) cache lines: val_len >> SHIFT_BITS must fit its byte and
     // the batch engine stages 128 entries of a launch in one workgroup's LDS
     if (cfg->big_objects && (cfg->extra_cache_lines < 1 || cfg->extra_cache_lines > 16))
@@ -315,6 +318,16 @@ int hkv_table_config(const hkv_table *t, hkv_config *out)
     return 0;
 }
 
+int hkv_table_set_skew(hkv_table *t, uint32_t skew_flags)
+{
+    if (!t) return fail(-1, "null table");
+    if (skew_flags & ~(HKV_SKEW_READ_COMPLETE | HKV_SKEW_WRITE_COALESCE)) return fail(-1, "unknown skew_flags %#x", skew_flags);
+    std::lock_guard<std::mutex> lk(t->mu);
+    t->cfg.skew_flags = skew_flags;
+    t->geo.skew = skew_flags;
+    return 0;
+}
+
 int hkv_table_populate(hkv_table *t, int64_t n, int val_len)
 {
     if (!t) return fail(-1, "null table");
@@ -374,22 +387,33 @@ int hkv_table_populate(hkv_table *t, int64_t n, int val_len)
     return 0;
 }
 
-int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
+// The element rules every launch obeys, whichever entry point it comes through: a known type,
+// elements of at least 16 bytes in 8-byte units (the engines move them in 8- and 16-byte words),
+// room for the value where the exec functions read or write one, and at most 255 ops per local
+// batch (op_buffer_index is a uint8, 255 = empty).
+static int check_elems(const hkv_table *t, int type, uint32_t elem_size, int64_t per_batch)
 {
-    if (!t || !d) return fail(-1, "null argument");
-    if (d->type < 0 || d->type > 4) return fail(-1, "bad batch type %d", d->type);
-    const bool packed = (d->flags & HKV_BATCH_PACKED) != 0;
-    if (d->n_batches < 0 || d->stride < 0 || (d->stride == 0 && !packed)) return fail(-1, "bad batch geometry");
-    if (d->elem_size < kOpMetaSize || (d->elem_size & 7)) return fail(-1, "elem_size %u must be >= 16 and a multiple of 8", d->elem_size);
+    if (type < 0 || type > 4) return fail(-1, "bad batch type %d", type);
+    if (elem_size < (uint32_t)kOpMetaSize || (elem_size & 7))
+        return fail(-1, "elem_size %u must be >= 16 and a multiple of 8", elem_size);
     // ACK batches of an RMW table carry INV-aborts, which hermes_exec_inv applies with their value
     // (hermesKV.c:877-890): they need op-sized elements, as the reference worker sends them
     // (hermes_worker.c:332)
-    const bool needs_value = d->type == kLocal || d->type == kLocalAfterMemb || d->type == kInvs ||
-                             (d->type == kAcks && t->geo.rmw_enabled);
-    if (needs_value && d->elem_size < kOpValueOff + t->geo.st_value)
-        return fail(-1, "elem_size %u too small for %u-byte values", d->elem_size, t->geo.st_value);
-    if (d->type == kLocal && d->stride > 255)
+    const bool needs_value = type == kLocal || type == kLocalAfterMemb || type == kInvs ||
+                             (type == kAcks && t->geo.rmw_enabled);
+    if (needs_value && elem_size < kOpValueOff + t->geo.st_value)
+        return fail(-1, "elem_size %u too small for %u-byte values", elem_size, t->geo.st_value);
+    if (type == kLocal && per_batch > 255)
         return fail(-1, "local batches hold at most 255 ops (uint8 op_buffer_index)");
+    return 0;
+}
+
+int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
+{
+    if (!t || !d) return fail(-1, "null argument");
+    const bool packed = (d->flags & HKV_BATCH_PACKED) != 0;
+    if (d->n_batches < 0 || d->stride < 0 || (d->stride == 0 && !packed)) return fail(-1, "bad batch geometry");
+    if (int rc = check_elems(t, d->type, d->elem_size, packed ? 0 : d->stride)) return rc;
     // HKV_BATCH_PACKED: d_counts holds n_batches + 1 element offsets and stride the total
     if (packed && d->type != kInvs && d->type != kVals && d->type != kAcks)
         return fail(-1, "HKV_BATCH_PACKED applies to INV, ACK and VAL batches");
@@ -680,7 +704,16 @@ static void host_launch_mixed(hkv_table *t, HostSet *set, std::unique_lock<std::
     set->small = true;
     if (g_host_stats) host_stats_note(nb);
     TRACE("mixed launch batches=%d elements=%lld", nb, (long long)elems);
-    if (launch_batch(bl, t->stream)) die("hermes_batch_ops_to_KVS (small launch)");
+    if (elems == 0) {
+        // nothing to apply (callers never queue empty batches; kept as a guard): no kernel would
+        // store the completion flag, so the host does
+        __atomic_store_n(set->flag, bl.done_value, __ATOMIC_RELEASE);
+    } else {
+        // t->mu orders the launch against hkv_table_populate, which moves geo.log_head
+        std::lock_guard<std::mutex> tl(t->mu);
+        bl.g = t->geo;
+        if (launch_batch(bl, t->stream)) die("hermes_batch_ops_to_KVS (small launch)");
+    }
     lk.lock();
     set->busy = true;
     set->refs = nb;
@@ -694,9 +727,20 @@ static void host_launch_mixed(hkv_table *t, HostSet *set, std::unique_lock<std::
 
 // Called with t->hmu held by a caller that found no combiner active: launches the compatible
 // batches at the head of the queue as one multi-batch launch (see "combining submit" above).
+// Test hook (hkv_debug_host_hold): a combiner first waits until this many batches are queued
+// (or 5 s pass), so a test can put batches from several threads into one launch in a known order.
+static std::atomic<int> g_host_hold{0};
+
 static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
 {
     t->combining = true;
+    if (const int hold = g_host_hold.load()) {
+        for (int spins = 0; (int)t->hq.size() < hold && spins < 50000; ++spins) {
+            lk.unlock();
+            usleep(100);
+            lk.lock();
+        }
+    }
     HostSet *set = nullptr;
     static const int n_sets = getenv("HKV_HOST_SETS") ? std::max(1, std::min(kHostSets, atoi(getenv("HKV_HOST_SETS")))) : kHostSets;
     for (;;) {
@@ -709,22 +753,6 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
         }
         if (set) break;
         t->hcv.wait(lk);
-    }
-    // While another launch is in flight the GPU has work: wait for the callers that are not
-    // waiting on it to queue their batches (or for it to finish), so one launch carries them all.
-    for (;;) {
-        int other = 0;
-        const HostSet *busy = nullptr;
-        for (const HostSet &hs : t->sets)
-            if (hs.busy) {
-                other += hs.refs;
-                busy = &hs;
-            }
-        if (!busy || (int)t->hq.size() >= t->inside - other || (int)t->hq.size() >= kSmallMaxBatches) break;
-        if (busy->small && __atomic_load_n(busy->flag, __ATOMIC_ACQUIRE) == busy->seq) break;
-        lk.unlock();
-        for (int k = 0; k < 64; ++k) __builtin_ia32_pause();
-        lk.lock();
     }
     std::vector<HostReq *> take;
     int stride = 0;
@@ -788,7 +816,10 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
     memcpy(d.membership, &r0->mb, 8);
     TRACE("combined launch type=%d batches=%d stride=%d", d.type, nb, stride);
     if (g_host_stats) host_stats_note(nb);
-    if (hkv_batch_async(t, &d, s)) die("hermes_batch_ops_to_KVS");
+    {
+        std::lock_guard<std::mutex> tl(t->mu);   // against hkv_table_populate (geo.log_head)
+        if (hkv_batch_async(t, &d, s)) die("hermes_batch_ops_to_KVS");
+    }
     if (hipMemcpyAsync(set->h, set->d, total, hipMemcpyDeviceToHost, s) != hipSuccess) die("copy out");
     if (hipEventRecord(set->ev, s) != hipSuccess) die("event record");
     lk.lock();
@@ -800,6 +831,25 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
     }
     t->combining = false;
     t->hcv.notify_all();
+}
+
+int hkv_debug_host_hold(int n_batches)
+{
+    if (n_batches < 0 || n_batches > kSmallMaxBatches) return fail(-1, "hold must be 0..%d", kSmallMaxBatches);
+    g_host_hold.store(n_batches);
+    return 0;
+}
+
+int hkv_debug_host_queued(void)
+{
+    hkv_table *t;
+    {
+        std::lock_guard<std::mutex> lk(g_default_mu);
+        t = g_default;
+    }
+    if (!t) return 0;
+    std::lock_guard<std::mutex> lk(t->hmu);
+    return (int)t->hq.size();
 }
 
 // see the ABI note in hermeskv.h: curr_membership arrives as gcc passes the reference struct
@@ -821,10 +871,12 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
         g_err = "spacetime_init was not called";
         die("hermes_batch_ops_to_KVS");
     }
-    if ((int)type < 0 || (int)type > 4 || (type == local_ops && op_num > 255) || (int64_t)op_num > kHostMaxElems) {
-        g_err = "bad batch (type, or more ops than a launch holds)";
+    if ((int64_t)op_num > kHostMaxElems) {
+        g_err = "more ops than a launch holds";
         die("hermes_batch_ops_to_KVS");
     }
+    // the same element rules as hkv_batch_async, before anything is queued (either launch path)
+    if (check_elems(t, (int)type, sizeof_op_elem, op_num)) die("hermes_batch_ops_to_KVS");
     if (hipSetDevice(t->cfg.device) != hipSuccess) die("hipSetDevice");
     HostReq r;
     r.type = (int)type;
@@ -836,7 +888,6 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
     r.rw = type == acks ? reinterpret_cast<uint8_t *>(read_write_ops) : nullptr;
     std::unique_lock<std::mutex> lk(t->hmu);
     t->hq.push_back(&r);
-    ++t->inside;
     while (!r.launched) {
         if (!t->combining) host_combine(t, lk);
         else t->hcv.wait(lk);
@@ -858,7 +909,6 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
     if (r.rw && r.rw_bytes) memcpy(r.rw, set->h + r.rw_off, r.rw_bytes);
     if (r.ns) memcpy(r.ns, set->h + r.ns_off, 4);
     lk.lock();
-    --t->inside;
     if (--set->refs == 0) {
         set->busy = false;
         t->hcv.notify_all();

@@ -164,9 +164,10 @@ __global__ __launch_bounds__(256) void k_fold_counters(unsigned long long *count
 __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, uint32_t op_size, uint32_t st_value,
                                                 uint32_t shift, const uint64_t *tkey, const uint8_t *top,
                                                 int32_t tlen, uint32_t *cursor, uint32_t machine_id,
-                                                int32_t first_iter, int32_t refill_all, unsigned long long *counters,
+                                                int32_t first_iter, uint32_t flags, unsigned long long *counters,
                                                 uint8_t *opc_out)
 {
+    const bool refill_all = (flags & HKV_WL_REFILL_ALL) != 0;
     extern __shared__ uint64_t slab[];
     const int w = blockIdx.x, i = threadIdx.x;
     const bool live = i < stride;
@@ -212,8 +213,12 @@ __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, ui
         op[8] = oc;
         op[9] = kNew;
         op[10] = oc == kOpGet ? 0 : (uint8_t)(st_value >> shift);
-        uint16_t flags = (uint16_t)((oc == kOpRmw ? 1u : 0u) | (first_iter ? 0u : 2u));  // RMW_flag, no_coales = 1
-        *reinterpret_cast<uint16_t *>(op + 16) = flags;
+        if (oc == kOpGet && (flags & HKV_WL_READ_TS_RESET)) {  // inline-util.h:268-272
+            op[11] = 0;
+            *reinterpret_cast<uint32_t *>(op + 12) = 0;
+        }
+        const uint16_t fl = (uint16_t)((oc == kOpRmw ? 1u : 0u) | (first_iter ? 0u : 2u));  // RMW_flag, no_coales = 1
+        *reinterpret_cast<uint16_t *>(op + 16) = fl;
         if (oc != kOpGet) {
             uint8_t v = (uint8_t)('a' + machine_id);
             for (uint32_t k = 0; k < st_value; ++k) op[kOpValueOff + k] = v;
@@ -230,15 +235,145 @@ __global__ __launch_bounds__(256) void k_refill(uint8_t *ops, int32_t stride, ui
     }
 }
 
+// refill_ops with ENABLE_COALESCE_OF_HOT_REQS (inline-util.h:237-257, config.h:77-78): a trace
+// command on one of the COALESCE_N_HOTTEST_KEYS hottest ids (GET or PUT) whose worker's last op
+// inserted for that id and opcode class (n_hottest_keys_in_ops_get/_put, hermes_worker.c:394-399:
+// per worker, kept across refills, never cleared) currently has the same opcode is absorbed into
+// it (no_coales + 1) instead of taking a slot; the pointer names a slot, not an op, so as in the
+// reference the slot may hold another key by then. A completed op counts no_coales commits. The
+// walk is sequential by nature (each command's fate depends on the pointers the previous ones
+// left), so one lane runs it over LDS copies of the slab, the pointers and a window of the trace;
+// the slab edits that do not feed the walk (key, value, timestamp) then go in parallel.
+constexpr int kHotKeys = 100;         // COALESCE_N_HOTTEST_KEYS, config.h:78
+constexpr int kHotWindow = 2048;      // trace commands staged in LDS (the walk reads on from memory)
+__global__ __launch_bounds__(256) void k_refill_hot(uint8_t *ops, int32_t stride, uint32_t op_size, uint32_t st_value,
+                                                    uint32_t shift, const uint64_t *tkey, const uint8_t *top,
+                                                    const uint32_t *tid, int32_t tlen, uint32_t *cursor,
+                                                    uint32_t machine_id, int32_t first_iter, uint32_t flags,
+                                                    unsigned long long *counters, uint8_t *opc_out, uint8_t *hot)
+{
+    extern __shared__ uint64_t slab[];
+    __shared__ uint32_t wid[kHotWindow];
+    __shared__ uint8_t wop[kHotWindow];
+    __shared__ uint8_t hp[2 * kHotKeys];     // [0, 100): GET pointers, [100, 200): PUT/RMW; 0xFF = NULL
+    __shared__ int32_t tpos[256];            // trace position a refilled slot takes, -1: kept
+    __shared__ unsigned long long tot[kCounters];
+    const int w = blockIdx.x, i = threadIdx.x;
+    const bool refill_all = (flags & HKV_WL_REFILL_ALL) != 0;
+    uint64_t *gslab = reinterpret_cast<uint64_t *>(ops + (int64_t)w * stride * op_size);
+    const int words = (int)((uint32_t)stride * op_size / 8u);
+    for (int k = i; k < words; k += 256) slab[k] = gslab[k];
+    const uint32_t base = cursor[w];
+    for (int k = i; k < kHotWindow; k += 256) {
+        const int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)k) % (uint32_t)tlen);
+        wid[k] = tid[t];
+        wop[k] = top[t];
+    }
+    for (int k = i; k < 2 * kHotKeys; k += 256) hp[k] = hot[(int64_t)w * 2 * kHotKeys + k];
+    __syncthreads();
+    uint8_t *sb = reinterpret_cast<uint8_t *>(slab);
+    if (i == 0) {
+        unsigned long long c = 0, m = 0, wr = 0, dr = 0, ab = 0;
+        uint32_t it = 0;   // commands consumed (window position)
+        auto cmd = [&](uint32_t k, uint32_t &id, uint8_t &oc) {
+            if (k < (uint32_t)kHotWindow) {
+                id = wid[k];
+                oc = wop[k];
+            } else {
+                const int64_t t = (int64_t)w * tlen + (int64_t)((base + k) % (uint32_t)tlen);
+                id = tid[t];
+                oc = top[t];
+            }
+        };
+        for (int s = 0; s < stride; ++s) {
+            uint8_t *op = sb + (uint32_t)s * op_size;
+            const uint8_t st = op[9];
+            const bool complete = is_complete(st);
+            const bool drop = !first_iter && refill_all && !complete && !in_flight(st);
+            if (!(first_iter || complete || drop)) {
+                tpos[s] = -1;
+                continue;
+            }
+            if (!first_iter) {
+                if (complete) {
+                    if (st == kMiss) ++m;
+                    else if (st != kRmwAbort) c += (unsigned long long)(*reinterpret_cast<uint16_t *>(op + 16) >> 1);
+                    if (st == kPutComplete) ++wr;
+                    if (st == kRmwAbort) ++ab;
+                }
+                if (drop) ++dr;
+                op[8] = kEmpty;   // reset op bucket: no_coales = 1, state = opcode = ST_EMPTY
+                op[9] = kEmpty;
+            }
+            uint32_t id;
+            uint8_t oc;
+            cmd(it, id, oc);
+            if (oc != kOpRmw) {   // coalesce while the command's hot id has a live op of its opcode
+                for (;;) {
+                    cmd(it, id, oc);
+                    const int arr = oc == kOpGet ? 0 : kHotKeys;
+                    if (id < (uint32_t)kHotKeys && hp[arr + id] != 0xFF &&
+                        sb[(uint32_t)hp[arr + id] * op_size + 8] == oc) {
+                        uint16_t *nc = reinterpret_cast<uint16_t *>(sb + (uint32_t)hp[arr + id] * op_size + 16);
+                        *nc = (uint16_t)((*nc & 1u) | ((((*nc >> 1) + 1u) & 0x7FFFu) << 1));
+                        ++it;
+                    } else {
+                        break;
+                    }
+                }
+                if (id < (uint32_t)kHotKeys) hp[(oc == kOpGet ? 0 : kHotKeys) + id] = (uint8_t)s;
+            }
+            tpos[s] = (int32_t)it;
+            op[8] = oc;
+            op[9] = kNew;
+            op[10] = oc == kOpGet ? 0 : (uint8_t)(st_value >> shift);
+            // no_coales := 1 (0 on the first pass, where refill_ops does not reset it), RMW_flag
+            *reinterpret_cast<uint16_t *>(op + 16) = (uint16_t)((oc == kOpRmw ? 1u : 0u) | (first_iter ? 0u : 2u));
+            ++it;
+        }
+        cursor[w] = (uint32_t)((base + it) % (uint32_t)tlen);
+        tot[0] = c;
+        tot[1] = m;
+        tot[2] = wr;
+        tot[3] = dr;
+        tot[4] = ab;
+    }
+    __syncthreads();
+    if (i < stride && tpos[i] >= 0) {   // key, timestamp, value of the refilled slots
+        uint8_t *op = sb + (uint32_t)i * op_size;
+        const uint32_t k = (uint32_t)tpos[i];
+        const int64_t t = (int64_t)w * tlen + (int64_t)((base + k) % (uint32_t)tlen);
+        *reinterpret_cast<uint64_t *>(op) = tkey[t];
+        const uint8_t oc = op[8];
+        if (oc == kOpGet && (flags & HKV_WL_READ_TS_RESET)) {
+            op[11] = 0;
+            *reinterpret_cast<uint32_t *>(op + 12) = 0;
+        }
+        if (oc != kOpGet) {
+            const uint8_t v = (uint8_t)('a' + machine_id);
+            for (uint32_t q = 0; q < st_value; ++q) op[kOpValueOff + q] = v;
+        }
+    }
+    if (opc_out && i < stride) opc_out[(int64_t)w * stride + i] = sb[(uint32_t)i * op_size + 8];
+    if (i < kCounters && tot[i]) {
+        unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + (w % kStripes) * 16;
+        atomicAdd(&stripe[i], tot[i]);
+    }
+    for (int k = i; k < 2 * kHotKeys; k += 256) hot[(int64_t)w * 2 * kHotKeys + k] = hp[k];
+    __syncthreads();
+    for (int k = i; k < words; k += 256) gslab[k] = slab[k];
+}
+
 // k_refill for big ops (312 B): staging a 78-KB slab per workgroup caps occupancy at two
 // workgroups per CU, so each thread edits its own op in place instead -- the same bytes as
 // k_refill (key, opcode, state, val_len, flags, and the value of a write), 8-B stores.
 __global__ __launch_bounds__(256) void k_refill_direct(uint8_t *ops, int32_t stride, uint32_t op_size,
                                                        uint32_t st_value, uint32_t shift, const uint64_t *tkey,
                                                        const uint8_t *top, int32_t tlen, uint32_t *cursor,
-                                                       uint32_t machine_id, int32_t first_iter, int32_t refill_all,
+                                                       uint32_t machine_id, int32_t first_iter, uint32_t rflags,
                                                        unsigned long long *counters, uint8_t *opc_out)
 {
+    const bool refill_all = (rflags & HKV_WL_REFILL_ALL) != 0;
     const int w = blockIdx.x, i = threadIdx.x;
     const bool live = i < stride;
     uint8_t *op = ops + ((int64_t)w * stride + (live ? i : 0)) * op_size;
@@ -271,7 +406,9 @@ __global__ __launch_bounds__(256) void k_refill_direct(uint8_t *ops, int32_t str
         // bytes 8..10 (opcode, state, val_len) of the second header word; 11..15 keep their bytes
         uint64_t *h1 = reinterpret_cast<uint64_t *>(op + 8);
         const uint64_t vl = oc == kOpGet ? 0 : (uint8_t)(st_value >> shift);
-        *h1 = (*h1 & ~0xFFFFFFull) | oc | ((uint64_t)kNew << 8) | (vl << 16);
+        // a GET's timestamp (bytes 11..15) is reset under HKV_WL_READ_TS_RESET (inline-util.h:268-272)
+        const uint64_t keep = oc == kOpGet && (rflags & HKV_WL_READ_TS_RESET) ? 0ull : ~0xFFFFFFull;
+        *h1 = (*h1 & keep) | oc | ((uint64_t)kNew << 8) | (vl << 16);
         if (oc == kOpGet) *reinterpret_cast<uint16_t *>(op + 16) = flags;
     }
     if (opc_out && live) opc_out[(int64_t)w * stride + i] = done ? oc : op[8];  // the opcode mirror
@@ -1110,24 +1247,33 @@ int hkv_wl_gen_trace(uint64_t *tkey, uint8_t *top, uint32_t *tid, int32_t n_work
 }
 
 int hkv_wl_refill(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint32_t st_value, uint32_t shift,
-                  const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor, uint32_t machine_id,
-                  int32_t first_iter, int32_t refill_all, unsigned long long *counters, uint8_t *opc_out,
-                  void *stream)
+                  const uint64_t *tkey, const uint8_t *top, const uint32_t *tid, int32_t tlen, uint32_t *cursor,
+                  uint32_t machine_id, int32_t first_iter, uint32_t flags, unsigned long long *counters,
+                  uint8_t *opc_out, uint8_t *hot, void *stream)
 {
-    if (stride > 256 || n_workers <= 0 || op_size % 8) return -1;
+    if (stride > 256 || n_workers <= 0 || op_size % 8 || tlen <= 0) return -1;
+    if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET | HKV_WL_COALESCE_HOT)) return -1;
+    const size_t lds = (size_t)stride * op_size;
+    if (flags & HKV_WL_COALESCE_HOT) {
+        // one 256-thread workgroup per worker, the slab and a slot index per pointer in LDS
+        if (!tid || !hot || stride > 255 || lds > 56 * 1024) return -1;
+        hipLaunchKernelGGL(k_refill_hot, dim3(n_workers), dim3(256), lds, (hipStream_t)stream, ops, stride, op_size,
+                           st_value, shift, tkey, top, tid, tlen, cursor, machine_id, first_iter, flags, counters,
+                           opc_out, hot);
+        return ok();
+    }
     if (op_size > 64 && st_value >= 6 && (kOpValueOff - 16 + st_value) / 8 + 7 <= 64) {  // big ops: in place
         hipLaunchKernelGGL(k_refill_direct, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
-                           st_value, shift, tkey, top, tlen, cursor, machine_id, first_iter, refill_all, counters,
+                           st_value, shift, tkey, top, tlen, cursor, machine_id, first_iter, flags, counters,
                            opc_out);
         return ok();
     }
-    const size_t lds = (size_t)stride * op_size;
     if (lds > 160 * 1024 - 64) return -1;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void *)k_refill, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return -1;
     hipLaunchKernelGGL(k_refill, dim3(n_workers), dim3(256), lds, (hipStream_t)stream, ops, stride, op_size, st_value,
-                       shift, tkey, top, tlen, cursor, machine_id, first_iter, refill_all, counters, opc_out);
+                       shift, tkey, top, tlen, cursor, machine_id, first_iter, flags, counters, opc_out);
     return ok();
 }
 

@@ -62,9 +62,14 @@ def hermes_batch_ops_to_KVS(btype: int, op_array: np.ndarray, op_num: int, sizeo
 # ---------------------------------------------------------------- tables
 def make_config(num_keys: int = 1_000_000, num_bkts: int = 2 * 1024 * 1024, log_cap: int = 1 << 30,
                 machine_id: int = 0, rmw: bool = False, big_objects: bool = False,
-                extra_cache_lines: int = 0, device: int = 0, rw_len: int = 250) -> HkvConfig:
-    return HkvConfig(ABI_VERSION, machine_id, int(rmw), int(big_objects), int(extra_cache_lines), device, rw_len, 0,
-                     num_keys, num_bkts, log_cap)
+                extra_cache_lines: int = 0, device: int = 0, rw_len: int = 250, skew: int = 0) -> HkvConfig:
+    """skew: hkv_config.skew_flags (SKEW_READ_COMPLETE | SKEW_WRITE_COALESCE, config.h:79-80)"""
+    return HkvConfig(ABI_VERSION, machine_id, int(rmw), int(big_objects), int(extra_cache_lines), device, rw_len,
+                     int(skew), num_keys, num_bkts, log_cap)
+
+
+SKEW_READ_COMPLETE = 1    # ENABLE_READ_COMPLETE_AFTER_VAL_RECV_OF_HOT_REQS (include/hermeskv.h)
+SKEW_WRITE_COALESCE = 2   # ENABLE_WRITE_COALESCE_TO_THE_SAME_KEY_IN_SAME_NODE
 
 
 def sized_geometry(num_keys: int, sizes: L.Sizes = L.DEFAULT) -> tuple[int, int]:
@@ -90,7 +95,7 @@ class HermesKV:
     def __init__(self, num_keys: int | None = 1_000_000, num_bkts: int | None = None,
                  log_cap: int | None = None, machine_id: int = 0, rmw: bool = False,
                  big_objects: bool = False, extra_cache_lines: int = 0, device: int = 0,
-                 rw_len: int = 250, populate: bool = True):
+                 rw_len: int = 250, populate: bool = True, skew: int = 0):
         self.sizes = L.Sizes(big_objects, extra_cache_lines if big_objects else 0)
         nk = num_keys or 0
         if num_bkts is None or log_cap is None:
@@ -98,7 +103,8 @@ class HermesKV:
             num_bkts = num_bkts or b
             log_cap = log_cap or c
         self.cfg = make_config(nk, num_bkts, log_cap, machine_id, rmw, big_objects,
-                               extra_cache_lines, device, rw_len)
+                               extra_cache_lines, device, rw_len, skew)
+        self.skew = int(skew)
         self.device = device
         self.machine_id = machine_id
         self.rmw = rmw
@@ -124,6 +130,7 @@ class HermesKV:
         self.sizes = L.Sizes(bool(self.cfg.big_objects), self.cfg.extra_cache_lines if self.cfg.big_objects else 0)
         self.device, self.machine_id = self.cfg.device, self.cfg.machine_id
         self.rmw, self.num_keys = bool(self.cfg.rmw_enabled), self.cfg.num_keys
+        self.skew = self.cfg.skew_flags
         return self
 
     def close(self) -> None:
@@ -138,6 +145,12 @@ class HermesKV:
             pass
 
     # -- setup
+    def set_skew(self, skew: int) -> None:
+        """hkv_table_set_skew: the table's skew optimisations from the next launch on"""
+        check(_L.hkv_table_set_skew(self.h, int(skew)), "hkv_table_set_skew")
+        self.cfg.skew_flags = int(skew)
+        self.skew = int(skew)
+
     def populate(self, n: int, val_len: int) -> None:
         check(_L.hkv_table_populate(self.h, int(n), int(val_len)), "hkv_table_populate")
 

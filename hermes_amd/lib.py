@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 HERE = os.path.dirname(os.path.abspath(__file__))
 # HKV_LIB: another build of the same library (A/B timing of two revisions in one GPU session)
 LIB_PATH = os.environ.get("HKV_LIB") or os.path.join(HERE, "libhermeskv.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
@@ -27,7 +27,7 @@ class HkvConfig(ctypes.Structure):
     _fields_ = [("abi_version", ctypes.c_uint32), ("machine_id", ctypes.c_uint32),
                 ("rmw_enabled", ctypes.c_uint32), ("big_objects", ctypes.c_uint32),
                 ("extra_cache_lines", ctypes.c_uint32), ("device", ctypes.c_int32),
-                ("rw_len", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("rw_len", ctypes.c_uint32), ("skew_flags", ctypes.c_uint32),
                 ("num_keys", ctypes.c_uint64), ("num_bkts", ctypes.c_uint64),
                 ("log_cap", ctypes.c_uint64)]
 
@@ -55,6 +55,7 @@ _L.hkv_table_create.argtypes = [ctypes.POINTER(HkvConfig), ctypes.POINTER(_P)]
 _L.hkv_table_destroy.argtypes = [_P]
 _L.hkv_table_populate.argtypes = [_P, ctypes.c_int64, ctypes.c_int]
 _L.hkv_table_config.argtypes = [_P, ctypes.POINTER(HkvConfig)]
+_L.hkv_table_set_skew.argtypes = [_P, ctypes.c_uint32]
 _L.hkv_batch_async.argtypes = [_P, ctypes.POINTER(HkvBatchDesc), _P]
 _L.hkv_sync.argtypes = [_P, _P]
 _L.hkv_copy_index.argtypes = [_P, _P, ctypes.c_uint64, ctypes.c_uint64]

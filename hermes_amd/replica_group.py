@@ -35,7 +35,7 @@ from . import layout as L
 from .kvs import HermesKV
 from .lib import check, raw
 from .hades import NO_VIEW, Hades, MajorityLost, exchange_views
-from .workload import HkvZipf, _ptr, _s, slots_per_worker  # noqa: F401 (re-exported)
+from .workload import HkvZipf, _ptr, _s, refill_flags, slots_per_worker  # noqa: F401 (re-exported)
 
 _L = raw()
 _P = ctypes.c_void_p
@@ -74,6 +74,7 @@ class ReplicaRound:
         self.ack_size = self.op if kvs.rmw else L.OP_META_SIZE
         self.mb = L.membership(world, rank)
         self.retry = retry_stalled
+        self.rflags = refill_flags(kvs, retry_stalled)
         self.C = slots or slots_per_worker(write_permille, rmw_permille)
         W, N, C = n_workers, world, self.C
         dev = torch.device("cuda", kvs.device)
@@ -139,8 +140,8 @@ class ReplicaRound:
         if self.failed:
             return
         check(_L.hkv_wl_refill(_ptr(self.ops), self.W, LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
-                               _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
-                               self.rank, int(first), int(not self.retry), _ptr(self.counters), _ptr(self.opcodes),
+                               _ptr(self.trace_key), _ptr(self.trace_op), None, self.trace_len, _ptr(self.cursor),
+                               self.rank, int(first), self.rflags, _ptr(self.counters), _ptr(self.opcodes), None,
                                _s()), "refill")
 
     def local(self):

@@ -32,7 +32,8 @@ class HkvZipf(ctypes.Structure):
 _L.hkv_wl_gen_trace.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(HkvZipf),
                                 ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, _P]
 _L.hkv_wl_refill.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
-                             _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P]
+                             _P, _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint32, _P, _P,
+                             _P, _P]
 _L.hkv_wl_fold_counters.argtypes = [_P, _P]
 _L.hkv_wl_marshal_invs.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_invs_cap.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
@@ -65,6 +66,24 @@ _L.hkv_wl_peer_locate.argtypes = [_P, _P, ctypes.c_int64, ctypes.c_uint32, _P, _
 _L.hkv_wl_peer_ts_at.argtypes = [_P, _P, _P, _P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_peer_ts_words.restype = ctypes.c_uint64
 _L.hkv_wl_peer_ts_words.argtypes = [_P]
+
+
+REFILL_ALL = 1      # hkv_wl_refill flags (include/hermeskv_workload.h)
+READ_TS_RESET = 2
+COALESCE_HOT = 4
+HOT_KEYS = 100      # COALESCE_N_HOTTEST_KEYS, config.h:78
+
+
+def refill_flags(kvs: HermesKV, retry: bool, coalesce_hot: bool = False) -> int:
+    """hkv_wl_refill flags for a policy: refill_ops' retry (the reference) or a fresh batch per
+    round; GET timestamps reset when the table completes stalled reads (the reference ties both to
+    ENABLE_READ_COMPLETE_AFTER_VAL_RECV_OF_HOT_REQS); hot-request coalescing on request."""
+    f = 0 if retry else REFILL_ALL
+    if kvs.skew & 1:   # SKEW_READ_COMPLETE
+        f |= READ_TS_RESET
+    if coalesce_hot:
+        f |= COALESCE_HOT
+    return f
 
 
 def slots_per_worker(write_permille: int, rmw_permille: int = 0, batch: int = 250) -> int:
@@ -111,7 +130,7 @@ class Round:
                  remote_per_peer: int = 50, trace_len: int = 8192, seed: int = 0x5EED,
                  virtual_peers: bool = True, max_steps: int = 64, retry_stalled: bool = False,
                  fit_ack_stride: bool = True, val_credits: int | None = None, pack_remote: bool = True,
-                 hades: bool = False):
+                 hades: bool = False, coalesce_hot: bool = False):
         self.kvs = kvs
         self.W = n_workers
         self.mb = membership
@@ -124,6 +143,8 @@ class Round:
         self.R = len(self.peers)
         self.virtual = virtual_peers
         self.retry = retry_stalled     # True: refill_ops semantics (stalled ops keep their slot)
+        self.coalesce_hot = coalesce_hot   # ENABLE_COALESCE_OF_HOT_REQS (refill_ops, inline-util.h:237-257)
+        self.rflags = refill_flags(kvs, retry_stalled, coalesce_hot)
         self.machine_id = kvs.machine_id
         dev = torch.device("cuda", kvs.device)
         W, S = n_workers, self.LOCAL
@@ -185,7 +206,10 @@ class Round:
         self.seed = seed
         self.trace_key = torch.empty(W * trace_len, dtype=torch.int64, device=dev)
         self.trace_op = torch.empty(W * trace_len, dtype=torch.uint8, device=dev)
-        check(_L.hkv_wl_gen_trace(_ptr(self.trace_key), _ptr(self.trace_op), None, W, trace_len,
+        # hot-request coalescing reads the trace's key ids and keeps its pointers per worker
+        self.trace_id = torch.empty(W * trace_len, dtype=torch.int32, device=dev) if coalesce_hot else None
+        self.hot = torch.full((W * 2 * HOT_KEYS,), 0xFF, dtype=torch.uint8, device=dev) if coalesce_hot else None
+        check(_L.hkv_wl_gen_trace(_ptr(self.trace_key), _ptr(self.trace_op), _ptr(self.trace_id), W, trace_len,
                                   ctypes.byref(zipf), write_permille, rmw_permille,
                                   ctypes.c_uint64(seed ^ (self.machine_id << 48)), _s()), "gen_trace")
         self.clock = 0
@@ -260,9 +284,9 @@ class Round:
     # -- pieces of one round
     def refill(self, first: bool = False):
         check(_L.hkv_wl_refill(_ptr(self.ops), self.W, self.LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
-                               _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
-                               self.machine_id, int(first), int(not self.retry), _ptr(self.counters),
-                               _ptr(self.opcodes), _s()),
+                               _ptr(self.trace_key), _ptr(self.trace_op), _ptr(self.trace_id), self.trace_len,
+                               _ptr(self.cursor), self.machine_id, int(first), self.rflags, _ptr(self.counters),
+                               _ptr(self.opcodes), _ptr(self.hot), _s()),
               "refill")
 
     def local_batch(self):

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HKV_ABI_VERSION 3
+#define HKV_ABI_VERSION 4
 
 /* ------------------------------------------------------------------ reference types
  * Declared here only when the reference's own spacetime.h has not been included; the
@@ -93,11 +93,26 @@ typedef struct hkv_config {
     uint32_t extra_cache_lines; /* EXTRA_CACHE_LINES (hrd.h:37) */
     int32_t  device;            /* HIP device ordinal */
     uint32_t rw_len;            /* elements of read_write_ops (max_batch_size, default 250) */
-    uint32_t reserved;
+    uint32_t skew_flags;        /* HKV_SKEW_*: the reference's opt-in skew optimisations (0 = off,
+                                   the reference's default configuration) */
     uint64_t num_keys;          /* SPACETIME_NUM_KEYS (spacetime.h:21) */
     uint64_t num_bkts;          /* SPACETIME_NUM_BKTS (spacetime.h:22), power of two <= 2^31 */
     uint64_t log_cap;           /* SPACETIME_LOG_CAP (spacetime.h:23), power of two */
 } hkv_config;
+
+/* hkv_config.skew_flags: the exec-side skew optimisations of config.h:77-80, compile-time
+ * switches in the reference and per table here. Both change only the op, never the key's meta.
+ *   HKV_SKEW_READ_COMPLETE   ENABLE_READ_COMPLETE_AFTER_VAL_RECV_OF_HOT_REQS (config.h:79,
+ *       hermesKV.c:224-238): a stalled GET records the key's timestamp the first time (its ts is
+ *       (0, 0) after a refill) and completes, without copying a value, once the key's version is
+ *       at least two above it (a write completed after the read was issued).
+ *   HKV_SKEW_WRITE_COALESCE  ENABLE_WRITE_COALESCE_TO_THE_SAME_KEY_IN_SAME_NODE (config.h:80,
+ *       hermesKV.c:196-221): a PUT stalling behind a local write records the key's version (16
+ *       bits) when its own ts.version is 0, and completes (PUT_COMPLETE, no INV) once the key's
+ *       version is at least two above it.
+ * The refill-side flag (ENABLE_COALESCE_OF_HOT_REQS) is hkv_wl_refill's. */
+#define HKV_SKEW_READ_COMPLETE  1u
+#define HKV_SKEW_WRITE_COALESCE 2u
 
 typedef struct hkv_table hkv_table;
 
@@ -144,6 +159,9 @@ int  hkv_table_destroy(hkv_table *t);
 /* spacetime_populate_fixed_len on the device (reverse id order, MICA slot rules) */
 int  hkv_table_populate(hkv_table *t, int64_t n, int val_len);
 int  hkv_table_config(const hkv_table *t, hkv_config *out);
+/* changes hkv_config.skew_flags of a table between launches (e.g. to time several policies on
+ * one table); ordered after the launches already enqueued on the table's streams by the caller */
+int  hkv_table_set_skew(hkv_table *t, uint32_t skew_flags);
 
 /* device-resident batch path, asynchronous on `stream` (NULL = the HIP null stream). One
  * stream at a time per table: launches share the table's round scratch (entry ids, stages,
@@ -168,6 +186,13 @@ void *hkv_device_log(hkv_table *t);
 /* default table used by the reference entry points */
 int  hkv_set_default_config(const hkv_config *cfg);
 hkv_table *hkv_default_table(void);
+
+/* test hooks of the host entry point's combining submit: with a hold of n, the caller that
+ * assembles the next launch first waits (up to 5 s) until n batches are queued, so a test can put
+ * batches from several threads into one launch in a known order; 0 (default) = no hold. queued =
+ * batches waiting in the default table's queue now. */
+int  hkv_debug_host_hold(int n_batches);
+int  hkv_debug_host_queued(void);
 
 /* synthetic workload helpers (device kernels) */
 /* keys_second[i] = CityHash128(&id_i, 4).second for ids[i] (mica_gen_keys, mica.c:149-165) */

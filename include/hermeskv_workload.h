@@ -47,10 +47,20 @@ int hkv_wl_gen_trace(uint64_t *d_trace_key, uint8_t *d_trace_op, uint32_t *d_tra
                      uint64_t seed, void *stream);
 
 /* refill_ops over n_workers buffers of `stride` ops (op_size bytes each). Slots that are
- * complete take the next trace command of their worker (all slots when first_iter). With
- * refill_all, stalled ops (GET/PUT/RMW stalls, ST_EMPTY, ST_NEW) are dropped instead of
- * retried and take a fresh command too; ops in flight (PUT/RMW/REPLAY_SUCCESS, IN_PROGRESS_*,
- * *_COMPLETE_SEND_VALS, membership change) always keep their slot.
+ * complete take the next trace command of their worker (all slots when first_iter); stalled ops
+ * keep their slot and are retried, as in the reference. flags (HKV_WL_*):
+ *   HKV_WL_REFILL_ALL    not the reference: stalled ops (GET/PUT/RMW stalls, ST_EMPTY, ST_NEW) are
+ *                        dropped (counted) and take a fresh command too; ops in flight
+ *                        (PUT/RMW/REPLAY_SUCCESS, IN_PROGRESS_*, *_COMPLETE_SEND_VALS, membership
+ *                        change) always keep their slot;
+ *   HKV_WL_READ_TS_RESET ENABLE_READ_COMPLETE_AFTER_VAL_RECV_OF_HOT_REQS (inline-util.h:268-272): a
+ *                        refilled GET's timestamp becomes (0, 0) (pairs with HKV_SKEW_READ_COMPLETE);
+ *   HKV_WL_COALESCE_HOT  ENABLE_COALESCE_OF_HOT_REQS (inline-util.h:237-257): GETs/PUTs on the 100
+ *                        hottest ids are absorbed into the worker's last op of that id and opcode
+ *                        (no_coales + 1; a completed op commits no_coales ops). Needs d_trace_id (the
+ *                        trace's key ids, rank = id) and d_hot (2 * 100 bytes per worker, 0xFF
+ *                        before the first refill: the n_hottest_keys_in_ops pointers as slot
+ *                        indexes, hermes_worker.c:394-399); op_size * stride <= 56 KiB.
  * Counts completed-and-committed ops (everything complete except ST_MISS and ST_RMW_ABORT),
  * misses, completed writes, dropped stalled ops and RMW aborts (ST_RMW_ABORT) into
  * d_counters: HKV_WL_COUNTER_WORDS words, zeroed by the caller once, of which the words from
@@ -60,10 +70,14 @@ int hkv_wl_gen_trace(uint64_t *d_trace_key, uint8_t *d_trace_op, uint32_t *d_tra
  * the mirror hkv_batch_desc.d_opcode_in takes. */
 #define HKV_WL_COUNTER_WORDS 4096
 #define HKV_WL_STRIPE_BASE 64
+#define HKV_WL_REFILL_ALL    1u
+#define HKV_WL_READ_TS_RESET 2u
+#define HKV_WL_COALESCE_HOT  4u
+#define HKV_WL_HOT_KEYS      100
 int hkv_wl_refill(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint32_t st_value,
-                  uint32_t shift, const uint64_t *d_trace_key, const uint8_t *d_trace_op, int32_t trace_len,
-                  uint32_t *d_cursor, uint32_t machine_id, int32_t first_iter, int32_t refill_all,
-                  unsigned long long *d_counters, uint8_t *d_opcode_out, void *stream);
+                  uint32_t shift, const uint64_t *d_trace_key, const uint8_t *d_trace_op, const uint32_t *d_trace_id,
+                  int32_t trace_len, uint32_t *d_cursor, uint32_t machine_id, int32_t first_iter, uint32_t flags,
+                  unsigned long long *d_counters, uint8_t *d_opcode_out, uint8_t *d_hot, void *stream);
 /* d_counters[0..4] += the refill stripes (which are cleared) */
 int hkv_wl_fold_counters(unsigned long long *d_counters, void *stream);
 

@@ -39,7 +39,8 @@ class TableSnapshot:
         L.hko_set_log_head.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         c = kvs.cfg
         self.c = c
-        self.cfg = Config(c.big_objects, c.extra_cache_lines, c.rmw_enabled, c.machine_id, c.num_bkts, c.log_cap)
+        self.cfg = Config(c.big_objects, c.extra_cache_lines, c.rmw_enabled, c.machine_id, c.num_bkts, c.log_cap,
+                          c.skew_flags, 0)
         self.h = L.hko_create(ctypes.byref(self.cfg))
         from hermes_amd.lib import check, raw
         R = raw()
@@ -56,11 +57,12 @@ class TableSnapshot:
 
 
 def run_cpu_baseline(kvs, zipf, write_permille: int, workers: int, seconds: float, seed: int,
-                     n_peers: int = 2, per_peer: int = 50, refill_all: bool = True, threads: int = 0,
+                     n_peers: int = 2, per_peer: int = 50, refill_flags: int = 1, threads: int = 0,
                      snapshot: TableSnapshot | None = None) -> dict:
     """threads = 0: one per usable core (host_threads()); workers = 0: one 250-op buffer per thread,
-    as the reference's workers (main.c:193-210). snapshot: a TableSnapshot taken earlier (consumed);
-    default: the table as it is now."""
+    as the reference's workers (main.c:193-210). refill_flags: hkv_wl_refill's (1 fresh batches, 2
+    GET timestamps reset, 4 hot-request coalescing; 0 = refill_ops' retry). The table's skew flags
+    come with it. snapshot: a TableSnapshot taken earlier (consumed); default: the table as it is now."""
     snap = snapshot if snapshot is not None else TableSnapshot(kvs)
     L, h, cfg, c = snap.L, snap.h, snap.cfg, snap.c
     threads = threads or host_threads()
@@ -74,13 +76,14 @@ def run_cpu_baseline(kvs, zipf, write_permille: int, workers: int, seconds: floa
         hz = HkoZipf(zipf.theta, zipf.zetan, zipf.alpha, zipf.eta, zipf.half_pow, zipf.n)
         rounds, secs = ctypes.c_int64(0), ctypes.c_double(0.0)
         committed = L.hko_bench_rounds(h, ctypes.byref(cfg), workers, threads, seconds, ctypes.byref(hz),
-                                       write_permille, n_peers, per_peer, seed, int(refill_all), ctypes.byref(rounds),
+                                       write_permille, n_peers, per_peer, seed, int(refill_flags), ctypes.byref(rounds),
                                        ctypes.byref(secs))
     finally:
         snap.close()
     return {"value": committed / secs.value, "unit": "ops/s", "cores": threads, "kind": "port",
             "sample": (f"{threads} worker threads sharing one table (per-key seqlocks, concur_ctrl.h:144-224), "
-                       f"{workers} x 250-op {'fresh' if refill_all else 'refilled'} local batches per round, "
+                       f"{workers} x 250-op {'fresh' if refill_flags & 1 else 'retried (refill_ops)'} local batches "
+                       f"per round, refill flags {refill_flags}, skew flags {c.skew_flags}, "
                        f">= {rounds.value} rounds each in {secs.value:.1f} s; +{n_peers} virtual peers (one write per "
                        f"key and round each, live timestamps, up to {per_peer} per worker-round), 2 ACKs per write; "
                        f"same table ({c.num_bkts} buckets, copied from HBM) and Zipf/write mix as the GPU run")}

@@ -320,6 +320,39 @@ static void read_into_op(hko_kvs *kv, uint8_t *op, uint8_t *entry)
     O_VALLEN(op) = get_val_len(kv, entry);
 }
 
+/* ---------------------------------------------------------------- skew optimisations (config.h:77-80) */
+#define SKEW_READ_COMPLETE 1u
+#define SKEW_WRITE_COALESCE 2u
+
+/* hermes_complete_hot_read_optimization, hermesKV.c:224-238 */
+static void hot_read_complete(uint8_t *op, uint32_t ts_ver, uint8_t ts_cid)
+{
+    if (O_STATE(op) != R_GET_STALL) return;
+    if (O_TSVER(op) == 0 && O_TSCID(op) == 0) {   /* first stall: remember the timestamp */
+        O_SET_TSVER(op, ts_ver);
+        O_TSCID(op) = ts_cid;
+    } else if (O_TSVER(op) + 1u < ts_ver) {      /* two versions later: complete (no value copied) */
+        O_STATE(op) = R_GET_COMPLETE;
+    }
+}
+
+/* hermes_marshal_write_coalesce_optimization, hermesKV.c:196-206 (the IN_PROGRESS_PUT it sets is
+ * overwritten with PUT_STALL by its caller) */
+static void write_coalesce_mark(hko_kvs *kv, uint8_t *op, uint16_t curr_version)
+{
+    if ((kv->cfg.skew_flags & SKEW_WRITE_COALESCE) && O_TSVER(op) == 0) {
+        O_SET_TSVER(op, curr_version);
+        O_STATE(op) = B_IN_PROGRESS_PUT;
+    }
+}
+
+/* hermes_complete_coalesced_write, hermesKV.c:208-221 */
+static void write_coalesce_complete(hko_kvs *kv, uint8_t *op, uint16_t curr_ts)
+{
+    if ((kv->cfg.skew_flags & SKEW_WRITE_COALESCE) && O_STATE(op) == R_PUT_STALL)
+        if (O_TSVER(op) > 0 && O_TSVER(op) + 1u < (uint32_t)curr_ts) O_STATE(op) = R_PUT_COMPLETE;
+}
+
 /* ---------------------------------------------------------------- exec functions */
 /* hermes_exec_read, hermesKV.c:251-311: a lock-free pass (copy the meta, act on the live state,
  * validate the copy's timestamp afterwards), or a locked one for INVALID keys */
@@ -328,15 +361,21 @@ static void ex_read(hko_kvs *kv, uint8_t *op, uint8_t *entry, uint8_t idx, const
     uint8_t *m = entry + ENTRY_META_OFF;
     uint8_t prev[OBJ_META_SIZE];
     int locked = 0;
+    uint32_t cur_ver;
+    uint8_t cur_cid;
     O_STATE(op) = B_EMPTY;
     do {
         racy_copy(prev, m, OBJ_META_SIZE);
+        cur_ver = M_TSVER(prev);
+        cur_cid = M_TSCID(prev);
         switch (__atomic_load_n(m, __ATOMIC_ACQUIRE)) {
         case S_VALID: read_into_op(kv, op, entry); break;
         case S_INVALID_WRITE: case S_WRITE: case S_REPLAY: O_STATE(op) = R_GET_STALL; break;
         default:
             locked = 1;
             cc_lock(m);
+            cur_ver = M_TSVER(m) - 1;   /* "when locking we do version++" */
+            cur_cid = M_TSCID(m);
             switch (M_STATE(m)) {
             case S_VALID: read_into_op(kv, op, entry); break;
             case S_INVALID_WRITE: case S_WRITE: case S_REPLAY: O_STATE(op) = R_GET_STALL; break;
@@ -347,25 +386,36 @@ static void ex_read(hko_kvs *kv, uint8_t *op, uint8_t *entry, uint8_t idx, const
             break;
         }
     } while (!snap_valid(prev, m) && !locked);
+    if (kv->cfg.skew_flags & SKEW_READ_COMPLETE) hot_read_complete(op, cur_ver, cur_cid);
 }
 
-/* hermes_exec_write, hermesKV.c:314-356 (write coalescing disabled, config.h:80) */
+/* hermes_exec_write, hermesKV.c:314-356 */
 static void ex_write(hko_kvs *kv, uint8_t *op, uint8_t *entry, uint8_t idx, const uint8_t *mb)
 {
     uint8_t *m = entry + ENTRY_META_OFF;
     O_STATE(op) = B_EMPTY;
     cc_lock(m);
+    const uint16_t curr_version = (uint16_t)(M_TSVER(m) - 1);
     switch (M_STATE(m)) {
     case S_VALID: case S_INVALID:
-        if (M_OBI(m) != OBI_EMPTY) cc_unlock_dec(m);
-        else update_and_unlock(kv, op, entry, idx, mb, 0);
+        if (M_OBI(m) != OBI_EMPTY) {
+            cc_unlock_dec(m);
+            write_coalesce_mark(kv, op, curr_version);
+        } else {
+            update_and_unlock(kv, op, entry, idx, mb, 0);
+        }
         break;
-    case S_INVALID_WRITE: case S_WRITE: case S_REPLAY:
+    case S_INVALID_WRITE: case S_WRITE:
+        write_coalesce_mark(kv, op, curr_version);
+        cc_unlock_dec(m);
+        break;
+    case S_REPLAY:
         cc_unlock_dec(m);
         break;
     default: break;
     }
     if (O_STATE(op) != R_PUT_SUCCESS) O_STATE(op) = R_PUT_STALL;
+    write_coalesce_complete(kv, op, curr_version);
 }
 
 /* hermes_exec_rmw, hermesKV.c:358-428 */

@@ -49,6 +49,9 @@ typedef struct hko_config {
     uint32_t machine_id;        /* global machine_id (hrd.h:87) */
     uint64_t num_bkts;          /* SPACETIME_NUM_BKTS (spacetime.h:22), power of two */
     uint64_t log_cap;           /* SPACETIME_LOG_CAP (spacetime.h:23), power of two */
+    uint32_t skew_flags;        /* bit 0: ENABLE_READ_COMPLETE_AFTER_VAL_RECV_OF_HOT_REQS (config.h:79),
+                                   bit 1: ENABLE_WRITE_COALESCE_TO_THE_SAME_KEY_IN_SAME_NODE (config.h:80) */
+    uint32_t pad;
 } hko_config;
 
 typedef struct hko_kvs hko_kvs;

@@ -8,8 +8,12 @@
  * ACKs from the virtual peers -> incoming INV batch -> ACK batch (rw = the worker's ops) ->
  * VAL marshal -> incoming VAL batch. Traces and peer INV/VAL slabs are generated before the
  * timed loop with the same generators (splitmix64 streams, Gray/YCSB Zipf, CityHash keys).
- * refill_all = 1 gives every worker a fresh batch each round (bench.py's default), 0 keeps
- * stalled ops in their slots as refill_ops does.
+ * refill flags (hkv_wl_refill's): 1 gives every worker a fresh batch each round (stalled ops
+ * dropped), else stalled ops keep their slots as refill_ops does; 2 resets a refilled GET's
+ * timestamp (ENABLE_READ_COMPLETE_AFTER_VAL_RECV_OF_HOT_REQS, inline-util.h:268-272); 4 coalesces
+ * requests on the 100 hottest ids into the worker's live op of that id and opcode
+ * (ENABLE_COALESCE_OF_HOT_REQS, inline-util.h:237-257; committed ops count no_coales each).
+ * The table's skew_flags (hko_config) select the exec-side optimisations.
  */
 #include <math.h>
 #include <pthread.h>
@@ -66,11 +70,13 @@ enum { BS = 250, BT = 8192, BP = 16 };   /* local batch, trace length, peer roun
 typedef struct {
     hko_kvs *kv;
     uint32_t osz, sv;
-    int n_peers, per_peer, rstride, refill_all;
+    int n_peers, per_peer, rstride, refill_all, ts_reset, coalesce;
     uint8_t mid;
     uint8_t *ops;
+    uint8_t *hot;   /* [n_workers][200]: n_hottest_keys_in_ops_get / _put as slot indexes, 255 = NULL */
     const uint64_t *tkey;
     const uint8_t *top;
+    const uint32_t *tid;
     uint32_t *cursor;
     const uint8_t *rinv_pool, *rval_pool;
     const int32_t *rcount;
@@ -107,6 +113,7 @@ static void *bench_worker(void *arg)
         for (int w = b->w0; w < b->w1; w++) {
             uint8_t *ow = b->ops + (size_t)w * S * osz;
             /* refill_ops (inline-util.h:149-303) */
+            uint8_t *hp = b->hot + (size_t)w * 200;
             for (int i = 0; i < S; i++) {
                 uint8_t *o = ow + (size_t)i * osz;
                 uint8_t st = o[9];
@@ -114,16 +121,40 @@ static void *bench_worker(void *arg)
                 /* in flight: PUT/RMW/REPLAY_SUCCESS, IN_PROGRESS_*, *_COMPLETE_SEND_VALS, membership change */
                 int in_flight = st == 122 || st == 135 || st == 123 || st == 143 || st == 148 || st == 144 ||
                                 st == 133 || st == 149 || st == 147 || st == 118;
-                if (!first && complete && st != 130 && st != 138) committed++;
+                if (!first && complete && st != 130 && st != 138)
+                    committed += b->coalesce ? (int64_t)((o[16] | o[17] << 8) >> 1) : 1;
                 /* stalled ops retry unless refill_all; ops in flight always keep their slot */
                 if (!(first || complete || (b->refill_all && !in_flight))) continue;
+                if (!first) o[8] = o[9] = 140;   /* reset op bucket */
                 int64_t ti = (int64_t)w * BT + b->cursor[w];
+                if (b->coalesce && b->top[ti] != 113) {   /* a hot command joins the worker's live op */
+                    uint32_t id;
+                    int col;
+                    for (;;) {
+                        ti = (int64_t)w * BT + b->cursor[w];
+                        id = b->tid[ti];
+                        col = b->top[ti] == OPC_GET ? 0 : 100;
+                        if (id < 100 && hp[col + id] != 255 && ow[(size_t)hp[col + id] * osz + 8] == b->top[ti]) {
+                            uint8_t *t = ow + (size_t)hp[col + id] * osz;
+                            uint16_t v = (uint16_t)(t[16] | t[17] << 8);
+                            v = (uint16_t)((v & 1u) | ((((v >> 1) + 1u) & 0x7FFFu) << 1));
+                            t[16] = (uint8_t)v;
+                            t[17] = (uint8_t)(v >> 8);
+                            b->cursor[w] = (b->cursor[w] + 1) % BT;
+                        } else {
+                            break;
+                        }
+                    }
+                    if (id < 100) hp[col + id] = (uint8_t)i;
+                }
+                ti = (int64_t)w * BT + b->cursor[w];
                 b->cursor[w] = (b->cursor[w] + 1) % BT;
                 memcpy(o, &b->tkey[ti], 8);
                 o[8] = b->top[ti];
                 o[9] = 141;
                 o[10] = b->top[ti] == OPC_GET ? 0 : (uint8_t)sv;
-                o[16] = 0;
+                if (b->top[ti] == OPC_GET && b->ts_reset) memset(o + 11, 0, 5);
+                o[16] = first ? 0 : 2;   /* no_coales = 1 (not reset on the first pass), RMW_flag 0 */
                 o[17] = 0;
                 if (b->top[ti] != OPC_GET) memset(o + 18, 'a' + mid, sv);
             }
@@ -181,8 +212,8 @@ static void *bench_worker(void *arg)
     }
     /* harvest the last round's completions (counted by the next refill in the reference) */
     for (int64_t i = (int64_t)b->w0 * S; i < (int64_t)b->w1 * S; i++) {
-        uint8_t st = b->ops[i * osz + 9];
-        if (st == 128 || st == 121 || st == 137) committed++;
+        const uint8_t *o = b->ops + i * osz;
+        if (o[9] == 128 || o[9] == 121 || o[9] == 137) committed += b->coalesce ? (int64_t)((o[16] | o[17] << 8) >> 1) : 1;
     }
     b->committed = committed;
     b->rounds = rounds;
@@ -195,7 +226,7 @@ static void *bench_worker(void *arg)
  * slowest thread's) through out-params */
 int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, int n_threads, double seconds,
                          const hko_zipf *z, uint32_t write_pm, int n_peers, int per_peer, uint64_t seed,
-                         int refill_all, int64_t *out_rounds, double *out_secs)
+                         int refill_flags, int64_t *out_rounds, double *out_secs)
 {
     const int T = BT, P = BP;
     const uint32_t osz = hko_op_size(cfg), sv = hko_st_value_size(cfg);
@@ -207,6 +238,9 @@ int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, int 
     uint8_t *rval_pool = calloc((size_t)n_workers * P * (rstride ? rstride : 1), 16);
     uint64_t *tkey = malloc(sizeof(uint64_t) * (size_t)n_workers * T);
     uint8_t *top = malloc((size_t)n_workers * T);
+    uint32_t *tid = malloc(sizeof(uint32_t) * (size_t)n_workers * T);
+    uint8_t *hot = malloc((size_t)n_workers * 200);
+    memset(hot, 255, (size_t)n_workers * 200);
     uint32_t *cursor = calloc(n_workers, 4);
     const uint8_t mid = (uint8_t)cfg->machine_id;
     /* traces (create_uni_trace / parse_trace shape) */
@@ -214,6 +248,7 @@ int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, int 
         uint64_t r1 = sm64(seed ^ (0x1000003ull * (uint64_t)g)), r2 = sm64(r1 ^ 0x5EEDull);
         uint32_t id = (uint32_t)zipf_draw(z, (double)(r1 >> 11) * (1.0 / 9007199254740992.0));
         tkey[g] = key_of(id);
+        tid[g] = id;
         top[g] = (uint32_t)(r2 % 1000u) < write_pm ? OPC_PUT : OPC_GET;
     }
     /* peer INVs + VALs, P round indices deep: per round, each virtual peer's first write of a key
@@ -269,24 +304,25 @@ int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, int 
     pthread_barrier_t start;
     pthread_barrier_init(&start, NULL, (unsigned)n_threads + 1);
     bench_thread *th = calloc((size_t)n_threads, sizeof(bench_thread));
-    pthread_t *tid = calloc((size_t)n_threads, sizeof(pthread_t));
+    pthread_t *thr = calloc((size_t)n_threads, sizeof(pthread_t));
     double t0 = 0;
     for (int k = 0; k < n_threads; k++) {
         bench_thread *b = &th[k];
         b->kv = kv; b->osz = osz; b->sv = sv; b->n_peers = n_peers; b->per_peer = per_peer; b->rstride = rstride;
-        b->refill_all = refill_all; b->mid = mid; b->ops = ops; b->tkey = tkey; b->top = top; b->cursor = cursor;
+        b->refill_all = refill_flags & 1; b->ts_reset = (refill_flags & 2) != 0; b->coalesce = (refill_flags & 4) != 0;
+        b->mid = mid; b->ops = ops; b->hot = hot; b->tkey = tkey; b->top = top; b->tid = tid; b->cursor = cursor;
         b->rinv_pool = rinv_pool; b->rval_pool = rval_pool; b->rcount = rcount; b->n_workers = n_workers;
         b->w0 = (int)((int64_t)n_workers * k / n_threads);
         b->w1 = (int)((int64_t)n_workers * (k + 1) / n_threads);
         b->seconds = seconds; b->start = &start; b->t0 = &t0;
-        pthread_create(&tid[k], NULL, bench_worker, b);
+        pthread_create(&thr[k], NULL, bench_worker, b);
     }
     t0 = now_s();
     pthread_barrier_wait(&start);
     int64_t committed = 0, rounds = -1;
     double t_end = t0;
     for (int k = 0; k < n_threads; k++) {
-        pthread_join(tid[k], NULL);
+        pthread_join(thr[k], NULL);
         committed += th[k].committed;
         if (rounds < 0 || th[k].rounds < rounds) rounds = th[k].rounds;
         if (th[k].t_end > t_end) t_end = th[k].t_end;
@@ -294,7 +330,7 @@ int64_t hko_bench_rounds(hko_kvs *kv, const hko_config *cfg, int n_workers, int 
     pthread_barrier_destroy(&start);
     *out_rounds = rounds;
     *out_secs = t_end - t0;
-    free(th); free(tid);
-    free(ops); free(rinv_pool); free(rval_pool); free(tkey); free(top); free(cursor); free(rcount);
+    free(th); free(thr);
+    free(ops); free(rinv_pool); free(rval_pool); free(tkey); free(top); free(tid); free(hot); free(cursor); free(rcount);
     return committed;
 }

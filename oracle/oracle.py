@@ -19,7 +19,8 @@ CITY_REF_PATH = os.path.join(HERE, "_ref", "libcity_ref.so")
 class Config(ctypes.Structure):
     _fields_ = [("big_objects", ctypes.c_uint32), ("extra_cache_lines", ctypes.c_uint32),
                 ("rmw_enabled", ctypes.c_uint32), ("machine_id", ctypes.c_uint32),
-                ("num_bkts", ctypes.c_uint64), ("log_cap", ctypes.c_uint64)]
+                ("num_bkts", ctypes.c_uint64), ("log_cap", ctypes.c_uint64),
+                ("skew_flags", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
 
 def build(force: bool = False) -> None:
@@ -85,8 +86,10 @@ class OracleKVS:
     """One MICA-herd/HermesKV table on the host, driven exactly like the reference."""
 
     def __init__(self, num_bkts: int, log_cap: int, machine_id: int = 0, rmw: bool = False,
-                 big_objects: bool = False, extra_cache_lines: int = 0):
-        self.cfg = Config(int(big_objects), int(extra_cache_lines), int(rmw), machine_id, num_bkts, log_cap)
+                 big_objects: bool = False, extra_cache_lines: int = 0, skew: int = 0):
+        """skew: hko_config.skew_flags (bit 0 read completion, bit 1 write coalescing, config.h:79-80)"""
+        self.cfg = Config(int(big_objects), int(extra_cache_lines), int(rmw), machine_id, num_bkts, log_cap,
+                          int(skew), 0)
         self.h = lib().hko_create(ctypes.byref(self.cfg))
         self.num_bkts, self.log_cap = num_bkts, log_cap
 

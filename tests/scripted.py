@@ -202,3 +202,89 @@ def required_outcomes(rmw: bool) -> set:
         req |= {(0, R.RMW_SUCCESS), (0, R.RMW_STALL), (0, R.RMW_ABORT), (0, B.EMPTY), (1, R.RMW_COMPLETE),
                 (1, B.RMW_COMPLETE_SEND_VALS), (2, R.OP_INV_ABORT), ("rw", R.RMW_COMPLETE)}
     return {(a, int(b)) for a, b in req}
+
+
+# ---------------------------------------------------------------- skew optimisations
+SK = {"hot": 500, "rep": 507, "trunc": 514}
+
+
+def _sk_ops(sizes, rows, keys):
+    """rows: (key name, opcode, (ts_ver, ts_cid)); state NEW"""
+    a = np.zeros(len(rows), dtype=L.op_dtype(sizes))
+    for i, (name, oc, ts) in enumerate(rows):
+        a[i]["key"] = keys[SK[name]]
+        a[i]["opcode"] = int(oc)
+        a[i]["state"] = int(B.NEW)
+        a[i]["ts_ver"], a[i]["ts_cid"] = ts
+        if oc == O.PUT:
+            a[i]["value"][:] = ord("p") + i
+            a[i]["val_len"] = sizes.st_value >> sizes.shift
+    return a
+
+
+def run_scripted_skew(runner, keys, sizes) -> set:
+    """The reference's skew optimisations (skew_flags 3: ENABLE_READ_COMPLETE_AFTER_VAL_RECV_OF_HOT_REQS
+    and ENABLE_WRITE_COALESCE_TO_THE_SAME_KEY_IN_SAME_NODE, config.h:79-80) on a 3-machine group,
+    outcomes written out from hermesKV.c:196-356: a stalled GET records the key's timestamp when its
+    own is (0, 0) and completes once the version is two above it; a stalled PUT records the key's
+    version (16 bits) when its own version is 0 -- not in REPLAY -- and completes (PUT_COMPLETE) once
+    that 16-bit version is two above its own. Returns (batch type, code) outcomes."""
+    seen = set()
+    mb = L.membership(3, 0)
+    # ---- 1. local: the first PUT of `hot` writes (2, 0); the rest stall behind it
+    l1 = _sk_ops(sizes, [("hot", O.PUT, (0, 0)), ("hot", O.GET, (0, 0)), ("hot", O.PUT, (0, 0)),
+                         ("hot", O.PUT, (1, 0)), ("hot", O.GET, (0, 7)), ("trunc", O.PUT, (0, 0))], keys)
+    runner(L.BatchType.local_ops, l1, mb)
+    _check("skew local 1", l1["state"], [R.PUT_SUCCESS, R.GET_STALL, R.PUT_STALL, R.PUT_STALL, R.GET_COMPLETE,
+                                         R.PUT_SUCCESS])
+    _check("skew local 1 ts", l1["ts_ver"], [2, 2, 2, 1, 0, 2])
+    _check("skew local 1 cid", l1["ts_cid"][:2], [0, 0])   # the GET recorded the key's (2, 0)
+    seen |= {(0, int(x)) for x in l1["state"]}
+    l1["state"][l1["state"] == R.PUT_SUCCESS] = B.IN_PROGRESS_PUT
+    # ---- 2. INVs: peer 1 beats hot's write; rep is written by node 4 (not a member); trunc jumps
+    #         past 2^16 (its version's low 16 bits are 4)
+    inv = np.zeros(3, dtype=L.op_dtype(sizes))
+    for i, (name, snd, ts) in enumerate([("hot", 1, (2, 1)), ("rep", 4, (2, 4)), ("trunc", 1, (0x10004, 1))]):
+        inv[i]["key"] = keys[SK[name]]
+        inv[i]["opcode"] = int(O.INV)
+        inv[i]["state"] = snd
+        inv[i]["ts_ver"], inv[i]["ts_cid"] = ts
+        inv[i]["val_len"] = sizes.st_value >> sizes.shift
+        inv[i]["value"][:] = ord("I") + i
+    runner(L.BatchType.invs, inv, mb)
+    _check("skew invs", inv["opcode"], [R.INV_SUCCESS] * 3)
+    # ---- 3. ACKs of hot's write: completes (INVALID_WRITE -> INVALID)
+    a = np.zeros(2, dtype=L.msg_dtype())
+    a["key"] = keys[SK["hot"]]
+    a["opcode"] = int(O.ACK)
+    a["sender"] = [1, 2]
+    a["ts_ver"], a["ts_cid"] = 2, 0
+    runner(L.BatchType.acks, a, mb, rw=l1)
+    _check("skew acks", a["opcode"], [R.ACK_SUCCESS] * 2)
+    assert int(l1["state"][0]) == R.PUT_COMPLETE
+    # ---- 4. retries and new ops: hot is INVALID (writer 1 alive) at (2, 1), rep INVALID (writer 4
+    #         gone), trunc INVALID_WRITE at (0x10004, 1)
+    l2 = _sk_ops(sizes, [("hot", O.GET, (2, 0)),      # INVALID, writer alive: stalls, 3 < 2 no
+                         ("hot", O.PUT, (2, 0)),      # INVALID, no write in flight: writes (4, 0)
+                         ("hot", O.PUT, (1, 0)),      # WRITE: 2 < 4 -> coalesced, PUT_COMPLETE
+                         ("hot", O.GET, (2, 0)),      # WRITE: 3 < 4 -> GET_COMPLETE
+                         ("hot", O.GET, (0, 0)),      # WRITE: records (4, 0)
+                         ("hot", O.PUT, (0, 0)),      # WRITE: records 4
+                         ("rep", O.GET, (0, 0)),      # write replay (REPLAY_SUCCESS, ts (2, 4))
+                         ("rep", O.PUT, (0, 0)),      # REPLAY: no record, stays 0
+                         ("rep", O.GET, (0, 0)),      # REPLAY: records (2, 4)
+                         ("rep", O.PUT, (3, 0)),      # REPLAY: 4 < 2 no
+                         ("trunc", O.PUT, (0, 0)),    # INVALID_WRITE: records 0x10004 & 0xFFFF = 4
+                         ("trunc", O.PUT, (5, 0)),    # 6 < 4 (16 bits) no
+                         ("trunc", O.PUT, (1, 0)),    # 2 < 4 -> PUT_COMPLETE
+                         ("trunc", O.GET, (0, 0)),    # records (0x10004, 1)
+                         ("trunc", O.GET, (5, 0))],   # reads compare 32 bits: 6 < 0x10004 -> complete
+                 keys)
+    runner(L.BatchType.local_ops, l2, mb)
+    _check("skew local 2", l2["state"], [R.GET_STALL, R.PUT_SUCCESS, R.PUT_COMPLETE, R.GET_COMPLETE, R.GET_STALL,
+                                         R.PUT_STALL, R.REPLAY_SUCCESS, R.PUT_STALL, R.GET_STALL, R.PUT_STALL,
+                                         R.PUT_STALL, R.PUT_STALL, R.PUT_COMPLETE, R.GET_STALL, R.GET_COMPLETE])
+    _check("skew local 2 ts", l2["ts_ver"], [2, 4, 1, 2, 4, 4, 2, 0, 2, 3, 4, 5, 1, 0x10004, 5])
+    _check("skew local 2 cid", l2["ts_cid"][[4, 6, 8, 13]], [0, 4, 4, 1])
+    seen |= {(0, int(x)) for x in l2["state"]}
+    return seen

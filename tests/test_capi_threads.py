@@ -3,6 +3,8 @@
 
 * tools/capi_known_answers: the SURVEY section 4 known-answer scenario through spacetime_init +
   hermes_batch_ops_to_KVS (the by-value membership ABI of a gcc caller).
+* tools/capi_threads shared: batches of several types on shared keys, combined into one launch
+  in a known order and replayed on the oracle in that order.
 * tools/capi_threads: 8 worker threads calling hermes_batch_ops_to_KVS concurrently on one table
   (main.c:193-210), their batches combined into shared launches by the library. Threads use
   disjoint keys, so any interleaving gives every key the same history: each thread's recorded
@@ -88,6 +90,42 @@ def test_concurrent_callers_match_oracle(tmp_path):
             if t == int(L.BatchType.local_ops):
                 n_put += int((eout.reshape(n, esz)[:, 9] == int(L.Resp.PUT_SUCCESS)).sum())
     assert n_put > 0
+
+
+def test_mixed_batches_on_shared_keys_match_oracle(tmp_path):
+    """Five gcc-built threads on 32 shared keys, their batches of four types combined into one
+    launch per round in thread order (hkv_debug_host_hold): local ops, INVs, the ACKs of the
+    previous round's writes (with read_write_ops), VALs, local ops. So one single-workgroup launch
+    applies an INV, a local PUT and an ACK completing an earlier write to the same key, each
+    batch under its own header (membership, read_write_ops). Replayed on the oracle round by
+    round in thread order, every call's elements and read_write_ops must match byte for byte."""
+    rounds = 20
+    p = subprocess.run([os.path.join(TOOLS, "capi_threads"), "shared", str(rounds), str(tmp_path)],
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout + p.stderr
+    o = OracleKVS(1 << 21, 1 << 30, machine_id=0)
+    o.populate(1_000_000, L.DEFAULT.kvs_value)
+    mb = L.membership(3, 0)
+    calls = [_read_calls(os.path.join(tmp_path, f"thread{k}.bin")) for k in range(5)]
+    assert all(len(c) == rounds for c in calls)
+    seen = set()
+    for r in range(rounds):
+        for k in range(5):
+            t, n, esz, ein, eout, rin, rout = calls[k][r]
+            e = ein.view(np.dtype((np.void, esz))).copy()
+            rw = rin.view(np.dtype((np.void, 56))).copy() if rin is not None else None
+            o.batch(t, e, mb, rw=rw)
+            assert np.array_equal(e.view(np.uint8), eout), f"round {r} thread {k} (type {t}): elements differ"
+            if rw is not None:
+                assert np.array_equal(rw.view(np.uint8), rout), f"round {r} thread {k}: read_write_ops differ"
+            out = eout.reshape(n, esz)
+            seen.update((t, int(c)) for c in out[:, 9 if t == int(L.BatchType.local_ops) else 8])
+    # the mix did what it is for: writes completed by ACKs in the same launch as new local ops, INVs
+    # that raised keys written locally, VALs that validated them
+    assert (int(L.BatchType.acks), int(L.Resp.LAST_ACK_SUCCESS)) in seen, sorted(seen)
+    assert (int(L.BatchType.local_ops), int(L.Resp.PUT_SUCCESS)) in seen
+    assert (int(L.BatchType.local_ops), int(L.Resp.GET_STALL)) in seen
+    assert (int(L.BatchType.invs), int(L.Resp.INV_SUCCESS)) in seen
 
 
 def test_concurrent_callers_throughput():

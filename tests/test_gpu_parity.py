@@ -38,11 +38,11 @@ def _kvs():
     return HermesKV
 
 
-def make_pair(n_keys, num_bkts, log_cap, rmw=False, big=False, machine_id=0):
+def make_pair(n_keys, num_bkts, log_cap, rmw=False, big=False, machine_id=0, skew=0):
     sizes = L.BIG if big else L.DEFAULT
     ecl = 4 if big else 0
-    g = _kvs()(n_keys, num_bkts, log_cap, machine_id, rmw, big, ecl)
-    o = OracleKVS(num_bkts, log_cap, machine_id, rmw, big, ecl)
+    g = _kvs()(n_keys, num_bkts, log_cap, machine_id, rmw, big, ecl, skew=skew)
+    o = OracleKVS(num_bkts, log_cap, machine_id, rmw, big, ecl, skew=skew)
     o.populate(n_keys, sizes.kvs_value)
     return g, o, sizes
 
@@ -162,6 +162,11 @@ CONFIGS = [
     pytest.param(dict(rmw=False, big=True), id="big"),
     pytest.param(dict(rmw=True, big=False), id="rmw"),
     pytest.param(dict(rmw=True, big=True), id="big_rmw"),
+    # the reference's skew optimisations (hkv_config.skew_flags, config.h:79-80): stalled GETs and
+    # PUTs complete once the key's version moved on
+    pytest.param(dict(rmw=False, big=False, skew=3), id="skew"),
+    pytest.param(dict(rmw=False, big=True, skew=3), id="big_skew"),
+    pytest.param(dict(rmw=True, big=False, skew=3), id="rmw_skew"),
 ]
 
 
@@ -187,11 +192,11 @@ def _run_both(g, o, btype, elems_g, elems_o, mb, n_batches, stride, counts, rw_g
 @pytest.mark.parametrize("cfg", CONFIGS)
 def test_random_protocol_rounds(cfg):
     rng = np.random.default_rng(20261015)
-    rmw, big = cfg["rmw"], cfg["big"]
+    rmw, big, skew = cfg["rmw"], cfg["big"], cfg.get("skew", 0)
     n_keys, num_bkts = 3000, 512
     sizes = L.BIG if big else L.DEFAULT
     log_cap = 1 << max(16, (n_keys * sizes.entry + 1024).bit_length())
-    g, o, sizes = make_pair(n_keys, num_bkts, log_cap, rmw=rmw, big=big, machine_id=0)
+    g, o, sizes = make_pair(n_keys, num_bkts, log_cap, rmw=rmw, big=big, machine_id=0, skew=skew)
     assert_tables_equal(g, o, "populate")
     keys = gen_keys(n_keys)
     tsp = gen.TsPool(rng)
@@ -203,6 +208,10 @@ def test_random_protocol_rounds(cfg):
         mb = mb_fail if rnd >= 9 else mb_full
         # local ops
         loc = gen.local_ops(rng, pool, W * S, sizes, rmw, tsp)
+        if skew:   # refilled GETs carry (0, 0) (inline-util.h:268-272); some PUTs version 0
+            z = rng.random(W * S) < 0.3
+            loc["ts_ver"][z] = 0
+            loc["ts_cid"][z & (loc["opcode"] == int(L.Op.GET))] = 0
         counts = rng.integers(S // 2, S + 1, size=W).astype(np.int32)
         loc_o = gen.bytecopy(loc)
         _run_both(g, o, L.BatchType.local_ops, loc, loc_o, mb, W, S, counts)
@@ -446,7 +455,7 @@ def test_inv_direct_path_edge_cases(big):
 
 @pytest.mark.parametrize("big", [False, True])
 def test_ack_direct_path_edge_cases(big):
-    """The ACK direct path (non-RMW ACK launches: T/F words, k_ack_resolve, k_ack_clear) against the
+    """The ACK direct path (non-RMW ACK launches: epoch-tagged T words, F, k_ack_resolve) against the
     oracle: ACKs matching each key's pending write or not, duplicate and out-of-range (>= 8)
     senders, quorums reached at different elements or never, LAST_ACK_* input opcodes, a
     membership with a dropped node, ragged counts and read_write_ops completions."""
@@ -520,6 +529,28 @@ def test_scripted_rare_outcomes(cfg):
     seen = run_scripted(runner, gen_keys(1000), sizes, rmw)
     missing = required_outcomes(rmw) - seen
     assert not missing, f"not produced: {sorted(missing, key=str)}"
+
+
+@pytest.mark.parametrize("big", [False, True])
+def test_scripted_skew_optimisations(big):
+    """tests/scripted.py's skew scenario (skew_flags 3, config.h:79-80) through the device path and
+    the oracle side by side: elements, read_write_ops and the table bit-exact, and the scripted
+    read completions and coalesced writes produced -- after a key's first write in the same
+    launch (S_1's timestamp), in REPLAY, and with the write path's 16-bit version."""
+    from tests.scripted import run_scripted_skew
+    g, o, sizes = make_pair(1000, 4096, 1 << 22, big=big, skew=3)
+
+    def runner(btype, elems, mb, rw=None, node_suspected=None):
+        eo, rwo = gen.bytecopy(elems), (gen.bytecopy(rw) if rw is not None else None)
+        g.batch_host(btype, elems, mb, rw=rw)
+        o.batch_multi(btype, eo, 1, len(eo), None, mb, rw=rwo)
+        assert_elems_equal(elems, eo, f"skew type {int(btype)}")
+        if rw is not None:
+            assert_elems_equal(rw, rwo, f"skew type {int(btype)} rw")
+        assert_tables_equal(g, o, f"skew type {int(btype)}")
+
+    seen = run_scripted_skew(runner, gen_keys(1000), sizes)
+    assert (0, int(L.Resp.PUT_COMPLETE)) in seen and (0, int(L.Resp.GET_COMPLETE)) in seen
 
 
 def test_local_opcode_mirror(engine_path):

@@ -120,3 +120,32 @@ def test_scripted_rare_outcomes_oracle(rmw, big):
     seen = run_scripted(runner, O.gen_keys(1000), sz, rmw)
     missing = required_outcomes(rmw) - seen
     assert not missing, f"not produced: {sorted(missing, key=str)}"
+
+
+@pytest.mark.parametrize("big", [False, True])
+def test_scripted_skew_optimisations_oracle(big):
+    """tests/scripted.py's skew scenario on the oracle (skew_flags 3): read completion and write
+    coalescing outcomes written out from hermesKV.c:196-356, incl. the 16-bit version of the
+    write path and the REPLAY exception."""
+    from tests.scripted import run_scripted_skew
+    sz = L.BIG if big else L.DEFAULT
+    kv = O.OracleKVS(1 << 12, 1 << 22, machine_id=0, big_objects=big, extra_cache_lines=4 if big else 0, skew=3)
+    kv.populate(1000, sz.kvs_value)
+    seen = run_scripted_skew(lambda bt, e, mb, rw=None, node_suspected=None: kv.batch(bt, e, mb, rw=rw),
+                             O.gen_keys(1000), sz)
+    assert (0, int(L.Resp.PUT_COMPLETE)) in seen and (0, int(L.Resp.GET_COMPLETE)) in seen
+
+
+def test_skew_flags_off_keep_stalls_oracle():
+    """The same first batch without the flags: every op behind the write stalls (the default build)."""
+    from tests.scripted import SK, _sk_ops
+    kv = O.OracleKVS(1 << 12, 1 << 22, machine_id=0)
+    kv.populate(1000, L.DEFAULT.kvs_value)
+    keys = O.gen_keys(1000)
+    l1 = _sk_ops(L.DEFAULT, [("hot", L.Op.PUT, (0, 0)), ("hot", L.Op.GET, (0, 0)), ("hot", L.Op.PUT, (0, 0)),
+                             ("hot", L.Op.GET, (0, 7))], keys)
+    kv.batch(L.BatchType.local_ops, l1, L.membership(3, 0))
+    assert [int(x) for x in l1["state"]] == [int(L.Resp.PUT_SUCCESS), int(L.Resp.GET_STALL), int(L.Resp.PUT_STALL),
+                                             int(L.Resp.GET_STALL)]
+    assert [int(x) for x in l1["ts_ver"]] == [2, 0, 0, 0]
+    assert SK["hot"] < 1000

@@ -57,6 +57,36 @@ def test_bench_round_mirrored(theta, workers, cfg3):
         assert st["rmw_aborts"] > 0, st
 
 
+@pytest.mark.parametrize("skew,hot", [(0, False), (3, False), (3, True)])
+def test_retry_round_mirrored(skew, hot):
+    """The bench round under refill_ops' retry policy (stalled ops keep their slots), alone and with
+    the reference's skew optimisations (skew_flags 3: read completion and write coalescing, GET
+    timestamps reset by the refill) and hot-request coalescing: every launch mirrored into an
+    oracle table with the same flags, bit-exact; with the flags, local batches complete stalled
+    GETs and PUTs (PUT_COMPLETE straight out of a local batch exists only through coalescing)."""
+    from hermes_amd.kvs import HermesKV
+    from hermes_amd.workload import Round, zipf_params
+    n_keys, bkts, cap = 60_000, 1 << 16, 1 << 23
+    g = HermesKV(n_keys, bkts, cap, machine_id=0, skew=skew)
+    o = OracleKVS(bkts, cap, 0, skew=skew)
+    o.populate(n_keys, g.sizes.kvs_value)
+    m = Mirror(g, o, "retry round")
+    r = Round(g, 40, L.membership(3, 0), [1, 2], zipf_params(n_keys, 0.99), 200, seed=0x5EED, max_steps=8,
+              trace_len=1024, retry_stalled=True, coalesce_hot=hot)
+    steps = 5
+    for _ in range(steps):
+        r.step()
+    torch.cuda.synchronize()
+    assert m.launches == steps * 4
+    st = r.stats()
+    assert st["committed"] > 0 and st["dropped"] == 0, st
+    assert g.take_error_flags() == 0
+    coalesced = m.codes[(int(L.BatchType.local_ops), "out9", int(L.Resp.PUT_COMPLETE))]
+    assert (coalesced > 0) == bool(skew & 2), m.codes
+    if hot:   # some committed ops were coalesced requests
+        assert st["committed"] > 0
+
+
 class _DeviceBytes:
     """A device byte range as a torch tensor, without a copy (__cuda_array_interface__)."""
 
@@ -286,70 +316,122 @@ def test_val_credits_round_mirrored(credits, cfg3):
 IN_FLIGHT = (122, 135, 123, 143, 148, 144, 133, 149, 147, 118)
 
 
-def _refill_ref(ops, W, S, osz, st_value, shift, tkey, top, tlen, cursor, mid, first, refill_all):
-    """refill_ops (inline-util.h:149-303) as hkv_wl_refill applies it, in numpy: per worker, the
-    completed ops (every op with refill_all / first) take the next trace entries in op order."""
+def _refill_ref(ops, W, S, osz, st_value, shift, tkey, top, tlen, cursor, mid, first, flags, tid=None, hot=None):
+    """refill_ops (inline-util.h:149-303) as hkv_wl_refill applies it, in numpy: per worker, walk
+    the op buffer in order; a completed op (every op on the first pass; with REFILL_ALL also a
+    stalled one) is counted (committed ops: no_coales of them under hot-request coalescing, else
+    one) and takes the next trace command. READ_TS_RESET zeroes a new GET's timestamp
+    (:268-272). COALESCE_HOT (:237-257): while the next command is a GET/PUT on an id below 100
+    and the worker's pointer for that id and opcode class names a slot whose opcode equals the
+    command's, that slot's no_coales grows and the command is consumed; the slot then inserted
+    becomes the pointer. hot: [W][200] slot indexes (255 = NULL), updated in place."""
     ops = ops.copy().reshape(W, S, osz)
     cursor = cursor.copy()
     cnt = np.zeros(5, dtype=np.int64)
     done_states = (130, 128, 138, 137, 119, 121)
+    refill_all, ts_reset, coalesce = flags & 1, flags & 2, flags & 4
+
+    def no_coales(o):
+        return (int(o[16]) | int(o[17]) << 8) >> 1
+
     for w in range(W):
-        rank = 0
+        it = 0
         for i in range(S):
             o = ops[w, i]
             st = int(o[9])
             complete = st in done_states
             drop = bool(refill_all) and not first and not complete and st not in IN_FLIGHT
             if not first and complete:
-                cnt[0] += st not in (130, 138)
+                cnt[0] += (no_coales(o) if coalesce else 1) if st not in (130, 138) else 0
                 cnt[1] += st == 130
                 cnt[2] += st == 128
             cnt[3] += drop
             cnt[4] += (not first) and st == 138
             if not (first or complete or drop):
                 continue
-            t = w * tlen + (int(cursor[w]) + rank) % tlen
-            rank += 1
+            if not first:
+                o[8] = o[9] = 140          # reset op bucket: opcode = state = ST_EMPTY
+            if coalesce and int(top[w * tlen + (int(cursor[w]) + it) % tlen]) != 113:
+                while True:
+                    t = w * tlen + (int(cursor[w]) + it) % tlen
+                    kid, oc = int(tid[t]), int(top[t])
+                    col = 0 if oc == 111 else 100
+                    p = int(hot[w, col + kid]) if kid < 100 else 255
+                    if p != 255 and int(ops[w, p, 8]) == oc:
+                        v = int(ops[w, p, 16]) | int(ops[w, p, 17]) << 8
+                        v = (v & 1) | ((((v >> 1) + 1) & 0x7FFF) << 1)
+                        ops[w, p, 16], ops[w, p, 17] = v & 0xFF, v >> 8
+                        it += 1
+                    else:
+                        break
+                if kid < 100:
+                    hot[w, col + kid] = i
+            t = w * tlen + (int(cursor[w]) + it) % tlen
+            it += 1
             oc = int(top[t])
             o[0:8] = np.frombuffer(np.uint64(tkey[t]).tobytes(), dtype=np.uint8)
             o[8], o[9] = oc, 141
             o[10] = 0 if oc == 111 else (st_value >> shift) & 0xFF
-            flags = (1 if oc == 113 else 0) | (0 if first else 2)
-            o[16], o[17] = flags & 0xFF, flags >> 8
+            if oc == 111 and ts_reset:
+                o[11:16] = 0
+            fl = (1 if oc == 113 else 0) | (0 if first else 2)
+            o[16], o[17] = fl & 0xFF, fl >> 8
             if oc != 111:
                 o[18:18 + st_value] = ord("a") + mid
-        cursor[w] = (int(cursor[w]) + rank) % tlen
+        cursor[w] = (int(cursor[w]) + it) % tlen
     return ops.reshape(-1), cursor, cnt
 
 
 @pytest.mark.parametrize("big", [False, True])
-@pytest.mark.parametrize("refill_all", [0, 1])
-def test_refill_kernel_matches_numpy(big, refill_all):
-    """hkv_wl_refill (LDS-staged for 56-B ops, in place for 312-B ops) against a numpy restatement:
-    slab bytes, trace cursors and the committed / miss / PUT_COMPLETE / dropped counters; with
-    refill_all, ops in flight keep their slots."""
+@pytest.mark.parametrize("flags", [0, 1, 2, 4, 6, 5])
+def test_refill_kernel_matches_numpy(big, flags):
+    """hkv_wl_refill (LDS-staged for 56-B ops, in place for 312-B ops, the sequential walk for
+    hot-request coalescing) against a numpy restatement: slab bytes, trace cursors, the
+    committed / miss / PUT_COMPLETE / dropped counters and the hot-key pointers. flags: 1 fresh
+    batches (ops in flight keep their slots), 2 GET timestamps reset, 4 hot-request coalescing
+    (56-B ops only), several passes so pointers carry over."""
     from hermes_amd import workload as WL
+    if big and flags & 4:
+        pytest.skip("hot-request coalescing stages the slab in LDS: 56-B ops")
     sz = L.BIG if big else L.DEFAULT
     W, S, osz, tlen, mid = 37, 250, sz.op, 300, 2
-    rng = np.random.default_rng(11 + big + 2 * refill_all)
+    rng = np.random.default_rng(11 + big + 2 * flags)
     states = np.array([130, 128, 138, 137, 119, 121, 131, 132, 136, 140, 141, *IN_FLIGHT], dtype=np.uint8)
     ops = rng.integers(0, 256, size=W * S * osz, dtype=np.uint8)
     ops.reshape(W, S, osz)[:, :, 9] = rng.choice(states, size=(W, S))
+    # opcodes as the refill leaves them, so pointers find live GET/PUT slots
+    ops.reshape(W, S, osz)[:, :, 8] = rng.choice(np.array([111, 112, 113], dtype=np.uint8), size=(W, S))
     tkey = rng.integers(0, 2**63, size=W * tlen, dtype=np.int64)
-    top = rng.choice(np.array([111, 112, 113], dtype=np.uint8), size=W * tlen)
+    top = rng.choice(np.array([111, 111, 111, 112, 113], dtype=np.uint8), size=W * tlen)
+    tid = np.where(rng.random(W * tlen) < 0.6, rng.integers(0, 12, W * tlen),
+                   rng.integers(0, 400, W * tlen)).astype(np.int32)
     cursor = rng.integers(0, tlen, size=W, dtype=np.int32)
-    exp_ops, exp_cur, exp_cnt = _refill_ref(ops, W, S, osz, sz.st_value, sz.shift, tkey.view(np.uint64), top, tlen,
-                                            cursor, mid, False, refill_all)
+    hot = np.full((W, 200), 255, np.uint8)
     d_ops = torch.from_numpy(ops.copy()).cuda()
     d_tkey, d_top = torch.from_numpy(tkey).cuda(), torch.from_numpy(top).cuda()
+    d_tid = torch.from_numpy(tid).cuda()
     d_cur = torch.from_numpy(cursor.copy()).cuda()
     d_cnt = torch.zeros(4096, dtype=torch.int64, device="cuda")
     d_opc = torch.zeros(W * S, dtype=torch.uint8, device="cuda")
-    WL.check(WL._L.hkv_wl_refill(WL._ptr(d_ops), W, S, osz, sz.st_value, sz.shift, WL._ptr(d_tkey), WL._ptr(d_top),
-                                 tlen, WL._ptr(d_cur), mid, 0, refill_all, WL._ptr(d_cnt), WL._ptr(d_opc), None),
-             "refill")
+    d_hot = torch.from_numpy(hot.reshape(-1).copy()).cuda()
+    passes = 3 if flags & 4 else 1
+    exp_ops, exp_cur = ops, cursor
+    exp_cnt = np.zeros(5, np.int64)
+    for p in range(passes):
+        if p:   # between passes: some ops complete, some stall, as a round would leave them
+            exp_ops = exp_ops.copy()
+            exp_ops.reshape(W, S, osz)[:, :, 9] = rng.choice(states, size=(W, S))
+            d_ops.copy_(torch.from_numpy(exp_ops))
+        exp_ops, exp_cur, c = _refill_ref(exp_ops, W, S, osz, sz.st_value, sz.shift, tkey.view(np.uint64), top, tlen,
+                                          exp_cur, mid, False, flags, tid, hot)
+        exp_cnt += c
+        WL.check(WL._L.hkv_wl_refill(WL._ptr(d_ops), W, S, osz, sz.st_value, sz.shift, WL._ptr(d_tkey),
+                                     WL._ptr(d_top), WL._ptr(d_tid), tlen, WL._ptr(d_cur), mid, 0, flags,
+                                     WL._ptr(d_cnt), WL._ptr(d_opc), WL._ptr(d_hot), None), "refill")
     WL.check(WL._L.hkv_wl_fold_counters(WL._ptr(d_cnt), None), "fold")
     torch.cuda.synchronize()
+    if flags & 4:
+        assert np.array_equal(d_hot.cpu().numpy().reshape(W, 200), hot), "hot-key pointers differ"
     got = d_ops.cpu().numpy()
     if not np.array_equal(got, exp_ops):
         bad = np.nonzero(got != exp_ops)[0]

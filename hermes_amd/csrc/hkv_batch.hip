@@ -95,6 +95,8 @@ struct BatchArgs {
     const SmallBatch *hdr;       // mixed small launches: the batch headers (in dev_region)
     uint8_t *state_out;          // local launches: each element's final state byte (may be NULL)
     const uint8_t *opc;          // local launches: the caller's opcode mirror (may be NULL, see k_local_pre)
+    const uint8_t *patch;        // local direct path: pending header writes (hkv_batch_desc.d_patch), or NULL
+    uint8_t *rws;                // ACK launches: read_write_ops state mirror (hkv_batch_desc.d_rw_state), or NULL
     int32_t dbg;                 // HKV_DBG: timing experiments that skip work (results invalid)
 };
 
@@ -199,6 +201,7 @@ __device__ __forceinline__ Ctx make_ctx(const BatchArgs &a)
     c.g_membership = a.g_membership;
     c.w_ack_init = a.w_ack_init;
     c.rw = nullptr;
+    c.rws = nullptr;
     return c;
 }
 
@@ -223,12 +226,14 @@ __device__ __forceinline__ int32_t batch_of(const BatchArgs &a, int64_t i, int64
 __device__ __forceinline__ void elem_at(const BatchArgs &a, uint32_t i, uint8_t *&x, uint8_t &idx, Ctx &c)
 {
     c.rw = nullptr;
+    c.rws = nullptr;
     idx = 0;
     if (a.rw || !a.offsets) {  // packed INV / VAL elements need neither (exec_inv / exec_val)
         int64_t start;
         const int32_t b = batch_of(a, i, start);
         idx = (uint8_t)(i - start);
         c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
+        c.rws = a.rws ? a.rws + (int64_t)b * (a.rw_stride / a.g.op_size) : nullptr;
     }
     x = a.elems + (int64_t)i * a.esz;
 }
@@ -755,9 +760,9 @@ __global__ __launch_bounds__(256) void k_ack_resolve(BatchArgs a)
             const int64_t b = batch_of(a, i, start);
             uint8_t *rw = a.rw + b * a.rw_stride + (size_t)obi0 * a.g.op_size;
             const uint8_t oc = rw[8];
-            if (oc == kOpGet) rw[9] = kNew;
-            else if (oc == kOpPut) rw[9] = kPutComplete;
-            else if (oc == kOpRmw) rw[9] = kRmwComplete;
+            const uint8_t ns = oc == kOpGet ? kNew : oc == kOpPut ? kPutComplete : oc == kOpRmw ? kRmwComplete : rw[9];
+            rw[9] = ns;
+            if (a.rws) a.rws[b * (a.rw_stride / a.g.op_size) + obi0] = ns;
         }
     }
     meta_store(entry, m);
@@ -1031,6 +1036,66 @@ __device__ __forceinline__ bool in_count(const BatchArgs &a, uint32_t i)
     return (int32_t)(i - b * (uint32_t)a.stride) < a.counts[b];
 }
 
+// ---- pending header writes (hkv_batch_desc.d_patch, HKV_PATCH_BYTES per element): the second
+// 8-B word of a patch holds opcode (bits 0..7), val_len (8..15), flags (16..31), the value fill
+// byte (32..39), ts reset (40..47) and valid (48..55).
+__device__ __forceinline__ bool patch_valid(uint64_t pb) { return ((pb >> 48) & 0xFFu) != 0; }
+
+// the key of element i as the launch sees it (patched or not)
+__device__ __forceinline__ uint64_t elem_key(const BatchArgs &a, int64_t i)
+{
+    if (a.patch && a.patch[i * 16 + 14]) return *reinterpret_cast<const uint64_t *>(a.patch + i * 16);
+    return *reinterpret_cast<const uint64_t *>(a.elems + i * a.esz);
+}
+
+// a patch applied to the 16-B chunk q (bytes 16q..16q+15) of a 56-B op with a 31-B value
+__device__ __forceinline__ uint4 patch_chunk(uint4 w, int q, uint64_t pa, uint64_t pb)
+{
+    const uint32_t fill = (uint32_t)((pb >> 32) & 0xFFu) * 0x01010101u;
+    const bool vfill = fill != 0, reset = ((pb >> 40) & 0xFFu) != 0;
+    if (q == 0) {
+        w.x = (uint32_t)pa;
+        w.y = (uint32_t)(pa >> 32);
+        // opcode, ST_NEW, val_len; ts.cid (byte 11) and ts.version (12..15) kept unless reset
+        w.z = (uint32_t)(pb & 0xFFu) | ((uint32_t)kNew << 8) | ((uint32_t)((pb >> 8) & 0xFFu) << 16) |
+              (reset ? 0u : (w.z & 0xFF000000u));
+        if (reset) w.w = 0;
+    } else if (q == 1) {
+        const uint32_t flags = (uint32_t)((pb >> 16) & 0xFFFFu);
+        w.x = flags | (vfill ? (fill & 0xFFFF0000u) : (w.x & 0xFFFF0000u));
+        if (vfill) w.y = w.z = w.w = fill;
+    } else if (q == 2) {
+        if (vfill) w.x = w.y = w.z = w.w = fill;
+    } else if (vfill) {  // bytes 48..55: byte 48 is the value's last
+        w.x = (w.x & 0xFFFFFF00u) | (fill & 0xFFu);
+    }
+    return w;
+}
+
+// Every other path: the patches go into the ops first (one thread per element), then the launch
+// runs as usual
+__global__ __launch_bounds__(256) void k_apply_patch(uint8_t *elems, const uint8_t *patch, int64_t n, int32_t esz,
+                                                     uint32_t st_value)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const U64x2 p = *reinterpret_cast<const U64x2 *>(patch + i * 16);
+    if (!patch_valid(p.b)) return;
+    uint8_t *x = elems + i * esz;
+    *reinterpret_cast<uint64_t *>(x) = p.a;
+    x[8] = (uint8_t)p.b;
+    x[9] = kNew;
+    x[10] = (uint8_t)(p.b >> 8);
+    if ((p.b >> 40) & 0xFFu) {
+        x[11] = 0;
+        *reinterpret_cast<uint32_t *>(x + 12) = 0;
+    }
+    *reinterpret_cast<uint16_t *>(x + 16) = (uint16_t)(p.b >> 16);
+    const uint8_t fill = (uint8_t)(p.b >> 32);
+    if (fill)
+        for (uint32_t k = 0; k < st_value; ++k) x[kOpValueOff + k] = fill;
+}
+
 __device__ __forceinline__ uint32_t pre_slot(uint64_t key) { return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 54) & (kPreHash - 1); }
 
 // (key -> smallest element) in an LDS table of kPreHash slots, key ~0 the empty mark; false when the
@@ -1098,12 +1163,20 @@ __global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
         in[k] = i < a.n && (own || i < head_end);
         opm[k] = a.opc ? a.opc[in[k] ? i : 0] : (uint8_t)kOpPut;
     }
+    U64x2 pt[kAllK];
 #pragma unroll
     for (int k = 0; k < kAllK; ++k) {
         const bool own = k < kOwnK;
         const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
         h[k] = *reinterpret_cast<const U64x2 *>(a.elems + (in[k] && opm[k] == kOpPut ? i : 0) * 56);
+        pt[k] = a.patch && in[k] && opm[k] == kOpPut ? *reinterpret_cast<const U64x2 *>(a.patch + i * 16) : U64x2{0, 0};
     }
+#pragma unroll
+    for (int k = 0; k < kAllK; ++k)
+        if (patch_valid(pt[k].b)) {   // a patched element: its key and opcode, state ST_NEW
+            h[k].a = pt[k].a;
+            h[k].b = (h[k].b & ~0xFFFFull) | (pt[k].b & 0xFFu) | ((uint64_t)kNew << 8);
+        }
 #pragma unroll
     for (int k = 0; k < kAllK; ++k) {
         const bool own = k < kOwnK;
@@ -1151,7 +1224,7 @@ __global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
             probe[k] = j < cnt;
             const uint32_t d = probe[k] ? dl[j] : 0u;
             idx[k] = !probe[k] ? kNone : d < (uint32_t)kPreHash ? hv[d] : ~d;
-            key[k] = !probe[k] ? 0 : d < (uint32_t)kPreHash ? hk[d] : *reinterpret_cast<const uint64_t *>(a.elems + (int64_t)idx[k] * 56);
+            key[k] = !probe[k] ? 0 : d < (uint32_t)kPreHash ? hk[d] : elem_key(a, (int64_t)idx[k]);
             if (probe[k] && head_end > 0 && key[k] != ~0ull) {  // a head PUT of the key comes first
                 uint32_t sl = pre_slot(key[k]);
                 for (int n = 0; n < kPreHash; ++n) {
@@ -1207,6 +1280,8 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         op[k] = make_uint4(0u, 0u, 0u, 0u);
         if (live[k]) {
             const uint8_t *xg = a.elems + i * 56 + 16 * q;
+            U64x2 p{0, 0};
+            if (a.patch) p = *reinterpret_cast<const U64x2 *>(a.patch + i * 16);
             if (q < 3) {
                 op[k] = *reinterpret_cast<const uint4 *>(xg);
             } else {
@@ -1214,6 +1289,7 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
                 op[k].x = (uint32_t)t;
                 op[k].y = (uint32_t)(t >> 32);
             }
+            if (patch_valid(p.b)) op[k] = patch_chunk(op[k], q, p.a, p.b);
         }
         sops[te[k] * 4 + q] = op[k];
     }
@@ -1649,6 +1725,7 @@ __device__ __forceinline__ SmallView small_at(const BatchArgs &a, const int32_t 
         v.b = b;
         v.live = a.counts == nullptr || idx < a.counts[b];
         c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
+        c.rws = a.rws ? a.rws + (int64_t)b * (a.rw_stride / a.g.op_size) : nullptr;
         return v;
     }
     int lo = 0, hi = a.n_batches;  // the last b with bstart[b] <= i
@@ -1667,6 +1744,7 @@ __device__ __forceinline__ SmallView small_at(const BatchArgs &a, const int32_t 
     c.g_membership = h.g_membership;
     c.w_ack_init = h.w_ack_init;
     c.rw = h.rw_off >= 0 ? a.dev_region + h.rw_off : nullptr;
+    c.rws = nullptr;
     return v;
 }
 
@@ -1977,6 +2055,8 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.offsets = bl.offsets;
     a.state_out = (bl.type == kLocal || bl.type == kLocalAfterMemb) ? bl.state_out : nullptr;
     a.opc = bl.type == kLocal ? bl.opcode_in : nullptr;
+    a.patch = nullptr;
+    a.rws = bl.type == kAcks ? bl.rw_state : nullptr;
     static const int dbg_env = getenv("HKV_DBG") ? atoi(getenv("HKV_DBG")) : 0;
     a.dbg = dbg_env;
     if (dbg_env) a.error_flags = nullptr;
@@ -2037,6 +2117,11 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     static const int ld_env = getenv("HKV_LOCAL_DIRECT") ? atoi(getenv("HKV_LOCAL_DIRECT")) : 1;
     const bool local_direct = ld_env != 0 && bl.type == kLocal && !bl.g.rmw_enabled && bl.esz == 56 &&
                               bl.g.st_value == 31 && bl.g.entry_size == 64 && !bl.offsets;
+    if (bl.patch && (small || !local_direct)) {  // the other paths take the patches as op writes first
+        hipLaunchKernelGGL(k_apply_patch, dim3(grid), dim3(256), 0, s, bl.elems, bl.patch, n, bl.esz, bl.g.st_value);
+    } else if (bl.patch) {
+        a.patch = bl.patch;
+    }
     if (small) {
         if (launch_small(a, s)) return -3;
         return 0;                              // node_suspected written by the kernel

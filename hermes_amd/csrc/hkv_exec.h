@@ -119,6 +119,7 @@ struct Ctx {           // per-launch constants
     uint8_t g_membership;
     uint8_t w_ack_init;
     uint8_t *rw;       // this element's batch read_write_ops (ACKs)
+    uint8_t *rws;      // its state-byte mirror (hkv_batch_desc.d_rw_state), or null
 };
 
 __device__ __forceinline__ bool is_last_ack(uint8_t bv, const Ctx &c)  // spacetime.h:253-259
@@ -333,9 +334,9 @@ __device__ __forceinline__ void exec_ack(uint8_t *ack, Meta &m, const Ctx &c)
         // own opcode), so concurrent segments completing one slot are benign
         uint8_t *w = c.rw + (size_t)done * c.g.op_size;
         uint8_t oc = w[8];
-        if (oc == kOpGet) w[9] = kNew;
-        else if (oc == kOpPut) w[9] = kPutComplete;
-        else if (oc == kOpRmw) w[9] = kRmwComplete;
+        const uint8_t ns = oc == kOpGet ? kNew : oc == kOpPut ? kPutComplete : oc == kOpRmw ? kRmwComplete : w[9];
+        w[9] = ns;
+        if (c.rws) c.rws[done] = ns;
     }
     if (ack[8] != kLastAckSuccess) ack[8] = kAckSuccess;
 }

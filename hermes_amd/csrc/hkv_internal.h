@@ -17,6 +17,8 @@ struct BatchLaunch {
     const int32_t *offsets;      // packed INV/VAL launches: n_batches + 1 batch offsets (counts NULL)
     uint8_t *state_out;          // local launches: each element's final state byte (may be NULL)
     const uint8_t *opcode_in;    // local launches: the caller's mirror of each element's opcode (may be NULL)
+    const uint8_t *patch;        // local launches: pending header writes, 16 B per element (may be NULL)
+    uint8_t *rw_state;           // ACK launches: state-byte mirror of read_write_ops (may be NULL)
     const uint8_t *index;
     uint8_t *log;
     uint8_t *rw;

@@ -445,6 +445,9 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.state_out = d->d_state_out;
     static const bool opc_off = getenv("HKV_OPCODE_IN") && atoi(getenv("HKV_OPCODE_IN")) == 0;  // experiments
     bl.opcode_in = d->type == kLocal && !opc_off ? d->d_opcode_in : nullptr;
+    bl.patch = d->type == kLocal ? d->d_patch : nullptr;
+    bl.rw_state = d->type == kAcks ? d->d_rw_state : nullptr;
+    if (bl.patch && ((uintptr_t)bl.patch & 15)) return fail(-1, "d_patch must be 16-byte aligned");
     bl.offsets = packed ? d->d_counts : nullptr;
     bl.index = t->d_index;
     bl.log = t->d_log;

@@ -442,13 +442,62 @@ __device__ __forceinline__ uint64_t with_op_state(uint64_t h, uint8_t op, uint8_
     return (h & ~0xFFFFull) | op | ((uint64_t)st << 8);
 }
 
+// refill_ops as a plan (hkv_wl_refill_plan): the same decisions, cursors and counts as k_refill,
+// made from the state mirror (one byte per op instead of every op's line); each refilled
+// slot gets a patch (hkv_batch_desc.d_patch) that the next local launch applies as it reads the op,
+// so the op slab is read and written once per round (by that launch) instead of twice.
+__global__ __launch_bounds__(256) void k_refill_plan(const uint8_t *states, int32_t stride, uint32_t st_value,
+                                                     uint32_t shift, const uint64_t *tkey, const uint8_t *top,
+                                                     int32_t tlen, uint32_t *cursor, uint32_t machine_id,
+                                                     uint32_t flags, unsigned long long *counters, uint8_t *opc,
+                                                     uint8_t *patch)
+{
+    const int w = blockIdx.x, i = threadIdx.x;
+    const bool live = i < stride;
+    const int64_t e = (int64_t)w * stride + i;
+    const uint8_t st = live ? states[e] : 0;
+    const bool complete = is_complete(st);
+    const bool drop = live && (flags & HKV_WL_REFILL_ALL) && !complete && !in_flight(st);
+    const bool done = live && (complete || drop);
+    const int commits = (live && complete && st != kMiss && st != kRmwAbort) ? 1 : 0;
+    int total;
+    const int rank = block_rank(done, total);
+    const uint32_t base = cursor[w];
+    const int c = block_sum(commits), m = block_sum(live && st == kMiss ? 1 : 0);
+    const int wr = block_sum(live && st == kPutComplete ? 1 : 0), dr = block_sum(drop ? 1 : 0);
+    const int ab = block_sum(live && st == kRmwAbort ? 1 : 0);
+    if (i == 0) {
+        cursor[w] = (uint32_t)((base + (uint32_t)total) % (uint32_t)tlen);
+        unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + (w % kStripes) * 16;
+        if (c) atomicAdd(&stripe[0], (unsigned long long)c);
+        if (m) atomicAdd(&stripe[1], (unsigned long long)m);
+        if (wr) atomicAdd(&stripe[2], (unsigned long long)wr);
+        if (dr) atomicAdd(&stripe[3], (unsigned long long)dr);
+        if (ab) atomicAdd(&stripe[4], (unsigned long long)ab);
+    }
+    if (!live) return;
+    W16 p{0, 0};
+    if (done) {
+        const int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)rank) % (uint32_t)tlen);
+        const uint8_t oc = top[t];
+        const bool get = oc == kOpGet;
+        p.a = tkey[t];
+        p.b = (uint64_t)oc | ((uint64_t)(get ? 0u : (uint8_t)(st_value >> shift)) << 8) |
+              ((uint64_t)((oc == kOpRmw ? 1u : 0u) | 2u) << 16) |             // RMW_flag, no_coales = 1
+              ((uint64_t)(get ? 0u : (uint8_t)('a' + machine_id)) << 32) |  // the written value
+              ((uint64_t)(get && (flags & HKV_WL_READ_TS_RESET) ? 1u : 0u) << 40) | (1ull << 48);
+        opc[e] = oc;
+    }
+    *reinterpret_cast<W16 *>(patch + e * 16) = p;
+}
+
 // wings_issue_pkts(inv) with the INV callbacks of hermes_worker.c:12-65. At most out_stride
 // INVs per worker go out per round (the send credits); the rest keep their state and are
 // sent by a later round, as with the reference's credit-limited wings sends.
 __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stride, uint32_t op_size, uint8_t *out,
                                                       int32_t out_stride, int32_t *count, uint32_t machine_id,
                                                       unsigned long long *held, const int32_t *aq_n, int32_t r_alive,
-                                                      const uint8_t *states)
+                                                      uint8_t *states)
 {
     const int w = blockIdx.x, i = threadIdx.x;
     const bool live = i < stride;
@@ -483,9 +532,12 @@ __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stri
                 dst[k] = k == 1 ? with_op_state(v, kOpInv, (uint8_t)machine_id) : v;
             }
         }
-        if (send && rank < send_cap)
-            op[9] = st == kPutSuccess ? kInProgressPut : st == kRmwSuccess ? kInProgressRmw
-                  : st == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
+        if (send && rank < send_cap) {
+            const uint8_t ns = st == kPutSuccess ? kInProgressPut : st == kRmwSuccess ? kInProgressRmw
+                             : st == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
+            op[9] = ns;
+            if (states) states[(int64_t)w * stride + i] = ns;
+        }
         return;
     }
     if (!send || rank >= send_cap) return;
@@ -496,8 +548,10 @@ __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stri
     uint32_t k = 16;
     for (; k + 16 <= op_size; k += 16) *reinterpret_cast<W16 *>(dst + k) = *reinterpret_cast<const W16 *>(op + k);
     if (k < op_size) *reinterpret_cast<uint64_t *>(dst + k) = *reinterpret_cast<const uint64_t *>(op + k);
-    op[9] = st == kPutSuccess ? kInProgressPut : st == kRmwSuccess ? kInProgressRmw
-          : st == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
+    const uint8_t ns = st == kPutSuccess ? kInProgressPut : st == kRmwSuccess ? kInProgressRmw
+                     : st == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
+    op[9] = ns;
+    if (states) states[(int64_t)w * stride + i] = ns;   // the mirror stays the ops' state bytes
 }
 
 // VALs of the writes and replays a membership change completed: wings_issue_pkts(val) over the
@@ -507,7 +561,7 @@ __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stri
 // *_COMPLETE_SEND_VALS -> PUT_COMPLETE / RMW_COMPLETE / NEW (a replayed GET is issued again).
 __global__ __launch_bounds__(256) void k_marshal_memb_vals(uint8_t *ops, int32_t stride, uint32_t op_size,
                                                            uint8_t *out, int32_t out_stride, int32_t *count,
-                                                           uint32_t machine_id)
+                                                           uint32_t machine_id, uint8_t *states)
 {
     const int w = blockIdx.x, i = threadIdx.x;
     const bool live = i < stride;
@@ -523,7 +577,9 @@ __global__ __launch_bounds__(256) void k_marshal_memb_vals(uint8_t *ops, int32_t
         *reinterpret_cast<W16 *>(out + ((int64_t)w * out_stride + rank) * kOpMetaSize) =
             W16{h.a, with_op_state(h.b, kOpVal, (uint8_t)machine_id)};
     }
-    op[9] = st == kPutCompleteSendVals ? kPutComplete : st == kRmwCompleteSendVals ? kRmwComplete : kNew;
+    const uint8_t ns = st == kPutCompleteSendVals ? kPutComplete : st == kRmwCompleteSendVals ? kRmwComplete : kNew;
+    op[9] = ns;
+    if (states) states[(int64_t)w * stride + i] = ns;
 }
 
 // The largest of n counts, stored straight into pinned host memory (one workgroup): the host
@@ -1277,6 +1333,18 @@ int hkv_wl_refill(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_s
     return ok();
 }
 
+int hkv_wl_refill_plan(const uint8_t *states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
+                       const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor, uint32_t machine_id,
+                       uint32_t flags, unsigned long long *counters, uint8_t *opc, uint8_t *patch, void *stream)
+{
+    if (stride > 256 || n_workers <= 0 || tlen <= 0 || !states || !opc || !patch) return -1;
+    if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET)) return -1;   // no hot-request coalescing
+    if (((uintptr_t)patch & 15) || st_value > 255) return -1;
+    hipLaunchKernelGGL(k_refill_plan, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, states, stride, st_value,
+                       shift, tkey, top, tlen, cursor, machine_id, flags, counters, opc, patch);
+    return ok();
+}
+
 int hkv_wl_fold_counters(unsigned long long *counters, void *stream)
 {
     hipLaunchKernelGGL(k_fold_counters, dim3(1), dim3(256), 0, (hipStream_t)stream, counters);
@@ -1289,7 +1357,7 @@ int hkv_wl_marshal_invs(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_
     if (stride > 256 || n_workers <= 0) return -1;
     hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
                        stride, count, machine_id, (unsigned long long *)nullptr, (const int32_t *)nullptr, 1,
-                       (const uint8_t *)nullptr);
+                       (uint8_t *)nullptr);
     return ok();
 }
 
@@ -1390,7 +1458,7 @@ uint64_t hkv_wl_peer_ts_words(const hkv_table *t)
 
 int hkv_wl_marshal_invs_cap(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint8_t *out,
                             int32_t out_stride, int32_t *count, uint32_t machine_id, unsigned long long *held,
-                            const uint8_t *states, void *stream)
+                            uint8_t *states, void *stream)
 {
     if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
     hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
@@ -1404,16 +1472,16 @@ int hkv_wl_marshal_invs_credits(uint8_t *ops, int32_t n_workers, int32_t stride,
 {
     if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
     hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
-                       out_stride, count, machine_id, held, aq_n, r_alive, (const uint8_t *)nullptr);
+                       out_stride, count, machine_id, held, aq_n, r_alive, (uint8_t *)nullptr);
     return ok();
 }
 
 int hkv_wl_marshal_memb_vals(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint8_t *out,
-                             int32_t out_stride, int32_t *count, uint32_t machine_id, void *stream)
+                             int32_t out_stride, int32_t *count, uint32_t machine_id, uint8_t *states, void *stream)
 {
     if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
     hipLaunchKernelGGL(k_marshal_memb_vals, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
-                       out, out_stride, count, machine_id);
+                       out, out_stride, count, machine_id, states);
     return ok();
 }
 

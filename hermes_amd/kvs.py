@@ -167,11 +167,14 @@ class HermesKV:
               membership: bytes, counts: torch.Tensor | None = None, rw: torch.Tensor | None = None,
               rw_stride_bytes: int = 0, node_suspected: torch.Tensor | None = None,
               stream: torch.cuda.Stream | None = None, offsets: torch.Tensor | None = None,
-              state_out: torch.Tensor | None = None, opcode_in: torch.Tensor | None = None) -> None:
+              state_out: torch.Tensor | None = None, opcode_in: torch.Tensor | None = None,
+              patch: torch.Tensor | None = None, rw_state: torch.Tensor | None = None) -> None:
         """Apply n_batches batches of one type, concatenated in `elems` (uint8, on the GPU),
         in concatenation order, asynchronously on `stream` (default: torch's current).
         offsets (INV / ACK / VAL batches): the batches stored back to back, batch b at elements
-        [offsets[b], offsets[b+1]); `stride` is then the total (HKV_BATCH_PACKED)."""
+        [offsets[b], offsets[b+1]); `stride` is then the total (HKV_BATCH_PACKED). patch (local
+        batches): 16 B per element of pending header writes (hkv_batch_desc.d_patch); rw_state (ACK
+        batches): the read_write_ops' state-byte mirror, kept up to date by the completions."""
         assert elems.is_cuda and elems.dtype == torch.uint8
         total = stride if offsets is not None else n_batches * stride
         assert elems.numel() >= total * elem_size
@@ -188,6 +191,12 @@ class HermesKV:
         if opcode_in is not None:   # local batches: the caller's mirror of each element's opcode byte
             assert opcode_in.is_cuda and opcode_in.dtype == torch.uint8 and opcode_in.numel() >= n_batches * stride
             d.d_opcode_in = opcode_in.data_ptr()
+        if patch is not None:
+            assert patch.is_cuda and patch.dtype == torch.uint8 and patch.numel() >= n_batches * stride * 16
+            d.d_patch = patch.data_ptr()
+        if rw_state is not None:
+            assert rw_state.is_cuda and rw_state.dtype == torch.uint8
+            d.d_rw_state = rw_state.data_ptr()
         if offsets is not None:
             assert counts is None and offsets.is_cuda and offsets.dtype == torch.int32
             assert offsets.numel() >= n_batches + 1

@@ -50,7 +50,7 @@ _L.hkv_wl_pack_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c
 _L.hkv_wl_marshal_acks_aligned.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P,
                                            ctypes.c_uint32, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_memb_vals.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
-                                        ctypes.c_uint32, _P]
+                                        ctypes.c_uint32, _P, _P]
 _L.hkv_wl_regroup_aligned.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_uint32,
                                       _P, ctypes.c_int32, _P, _P]
 
@@ -63,7 +63,8 @@ class ReplicaRound:
 
     def __init__(self, kvs: HermesKV, n_workers: int, world: int, rank: int, zipf: HkvZipf,
                  write_permille: int = 200, rmw_permille: int = 0, seed: int = 0x5EED,
-                 trace_len: int = 8192, retry_stalled: bool = False, slots: int | None = None):
+                 trace_len: int = 8192, retry_stalled: bool = False, slots: int | None = None,
+                 fused_refill: bool = True):
         if not 2 <= world <= MAX_REPLICAS:
             raise ValueError(f"a replica group has 2..{MAX_REPLICAS} replicas, got {world}")
         if kvs.machine_id != rank:
@@ -83,6 +84,9 @@ class ReplicaRound:
         self.ops = torch.zeros(W * LOCAL * self.op, **u8)
         self.states = torch.zeros(W * LOCAL, dtype=torch.uint8, device=dev)  # local batch state mirror
         self.opcodes = torch.zeros(W * LOCAL, dtype=torch.uint8, device=dev)  # the refill's opcode mirror
+        # refills planned from the state mirror and applied by the next local launch (workload.Round)
+        self.fused = fused_refill and self.op <= 64
+        self.patch = torch.zeros(W * LOCAL * 16, **u8) if self.fused else None
         # outgoing INVs: [W][C] rows, then packed (worker w at inv_off[w]; inv_off[W] = total)
         self.inv_slab = torch.zeros(W * C * self.op, **u8)
         self.inv_count = torch.zeros(W, **i32)
@@ -139,6 +143,12 @@ class ReplicaRound:
     def refill(self, first: bool = False):
         if self.failed:
             return
+        if self.fused and not first:
+            check(_L.hkv_wl_refill_plan(_ptr(self.states), self.W, LOCAL, self.sizes.st_value, self.sizes.shift,
+                                        _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
+                                        self.rank, self.rflags, _ptr(self.counters), _ptr(self.opcodes),
+                                        _ptr(self.patch), _s()), "refill_plan")
+            return
         check(_L.hkv_wl_refill(_ptr(self.ops), self.W, LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
                                _ptr(self.trace_key), _ptr(self.trace_op), None, self.trace_len, _ptr(self.cursor),
                                self.rank, int(first), self.rflags, _ptr(self.counters), _ptr(self.opcodes), None,
@@ -152,7 +162,7 @@ class ReplicaRound:
             self.inv_maxc.zero_()
             return
         self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, LOCAL, self.op, self.mb, state_out=self.states,
-                       opcode_in=self.opcodes)
+                       opcode_in=self.opcodes, patch=self.patch)
         check(_L.hkv_wl_marshal_invs_cap(_ptr(self.ops), self.W, LOCAL, self.op, _ptr(self.inv_slab), self.C,
                                          _ptr(self.inv_count), self.rank, _ptr(self.held), _ptr(self.states), _s()),
               "marshal_invs")
@@ -215,7 +225,7 @@ class ReplicaRound:
         if self.count_elems:
             self.elem_totals[1] += self.ack_batch_count.sum()
         self.kvs.batch(L.BatchType.acks, self.ack_batch, W, stride, self.ack_size, self.mb,
-                       counts=self.ack_batch_count, rw=self.ops, rw_stride_bytes=LOCAL * self.op)
+                       counts=self.ack_batch_count, rw=self.ops, rw_stride_bytes=LOCAL * self.op, rw_state=self.states)
         check(_L.hkv_wl_collect_vals(_ptr(self.ack_batch), _ptr(self.ack_batch_count), W, stride, self.ack_size,
                                      _ptr(self.val_slab), C, _ptr(self.val_count), self.rank,
                                      _ptr(self.held[1:]), None, _s()), "collect_vals")
@@ -251,9 +261,10 @@ class ReplicaRound:
         else:
             g = self.mb[1] & ~(1 << peer) & 0xFF
             self.mb = L.membership(0, self.rank, alive=g)
-        self.kvs.batch(L.BatchType.local_ops_after_membership_change, self.ops, W, LOCAL, self.op, self.mb)
+        self.kvs.batch(L.BatchType.local_ops_after_membership_change, self.ops, W, LOCAL, self.op, self.mb,
+                       state_out=self.states)
         check(_L.hkv_wl_marshal_memb_vals(_ptr(self.ops), W, LOCAL, self.op, _ptr(self.val_slab), C,
-                                          _ptr(self.val_count), self.rank, _s()), "marshal_memb_vals")
+                                          _ptr(self.val_count), self.rank, _ptr(self.states), _s()), "marshal_memb_vals")
         check(_L.hkv_wl_pack_rows(_ptr(self.val_slab), _ptr(self.val_count), W, C, L.OP_META_SIZE,
                                   _ptr(self.val_pack), _ptr(self.val_off), _s()), "pack memb vals")
 

@@ -35,12 +35,14 @@ _L.hkv_wl_refill.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32
                              _P, _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint32, _P, _P,
                              _P, _P]
 _L.hkv_wl_fold_counters.argtypes = [_P, _P]
+_L.hkv_wl_refill_plan.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, _P, _P,
+                                  ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _P]
 _L.hkv_wl_marshal_invs.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_invs_cap.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
                                        ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_marshal_acks.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_memb_vals.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
-                                        ctypes.c_uint32, _P]
+                                        ctypes.c_uint32, _P, _P]
 _L.hkv_wl_max_to_host.argtypes = [_P, ctypes.c_int32, _P, _P]
 _L.hkv_wl_marshal_vals.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_collect_vals.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
@@ -130,7 +132,7 @@ class Round:
                  remote_per_peer: int = 50, trace_len: int = 8192, seed: int = 0x5EED,
                  virtual_peers: bool = True, max_steps: int = 64, retry_stalled: bool = False,
                  fit_ack_stride: bool = True, val_credits: int | None = None, pack_remote: bool = True,
-                 hades: bool = False, coalesce_hot: bool = False):
+                 hades: bool = False, coalesce_hot: bool = False, fused_refill: bool | None = None):
         self.kvs = kvs
         self.W = n_workers
         self.mb = membership
@@ -145,6 +147,12 @@ class Round:
         self.retry = retry_stalled     # True: refill_ops semantics (stalled ops keep their slot)
         self.coalesce_hot = coalesce_hot   # ENABLE_COALESCE_OF_HOT_REQS (refill_ops, inline-util.h:237-257)
         self.rflags = refill_flags(kvs, retry_stalled, coalesce_hot)
+        # fused_refill: the refill is planned from the state mirror (hkv_wl_refill_plan) and applied by
+        # the next local launch as patches, so the op slab is read and written once per round. Not with
+        # hot-request coalescing (a sequential walk over the ops), VAL credits (their marshal keeps no
+        # mirror) or 312-B ops (refilled in place). Default: wherever it applies.
+        can_fuse = not coalesce_hot and val_credits is None and self.op <= 64
+        self.fused = can_fuse if fused_refill is None else (fused_refill and can_fuse)
         self.machine_id = kvs.machine_id
         dev = torch.device("cuda", kvs.device)
         W, S = n_workers, self.LOCAL
@@ -152,6 +160,7 @@ class Round:
         self.ops = torch.zeros(W * S * self.op, **u8)
         self.states = torch.zeros(W * S, **u8)   # the local batch's mirror of every op's state byte
         self.opcodes = torch.zeros(W * S, **u8)  # the refill's mirror of every op's opcode byte
+        self.patch = torch.zeros(W * S * 16, **u8) if self.fused else None   # planned refills (d_patch)
         self.C = slots_per_worker(write_permille, rmw_permille)   # INV send credits per worker
         self.inv_out = torch.zeros(W * self.C * self.op, **u8)
         self.inv_count = torch.zeros(W, dtype=torch.int32, device=dev)
@@ -283,6 +292,12 @@ class Round:
 
     # -- pieces of one round
     def refill(self, first: bool = False):
+        if self.fused and not first:   # a plan the next local launch applies (the ops stay as they are)
+            check(_L.hkv_wl_refill_plan(_ptr(self.states), self.W, self.LOCAL, self.sizes.st_value, self.sizes.shift,
+                                        _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
+                                        self.machine_id, self.rflags, _ptr(self.counters), _ptr(self.opcodes),
+                                        _ptr(self.patch), _s()), "refill_plan")
+            return
         check(_L.hkv_wl_refill(_ptr(self.ops), self.W, self.LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
                                _ptr(self.trace_key), _ptr(self.trace_op), _ptr(self.trace_id), self.trace_len,
                                _ptr(self.cursor), self.machine_id, int(first), self.rflags, _ptr(self.counters),
@@ -291,7 +306,7 @@ class Round:
 
     def local_batch(self):
         self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb, state_out=self.states,
-                       opcode_in=self.opcodes)
+                       opcode_in=self.opcodes, patch=self.patch)
 
     def marshal_invs(self):
         if self.V is not None:
@@ -336,11 +351,12 @@ class Round:
         acks = self.acks if acks is None else acks
         if self.fit and stride is None:   # this round's packed ACKs
             self.kvs.batch(L.BatchType.acks, acks, self.W, self.ack_total, self.ack_size, self.mb,
-                           rw=self.ops, rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off)
+                           rw=self.ops, rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off,
+                           rw_state=self.states)
             return
         self.kvs.batch(L.BatchType.acks, acks, n_batches or self.W, stride or self.ack_width, self.ack_size,
                        self.mb, counts=self.ack_count if counts is None else counts, rw=self.ops,
-                       rw_stride_bytes=self.LOCAL * self.op)
+                       rw_stride_bytes=self.LOCAL * self.op, rw_state=self.states)
 
     def marshal_vals(self, acks: torch.Tensor, n: int, out: torch.Tensor):
         check(_L.hkv_wl_marshal_vals(_ptr(acks), n, self.ack_size, _ptr(out), self.machine_id, _s()),
@@ -517,10 +533,11 @@ class Round:
 
     def _after_membership_change(self, mb: bytes):
         self.mb = mb
-        self.kvs.batch(L.BatchType.local_ops_after_membership_change, self.ops, self.W, self.LOCAL, self.op, self.mb)
+        self.kvs.batch(L.BatchType.local_ops_after_membership_change, self.ops, self.W, self.LOCAL, self.op, self.mb,
+                       state_out=self.states)
         check(_L.hkv_wl_marshal_memb_vals(_ptr(self.ops), self.W, self.LOCAL, self.op, _ptr(self.val_out),
-                                          self.ack_stride, _ptr(self.val_count), self.machine_id, _s()),
-              "marshal_memb_vals")
+                                          self.ack_stride, _ptr(self.val_count), self.machine_id, _ptr(self.states),
+                                          _s()), "marshal_memb_vals")
 
     # -- Hades: this replica and every virtual peer run the agreement
     def _hades_start(self):

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HKV_ABI_VERSION 4
+#define HKV_ABI_VERSION 5
 
 /* ------------------------------------------------------------------ reference types
  * Declared here only when the reference's own spacetime.h has not been included; the
@@ -139,7 +139,23 @@ typedef struct hkv_batch_desc {
                                    (hkv_wl_refill); lets the launch find its PUTs without reading
                                    every op. A PUT the mirror misses raises error flag bit 3.
                                    NULL = read the ops (ABI 3) */
+    const uint8_t *d_patch;     /* device, local batches: pending header writes, HKV_PATCH_BYTES per element
+                                   (n_batches * stride), NULL = none (ABI 5). An element whose patch is
+                                   valid first gets the patch's bytes, exactly as if the caller had written
+                                   them into the op before the launch; hkv_wl_refill_plan writes a refill
+                                   this way, so the launch's own write-back of every op replaces the
+                                   refill's pass over the op slab. The mirrors (d_opcode_in) must already
+                                   describe the patched ops. */
+    uint8_t *d_rw_state;        /* device, ACK batches: a mirror of the read_write_ops' state bytes
+                                   (rw_stride_bytes / op size per batch); every completion a launch writes
+                                   into read_write_ops is also written here. NULL = none (ABI 5) */
 } hkv_batch_desc;
+
+/* d_patch layout (16 bytes per element): key 0..7, opcode 8, val_len 9, flags (RMW_flag | no_coales
+ * << 1) 10..11, value fill byte 12 (0: the value is kept), ts reset 13 (1: ts bytes 11..15 := 0),
+ * valid 14 (1: apply), 15 unused. Applying sets op bytes 0..7 = key, 8 = opcode, 9 = ST_NEW,
+ * 10 = val_len, [11..15 = 0], 16..17 = flags and, with a fill byte, the ST_VALUE_SIZE value bytes. */
+#define HKV_PATCH_BYTES 16
 
 /* hkv_batch_desc.flags. By default launches of at most 4096 elements run as one single-workgroup
  * kernel and larger ones on the multi-kernel engine; both give the same bytes. */

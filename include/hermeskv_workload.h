@@ -78,6 +78,17 @@ int hkv_wl_refill(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op
                   uint32_t shift, const uint64_t *d_trace_key, const uint8_t *d_trace_op, const uint32_t *d_trace_id,
                   int32_t trace_len, uint32_t *d_cursor, uint32_t machine_id, int32_t first_iter, uint32_t flags,
                   unsigned long long *d_counters, uint8_t *d_opcode_out, uint8_t *d_hot, void *stream);
+/* refill_ops as a plan for the next local launch: the decisions, trace cursors and counts of
+ * hkv_wl_refill (not on the first pass; flags HKV_WL_REFILL_ALL and HKV_WL_READ_TS_RESET), made from
+ * d_states -- the ops' state bytes, kept by the round (the local launch's d_state_out, the INV and
+ * membership marshals, the ACK launch's d_rw_state) -- instead of the ops. Each refilled op gets a
+ * valid patch in d_patch (HKV_PATCH_BYTES per op, include/hermeskv.h), every other op an invalid one;
+ * d_opcode (the opcode mirror) takes the refilled ops' opcodes. The ops themselves are untouched:
+ * the next local launch, given d_patch, applies the patches as it reads them. */
+int hkv_wl_refill_plan(const uint8_t *d_states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
+                       const uint64_t *d_trace_key, const uint8_t *d_trace_op, int32_t trace_len, uint32_t *d_cursor,
+                       uint32_t machine_id, uint32_t flags, unsigned long long *d_counters, uint8_t *d_opcode,
+                       uint8_t *d_patch, void *stream);
 /* d_counters[0..4] += the refill stripes (which are cleared) */
 int hkv_wl_fold_counters(unsigned long long *d_counters, void *stream);
 
@@ -165,10 +176,11 @@ int hkv_wl_ack_offsets(const int32_t *d_inv_count, int32_t n_workers, int32_t n_
  * hermes_worker.c:163-203): per worker w, ops in state PUT/RMW/REPLAY_COMPLETE_SEND_VALS are
  * compacted in op order into d_val_out[w*out_stride ...] (16-B VALs: the op's key and ts,
  * ST_OP_VAL, sender machine_id), d_count[w] = how many (at most out_stride); the ops become
- * PUT_COMPLETE / RMW_COMPLETE / ST_NEW. stride <= 256. */
+ * PUT_COMPLETE / RMW_COMPLETE / ST_NEW. stride <= 256. d_states (may be NULL): the ops' state
+ * mirror, updated the same way. */
 int hkv_wl_marshal_memb_vals(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size,
                              uint8_t *d_val_out, int32_t out_stride, int32_t *d_count, uint32_t machine_id,
-                             void *stream);
+                             uint8_t *d_states, void *stream);
 
 /* *h_out = max(d_counts[0..n)), written by the kernel into pinned host memory (hipHostMalloc /
  * hipHostRegister; valid once the stream passes this call): a round's width without a copy. */
@@ -177,10 +189,11 @@ int hkv_wl_max_to_host(const int32_t *d_counts, int32_t n, int32_t *h_out, void 
 /* hkv_wl_marshal_invs with at most out_stride INVs per worker per round (d_inv_out rows of
  * out_stride); further sendable ops keep their state for a later round and are counted in
  * *d_held (may be NULL). d_states (may be NULL): the state mirror the local batch wrote
- * (hkv_batch_desc.d_state_out), read instead of each op's state byte. */
+ * (hkv_batch_desc.d_state_out), read instead of each op's state byte, and updated with the states
+ * the sent ops move to. */
 int hkv_wl_marshal_invs_cap(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size,
                             uint8_t *d_inv_out, int32_t out_stride, int32_t *d_inv_count, uint32_t machine_id,
-                            unsigned long long *d_held, const uint8_t *d_states, void *stream);
+                            unsigned long long *d_held, uint8_t *d_states, void *stream);
 
 /* ACKs for `rows` rows of received INVs (row r: d_in_count[r] INVs at d_invs + r*C*op_size),
  * compacted to the front of row r of d_ack_out (row stride C), d_out_count[r] ACKs; INV

@@ -59,28 +59,38 @@ class TableSnapshot:
 def run_cpu_baseline(kvs, zipf, write_permille: int, workers: int, seconds: float, seed: int,
                      n_peers: int = 2, per_peer: int = 50, refill_flags: int = 1, threads: int = 0,
                      snapshot: TableSnapshot | None = None) -> dict:
-    """threads = 0: one per usable core (host_threads()); workers = 0: one 250-op buffer per thread,
-    as the reference's workers (main.c:193-210). refill_flags: hkv_wl_refill's (1 fresh batches, 2
-    GET timestamps reset, 4 hot-request coalescing; 0 = refill_ops' retry). The table's skew flags
-    come with it. snapshot: a TableSnapshot taken earlier (consumed); default: the table as it is now."""
+    """threads = 0: the thread count among 1, 4, 8, ... host_threads() that runs this workload fastest,
+    by a short probe of each (the reference's seqlocks make hot keys contended, and under refill_ops'
+    retry more threads can be slower); workers = 0: one 250-op buffer per thread, as the reference's
+    workers (main.c:193-210). refill_flags: hkv_wl_refill's (1 fresh batches, 2 GET timestamps
+    reset, 4 hot-request coalescing; 0 = refill_ops' retry). The table's skew flags come with it.
+    snapshot: a TableSnapshot taken earlier (consumed); default: the table as it is now."""
     snap = snapshot if snapshot is not None else TableSnapshot(kvs)
     L, h, cfg, c = snap.L, snap.h, snap.cfg, snap.c
-    threads = threads or host_threads()
-    workers = workers or threads
     L.hko_bench_rounds.restype = ctypes.c_int64
     L.hko_bench_rounds.argtypes = [ctypes.c_void_p, ctypes.POINTER(Config), ctypes.c_int, ctypes.c_int,
                                    ctypes.c_double, ctypes.POINTER(HkoZipf), ctypes.c_uint32, ctypes.c_int,
                                    ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
                                    ctypes.POINTER(ctypes.c_double)]
+    probe = {}
     try:
         hz = HkoZipf(zipf.theta, zipf.zetan, zipf.alpha, zipf.eta, zipf.half_pow, zipf.n)
         rounds, secs = ctypes.c_int64(0), ctypes.c_double(0.0)
-        committed = L.hko_bench_rounds(h, ctypes.byref(cfg), workers, threads, seconds, ctypes.byref(hz),
-                                       write_permille, n_peers, per_peer, seed, int(refill_flags), ctypes.byref(rounds),
-                                       ctypes.byref(secs))
+
+        def run(t, w, s):
+            return L.hko_bench_rounds(h, ctypes.byref(cfg), w, t, s, ctypes.byref(hz), write_permille, n_peers,
+                                      per_peer, seed, int(refill_flags), ctypes.byref(rounds), ctypes.byref(secs))
+        if not threads:
+            top = host_threads()
+            for t in sorted({1, 4, 8, top} & set(range(1, top + 1))):
+                probe[t] = run(t, workers or t, min(1.5, seconds / 8)) / secs.value
+            threads = max(probe, key=probe.get)
+        workers = workers or threads
+        committed = run(threads, workers, seconds)
     finally:
         snap.close()
     return {"value": committed / secs.value, "unit": "ops/s", "cores": threads, "kind": "port",
+            "probe_ops_per_s_by_threads": probe,
             "sample": (f"{threads} worker threads sharing one table (per-key seqlocks, concur_ctrl.h:144-224), "
                        f"{workers} x 250-op {'fresh' if refill_flags & 1 else 'retried (refill_ops)'} local batches "
                        f"per round, refill flags {refill_flags}, skew flags {c.skew_flags}, "

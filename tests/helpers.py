@@ -94,15 +94,21 @@ class Mirror:
             self.codes[(int(btype), tag, x)] += c
 
     def batch(self, btype, elems, n_batches, stride, elem_size, membership, counts=None, rw=None,
-              rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None, state_out=None, opcode_in=None):
+              rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None, state_out=None, opcode_in=None,
+              patch=None, rw_state=None):
         import torch
         if offsets is not None:
             return self._packed(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
-                                rw_stride_bytes)
+                                rw_stride_bytes, rw_state)
         torch.cuda.synchronize()
         n = n_batches * stride * elem_size
         vt = np.dtype((np.void, elem_size))
-        e_in = elems[:n].cpu().numpy().copy().view(vt)
+        e_in = elems[:n].cpu().numpy().copy()
+        if patch is not None:   # the pending refill the launch applies first (hkv_batch_desc.d_patch)
+            from tests.test_workload_gpu import _apply_patches
+            e_in = _apply_patches(e_in, patch[: n_batches * stride * 16].cpu().numpy(), elem_size,
+                                  self.g.sizes.st_value)
+        e_in = e_in.view(vt)
         c_in = counts[:n_batches].cpu().numpy().copy() if counts is not None else None
         if opcode_in is not None:   # the caller's opcode mirror must be every element's opcode byte
             assert np.array_equal(opcode_in[: n_batches * stride].cpu().numpy(),
@@ -111,8 +117,10 @@ class Mirror:
         rw_in = rw_op = None
         if rw is not None:
             rw_in = rw.cpu().numpy().copy().view(np.dtype((np.void, self.g.sizes.op)))
+            st_before = rw_in.view(np.uint8).reshape(-1, self.g.sizes.op)[:, 9].copy()
+        rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
         self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
-                   node_suspected, stream, state_out=state_out, opcode_in=opcode_in)
+                   node_suspected, stream, state_out=state_out, opcode_in=opcode_in, patch=patch, rw_state=rw_state)
         torch.cuda.synchronize()
         self.o.batch_multi(int(btype), e_in, n_batches, stride, c_in, membership, rw_in,
                            rw_stride_bytes // self.g.sizes.op if rw is not None else 0)
@@ -126,6 +134,7 @@ class Mirror:
         if rw is not None:
             rw_op = rw.cpu().numpy()
             assert np.array_equal(rw_op, rw_in.view(np.uint8)), f"{what}: read_write_ops differ"
+            self._check_rw_state(rw_state, rws_in, st_before, rw_op.reshape(-1, self.g.sizes.op)[:, 9], what)
         gl, ol = self.g.log_bytes(), self.o.log_bytes()[: self.g.cfg.log_cap]
         if not np.array_equal(gl, ol):
             bad = np.nonzero(gl != ol)[0]
@@ -139,8 +148,17 @@ class Mirror:
             assert np.array_equal(mirror, got.reshape(-1, elem_size)[:, 9]), f"{what}: state mirror differs"
         self.launches += 1
 
+    def _check_rw_state(self, rw_state, rws_in, st_before, st_after, what):
+        """d_rw_state: every completion the launch wrote into read_write_ops is in the mirror too, so a
+        mirror that matched the ops' state bytes before the launch still matches them after it"""
+        if rw_state is None:
+            return
+        n = min(len(st_before), len(rws_in))
+        assert np.array_equal(rws_in[:n], st_before[:n]), f"{what}: the caller's state mirror was already stale"
+        assert np.array_equal(rw_state.cpu().numpy()[:n], st_after[:n]), f"{what}: read_write_ops state mirror differs"
+
     def _packed(self, btype, elems, n_batches, total, elem_size, membership, offsets, stream, rw=None,
-                rw_stride_bytes=0):
+                rw_stride_bytes=0, rw_state=None):
         """A packed (HKV_BATCH_PACKED) INV / ACK / VAL launch: the oracle applies the same batches
         laid out in rows; the device's packed output must equal the oracle's rows packed again."""
         import torch
@@ -155,8 +173,10 @@ class Mirror:
         rows[pos] = flat
         self._count(btype, "in8", 8, rows.reshape(-1), n_batches, width, elem_size, cnt)
         rw_in = rw.cpu().numpy().copy().view(np.dtype((np.void, self.g.sizes.op))) if rw is not None else None
+        st_before = rw_in.view(np.uint8).reshape(-1, self.g.sizes.op)[:, 9].copy() if rw is not None else None
+        rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
         self._orig(btype, elems, n_batches, total, elem_size, membership, rw=rw, rw_stride_bytes=rw_stride_bytes,
-                   stream=stream, offsets=offsets)
+                   stream=stream, offsets=offsets, rw_state=rw_state)
         torch.cuda.synchronize()
         e_in = rows.reshape(-1).view(np.dtype((np.void, elem_size))).copy()
         self.o.batch_multi(int(btype), e_in, n_batches, width, cnt, membership, rw_in,
@@ -172,7 +192,9 @@ class Mirror:
             bad = np.nonzero((got != want).any(axis=1))[0]
             pytest.fail(f"{what}: elements differ at {len(bad)} elements, first {bad[:8]}")
         if rw is not None:
-            assert np.array_equal(rw.cpu().numpy(), rw_in.view(np.uint8)), f"{what}: read_write_ops differ"
+            rw_op = rw.cpu().numpy()
+            assert np.array_equal(rw_op, rw_in.view(np.uint8)), f"{what}: read_write_ops differ"
+            self._check_rw_state(rw_state, rws_in, st_before, rw_op.reshape(-1, self.g.sizes.op)[:, 9], what)
         gl, ol = self.g.log_bytes(), self.o.log_bytes()[: self.g.cfg.log_cap]
         if not np.array_equal(gl, ol):
             bad = np.nonzero(gl != ol)[0]

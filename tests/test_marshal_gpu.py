@@ -212,10 +212,12 @@ def test_marshal_memb_vals():
     d_ops = _dev(ops.reshape(-1))
     d_out = torch.zeros(W * C * 16, dtype=torch.uint8, device="cuda")
     d_cnt = torch.zeros(W, dtype=torch.int32, device="cuda")
-    WL.check(_L.hkv_wl_marshal_memb_vals(WL._ptr(d_ops), W, S, osz, WL._ptr(d_out), C, WL._ptr(d_cnt), mid, None),
-             "memb_vals")
+    d_st = _dev(ops[:, :, 9].reshape(-1).copy())   # the state mirror follows the ops
+    WL.check(_L.hkv_wl_marshal_memb_vals(WL._ptr(d_ops), W, S, osz, WL._ptr(d_out), C, WL._ptr(d_cnt), mid,
+                                         WL._ptr(d_st), None), "memb_vals")
     torch.cuda.synchronize()
     got_ops = d_ops.cpu().numpy().reshape(W, S, osz)
+    assert np.array_equal(d_st.cpu().numpy(), got_ops[:, :, 9].reshape(-1)), "state mirror differs"
     got_out, got_cnt = d_out.cpu().numpy().reshape(W, C, 16), d_cnt.cpu().numpy()
     for w in range(W):
         k = 0

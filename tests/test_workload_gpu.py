@@ -442,11 +442,67 @@ def test_refill_kernel_matches_numpy(big, flags):
     assert np.array_equal(d_opc.cpu().numpy(), exp_ops.reshape(W * S, osz)[:, 8])
 
 
+def _apply_patches(ops, patch, osz, st_value):
+    """d_patch applied in numpy (include/hermeskv.h: the 16-B layout and what applying does)"""
+    ops = ops.copy().reshape(-1, osz)
+    p = patch.reshape(-1, 16)
+    for i in np.nonzero(p[:, 14])[0]:
+        o = ops[i]
+        o[0:8] = p[i, 0:8]
+        o[8], o[9], o[10] = p[i, 8], 141, p[i, 9]
+        if p[i, 13]:
+            o[11:16] = 0
+        o[16:18] = p[i, 10:12]
+        if p[i, 12]:
+            o[18:18 + st_value] = p[i, 12]
+    return ops.reshape(-1)
+
+
+@pytest.mark.parametrize("flags", [0, 1, 2])
+def test_refill_plan_matches_refill(flags):
+    """hkv_wl_refill_plan + the next local launch's patches give exactly what hkv_wl_refill gives:
+    the numpy refill restatement's ops after applying the plan's patches (numpy), the same cursors,
+    counters and opcode mirror; non-refilled ops get invalid patches."""
+    from hermes_amd import workload as WL
+    sz = L.DEFAULT
+    W, S, osz, tlen, mid = 37, 250, sz.op, 300, 2
+    rng = np.random.default_rng(77 + flags)
+    states = np.array([130, 128, 138, 137, 119, 121, 131, 132, 136, 140, 141, *IN_FLIGHT], dtype=np.uint8)
+    ops = rng.integers(0, 256, size=W * S * osz, dtype=np.uint8)
+    ops.reshape(W, S, osz)[:, :, 9] = rng.choice(states, size=(W, S))
+    tkey = rng.integers(0, 2**63, size=W * tlen, dtype=np.int64)
+    top = rng.choice(np.array([111, 112, 113], dtype=np.uint8), size=W * tlen)
+    cursor = rng.integers(0, tlen, size=W, dtype=np.int32)
+    exp_ops, exp_cur, exp_cnt = _refill_ref(ops, W, S, osz, sz.st_value, sz.shift, tkey.view(np.uint64), top, tlen,
+                                            cursor, mid, False, flags)
+    d_st = torch.from_numpy(ops.reshape(W * S, osz)[:, 9].copy()).cuda()
+    d_tkey, d_top = torch.from_numpy(tkey).cuda(), torch.from_numpy(top).cuda()
+    d_cur = torch.from_numpy(cursor.copy()).cuda()
+    d_cnt = torch.zeros(4096, dtype=torch.int64, device="cuda")
+    opc0 = ops.reshape(W * S, osz)[:, 8].copy()
+    d_opc = torch.from_numpy(opc0.copy()).cuda()
+    d_patch = torch.full((W * S * 16,), 0xAB, dtype=torch.uint8, device="cuda")   # stale bytes get overwritten
+    WL.check(WL._L.hkv_wl_refill_plan(WL._ptr(d_st), W, S, sz.st_value, sz.shift, WL._ptr(d_tkey), WL._ptr(d_top),
+                                      tlen, WL._ptr(d_cur), mid, flags, WL._ptr(d_cnt), WL._ptr(d_opc),
+                                      WL._ptr(d_patch), None), "refill_plan")
+    WL.check(WL._L.hkv_wl_fold_counters(WL._ptr(d_cnt), None), "fold")
+    torch.cuda.synchronize()
+    patch = d_patch.cpu().numpy()
+    assert set(np.unique(patch.reshape(-1, 16)[:, 14]).tolist()) <= {0, 1}
+    got = _apply_patches(ops, patch, osz, sz.st_value)
+    assert np.array_equal(got, exp_ops), "patched ops differ from the refill"
+    assert np.array_equal(d_cur.cpu().numpy(), exp_cur)
+    assert d_cnt[:5].cpu().tolist() == exp_cnt.tolist()
+    assert np.array_equal(d_opc.cpu().numpy(), exp_ops.reshape(W * S, osz)[:, 8])
+
+
+@pytest.mark.parametrize("mirror", [False, True])
 @pytest.mark.parametrize("big", [False, True])
-def test_marshal_invs_kernel_matches_numpy(big):
+def test_marshal_invs_kernel_matches_numpy(big, mirror):
     """hkv_wl_marshal_invs_cap (per-thread 16-B copies for 56-B ops, one wave-wide copy per op for
     312-B ops) against a numpy restatement of inv_skip_or_get_sender_id /
-    inv_copy_and_modify_elem / inv_modify_elem_after_send (hermes_worker.c:12-65) with C credits."""
+    inv_copy_and_modify_elem / inv_modify_elem_after_send (hermes_worker.c:12-65) with C credits;
+    with the state mirror, it is read instead of the ops and follows their new states."""
     from hermes_amd import workload as WL
     sz = L.BIG if big else L.DEFAULT
     W, S, osz, C, mid = 29, 250, sz.op, 40, 3
@@ -476,9 +532,12 @@ def test_marshal_invs_kernel_matches_numpy(big):
     d_out = torch.zeros(W * C * osz, dtype=torch.uint8, device="cuda")
     d_cnt = torch.zeros(W, dtype=torch.int32, device="cuda")
     d_held = torch.zeros(1, dtype=torch.int64, device="cuda")
+    d_st = torch.from_numpy(ops.reshape(W * S, osz)[:, 9].copy()).cuda() if mirror else None
     WL.check(WL._L.hkv_wl_marshal_invs_cap(WL._ptr(d_ops), W, S, osz, WL._ptr(d_out), C, WL._ptr(d_cnt), mid,
-                                           WL._ptr(d_held), None, None), "marshal_invs")
+                                           WL._ptr(d_held), WL._ptr(d_st), None), "marshal_invs")
     torch.cuda.synchronize()
+    if mirror:
+        assert np.array_equal(d_st.cpu().numpy(), exp_ops.reshape(W * S, osz)[:, 9]), "state mirror differs"
     cnt = d_cnt.cpu().numpy()
     assert np.array_equal(cnt, exp_cnt)
     out = d_out.cpu().numpy().reshape(W, C, osz)

@@ -1,5 +1,5 @@
 """HBM bytes per local batch launch from a tools/pmc.sh run (FETCH_SIZE and WRITE_SIZE passes):
-    python tools/pmc_local.py TAG OUT.json
+    python tools/pmc_local.py TAG OUT.json [WORKERS KEYS REFILL SKEW]
 
 A local launch is k_local_pre, k_local_fused, k_local_deferred and the k_commit after them (the
 direct path), or, on the rounds engine, the two k_lookup dispatches before a k_resolve0<0, ...>
@@ -53,6 +53,9 @@ def main():
         "write_bytes": statistics.median(wl),
     }
     res["traffic_bytes"] = res["fetch_bytes"] + res["write_bytes"]
+    if len(sys.argv) > 6:   # the bench configuration the counters belong to (bench.py checks it)
+        res["config"] = {"workers": int(sys.argv[3]), "keys": int(sys.argv[4]), "refill": sys.argv[5],
+                         "skew": int(sys.argv[6])}
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res))
 

@@ -98,6 +98,7 @@ struct BatchArgs {
     const uint8_t *patch;        // local direct path: pending header writes (hkv_batch_desc.d_patch), or NULL
     uint8_t *rws;                // ACK launches: read_write_ops state mirror (hkv_batch_desc.d_rw_state), or NULL
     int32_t dbg;                 // HKV_DBG: timing experiments that skip work (results invalid)
+    int32_t check_unique;        // HKV_CHECK_UNIQUE: HKV_BATCH_UNIQUE launches verify their keys are unique
 };
 
 // Rounds after round 0 per batch type: how often a hot key usually mutates in one launch beyond
@@ -1380,6 +1381,83 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
     }
 }
 
+// ------------------------------------------------------------------ launches with unique keys
+// HKV_BATCH_UNIQUE: no key appears twice among the launch's elements, so every element is its key's
+// only one and sees S_0 in any serial order: after k_lookup's lookup (four lanes per element, two
+// elements per lane group) lane 0 of the group runs the exec function on the element and the entry
+// in place and stores the meta back -- one pass, each entry line read and written once. (INV
+// launches: a peer's round slab, see hermeskv.h.) With check_unique every element also swaps its
+// index into its key's F word, tagged with the launch; finding the launch's tag there means a
+// second element of the key (error bit 4).
+template <int TYPE, int SV>
+__global__ __launch_bounds__(256) void k_unique(BatchArgs a)
+{
+    const int q = threadIdx.x & 3;
+    const int gbase = (threadIdx.x & 63) & ~3;
+    int64_t gi[kLookupPair];
+    uint64_t key[kLookupPair], hdr[kLookupPair];
+    bool probe[kLookupPair];
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        gi[k] = ((int64_t)blockIdx.x * kLookupPair + k) * 64 + (threadIdx.x >> 2);
+        uint64_t kk = 0, hh = 0;
+        bool p = false;
+        if (gi[k] < a.n && q == 0) {
+            int64_t start = 0;
+            int32_t b = 0;
+            bool in = true;
+            if (a.offsets) {
+                b = batch_of(a, gi[k], start);
+            } else {
+                b = (int32_t)(gi[k] / a.stride);
+                start = (int64_t)b * a.stride;
+                in = a.counts == nullptr || gi[k] - start < a.counts[b];
+            }
+            if (in) {
+                const U64x2 h = *reinterpret_cast<const U64x2 *>(a.elems + gi[k] * a.esz);
+                kk = h.a;
+                hh = h.b;
+                if (skip_elem_os(TYPE, (uint8_t)hh, (uint8_t)(hh >> 8))) {
+                    if (TYPE == kInvs && a.ns_idx) atomicMax(&a.ns_idx[b], (int32_t)(gi[k] - start));
+                } else {
+                    p = true;
+                }
+            }
+        }
+        key[k] = (uint64_t)(uint32_t)__shfl((int)(uint32_t)kk, 0, 4) | ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(kk >> 32), 0, 4) << 32);
+        probe[k] = __shfl((int)p, 0, 4) != 0;
+        hdr[k] = hh;
+    }
+    bool ok[kLookupPair];
+    uint64_t phys[kLookupPair];
+    uint4 ln[kLookupPair];
+    lookup_pair(a, key, probe, q, gbase, ok, phys, ln);
+    Meta m[kLookupPair];
+    uint64_t ek[kLookupPair];
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) ek[k] = line_key_meta(ln[k], m[k]);
+    if (q != 0) return;
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        if (!probe[k]) continue;
+        uint8_t *x = a.elems + gi[k] * a.esz;
+        if (!(ok[k] && ek[k] == key[k])) {
+            x[9] = kMiss;
+            continue;
+        }
+        if (a.check_unique) {
+            const unsigned long long v = ((unsigned long long)(~a.rtag0) << 32) | (uint32_t)gi[k];
+            const unsigned long long old = atomicExch(a.fw + fw_index(a, phys[k]), v);
+            if ((uint32_t)(old >> 32) == ~a.rtag0 && a.error_flags) atomicOr(a.error_flags, 16u);
+        }
+        uint8_t *entry = a.log + phys[k];
+        Ctx c = make_ctx(a);
+        Meta t = m[k];
+        dispatch<SV>(TYPE, x, entry, 0, t, c);
+        if (!meta_equal(t, m[k])) meta_store(entry, t);
+    }
+}
+
 // Elements of keys that were INVALID at S_0, against their key's final F (k_resolve0_direct's rules)
 __global__ __launch_bounds__(256) void k_local_deferred(BatchArgs a)
 {
@@ -2059,6 +2137,8 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.rws = bl.type == kAcks ? bl.rw_state : nullptr;
     static const int dbg_env = getenv("HKV_DBG") ? atoi(getenv("HKV_DBG")) : 0;
     a.dbg = dbg_env;
+    static const int check_unique_env = getenv("HKV_CHECK_UNIQUE") ? atoi(getenv("HKV_CHECK_UNIQUE")) : 0;
+    a.check_unique = check_unique_env;
     if (dbg_env) a.error_flags = nullptr;
     a.index = bl.index;
     a.log = bl.log;
@@ -2130,6 +2210,12 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
         hipLaunchKernelGGL(k_local_fused, dim3((unsigned)((n + kLfElems - 1) / kLfElems)), dim3(64), 0, s, a);
         hipLaunchKernelGGL(k_local_deferred, dim3(8), dim3(256), 0, s, a);
         hipLaunchKernelGGL((k_commit<31>), dim3(grid), dim3(256), 0, s, a);
+    } else if (bl.unique && bl.type == kInvs) {  // one pass: every key has one element
+        constexpr int64_t kPerU = 64 * kLookupPair;
+        const unsigned ugrid = (unsigned)((n + kPerU - 1) / kPerU);
+        if (bl.g.st_value == 31) hipLaunchKernelGGL((k_unique<kInvs, 31>), dim3(ugrid), dim3(256), 0, s, a);
+        else if (bl.g.st_value == 287) hipLaunchKernelGGL((k_unique<kInvs, 287>), dim3(ugrid), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_unique<kInvs, 0>), dim3(ugrid), dim3(256), 0, s, a);
     } else if (bl.type == kVals) {             // one pass (see k_lookup)
         hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, n);
         return hipGetLastError() == hipSuccess ? 0 : -3;

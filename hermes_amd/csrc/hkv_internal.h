@@ -44,6 +44,7 @@ struct BatchLaunch {
     uint8_t g_membership;
     uint8_t w_ack_init;
     int32_t path;                             // kPath*: which engine runs the launch
+    int32_t unique;                           // HKV_BATCH_UNIQUE: no key twice in the launch
     // small launches staged in host memory (the combining submit of hermes_batch_ops_to_KVS): the
     // kernel first copies region_bytes from host_src to dev_region (where elems, counts, rw and
     // node_suspected point), at the end copies them back to host_dst, then stores done_value into

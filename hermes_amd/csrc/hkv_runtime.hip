@@ -476,6 +476,7 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.w_ack_init = d->membership[2];
     bl.path = (d->flags & HKV_BATCH_ENGINE) || packed ? kPathEngine
             : (d->flags & HKV_BATCH_SMALL) ? kPathSmall : kPathAuto;
+    bl.unique = (d->flags & HKV_BATCH_UNIQUE) && d->type == kInvs ? 1 : 0;
     TRACE("batch_async type=%d n=%lld", d->type, (long long)n);
     rc = launch_batch(bl, s);
     if (rc) return fail(rc, "batch launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));

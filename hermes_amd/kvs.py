@@ -85,6 +85,7 @@ def sized_geometry(num_keys: int, sizes: L.Sizes = L.DEFAULT) -> tuple[int, int]
 BATCH_ENGINE = 1   # hkv_batch_desc.flags (include/hermeskv.h): the multi-kernel engine
 BATCH_SMALL = 2    # the single-workgroup kernel (launches of at most 4096 elements)
 BATCH_PACKED = 4   # INV / VAL batches back to back, d_counts = n_batches + 1 offsets
+BATCH_UNIQUE = 8   # no key twice in the launch (INV batches: one pass)
 
 
 class HermesKV:
@@ -168,13 +169,15 @@ class HermesKV:
               rw_stride_bytes: int = 0, node_suspected: torch.Tensor | None = None,
               stream: torch.cuda.Stream | None = None, offsets: torch.Tensor | None = None,
               state_out: torch.Tensor | None = None, opcode_in: torch.Tensor | None = None,
-              patch: torch.Tensor | None = None, rw_state: torch.Tensor | None = None) -> None:
+              patch: torch.Tensor | None = None, rw_state: torch.Tensor | None = None,
+              unique: bool = False) -> None:
         """Apply n_batches batches of one type, concatenated in `elems` (uint8, on the GPU),
         in concatenation order, asynchronously on `stream` (default: torch's current).
         offsets (INV / ACK / VAL batches): the batches stored back to back, batch b at elements
         [offsets[b], offsets[b+1]); `stride` is then the total (HKV_BATCH_PACKED). patch (local
         batches): 16 B per element of pending header writes (hkv_batch_desc.d_patch); rw_state (ACK
-        batches): the read_write_ops' state-byte mirror, kept up to date by the completions."""
+        batches): the read_write_ops' state-byte mirror, kept up to date by the completions. unique
+        (INV batches): no key appears twice in the launch (HKV_BATCH_UNIQUE, one pass)."""
         assert elems.is_cuda and elems.dtype == torch.uint8
         total = stride if offsets is not None else n_batches * stride
         assert elems.numel() >= total * elem_size
@@ -183,7 +186,7 @@ class HermesKV:
         d.n_batches = int(n_batches)
         d.stride = int(stride)
         d.elem_size = int(elem_size)
-        d.flags = self.default_flags
+        d.flags = self.default_flags | (BATCH_UNIQUE if unique else 0)
         d.d_elems = elems.data_ptr()
         if state_out is not None:   # local batches: the mirror of each element's final state byte
             assert state_out.is_cuda and state_out.dtype == torch.uint8 and state_out.numel() >= n_batches * stride
@@ -220,7 +223,7 @@ class HermesKV:
     def batch_host(self, btype: int, elems: np.ndarray, membership: bytes, rw: np.ndarray | None = None,
                    n_batches: int = 1, stride: int | None = None, counts: np.ndarray | None = None,
                    rw_stride_elems: int = 0, node_suspected: np.ndarray | None = None,
-                   offsets: np.ndarray | None = None) -> None:
+                   offsets: np.ndarray | None = None, unique: bool = False) -> None:
         """Round-trip numpy arrays through the device path (parity tests). offsets: packed INV /
         VAL batches (HKV_BATCH_PACKED), batch b = elems[offsets[b]:offsets[b+1]]."""
         dev = torch.device("cuda", self.device)
@@ -232,7 +235,7 @@ class HermesKV:
             tr = torch.from_numpy(rw.view(np.uint8).reshape(-1).copy()).to(dev) if rw is not None else None
             self.batch(btype, t, n_batches, len(elems), elems.dtype.itemsize, membership, rw=tr,
                        rw_stride_bytes=rw_stride_elems * (rw.dtype.itemsize if rw is not None else 0),
-                       node_suspected=tn, offsets=to)
+                       node_suspected=tn, offsets=to, unique=unique)
             torch.cuda.synchronize(dev)
             elems.view(np.uint8).reshape(-1)[:] = t.cpu().numpy()
             if rw is not None:
@@ -250,7 +253,7 @@ class HermesKV:
         tr = torch.from_numpy(rw.view(np.uint8).reshape(-1).copy()).to(dev) if rw is not None else None
         tn = torch.from_numpy(np.ascontiguousarray(node_suspected, dtype=np.int32)).to(dev) if node_suspected is not None else None
         self.batch(btype, t, n_batches, stride, esz, membership, tc, tr,
-                   rw_stride_elems * (rw.dtype.itemsize if rw is not None else 0), tn, state_out=st)
+                   rw_stride_elems * (rw.dtype.itemsize if rw is not None else 0), tn, state_out=st, unique=unique)
         torch.cuda.synchronize(dev)
         elems.view(np.uint8).reshape(-1)[:] = t.cpu().numpy()
         if st is not None and not np.array_equal(st.cpu().numpy(),

@@ -207,7 +207,12 @@ class ReplicaRound:
             return
         if self.count_elems:
             self.elem_totals[0] += self.inv_totals.sum()
-        self.kvs.batch(L.BatchType.invs, self.inv_recv, self.N, width, self.op, self.mb, counts=self.inv_totals)
+        # one launch per peer, in rank order: a peer's slab holds at most one INV per key (one write in
+        # flight per key and coordinator), so each applies in one pass (HKV_BATCH_UNIQUE)
+        for p in range(self.N):
+            if p != self.rank:
+                self.kvs.batch(L.BatchType.invs, self.inv_recv[p * width * self.op:], 1, width, self.op, self.mb,
+                               counts=self.inv_totals[p:p + 1], unique=True)
         check(_L.hkv_wl_marshal_acks_aligned(_ptr(self.inv_recv), _ptr(self.inv_totals), self.N, width, self.op,
                                              _ptr(self.ack_slab), self.ack_size, self.rank, _s()), "marshal_acks")
 
@@ -333,6 +338,11 @@ class ReplicaGroupRound:
     def _gather(self, out, inp):
         self.dist.all_gather_into_tensor(out, inp, group=self.group)
 
+    def _gather_async(self, out, inp):
+        """the same all-gather, returned unwaited: the collective runs on the backend's stream (RCCL's
+        own) while torch's stream goes on; work.wait() orders the consumer after it"""
+        return self.dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True)
+
     def _a2a(self, out, inp):
         self.dist.all_to_all_single(out, inp, group=self.group)
 
@@ -393,6 +403,16 @@ class ReplicaGroupRound:
         _timed(events, "invs", lambda: r.invs(width), timed_batches)
         self._a2a(*r.ack_io(width))
         _timed(events, "acks", lambda: r.acks(width, stride), timed_batches)
+        if not self.hades and drop is None:
+            # the VAL exchange overlaps the refill: the refill touches only this replica's op slab and
+            # its mirrors, the VAL batch only the table, so their order does not matter
+            w_tot = self._gather_async(*r.val_total_io())
+            w_val = self._gather_async(*r.val_io(width))
+            r.refill()
+            w_tot.wait()
+            w_val.wait()
+            _timed(events, "vals", lambda: r.vals(width), timed_batches)
+            return
         self._gather(*r.val_total_io())
         self._gather(*r.val_io(width))
         _timed(events, "vals", lambda: r.vals(width), timed_batches)

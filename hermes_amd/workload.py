@@ -273,21 +273,30 @@ class Round:
             self.remote_inv.append(ri)
             self.remote_val.append(rv)
             if self.pack_remote:
-                # the same elements back to back (HKV_BATCH_PACKED): rounds where every peer is live
-                # launch over the live INVs / VALs only, not the slabs' empty slots
-                full = self.remote_counts[-1][R]
-                off = torch.zeros(W + 1, dtype=torch.int32, device=dev)
-                torch.cumsum(full, 0, dtype=torch.int32, out=off[1:])
-                total = int(off[W].item())
-                pi = torch.empty(max(total, 1) * self.op, **u8)
-                pv = torch.empty(max(total, 1) * L.OP_META_SIZE, **u8)
-                check(_L.hkv_wl_pack_rows(_ptr(ri), _ptr(full), W, self.rstride, self.op, _ptr(pi), _ptr(off), _s()),
-                      "pack remote invs")
-                check(_L.hkv_wl_pack_rows(_ptr(rv), _ptr(full), W, self.rstride, L.OP_META_SIZE, _ptr(pv), _ptr(off),
-                                          _s()), "pack remote vals")
+                # the same elements back to back (HKV_BATCH_PACKED), peer-major: rounds where every peer
+                # is live launch over the live INVs / VALs only, not the slabs' empty slots, and each
+                # peer's INVs -- at most one per key, as a coordinator has one write per key in flight --
+                # go in a launch of their own with HKV_BATCH_UNIQUE (one pass). Batch r * W + w holds
+                # peer r's elements of worker w's row. (Drawn once per round index, outside timed steps.)
+                pcw = pc.view(W, R).long()
+                start = torch.cumsum(pcw, dim=1) - pcw                 # where peer r starts in row w
+                cnt = pcw.t().reshape(-1)                              # batch (r, w), peer-major
+                off = torch.zeros(R * W + 1, dtype=torch.int64, device=dev)
+                torch.cumsum(cnt, 0, out=off[1:])
+                total = int(off[-1].item())
+                b = torch.repeat_interleave(torch.arange(R * W, device=dev), cnt)
+                j = torch.arange(total, device=dev) - off[b]
+                r_, w_ = b // W, b % W
+                src = w_ * self.rstride + start.t().reshape(-1)[b] + j   # element of the row layout
+                pi = ri.view(-1, self.op)[src].reshape(-1) if total else torch.empty(self.op, **u8)
+                pv = rv.view(-1, L.OP_META_SIZE)[src].reshape(-1) if total else torch.empty(L.OP_META_SIZE, **u8)
+                off32 = off.to(torch.int32)
+                base = [int(off[r * W].item()) for r in range(R + 1)]
+                per_peer = [(base[r], base[r + 1] - base[r], (off[r * W:(r + 1) * W + 1] - base[r]).to(torch.int32))
+                            for r in range(R)]
                 phys = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
                 check(_L.hkv_wl_peer_locate(self.kvs.h, _ptr(pi), total, self.op, _ptr(phys), _s()), "peer_locate")
-                self.remote_packed.append((pi, pv, off, total, phys))
+                self.remote_packed.append((pi, pv, off32, total, phys, per_peer))
         del scratch
 
     # -- pieces of one round
@@ -334,13 +343,21 @@ class Round:
 
     def peer_timestamps_packed(self, k: int):
         """the same for the packed slabs, whose INVs' entries were located when they were drawn"""
-        pi, pv, _, total, phys = self.remote_packed[k]
+        pi, pv, _, total, phys, _ = self.remote_packed[k]
         check(_L.hkv_wl_peer_ts_at(self.kvs.h, _ptr(pi), _ptr(pv), _ptr(phys), total, self.op, _ptr(self.peer_ts),
                                    self.clock, _s()), "peer_ts_at")
 
     def inv_batch(self, invs: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None,
-                  offsets: torch.Tensor | None = None):
-        self.kvs.batch(L.BatchType.invs, invs, n_batches, stride, self.op, self.mb, counts=counts, offsets=offsets)
+                  offsets: torch.Tensor | None = None, unique: bool = False):
+        self.kvs.batch(L.BatchType.invs, invs, n_batches, stride, self.op, self.mb, counts=counts, offsets=offsets,
+                       unique=unique)
+
+    def inv_batches_per_peer(self, k: int):
+        """Every peer's INVs of round index k as a launch of its own (HKV_BATCH_UNIQUE), in peer order"""
+        pi, _, _, _, _, per_peer = self.remote_packed[k]
+        for base, n, off in per_peer:
+            if n:
+                self.inv_batch(pi[base * self.op:], self.W, n, offsets=off, unique=True)
 
     def marshal_acks(self, invs: torch.Tensor, n: int, out: torch.Tensor):
         check(_L.hkv_wl_marshal_acks(_ptr(invs), n, self.op, _ptr(out), self.ack_size, self.machine_id, _s()),
@@ -451,8 +468,8 @@ class Round:
             ri, rv = self.remote_inv[k], self.remote_val[k]
             ic = self._slot_counts(k, sent)
             if packed:
-                pi, pv, off, total, _ = self.remote_packed[k]
-                timed("invs", lambda: self.inv_batch(pi, self.W, total, offsets=off))
+                pi, pv, off, total, _, _ = self.remote_packed[k]
+                timed("invs", lambda: self.inv_batches_per_peer(k))
                 self.marshal_acks(pi, total, self.ack_out)
             else:
                 timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride, counts=ic))
@@ -489,7 +506,7 @@ class Round:
             # a dropped peer sent its INVs but fails before its VALs
             vc = self._slot_counts(k, alive)
             if packed:
-                timed("vals", lambda: self.val_batch(pv, self.W, total, offsets=off))
+                timed("vals", lambda: self.val_batch(pv, self.R * self.W, total, offsets=off))
             else:
                 timed("vals", lambda: self.val_batch(rv, self.W, self.rstride, counts=vc))
             if self.count_elems:

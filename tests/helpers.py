@@ -95,11 +95,11 @@ class Mirror:
 
     def batch(self, btype, elems, n_batches, stride, elem_size, membership, counts=None, rw=None,
               rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None, state_out=None, opcode_in=None,
-              patch=None, rw_state=None):
+              patch=None, rw_state=None, unique=False):
         import torch
         if offsets is not None:
             return self._packed(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
-                                rw_stride_bytes, rw_state)
+                                rw_stride_bytes, rw_state, unique)
         torch.cuda.synchronize()
         n = n_batches * stride * elem_size
         vt = np.dtype((np.void, elem_size))
@@ -109,6 +109,7 @@ class Mirror:
             e_in = _apply_patches(e_in, patch[: n_batches * stride * 16].cpu().numpy(), elem_size,
                                   self.g.sizes.st_value)
         e_in = e_in.view(vt)
+        e_orig = e_in.copy()
         c_in = counts[:n_batches].cpu().numpy().copy() if counts is not None else None
         if opcode_in is not None:   # the caller's opcode mirror must be every element's opcode byte
             assert np.array_equal(opcode_in[: n_batches * stride].cpu().numpy(),
@@ -120,7 +121,8 @@ class Mirror:
             st_before = rw_in.view(np.uint8).reshape(-1, self.g.sizes.op)[:, 9].copy()
         rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
         self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
-                   node_suspected, stream, state_out=state_out, opcode_in=opcode_in, patch=patch, rw_state=rw_state)
+                   node_suspected, stream, state_out=state_out, opcode_in=opcode_in, patch=patch, rw_state=rw_state,
+                   unique=unique)
         torch.cuda.synchronize()
         self.o.batch_multi(int(btype), e_in, n_batches, stride, c_in, membership, rw_in,
                            rw_stride_bytes // self.g.sizes.op if rw is not None else 0)
@@ -130,7 +132,12 @@ class Mirror:
         self._count(btype, "out9", 9, got, n_batches, stride, elem_size, c_in)
         if not np.array_equal(got, e_in.view(np.uint8)):
             bad = np.nonzero(got != e_in.view(np.uint8))[0]
-            pytest.fail(f"{what}: elements differ at {len(bad)} bytes, first elems {np.unique(bad // elem_size)[:8]}")
+            rows = np.unique(bad // elem_size)[:4]
+            show = "; ".join(f"elem {r}: in {e_orig.view(np.uint8).reshape(-1, elem_size)[r][:24].tolist()} "
+                             f"dev {got.reshape(-1, elem_size)[r][:24].tolist()} "
+                             f"oracle {e_in.view(np.uint8).reshape(-1, elem_size)[r][:24].tolist()}" for r in rows)
+            pytest.fail(f"{what}: elements differ at {len(bad)} bytes, first elems {np.unique(bad // elem_size)[:8]}"
+                        f" -- {show}")
         if rw is not None:
             rw_op = rw.cpu().numpy()
             assert np.array_equal(rw_op, rw_in.view(np.uint8)), f"{what}: read_write_ops differ"
@@ -158,7 +165,7 @@ class Mirror:
         assert np.array_equal(rw_state.cpu().numpy()[:n], st_after[:n]), f"{what}: read_write_ops state mirror differs"
 
     def _packed(self, btype, elems, n_batches, total, elem_size, membership, offsets, stream, rw=None,
-                rw_stride_bytes=0, rw_state=None):
+                rw_stride_bytes=0, rw_state=None, unique=False):
         """A packed (HKV_BATCH_PACKED) INV / ACK / VAL launch: the oracle applies the same batches
         laid out in rows; the device's packed output must equal the oracle's rows packed again."""
         import torch
@@ -176,7 +183,7 @@ class Mirror:
         st_before = rw_in.view(np.uint8).reshape(-1, self.g.sizes.op)[:, 9].copy() if rw is not None else None
         rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
         self._orig(btype, elems, n_batches, total, elem_size, membership, rw=rw, rw_stride_bytes=rw_stride_bytes,
-                   stream=stream, offsets=offsets, rw_state=rw_state)
+                   stream=stream, offsets=offsets, rw_state=rw_state, unique=unique)
         torch.cuda.synchronize()
         e_in = rows.reshape(-1).view(np.dtype((np.void, elem_size))).copy()
         self.o.batch_multi(int(btype), e_in, n_batches, width, cnt, membership, rw_in,

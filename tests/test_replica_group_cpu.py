@@ -43,6 +43,7 @@ class TagReplica:
         self.count_elems = True
         self.checked = 0
         self.round = 0
+        self.pending = 0
 
     def dead(self, p, after=False):
         """p has failed by this round (after=True: before this round's INVs)"""
@@ -67,6 +68,11 @@ class TagReplica:
         return [(w, j) for w in range(self.W) for j in range(self.count(origin, w))]
 
     def local(self):
+        # the refill may run before the round's VAL batch (ReplicaGroupRound overlaps it with the
+        # VAL exchange): the next round starts here
+        self.round += self.pending
+        self.pending = 0
+        self.in_memb = False
         self._pack(self.inv_pack, self.inv_off, 1)
 
     def fail(self):
@@ -149,8 +155,7 @@ class TagReplica:
                 self.checked += 1
 
     def refill(self):
-        self.round += 1
-        self.in_memb = False
+        self.pending += 1
 
 
 def _worker(rank, world, port, rounds, q, drop=None):

@@ -1452,8 +1452,13 @@ __global__ __launch_bounds__(256) void k_unique(BatchArgs a)
         }
         uint8_t *entry = a.log + phys[k];
         Ctx c = make_ctx(a);
+        uint8_t idx = 0;
+        if (TYPE == kAcks) {   // the element's batch: its read_write_ops and their state mirror
+            uint8_t *xx;
+            elem_at(a, (uint32_t)gi[k], xx, idx, c);
+        }
         Meta t = m[k];
-        dispatch<SV>(TYPE, x, entry, 0, t, c);
+        dispatch<SV>(TYPE, x, entry, idx, t, c);
         if (!meta_equal(t, m[k])) meta_store(entry, t);
     }
 }
@@ -1784,7 +1789,8 @@ __device__ __forceinline__ uint32_t small_slot(uint32_t *hkey, uint32_t e)
 // the batch b with bstart[b] <= i < bstart[b + 1].
 struct SmallView {
     uint8_t *x;
-    uint8_t idx;
+    uint8_t idx;      // op buffer index (local batches: < 256)
+    int32_t pos;      // the element's position in its batch (INV batches run to 900 and beyond)
     int type;
     int b;
     bool live;
@@ -1799,6 +1805,7 @@ __device__ __forceinline__ SmallView small_at(const BatchArgs &a, const int32_t 
         const int32_t b = i / a.stride, idx = i - b * a.stride;
         v.x = a.elems + (int64_t)i * a.esz;
         v.idx = (uint8_t)idx;
+        v.pos = idx;
         v.type = a.type;
         v.b = b;
         v.live = a.counts == nullptr || idx < a.counts[b];
@@ -1816,6 +1823,7 @@ __device__ __forceinline__ SmallView small_at(const BatchArgs &a, const int32_t 
     const int idx = i - bstart[lo];
     v.x = a.dev_region + h.elem_off + (int64_t)idx * h.esz;
     v.idx = (uint8_t)idx;
+    v.pos = idx;
     v.type = h.type;
     v.b = lo;
     v.live = true;
@@ -1880,7 +1888,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small(BatchArgs a)
         if (v.live) {
             const U64x2 h = *reinterpret_cast<const U64x2 *>(v.x);
             if (skip_elem_os(v.type, (uint8_t)h.b, (uint8_t)(h.b >> 8))) {
-                if (v.type == kInvs) atomicMax(&ns[v.b], (int)v.idx);   // hermes_skip_inv: the last one wins
+                if (v.type == kInvs) atomicMax(&ns[v.b], v.pos);   // hermes_skip_inv: the last one wins
             } else {
                 const uint64_t key = h.a;
                 const uint4 *bk = reinterpret_cast<const uint4 *>(a.index + ((key & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u);
@@ -2210,12 +2218,18 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
         hipLaunchKernelGGL(k_local_fused, dim3((unsigned)((n + kLfElems - 1) / kLfElems)), dim3(64), 0, s, a);
         hipLaunchKernelGGL(k_local_deferred, dim3(8), dim3(256), 0, s, a);
         hipLaunchKernelGGL((k_commit<31>), dim3(grid), dim3(256), 0, s, a);
-    } else if (bl.unique && bl.type == kInvs) {  // one pass: every key has one element
+    } else if (bl.unique && (bl.type == kInvs || bl.type == kAcks)) {  // one pass: every key has one element
         constexpr int64_t kPerU = 64 * kLookupPair;
         const unsigned ugrid = (unsigned)((n + kPerU - 1) / kPerU);
-        if (bl.g.st_value == 31) hipLaunchKernelGGL((k_unique<kInvs, 31>), dim3(ugrid), dim3(256), 0, s, a);
-        else if (bl.g.st_value == 287) hipLaunchKernelGGL((k_unique<kInvs, 287>), dim3(ugrid), dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_unique<kInvs, 0>), dim3(ugrid), dim3(256), 0, s, a);
+#define HKV_UNIQUE(T)                                                                                  \
+    do {                                                                                               \
+        if (bl.g.st_value == 31) hipLaunchKernelGGL((k_unique<T, 31>), dim3(ugrid), dim3(256), 0, s, a); \
+        else if (bl.g.st_value == 287) hipLaunchKernelGGL((k_unique<T, 287>), dim3(ugrid), dim3(256), 0, s, a); \
+        else hipLaunchKernelGGL((k_unique<T, 0>), dim3(ugrid), dim3(256), 0, s, a);                   \
+    } while (0)
+        if (bl.type == kInvs) HKV_UNIQUE(kInvs);
+        else HKV_UNIQUE(kAcks);
+#undef HKV_UNIQUE
     } else if (bl.type == kVals) {             // one pass (see k_lookup)
         hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, n);
         return hipGetLastError() == hipSuccess ? 0 : -3;

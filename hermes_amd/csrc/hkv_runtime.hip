@@ -420,7 +420,11 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     if (packed && !d->d_counts) return fail(-1, "HKV_BATCH_PACKED needs the batch offsets in d_counts");
     int64_t n = packed ? (int64_t)d->stride : (int64_t)d->n_batches * d->stride;
     if (n == 0 || d->n_batches == 0) return 0;
-    if ((uintptr_t)d->d_elems & 15) return fail(-1, "d_elems must be 16-byte aligned");
+    // 16-byte aligned slabs let the LDS-staged passes move whole 16-B words; a one-pass unique launch
+    // reads each element on its own (its 8-byte alignment suffices), so a peer's slab can start at
+    // any element of a larger buffer
+    if ((uintptr_t)d->d_elems & ((d->flags & HKV_BATCH_UNIQUE) ? 7 : 15))
+        return fail(-1, "d_elems must be 16-byte aligned (8 with HKV_BATCH_UNIQUE)");
     if (n > 0x7FFFFFFFll) return fail(-1, "too many elements in one launch");
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream, as in every HIP API
     int rc = ensure_batch_scratch(t, n);
@@ -476,7 +480,7 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.w_ack_init = d->membership[2];
     bl.path = (d->flags & HKV_BATCH_ENGINE) || packed ? kPathEngine
             : (d->flags & HKV_BATCH_SMALL) ? kPathSmall : kPathAuto;
-    bl.unique = (d->flags & HKV_BATCH_UNIQUE) && d->type == kInvs ? 1 : 0;
+    bl.unique = (d->flags & HKV_BATCH_UNIQUE) && (d->type == kInvs || d->type == kAcks) ? 1 : 0;
     TRACE("batch_async type=%d n=%lld", d->type, (long long)n);
     rc = launch_batch(bl, s);
     if (rc) return fail(rc, "batch launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));

@@ -656,16 +656,19 @@ __global__ __launch_bounds__(256) void k_regroup(const uint8_t *in, const int32_
 __global__ __launch_bounds__(64) void k_collect_vals(uint8_t *acks, const int32_t *count, int32_t stride,
                                                      uint32_t ack_size, uint8_t *out, int32_t C, int32_t *out_count,
                                                      uint32_t machine_id, unsigned long long *held,
-                                                     const int32_t *offsets)
+                                                     const int32_t *offsets, int32_t n_blocks)
 {
     // one wave per worker (a worker's round has a few dozen ACKs)
     const int64_t w = blockIdx.x;
     const int lane = (int)threadIdx.x;
-    // rows: worker w's ACKs at w * stride, count[w] of them; packed: [offsets[w], offsets[w+1])
+    // rows: worker w's ACKs at w * stride, count[w] of them; packed: [offsets[w], offsets[w+1]);
+    // n_blocks > 1: peer-major blocks of offsets[gridDim.x] elements, worker w's part in each
     const int n = offsets ? offsets[w + 1] - offsets[w] : count[w];
-    const int64_t row = offsets ? (int64_t)offsets[w] : w * stride;
+    const int64_t block = n_blocks > 1 ? (int64_t)offsets[gridDim.x] : 0;
     int base = 0;
+    for (int blk = 0; blk < n_blocks; ++blk)
     for (int j0 = 0; j0 < n; j0 += 64) {
+        const int64_t row = (offsets ? (int64_t)offsets[w] : w * stride) + blk * block;
         const int j = j0 + lane;
         uint8_t *x = acks + (row + j) * (int64_t)ack_size;
         const uint8_t oc = j < n ? x[8] : 0;
@@ -1066,7 +1069,8 @@ __device__ __forceinline__ void peer_answer(const uint8_t *x, uint8_t *y, uint32
 __global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32_t inv_stride, uint32_t op_size,
                             uint8_t *acks, uint32_t ack_size, int32_t out_stride, int32_t *ack_count,
                             const uint8_t *peers, int32_t n_peers, int64_t total, TableView t,
-                            const unsigned long long *peer_ts, uint32_t round, const int32_t *out_off)
+                            const unsigned long long *peer_ts, uint32_t round, const int32_t *out_off,
+                            int32_t pm_workers)
 {
     int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= total) return;
@@ -1078,7 +1082,10 @@ __global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32
     if (rem == 0 && ack_count) ack_count[w] = n * n_peers;
     if (j >= n) return;
     const uint8_t *x = invs + ((int64_t)w * inv_stride + j) * op_size;
-    const int64_t pos = out_off ? (int64_t)out_off[w] + rem : (int64_t)w * out_stride + rem;
+    // peer-major (pm_workers > 0): peer r's answers to every INV of the round as one block of
+    // T = out_off[pm_workers] elements, worker w's at out_off[w] in it
+    const int64_t pos = pm_workers > 0 ? (int64_t)r * out_off[pm_workers] + out_off[w] + j
+                      : out_off ? (int64_t)out_off[w] + rem : (int64_t)w * out_stride + rem;
     peer_answer(x, acks + pos * ack_size, op_size, ack_size, peers[r], t, peer_ts, round);
 }
 
@@ -1378,6 +1385,23 @@ int hkv_wl_marshal_vals(uint8_t *acks, int64_t n, uint32_t ack_size, uint8_t *ou
     return ok();
 }
 
+int hkv_wl_peer_acks_pm(hkv_table *t, const uint8_t *inv_out, const int32_t *inv_count, int32_t n_workers,
+                        int32_t inv_stride, uint32_t op_size, uint8_t *acks, uint32_t ack_size, int32_t max_invs,
+                        int32_t *ack_count, const uint8_t *peer_ids, int32_t n_peers,
+                        const unsigned long long *peer_ts, uint32_t round, const int32_t *inv_off, void *stream)
+{
+    if (n_peers <= 0 || n_workers <= 0 || ack_size < kOpMetaSize || ack_size % 8 || !inv_off) return -1;
+    if (max_invs <= 0 || max_invs > inv_stride) return -1;
+    TableView tv{};
+    if (peer_ts && table_view(t, &tv)) return -1;
+    const int32_t out_stride = max_invs * n_peers;
+    int64_t total = (int64_t)n_workers * out_stride;
+    hipLaunchKernelGGL(k_peer_acks, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, inv_out, inv_count,
+                       inv_stride, op_size, acks, ack_size, out_stride, ack_count, peer_ids, n_peers, total, tv,
+                       peer_ts, round, inv_off, n_workers);
+    return ok();
+}
+
 int hkv_wl_peer_acks(hkv_table *t, const uint8_t *inv_out, const int32_t *inv_count, int32_t n_workers,
                      int32_t inv_stride, uint32_t op_size, uint8_t *acks, uint32_t ack_size, int32_t out_stride,
                      int32_t *ack_count, const uint8_t *peer_ids, int32_t n_peers,
@@ -1390,7 +1414,7 @@ int hkv_wl_peer_acks(hkv_table *t, const uint8_t *inv_out, const int32_t *inv_co
     int64_t total = (int64_t)n_workers * out_stride;
     hipLaunchKernelGGL(k_peer_acks, dim3(blocks_for(total)), dim3(256), 0, (hipStream_t)stream, inv_out, inv_count,
                        inv_stride, op_size, acks, ack_size, out_stride, ack_count, peer_ids, n_peers, total, tv,
-                       peer_ts, round, out_off);
+                       peer_ts, round, out_off, 0);
     return ok();
 }
 
@@ -1518,10 +1542,18 @@ int hkv_wl_collect_vals(uint8_t *acks, const int32_t *count, int32_t n_workers, 
                         uint8_t *out, int32_t C, int32_t *out_count, uint32_t machine_id, unsigned long long *held,
                         const int32_t *offsets, void *stream)
 {
+    return hkv_wl_collect_vals_blocks(acks, count, n_workers, stride, ack_size, out, C, out_count, machine_id, held,
+                                      offsets, 1, stream);
+}
+
+int hkv_wl_collect_vals_blocks(uint8_t *acks, const int32_t *count, int32_t n_workers, int32_t stride,
+                               uint32_t ack_size, uint8_t *out, int32_t C, int32_t *out_count, uint32_t machine_id,
+                               unsigned long long *held, const int32_t *offsets, int32_t n_blocks, void *stream)
+{
     if (n_workers <= 0) return 0;
-    if (C <= 0 || ack_size % 8) return -1;
+    if (C <= 0 || ack_size % 8 || n_blocks < 1 || (n_blocks > 1 && !offsets)) return -1;
     hipLaunchKernelGGL(k_collect_vals, dim3(n_workers), dim3(64), 0, (hipStream_t)stream, acks, count, stride,
-                       ack_size, out, C, out_count, machine_id, held, offsets);
+                       ack_size, out, C, out_count, machine_id, held, offsets, n_blocks);
     return ok();
 }
 

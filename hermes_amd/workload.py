@@ -47,6 +47,10 @@ _L.hkv_wl_max_to_host.argtypes = [_P, ctypes.c_int32, _P, _P]
 _L.hkv_wl_marshal_vals.argtypes = [_P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_collect_vals.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
                                    _P, ctypes.c_uint32, _P, _P, _P]
+_L.hkv_wl_peer_acks_pm.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_uint32,
+                                   ctypes.c_int32, _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, _P, _P]
+_L.hkv_wl_collect_vals_blocks.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
+                                          _P, ctypes.c_uint32, _P, _P, ctypes.c_int32, _P]
 _L.hkv_wl_peer_acks.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_uint32,
                                 ctypes.c_int32, _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, _P, _P]
 _L.hkv_wl_peer_round_scratch.restype = ctypes.c_size_t
@@ -193,6 +197,12 @@ class Round:
         self._ack_flag = ctypes.c_int32.from_address(self.maxc_h.data_ptr() + 8) if self.fit else None
         self.ack_off = torch.zeros(W + 1, dtype=torch.int32, device=dev) if self.fit else None
         self.ack_total = 0
+        # peer-major ACKs (fit path): each virtual peer's answers to the round's INVs as one block,
+        # applied as a launch of its own with HKV_BATCH_UNIQUE (one ACK per key and peer: a key has at
+        # most one local write in flight); ack_off then holds the INV offsets and inv_round the INV total
+        self.ack_pm = self.fit and os.environ.get("HKV_ACK_PM", "1") != "0"
+        self.inv_round = 0
+        self.ack_m = self.C
         self.maxc_ev = torch.cuda.Event() if self.fit else None
         # HKV_ACKOFF_SIDE=1: the one-workgroup ACK-offsets scan runs on a side stream beside the INV batch
         self.ackoff_side = self.fit and self.ack_spin and os.environ.get("HKV_ACKOFF_SIDE", "0") == "1"
@@ -330,6 +340,12 @@ class Round:
     def virtual_peer_acks(self, n_peers: int | None = None):
         """ACKs (INV-aborts for RMWs a peer's own write beats) of the first n_peers virtual peers
         (default all) to this round's INVs"""
+        if self.ack_pm:
+            check(_L.hkv_wl_peer_acks_pm(self.kvs.h, _ptr(self.inv_out), _ptr(self.inv_count), self.W, self.C,
+                                         self.op, _ptr(self.acks), self.ack_size, self.ack_m,
+                                         _ptr(self.ack_count), _ptr(self.peer_t), self.R if n_peers is None else n_peers,
+                                         _ptr(self.peer_ts), self.clock, _ptr(self.ack_off), _s()), "peer_acks_pm")
+            return
         check(_L.hkv_wl_peer_acks(self.kvs.h, _ptr(self.inv_out), _ptr(self.inv_count), self.W, self.C, self.op,
                                   _ptr(self.acks), self.ack_size, self.ack_width, _ptr(self.ack_count),
                                   _ptr(self.peer_t), self.R if n_peers is None else n_peers, _ptr(self.peer_ts),
@@ -366,6 +382,13 @@ class Round:
     def ack_batch(self, acks: torch.Tensor | None = None, n_batches: int | None = None, stride: int | None = None,
                   counts: torch.Tensor | None = None):
         acks = self.acks if acks is None else acks
+        if self.fit and stride is None and self.ack_pm:   # one launch per peer, in peer order
+            T = self.inv_round
+            for r in range(self.ack_total // max(T, 1) if T else 0):
+                self.kvs.batch(L.BatchType.acks, acks[r * T * self.ack_size:], self.W, T, self.ack_size, self.mb,
+                               rw=self.ops, rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off,
+                               rw_state=self.states, unique=True)
+            return
         if self.fit and stride is None:   # this round's packed ACKs
             self.kvs.batch(L.BatchType.acks, acks, self.W, self.ack_total, self.ack_size, self.mb,
                            rw=self.ops, rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off,
@@ -382,6 +405,13 @@ class Round:
     def collect_vals(self):
         """VALs of the writes this round's ACK batch completed, compacted per worker (val_out
         [W][ack_stride], val_count): only the ACK slab's live elements are read."""
+        if self.ack_pm:
+            check(_L.hkv_wl_collect_vals_blocks(_ptr(self.acks), _ptr(self.ack_count), self.W, self.ack_width,
+                                                self.ack_size, _ptr(self.val_out), self.C, _ptr(self.val_count),
+                                                self.machine_id, None, _ptr(self.ack_off),
+                                                self.ack_total // max(self.inv_round, 1) if self.inv_round else 1,
+                                                _s()), "collect_vals")
+            return
         check(_L.hkv_wl_collect_vals(_ptr(self.acks), _ptr(self.ack_count), self.W, self.ack_width, self.ack_size,
                                      _ptr(self.val_out), self.C, _ptr(self.val_count), self.machine_id,
                                      None, _ptr(self.ack_off) if self.fit else None, _s()), "collect_vals")
@@ -456,12 +486,13 @@ class Round:
                 self.ao_start.record()
                 self.side2.wait_event(self.ao_start)
                 with torch.cuda.stream(self.side2):
-                    check(_L.hkv_wl_ack_offsets(_ptr(self.inv_count), self.W, alive, _ptr(self.ack_off),
-                                                _ptr(self.maxc_h), self._ack_seq, _s()), "ack_offsets")
+                    check(_L.hkv_wl_ack_offsets(_ptr(self.inv_count), self.W, 1 if self.ack_pm else alive,
+                                                _ptr(self.ack_off), _ptr(self.maxc_h), self._ack_seq, _s()),
+                          "ack_offsets")
                 self.ao_done.record(self.side2)
             else:
-                check(_L.hkv_wl_ack_offsets(_ptr(self.inv_count), self.W, alive, _ptr(self.ack_off),
-                                            _ptr(self.maxc_h), self._ack_seq, _s()), "ack_offsets")
+                check(_L.hkv_wl_ack_offsets(_ptr(self.inv_count), self.W, 1 if self.ack_pm else alive,
+                                            _ptr(self.ack_off), _ptr(self.maxc_h), self._ack_seq, _s()), "ack_offsets")
             if not self.ack_spin:
                 self.maxc_ev.record()
         if self.R:
@@ -489,6 +520,9 @@ class Round:
                 if self.ackoff_side:
                     torch.cuda.current_stream().wait_event(self.ao_done)
                 self.ack_total = int(self.maxc_h[0])
+                if self.ack_pm:   # the offsets counted INVs: one block of them per answering peer
+                    self.inv_round = self.ack_total
+                    self.ack_total *= alive
                 m = min(int(self.maxc_h[1]), self.C)
             if alive and self.V is not None:
                 self.peer_acks_queued(alive)
@@ -497,7 +531,8 @@ class Round:
                     self.elem_totals[1] += self.ack_count.sum()
                 self.vals_under_credits()
             elif alive:
-                self.ack_width = max(1, m) * alive
+                self.ack_m = max(1, m)
+                self.ack_width = self.ack_m * alive
                 self.virtual_peer_acks(alive)
                 timed("acks", self.ack_batch)
                 if self.count_elems:

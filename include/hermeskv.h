@@ -166,12 +166,13 @@ typedef struct hkv_batch_desc {
  * an ACK batch b still completes into d_rw + b * rw_stride_bytes. Same results as the row layout;
  * no empty slots to launch over. */
 #define HKV_BATCH_PACKED 4u
-/* The caller guarantees that no key appears twice among the launch's elements (INV launches): each
- * element is then its key's only one and is applied to the entry in a single pass, in any order.
- * A replica's INV slab of one round has this property (a coordinator has at most one write in
- * flight per key: hermes_exec_write stalls while op_buffer_index is set, hermesKV.c:331-344), so a
- * receiver applies each peer's slab as one such launch. A duplicate breaks the results; with
- * HKV_CHECK_UNIQUE=1 in the environment every launch checks and raises error flag bit 4. */
+/* The caller guarantees that no key appears twice among the launch's elements (INV and ACK
+ * launches): each element is then its key's only one and is applied to the entry in a single pass,
+ * in any order. A replica's INV slab of one round has this property (a coordinator has at most one
+ * write in flight per key: hermes_exec_write stalls while op_buffer_index is set,
+ * hermesKV.c:331-344), and so have one peer's ACKs to it, so a receiver applies each peer's slab as
+ * one such launch. A duplicate breaks the results; with HKV_CHECK_UNIQUE=1 in the environment every
+ * launch checks and raises error flag bit 4. */
 #define HKV_BATCH_UNIQUE 8u
 
 int  hkv_abi_version(void);

@@ -162,6 +162,15 @@ int hkv_wl_peer_acks(hkv_table *t, const uint8_t *d_inv_out, const int32_t *d_in
                      int32_t *d_ack_count, const uint8_t *peer_ids, int32_t n_peers,
                      const unsigned long long *d_peer_ts, uint32_t round, const int32_t *d_out_off, void *stream);
 
+/* The same answers laid out peer-major, for one HKV_BATCH_UNIQUE ACK launch per peer: peer r's
+ * answers to all INVs of the round form block r of T = d_inv_off[n_workers] elements, worker w's at
+ * d_inv_off[w] within it (d_inv_off: the INV offsets, hkv_wl_ack_offsets with n_peers = 1).
+ * max_invs >= every d_inv_count[w] (it sizes the grid). */
+int hkv_wl_peer_acks_pm(hkv_table *t, const uint8_t *d_inv_out, const int32_t *d_inv_count, int32_t n_workers,
+                        int32_t inv_stride, uint32_t op_size, uint8_t *d_acks, uint32_t ack_size, int32_t max_invs,
+                        int32_t *d_ack_count, const uint8_t *peer_ids, int32_t n_peers,
+                        const unsigned long long *d_peer_ts, uint32_t round, const int32_t *d_inv_off, void *stream);
+
 /* Offsets of a packed ACK batch answering d_inv_count[0..n_workers) INVs from n_peers peers:
  * d_offsets[w] = n_peers * (INVs of workers before w), d_offsets[n_workers] = the total. h_out
  * (pinned host memory, 3 ints) receives the total and the largest d_inv_count: seq = 0, once
@@ -215,6 +224,12 @@ int hkv_wl_regroup(const uint8_t *d_in, const int32_t *d_counts, int32_t n_peers
 int hkv_wl_collect_vals(uint8_t *d_acks, const int32_t *d_count, int32_t n_workers, int32_t stride,
                         uint32_t ack_size, uint8_t *d_val_out, int32_t C, int32_t *d_val_count,
                         uint32_t machine_id, unsigned long long *d_held, const int32_t *d_offsets, void *stream);
+/* The same over n_blocks peer-major blocks (hkv_wl_peer_acks_pm's layout: block b holds
+ * d_offsets[n_workers] elements, worker w's at d_offsets[w]); a worker's VALs in block order. */
+int hkv_wl_collect_vals_blocks(uint8_t *d_acks, const int32_t *d_count, int32_t n_workers, int32_t stride,
+                               uint32_t ack_size, uint8_t *d_val_out, int32_t C, int32_t *d_val_count,
+                               uint32_t machine_id, unsigned long long *d_held, const int32_t *d_offsets,
+                               int32_t n_blocks, void *stream);
 
 /* ---- VAL credits and the outstanding-VAL gate (hermes_worker.c:479-503, wings.h:424-540, 862-916)
  * Per worker: an ACK queue (d_aq rows of q_stride elements of ack_size bytes, d_aq_n queued) and a

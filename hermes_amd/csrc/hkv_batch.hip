@@ -1182,7 +1182,9 @@ __global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
     for (int k = 0; k < kAllK; ++k) {
         const bool own = k < kOwnK;
         const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
-        in[k] = in[k] && in_count(a, (uint32_t)i);
+        // a non-PUT read element 0's raw header, which a patch may have made stale: only the
+        // mirror's PUTs take part
+        in[k] = in[k] && opm[k] == kOpPut && in_count(a, (uint32_t)i);
     }
     if (a.dbg & 16) {
         uint64_t acc = 0;
@@ -2205,7 +2207,9 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     static const int ld_env = getenv("HKV_LOCAL_DIRECT") ? atoi(getenv("HKV_LOCAL_DIRECT")) : 1;
     const bool local_direct = ld_env != 0 && bl.type == kLocal && !bl.g.rmw_enabled && bl.esz == 56 &&
                               bl.g.st_value == 31 && bl.g.entry_size == 64 && !bl.offsets;
-    if (bl.patch && (small || !local_direct)) {  // the other paths take the patches as op writes first
+    // HKV_PATCH_APPLY=1: patches always written into the ops first (experiments)
+    static const bool patch_apply_env = getenv("HKV_PATCH_APPLY") && atoi(getenv("HKV_PATCH_APPLY")) != 0;
+    if (bl.patch && (small || !local_direct || patch_apply_env)) {  // the other paths take the patches as op writes first
         hipLaunchKernelGGL(k_apply_patch, dim3(grid), dim3(256), 0, s, bl.elems, bl.patch, n, bl.esz, bl.g.st_value);
     } else if (bl.patch) {
         a.patch = bl.patch;

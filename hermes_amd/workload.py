@@ -379,6 +379,11 @@ class Round:
         check(_L.hkv_wl_marshal_acks(_ptr(invs), n, self.op, _ptr(out), self.ack_size, self.machine_id, _s()),
               "marshal_acks")
 
+    def _rws(self):
+        """the state mirror the ACK batch keeps current (only the fused refill plans from it; the
+        VAL-credits marshal does not maintain it)"""
+        return self.states if self.fused else None
+
     def ack_batch(self, acks: torch.Tensor | None = None, n_batches: int | None = None, stride: int | None = None,
                   counts: torch.Tensor | None = None):
         acks = self.acks if acks is None else acks
@@ -387,16 +392,16 @@ class Round:
             for r in range(self.ack_total // max(T, 1) if T else 0):
                 self.kvs.batch(L.BatchType.acks, acks[r * T * self.ack_size:], self.W, T, self.ack_size, self.mb,
                                rw=self.ops, rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off,
-                               rw_state=self.states, unique=True)
+                               rw_state=self._rws(), unique=True)
             return
         if self.fit and stride is None:   # this round's packed ACKs
             self.kvs.batch(L.BatchType.acks, acks, self.W, self.ack_total, self.ack_size, self.mb,
                            rw=self.ops, rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off,
-                           rw_state=self.states)
+                           rw_state=self._rws())
             return
         self.kvs.batch(L.BatchType.acks, acks, n_batches or self.W, stride or self.ack_width, self.ack_size,
                        self.mb, counts=self.ack_count if counts is None else counts, rw=self.ops,
-                       rw_stride_bytes=self.LOCAL * self.op, rw_state=self.states)
+                       rw_stride_bytes=self.LOCAL * self.op, rw_state=self._rws())
 
     def marshal_vals(self, acks: torch.Tensor, n: int, out: torch.Tensor):
         check(_L.hkv_wl_marshal_vals(_ptr(acks), n, self.ack_size, _ptr(out), self.machine_id, _s()),

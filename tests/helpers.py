@@ -136,6 +136,13 @@ class Mirror:
             show = "; ".join(f"elem {r}: in {e_orig.view(np.uint8).reshape(-1, elem_size)[r][:24].tolist()} "
                              f"dev {got.reshape(-1, elem_size)[r][:24].tolist()} "
                              f"oracle {e_in.view(np.uint8).reshape(-1, elem_size)[r][:24].tolist()}" for r in rows)
+            # every element of the first bad element's key: index, opcode, state in / dev / oracle
+            eo = e_orig.view(np.uint8).reshape(-1, elem_size)
+            k0 = eo[rows[0], :8].tobytes()
+            same = np.nonzero((eo[:, :8] == eo[rows[0], :8]).all(axis=1))[0][:24]
+            gg, oo = got.reshape(-1, elem_size), e_in.view(np.uint8).reshape(-1, elem_size)
+            show += f" || key {k0.hex()} elems " + " ".join(
+                f"{j}:{eo[j, 8]}/{eo[j, 9]}->{gg[j, 9]}|{oo[j, 9]}" for j in same)
             pytest.fail(f"{what}: elements differ at {len(bad)} bytes, first elems {np.unique(bad // elem_size)[:8]}"
                         f" -- {show}")
         if rw is not None:

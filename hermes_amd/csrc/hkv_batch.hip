@@ -1465,6 +1465,120 @@ __global__ __launch_bounds__(256) void k_unique(BatchArgs a)
     }
 }
 
+// k_unique for 64-B entries: the lookup as in k_local_fused (one wave per block, four lanes per
+// element, each holding 16 B of the element and of the entry line), both staged in LDS, then one
+// lane per element runs the exec function on the LDS copies; each lane writes back its 16-B chunks
+// of the element and of the entry line that changed. The exec code touches LDS only, and the
+// global writes are whole 16-B words.
+__device__ __forceinline__ uint4 load_chunk(const uint8_t *x, int q, int32_t esz)
+{
+    if (16 * q + 16 <= esz) return *reinterpret_cast<const uint4 *>(x + 16 * q);
+    if (16 * q + 8 <= esz) {
+        const uint64_t t = *reinterpret_cast<const uint64_t *>(x + 16 * q);
+        return make_uint4((uint32_t)t, (uint32_t)(t >> 32), 0u, 0u);
+    }
+    return make_uint4(0u, 0u, 0u, 0u);
+}
+
+__device__ __forceinline__ bool chunk_equal(const uint4 &a, const uint4 &b)
+{
+    return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+}
+
+template <int TYPE>
+__global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
+{
+    __shared__ uint4 sops[kLfElems * 4];
+    __shared__ uint4 sln[kLfElems * 4];
+    __shared__ uint32_t sent[kLfElems];
+    __shared__ uint8_t sprb[kLfElems];
+    const int tid = threadIdx.x, q = tid & 3, gbase = tid & ~3;
+    const int64_t i0 = (int64_t)blockIdx.x * kLfElems;
+    uint64_t key[kLookupPair];
+    bool probe[kLookupPair], ok[kLookupPair], live[kLookupPair];
+    uint64_t phys[kLookupPair];
+    uint4 ln[kLookupPair], op[kLookupPair];
+    int te[kLookupPair];
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        te[k] = k * 16 + (tid >> 2);
+        const int64_t i = i0 + te[k];
+        live[k] = i < a.n;
+        op[k] = live[k] ? load_chunk(a.elems + i * a.esz, q, a.esz) : make_uint4(0u, 0u, 0u, 0u);
+        sops[te[k] * 4 + q] = op[k];
+    }
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        key[k] = (uint64_t)(uint32_t)__shfl((int)op[k].x, 0, 4) | ((uint64_t)(uint32_t)__shfl((int)op[k].y, 0, 4) << 32);
+        const uint32_t h0 = (uint32_t)__shfl((int)op[k].z, 0, 4);
+        probe[k] = false;
+        const int64_t i = i0 + te[k];
+        if (live[k] && (a.offsets || in_count(a, (uint32_t)i))) {
+            if (!skip_elem_os(TYPE, (uint8_t)h0, (uint8_t)(h0 >> 8))) {
+                probe[k] = true;
+            } else if (TYPE == kInvs && a.ns_idx && q == 0) {
+                int64_t start;
+                const int32_t b = batch_of(a, i, start);
+                atomicMax(&a.ns_idx[b], (int32_t)(i - start));
+            }
+        }
+    }
+    lookup_pair(a, key, probe, q, gbase, ok, phys, ln);
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        Meta m;
+        const uint64_t ek = line_key_meta(ln[k], m);
+        const bool hit = ok[k] && ek == key[k];
+        sln[te[k] * 4 + q] = ln[k];
+        if (q == 0) {
+            sent[te[k]] = hit ? (uint32_t)(phys[k] / a.g.entry_unit) : kNone;
+            sprb[te[k]] = probe[k];
+        }
+    }
+    __syncthreads();
+    if (tid < kLfElems && i0 + tid < a.n) {
+        const int64_t i = i0 + tid;
+        uint8_t *x = reinterpret_cast<uint8_t *>(&sops[tid * 4]);
+        uint8_t *ent = reinterpret_cast<uint8_t *>(&sln[tid * 4]);
+        const uint32_t e = sent[tid];
+        if (e != kNone) {
+            if (a.check_unique) {
+                const unsigned long long v = ((unsigned long long)(~a.rtag0) << 32) | (uint32_t)i;
+                const unsigned long long old = atomicExch(a.fw + fw_index(a, phys_of(a, e)), v);
+                if ((uint32_t)(old >> 32) == ~a.rtag0 && a.error_flags) atomicOr(a.error_flags, 16u);
+            }
+            Ctx c = make_ctx(a);
+            uint8_t idx = 0;
+            if (TYPE == kAcks) {   // the element's batch: its read_write_ops and their state mirror
+                uint8_t *xx;
+                elem_at(a, (uint32_t)i, xx, idx, c);
+            }
+            Meta m;
+            meta_load(ent, m);
+            Meta t = m;
+            dispatch<31>(TYPE, x, ent, idx, t, c);
+            if (!meta_equal(t, m)) meta_store(ent, t);
+        } else if (sprb[tid]) {
+            x[9] = kMiss;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        if (!live[k]) continue;
+        const uint4 w = sops[te[k] * 4 + q];
+        if (!chunk_equal(w, op[k])) {
+            uint8_t *xg = a.elems + (i0 + te[k]) * a.esz + 16 * q;
+            if (16 * q + 16 <= a.esz) *reinterpret_cast<uint4 *>(xg) = w;
+            else *reinterpret_cast<uint64_t *>(xg) = (uint64_t)w.x | ((uint64_t)w.y << 32);
+        }
+        if (ok[k] && q > 0) {   // bytes 0..15 of a log line (the MICA key) never change
+            const uint4 l = sln[te[k] * 4 + q];
+            if (!chunk_equal(l, ln[k])) reinterpret_cast<uint4 *>(a.log + phys[k])[q] = l;
+        }
+    }
+}
+
 // Elements of keys that were INVALID at S_0, against their key's final F (k_resolve0_direct's rules)
 __global__ __launch_bounds__(256) void k_local_deferred(BatchArgs a)
 {
@@ -2231,7 +2345,13 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
         else if (bl.g.st_value == 287) hipLaunchKernelGGL((k_unique<T, 287>), dim3(ugrid), dim3(256), 0, s, a); \
         else hipLaunchKernelGGL((k_unique<T, 0>), dim3(ugrid), dim3(256), 0, s, a);                   \
     } while (0)
-        if (bl.type == kInvs) HKV_UNIQUE(kInvs);
+        // 64-B entries: the LDS-staged pass (HKV_UNIQUE_LDS=0: the in-place one, experiments)
+        static const bool ulds_env = !getenv("HKV_UNIQUE_LDS") || atoi(getenv("HKV_UNIQUE_LDS")) != 0;
+        if (ulds_env && bl.g.st_value == 31 && bl.g.entry_size == 64 && bl.esz <= 64) {
+            const unsigned lgrid = (unsigned)((n + kLfElems - 1) / kLfElems);
+            if (bl.type == kInvs) hipLaunchKernelGGL(k_unique_lds<kInvs>, dim3(lgrid), dim3(64), 0, s, a);
+            else hipLaunchKernelGGL(k_unique_lds<kAcks>, dim3(lgrid), dim3(64), 0, s, a);
+        } else if (bl.type == kInvs) HKV_UNIQUE(kInvs);
         else HKV_UNIQUE(kAcks);
 #undef HKV_UNIQUE
     } else if (bl.type == kVals) {             // one pass (see k_lookup)

@@ -120,6 +120,7 @@ struct Ctx {           // per-launch constants
     uint8_t w_ack_init;
     uint8_t *rw;       // this element's batch read_write_ops (ACKs)
     uint8_t *rws;      // its state-byte mirror (hkv_batch_desc.d_rw_state), or null
+    int *rw_done;      // non-null: exec_ack leaves the read_write_ops completion to the caller
 };
 
 __device__ __forceinline__ bool is_last_ack(uint8_t bv, const Ctx &c)  // spacetime.h:253-259
@@ -329,7 +330,9 @@ __device__ __forceinline__ void exec_ack(uint8_t *ack, Meta &m, const Ctx &c)
             }
         }
     }
-    if ((ack[8] == kLastAckSuccess || ack[8] == kLastAckNoBcast) && done != kObiEmpty && c.rw != nullptr) {
+    if ((ack[8] == kLastAckSuccess || ack[8] == kLastAckNoBcast) && done != kObiEmpty && c.rw_done) {
+        *c.rw_done = done;   // the caller completes the slot (complete_rw_slot)
+    } else if ((ack[8] == kLastAckSuccess || ack[8] == kLastAckNoBcast) && done != kObiEmpty && c.rw != nullptr) {
         // every completer of this slot writes the same byte (it depends only on the slot's
         // own opcode), so concurrent segments completing one slot are benign
         uint8_t *w = c.rw + (size_t)done * c.g.op_size;
@@ -339,6 +342,17 @@ __device__ __forceinline__ void exec_ack(uint8_t *ack, Meta &m, const Ctx &c)
         if (c.rws) c.rws[done] = ns;
     }
     if (ack[8] != kLastAckSuccess) ack[8] = kAckSuccess;
+}
+
+// exec_ack's read_write_ops completion of slot `done` (hermesKV.c:660-668), for callers that find
+// the batch only for completing ACKs
+__device__ __forceinline__ void complete_rw_slot(const Ctx &c, int done)
+{
+    uint8_t *w = c.rw + (size_t)done * c.g.op_size;
+    const uint8_t oc = w[8];
+    const uint8_t ns = oc == kOpGet ? kNew : oc == kOpPut ? kPutComplete : oc == kOpRmw ? kRmwComplete : w[9];
+    w[9] = ns;
+    if (c.rws) c.rws[done] = ns;
 }
 
 // hermes_exec_val, hermesKV.c:676-703

@@ -442,31 +442,57 @@ __device__ __forceinline__ uint64_t with_op_state(uint64_t h, uint8_t op, uint8_
     return (h & ~0xFFFFull) | op | ((uint64_t)st << 8);
 }
 
+// ---- one wave per worker (stride <= 256: slot r * 64 + lane, four rows): ranks and counts come
+// from ballots, with no block barrier, so a CU holds 32 workers in flight instead of 8 -- these
+// kernels are a few dependent loads per worker, bound by latency, not bytes.
+__device__ __forceinline__ void wave_ranks(const unsigned long long *b, int lane, int *rank, int &total)
+{
+    const unsigned long long lower = (1ull << lane) - 1ull;
+    int before = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        rank[r] = before + __popcll(b[r] & lower);
+        before += __popcll(b[r]);
+    }
+    total = before;
+}
+
 // refill_ops as a plan (hkv_wl_refill_plan): the same decisions, cursors and counts as k_refill,
 // made from the state mirror (one byte per op instead of every op's line); each refilled
 // slot gets a patch (hkv_batch_desc.d_patch) that the next local launch applies as it reads the op,
 // so the op slab is read and written once per round (by that launch) instead of twice.
-__global__ __launch_bounds__(256) void k_refill_plan(const uint8_t *states, int32_t stride, uint32_t st_value,
-                                                     uint32_t shift, const uint64_t *tkey, const uint8_t *top,
-                                                     int32_t tlen, uint32_t *cursor, uint32_t machine_id,
-                                                     uint32_t flags, unsigned long long *counters, uint8_t *opc,
-                                                     uint8_t *patch)
+// One wave per worker.
+__global__ __launch_bounds__(256) void k_refill_plan_w(const uint8_t *states, int32_t n_workers, int32_t stride,
+                                                       uint32_t st_value, uint32_t shift, const uint64_t *tkey,
+                                                       const uint8_t *top, int32_t tlen, uint32_t *cursor,
+                                                       uint32_t machine_id, uint32_t flags,
+                                                       unsigned long long *counters, uint8_t *opc, uint8_t *patch)
 {
-    const int w = blockIdx.x, i = threadIdx.x;
-    const bool live = i < stride;
-    const int64_t e = (int64_t)w * stride + i;
-    const uint8_t st = live ? states[e] : 0;
-    const bool complete = is_complete(st);
-    const bool drop = live && (flags & HKV_WL_REFILL_ALL) && !complete && !in_flight(st);
-    const bool done = live && (complete || drop);
-    const int commits = (live && complete && st != kMiss && st != kRmwAbort) ? 1 : 0;
-    int total;
-    const int rank = block_rank(done, total);
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (w >= n_workers) return;
+    const int64_t e0 = (int64_t)w * stride;
+    uint8_t st[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st[r] = r * 64 + lane < stride ? states[e0 + r * 64 + lane] : 0;
     const uint32_t base = cursor[w];
-    const int c = block_sum(commits), m = block_sum(live && st == kMiss ? 1 : 0);
-    const int wr = block_sum(live && st == kPutComplete ? 1 : 0), dr = block_sum(drop ? 1 : 0);
-    const int ab = block_sum(live && st == kRmwAbort ? 1 : 0);
-    if (i == 0) {
+    unsigned long long bd[4];
+    int c = 0, m = 0, wr = 0, dr = 0, ab = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const bool live = r * 64 + lane < stride;
+        const bool complete = is_complete(st[r]);
+        const bool drop = live && (flags & HKV_WL_REFILL_ALL) && !complete && !in_flight(st[r]);
+        bd[r] = __ballot(live && (complete || drop));
+        c += __popcll(__ballot(live && complete && st[r] != kMiss && st[r] != kRmwAbort));
+        m += __popcll(__ballot(live && st[r] == kMiss));
+        wr += __popcll(__ballot(live && st[r] == kPutComplete));
+        dr += __popcll(__ballot(drop));
+        ab += __popcll(__ballot(live && st[r] == kRmwAbort));
+    }
+    int rank[4], total;
+    wave_ranks(bd, lane, rank, total);
+    if (lane == 0) {
         cursor[w] = (uint32_t)((base + (uint32_t)total) % (uint32_t)tlen);
         unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + (w % kStripes) * 16;
         if (c) atomicAdd(&stripe[0], (unsigned long long)c);
@@ -475,20 +501,74 @@ __global__ __launch_bounds__(256) void k_refill_plan(const uint8_t *states, int3
         if (dr) atomicAdd(&stripe[3], (unsigned long long)dr);
         if (ab) atomicAdd(&stripe[4], (unsigned long long)ab);
     }
-    if (!live) return;
-    W16 p{0, 0};
-    if (done) {
-        const int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)rank) % (uint32_t)tlen);
-        const uint8_t oc = top[t];
-        const bool get = oc == kOpGet;
-        p.a = tkey[t];
-        p.b = (uint64_t)oc | ((uint64_t)(get ? 0u : (uint8_t)(st_value >> shift)) << 8) |
-              ((uint64_t)((oc == kOpRmw ? 1u : 0u) | 2u) << 16) |             // RMW_flag, no_coales = 1
-              ((uint64_t)(get ? 0u : (uint8_t)('a' + machine_id)) << 32) |  // the written value
-              ((uint64_t)(get && (flags & HKV_WL_READ_TS_RESET) ? 1u : 0u) << 40) | (1ull << 48);
-        opc[e] = oc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = r * 64 + lane;
+        if (i >= stride) continue;
+        const int64_t e = e0 + i;
+        W16 p{0, 0};
+        if ((bd[r] >> lane) & 1ull) {
+            const int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)rank[r]) % (uint32_t)tlen);
+            const uint8_t oc = top[t];
+            const bool get = oc == kOpGet;
+            p.a = tkey[t];
+            p.b = (uint64_t)oc | ((uint64_t)(get ? 0u : (uint8_t)(st_value >> shift)) << 8) |
+                  ((uint64_t)((oc == kOpRmw ? 1u : 0u) | 2u) << 16) |
+                  ((uint64_t)(get ? 0u : (uint8_t)('a' + machine_id)) << 32) |
+                  ((uint64_t)(get && (flags & HKV_WL_READ_TS_RESET) ? 1u : 0u) << 40) | (1ull << 48);
+            opc[e] = oc;
+        }
+        *reinterpret_cast<W16 *>(patch + e * 16) = p;
     }
-    *reinterpret_cast<W16 *>(patch + e * 16) = p;
+}
+
+// k_marshal_invs for ops of at most 64 bytes, one wave per worker
+__global__ __launch_bounds__(256) void k_marshal_invs_w(uint8_t *ops, int32_t n_workers, int32_t stride,
+                                                        uint32_t op_size, uint8_t *out, int32_t out_stride,
+                                                        int32_t *count, uint32_t machine_id,
+                                                        unsigned long long *held, const int32_t *aq_n,
+                                                        int32_t r_alive, uint8_t *states)
+{
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (w >= n_workers) return;
+    const int64_t e0 = (int64_t)w * stride;
+    uint8_t st[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = r * 64 + lane;
+        st[r] = i < stride ? (states ? states[e0 + i] : ops[(e0 + i) * op_size + 9]) : 0;
+    }
+    unsigned long long bs[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        bs[r] = __ballot(r * 64 + lane < stride &&
+                         (st[r] == kPutSuccess || st[r] == kRmwSuccess || st[r] == kReplaySuccess ||
+                          st[r] == kOpMembChange));
+    int rank[4], total;
+    wave_ranks(bs, lane, rank, total);
+    const int cap = aq_n ? max(0, out_stride - aq_n[w] / max(1, r_alive)) : out_stride;
+    if (lane == 0) {
+        count[w] = total < cap ? total : cap;
+        if (total > cap && held) atomicAdd(held, (unsigned long long)(total - cap));
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        if (!((bs[r] >> lane) & 1ull) || rank[r] >= cap) continue;
+        const int64_t e = e0 + r * 64 + lane;
+        uint8_t *op = ops + e * op_size;
+        uint8_t *dst = out + ((int64_t)w * out_stride + rank[r]) * op_size;
+        const W16 h = *reinterpret_cast<const W16 *>(op);
+        *reinterpret_cast<W16 *>(dst) = W16{h.a, with_op_state(h.b, kOpInv, (uint8_t)machine_id)};
+        uint32_t k = 16;
+        for (; k + 16 <= op_size; k += 16) *reinterpret_cast<W16 *>(dst + k) = *reinterpret_cast<const W16 *>(op + k);
+        if (k < op_size) *reinterpret_cast<uint64_t *>(dst + k) = *reinterpret_cast<const uint64_t *>(op + k);
+        const uint8_t s = st[r];
+        const uint8_t ns = s == kPutSuccess ? kInProgressPut : s == kRmwSuccess ? kInProgressRmw
+                         : s == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
+        op[9] = ns;
+        if (states) states[e] = ns;
+    }
 }
 
 // wings_issue_pkts(inv) with the INV callbacks of hermes_worker.c:12-65. At most out_stride
@@ -1095,19 +1175,32 @@ __global__ void k_peer_acks(const uint8_t *invs, const int32_t *inv_count, int32
 __global__ __launch_bounds__(1024) void k_ack_offsets(const int32_t *counts, int32_t n, int32_t n_peers, int32_t *off,
                                                       int32_t *h, int32_t seq)
 {
-    // each thread owns 8 consecutive counts (one pass up to 8192 workers, loads issued together)
+    // each thread owns 16 consecutive counts (one pass up to 16384 workers, loads issued together)
     __shared__ int32_t part[16], pmax[16];
     __shared__ int32_t carry;
     if (threadIdx.x == 0) carry = 0;
     int32_t mx = 0;
-    for (int32_t i0 = 0; i0 < n; i0 += 8192) {
+    const bool vec = (((uintptr_t)counts | (uintptr_t)off) & 15u) == 0;
+    for (int32_t i0 = 0; i0 < n; i0 += 16384) {
         __syncthreads();
-        const int32_t b = i0 + (int32_t)threadIdx.x * 8;
-        int32_t c[8], sum = 0;
+        const int32_t b = i0 + (int32_t)threadIdx.x * 16;
+        int32_t c[16], sum = 0;
+        if (vec && b + 16 <= n) {
+            const int4 *p = reinterpret_cast<const int4 *>(counts + b);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) c[k] = b + k < n ? counts[b + k] : 0;
+            for (int k = 0; k < 4; ++k) {
+                const int4 v = p[k];
+                c[4 * k] = v.x;
+                c[4 * k + 1] = v.y;
+                c[4 * k + 2] = v.z;
+                c[4 * k + 3] = v.w;
+            }
+        } else {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+            for (int k = 0; k < 16; ++k) c[k] = b + k < n ? counts[b + k] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
             mx = c[k] > mx ? c[k] : mx;
             sum += c[k] * n_peers;
         }
@@ -1121,10 +1214,27 @@ __global__ __launch_bounds__(1024) void k_ack_offsets(const int32_t *counts, int
         int32_t run = carry;
         for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) run += part[k];
         run += v - sum;
+        if (vec && b + 16 <= n) {
+            int4 *q = reinterpret_cast<int4 *>(off + b);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (b + k < n) off[b + k] = run;
-            run += c[k] * n_peers;
+            for (int k = 0; k < 4; ++k) {
+                int4 o4;
+                o4.x = run;
+                run += c[4 * k] * n_peers;
+                o4.y = run;
+                run += c[4 * k + 1] * n_peers;
+                o4.z = run;
+                run += c[4 * k + 2] * n_peers;
+                o4.w = run;
+                run += c[4 * k + 3] * n_peers;
+                q[k] = o4;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                if (b + k < n) off[b + k] = run;
+                run += c[k] * n_peers;
+            }
         }
         __syncthreads();
         if (threadIdx.x == 1023) carry = run;
@@ -1347,8 +1457,9 @@ int hkv_wl_refill_plan(const uint8_t *states, int32_t n_workers, int32_t stride,
     if (stride > 256 || n_workers <= 0 || tlen <= 0 || !states || !opc || !patch) return -1;
     if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET)) return -1;   // no hot-request coalescing
     if (((uintptr_t)patch & 15) || st_value > 255) return -1;
-    hipLaunchKernelGGL(k_refill_plan, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, states, stride, st_value,
-                       shift, tkey, top, tlen, cursor, machine_id, flags, counters, opc, patch);
+    hipLaunchKernelGGL(k_refill_plan_w, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                       states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
+                       counters, opc, patch);
     return ok();
 }
 
@@ -1485,8 +1596,13 @@ int hkv_wl_marshal_invs_cap(uint8_t *ops, int32_t n_workers, int32_t stride, uin
                             uint8_t *states, void *stream)
 {
     if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
-    hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
-                       out_stride, count, machine_id, held, (const int32_t *)nullptr, 1, states);
+    if (op_size <= 64)
+        hipLaunchKernelGGL(k_marshal_invs_w, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                           ops, n_workers, stride, op_size, out, out_stride, count, machine_id, held,
+                           (const int32_t *)nullptr, 1, states);
+    else
+        hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
+                           out, out_stride, count, machine_id, held, (const int32_t *)nullptr, 1, states);
     return ok();
 }
 
@@ -1495,8 +1611,13 @@ int hkv_wl_marshal_invs_credits(uint8_t *ops, int32_t n_workers, int32_t stride,
                                 const int32_t *aq_n, int32_t r_alive, void *stream)
 {
     if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
-    hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size, out,
-                       out_stride, count, machine_id, held, aq_n, r_alive, (uint8_t *)nullptr);
+    if (op_size <= 64)
+        hipLaunchKernelGGL(k_marshal_invs_w, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                           ops, n_workers, stride, op_size, out, out_stride, count, machine_id, held, aq_n, r_alive,
+                           (uint8_t *)nullptr);
+    else
+        hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
+                           out, out_stride, count, machine_id, held, aq_n, r_alive, (uint8_t *)nullptr);
     return ok();
 }
 

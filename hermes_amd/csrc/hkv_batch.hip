@@ -203,6 +203,7 @@ __device__ __forceinline__ Ctx make_ctx(const BatchArgs &a)
     c.w_ack_init = a.w_ack_init;
     c.rw = nullptr;
     c.rws = nullptr;
+    c.rw_done = nullptr;
     return c;
 }
 
@@ -1548,16 +1549,19 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
                 if ((uint32_t)(old >> 32) == ~a.rtag0 && a.error_flags) atomicOr(a.error_flags, 16u);
             }
             Ctx c = make_ctx(a);
-            uint8_t idx = 0;
-            if (TYPE == kAcks) {   // the element's batch: its read_write_ops and their state mirror
-                uint8_t *xx;
-                elem_at(a, (uint32_t)i, xx, idx, c);
-            }
+            int done = -1;
+            if (TYPE == kAcks) c.rw_done = &done;   // the batch is found only for a completion
             Meta m;
             meta_load(ent, m);
             Meta t = m;
-            dispatch<31>(TYPE, x, ent, idx, t, c);
+            dispatch<31>(TYPE, x, ent, 0, t, c);
             if (!meta_equal(t, m)) meta_store(ent, t);
+            if (TYPE == kAcks && done >= 0 && a.rw) {   // its read_write_ops slot and state mirror
+                uint8_t *xx;
+                uint8_t idx;
+                elem_at(a, (uint32_t)i, xx, idx, c);
+                complete_rw_slot(c, done);
+            }
         } else if (sprb[tid]) {
             x[9] = kMiss;
         }

@@ -38,6 +38,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "hkv_exec.h"
 #include "hkv_internal.h"
@@ -2206,6 +2207,435 @@ int launch_small(const BatchArgs &a0, hipStream_t s)
         for (int p = 0; p < 5; ++p) prof_sum[p] += (double)(prof[p + 1] - prof[p]) * 10.0 / 1000.0;  // 100 MHz ticks -> us
         fprintf(stderr, "[hkv] k_small phases (us, avg of %ld): copy-in+init %.2f lookup %.2f rounds %.2f fallback %.2f copy-out %.2f\n", k,
                 prof_sum[0] / k, prof_sum[1] / k, prof_sum[2] / k, prof_sum[3] / k, prof_sum[4] / k);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// ------------------------------------------------------------------ partitioned host launches
+// The combining submit's launches on 64-B entries (HostPartLaunch, hkv_internal.h). Workgroup g
+// takes partition g of every batch: all elements of its keys, in element order, and no other
+// workgroup's. So the k_small rounds run per workgroup with no communication at all, and a
+// launch's latency stays that of one partition however many callers it combines:
+//   load    its slice of each batch straight from the callers' pinned buffers into LDS (one
+//           thread per element, four 16-B loads), with each element's position in its batch
+//   lookup  one thread per element (hermesKV.c:938-993): bucket, tag probe, wrap, the whole
+//           64-B entry line into LDS; the elements of one entry share the copy of its first one
+//   rounds  k_small's element-order rounds on the LDS copies (candidates lower their key's F,
+//           elements before F resolve on private metas, F applies to the shared copy); after
+//           kHpRounds the first pending element of a key finishes it serially
+//   store   changed entry lines back to HBM (the 48 bytes after the MICA key), every element back
+//           to its caller's buffer with system-scope stores, then flags[g] = seq
+// A completing ACK marks its read_write_ops slot in the caller's pinned copy directly (one byte,
+// system scope); node_suspected is the host's (hermes_skip_inv depends on the element alone).
+constexpr int kHpThreads = kPartCap;          // one element per thread
+constexpr int kHpSlots = 2 * kPartCap;        // entry-id hash slots
+constexpr int kHpRounds = 8;
+constexpr int kHpWords = kPartCap * 8 / kHpThreads;   // 8-byte words of elements per thread (esz <= 64)
+
+__device__ __forceinline__ uint32_t hp_slot(uint32_t *hkey, uint32_t e)
+{
+    uint32_t h = (e * 0x9E3779B1u) >> (32 - 9);   // kHpSlots = 2^9
+    for (;;) {
+        const uint32_t old = atomicCAS(&hkey[h], kNone, e);
+        if (old == kNone || old == e) return h;
+        h = (h + 1) & (kHpSlots - 1);
+    }
+}
+
+// Host memory the callers rewrite between launches is read with system-scope (uncached) loads: the
+// serving kernel (k_hserve) outlives many launches, so no kernel start invalidates stale lines for it.
+__device__ __forceinline__ uint64_t ld_sys64(const void *p)
+{
+    return __hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t ld_sys32(const void *p)
+{
+    return __hip_atomic_load(reinterpret_cast<const uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t ld_sys_u16(const uint16_t *p)   // 2-byte aligned
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    return (ld_sys32(reinterpret_cast<const void *>(a & ~(uintptr_t)3)) >> (8 * (a & 2))) & 0xFFFFu;
+}
+__device__ __forceinline__ uint32_t ld_sys_u8(const uint8_t *p)
+{
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    return (ld_sys32(reinterpret_cast<const void *>(a & ~(uintptr_t)3)) >> (8 * (a & 3))) & 0xFFu;
+}
+
+// exec_ack's read_write_ops completion of slot `done` in a caller's pinned copy (hermesKV.c:660-668)
+__device__ __forceinline__ void hp_complete_rw(uint8_t *rw, int done, uint32_t op_size)
+{
+    uint8_t *w = rw + (size_t)done * op_size;
+    const uint8_t oc = (uint8_t)ld_sys_u8(w + 8);
+    const uint8_t ns = oc == kOpGet ? kNew : oc == kOpPut ? kPutComplete : oc == kOpRmw ? kRmwComplete : (uint8_t)ld_sys_u8(w + 9);
+    __hip_atomic_store(w + 9, ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The LDS of one partition's work (both kernels)
+struct HpLds {
+    uint4 sel[kPartCap * 4];        // elements (64 B per slot, esz used)
+    uint4 sln[kPartCap * 4];        // entry lines; a key's elements use its first slot's
+    HostPartHdr bh[kPartMaxB];
+    int32_t base[kPartMaxB + 1], lo[kPartMaxB], wbase[kPartMaxB + 1];
+    uint16_t prow[2][kPartMaxB];    // part[g][*], part[g + 1][*]
+    uint32_t hkey[kHpSlots], hmin[kHpSlots], hf[kHpSlots];
+    uint8_t sdirty[kPartCap], spend[kPartCap];
+    uint16_t shs[kPartCap];
+    int cmd;
+    int32_t nb;
+};
+
+// The batch ranges of partition g (bh, prow in LDS): per-batch slot and word offsets (one wave)
+__device__ __forceinline__ void hp_scan(HpLds &L, int nb)
+{
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        int32_t c = 0, cw = 0;
+        if (tid < nb) {
+            const int32_t a0 = L.prow[0][tid], a1 = L.prow[1][tid];
+            L.lo[tid] = a0;
+            c = a1 - a0;
+            cw = c * (L.bh[tid].esz / 8);
+        }
+        int32_t incl = c, inclw = cw;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int32_t v = __shfl_up(incl, d, 64), vw = __shfl_up(inclw, d, 64);
+            if (tid >= d) {
+                incl += v;
+                inclw += vw;
+            }
+        }
+        if (tid < nb) {
+            L.base[tid + 1] = incl;
+            L.wbase[tid + 1] = inclw;
+        }
+        if (tid == 0) {
+            L.base[0] = 0;
+            L.wbase[0] = 0;
+        }
+    }
+}
+
+__device__ __forceinline__ int hp_batch_of(const int32_t *offs, int nb, int v)   // the last b with offs[b] <= v
+{
+    int l = 0, h = nb;
+    while (h - l > 1) {
+        const int mid = (l + h) >> 1;
+        if (offs[mid] <= v) l = mid;
+        else h = mid;
+    }
+    return l;
+}
+
+// Partition g of one launch whose headers and ranges are in L (after hp_scan and a barrier):
+// load, lookup, rounds, store back, then flags[g] = seq. See the section comment.
+__device__ void hp_partition(const HostPartCommon &p, HpLds &L, int g, int nb, uint32_t seq)
+{
+    const int tid = threadIdx.x;
+    const bool pr = p.prof && g == 0 && tid == 0;
+    if (pr) p.prof[1] = wall_clock64();
+    for (int j = tid; j < kHpSlots; j += kHpThreads) {
+        L.hkey[j] = kNone;
+        L.hmin[j] = kNone;
+        L.hf[j] = kNone;
+    }
+    const int P = L.base[nb];   // at most kPartCap (the host's check)
+    const int s = tid;
+    const bool live = s < P;
+    const int b = live ? hp_batch_of(L.base, nb, s) : 0;
+    const HostPartHdr &hd = L.bh[b];
+    const int64_t j = live ? (int64_t)L.lo[b] + (s - L.base[b]) : 0;
+    // the elements: each batch's slice is contiguous in its caller's buffer, so consecutive lanes
+    // copy consecutive 8-byte words of it (coalesced requests over PCIe), all loads in flight at once
+    const uint16_t pos = live ? (uint16_t)ld_sys_u16(reinterpret_cast<const uint16_t *>(hd.pos) + j) : (uint16_t)0;
+    {
+        const int TW = L.wbase[nb];   // at most kPartCap * 8
+        uint64_t w[kHpWords];
+        int dst[kHpWords];
+#pragma unroll
+        for (int r = 0; r < kHpWords; ++r) {
+            const int idx = tid + r * kHpThreads;
+            dst[r] = -1;
+            w[r] = 0;
+            if (idx < TW) {
+                const int l = hp_batch_of(L.wbase, nb, idx);
+                const int per = L.bh[l].esz / 8, wi = idx - L.wbase[l];
+                w[r] = ld_sys64(reinterpret_cast<const uint8_t *>(L.bh[l].elems) + ((int64_t)L.lo[l] * L.bh[l].esz + 8 * wi));
+                dst[r] = (L.base[l] + wi / per) * 8 + wi % per;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kHpWords; ++r)
+            if (dst[r] >= 0) reinterpret_cast<uint64_t *>(L.sel)[dst[r]] = w[r];
+    }
+    __syncthreads();
+    uint8_t *x = reinterpret_cast<uint8_t *>(&L.sel[s * 4]);
+    Ctx c;
+    c.g = p.g;
+    c.g_membership = hd.g_membership;
+    c.w_ack_init = hd.w_ack_init;
+    c.rw = reinterpret_cast<uint8_t *>(hd.rw);
+    c.rws = nullptr;
+    c.rw_done = nullptr;
+    const int type = hd.type;
+    // lookup (hermesKV.c:938-993)
+    uint32_t e = kNone;
+    uint64_t phys = 0;
+    if (live && !skip_elem_os(type, x[8], x[9])) {
+        const uint64_t key = *reinterpret_cast<const uint64_t *>(x);
+        const uint4 *bk = reinterpret_cast<const uint4 *>(p.index + ((key & 0xFFFFFFFFFFFFULL) & p.g.bkt_mask) * 64u);
+        const uint4 q0 = bk[0], q1 = bk[1], q2 = bk[2], q3 = bk[3];
+        const uint64_t sl[8] = {(uint64_t)q0.x | ((uint64_t)q0.y << 32), (uint64_t)q0.z | ((uint64_t)q0.w << 32),
+                                (uint64_t)q1.x | ((uint64_t)q1.y << 32), (uint64_t)q1.z | ((uint64_t)q1.w << 32),
+                                (uint64_t)q2.x | ((uint64_t)q2.y << 32), (uint64_t)q2.z | ((uint64_t)q2.w << 32),
+                                (uint64_t)q3.x | ((uint64_t)q3.y << 32), (uint64_t)q3.z | ((uint64_t)q3.w << 32)};
+        const uint32_t tag = (uint32_t)(key >> 48);
+        int hit = -1;
+#pragma unroll
+        for (int q = 7; q >= 0; --q)
+            if ((sl[q] & 1u) && ((uint32_t)(sl[q] >> 1) & 0x7FFFFFu) == tag) hit = q;
+        if (hit >= 0) {
+            const uint64_t off = sl[hit] >> 24;
+            if (p.g.log_head - off < p.g.log_cap) {
+                phys = off & p.g.log_mask;
+                const uint4 *ln = reinterpret_cast<const uint4 *>(p.log + phys);
+                const uint4 l0 = ln[0], l1 = ln[1], l2 = ln[2], l3 = ln[3];
+                if (((uint64_t)l0.z | ((uint64_t)l0.w << 32)) == key) {
+                    e = (uint32_t)(phys / p.g.entry_unit);
+                    L.sln[s * 4 + 0] = l0;
+                    L.sln[s * 4 + 1] = l1;
+                    L.sln[s * 4 + 2] = l2;
+                    L.sln[s * 4 + 3] = l3;
+                }
+            }
+        }
+        if (e == kNone) x[9] = kMiss;
+    }
+    if (pr) p.prof[2] = wall_clock64();
+    uint32_t hs = 0;
+    if (e != kNone) {
+        hs = hp_slot(L.hkey, e);
+        atomicMin(&L.hmin[hs], (uint32_t)s);
+    }
+    __syncthreads();
+    const int cs = e != kNone ? (int)L.hmin[hs] : s;   // the slot whose line copy the key's elements share
+    uint8_t *ent = reinterpret_cast<uint8_t *>(&L.sln[cs * 4]);
+    const uint8_t idx = (uint8_t)pos;
+    bool pend = e != kNone, dirty = false;
+    int done = -1;
+    c.rw_done = type == kAcks ? &done : nullptr;
+    bool any = true;
+    for (int r = 0;; ++r) {
+        any = __syncthreads_or(pend);
+        if (!any || r == kHpRounds) break;
+        Meta m;
+        if (pend) {
+            meta_load(ent, m);
+            if (would_mutate(type, x, m, c)) atomicMin(&L.hf[hs], (uint32_t)s);
+        }
+        __syncthreads();
+        if (pend && L.hf[hs] > (uint32_t)s) {   // before the key's candidate: S_r, unchanged
+            Meta t = m;
+            dispatch<31>(type, x, ent, idx, t, c);
+            if (p.error_flags && !meta_equal(t, m)) atomicOr(p.error_flags, 1u);
+            pend = false;
+        }
+        __syncthreads();   // every read of S_r precedes the mutation
+        if (pend && L.hf[hs] == (uint32_t)s) {  // the candidate: S_r -> S_{r+1}
+            dispatch<31>(type, x, ent, idx, m, c);
+            meta_store(ent, m);
+            L.hf[hs] = kNone;
+            dirty = true;
+            pend = false;
+        }
+    }
+    if (any) {  // keys that kept mutating: each key's first pending element finishes it in order
+        L.spend[s] = pend;
+        L.shs[s] = (uint16_t)hs;
+        __syncthreads();   // (every F of the last round was reset to kNone when it applied)
+        if (pend) atomicMin(&L.hf[hs], (uint32_t)s);
+        __syncthreads();
+        if (pend && L.hf[hs] == (uint32_t)s) {
+            Meta m;
+            meta_load(ent, m);
+            for (int k = s; k < P; ++k) {
+                if (!L.spend[k] || L.shs[k] != (uint16_t)hs) continue;   // hash slot = entry = key
+                uint8_t *xk = reinterpret_cast<uint8_t *>(&L.sel[k * 4]);
+                Ctx ck = c;
+                int dk = -1;
+                ck.rw_done = type == kAcks ? &dk : nullptr;
+                const int l = hp_batch_of(L.base, nb, k);   // the element's own batch
+                ck.g_membership = L.bh[l].g_membership;
+                ck.w_ack_init = L.bh[l].w_ack_init;
+                ck.rw = reinterpret_cast<uint8_t *>(L.bh[l].rw);
+                const int64_t jk = (int64_t)L.lo[l] + (k - L.base[l]);
+                const uint8_t ik = (uint8_t)ld_sys_u16(reinterpret_cast<const uint16_t *>(L.bh[l].pos) + jk);
+                dispatch<31>(L.bh[l].type, xk, ent, ik, m, ck);
+                if (dk >= 0 && ck.rw) hp_complete_rw(ck.rw, dk, p.g.op_size);
+            }
+            meta_store(ent, m);
+            dirty = true;
+        }
+    }
+    // a completing ACK of the rounds marks its read_write_ops slot (exec_ack left it to us)
+    if (done >= 0 && c.rw) hp_complete_rw(c.rw, done, p.g.op_size);
+    if (pr) p.prof[3] = wall_clock64();
+    L.sdirty[s] = 0;
+    __syncthreads();
+    if (dirty) L.sdirty[cs] = 1;
+    __syncthreads();
+    // the changed entry lines back to HBM (bytes 16..63: the MICA key never changes)
+    if (live && e != kNone && cs == s && L.sdirty[s]) {
+        uint4 *dst = reinterpret_cast<uint4 *>(p.log + phys);
+        dst[1] = L.sln[s * 4 + 1];
+        dst[2] = L.sln[s * 4 + 2];
+        dst[3] = L.sln[s * 4 + 3];
+    }
+    // every element back to its caller (consecutive lanes, consecutive words), then the flag (see
+    // k_small's copy-out)
+    for (int w = tid; w < L.wbase[nb]; w += kHpThreads) {
+        const int l = hp_batch_of(L.wbase, nb, w);
+        const int per = L.bh[l].esz / 8, wi = w - L.wbase[l];
+        unsigned long long *d = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(L.bh[l].elems) +
+                                                                       (int64_t)L.lo[l] * L.bh[l].esz) + wi;
+        __hip_atomic_store(d, (unsigned long long)reinterpret_cast<const uint64_t *>(L.sel)[(L.base[l] + wi / per) * 8 + wi % per],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (pr) p.prof[4] = wall_clock64();
+    if (tid == 0) __hip_atomic_store(p.flags + g, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One launch, its headers in the kernel arguments
+__global__ __launch_bounds__(kHpThreads) void k_hpart(HostPartLaunch p)
+{
+    __shared__ HpLds L;
+    const int tid = threadIdx.x, g = blockIdx.x, nb = p.n_batches;
+    if (p.c.prof && g == 0 && tid == 0) p.c.prof[0] = wall_clock64();
+    if (tid < nb) {
+        L.bh[tid] = p.hdr[tid];
+        L.prow[0][tid] = p.part[g][tid];
+        L.prow[1][tid] = p.part[g + 1][tid];
+    }
+    __syncthreads();
+    hp_scan(L, nb);
+    __syncthreads();
+    hp_partition(p.c, L, g, nb, p.seq);
+}
+
+// The serving kernel: workgroup g takes partition g of every launch published in the pinned ring,
+// in order, from p.start[g] on -- no kernel launch per combined batch. Thread 0 polls the next
+// slot's seq (uncached, backing off with s_sleep); the workgroup leaves when the host raises *stop,
+// after idle_ticks without a launch, or once life_ticks have passed (then between launches), and
+// records p.epoch in exited[g] so the host knows to launch a new server for what it publishes next.
+__global__ __launch_bounds__(kHpThreads) void k_hserve(HostServeLaunch p)
+{
+    __shared__ HpLds L;
+    const int tid = threadIdx.x, g = blockIdx.x;
+    uint32_t next = p.start[g];
+    const uint64_t t0 = wall_clock64();
+    uint64_t idle_since = t0;
+    for (;;) {
+        const HostRingSlot *sl = p.ring + (next % (uint32_t)p.ring_n);
+        if (tid == 0) {
+            int cmd = 0;
+            for (;;) {
+                if (ld_sys32(&sl->seq) == next) {
+                    cmd = 1;
+                    L.nb = (int32_t)ld_sys32(&sl->n_batches);
+                    break;
+                }
+                const uint64_t now = wall_clock64();
+                if (ld_sys32(p.stop) || now - idle_since > p.idle_ticks || now - t0 > p.life_ticks) {
+                    cmd = 2;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+            L.cmd = cmd;
+        }
+        __syncthreads();
+        if (L.cmd == 2) break;
+        const bool pr = p.c.prof && g == 0 && tid == 0;
+        const uint64_t t_seen = pr ? wall_clock64() : 0;
+        const int nb = L.nb;
+        if (tid < 6 * nb) {   // the headers, 8 bytes per thread
+            reinterpret_cast<uint64_t *>(L.bh)[tid] = ld_sys64(reinterpret_cast<const uint64_t *>(sl->hdr) + tid);
+        } else if (tid >= 128 && tid < 128 + 2 * (kPartMaxB / 4)) {   // part rows g and g + 1, 8 bytes per thread
+            const int k = tid - 128, row = k / (kPartMaxB / 4), wd = k % (kPartMaxB / 4);
+            reinterpret_cast<uint64_t *>(L.prow[row])[wd] = ld_sys64(reinterpret_cast<const uint64_t *>(sl->part[g + row]) + wd);
+        }
+        __syncthreads();
+        hp_scan(L, nb);
+        __syncthreads();
+        hp_partition(p.c, L, g, nb, next);
+        if (pr) {   // HKV_PART_PROF: workgroup 0's phase sums over the launches it served (debug)
+            unsigned long long *q = p.c.prof;
+            q[8] += t_seen - idle_since;
+            q[9] += q[1] - t_seen;
+            q[10] += q[2] - q[1];
+            q[11] += q[3] - q[2];
+            q[12] += q[4] - q[3];
+            q[13] += 1;
+        }
+        ++next;
+        idle_since = wall_clock64();
+        __syncthreads();   // LDS reuse by the next launch
+    }
+    if (tid == 0) __hip_atomic_store(p.exited + g, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+static unsigned long long *g_serve_prof = nullptr;
+static void serve_prof_print()
+{
+    const unsigned long long *q = g_serve_prof;
+    const double n = q[13] ? (double)q[13] : 1.0;
+    fprintf(stderr, "[hkv] k_hserve phases (us, avg of %llu launches, workgroup 0): wait %.2f headers %.2f load+lookup %.2f "
+            "rounds %.2f store %.2f\n", q[13], q[8] / n / 100.0, q[9] / n / 100.0, q[10] / n / 100.0, q[11] / n / 100.0,
+            q[12] / n / 100.0);
+}
+
+int launch_host_serve(const HostServeLaunch &sl0, hipStream_t s)
+{
+    HostServeLaunch sl = sl0;
+    if (getenv("HKV_PART_PROF")) {   // (debug) phase sums, printed at exit
+        if (!g_serve_prof) {
+            if (hipHostMalloc((void **)&g_serve_prof, 256, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return -3;
+            memset(g_serve_prof, 0, 256);
+            atexit(serve_prof_print);
+        }
+        sl.c.prof = g_serve_prof;
+    }
+    hipLaunchKernelGGL(k_hserve, dim3(kPartG), dim3(kHpThreads), 0, s, sl);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int launch_host_part(const HostPartLaunch &pl, hipStream_t s)
+{
+    if (pl.n_batches <= 0 || pl.n_batches > kPartMaxB || pl.c.g.entry_size != 64 || pl.c.g.st_value != 31) return -1;
+    // HKV_PART_PROF=N: every N-th launch records workgroup 0's phase timestamps and prints the running
+    // average (debug; synchronises the stream)
+    static const int prof_every = getenv("HKV_PART_PROF") ? atoi(getenv("HKV_PART_PROF")) : 0;
+    static unsigned long long *prof = nullptr;
+    static long prof_n = 0, k = 0;
+    static double sum[4] = {0, 0, 0, 0};
+    HostPartLaunch p = pl;
+    p.c.prof = nullptr;
+    const bool sample = prof_every > 0 && (++prof_n % prof_every) == 0;
+    if (sample) {
+        if (!prof && hipHostMalloc((void **)&prof, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return -3;
+        p.c.prof = prof;
+    }
+    hipLaunchKernelGGL(k_hpart, dim3(kPartG), dim3(kHpThreads), 0, s, p);
+    if (sample) {
+        hipStreamSynchronize(s);
+        ++k;
+        for (int i = 0; i < 4; ++i) sum[i] += (double)(prof[i + 1] - prof[i]) * 10.0 / 1000.0;  // 100 MHz ticks -> us
+        fprintf(stderr, "[hkv] k_hpart phases (us, avg of %ld): headers %.2f load+lookup %.2f rounds %.2f store %.2f\n", k,
+                sum[0] / k, sum[1] / k, sum[2] / k, sum[3] / k);
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -69,6 +69,65 @@ struct SmallBatch {
 };
 constexpr int kSmallMaxBatches = 64;
 
+// ---- partitioned host launches (the combining submit of hermes_batch_ops_to_KVS, 64-B entries):
+// every element goes to the workgroup that owns its key, part_of(key) of kPartG, so workgroups
+// never share a key and need no communication. Each caller stages its own batch, partition-major
+// (elements in element order within a partition), in its own pinned buffer; the launch carries one
+// HostPartHdr per batch and part[g][b]: batch b's elements of partition g are
+// [part[g][b], part[g + 1][b]) of its staged array -- all in the kernel arguments, which the
+// dispatch delivers with the launch (no PCIe round trip for them).
+constexpr int kPartG = 32;       // workgroups of one launch
+constexpr int kPartCap = 256;    // elements one workgroup takes
+constexpr int kPartMaxB = 16;    // batches one launch combines
+__host__ __device__ inline uint32_t part_of(uint64_t key)
+{
+    return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 59);   // kPartG = 32
+}
+struct HostPartHdr {
+    uint64_t elems;   // device address: the staged elements, partition-major
+    uint64_t pos;     // device address: u16 position in the batch of each staged element
+    uint64_t rw;      // ACK batches: device address of the read_write_ops copy, else 0
+    int32_t type, count, esz;
+    uint8_t g_membership, w_ack_init, pad0, pad1;
+    uint64_t pad2;
+};
+static_assert(sizeof(HostPartHdr) == 48, "HostPartHdr is three 16-byte loads");
+struct HostPartCommon {
+    Geometry g;
+    const uint8_t *index;
+    uint8_t *log;
+    unsigned int *error_flags;
+    uint32_t *flags;             // device address: kPartG words, workgroup g stores seq into flags[g]
+    unsigned long long *prof;    // HKV_PART_PROF: workgroup 0's phase timestamps (debug), or NULL
+};
+struct HostPartLaunch {          // one launch, everything in the kernel arguments
+    HostPartCommon c;
+    uint32_t seq;
+    int32_t n_batches;
+    HostPartHdr hdr[kPartMaxB];
+    uint16_t part[kPartG + 1][kPartMaxB];
+};
+// one launch published to the serving kernel (pinned ring slot; seq written last)
+struct alignas(128) HostRingSlot {
+    uint32_t seq;
+    int32_t n_batches;
+    uint32_t pad[2];
+    HostPartHdr hdr[kPartMaxB];
+    uint16_t part[kPartG + 1][kPartMaxB];
+};
+struct HostServeLaunch {
+    HostPartCommon c;
+    const HostRingSlot *ring;    // device address of ring_n slots (pinned); launch n in slot n % ring_n
+    int32_t ring_n;
+    uint32_t epoch;
+    const uint32_t *stop;        // pinned: non-zero makes every workgroup leave between launches
+    uint32_t *exited;            // pinned: workgroup g stores epoch into exited[g] when it leaves
+    uint64_t idle_ticks, life_ticks;   // wall_clock64 ticks (100 MHz)
+    uint32_t start[kPartG];      // the first launch each workgroup takes
+};
+int launch_host_serve(const HostServeLaunch &sl, hipStream_t s);
+int launch_host_part(const HostPartLaunch &pl, hipStream_t s);
+
 enum : int32_t { kPathAuto = 0, kPathEngine = 1, kPathSmall = 2 };
 
 struct PopulateLaunch {

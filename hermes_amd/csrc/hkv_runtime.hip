@@ -36,23 +36,41 @@ using namespace hkv;
 // Launches on one stream run in order, so the combined result is the serial order of the sets'
 // concatenations -- an order the reference could have produced. With several sets, the next
 // combiner stages while the GPU runs the previous launch.
-constexpr int kHostSets = 2;
+//
+// Partitioned launches (64-B entries, the common case): each caller first stages its own batch in
+// a pinned buffer of its thread, partition-major by key (part_of, hkv_internal.h), so the combiner
+// copies nothing -- it writes one 48-byte header per batch and launches k_hpart, whose kPartG
+// workgroups each own a partition of the keys and read their elements straight from the callers'
+// buffers. A launch's latency is then that of one partition, whatever it combines. Batches that
+// overflow a partition (one key hammered by more than kPartCap elements) and big objects take the
+// single-workgroup kernel (k_small) or the multi-kernel engine as before.
+constexpr int kHostSets = 4;
 constexpr int kHostMaxBatches = 64;
 constexpr int64_t kHostMaxElems = 32768;
 
+enum { kModeEvent = 0, kModeSmall = 1, kModePart = 2 };
+
 struct HostSet {
-    uint8_t *h = nullptr;    // pinned, coherent: counts | node_suspected | ops | rw
+    uint8_t *h = nullptr;    // pinned, coherent: counts | node_suspected | ops | rw (or the part table)
     uint8_t *hd = nullptr;   // the same bytes as the device sees them
     uint8_t *d = nullptr;
     size_t cap = 0;
     hipEvent_t ev = nullptr;
-    uint32_t *flag = nullptr;   // pinned: the launch's kernel stores `seq` when its results are in h
-    uint32_t *flag_d = nullptr;
+    uint32_t *flag = nullptr;   // pinned: k_small stores `seq` when its results are in h (flag[0]),
+    uint32_t *flag_d = nullptr; // k_hpart's workgroup g into flag[g]
     uint32_t seq = 0;
-    bool small = false;      // this launch signals through flag (else through ev)
+    int mode = kModeEvent;   // how this launch signals completion
     int refs = 0;            // callers still to copy their results out
     bool busy = false;
 };
+
+// a caller thread's pinned staging for partitioned launches: elements | u16 positions | rw copy
+struct CallerStage {
+    uint8_t *h = nullptr, *d = nullptr;
+    size_t cap = 0;
+    std::vector<uint32_t> perm;   // element i of the caller's batch sits at staged slot perm[i]
+};
+static thread_local CallerStage t_stage;
 
 struct HostReq {
     int type;
@@ -64,7 +82,12 @@ struct HostReq {
     uint8_t *rw;
     HostSet *set = nullptr;
     size_t ops_off = 0, rw_off = 0, ns_off = 0, rw_bytes = 0;
-    bool launched = false;
+    std::atomic<bool> launched{false};
+    // partitioned: staged in the caller's t_stage (device addresses), partition g at [poff[g], poff[g+1])
+    bool part = false;
+    uint32_t pseq = 0;     // launched as partitioned launch pseq (0: in a set's launch)
+    uint64_t st_elems = 0, st_pos = 0, st_rw = 0;
+    uint16_t poff[kPartG + 1];
 };
 
 struct hkv_table {
@@ -90,10 +113,22 @@ struct hkv_table {
     std::mutex hmu;
     std::condition_variable hcv;
     std::deque<HostReq *> hq;
-    bool combining = false;
+    std::atomic<bool> combining{false};
     HostSet sets[kHostSets];
+    // partitioned launches: workgroup g of launch n stores n into pflags[g] (pinned; launches run in
+    // stream order, so each word only grows); pseq counts the launches
+    uint32_t *pflags = nullptr, *pflags_d = nullptr;
+    uint32_t pseq = 0;
+    // the serving kernel (k_hserve): launches are published in a pinned ring instead of launched
+    HostRingSlot *ring = nullptr, *ring_d = nullptr;
+    uint32_t *srv_words = nullptr, *srv_words_d = nullptr;   // [0] stop, [32..63] exited per workgroup
+    uint32_t srv_epoch = 0;
+    bool srv_running = false;
+    hipEvent_t srv_ev = nullptr;
     std::mutex mu;
 };
+
+static void srv_stop(hkv_table *t);   // the serving kernel (see "combining submit") stopped
 
 static thread_local std::string g_err;
 static const bool g_trace = getenv("HKV_TRACE") != nullptr;
@@ -306,6 +341,14 @@ int hkv_table_destroy(hkv_table *t)
         hipHostFree(hs.flag);
         if (hs.ev) hipEventDestroy(hs.ev);
     }
+    if (t->srv_running) {
+        __atomic_store_n(t->srv_words, 1u, __ATOMIC_RELEASE);
+        hipEventSynchronize(t->srv_ev);
+    }
+    if (t->srv_ev) hipEventDestroy(t->srv_ev);
+    if (t->ring) hipHostFree(t->ring);
+    if (t->srv_words) hipHostFree(t->srv_words);
+    if (t->pflags) hipHostFree(t->pflags);
     if (t->stream) hipStreamDestroy(t->stream);
     delete t;
     return 0;
@@ -322,6 +365,7 @@ int hkv_table_set_skew(hkv_table *t, uint32_t skew_flags)
 {
     if (!t) return fail(-1, "null table");
     if (skew_flags & ~(HKV_SKEW_READ_COMPLETE | HKV_SKEW_WRITE_COALESCE)) return fail(-1, "unknown skew_flags %#x", skew_flags);
+    srv_stop(t);   // it holds the geometry it was started with
     std::lock_guard<std::mutex> lk(t->mu);
     t->cfg.skew_flags = skew_flags;
     t->geo.skew = skew_flags;
@@ -333,6 +377,7 @@ int hkv_table_populate(hkv_table *t, int64_t n, int val_len)
     if (!t) return fail(-1, "null table");
     if (n <= 0) return fail(-1, "populate: n must be > 0");
     if (val_len <= 0 || (uint32_t)val_len > t->geo.kvs_value) return fail(-1, "populate: bad val_len %d", val_len);
+    srv_stop(t);
     if (n > 0x7FFFFFFFll) return fail(-1, "populate: at most 2^31-1 keys (32-bit key ids)");
     std::lock_guard<std::mutex> lk(t->mu);
     HIP_TRY(hipSetDevice(t->cfg.device));
@@ -411,6 +456,7 @@ static int check_elems(const hkv_table *t, int type, uint32_t elem_size, int64_t
 int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
 {
     if (!t || !d) return fail(-1, "null argument");
+    srv_stop(t);
     const bool packed = (d->flags & HKV_BATCH_PACKED) != 0;
     if (d->n_batches < 0 || d->stride < 0 || (d->stride == 0 && !packed)) return fail(-1, "bad batch geometry");
     if (int rc = check_elems(t, d->type, d->elem_size, packed ? 0 : d->stride)) return rc;
@@ -490,6 +536,7 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
 int hkv_sync(hkv_table *t, void *stream)
 {
     if (!t) return fail(-1, "null table");
+    srv_stop(t);
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     HIP_TRY(hipStreamSynchronize(t->stream));
     return 0;
@@ -499,6 +546,7 @@ int hkv_copy_index(hkv_table *t, void *dst, uint64_t off, uint64_t bytes)
 {
     if (!t || !dst) return fail(-1, "null argument");
     if (off + bytes > t->cfg.num_bkts * 64) return fail(-1, "index range out of bounds");
+    srv_stop(t);
     HIP_TRY(hipStreamSynchronize(t->stream));
     HIP_TRY(hipMemcpy(dst, t->d_index + off, bytes, hipMemcpyDeviceToHost));
     return 0;
@@ -508,6 +556,7 @@ int hkv_copy_log(hkv_table *t, void *dst, uint64_t off, uint64_t bytes)
 {
     if (!t || !dst) return fail(-1, "null argument");
     if (off + bytes > t->cfg.log_cap + t->geo.entry_size) return fail(-1, "log range out of bounds");
+    srv_stop(t);
     HIP_TRY(hipStreamSynchronize(t->stream));
     HIP_TRY(hipMemcpy(dst, t->d_log + off, bytes, hipMemcpyDeviceToHost));
     return 0;
@@ -528,6 +577,7 @@ void *hkv_device_index(hkv_table *t) { return t ? t->d_index : nullptr; }
 int hkv_take_error_flags(hkv_table *t, uint32_t *out)
 {
     if (!t || !out) return fail(-1, "null argument");
+    srv_stop(t);
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(out, t->d_error_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemset(t->d_error_flags, 0, sizeof(uint32_t)));
@@ -603,6 +653,23 @@ static void host_stats_note(int nb)
 
 static const bool g_staging_nc = getenv("HKV_STAGING_NC") != nullptr;  // experiment: non-coherent staging
 
+// HKV_HOST_TIMING=1: where a host-pointer call's time goes (staging, queue + launch + GPU, copy-out),
+// averaged over the calls and printed at exit
+static const bool g_host_timing = getenv("HKV_HOST_TIMING") != nullptr;
+static std::atomic<long> g_ht_calls{0}, g_ht_stage{0}, g_ht_wait{0}, g_ht_out{0};
+static void host_timing_print()
+{
+    const long n = std::max(1L, g_ht_calls.load());
+    fprintf(stderr, "[hkv] host call timing (us, avg of %ld): stage %.2f wait %.2f copy-out %.2f\n", n,
+            g_ht_stage.load() / 1e3 / n, g_ht_wait.load() / 1e3 / n, g_ht_out.load() / 1e3 / n);
+}
+static long now_ns()
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1000000000L + ts.tv_nsec;
+}
+
 static bool host_compatible(const HostReq *a, const HostReq *b)
 {
     return a->type == b->type && a->esz == b->esz && a->mb == b->mb && (a->rw != nullptr) == (b->rw != nullptr) &&
@@ -628,10 +695,10 @@ static void host_set_reserve(HostSet *set, size_t total)
     }
     if (!set->ev && hipEventCreateWithFlags(&set->ev, hipEventDisableTiming) != hipSuccess) die("event");
     if (!set->flag) {
-        if (hipHostMalloc((void **)&set->flag, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        if (hipHostMalloc((void **)&set->flag, 4 * kPartG, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
             hipHostGetDevicePointer((void **)&set->flag_d, set->flag, 0) != hipSuccess)
             die("flag alloc");
-        __atomic_store_n(set->flag, 0u, __ATOMIC_RELEASE);
+        for (int g = 0; g < kPartG; ++g) __atomic_store_n(set->flag + g, 0u, __ATOMIC_RELEASE);
     }
 }
 
@@ -709,7 +776,7 @@ static void host_launch_mixed(hkv_table *t, HostSet *set, std::unique_lock<std::
     bl.done_flag = set->flag_d;
     bl.done_value = ++set->seq;
     bl.hdr = reinterpret_cast<const SmallBatch *>(set->d);
-    set->small = true;
+    set->mode = kModeSmall;
     if (g_host_stats) host_stats_note(nb);
     TRACE("mixed launch batches=%d elements=%lld", nb, (long long)elems);
     if (elems == 0) {
@@ -727,10 +794,228 @@ static void host_launch_mixed(hkv_table *t, HostSet *set, std::unique_lock<std::
     set->refs = nb;
     for (HostReq *r : take) {
         r->set = set;
-        r->launched = true;
+        r->launched.store(true, std::memory_order_release);
     }
     t->combining = false;
     t->hcv.notify_all();
+}
+
+constexpr int kRingN = 16;   // ring slots of the serving kernel (launches in flight at most)
+
+// The serving kernel has started leaving (some workgroup recorded the current epoch)
+static bool srv_exited(const hkv_table *t)
+{
+    for (int g = 0; g < kPartG; ++g)
+        if (__atomic_load_n(t->srv_words + 32 + g, __ATOMIC_ACQUIRE) == t->srv_epoch) return true;
+    return false;
+}
+
+// With t->hmu held: every workgroup of the serving kernel gone (it may have left by itself already)
+static void srv_stop_locked(hkv_table *t)
+{
+    if (!t->srv_running) return;
+    __atomic_store_n(t->srv_words, 1u, __ATOMIC_RELEASE);
+    if (hipEventSynchronize(t->srv_ev) != hipSuccess) die("serving kernel");
+    __atomic_store_n(t->srv_words, 0u, __ATOMIC_RELEASE);
+    t->srv_running = false;
+}
+
+static void srv_stop(hkv_table *t)
+{
+    std::lock_guard<std::mutex> lk(t->hmu);
+    srv_stop_locked(t);
+}
+
+// With t->hmu held, after a launch was published: a serving kernel will take it. If the running one
+// is leaving (idle or lifetime limit), wait until it has gone and start another at every
+// partition's first unfinished launch.
+static void srv_ensure(hkv_table *t)
+{
+    if (t->srv_running && !srv_exited(t)) return;
+    if (t->srv_running) {
+        if (hipEventSynchronize(t->srv_ev) != hipSuccess) die("serving kernel");
+        t->srv_running = false;
+    }
+    static const double idle_ms = getenv("HKV_SERVE_IDLE_MS") ? atof(getenv("HKV_SERVE_IDLE_MS")) : 2.0;
+    HostServeLaunch sl;
+    memset(&sl, 0, sizeof sl);
+    {
+        std::lock_guard<std::mutex> tl(t->mu);   // against hkv_table_populate (geo.log_head)
+        sl.c.g = t->geo;
+    }
+    sl.c.index = t->d_index;
+    sl.c.log = t->d_log;
+    sl.c.error_flags = t->d_error_flags;
+    sl.c.flags = t->pflags_d;
+    sl.ring = t->ring_d;
+    sl.ring_n = kRingN;
+    sl.epoch = ++t->srv_epoch;
+    sl.stop = t->srv_words_d;
+    sl.exited = t->srv_words_d + 32;
+    sl.idle_ticks = (uint64_t)(idle_ms * 1e5);     // wall_clock64: 100 MHz
+    sl.life_ticks = (uint64_t)1e8;                 // 1 s, then a fresh server
+    for (int g = 0; g < kPartG; ++g) sl.start[g] = __atomic_load_n(t->pflags + g, __ATOMIC_ACQUIRE) + 1;
+    __atomic_store_n(t->srv_words, 0u, __ATOMIC_RELEASE);
+    if (!t->srv_ev && hipEventCreateWithFlags(&t->srv_ev, hipEventDisableTiming) != hipSuccess) die("event");
+    if (launch_host_serve(sl, t->stream) || hipEventRecord(t->srv_ev, t->stream) != hipSuccess) die("serving kernel launch");
+    t->srv_running = true;
+    TRACE("serving kernel epoch %u", sl.epoch);
+}
+
+// The last partitioned launch every workgroup has finished
+static uint32_t part_done(const hkv_table *t)
+{
+    uint32_t m = __atomic_load_n(t->pflags, __ATOMIC_ACQUIRE);
+    for (int g = 1; g < kPartG; ++g) {
+        const uint32_t v = __atomic_load_n(t->pflags + g, __ATOMIC_ACQUIRE);
+        if ((int32_t)(v - m) < 0) m = v;
+    }
+    return m;
+}
+
+// The queued partition-staged batches (in queue order, as many as keep every partition within
+// kPartCap and the launch within kPartMaxB batches) as ONE k_hpart launch, its headers in the kernel
+// arguments. At most HKV_PART_INFLIGHT (default 2) partitioned launches are in flight: a combiner
+// first waits for the oldest, and batches queued meanwhile join its launch. Called with t->hmu held.
+static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
+{
+    // HKV_HOST_SERVE=1: publish to the serving kernel (k_hserve) instead of one k_hpart launch per
+    // combined batch. Measured, not adopted: the same rates (6.4 / 22.8 / 41.1 M local ops/s from
+    // 1 / 8 / 16 threads with launches, 5.7 / 23.3 / 40.7 M served): a launch's dispatch is not what
+    // bounds a call, its PCIe round trips are (descriptor, elements, results: about 2.5 us each)
+    static const bool serve = getenv("HKV_HOST_SERVE") && atoi(getenv("HKV_HOST_SERVE")) != 0;
+    static const int inflight = std::min(kRingN, getenv("HKV_PART_INFLIGHT") ? std::max(1, atoi(getenv("HKV_PART_INFLIGHT")))
+                                                                              : serve ? 4 : 2);
+    if (!t->pflags) {
+        if (hipHostMalloc((void **)&t->pflags, 4 * kPartG, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&t->pflags_d, t->pflags, 0) != hipSuccess)
+            die("flag alloc");
+        for (int g = 0; g < kPartG; ++g) __atomic_store_n(t->pflags + g, 0u, __ATOMIC_RELEASE);
+    }
+    if (serve && !t->ring) {
+        if (hipHostMalloc((void **)&t->ring, sizeof(HostRingSlot) * kRingN, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&t->ring_d, t->ring, 0) != hipSuccess ||
+            hipHostMalloc((void **)&t->srv_words, 4 * 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&t->srv_words_d, t->srv_words, 0) != hipSuccess)
+            die("ring alloc");
+        memset(t->ring, 0, sizeof(HostRingSlot) * kRingN);
+        for (int k = 0; k < 64; ++k) __atomic_store_n(t->srv_words + k, 0u, __ATOMIC_RELEASE);
+    }
+    for (uint32_t spins = 0; (int32_t)(t->pseq - part_done(t)) >= inflight; ++spins) {
+        if (serve && t->srv_running && srv_exited(t)) srv_ensure(t);   // a server that left has work to do
+        lk.unlock();
+        __builtin_ia32_pause();
+        if ((spins & 255u) == 255u) sched_yield();
+        lk.lock();
+    }
+    HostPartLaunch pl;
+    memset(&pl, 0, sizeof pl);
+    std::vector<HostReq *> take;
+    int tot[kPartG] = {0};
+    for (auto it = t->hq.begin(); it != t->hq.end() && (int)take.size() < kPartMaxB;) {
+        HostReq *r = *it;
+        bool fits = r->part;
+        for (int g = 0; fits && g < kPartG; ++g) fits = tot[g] + (r->poff[g + 1] - r->poff[g]) <= kPartCap;
+        if (!fits) {  // taken later (another caller's batch: any order of callers is a serial order)
+            ++it;
+            continue;
+        }
+        for (int g = 0; g < kPartG; ++g) tot[g] += r->poff[g + 1] - r->poff[g];
+        take.push_back(r);
+        it = t->hq.erase(it);
+    }
+    const uint32_t seq = ++t->pseq;
+    lk.unlock();
+    const int nb = (int)take.size();
+    for (int b = 0; b < nb; ++b) {
+        const HostReq *r = take[b];
+        HostPartHdr &h = pl.hdr[b];
+        h.elems = r->st_elems;
+        h.pos = r->st_pos;
+        h.rw = r->st_rw;
+        h.type = r->type;
+        h.count = r->n;
+        h.esz = r->esz;
+        h.g_membership = (uint8_t)(r->mb >> 8);
+        h.w_ack_init = (uint8_t)(r->mb >> 16);
+        for (int g = 0; g <= kPartG; ++g) pl.part[g][b] = r->poff[g];
+    }
+    pl.c.index = t->d_index;
+    pl.c.log = t->d_log;
+    pl.c.error_flags = t->d_error_flags;
+    pl.n_batches = nb;
+    pl.c.flags = t->pflags_d;
+    pl.seq = seq;
+    if (g_host_stats) host_stats_note(nb);
+    TRACE("partitioned launch %u batches=%d", seq, nb);
+    if (serve) {   // publish: the slot's contents, then its seq (x86 stores stay in order)
+        HostRingSlot &slot = t->ring[seq % kRingN];
+        slot.n_batches = nb;
+        memcpy(slot.hdr, pl.hdr, sizeof(HostPartHdr) * (size_t)nb);
+        memcpy(slot.part, pl.part, sizeof slot.part);
+        __atomic_store_n(&slot.seq, seq, __ATOMIC_RELEASE);
+        lk.lock();
+        srv_ensure(t);
+    } else {
+        {
+            std::lock_guard<std::mutex> tl(t->mu);   // against hkv_table_populate (geo.log_head)
+            pl.c.g = t->geo;
+            if (launch_host_part(pl, t->stream)) die("hermes_batch_ops_to_KVS (partitioned launch)");
+        }
+        lk.lock();
+    }
+    for (HostReq *r : take) {
+        r->pseq = seq;
+        r->launched.store(true, std::memory_order_release);
+    }
+    t->combining = false;
+}
+
+// Stages a caller's batch for a partitioned launch in its thread's pinned buffer (see "combining
+// submit"): the elements partition-major, each with its position in the batch, and an ACK batch's
+// read_write_ops. False when the table or the batch does not fit the partitioned kernel.
+static bool host_stage_part(const hkv_table *t, HostReq &r)
+{
+    if (t->geo.entry_size != 64 || t->geo.st_value != 31 || r.esz > 64 || r.n > kPartG * kPartCap) return false;
+    int cnt[kPartG] = {0};
+    for (int i = 0; i < r.n; ++i) {
+        const uint64_t key = *reinterpret_cast<const uint64_t *>(r.ops + (size_t)i * r.esz);
+        if (++cnt[part_of(key)] > kPartCap) return false;
+    }
+    r.poff[0] = 0;
+    for (int g = 0; g < kPartG; ++g) r.poff[g + 1] = (uint16_t)(r.poff[g] + cnt[g]);
+    const size_t ebytes = align16((size_t)r.n * r.esz), pbytes = align16((size_t)r.n * 2);
+    const size_t rw_bytes = r.type == acks && r.rw ? (size_t)t->cfg.rw_len * t->geo.op_size : 0;
+    const size_t total = ebytes + pbytes + rw_bytes;
+    CallerStage &st = t_stage;
+    if (total > st.cap) {
+        if (st.h) hipHostFree(st.h);
+        st.h = st.d = nullptr;
+        const size_t cap = std::max(total, (size_t)1 << 20);
+        if (hipHostMalloc((void **)&st.h, cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&st.d, st.h, 0) != hipSuccess)
+            die("caller staging alloc");
+        st.cap = cap;
+    }
+    if ((int)st.perm.size() < r.n) st.perm.resize(r.n);
+    uint16_t cur[kPartG];
+    for (int g = 0; g < kPartG; ++g) cur[g] = r.poff[g];
+    uint16_t *pos = reinterpret_cast<uint16_t *>(st.h + ebytes);
+    for (int i = 0; i < r.n; ++i) {
+        const uint8_t *x = r.ops + (size_t)i * r.esz;
+        const uint32_t slot = cur[part_of(*reinterpret_cast<const uint64_t *>(x))]++;
+        memcpy(st.h + (size_t)slot * r.esz, x, r.esz);
+        pos[slot] = (uint16_t)i;
+        st.perm[i] = slot;
+    }
+    if (rw_bytes) memcpy(st.h + ebytes + pbytes, r.rw, rw_bytes);
+    r.rw_bytes = rw_bytes;
+    r.st_elems = (uint64_t)(uintptr_t)st.d;
+    r.st_pos = (uint64_t)(uintptr_t)(st.d + ebytes);
+    r.st_rw = rw_bytes ? (uint64_t)(uintptr_t)(st.d + ebytes + pbytes) : 0;
+    r.rw_off = ebytes + pbytes;
+    r.part = true;
+    return true;
 }
 
 // Called with t->hmu held by a caller that found no combiner active: launches the compatible
@@ -749,6 +1034,11 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
             lk.lock();
         }
     }
+    if (t->hq.front()->part) {  // partition-staged batches: one k_hpart launch, no staging set
+        host_launch_part(t, lk);
+        return;
+    }
+    srv_stop_locked(t);   // the launches below run on the table's stream, behind the serving kernel
     HostSet *set = nullptr;
     static const int n_sets = getenv("HKV_HOST_SETS") ? std::max(1, std::min(kHostSets, atoi(getenv("HKV_HOST_SETS")))) : kHostSets;
     for (;;) {
@@ -808,7 +1098,7 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
         if (with_rw) memcpy(set->h + r->rw_off, r->rw, rw_bytes);
     }
     hipStream_t s = t->stream;
-    set->small = false;
+    set->mode = kModeEvent;
     if (hipMemcpyAsync(set->d, set->h, total, hipMemcpyHostToDevice, s) != hipSuccess) die("copy in");
     hkv_batch_desc d;
     memset(&d, 0, sizeof d);
@@ -835,7 +1125,7 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
     set->refs = nb;
     for (HostReq *r : take) {
         r->set = set;
-        r->launched = true;
+        r->launched.store(true, std::memory_order_release);
     }
     t->combining = false;
     t->hcv.notify_all();
@@ -894,18 +1184,46 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
     r.mb = curr_membership;
     r.ns = type == invs ? node_suspected : nullptr;
     r.rw = type == acks ? reinterpret_cast<uint8_t *>(read_write_ops) : nullptr;
-    std::unique_lock<std::mutex> lk(t->hmu);
-    t->hq.push_back(&r);
-    while (!r.launched) {
-        if (!t->combining) host_combine(t, lk);
-        else t->hcv.wait(lk);
+    static const bool part_on = !getenv("HKV_HOST_PART") || atoi(getenv("HKV_HOST_PART")) != 0;
+    const long t0 = g_host_timing ? now_ns() : 0;
+    if (part_on) host_stage_part(t, r);   // else (or when it does not fit) the k_small / engine paths
+    const long t1 = g_host_timing ? now_ns() : 0;
+    {
+        std::lock_guard<std::mutex> lk(t->hmu);
+        t->hq.push_back(&r);
     }
-    HostSet *set = r.set;
-    const uint32_t seq = set->seq;
-    const bool small = set->small;
-    lk.unlock();
-    if (small) {  // the kernel's completion flag in pinned memory; yield now and then, so callers
-                  // that outnumber the cores leave the next combiner CPU time
+    // until some combiner (maybe this caller) has launched the batch; spinning rather than sleeping
+    // on a condition variable: a futex wake-up costs about as long as a whole launch
+    for (uint32_t spins = 0; !r.launched.load(std::memory_order_acquire); ++spins) {
+        if (!t->combining.load(std::memory_order_relaxed)) {
+            std::unique_lock<std::mutex> lk(t->hmu);
+            if (!r.launched.load(std::memory_order_acquire) && !t->combining.load()) host_combine(t, lk);
+            continue;
+        }
+        __builtin_ia32_pause();
+        if ((spins & 255u) == 255u) sched_yield();
+    }
+    HostSet *set = r.pseq ? nullptr : r.set;
+    const int mode = set ? set->mode : kModePart;
+    uint32_t seq = 0;
+    if (set) {
+        std::lock_guard<std::mutex> lk(t->hmu);
+        seq = set->seq;
+    }
+    if (mode == kModePart) {  // every workgroup's flag at or past this launch (they only grow); yield
+                              // now and then, so callers that outnumber the cores leave the combiner CPU time
+        for (uint32_t spins = 0;; ++spins) {
+            bool all = true;
+            for (int g = 0; all && g < kPartG; ++g) all = (int32_t)(__atomic_load_n(t->pflags + g, __ATOMIC_ACQUIRE) - r.pseq) >= 0;
+            if (all) break;
+            __builtin_ia32_pause();
+            if ((spins & 1023u) == 1023u) {
+                sched_yield();
+                std::lock_guard<std::mutex> lk(t->hmu);
+                if (t->srv_running && srv_exited(t)) srv_ensure(t);   // it left before taking this launch
+            }
+        }
+    } else if (mode == kModeSmall) {  // the kernel's completion flag in pinned memory
         for (uint32_t spins = 0; __atomic_load_n(set->flag, __ATOMIC_ACQUIRE) != seq; ++spins) {
             __builtin_ia32_pause();
             if ((spins & 1023u) == 1023u) sched_yield();
@@ -913,13 +1231,41 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
     } else if (hipEventSynchronize(set->ev) != hipSuccess) {
         die("sync");
     }
-    memcpy(op_array, set->h + r.ops_off, (size_t)op_num * sizeof_op_elem);
-    if (r.rw && r.rw_bytes) memcpy(r.rw, set->h + r.rw_off, r.rw_bytes);
-    if (r.ns) memcpy(r.ns, set->h + r.ns_off, 4);
-    lk.lock();
-    if (--set->refs == 0) {
-        set->busy = false;
-        t->hcv.notify_all();
+    const long t2 = g_host_timing ? now_ns() : 0;
+    if (mode == kModePart) {
+        // results from this thread's staging, back in element order; node_suspected is
+        // hermes_skip_inv's, a function of the elements alone: the last membership-change INV's
+        // value[0] (hermesKV.c:735-744)
+        const CallerStage &st = t_stage;
+        for (int i = 0; i < op_num; ++i)
+            memcpy(op_array + (size_t)i * sizeof_op_elem, st.h + (size_t)st.perm[i] * sizeof_op_elem, sizeof_op_elem);
+        if (r.rw && r.rw_bytes) memcpy(r.rw, st.h + r.rw_off, r.rw_bytes);
+        if (r.ns) {
+            for (int i = op_num - 1; i >= 0; --i)
+                if (op_array[(size_t)i * sizeof_op_elem + 8] == kOpMembChange) {
+                    *r.ns = op_array[(size_t)i * sizeof_op_elem + kOpValueOff];
+                    break;
+                }
+        }
+    } else {
+        memcpy(op_array, set->h + r.ops_off, (size_t)op_num * sizeof_op_elem);
+        if (r.rw && r.rw_bytes) memcpy(r.rw, set->h + r.rw_off, r.rw_bytes);
+        if (r.ns) memcpy(r.ns, set->h + r.ns_off, 4);
+    }
+    if (g_host_timing) {
+        static std::once_flag once;
+        std::call_once(once, [] { atexit(host_timing_print); });
+        g_ht_calls++;
+        g_ht_stage += t1 - t0;
+        g_ht_wait += t2 - t1;
+        g_ht_out += now_ns() - t2;
+    }
+    if (set) {
+        std::lock_guard<std::mutex> lk(t->hmu);
+        if (--set->refs == 0) {
+            set->busy = false;
+            t->hcv.notify_all();
+        }
     }
     TRACE("done");
 }

@@ -4,6 +4,8 @@ Every comparison is on the reference's byte images: element arrays, read_write_o
 node_suspected, and the whole MICA index + log after every batch. The oracle is the CPU
 restatement pinned in tests/test_oracle.py.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -154,6 +156,94 @@ def test_known_answers_reference_entry_points():
     from hermes_amd import kvs
     kvs.spacetime_init(0)
     run_known_answers(_RefApiEngine(kvs), gen_keys(1_000_000))
+
+
+def _oracle_from_device(kvs, skew):
+    """An oracle table holding the device table's current image (index, log, head)"""
+    from oracle.oracle import lib as olib
+    c = kvs.cfg
+    o = OracleKVS(c.num_bkts, c.log_cap, c.machine_id, bool(c.rmw_enabled), bool(c.big_objects), c.extra_cache_lines,
+                  skew=skew)
+    o.index_bytes()[:] = kvs.index_bytes()
+    used = min(kvs.log_head, c.log_cap)
+    o.log_bytes()[:used] = kvs.log_bytes(0, used)
+    olib().hko_set_log_head.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    olib().hko_set_log_head(o.h, kvs.log_head)
+    return o
+
+
+@pytest.mark.parametrize("skew", [0, 3])
+def test_random_rounds_reference_entry_points(skew):
+    """Randomized protocol rounds through the drop-in entry point itself (spacetime_init +
+    hermes_batch_ops_to_KVS on the default 1M-key table), one call per worker batch as the
+    reference's workers make them (hermes_worker.c:451-509): local ops, INVs (with membership-change
+    INVs: node_suspected), ACKs against the worker's own op buffer as read_write_ops, VALs, and the
+    after-membership-change batch. Small calls take the partitioned launch (k_hpart: one workgroup
+    per key partition); a call piling more than a partition's capacity on one key (the hot round's
+    900-element batches) takes the single-workgroup kernel. Each call is replayed on an oracle copy
+    of the table; elements, read_write_ops, node_suspected and the touched keys' entries must match."""
+    from hermes_amd import kvs as K
+    K.spacetime_init(0)
+    d = K.HermesKV.default_table()
+    d.set_skew(skew)
+    try:
+        o = _oracle_from_device(d, skew)
+        keys = gen_keys(1_000_000)
+        rng = np.random.default_rng(20261017 + skew)
+        tsp = gen.TsPool(rng)
+        sizes = L.DEFAULT
+        mb_full, mb_fail = L.membership(5, 0), L.membership(5, 0, alive=0b01111)
+        W = 4
+
+        def call(btype, e, mb, rw=None, what=""):
+            eo = gen.bytecopy(e)
+            rwo = gen.bytecopy(rw) if rw is not None else None
+            ns_g, ns_o = [-1], None
+            K.hermes_batch_ops_to_KVS(btype, e, len(e), e.dtype.itemsize, mb, ns_g, rw, 0)
+            ns_o = o.batch(btype, eo, mb, rw=rwo)
+            assert_elems_equal(e, eo, what)
+            if rw is not None:
+                assert_elems_equal(rw, rwo, what + " rw")
+            assert ns_g[0] == ns_o, f"{what}: node_suspected {ns_g[0]} vs {ns_o}"
+
+        def entries_equal(pool, what):
+            for k in pool:
+                off = o.lookup(int(k))
+                if off is None:
+                    continue
+                assert np.array_equal(d.log_bytes(off, 64), o.log_bytes()[off:off + 64]), f"{what}: entry of {int(k):#x}"
+
+        for rnd in range(12):
+            hot = rnd in (5, 11)
+            pool = keys[[rng.integers(0, 1_000_000)]] if hot else gen.key_pool(rng, keys, hot=24 if rnd % 2 else 300)
+            mb = mb_fail if rnd >= 8 else mb_full
+            n_loc, n_msg = (250, 900) if hot else (int(rng.integers(100, 251)), int(rng.integers(20, 200)))
+            bufs = []
+            for w in range(W):
+                loc = gen.local_ops(rng, pool, n_loc, sizes, False, tsp)
+                if skew:
+                    z = rng.random(n_loc) < 0.3
+                    loc["ts_ver"][z] = 0
+                    loc["ts_cid"][z & (loc["opcode"] == int(L.Op.GET))] = 0
+                call(L.BatchType.local_ops, loc, mb, what=f"round {rnd} worker {w} local")
+                gen.harvest_ts(tsp, loc)
+                rw = np.zeros(250, dtype=L.op_dtype())
+                rw[:n_loc] = loc
+                bufs.append(rw)
+            for w in range(W):
+                call(L.BatchType.invs, gen.invs(rng, pool, n_msg, sizes, False, tsp), mb, what=f"round {rnd} invs {w}")
+            for w in range(W):
+                call(L.BatchType.acks, gen.acks(rng, pool, n_msg, sizes, False, tsp), mb, rw=bufs[w],
+                     what=f"round {rnd} acks {w}")
+            for w in range(W):
+                call(L.BatchType.vals, gen.vals(rng, pool, n_msg, sizes, False, tsp), mb, what=f"round {rnd} vals {w}")
+            if rnd >= 8:
+                call(L.BatchType.local_ops_after_membership_change, gen.memb_ops(rng, pool, n_loc, sizes, False, tsp),
+                     mb_fail, what=f"round {rnd} membership")
+            entries_equal(pool, f"round {rnd}")
+        assert d.take_error_flags() == 0
+    finally:
+        d.set_skew(0)
 
 
 # ------------------------------------------------------------------ randomized protocol rounds

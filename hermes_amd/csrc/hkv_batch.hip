@@ -1584,6 +1584,100 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
     }
 }
 
+// k_unique for big objects (320-B entries, elements of up to 320 B: configs[2]): the same one pass,
+// with each element and its whole entry staged in LDS by the element's four lanes (16-B chunks,
+// coalesced), so the exec code -- 287-byte value copies included -- runs on LDS copies, and only the
+// 16-B chunks that changed go back. One wave per kUbElems elements.
+constexpr int kUbElems = 16;
+constexpr int kUbChunks = 20;   // 320 B
+template <int TYPE>
+__global__ __launch_bounds__(64) void k_unique_big(BatchArgs a)
+{
+    __shared__ uint4 sx[kUbElems * kUbChunks], sx0[kUbElems * kUbChunks];   // elements, as loaded
+    __shared__ uint4 se[kUbElems * kUbChunks], se0[kUbElems * kUbChunks];   // entries, as loaded
+    const int tid = threadIdx.x, q = tid & 3, el = tid >> 2, gbase = tid & ~3;
+    const int64_t i = (int64_t)blockIdx.x * kUbElems + el;
+    const bool live = i < a.n;
+    const int nch = (a.esz + 15) / 16;
+    uint8_t *xg = a.elems + i * a.esz;
+    for (int c = q; c < nch; c += 4) {
+        const uint4 v = live ? load_chunk(xg, c, a.esz) : make_uint4(0u, 0u, 0u, 0u);
+        sx[el * kUbChunks + c] = v;
+        sx0[el * kUbChunks + c] = v;
+    }
+    const uint4 c0 = sx[el * kUbChunks];   // the element's key and header (every lane of the group)
+    const uint64_t key = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
+    bool probe = false;
+    if (live && (a.offsets || in_count(a, (uint32_t)i))) {
+        if (!skip_elem_os(TYPE, (uint8_t)c0.z, (uint8_t)(c0.z >> 8))) {
+            probe = true;
+        } else if (TYPE == kInvs && a.ns_idx && q == 0) {
+            int64_t start;
+            const int32_t b = batch_of(a, i, start);
+            atomicMax(&a.ns_idx[b], (int32_t)(i - start));
+        }
+    }
+    bool ok;
+    uint64_t phys;
+    uint4 ln;
+    lookup_pair<1>(a, &key, &probe, q, gbase, &ok, &phys, &ln);
+    Meta m0;
+    const uint64_t ek = line_key_meta(ln, m0);
+    const bool hit = ok && ek == key;
+    if (hit) {
+        const uint4 *eg = reinterpret_cast<const uint4 *>(a.log + phys);
+        for (int c = q; c < kUbChunks; c += 4) {
+            const uint4 v = c < 4 ? ln : eg[c];
+            se[el * kUbChunks + c] = v;
+            se0[el * kUbChunks + c] = v;
+        }
+    }
+    __syncthreads();
+    if (q == 0 && live) {
+        uint8_t *x = reinterpret_cast<uint8_t *>(&sx[el * kUbChunks]);
+        uint8_t *ent = reinterpret_cast<uint8_t *>(&se[el * kUbChunks]);
+        if (hit) {
+            if (a.check_unique) {
+                const unsigned long long v = ((unsigned long long)(~a.rtag0) << 32) | (uint32_t)i;
+                const unsigned long long old = atomicExch(a.fw + fw_index(a, phys), v);
+                if ((uint32_t)(old >> 32) == ~a.rtag0 && a.error_flags) atomicOr(a.error_flags, 16u);
+            }
+            Ctx c = make_ctx(a);
+            int done = -1;
+            if (TYPE == kAcks) c.rw_done = &done;   // the batch is found only for a completion
+            Meta m;
+            meta_load(ent, m);
+            Meta t = m;
+            dispatch<287>(TYPE, x, ent, 0, t, c);
+            if (!meta_equal(t, m)) meta_store(ent, t);
+            if (TYPE == kAcks && done >= 0 && a.rw) {   // its read_write_ops slot and state mirror
+                uint8_t *xx;
+                uint8_t idx;
+                elem_at(a, (uint32_t)i, xx, idx, c);
+                complete_rw_slot(c, done);
+            }
+        } else if (probe) {
+            x[9] = kMiss;
+        }
+    }
+    __syncthreads();
+    if (live) {
+        for (int c = q; c < nch; c += 4) {
+            const uint4 w = sx[el * kUbChunks + c];
+            if (chunk_equal(w, sx0[el * kUbChunks + c])) continue;
+            if (16 * c + 16 <= a.esz) *reinterpret_cast<uint4 *>(xg + 16 * c) = w;
+            else *reinterpret_cast<uint64_t *>(xg + 16 * c) = (uint64_t)w.x | ((uint64_t)w.y << 32);
+        }
+    }
+    if (hit) {   // bytes 0..15 of an entry (the MICA key) never change
+        uint4 *eg = reinterpret_cast<uint4 *>(a.log + phys);
+        for (int c = q; c < kUbChunks; c += 4) {
+            const uint4 w = se[el * kUbChunks + c];
+            if (c > 0 && !chunk_equal(w, se0[el * kUbChunks + c])) eg[c] = w;
+        }
+    }
+}
+
 // Elements of keys that were INVALID at S_0, against their key's final F (k_resolve0_direct's rules)
 __global__ __launch_bounds__(256) void k_local_deferred(BatchArgs a)
 {
@@ -2785,6 +2879,10 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
             const unsigned lgrid = (unsigned)((n + kLfElems - 1) / kLfElems);
             if (bl.type == kInvs) hipLaunchKernelGGL(k_unique_lds<kInvs>, dim3(lgrid), dim3(64), 0, s, a);
             else hipLaunchKernelGGL(k_unique_lds<kAcks>, dim3(lgrid), dim3(64), 0, s, a);
+        } else if (ulds_env && bl.type == kInvs && bl.g.st_value == 287 && bl.g.entry_size == 320 && bl.esz <= 320) {
+            // big-object INVs, whose raises copy 287-B values: staged through LDS (cfg3: 460 -> 326 us per
+            // round). ACKs touch the header and the meta only, so they stay in place (LDS-staged: 110 -> 191 us)
+            hipLaunchKernelGGL(k_unique_big<kInvs>, dim3((unsigned)((n + kUbElems - 1) / kUbElems)), dim3(64), 0, s, a);
         } else if (bl.type == kInvs) HKV_UNIQUE(kInvs);
         else HKV_UNIQUE(kAcks);
 #undef HKV_UNIQUE

@@ -676,28 +676,30 @@ def test_local_opcode_mirror(engine_path):
     assert g.take_error_flags() & 8
 
 
-def test_unique_inv_launch_matches_oracle(engine_path):
-    """HKV_BATCH_UNIQUE INV launches (one pass, each element straight onto its entry): a peer's slab
-    with one INV per key -- raises, equal and smaller timestamps, keys in WRITE (OUT_OF_GROUP),
+@pytest.mark.parametrize("rmw,big", [(False, False), (False, True), (True, True)], ids=["default", "big", "big_rmw"])
+def test_unique_inv_launch_matches_oracle(engine_path, rmw, big):
+    """HKV_BATCH_UNIQUE INV launches (one pass, each element straight onto its entry; big objects:
+    element and entry staged in LDS, k_unique_big): a peer's slab with one INV per key -- raises,
+    equal and smaller timestamps, keys in WRITE (OUT_OF_GROUP), RMW INVs answered with INV-aborts,
     membership-change INVs (node_suspected), ragged counts and misses -- against the oracle; a slab
     with a repeated key raises error flag bit 4 (HKV_CHECK_UNIQUE, set by conftest)."""
     import os
     assert os.environ.get("HKV_CHECK_UNIQUE") == "1"
     rng = np.random.default_rng(4242)
-    g, o, sizes = make_pair(4000, 1024, 1 << 18)
+    g, o, sizes = make_pair(4000, 1024, 1 << 21 if big else 1 << 18, rmw=rmw, big=big)
     keys = gen_keys(4000)
     tsp = gen.TsPool(rng)
     mb = L.membership(5, 0)
     for rnd in range(6):
         # local writes first, so some keys sit in WRITE with a pending timestamp
-        loc = gen.local_ops(rng, gen.key_pool(rng, keys, hot=300), 2000, sizes, False, tsp)
+        loc = gen.local_ops(rng, gen.key_pool(rng, keys, hot=300), 2000, sizes, rmw, tsp)
         loc_o = gen.bytecopy(loc)
         _run_both(g, o, L.BatchType.local_ops, loc, loc_o, mb, 8, 250, None)
         gen.harvest_ts(tsp, loc)
         ids = rng.choice(4000, size=3000, replace=False)
         pool = np.concatenate([keys[ids], rng.integers(1, 2**63, size=16, dtype=np.int64).astype(np.uint64)])
         rng.shuffle(pool)
-        inv = gen.invs(rng, pool, len(pool), sizes, False, tsp)
+        inv = gen.invs(rng, pool, len(pool), sizes, rmw, tsp)
         inv["key"] = pool                           # every key once
         W, M = 4, len(pool) // 4
         counts = rng.integers(M // 2, M + 1, size=W).astype(np.int32)
@@ -710,7 +712,7 @@ def test_unique_inv_launch_matches_oracle(engine_path):
         np.testing.assert_array_equal(ns_g, ns_o)
         assert_tables_equal(g, o, f"round {rnd} unique invs")
     if engine_path == "engine":   # the check runs in the one-pass kernel
-        dup = gen.invs(rng, keys[:64], 512, sizes, False, tsp)
+        dup = gen.invs(rng, keys[:64], 512, sizes, rmw, tsp)
         dup["opcode"] = int(L.Op.INV)
         g.batch_host(L.BatchType.invs, dup, mb, n_batches=1, stride=512, unique=True)
         assert g.take_error_flags() & 16

@@ -9,7 +9,7 @@ i=0
 for v in "${variants[@]}"; do
   for w in $workers; do
     echo "v$i w$w: $common $v" >> $out/index.txt
-    timeout -k 10 180 python bench.py $common $v --workers $w --cpu-seconds 0 --host-api-seconds 0 --retry-steps 0 \
+    timeout -k 10 180 python bench.py $common $v --workers $w --cpu-seconds 0 --host-api-seconds 0 --policy-steps 0 \
       > $out/v${i}_w$w.log 2>&1 || exit 1
   done
   i=$((i+1))

@@ -736,15 +736,16 @@ __global__ __launch_bounds__(256) void k_regroup(const uint8_t *in, const int32_
 __global__ __launch_bounds__(64) void k_collect_vals(uint8_t *acks, const int32_t *count, int32_t stride,
                                                      uint32_t ack_size, uint8_t *out, int32_t C, int32_t *out_count,
                                                      uint32_t machine_id, unsigned long long *held,
-                                                     const int32_t *offsets, int32_t n_blocks)
+                                                     const int32_t *offsets, int32_t n_blocks, int64_t block_stride)
 {
     // one wave per worker (a worker's round has a few dozen ACKs)
     const int64_t w = blockIdx.x;
     const int lane = (int)threadIdx.x;
     // rows: worker w's ACKs at w * stride, count[w] of them; packed: [offsets[w], offsets[w+1]);
-    // n_blocks > 1: peer-major blocks of offsets[gridDim.x] elements, worker w's part in each
+    // n_blocks > 1: peer-major blocks of block_stride elements (0: offsets[gridDim.x], back to back),
+    // worker w's part in each
     const int n = offsets ? offsets[w + 1] - offsets[w] : count[w];
-    const int64_t block = n_blocks > 1 ? (int64_t)offsets[gridDim.x] : 0;
+    const int64_t block = n_blocks > 1 ? (block_stride > 0 ? block_stride : (int64_t)offsets[gridDim.x]) : 0;
     int base = 0;
     for (int blk = 0; blk < n_blocks; ++blk)
     for (int j0 = 0; j0 < n; j0 += 64) {
@@ -852,8 +853,12 @@ __global__ void k_marshal_acks_aligned(uint8_t *invs, const int32_t *counts, int
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint8_t *y = out + i * ack_size;
+    // a slot that carries no ACK: ST_EMPTY, with ST_OP_MEMBERSHIP_CHANGE in byte 9, which
+    // hermes_skip_ack skips (hermesKV.c:746-750), so a coordinator may apply a whole row as it
+    // arrives (ReplicaRound.acks); regrouping drops these slots by their opcode
     if ((int32_t)(i % width) >= counts[i / width]) {
         y[8] = kEmpty;
+        y[9] = kOpMembChange;
         return;
     }
     uint8_t *x = invs + i * op_size;
@@ -867,6 +872,7 @@ __global__ void k_marshal_acks_aligned(uint8_t *invs, const int32_t *counts, int
                 *reinterpret_cast<uint64_t *>(y + k) = *reinterpret_cast<const uint64_t *>(x + k);
     } else {
         y[8] = kEmpty;
+        y[9] = kOpMembChange;
     }
     if (oc == kInvSuccess || oc == kOpInvAbort || oc == kOpMembChange) x[8] = kEmpty;
 }
@@ -1674,7 +1680,18 @@ int hkv_wl_collect_vals_blocks(uint8_t *acks, const int32_t *count, int32_t n_wo
     if (n_workers <= 0) return 0;
     if (C <= 0 || ack_size % 8 || n_blocks < 1 || (n_blocks > 1 && !offsets)) return -1;
     hipLaunchKernelGGL(k_collect_vals, dim3(n_workers), dim3(64), 0, (hipStream_t)stream, acks, count, stride,
-                       ack_size, out, C, out_count, machine_id, held, offsets, n_blocks);
+                       ack_size, out, C, out_count, machine_id, held, offsets, n_blocks, (int64_t)0);
+    return ok();
+}
+
+int hkv_wl_collect_vals_rows(uint8_t *acks, int32_t n_workers, int32_t n_rows, int64_t row_stride, uint32_t ack_size,
+                             uint8_t *out, int32_t C, int32_t *out_count, uint32_t machine_id,
+                             unsigned long long *held, const int32_t *offsets, void *stream)
+{
+    if (n_workers <= 0) return 0;
+    if (C <= 0 || ack_size % 8 || n_rows < 1 || row_stride <= 0 || !offsets) return -1;
+    hipLaunchKernelGGL(k_collect_vals, dim3(n_workers), dim3(64), 0, (hipStream_t)stream, acks, nullptr, 0, ack_size,
+                       out, C, out_count, machine_id, held, offsets, n_rows, row_stride);
     return ok();
 }
 

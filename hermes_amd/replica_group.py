@@ -28,6 +28,7 @@ collectives done by tensor copies).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -53,6 +54,8 @@ _L.hkv_wl_marshal_memb_vals.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctyp
                                         ctypes.c_uint32, _P, _P]
 _L.hkv_wl_regroup_aligned.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_uint32,
                                       _P, ctypes.c_int32, _P, _P]
+_L.hkv_wl_collect_vals_rows.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, _P,
+                                        ctypes.c_int32, _P, ctypes.c_uint32, _P, _P, _P]
 
 MAX_REPLICAS = 8
 LOCAL = 250  # MAX_BATCH_KVS_OPS_SIZE, config.h:42
@@ -119,6 +122,11 @@ class ReplicaRound:
                                   ctypes.byref(zipf), write_permille, rmw_permille,
                                   ctypes.c_uint64(seed ^ (rank << 48)), _s()), "gen_trace")
         self.failed = False            # this replica has failed (fail()): it sends nothing more
+        # ACK rows applied as they arrive, one unique-key launch per peer (a peer answers each of this
+        # replica's INVs once, and a key has one local write in flight), with no regroup pass; once any
+        # replica has failed, its rows hold empty slots and the regrouped batch takes over for good
+        self.unique_acks = os.environ.get("HKV_GROUP_UNIQUE_ACKS", "1") != "0"
+        self.own_total = 0             # this round's packed INV total (round_shape)
         self.refill(first=True)
 
     # -- Hades: one view-update period per round when enabled
@@ -139,6 +147,11 @@ class ReplicaRound:
         """This replica fails after its INVs of the current round went out: from now on it sends
         no ACKs, VALs or INVs (it still joins the collectives, with empty slabs)."""
         self.failed = True
+        self.unique_acks = False
+
+    def peer_failing(self):
+        """Some replica fails this round: its ACK rows hold empty slots from now on"""
+        self.unique_acks = False
 
     def refill(self, first: bool = False):
         if self.failed:
@@ -179,8 +192,10 @@ class ReplicaRound:
     def round_shape(self) -> tuple[int, int]:
         """After the totals are gathered (host synchronisation): the round's width (the largest
         INV total of any rank) and this rank's ACK batch stride ((N-1) x its largest per-worker
-        INV count: a worker gets at most one ACK per INV from every peer)."""
-        v = torch.cat([self.inv_totals.max().view(1), self.inv_maxc]).cpu().tolist()
+        INV count: a worker gets at most one ACK per INV from every peer). Also keeps this rank's
+        own INV total (own_total) for the per-peer ACK launches."""
+        v = torch.cat([self.inv_totals.max().view(1), self.inv_maxc, self.inv_off[self.W:]]).cpu().tolist()
+        self.own_total = int(v[2])
         return max(1, int(v[0])), max(1, (self.N - 1) * int(v[1]))
 
     def inv_io(self, width: int):
@@ -223,6 +238,23 @@ class ReplicaRound:
         N, W, C = self.N, self.W, self.C
         if self.failed:
             self.val_off[W:].zero_()
+            return
+        if self.unique_acks:
+            # row p of ack_recv: peer p's ACKs lined up with inv_pack, worker w's at [inv_off[w], inv_off[w+1])
+            T = self.own_total
+            if T:
+                for p in range(N):
+                    if p != self.rank:
+                        self.kvs.batch(L.BatchType.acks, self.ack_recv[p * width * self.ack_size:], W, T, self.ack_size,
+                                       self.mb, rw=self.ops, rw_stride_bytes=LOCAL * self.op, offsets=self.inv_off,
+                                       rw_state=self.states, unique=True)
+            if self.count_elems:
+                self.elem_totals[1] += (N - 1) * T
+            check(_L.hkv_wl_collect_vals_rows(_ptr(self.ack_recv), W, N, width, self.ack_size, _ptr(self.val_slab), C,
+                                              _ptr(self.val_count), self.rank, _ptr(self.held[1:]), _ptr(self.inv_off),
+                                              _s()), "collect_vals_rows")
+            check(_L.hkv_wl_pack_rows(_ptr(self.val_slab), _ptr(self.val_count), W, C, L.OP_META_SIZE,
+                                      _ptr(self.val_pack), _ptr(self.val_off), _s()), "pack vals")
             return
         check(_L.hkv_wl_regroup_aligned(_ptr(self.ack_recv), N, width, _ptr(self.inv_off), _ptr(self.inv_count), W,
                                         self.ack_size, _ptr(self.ack_batch), stride, _ptr(self.ack_batch_count),
@@ -398,8 +430,10 @@ class ReplicaGroupRound:
         self._gather(*r.inv_total_io())
         width, stride = r.round_shape()  # the round's one host synchronisation
         self._gather(*r.inv_io(width))
-        if drop is not None and drop == r.rank:
-            r.fail()
+        if drop is not None:
+            r.peer_failing()
+            if drop == r.rank:
+                r.fail()
         _timed(events, "invs", lambda: r.invs(width), timed_batches)
         self._a2a(*r.ack_io(width))
         _timed(events, "acks", lambda: r.acks(width, stride), timed_batches)
@@ -505,6 +539,8 @@ class LoopbackGroup:
         width = shapes[0][0]                 # the same on every replica (max of the same totals)
         self._gather_io([r.inv_io(width) for r in rs])
         if drop is not None:
+            for r in rs:
+                r.peer_failing()
             rs[drop].fail()
         for r in rs:
             r.invs(width)

@@ -231,6 +231,13 @@ int hkv_wl_collect_vals_blocks(uint8_t *d_acks, const int32_t *d_count, int32_t 
                                uint32_t machine_id, unsigned long long *d_held, const int32_t *d_offsets,
                                int32_t n_blocks, void *stream);
 
+/* The same over the ACK rows a replica-group coordinator receives (ReplicaRound: n_rows rows of
+ * row_stride elements, row p from rank p, lined up with its packed INV slab): worker w's ACKs of
+ * every row are [d_offsets[w], d_offsets[w+1]) of the row; empty slots (ST_EMPTY) send nothing. */
+int hkv_wl_collect_vals_rows(uint8_t *d_acks, int32_t n_workers, int32_t n_rows, int64_t row_stride,
+                             uint32_t ack_size, uint8_t *d_val_out, int32_t C, int32_t *d_val_count,
+                             uint32_t machine_id, unsigned long long *d_held, const int32_t *d_offsets, void *stream);
+
 /* ---- VAL credits and the outstanding-VAL gate (hermes_worker.c:479-503, wings.h:424-540, 862-916)
  * Per worker: an ACK queue (d_aq rows of q_stride elements of ack_size bytes, d_aq_n queued) and a
  * carried-VAL queue (d_vq rows of vq_stride 16-B VALs, d_vq_n carried).

@@ -128,7 +128,8 @@ def test_marshal_acks_flat_rows_aligned(op_size, ack_size):
         assert got_oc[r] == len(want), r
         for k, y in enumerate(want):
             assert np.array_equal(got_out[r, k, :len(y)], y), (r, k)
-    # aligned: [rows][width], ACK in the INV's position, ST_EMPTY past each row's count
+    # aligned: [rows][width], ACK in the INV's position, ST_EMPTY past each row's count and where no ACK
+    # goes, with ST_OP_MEMBERSHIP_CHANGE in byte 9 (hermes_skip_ack skips such a slot)
     d_inv = _dev(inv.reshape(-1))
     d_out = torch.zeros(rows * C * ack_size, dtype=torch.uint8, device="cuda")
     WL.check(_L.hkv_wl_marshal_acks_aligned(WL._ptr(d_inv), WL._ptr(d_cnt), rows, C, op_size, WL._ptr(d_out),
@@ -139,7 +140,7 @@ def test_marshal_acks_flat_rows_aligned(op_size, ack_size):
         for j in range(C):
             y = _ack_ref(inv[r, j], ack_size, mid)[0] if j < cnt[r] else None
             if y is None:
-                assert got_out[r, j, 8] == OPC["EMPTY"], (r, j)
+                assert got_out[r, j, 8] == OPC["EMPTY"] and got_out[r, j, 9] == OPC["MEMB"], (r, j)
             else:
                 assert np.array_equal(got_out[r, j, :len(y)], y), (r, j)
 

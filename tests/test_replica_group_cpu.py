@@ -79,6 +79,9 @@ class TagReplica:
         assert self.drop == (self.rank, self.round)
         self.failed = True
 
+    def peer_failing(self):
+        assert self.drop is not None and self.drop[1] == self.round
+
     def membership_change(self, peer):
         assert self.drop == (peer, self.round)
         self.in_memb = True

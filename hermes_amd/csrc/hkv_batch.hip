@@ -100,6 +100,7 @@ struct BatchArgs {
     uint8_t *rws;                // ACK launches: read_write_ops state mirror (hkv_batch_desc.d_rw_state), or NULL
     int32_t dbg;                 // HKV_DBG: timing experiments that skip work (results invalid)
     int32_t check_unique;        // HKV_CHECK_UNIQUE: HKV_BATCH_UNIQUE launches verify their keys are unique
+    int32_t wave_copy;           // big values copied a wave per value (HKV_WAVE_COPY=0: by their own lane)
 };
 
 // Rounds after round 0 per batch type: how often a hot key usually mutates in one launch beyond
@@ -205,6 +206,7 @@ __device__ __forceinline__ Ctx make_ctx(const BatchArgs &a)
     c.rw = nullptr;
     c.rws = nullptr;
     c.rw_done = nullptr;
+    c.vc = nullptr;
     return c;
 }
 
@@ -921,17 +923,52 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
 
 // k_resolve0 for big ops (312 B) in place: one thread per element on its global copy, no LDS, so
 // occupancy is bound by registers instead of by 312 B of LDS per element (local and ACK launches)
+// The value copies the wave's exec calls recorded (Ctx::vc), one value at a time by the whole wave:
+// byte k of a value by lane k % 64, so each instruction moves 64 consecutive bytes. Every lane of the
+// wave calls it.
+__device__ __forceinline__ void wave_value_copies(const VCopy &v, uint32_t n)
+{
+    const int lane = threadIdx.x & 63;
+    unsigned long long todo = __ballot(v.dst != nullptr);
+    while (todo) {
+        const int j = __ffsll((long long)todo) - 1;
+        todo &= todo - 1;
+        const uint64_t d = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(uintptr_t)v.dst, j, 64) |
+                           ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)v.dst >> 32), j, 64) << 32);
+        const uint64_t s = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(uintptr_t)v.src, j, 64) |
+                           ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)v.src >> 32), j, 64) << 32);
+        uint8_t *dp = reinterpret_cast<uint8_t *>(d);
+        const uint8_t *sp = reinterpret_cast<const uint8_t *>(s);
+        uint8_t b[5];
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {   // values up to 320 B; all loads before the stores
+            const uint32_t k = (uint32_t)lane + 64u * r;
+            b[r] = k < n ? sp[k] : 0;
+        }
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            const uint32_t k = (uint32_t)lane + 64u * r;
+            if (k < n) dp[k] = b[r];
+        }
+    }
+}
+
 template <int TYPE, int SV>
 __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
 {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.n) return;
-    const uint32_t e = a.ent[i];
+    const bool in = i < a.n;
+    const uint32_t e = in ? a.ent[i] : kNone;
     uint8_t st = kStDone;
-    uint8_t *xg;
-    uint8_t idx;
+    uint8_t *xg = nullptr;
+    uint8_t idx = 0;
     Ctx c = make_ctx(a);
-    elem_at(a, (uint32_t)i, xg, idx, c);
+    // big values: the exec calls record their value copy, made by the whole wave afterwards (the
+    // key's entry is not written in this pass -- its first candidate writes its own shadow -- and
+    // the op is this lane's own)
+    VCopy vc{nullptr, nullptr};
+    if (SV != 31 && a.wave_copy && a.g.st_value <= 320) c.vc = &vc;
+    if (in) elem_at(a, (uint32_t)i, xg, idx, c);
     if (e != kNone) {
         Meta m;
         meta_load(entry_of(a, e), m);
@@ -953,6 +990,8 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
             st = kStPend;
         }
     }
+    if (SV != 31) wave_value_copies(vc, a.g.st_value);
+    if (!in) return;
     a.st[i] = st;
     note_state(a, i, xg);
 }
@@ -2473,6 +2512,7 @@ __device__ void hp_partition(const HostPartCommon &p, HpLds &L, int g, int nb, u
     c.rw = reinterpret_cast<uint8_t *>(hd.rw);
     c.rws = nullptr;
     c.rw_done = nullptr;
+    c.vc = nullptr;
     const int type = hd.type;
     // lookup (hermesKV.c:938-993)
     uint32_t e = kNone;
@@ -2791,6 +2831,8 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.dbg = dbg_env;
     static const int check_unique_env = getenv("HKV_CHECK_UNIQUE") ? atoi(getenv("HKV_CHECK_UNIQUE")) : 0;
     a.check_unique = check_unique_env;
+    static const int wave_copy_env = !getenv("HKV_WAVE_COPY") || atoi(getenv("HKV_WAVE_COPY")) != 0;
+    a.wave_copy = wave_copy_env;
     if (dbg_env) a.error_flags = nullptr;
     a.index = bl.index;
     a.log = bl.log;

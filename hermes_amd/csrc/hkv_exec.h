@@ -114,6 +114,14 @@ __device__ __forceinline__ void copy_value(uint8_t *__restrict__ dst, const uint
     copy_bytes(dst, src, SV > 0 ? (uint32_t)SV : n);
 }
 
+// A value copy an exec function leaves to its caller (Ctx::vc): big values (287 B) copied by one
+// lane touch a few cache lines per dword, 64 lines per wave instruction; the caller copies them
+// afterwards a whole wave per value (wave_value_copies)
+struct VCopy {
+    uint8_t *dst;
+    const uint8_t *src;
+};
+
 struct Ctx {           // per-launch constants
     Geometry g;
     uint8_t g_membership;
@@ -121,7 +129,20 @@ struct Ctx {           // per-launch constants
     uint8_t *rw;       // this element's batch read_write_ops (ACKs)
     uint8_t *rws;      // its state-byte mirror (hkv_batch_desc.d_rw_state), or null
     int *rw_done;      // non-null: exec_ack leaves the read_write_ops completion to the caller
+    VCopy *vc;         // non-null: big-value copies are recorded here instead of made (at most one per dispatch)
 };
+
+template <int SV>
+__device__ __forceinline__ void copy_value_c(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint32_t n,
+                                             const Ctx &c)
+{
+    if (SV != 31 && c.vc) {
+        c.vc->dst = dst;
+        c.vc->src = src;
+        return;
+    }
+    copy_value<SV>(dst, src, n);
+}
 
 __device__ __forceinline__ bool is_last_ack(uint8_t bv, const Ctx &c)  // spacetime.h:253-259
 {
@@ -136,7 +157,7 @@ __device__ __forceinline__ void local_state_to_op(uint8_t *op, const Meta &m, co
     op[9] = kReplaySuccess;
     e_set_ts(op, m.ver, m_cid(m));
     op[10] = (uint8_t)(c.g.st_value >> c.g.shift);
-    copy_value<SV>(op + kOpValueOff, entry + kEntryValueOff, c.g.st_value);
+    copy_value_c<SV>(op + kOpValueOff, entry + kEntryValueOff, c.g.st_value, c);
 }
 
 // hermes_write_replay_actions, hermesKV.c:155-175
@@ -164,7 +185,7 @@ __device__ __forceinline__ void membership_replay(uint8_t *op, uint8_t idx, Meta
 template <int SV>
 __device__ __forceinline__ void update_actions(uint8_t *op, uint8_t *entry, uint8_t idx, Meta &m, const Ctx &c, uint8_t rmw_flag)
 {
-    copy_value<SV>(entry + kEntryValueOff, op + kOpValueOff, c.g.st_value);
+    copy_value_c<SV>(entry + kEntryValueOff, op + kOpValueOff, c.g.st_value, c);
     m_set_val_len(m, (uint8_t)((op[10] >> c.g.shift) + kOpMetaSize));
     m_set_rmw(m, rmw_flag);
     m_set_state(m, kWrite);
@@ -199,7 +220,7 @@ __device__ __forceinline__ void exec_read(uint8_t *op, uint8_t *entry, uint8_t i
 {
     uint8_t st = m_state(m);
     if (st == kValid) {
-        copy_value<SV>(op + kOpValueOff, entry + kEntryValueOff, c.g.st_value);
+        copy_value_c<SV>(op + kOpValueOff, entry + kEntryValueOff, c.g.st_value, c);
         op[9] = kGetComplete;
         op[10] = (uint8_t)((m_val_len(m) >> c.g.shift) - kOpMetaSize);
     } else if (st == kInvalidWrite || st == kWrite || st == kReplay) {
@@ -292,7 +313,7 @@ __device__ __forceinline__ void exec_inv(uint8_t *inv, uint8_t *entry, Meta &m, 
             m_set_val_len(m, (uint8_t)c.g.kvs_value);
             m_set_rmw(m, inv_rmw);
             m_set_lwid(m, inv[9]);
-            copy_value<SV>(entry + kEntryValueOff, inv + kOpValueOff, c.g.st_value);
+            copy_value_c<SV>(entry + kEntryValueOff, inv + kOpValueOff, c.g.st_value, c);
             m.ver = (uint32_t)(its >> 8);
             m_set_cid(m, (uint8_t)its);
         } else if (cur == its) {

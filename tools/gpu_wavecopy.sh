@@ -1,0 +1,14 @@
+#!/bin/bash
+# Big-value copies a wave per value (k_resolve0_direct): parity tests, an A/B of HKV_WAVE_COPY on
+# configs[2] (3 alternating reps), and a cfg3 kernel-stats profile with it on.   tools/gpu_wavecopy.sh TAG
+tag=$1; out=gpurun_out/$tag; mkdir -p $out; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_workload_gpu.py -x -v --timeout 120 \
+  --timeout-method thread > $out/tests.log 2>&1 || exit 1
+for rep in 1 2 3; do
+  for v in 1 0; do
+    HKV_WAVE_COPY=$v timeout -k 10 240 python bench.py --config cfg3 --steps 20 --warmup 3 --cpu-seconds 0 \
+      --host-api-seconds 0 --policy-steps 0 > $out/b_${v}_$rep.log 2>&1 || exit 2
+  done
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/$out/prof -o run -- python3 bench.py \
+  --config cfg3 --steps 10 --warmup 3 --cpu-seconds 0 --host-api-seconds 0 --policy-steps 0 > $out/prof.log 2>&1 || exit 3

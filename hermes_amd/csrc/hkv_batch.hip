@@ -296,9 +296,11 @@ __device__ __forceinline__ uint32_t agg_ticket(uint32_t *arr, uint32_t j, bool a
 
 // x: the element (global), or its LDS copy
 template <int TYPE, int SV>
-__device__ __forceinline__ void resolve_elem(const BatchArgs &a, uint32_t i, uint8_t *x, uint8_t *entry)
+__device__ __forceinline__ void resolve_elem(const BatchArgs &a, uint32_t i, uint8_t *x, uint8_t *entry,
+                                             VCopy *vc = nullptr)
 {
     Ctx c = make_ctx(a);
+    c.vc = vc;
     uint8_t *xg;
     uint8_t idx;
     elem_at(a, i, xg, idx, c);
@@ -1763,6 +1765,10 @@ __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
     const bool kStage = SV == 31 && a.esz <= 16;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     bool left = false;
+    // big values: copied a wave per value after the exec calls (see k_resolve0_direct); the shadow
+    // they read (round r-1's first candidate's) is not written in this round
+    VCopy vc{nullptr, nullptr};
+    VCopy *vcp = SV != 31 && a.wave_copy && a.g.st_value <= 320 ? &vc : nullptr;
     if (i < a.n && a.st[i] == kStPend) {
         const uint32_t e = a.ent[i];
         const uint32_t f = first_cand(*fw_of(a, e), a.rtag0 + (uint32_t)r);
@@ -1773,7 +1779,7 @@ __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
             if (kStage) copy_elem(xl, xg, a.esz);
             if ((uint32_t)i != f) {
                 if (kStage) resolve_elem<TYPE, SV>(a, (uint32_t)i, xl, shadow_of(a, prev));
-                else resolve_elem<TYPE, SV>(a, (uint32_t)i, xg, shadow_of(a, prev));
+                else resolve_elem<TYPE, SV>(a, (uint32_t)i, xg, shadow_of(a, prev), vcp);
                 a.st[i] = kStDone;
             } else {
                 apply_to_shadow<TYPE, SV>(a, kStage ? xl : nullptr, (uint32_t)i, shadow_of(a, prev));
@@ -1787,6 +1793,7 @@ __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
             left = r == a.rounds;
         }
     }
+    if (SV != 31) wave_value_copies(vc, a.g.st_value);
     if (r == a.rounds) {  // wave-aggregated append (uniform branch)
         const uint32_t t = agg_ticket(&a.ctr[kCtrFbL], 0u, left);
         if (left) a.fbl[t] = (uint32_t)i;

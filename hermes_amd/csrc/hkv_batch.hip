@@ -1841,6 +1841,46 @@ __global__ __launch_bounds__(256) void k_commit(BatchArgs a)
     }
 }
 
+// k_commit for 64-B entries over few commits (the local direct path: one per key a PUT first
+// wrote): each wave takes 1024 elements, reads their stage bytes 16 per lane, lists the committing
+// ones in LDS (a wave-wide prefix sum of the per-lane counts), then copies their shadows 16
+// entries at a time, four lanes per entry. One wave per 1024 elements instead of one thread per
+// element: k_commit's cost was its 4M threads, not its copies.
+constexpr int kCwElems = 1024;
+__global__ __launch_bounds__(256) void k_commit_w(BatchArgs a)
+{
+    __shared__ uint32_t lst[4][kCwElems];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t e0 = ((int64_t)blockIdx.x * 4 + w) * kCwElems + 16 * lane;
+    uint32_t m = 0;
+    if (e0 + 16 <= a.n) {   // st is 256-byte aligned and e0 a multiple of 16
+        const uint4 s4 = *reinterpret_cast<const uint4 *>(a.st + e0);
+        const uint32_t sw[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+        for (int b = 0; b < 16; ++b)
+            if (((sw[b >> 2] >> (8 * (b & 3))) & 0xFFu) == kStCommit) m |= 1u << b;
+    } else {
+        for (int b = 0; b < 16; ++b)
+            if (e0 + b < a.n && a.st[e0 + b] == kStCommit) m |= 1u << b;
+    }
+    const uint32_t c = __popc(m);
+    uint32_t incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, d, 64);
+        if (lane >= d) incl += v;
+    }
+    const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
+    for (uint32_t pos = incl - c; m; m &= m - 1) lst[w][pos++] = (uint32_t)e0 + (uint32_t)(__ffs(m) - 1);
+    __syncthreads();
+    const int q = lane & 3;
+    for (uint32_t j = (uint32_t)(lane >> 2); j < total; j += 16) {
+        const uint32_t i = lst[w][j];
+        const uint4 v = reinterpret_cast<const uint4 *>(shadow_of(a, i))[q];
+        reinterpret_cast<uint4 *>(entry_of(a, a.ent[i]))[q] = v;
+    }
+}
+
 constexpr int kFbThreads = 1024;
 constexpr int kFbPerThread = 8;
 constexpr int kFbChunk = kFbThreads * kFbPerThread;
@@ -2912,7 +2952,12 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
         hipLaunchKernelGGL(k_local_pre, dim3((unsigned)((n + kPreElems - 1) / kPreElems)), dim3(256), 0, s, a);
         hipLaunchKernelGGL(k_local_fused, dim3((unsigned)((n + kLfElems - 1) / kLfElems)), dim3(64), 0, s, a);
         hipLaunchKernelGGL(k_local_deferred, dim3(8), dim3(256), 0, s, a);
-        hipLaunchKernelGGL((k_commit<31>), dim3(grid), dim3(256), 0, s, a);
+        // HKV_COMMIT_W=0: the thread-per-element k_commit (experiments)
+        static const bool commit_w_env = !getenv("HKV_COMMIT_W") || atoi(getenv("HKV_COMMIT_W")) != 0;
+        if (commit_w_env)
+            hipLaunchKernelGGL(k_commit_w, dim3((unsigned)((n + 4 * kCwElems - 1) / (4 * kCwElems))), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_commit<31>), dim3(grid), dim3(256), 0, s, a);
     } else if (bl.unique && (bl.type == kInvs || bl.type == kAcks)) {  // one pass: every key has one element
         constexpr int64_t kPerU = 64 * kLookupPair;
         const unsigned ugrid = (unsigned)((n + kPerU - 1) / kPerU);

@@ -100,6 +100,7 @@ struct BatchArgs {
     uint8_t *rws;                // ACK launches: read_write_ops state mirror (hkv_batch_desc.d_rw_state), or NULL
     int32_t dbg;                 // HKV_DBG: timing experiments that skip work (results invalid)
     int32_t check_unique;        // HKV_CHECK_UNIQUE: HKV_BATCH_UNIQUE launches verify their keys are unique
+    int32_t pre_patch_first;     // k_local_pre reads a PUT's header only when it has no patch (HKV_PRE_PATCH_FIRST)
     int32_t wave_copy;           // big values copied a wave per value (HKV_WAVE_COPY=0: by their own lane)
 };
 
@@ -1208,12 +1209,30 @@ __global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
         opm[k] = a.opc ? a.opc[in[k] ? i : 0] : (uint8_t)kOpPut;
     }
     U64x2 pt[kAllK];
+    if (a.pre_patch_first && a.patch) {
+        // the patches first: a refilled PUT's patch holds all the prepass needs (key, opcode, ST_NEW),
+        // so only the PUTs kept from the last round read their op header (a second dependent load
+        // for them, against a third of the op slab's lines fetched for nothing)
 #pragma unroll
-    for (int k = 0; k < kAllK; ++k) {
-        const bool own = k < kOwnK;
-        const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
-        h[k] = *reinterpret_cast<const U64x2 *>(a.elems + (in[k] && opm[k] == kOpPut ? i : 0) * 56);
-        pt[k] = a.patch && in[k] && opm[k] == kOpPut ? *reinterpret_cast<const U64x2 *>(a.patch + i * 16) : U64x2{0, 0};
+        for (int k = 0; k < kAllK; ++k) {
+            const bool own = k < kOwnK;
+            const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
+            pt[k] = in[k] && opm[k] == kOpPut ? *reinterpret_cast<const U64x2 *>(a.patch + i * 16) : U64x2{0, 0};
+        }
+#pragma unroll
+        for (int k = 0; k < kAllK; ++k) {
+            const bool own = k < kOwnK;
+            const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
+            h[k] = *reinterpret_cast<const U64x2 *>(a.elems + (in[k] && opm[k] == kOpPut && !patch_valid(pt[k].b) ? i : 0) * 56);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kAllK; ++k) {
+            const bool own = k < kOwnK;
+            const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
+            h[k] = *reinterpret_cast<const U64x2 *>(a.elems + (in[k] && opm[k] == kOpPut ? i : 0) * 56);
+            pt[k] = a.patch && in[k] && opm[k] == kOpPut ? *reinterpret_cast<const U64x2 *>(a.patch + i * 16) : U64x2{0, 0};
+        }
     }
 #pragma unroll
     for (int k = 0; k < kAllK; ++k)
@@ -2878,6 +2897,8 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.dbg = dbg_env;
     static const int check_unique_env = getenv("HKV_CHECK_UNIQUE") ? atoi(getenv("HKV_CHECK_UNIQUE")) : 0;
     a.check_unique = check_unique_env;
+    static const int ppf_env = !getenv("HKV_PRE_PATCH_FIRST") || atoi(getenv("HKV_PRE_PATCH_FIRST")) != 0;
+    a.pre_patch_first = ppf_env;
     static const int wave_copy_env = !getenv("HKV_WAVE_COPY") || atoi(getenv("HKV_WAVE_COPY")) != 0;
     a.wave_copy = wave_copy_env;
     if (dbg_env) a.error_flags = nullptr;

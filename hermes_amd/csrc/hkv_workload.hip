@@ -371,13 +371,18 @@ __global__ __launch_bounds__(256) void k_refill_direct(uint8_t *ops, int32_t str
                                                        uint32_t st_value, uint32_t shift, const uint64_t *tkey,
                                                        const uint8_t *top, int32_t tlen, uint32_t *cursor,
                                                        uint32_t machine_id, int32_t first_iter, uint32_t rflags,
-                                                       unsigned long long *counters, uint8_t *opc_out)
+                                                       unsigned long long *counters, uint8_t *opc_out,
+                                                       uint8_t *states)
 {
     const bool refill_all = (rflags & HKV_WL_REFILL_ALL) != 0;
     const int w = blockIdx.x, i = threadIdx.x;
     const bool live = i < stride;
-    uint8_t *op = ops + ((int64_t)w * stride + (live ? i : 0)) * op_size;
-    const uint8_t st = live ? op[9] : 0;
+    const int64_t e = (int64_t)w * stride + (live ? i : 0);
+    uint8_t *op = ops + e * op_size;
+    // states: the caller's state mirror (every op's state byte, kept by the batches and marshals),
+    // read instead of the op, so a slot that is not refilled is not touched at all (312-B ops: one
+    // line each), and the refilled ones are only written
+    const uint8_t st = live ? (states ? states[e] : op[9]) : 0;
     const bool complete = is_complete(st);
     const bool drop = live && !first_iter && refill_all && !complete && !in_flight(st);
     const bool done = live && (first_iter || complete || drop);
@@ -407,11 +412,24 @@ __global__ __launch_bounds__(256) void k_refill_direct(uint8_t *ops, int32_t str
         uint64_t *h1 = reinterpret_cast<uint64_t *>(op + 8);
         const uint64_t vl = oc == kOpGet ? 0 : (uint8_t)(st_value >> shift);
         // a GET's timestamp (bytes 11..15) is reset under HKV_WL_READ_TS_RESET (inline-util.h:268-272)
-        const uint64_t keep = oc == kOpGet && (rflags & HKV_WL_READ_TS_RESET) ? 0ull : ~0xFFFFFFull;
-        *h1 = (*h1 & keep) | oc | ((uint64_t)kNew << 8) | (vl << 16);
+        const bool reset = oc == kOpGet && (rflags & HKV_WL_READ_TS_RESET);
+        if (states) {   // stores only (no read of the op's line)
+            op[8] = oc;
+            op[9] = kNew;
+            op[10] = (uint8_t)vl;
+            if (reset) {
+                op[11] = 0;
+                *reinterpret_cast<uint32_t *>(op + 12) = 0;
+            }
+            states[e] = kNew;
+        } else {
+            const uint64_t keep = reset ? 0ull : ~0xFFFFFFull;
+            *h1 = (*h1 & keep) | oc | ((uint64_t)kNew << 8) | (vl << 16);
+        }
         if (oc == kOpGet) *reinterpret_cast<uint16_t *>(op + 16) = flags;
     }
-    if (opc_out && live) opc_out[(int64_t)w * stride + i] = done ? oc : op[8];  // the opcode mirror
+    // the opcode mirror (with the state mirror, a slot that is not refilled keeps its mirror byte)
+    if (opc_out && live && (done || !states)) opc_out[(int64_t)w * stride + i] = done ? oc : op[8];
     // the values of the writes, one op at a time per wave: lane k stores 8-B word k of bytes
     // 16 .. 18 + st_value (word 0 carries the flags), the tail bytes go to the lanes after them
     const uint64_t vv = 0x0101010101010101ull * (uint8_t)('a' + machine_id);
@@ -1444,7 +1462,7 @@ int hkv_wl_refill(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_s
     if (op_size > 64 && st_value >= 6 && (kOpValueOff - 16 + st_value) / 8 + 7 <= 64) {  // big ops: in place
         hipLaunchKernelGGL(k_refill_direct, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
                            st_value, shift, tkey, top, tlen, cursor, machine_id, first_iter, flags, counters,
-                           opc_out);
+                           opc_out, (uint8_t *)nullptr);
         return ok();
     }
     if (lds > 160 * 1024 - 64) return -1;
@@ -1453,6 +1471,19 @@ int hkv_wl_refill(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_s
         return -1;
     hipLaunchKernelGGL(k_refill, dim3(n_workers), dim3(256), lds, (hipStream_t)stream, ops, stride, op_size, st_value,
                        shift, tkey, top, tlen, cursor, machine_id, first_iter, flags, counters, opc_out);
+    return ok();
+}
+
+int hkv_wl_refill_st(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint32_t st_value,
+                     uint32_t shift, const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor,
+                     uint32_t machine_id, uint32_t flags, unsigned long long *counters, uint8_t *opc,
+                     uint8_t *states, void *stream)
+{
+    if (stride > 256 || n_workers <= 0 || tlen <= 0 || !states || !opc) return -1;
+    if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET)) return -1;   // no hot-request coalescing
+    if (!(op_size > 64 && op_size % 8 == 0 && st_value >= 6 && (kOpValueOff - 16 + st_value) / 8 + 7 <= 64)) return -1;
+    hipLaunchKernelGGL(k_refill_direct, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
+                       st_value, shift, tkey, top, tlen, cursor, machine_id, 0, flags, counters, opc, states);
     return ok();
 }
 

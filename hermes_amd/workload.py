@@ -35,6 +35,8 @@ _L.hkv_wl_refill.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32
                              _P, _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint32, _P, _P,
                              _P, _P]
 _L.hkv_wl_fold_counters.argtypes = [_P, _P]
+_L.hkv_wl_refill_st.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _P]
 _L.hkv_wl_refill_plan.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, _P, _P,
                                   ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _P]
 _L.hkv_wl_marshal_invs.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]
@@ -157,6 +159,10 @@ class Round:
         # mirror) or 312-B ops (refilled in place). Default: wherever it applies.
         can_fuse = not coalesce_hot and val_credits is None and self.op <= 64
         self.fused = can_fuse if fused_refill is None else (fused_refill and can_fuse)
+        # 312-B ops are refilled in place, but from the same state mirror (hkv_wl_refill_st), so a slot
+        # the refill keeps is not read (HKV_REFILL_ST=0: from the ops, experiments)
+        self.st_refill = (not coalesce_hot and val_credits is None and self.op > 64
+                          and os.environ.get("HKV_REFILL_ST", "1") != "0")
         self.machine_id = kvs.machine_id
         dev = torch.device("cuda", kvs.device)
         W, S = n_workers, self.LOCAL
@@ -317,6 +323,12 @@ class Round:
                                         self.machine_id, self.rflags, _ptr(self.counters), _ptr(self.opcodes),
                                         _ptr(self.patch), _s()), "refill_plan")
             return
+        if self.st_refill and not first:
+            check(_L.hkv_wl_refill_st(_ptr(self.ops), self.W, self.LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
+                                      _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
+                                      self.machine_id, self.rflags, _ptr(self.counters), _ptr(self.opcodes),
+                                      _ptr(self.states), _s()), "refill_st")
+            return
         check(_L.hkv_wl_refill(_ptr(self.ops), self.W, self.LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
                                _ptr(self.trace_key), _ptr(self.trace_op), _ptr(self.trace_id), self.trace_len,
                                _ptr(self.cursor), self.machine_id, int(first), self.rflags, _ptr(self.counters),
@@ -382,7 +394,7 @@ class Round:
     def _rws(self):
         """the state mirror the ACK batch keeps current (only the fused refill plans from it; the
         VAL-credits marshal does not maintain it)"""
-        return self.states if self.fused else None
+        return self.states if self.fused or self.st_refill else None
 
     def ack_batch(self, acks: torch.Tensor | None = None, n_batches: int | None = None, stride: int | None = None,
                   counts: torch.Tensor | None = None):

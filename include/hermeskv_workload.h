@@ -89,6 +89,14 @@ int hkv_wl_refill_plan(const uint8_t *d_states, int32_t n_workers, int32_t strid
                        const uint64_t *d_trace_key, const uint8_t *d_trace_op, int32_t trace_len, uint32_t *d_cursor,
                        uint32_t machine_id, uint32_t flags, unsigned long long *d_counters, uint8_t *d_opcode,
                        uint8_t *d_patch, void *stream);
+/* hkv_wl_refill for big ops (op_size > 64, refilled in place; not on the first pass, flags
+ * HKV_WL_REFILL_ALL and HKV_WL_READ_TS_RESET), deciding from d_states, the state mirror
+ * hkv_wl_refill_plan reads: an op that is not refilled is not touched, a refilled one is only
+ * written (and its mirror byte set to ST_NEW); d_opcode takes the refilled ops' opcodes. */
+int hkv_wl_refill_st(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint32_t st_value,
+                     uint32_t shift, const uint64_t *d_trace_key, const uint8_t *d_trace_op, int32_t trace_len,
+                     uint32_t *d_cursor, uint32_t machine_id, uint32_t flags, unsigned long long *d_counters,
+                     uint8_t *d_opcode, uint8_t *d_states, void *stream);
 /* d_counters[0..4] += the refill stripes (which are cleared) */
 int hkv_wl_fold_counters(unsigned long long *d_counters, void *stream);
 

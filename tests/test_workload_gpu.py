@@ -545,3 +545,35 @@ def test_marshal_invs_kernel_matches_numpy(big, mirror):
         assert np.array_equal(out[w, :cnt[w]], exp_out[w, :cnt[w]]), f"worker {w}: INV rows differ"
     assert np.array_equal(d_ops.cpu().numpy(), exp_ops.reshape(-1)), "op states differ"
     assert int(d_held.item()) == held
+
+
+def test_big_op_refill_from_state_mirror():
+    """configs[2]'s refill (312-B ops, refilled in place) decides from the state mirror
+    (hkv_wl_refill_st) instead of each op's state byte: the mirror must equal the ops' state bytes
+    and the opcode mirror their opcodes after every round, and the ops, cursors and counters must
+    match a twin round refilled from the ops themselves, byte for byte."""
+    from hermes_amd.kvs import HermesKV
+    from hermes_amd.workload import Round, zipf_params
+    n_keys, bkts, cap = 60_000, 1 << 16, 1 << 25
+    rounds = []
+    for st_refill in (True, False):
+        g = HermesKV(n_keys, bkts, cap, machine_id=0, rmw=True, big_objects=True, extra_cache_lines=4, skew=3)
+        r = Round(g, 40, L.membership(3, 0), [1, 2], zipf_params(n_keys, 0.99), 500, 500, seed=0x5EED,
+                  max_steps=8, trace_len=1024, retry_stalled=True)
+        r.st_refill = st_refill and r.st_refill
+        rounds.append((g, r))
+    assert rounds[0][1].st_refill, "configs[2] rounds refill from the state mirror"
+    for _ in range(6):
+        for _, r in rounds:
+            r.step()
+        torch.cuda.synchronize()
+        a, b = rounds[0][1], rounds[1][1]
+        ops = a.ops.view(-1, a.op)
+        assert torch.equal(a.states, ops[:, 9]), "state mirror differs from the ops' state bytes"
+        assert torch.equal(a.opcodes, ops[:, 8]), "opcode mirror differs from the ops' opcodes"
+        assert torch.equal(a.ops, b.ops), "refill from the mirror differs from the refill from the ops"
+        assert torch.equal(a.cursor, b.cursor)
+    assert rounds[0][1].stats() == rounds[1][1].stats()
+    assert rounds[0][1].stats()["committed"] > 0
+    for g, _ in rounds:
+        assert g.take_error_flags() == 0

@@ -25,6 +25,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 EVENT_EVERY = 4                # timed steps per sampled local-launch duration
 PROBE_STEPS = 3                # untimed steps with every batch launch timed
+AUDIT_STEPS = 6                # untimed steps whose commits are broken down by outcome (CommitAudit)
 # algorithmic bytes per element, SURVEY.md 8(d): S_op (56, or 312 big), bucket 64, entry (64, or
 # 320 big), S_msg 16 (ACKs carry S_op with RMWs)
 def elem_bytes(op: int, entry: int, ack: int) -> dict:
@@ -34,6 +35,31 @@ def elem_bytes(op: int, entry: int, ack: int) -> dict:
     meta = min(entry, 64)
     return {"get": op + 64 + entry + op, "put": op + 64 + 2 * entry + op, "inv": op + 64 + 2 * entry + op,
             "ack": ack + 64 + 2 * meta + ack, "val": 16 + 64 + 2 * meta + 16}
+
+
+def table_digest(kvs, n_keys: int, chunk: int = 1 << 23) -> tuple[int, int]:
+    """(digest, keys not VALID) of a replica's protocol state: each populated log entry's state,
+    timestamp (cid, version) and value, position-weighted (the populated entries sit back to back
+    in the same order on every replica). Equal digests on all replicas = the group converged."""
+    import torch
+
+    class _Dev:   # the log as a torch tensor without a copy (__cuda_array_interface__)
+        def __init__(self, ptr, n):
+            self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False), "version": 3}
+    e = kvs.sizes.entry
+    cols = torch.tensor([18] + list(range(23, 28)) + list(range(33, 33 + min(31, kvs.sizes.st_value))),
+                        device=f"cuda:{kvs.device}")
+    w = (torch.arange(cols.numel(), device=cols.device, dtype=torch.int64) * 0x9E3779B1 + 0x7F4A7C15) | 1
+    log = torch.as_tensor(_Dev(kvs.device_log(), n_keys * e), device=f"cuda:{kvs.device}").view(n_keys, e)
+    dig = torch.zeros((), dtype=torch.int64, device=cols.device)
+    bad = torch.zeros((), dtype=torch.int64, device=cols.device)
+    for lo in range(0, n_keys, chunk):
+        x = log[lo:lo + chunk].index_select(1, cols).to(torch.int64)
+        h = (x * w).sum(1)
+        pos = torch.arange(lo, lo + x.shape[0], device=cols.device, dtype=torch.int64) * 0x2545F491 + 1
+        dig += ((h * pos) & 0xFFFFFFFFFFFF).sum()
+        bad += (x[:, 0] != 1).sum()      # VALID_STATE
+    return int(dig.item()), int(bad.item())
 
 
 def parse():
@@ -157,12 +183,15 @@ def main():
     z = zipf_params(a.keys, a.zipf)
     total_steps = a.warmup + a.steps
     cpu = None
-    snap = None
+    snaps = {}
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
         # the CPU baseline runs on the freshly populated table image (copied out of HBM now), after
-        # the GPU's timed region so that its threads never compete with the GPU run's host thread
+        # the GPU's timed region so that its threads never compete with the GPU run's host thread;
+        # a second image runs the reference's shipped configuration (retry, no skew flags) beside it
         from oracle.cpu_baseline import TableSnapshot
-        snap = TableSnapshot(kvs)
+        snaps["headline"] = TableSnapshot(kvs)
+        if retry and a.skew and not a.coalesce_hot:
+            snaps["retry"] = TableSnapshot(kvs, skew=0)
 
     if world > 1:
         from hermes_amd.replica_group import ReplicaGroupRound
@@ -216,15 +245,29 @@ def main():
     torch.cuda.synchronize()
     n_inv, n_ack, n_val = ((rnd.elem_totals - e0).double() / PROBE_STEPS).tolist()
     puts_per_step = float((rnd.inv_total - inv0).item()) / PROBE_STEPS
+    # how the committed ops completed (value-less GETs, coalesced PUTs: DESIGN.md section 5), over
+    # untimed rounds that continue the timed ones
+    audit = rnd.audit_rounds(AUDIT_STEPS) if world == 1 and not a.coalesce_hot else None
     flags = kvs.take_error_flags()
 
+    convergence = None
     if world > 1:
-        tt = torch.tensor([committed, elapsed * 1e9, flags], dtype=torch.float64, device="cuda")
+        # every replica's table after the last round (no write in flight): the live replicas must
+        # agree on every key's state, timestamp and value, and every key must be VALID again (cfg5:
+        # INVALID only where the failed replica's last writes were never validated)
+        digest, not_valid = table_digest(kvs, a.keys)
+        tt = torch.tensor([committed, elapsed * 1e9, flags, not_valid], dtype=torch.float64, device="cuda")
         allc = [torch.zeros_like(tt) for _ in range(world)]
         dist.all_gather(allc, tt)
+        dg = torch.tensor([digest], dtype=torch.int64, device="cuda")
+        alld = [torch.zeros_like(dg) for _ in range(world)]
+        dist.all_gather(alld, dg)
         committed_all = int(sum(x[0].item() for x in allc))
         elapsed_max = max(x[1].item() for x in allc) / 1e9
         flags_any = int(max(x[2].item() for x in allc))
+        live = [r for r in range(world) if not (cfg5 and r == drop_id)]
+        convergence = {"digests": [int(x.item()) for x in alld], "not_valid": [int(x[3].item()) for x in allc],
+                       "live_ranks_agree": len({int(alld[r].item()) for r in live}) == 1}
     else:
         committed_all, elapsed_max, flags_any = committed, elapsed, flags
 
@@ -336,6 +379,18 @@ def main():
             "round_stats_rank0": rnd.stats(),
         },
     }
+    if convergence is not None:
+        out["detail"]["convergence"] = convergence
+    if audit is not None:
+        out["detail"]["commit_breakdown"] = audit
+        # committed ops excluding value-less GETs and PUTs completed by an inherited timestamp, at
+        # the audited rounds' share of the timed rate
+        out["detail"]["committed_strict"] = {
+            "value": value * audit["strict_fraction"] if audit["strict_fraction"] is not None else None,
+            "unit": "ops/s", "strict_fraction": audit["strict_fraction"],
+            "what": "GET_COMPLETE with a value + PUT_COMPLETE by the PUT's own write or coalesced on a timestamp "
+                    "the PUT recorded itself + RMW_COMPLETE, as a share of all commits over "
+                    f"{audit['rounds']} audited rounds after the timed ones, times value"}
     if flags_any and not os.environ.get("HKV_DBG"):   # HKV_DBG: timing experiments that skip work
         print(json.dumps({"error": f"device consistency flags {flags_any:#x} raised", "partial": out}), flush=True)
         raise SystemExit(3)
@@ -347,15 +402,24 @@ def main():
         out["detail"]["membership"].update(agreement="hades", epoch=hz.state()[1] if hz else None)
         if world == 1:
             out["detail"]["membership"]["agreed_at_round"] = [c[0] for c in rnd.hades_changes]
-    if snap is not None:
-        from oracle.cpu_baseline import run_cpu_baseline
+    if snaps:
+        from oracle.cpu_baseline import host_cores, run_cpu_baseline
         from hermes_amd.workload import refill_flags
         cpu = run_cpu_baseline(kvs, z, a.write_permille, a.cpu_workers, a.cpu_seconds, a.seed,
                                refill_flags=refill_flags(kvs, retry, a.coalesce_hot), threads=a.cpu_threads,
-                               snapshot=snap)
+                               snapshot=snaps["headline"])
+        cpu.update(host_cores())
+        if "retry" in snaps:   # refill_ops without skew flags: no GET timestamp reset either
+            c0 = run_cpu_baseline(kvs, z, a.write_permille, a.cpu_workers, a.cpu_seconds, a.seed,
+                                  refill_flags=0, threads=a.cpu_threads, snapshot=snaps["retry"])
+            cpu["policies"] = {"retry": {k: c0[k] for k in ("value", "unit", "cores", "kind", "sample",
+                                                           "probe_ops_per_s_by_threads")}}
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if world == 1 and a.policy_steps > 0 and not cfg5:
+        # the policies start from the table this run leaves: every write of it must have completed,
+        # which holds only when no INV was held back by the send credits (nothing else is in flight)
+        assert int(rnd.held.item()) == 0, "INVs held back: writes in flight would skew the other policies"
         out["detail"]["policies"] = policy_rates(a, kvs, z, L, Round, (retry, a.skew, a.coalesce_hot))
     if rank == 0 and world == 1 and a.host_api_seconds > 0:
         out["detail"]["host_api"] = host_api_rate(a.host_api_seconds)
@@ -386,6 +450,8 @@ def policy_rates(a, kvs, z, L, Round, headline) -> dict:
     out = {}
     skew0 = kvs.skew
     warm = max(a.warmup, 10)
+    # every policy starts from a table with no write in flight: the headline round's INVs all went
+    # out (none held back by the send credits), so its last ACK batch completed every write
     for name, retry, skew, hot, what in POLICIES:
         if (retry, skew, hot) == headline:
             continue
@@ -402,9 +468,14 @@ def policy_rates(a, kvs, z, L, Round, headline) -> dict:
         torch.cuda.synchronize()
         dt = time.perf_counter() - t
         c = (r.fold_counters()[:4] - c0).tolist()
+        audit = r.audit_rounds(3) if not hot else None
+        held = int(r.held.item())
+        assert held == 0, f"policy {name}: INVs held back"   # the next policy needs a quiet table
         out[name] = {"value": c[0] / dt, "unit": "ops/s", "steps": a.policy_steps, "warmup": warm,
                      "ms_per_step": dt * 1e3 / a.policy_steps, "committed_per_step": c[0] / a.policy_steps,
                      "writes_completed_per_step": c[2] / a.policy_steps, "dropped_per_step": c[3] / a.policy_steps,
+                     "invs_held": held, "commit_breakdown": audit,
+                     "committed_strict": c[0] / dt * audit["strict_fraction"] if audit and audit["strict_fraction"] else None,
                      "what": what}
         del r
     kvs.set_skew(skew0)

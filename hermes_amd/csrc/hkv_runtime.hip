@@ -69,6 +69,12 @@ struct CallerStage {
     uint8_t *h = nullptr, *d = nullptr;
     size_t cap = 0;
     std::vector<uint32_t> perm;   // element i of the caller's batch sits at staged slot perm[i]
+    // a caller returns only after its launch's flags arrived, so nothing reads the staging when
+    // its thread exits: threads that come and go do not leak pinned memory
+    ~CallerStage()
+    {
+        if (h) (void)hipHostFree(h);
+    }
 };
 static thread_local CallerStage t_stage;
 

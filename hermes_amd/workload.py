@@ -124,6 +124,97 @@ def _ptr(t: torch.Tensor | None):
     return _P(t.data_ptr()) if t is not None else None
 
 
+class CommitAudit:
+    """How the ops a round commits completed (diagnostics: run only in untimed steps).
+
+    refill_ops counts GET_COMPLETE, PUT_COMPLETE and RMW_COMPLETE alike (inline-util.h:189-217),
+    but under the opt-in skew optimisations (config.h:79-80) two of them can complete without
+    doing what the name says:
+    * hermes_complete_hot_read_optimization (hermesKV.c:224-238) completes a stalled GET without
+      copying a value. Its val_len stays 0 (refill_ops zeroes a GET's, inline-util.h:276), where
+      hermes_read_actions (:240-246) sets the entry's;
+    * hermes_complete_coalesced_write (:209-221) completes a stalled PUT in the local batch,
+      without a write of its own, against the 16-bit version in its ts. That version was either
+      recorded by this PUT at its first stall (its slot's ts.version was 0 when refill_ops put it
+      there) or inherited from the slot's previous op, since refill_ops never resets a PUT's
+      timestamp (:260-276).
+    A PUT's own write completes in the ACK batch (or the after-membership-change batch), never in
+    the local batch. Provenance is known only for PUTs refilled while the audit runs: PUT_COMPLETEs
+    of older PUTs are counted under `put_coalesced_unknown`."""
+
+    FIELDS = ("get_value", "get_no_value", "put_own", "put_coalesced_recorded", "put_coalesced_inherited",
+              "put_coalesced_unknown", "rmw", "other")
+
+    def __init__(self, rnd):
+        self.r = rnd
+        n = rnd.ops.numel() // rnd.op
+        dev = rnd.ops.device
+        self.prov = torch.full((n,), 3, dtype=torch.uint8, device=dev)   # 3 unknown, 1 recorded, 2 inherited
+        self.after_local = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.acc = torch.zeros(len(self.FIELDS), dtype=torch.int64, device=dev)
+        self.counting = False          # False: provenance tracking only (the first audited round)
+        self.rounds = 0
+
+    def _view(self):
+        return self.r.ops.view(-1, self.r.op)
+
+    def pre_local(self):
+        """before the local launch: the provenance of every slot refilled for this round"""
+        ops = self._view()
+        patch = getattr(self.r, "patch", None)
+        if getattr(self.r, "fused", False) and patch is not None:
+            p = patch.view(-1, 16)
+            fresh, oc = p[:, 14] == 1, p[:, 8]
+        else:
+            fresh, oc = ops[:, 9] == int(L.Bucket.NEW), ops[:, 8]
+        tsv = ops[:, 12:16].contiguous().view(torch.int32).view(-1)
+        put = fresh & (oc == int(L.Op.PUT))
+        self.prov = torch.where(put, torch.where(tsv != 0, 2, 1).to(torch.uint8),
+                                torch.where(fresh, torch.zeros_like(self.prov), self.prov))
+
+    def post_local(self):
+        ops = self._view()
+        st, oc, vl = ops[:, 9], ops[:, 8], ops[:, 10]
+        self.after_local.copy_(st)
+        if not self.counting:
+            return
+        get_c = (oc == int(L.Op.GET)) & (st == int(L.Resp.GET_COMPLETE))
+        put_c = st == int(L.Resp.PUT_COMPLETE)
+        self.acc[0] += (get_c & (vl != 0)).sum()
+        self.acc[1] += (get_c & (vl == 0)).sum()
+        self.acc[3] += (put_c & (self.prov == 1)).sum()
+        self.acc[4] += (put_c & (self.prov == 2)).sum()
+        self.acc[5] += (put_c & (self.prov >= 3)).sum()
+
+    def end(self):
+        """after the round, before the refill counts it"""
+        if not self.counting:
+            self.counting = True
+            return
+        st = self._view()[:, 9]
+        put_c = st == int(L.Resp.PUT_COMPLETE)
+        self.acc[2] += (put_c & (self.after_local != int(L.Resp.PUT_COMPLETE))).sum()
+        self.acc[6] += (st == int(L.Resp.RMW_COMPLETE)).sum()
+        self.acc[7] += (st == int(L.Op.MEMBERSHIP_COMPLETE)).sum()
+        self.rounds += 1
+
+    def result(self, committed: int | None = None) -> dict:
+        """per-round means; `committed`: the refill's commit count over the same rounds (the sum
+        of the breakdown must equal it)"""
+        v = self.acc.cpu().tolist()
+        d = dict(zip(self.FIELDS, v))
+        total = sum(v)
+        strict = d["get_value"] + d["put_own"] + d["put_coalesced_recorded"] + d["rmw"] + d["other"]
+        n = max(self.rounds, 1)
+        out = {"rounds": self.rounds, "per_round": {k: x / n for k, x in d.items()},
+               "committed_per_round": total / n, "committed_strict_per_round": strict / n,
+               "strict_fraction": strict / total if total else None}
+        if committed is not None:
+            out["refill_committed_per_round"] = committed / n
+            out["consistent"] = committed == total
+        return out
+
+
 def _s(stream=None):
     return _P((stream or torch.cuda.current_stream()).cuda_stream)
 
@@ -160,8 +251,8 @@ class Round:
         can_fuse = not coalesce_hot and val_credits is None and self.op <= 64
         self.fused = can_fuse if fused_refill is None else (fused_refill and can_fuse)
         # 312-B ops are refilled in place, but from the same state mirror (hkv_wl_refill_st), so a slot
-        # the refill keeps is not read (HKV_REFILL_ST=0: from the ops, experiments)
-        self.st_refill = (not coalesce_hot and val_credits is None and self.op > 64
+        # the refill keeps is not read (fused_refill=False or HKV_REFILL_ST=0: from the ops)
+        self.st_refill = (not coalesce_hot and val_credits is None and self.op > 64 and fused_refill is not False
                           and os.environ.get("HKV_REFILL_ST", "1") != "0")
         self.machine_id = kvs.machine_id
         dev = torch.device("cuda", kvs.device)
@@ -261,6 +352,7 @@ class Round:
         # (tbl_ready, recorded before each refill) to the local batch, which waits for them.
         # Measured slower (1.884 vs 1.907 G ops/s, 3 x 30 steps each), so in line by default.
         self.overlap = os.environ.get("HKV_PEER_OVERLAP", "0") == "1" and self.pack_remote
+        self.audit: CommitAudit | None = None   # audit_rounds(): per-outcome commit breakdown (untimed)
         if self.overlap:
             self.side = torch.cuda.Stream(device=dev)
             self.tbl_ready, self.pts_done = torch.cuda.Event(), torch.cuda.Event()
@@ -493,7 +585,11 @@ class Round:
                 self.peer_timestamps_packed(k)
             else:
                 self.peer_timestamps(k, sent)
+        if self.audit is not None:
+            self.audit.pre_local()
         timed("local", self.local_batch)
+        if self.audit is not None:
+            self.audit.post_local()
         self.marshal_invs()
         if self.count_elems:
             self.inv_total += self.inv_count.sum()
@@ -573,6 +669,8 @@ class Round:
             self.membership_change(drop)
         if self.overlap:
             self.tbl_ready.record()
+        if self.audit is not None:
+            self.audit.end()
         self.refill()
         self.clock += 1
 
@@ -645,6 +743,19 @@ class Round:
         """counters[0..4] brought up to date (refill leaves per-worker-group partial sums)"""
         check(_L.hkv_wl_fold_counters(_ptr(self.counters), _s()), "fold_counters")
         return self.counters
+
+    def audit_rounds(self, n: int) -> dict:
+        """One round that only tracks provenance, then n rounds whose commits are broken down by
+        outcome (CommitAudit); checked against the refill's own commit count over the same rounds."""
+        self.audit = CommitAudit(self)
+        self.step()
+        c0 = int(self.fold_counters()[0].item())
+        for _ in range(n):
+            self.step()
+        c1 = int(self.fold_counters()[0].item())
+        out = self.audit.result(c1 - c0)
+        self.audit = None
+        return out
 
     def committed(self) -> int:
         return int(self.fold_counters()[0].item())

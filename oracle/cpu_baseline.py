@@ -28,19 +28,27 @@ def host_threads(cap: int = 16) -> int:
     return max(1, min(n, cap))
 
 
+def host_cores() -> dict:
+    """The host's cores beside the ones the baseline may use: the machine's CPUs, this process's
+    affinity set, and the usable count (host_threads: capped by OMP_NUM_THREADS, 16 on the GPU box)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"host_cpus": os.cpu_count(), "host_affinity_cpus": aff, "host_usable_threads": host_threads()}
+
+
 class TableSnapshot:
     """The device table's image (index and log) copied into an oracle table, taken before the GPU
     rounds change it, so the CPU baseline can run after the GPU's timed region (nothing of it then
     competes with the GPU run's host thread)."""
 
-    def __init__(self, kvs):
+    def __init__(self, kvs, skew: int | None = None):
+        """skew: the oracle table's skew flags (default: the device table's)"""
         build()
         self.L = L = lib()
         L.hko_set_log_head.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         c = kvs.cfg
         self.c = c
         self.cfg = Config(c.big_objects, c.extra_cache_lines, c.rmw_enabled, c.machine_id, c.num_bkts, c.log_cap,
-                          c.skew_flags, 0)
+                          c.skew_flags if skew is None else int(skew), 0)
         self.h = L.hko_create(ctypes.byref(self.cfg))
         from hermes_amd.lib import check, raw
         R = raw()
@@ -66,7 +74,7 @@ def run_cpu_baseline(kvs, zipf, write_permille: int, workers: int, seconds: floa
     reset, 4 hot-request coalescing; 0 = refill_ops' retry). The table's skew flags come with it.
     snapshot: a TableSnapshot taken earlier (consumed); default: the table as it is now."""
     snap = snapshot if snapshot is not None else TableSnapshot(kvs)
-    L, h, cfg, c = snap.L, snap.h, snap.cfg, snap.c
+    L, h, cfg = snap.L, snap.h, snap.cfg
     L.hko_bench_rounds.restype = ctypes.c_int64
     L.hko_bench_rounds.argtypes = [ctypes.c_void_p, ctypes.POINTER(Config), ctypes.c_int, ctypes.c_int,
                                    ctypes.c_double, ctypes.POINTER(HkoZipf), ctypes.c_uint32, ctypes.c_int,
@@ -93,7 +101,7 @@ def run_cpu_baseline(kvs, zipf, write_permille: int, workers: int, seconds: floa
             "probe_ops_per_s_by_threads": probe,
             "sample": (f"{threads} worker threads sharing one table (per-key seqlocks, concur_ctrl.h:144-224), "
                        f"{workers} x 250-op {'fresh' if refill_flags & 1 else 'retried (refill_ops)'} local batches "
-                       f"per round, refill flags {refill_flags}, skew flags {c.skew_flags}, "
+                       f"per round, refill flags {refill_flags}, skew flags {cfg.skew_flags}, "
                        f">= {rounds.value} rounds each in {secs.value:.1f} s; +{n_peers} virtual peers (one write per "
                        f"key and round each, live timestamps, up to {per_peer} per worker-round), 2 ACKs per write; "
-                       f"same table ({c.num_bkts} buckets, copied from HBM) and Zipf/write mix as the GPU run")}
+                       f"same table ({cfg.num_bkts} buckets, copied from HBM) and Zipf/write mix as the GPU run")}

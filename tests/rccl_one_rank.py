@@ -8,6 +8,7 @@ as ReplicaGroupRound lays it out ([N][width] rows, row p = replica p) and then m
 (all_gather_into_tensor / all_to_all_single over the one rank, async_op with the wait before the
 consumer, on torch's stream), with the tensors, sizes and dtypes of a real round. Every batch launch
 is mirrored into an oracle table and every key must converge. Prints one JSON line.
+`--retry-skew`: bench.py's configuration (refill_ops' retry and the skew flags 3).
 """
 import json
 import os
@@ -57,15 +58,17 @@ def main():
                 calls["all_to_all_single"] += 1
                 calls["bytes"] += o.numel() * o.element_size()
 
+    retry_skew = "--retry-skew" in sys.argv
+    skew = 3 if retry_skew else 0
     n_rep, n_keys, bkts, cap = 3, 4000, 8192, 1 << 20
     z = zipf_params(n_keys, 0.99)
     reps, mirrors = [], []
     for r in range(n_rep):
-        g = HermesKV(n_keys, bkts, cap, machine_id=r)
-        o = OracleKVS(bkts, cap, r)
+        g = HermesKV(n_keys, bkts, cap, machine_id=r, skew=skew)
+        o = OracleKVS(bkts, cap, r, skew=skew)
         o.populate(n_keys, L.DEFAULT.kvs_value)
         mirrors.append(Mirror(g, o, f"replica {r}"))
-        reps.append(ReplicaRound(g, 16, n_rep, r, z, 300, seed=99 + r, trace_len=512))
+        reps.append(ReplicaRound(g, 16, n_rep, r, z, 300, seed=99 + r, trace_len=512, retry_stalled=retry_skew))
     grp = RcclLoopback(reps)
     keys = gen_keys(n_keys)
     for _ in range(3):
@@ -88,7 +91,8 @@ def main():
     except Exception:   # noqa: BLE001 -- the version is informational
         ver = None
     print(json.dumps({"launches": [m.launches for m in mirrors], "calls": calls, "diverged_keys": bad,
-                      "committed": [s["committed"] for s in stats], "rccl_version": ver}))
+                      "committed": [s["committed"] for s in stats], "rccl_version": ver, "skew": skew,
+                      "retry": retry_skew}))
 
 
 if __name__ == "__main__":

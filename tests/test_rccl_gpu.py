@@ -24,12 +24,14 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def test_one_rank_rccl_group_round():
+@pytest.mark.parametrize("args", [[], ["--retry-skew"]])
+def test_one_rank_rccl_group_round(args):
+    """args: [] the fresh policy; --retry-skew bench.py --gpus N's configuration (retry, skew flags 3)"""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
                LOCAL_RANK="0")
-    p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_one_rank.py")], capture_output=True,
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_one_rank.py"), *args], capture_output=True,
                        text=True, timeout=170, env=env, cwd=ROOT)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     d = json.loads(p.stdout.strip().splitlines()[-1])

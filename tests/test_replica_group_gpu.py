@@ -43,12 +43,15 @@ def _key_images(g, o, keys):
     return rows
 
 
-@pytest.mark.parametrize("n_rep,workers,write_pm,rounds", [(2, 24, 300, 4), (3, 16, 400, 4), (4, 8, 500, 3),
-                                                           (8, 16, 200, 3)])
-def test_loopback_group_parity_and_convergence(n_rep, workers, write_pm, rounds):
+@pytest.mark.parametrize("n_rep,workers,write_pm,rounds,retry,skew", [
+    (2, 24, 300, 4, False, 0), (3, 16, 400, 4, False, 0), (4, 8, 500, 3, False, 0), (8, 16, 200, 3, False, 0),
+    (8, 16, 200, 4, True, 3), (8, 16, 200, 4, True, 0), (3, 24, 400, 5, True, 3)])
+def test_loopback_group_parity_and_convergence(n_rep, workers, write_pm, rounds, retry, skew):
     """(8, 16, 200, 3) is BASELINE configs[3]'s group on one GPU: 8 replicas (the width of the
     membership vectors), 20 % writes, Zipf 0.99 -- every phase, kernel and slab layout of the RCCL
-    run, with every launch of every replica mirrored into its oracle twin."""
+    run, with every launch of every replica mirrored into its oracle twin. retry / skew: the
+    configuration bench.py --gpus N runs (refill_ops' retry, stalled ops keep their slots, and the
+    reference's skew optimisations, config.h:79-80) and the reference's shipped one (skew 0)."""
     from hermes_amd.kvs import HermesKV
     from hermes_amd.replica_group import LoopbackGroup, ReplicaRound
     from hermes_amd.workload import zipf_params
@@ -57,11 +60,11 @@ def test_loopback_group_parity_and_convergence(n_rep, workers, write_pm, rounds)
     z = zipf_params(n_keys, 0.99)
     reps, mirrors = [], []
     for r in range(n_rep):
-        g = HermesKV(n_keys, bkts, cap, machine_id=r)
-        o = OracleKVS(bkts, cap, r)
+        g = HermesKV(n_keys, bkts, cap, machine_id=r, skew=skew)
+        o = OracleKVS(bkts, cap, r, skew=skew)
         o.populate(n_keys, L.DEFAULT.kvs_value)
         mirrors.append(Mirror(g, o, f"replica {r}"))
-        reps.append(ReplicaRound(g, workers, n_rep, r, z, write_pm, seed=77 + r, trace_len=512))
+        reps.append(ReplicaRound(g, workers, n_rep, r, z, write_pm, seed=77 + r, trace_len=512, retry_stalled=retry))
     grp = LoopbackGroup(reps)
     keys = gen_keys(n_keys)
     for step in range(rounds):
@@ -84,6 +87,13 @@ def test_loopback_group_parity_and_convergence(n_rep, workers, write_pm, rounds)
     inv_sent = sum(int(r.inv_total.item()) for r in reps)
     inv_applied = sum(int(r.elem_totals[0].item()) for r in reps)
     assert inv_applied == inv_sent * (n_rep - 1)
+    if retry:
+        # stalled ops kept their slots (nothing dropped) and the skew flags' outcomes occurred
+        stalls = sum(m.codes[(int(L.BatchType.local_ops), "out9", int(c))] for m in mirrors
+                     for c in (L.Resp.GET_STALL, L.Resp.PUT_STALL))
+        assert stalls > 0
+        coalesced = sum(m.codes[(int(L.BatchType.local_ops), "out9", int(L.Resp.PUT_COMPLETE))] for m in mirrors)
+        assert (coalesced > 0) == bool(skew & 2), coalesced
 
 
 @pytest.mark.parametrize("n_rep", [3, 4])
@@ -253,7 +263,7 @@ def test_loopback_group_hconsistent_between_phases(n_rep, hades):
         assert grp.hades_changes and all(c[2][1] == ((1 << n_rep) - 1) & ~(1 << dead) for c in grp.hades_changes)
 
 
-def _dist_child(rank, world, port, q, drop=None):
+def _dist_child(rank, world, port, q, drop=None, retry=False, skew=0):
     import os
 
     import torch.distributed as dist
@@ -265,9 +275,9 @@ def _dist_child(rank, world, port, q, drop=None):
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         n_keys = 4000
-        g = HermesKV(n_keys, 8192, 1 << 20, machine_id=rank)
+        g = HermesKV(n_keys, 8192, 1 << 20, machine_id=rank, skew=skew)
         drv = ReplicaGroupRound(g, 16, zipf_params(n_keys, 0.99), 400, seed=99, world=world, rank=rank,
-                                trace_len=512)
+                                trace_len=512, retry_stalled=retry)
         for k in range(4 if drop is not None else 3):
             drv.step(drop=drop if k == 1 else None)
         torch.cuda.synchronize()
@@ -286,10 +296,12 @@ def _dist_child(rank, world, port, q, drop=None):
         q.put((rank, None, None, 0, repr(e)))
 
 
-@pytest.mark.parametrize("world,drop", [(2, None), (3, None), (3, 2)])
-def test_dist_group_driver_one_gpu(world, drop):
+@pytest.mark.parametrize("world,drop,retry,skew", [(2, None, False, 0), (3, None, False, 0), (3, 2, False, 0),
+                                                   (3, None, True, 3)])
+def test_dist_group_driver_one_gpu(world, drop, retry, skew):
     """ReplicaGroupRound itself (the driver bench.py runs over RCCL), with `world` processes
-    sharing one GPU over gloo (which takes CUDA tensors): every key converges across ranks."""
+    sharing one GPU over gloo (which takes CUDA tensors): every key converges across ranks; also
+    under bench.py's configuration (retry + skew flags 3)."""
     import socket
 
     import torch.multiprocessing as mp
@@ -299,7 +311,7 @@ def test_dist_group_driver_one_gpu(world, drop):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dist_child, args=(r, world, port, q, drop)) for r in range(world)]
+    procs = [ctx.Process(target=_dist_child, args=(r, world, port, q, drop, retry, skew)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in procs], key=lambda x: x[0])
@@ -352,6 +364,11 @@ def test_bench_multi_rank_over_gloo(world, config):
     line = [x for x in p.stdout.splitlines() if x.startswith("{")][-1]
     d = json.loads(line)
     assert d["n_gpus"] == world and d["value"] > 0 and d["detail"]["error_flags"] == 0, d
+    conv = d["detail"]["convergence"]
+    assert conv["live_ranks_agree"], conv          # every live replica holds the same keys
+    if config == "cfg2":
+        assert conv["not_valid"] == [0] * world, conv
+        assert d["config"]["refill"] == "retry" and d["config"]["skew_flags"] == 3
     assert d["config"]["parallelism"] == f"replicas{world}"
     assert d["roofline"]["launches"]["invs"]["elements"] > 0
     if config == "cfg5":

@@ -85,6 +85,20 @@ def test_retry_round_mirrored(skew, hot):
     assert (coalesced > 0) == bool(skew & 2), m.codes
     if hot:   # some committed ops were coalesced requests
         assert st["committed"] > 0
+    else:
+        # the per-outcome breakdown bench.py reports (CommitAudit): it adds up to the refill's own
+        # commit count, and the value-less GETs / coalesced PUTs exist only under their skew flag
+        a = r.audit_rounds(3)
+        assert a["consistent"], a
+        pr = a["per_round"]
+        assert pr["get_value"] > 0 and pr["put_own"] > 0, a
+        if not skew & 1:
+            assert pr["get_no_value"] == 0, a
+        if not skew & 2:
+            assert pr["put_coalesced_recorded"] + pr["put_coalesced_inherited"] + pr["put_coalesced_unknown"] == 0, a
+        if skew == 3:
+            assert pr["get_no_value"] + pr["put_coalesced_recorded"] + pr["put_coalesced_inherited"] > 0, a
+        assert g.take_error_flags() == 0
 
 
 class _DeviceBytes:

@@ -381,6 +381,10 @@ def main():
     }
     if convergence is not None:
         out["detail"]["convergence"] = convergence
+        plan = getattr(rnd, "plan", None)
+        if plan is not None:   # slabs sized without a host read in all but every calib_every-th round
+            out["detail"]["slab_width"] = {"width": plan.width, "calib_every": plan.calib_every, "slack": plan.slack,
+                                           "rounds": plan.k}
     if audit is not None:
         out["detail"]["commit_breakdown"] = audit
         # committed ops excluding value-less GETs and PUTs completed by an inherited timestamp, at

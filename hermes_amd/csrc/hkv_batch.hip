@@ -98,6 +98,9 @@ struct BatchArgs {
     const uint8_t *opc;          // local launches: the caller's opcode mirror (may be NULL, see k_local_pre)
     const uint8_t *patch;        // local direct path: pending header writes (hkv_batch_desc.d_patch), or NULL
     uint8_t *rws;                // ACK launches: read_write_ops state mirror (hkv_batch_desc.d_rw_state), or NULL
+    const uint64_t *pkeys;       // local direct path: the PUT-key mirror (hkv_batch_desc.d_put_keys), or NULL
+    int32_t n_rows, skip_row;    // HKV_BATCH_ROWS: rows applied in order (k_unique_rows), one skipped (-1: none)
+    int64_t row_stride;          // elements between rows
     int32_t dbg;                 // HKV_DBG: timing experiments that skip work (results invalid)
     int32_t check_unique;        // HKV_CHECK_UNIQUE: HKV_BATCH_UNIQUE launches verify their keys are unique
     int32_t pre_patch_first;     // k_local_pre reads a PUT's header only when it has no patch (HKV_PRE_PATCH_FIRST)
@@ -1201,6 +1204,29 @@ __global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
     U64x2 h[kAllK];
     bool in[kAllK];
     uint8_t opm[kAllK];
+    U64x2 pt[kAllK];
+    if (a.pkeys) {
+        // the caller's PUT-key mirror and entry states (hkv_batch_desc.d_put_keys): two dense arrays,
+        // one load each and no dependence between them, instead of opcode mirror -> patch -> op header
+        // (k_local_fused checks both mirrors against every element)
+        uint64_t pk[kAllK];
+        uint8_t ps[kAllK];
+#pragma unroll
+        for (int k = 0; k < kAllK; ++k) {
+            const bool own = k < kOwnK;
+            const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
+            in[k] = i < a.n && (own || i < head_end);
+            pk[k] = in[k] ? a.pkeys[i] : ~0ull;
+            ps[k] = in[k] ? a.state_out[i] : (uint8_t)0;
+        }
+#pragma unroll
+        for (int k = 0; k < kAllK; ++k) {
+            h[k].a = pk[k];
+            h[k].b = (uint64_t)(pk[k] != ~0ull ? kOpPut : kOpGet) | ((uint64_t)ps[k] << 8);
+            opm[k] = (uint8_t)h[k].b;
+            pt[k] = U64x2{0, 0};
+        }
+    } else {
 #pragma unroll
     for (int k = 0; k < kAllK; ++k) {
         const bool own = k < kOwnK;
@@ -1208,7 +1234,6 @@ __global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
         in[k] = i < a.n && (own || i < head_end);
         opm[k] = a.opc ? a.opc[in[k] ? i : 0] : (uint8_t)kOpPut;
     }
-    U64x2 pt[kAllK];
     if (a.pre_patch_first && a.patch) {
         // the patches first: a refilled PUT's patch holds all the prepass needs (key, opcode, ST_NEW),
         // so only the PUTs kept from the last round read their op header (a second dependent load
@@ -1240,6 +1265,7 @@ __global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
             h[k].a = pt[k].a;
             h[k].b = (h[k].b & ~0xFFFFull) | (pt[k].b & 0xFFu) | ((uint64_t)kNew << 8);
         }
+    }
 #pragma unroll
     for (int k = 0; k < kAllK; ++k) {
         const bool own = k < kOwnK;
@@ -1320,25 +1346,29 @@ __global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
 // nothing shared beyond it. The lookup runs four lanes per element (each lane holds 16 B of the op
 // and of the log line); the wave-private LDS copies of op and entry are then resolved one element
 // per lane, so the exec code's branches are paid once per 32 elements; the ops go back whole.
+template <int P>
 __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
 {
-    __shared__ uint4 sops[kLfElems * 4];   // 64 B per op (56 used)
-    __shared__ uint4 sln[kLfElems * 4];
-    __shared__ unsigned long long sfw[kLfElems];
-    __shared__ uint32_t sent[kLfElems];     // entry id of a hit, kNone otherwise
-    __shared__ uint8_t sprb[kLfElems];      // probed (not skipped)
-    __shared__ uint32_t sdef[kLfElems];
+    constexpr int E = 16 * P;   // elements per wave: P per lane group
+    __shared__ uint4 sops[E * 4];   // 64 B per op (56 used)
+    __shared__ uint4 sln[E * 4];
+    __shared__ unsigned long long sfw[E];
+    __shared__ uint32_t sent[E];     // entry id of a hit, kNone otherwise
+    __shared__ uint8_t sprb[E];      // probed (not skipped)
+    __shared__ uint32_t sdef[E];
     __shared__ uint32_t ndef;
+    __shared__ unsigned long long spk[E];  // the PUT-key mirror's word (a.pkeys)
+    __shared__ uint8_t sps[E];             // the entry state the mirror gives
     const int tid = threadIdx.x, q = tid & 3, gbase = tid & ~3;
-    const int64_t i0 = (int64_t)blockIdx.x * kLfElems;
+    const int64_t i0 = (int64_t)blockIdx.x * E;
     if (tid == 0) ndef = 0;
-    uint64_t key[kLookupPair];
-    bool probe[kLookupPair], ok[kLookupPair], live[kLookupPair];
-    uint64_t phys[kLookupPair];
-    uint4 ln[kLookupPair], op[kLookupPair];
-    int te[kLookupPair];
+    uint64_t key[P];
+    bool probe[P], ok[P], live[P];
+    uint64_t phys[P];
+    uint4 ln[P], op[P];
+    int te[P];
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         te[k] = k * 16 + (tid >> 2);
         const int64_t i = i0 + te[k];
         live[k] = i < a.n;
@@ -1355,11 +1385,15 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
                 op[k].y = (uint32_t)(t >> 32);
             }
             if (patch_valid(p.b)) op[k] = patch_chunk(op[k], q, p.a, p.b);
+            if (a.pkeys && q == 0) {   // the mirrors k_local_pre worked from, checked below
+                spk[te[k]] = a.pkeys[i];
+                sps[te[k]] = a.state_out[i];
+            }
         }
         sops[te[k] * 4 + q] = op[k];
     }
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         // lane 0 of the group holds op bytes 0..15: the key and the header
         key[k] = (uint64_t)(uint32_t)__shfl((int)op[k].x, 0, 4) | ((uint64_t)(uint32_t)__shfl((int)op[k].y, 0, 4) << 32);
         const uint32_t h0 = (uint32_t)__shfl((int)op[k].z, 0, 4);
@@ -1367,10 +1401,10 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         if (live[k])
             probe[k] = in_count(a, (uint32_t)(i0 + te[k])) && !skip_elem_os(kLocal, (uint8_t)h0, (uint8_t)(h0 >> 8));
     }
-    lookup_pair(a, key, probe, q, gbase, ok, phys, ln);
+    lookup_pair<P>(a, key, probe, q, gbase, ok, phys, ln);
     // F of a key tagged by k_local_pre, loaded for both elements before either is resolved
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         Meta m;
         const uint64_t ek = line_key_meta(ln[k], m);
         const bool hit = ok[k] && ek == key[k];
@@ -1384,12 +1418,17 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         }
     }
     __syncthreads();
-    if (tid < kLfElems && i0 + tid < a.n) {
+    if (tid < E && i0 + tid < a.n) {
         const int64_t i = i0 + tid;
         uint8_t *x = reinterpret_cast<uint8_t *>(&sops[tid * 4]);
         uint8_t *ent = reinterpret_cast<uint8_t *>(&sln[tid * 4]);
         const uint32_t e = sent[tid];
         uint8_t st = kStDone;
+        // the mirrors k_local_pre worked from must describe this element: the PUT-key word, and for
+        // a PUT the state the skip rule was applied to
+        if (a.pkeys && a.error_flags &&
+            (spk[tid] != (x[8] == kOpPut ? ld64(x) : ~0ull) || (x[8] == kOpPut && sps[tid] != x[9])))
+            atomicOr(a.error_flags, 8u);
         if (e != kNone) {
             Ctx c = make_ctx(a);
             const uint8_t bidx = (uint8_t)((uint32_t)i % (uint32_t)a.stride);
@@ -1436,7 +1475,7 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         for (uint32_t j = 0; j < ndef; ++j) a.fbl[base + j] = sdef[j];
     }
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         if (!live[k]) continue;
         uint8_t *xg = a.elems + (i0 + te[k]) * 56 + 16 * q;
         const uint4 w = sops[te[k] * 4 + q];
@@ -1556,6 +1595,7 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
     __shared__ uint8_t sprb[kLfElems];
     const int tid = threadIdx.x, q = tid & 3, gbase = tid & ~3;
     const int64_t i0 = (int64_t)blockIdx.x * kLfElems;
+    const int64_t n_live = a.offsets ? (int64_t)a.offsets[a.n_batches] : a.n;   // packed: past the last offset
     uint64_t key[kLookupPair];
     bool probe[kLookupPair], ok[kLookupPair], live[kLookupPair];
     uint64_t phys[kLookupPair];
@@ -1565,7 +1605,7 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
     for (int k = 0; k < kLookupPair; ++k) {
         te[k] = k * 16 + (tid >> 2);
         const int64_t i = i0 + te[k];
-        live[k] = i < a.n;
+        live[k] = i < a.n && i < n_live;
         op[k] = live[k] ? load_chunk(a.elems + i * a.esz, q, a.esz) : make_uint4(0u, 0u, 0u, 0u);
         sops[te[k] * 4 + q] = op[k];
     }
@@ -1598,7 +1638,7 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
         }
     }
     __syncthreads();
-    if (tid < kLfElems && i0 + tid < a.n) {
+    if (tid < kLfElems && i0 + tid < n_live) {
         const int64_t i = i0 + tid;
         uint8_t *x = reinterpret_cast<uint8_t *>(&sops[tid * 4]);
         uint8_t *ent = reinterpret_cast<uint8_t *>(&sln[tid * 4]);
@@ -1636,6 +1676,132 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
             uint8_t *xg = a.elems + (i0 + te[k]) * a.esz + 16 * q;
             if (16 * q + 16 <= a.esz) *reinterpret_cast<uint4 *>(xg) = w;
             else *reinterpret_cast<uint64_t *>(xg) = (uint64_t)w.x | ((uint64_t)w.y << 32);
+        }
+        if (ok[k] && q > 0) {   // bytes 0..15 of a log line (the MICA key) never change
+            const uint4 l = sln[te[k] * 4 + q];
+            if (!chunk_equal(l, ln[k])) reinterpret_cast<uint4 *>(a.log + phys[k])[q] = l;
+        }
+    }
+}
+
+// HKV_BATCH_ROWS: k_unique_lds over positions instead of elements. Position j holds element j of
+// every row, all of one key (or holes, opcode 0): the four lanes of a position load its element of
+// every row and look the key up once, one lane applies the row elements in row order to the LDS copy
+// of the entry -- exactly the rows' launches one after another, since each row holds the key once --
+// and each element and the entry line are written back where they changed. An ACK's completion finds
+// its read_write_ops once per position (the rows share the batch layout).
+template <int TYPE, int RMAX, int CH>
+__global__ __launch_bounds__(64) void k_unique_rows(BatchArgs a)
+{
+    // CH: 16-B chunks of an element held in LDS (1 for 16-B ACKs, 4 for 56-B INVs)
+    __shared__ uint4 sops[RMAX][kLfElems * CH];
+    __shared__ uint4 sln[kLfElems * 4];
+    __shared__ uint32_t sent[kLfElems];
+    __shared__ uint8_t spart[kLfElems];   // bit r: row r's element takes part (present, in count, not skipped)
+    const int tid = threadIdx.x, q = tid & 3, gbase = tid & ~3;
+    const int64_t i0 = (int64_t)blockIdx.x * kLfElems;
+    const int R = a.n_rows < RMAX ? a.n_rows : RMAX;
+    // packed rows may end before the stride: elements past the last batch offset are in no batch
+    const int64_t n_live = a.offsets ? (int64_t)a.offsets[a.n_batches] : a.n;
+    uint64_t key[kLookupPair];
+    bool probe[kLookupPair], ok[kLookupPair], live[kLookupPair];
+    uint64_t phys[kLookupPair];
+    uint4 ln[kLookupPair], op[RMAX][kLookupPair];
+    uint32_t part[kLookupPair];
+    int te[kLookupPair];
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        te[k] = k * 16 + (tid >> 2);
+        const int64_t i = i0 + te[k];
+        live[k] = i < a.n && i < n_live && (a.offsets || in_count(a, (uint32_t)i));
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) {
+            const bool on = live[k] && r < R && r != a.skip_row;
+            op[r][k] = on && q < CH ? load_chunk(a.elems + (r * a.row_stride + i) * a.esz, q, a.esz)
+                                    : make_uint4(0u, 0u, 0u, 0u);
+            if (q < CH) sops[r][te[k] * CH + q] = op[r][k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        uint64_t kk = 0;
+        uint32_t p = 0;
+        bool mismatch = false;
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) {
+            const uint64_t kr = (uint64_t)(uint32_t)__shfl((int)op[r][k].x, 0, 4) |
+                                ((uint64_t)(uint32_t)__shfl((int)op[r][k].y, 0, 4) << 32);
+            const uint32_t h0 = (uint32_t)__shfl((int)op[r][k].z, 0, 4);
+            if (!live[k] || r >= R || r == a.skip_row || (uint8_t)h0 == 0) continue;   // a hole
+            if (skip_elem_os(TYPE, (uint8_t)h0, (uint8_t)(h0 >> 8))) continue;
+            if (p && kr != kk) mismatch = true;
+            if (!p) kk = kr;
+            p |= 1u << r;
+        }
+        if (mismatch && q == 0 && a.error_flags) atomicOr(a.error_flags, 16u);
+        key[k] = kk;
+        part[k] = mismatch ? 0u : p;
+        probe[k] = part[k] != 0;
+    }
+    lookup_pair(a, key, probe, q, gbase, ok, phys, ln);
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        Meta m;
+        const uint64_t ek = line_key_meta(ln[k], m);
+        const bool hit = ok[k] && ek == key[k];
+        sln[te[k] * 4 + q] = ln[k];
+        if (q == 0) {
+            sent[te[k]] = hit ? (uint32_t)(phys[k] / a.g.entry_unit) : kNone;
+            spart[te[k]] = (uint8_t)part[k];
+        }
+    }
+    __syncthreads();
+    if (tid < kLfElems && i0 + tid < n_live) {
+        const int64_t i = i0 + tid;
+        uint8_t *ent = reinterpret_cast<uint8_t *>(&sln[tid * 4]);
+        const uint32_t e = sent[tid];
+        const uint32_t p = spart[tid];
+        if (e != kNone && p) {
+            if (a.check_unique) {
+                const unsigned long long v = ((unsigned long long)(~a.rtag0) << 32) | (uint32_t)i;
+                const unsigned long long old = atomicExch(a.fw + fw_index(a, phys_of(a, e)), v);
+                if ((uint32_t)(old >> 32) == ~a.rtag0 && a.error_flags) atomicOr(a.error_flags, 16u);
+            }
+            Ctx c = make_ctx(a);
+            int done = -1;
+            if (TYPE == kAcks) c.rw_done = &done;   // the batch is found only for a completion
+            Meta m;
+            meta_load(ent, m);
+            Meta t = m;
+#pragma unroll
+            for (int r = 0; r < RMAX; ++r)
+                if ((p >> r) & 1u) dispatch<31>(TYPE, reinterpret_cast<uint8_t *>(&sops[r][tid * CH]), ent, 0, t, c);
+            if (!meta_equal(t, m)) meta_store(ent, t);
+            if (TYPE == kAcks && done >= 0 && a.rw) {
+                uint8_t *xx;
+                uint8_t idx;
+                elem_at(a, (uint32_t)i, xx, idx, c);
+                complete_rw_slot(c, done);
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < RMAX; ++r)
+                if ((p >> r) & 1u) reinterpret_cast<uint8_t *>(&sops[r][tid * CH])[9] = kMiss;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kLookupPair; ++k) {
+        if (!live[k]) continue;
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) {
+            if (r >= R || r == a.skip_row || q >= CH) continue;
+            const uint4 w = sops[r][te[k] * CH + q];
+            if (!chunk_equal(w, op[r][k])) {
+                uint8_t *xg = a.elems + (r * a.row_stride + i0 + te[k]) * a.esz + 16 * q;
+                if (16 * q + 16 <= a.esz) *reinterpret_cast<uint4 *>(xg) = w;
+                else *reinterpret_cast<uint64_t *>(xg) = (uint64_t)w.x | ((uint64_t)w.y << 32);
+            }
         }
         if (ok[k] && q > 0) {   // bytes 0..15 of a log line (the MICA key) never change
             const uint4 l = sln[te[k] * 4 + q];
@@ -2892,6 +3058,10 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.state_out = (bl.type == kLocal || bl.type == kLocalAfterMemb) ? bl.state_out : nullptr;
     a.opc = bl.type == kLocal ? bl.opcode_in : nullptr;
     a.patch = nullptr;
+    a.pkeys = nullptr;
+    a.n_rows = bl.n_rows;
+    a.skip_row = bl.skip_row;
+    a.row_stride = bl.row_stride;
     a.rws = bl.type == kAcks ? bl.rw_state : nullptr;
     static const int dbg_env = getenv("HKV_DBG") ? atoi(getenv("HKV_DBG")) : 0;
     a.dbg = dbg_env;
@@ -2966,12 +3136,18 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     } else if (bl.patch) {
         a.patch = bl.patch;
     }
+    if (local_direct && !small && bl.put_keys && a.state_out) a.pkeys = bl.put_keys;
     if (small) {
         if (launch_small(a, s)) return -3;
         return 0;                              // node_suspected written by the kernel
     } else if (local_direct) {
         hipLaunchKernelGGL(k_local_pre, dim3((unsigned)((n + kPreElems - 1) / kPreElems)), dim3(256), 0, s, a);
-        hipLaunchKernelGGL(k_local_fused, dim3((unsigned)((n + kLfElems - 1) / kLfElems)), dim3(64), 0, s, a);
+        // HKV_LF_PAIR: elements per lane group in k_local_fused (2: 32 per wave; 4: 64, more loads in flight)
+        static const int lfp_env = getenv("HKV_LF_PAIR") ? atoi(getenv("HKV_LF_PAIR")) : 2;
+        if (lfp_env == 4)
+            hipLaunchKernelGGL(k_local_fused<4>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_local_fused<2>, dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
         hipLaunchKernelGGL(k_local_deferred, dim3(8), dim3(256), 0, s, a);
         // HKV_COMMIT_W=0: the thread-per-element k_commit (experiments)
         static const bool commit_w_env = !getenv("HKV_COMMIT_W") || atoi(getenv("HKV_COMMIT_W")) != 0;
@@ -2979,6 +3155,19 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
             hipLaunchKernelGGL(k_commit_w, dim3((unsigned)((n + 4 * kCwElems - 1) / (4 * kCwElems))), dim3(256), 0, s, a);
         else
             hipLaunchKernelGGL((k_commit<31>), dim3(grid), dim3(256), 0, s, a);
+    } else if (bl.n_rows > 0 && bl.unique) {  // HKV_BATCH_ROWS: one pass over positions of all rows
+        const unsigned lgrid = (unsigned)((n + kLfElems - 1) / kLfElems);
+        // elements of 16 B (ACKs without RMWs) keep one chunk each in LDS, others four
+        if (bl.type == kInvs) {
+            if (bl.n_rows <= 2) hipLaunchKernelGGL((k_unique_rows<kInvs, 2, 4>), dim3(lgrid), dim3(64), 0, s, a);
+            else hipLaunchKernelGGL((k_unique_rows<kInvs, 8, 4>), dim3(lgrid), dim3(64), 0, s, a);
+        } else if (bl.esz <= 16) {
+            if (bl.n_rows <= 2) hipLaunchKernelGGL((k_unique_rows<kAcks, 2, 1>), dim3(lgrid), dim3(64), 0, s, a);
+            else hipLaunchKernelGGL((k_unique_rows<kAcks, 8, 1>), dim3(lgrid), dim3(64), 0, s, a);
+        } else {
+            if (bl.n_rows <= 2) hipLaunchKernelGGL((k_unique_rows<kAcks, 2, 4>), dim3(lgrid), dim3(64), 0, s, a);
+            else hipLaunchKernelGGL((k_unique_rows<kAcks, 8, 4>), dim3(lgrid), dim3(64), 0, s, a);
+        }
     } else if (bl.unique && (bl.type == kInvs || bl.type == kAcks)) {  // one pass: every key has one element
         constexpr int64_t kPerU = 64 * kLookupPair;
         const unsigned ugrid = (unsigned)((n + kPerU - 1) / kPerU);

@@ -19,6 +19,7 @@ struct BatchLaunch {
     const uint8_t *opcode_in;    // local launches: the caller's mirror of each element's opcode (may be NULL)
     const uint8_t *patch;        // local launches: pending header writes, 16 B per element (may be NULL)
     uint8_t *rw_state;           // ACK launches: state-byte mirror of read_write_ops (may be NULL)
+    const uint64_t *put_keys;    // local launches: PUT-key mirror (state_out holds the entry states), or NULL
     const uint8_t *index;
     uint8_t *log;
     uint8_t *rw;
@@ -45,6 +46,8 @@ struct BatchLaunch {
     uint8_t w_ack_init;
     int32_t path;                             // kPath*: which engine runs the launch
     int32_t unique;                           // HKV_BATCH_UNIQUE: no key twice in the launch
+    int32_t n_rows, skip_row;                 // HKV_BATCH_ROWS (n_rows 0: a plain launch)
+    int64_t row_stride;
     // small launches staged in host memory (the combining submit of hermes_batch_ops_to_KVS): the
     // kernel first copies region_bytes from host_src to dev_region (where elems, counts, rw and
     // node_suspected point), at the end copies them back to host_dst, then stores done_value into

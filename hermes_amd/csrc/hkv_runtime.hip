@@ -503,7 +503,11 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.opcode_in = d->type == kLocal && !opc_off ? d->d_opcode_in : nullptr;
     bl.patch = d->type == kLocal ? d->d_patch : nullptr;
     bl.rw_state = d->type == kAcks ? d->d_rw_state : nullptr;
+    // HKV_PUT_KEYS=0: the PUT-key mirror ignored (experiments)
+    static const bool pk_off = getenv("HKV_PUT_KEYS") && atoi(getenv("HKV_PUT_KEYS")) == 0;
+    bl.put_keys = d->type == kLocal && d->d_state_out && !pk_off ? d->d_put_keys : nullptr;
     if (bl.patch && ((uintptr_t)bl.patch & 15)) return fail(-1, "d_patch must be 16-byte aligned");
+    if (bl.put_keys && ((uintptr_t)bl.put_keys & 7)) return fail(-1, "d_put_keys must be 8-byte aligned");
     bl.offsets = packed ? d->d_counts : nullptr;
     bl.index = t->d_index;
     bl.log = t->d_log;
@@ -533,6 +537,18 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.path = (d->flags & HKV_BATCH_ENGINE) || packed ? kPathEngine
             : (d->flags & HKV_BATCH_SMALL) ? kPathSmall : kPathAuto;
     bl.unique = (d->flags & HKV_BATCH_UNIQUE) && (d->type == kInvs || d->type == kAcks) ? 1 : 0;
+    if (d->flags & HKV_BATCH_ROWS) {
+        if (!bl.unique || t->geo.entry_size != 64 || t->geo.st_value != 31 || d->elem_size > 64)
+            return fail(-1, "HKV_BATCH_ROWS: unique INV or ACK launches of 64-byte entries and elements only");
+        if (d->n_rows < 1 || d->n_rows > HKV_MAX_ROWS || d->skip_row >= d->n_rows || d->d_node_suspected)
+            return fail(-1, "HKV_BATCH_ROWS: 1..%d rows, a skip row among them (or -1), no node_suspected",
+                        HKV_MAX_ROWS);
+        if (d->n_rows > 1 && d->row_stride < n) return fail(-1, "HKV_BATCH_ROWS: rows overlap");
+        bl.n_rows = d->n_rows;
+        bl.skip_row = d->skip_row < 0 ? -1 : d->skip_row;
+        bl.row_stride = d->row_stride;
+        bl.path = kPathEngine;
+    }
     TRACE("batch_async type=%d n=%lld", d->type, (long long)n);
     rc = launch_batch(bl, s);
     if (rc) return fail(rc, "batch launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));

@@ -5,6 +5,7 @@
 // is kept with a wave-ballot prefix count instead of a serial loop.
 #include <hip/hip_runtime.h>
 
+#include "../../include/hermeskv.h"
 #include "../../include/hermeskv_workload.h"
 #include "hkv_codes.h"
 #include "hkv_internal.h"
@@ -480,11 +481,12 @@ __device__ __forceinline__ void wave_ranks(const unsigned long long *b, int lane
 // slot gets a patch (hkv_batch_desc.d_patch) that the next local launch applies as it reads the op,
 // so the op slab is read and written once per round (by that launch) instead of twice.
 // One wave per worker.
-__global__ __launch_bounds__(256) void k_refill_plan_w(const uint8_t *states, int32_t n_workers, int32_t stride,
+__global__ __launch_bounds__(256) void k_refill_plan_w(uint8_t *states, int32_t n_workers, int32_t stride,
                                                        uint32_t st_value, uint32_t shift, const uint64_t *tkey,
                                                        const uint8_t *top, int32_t tlen, uint32_t *cursor,
                                                        uint32_t machine_id, uint32_t flags,
-                                                       unsigned long long *counters, uint8_t *opc, uint8_t *patch)
+                                                       unsigned long long *counters, uint8_t *opc, uint8_t *patch,
+                                                       uint64_t *put_keys)
 {
     const int lane = threadIdx.x & 63;
     const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
@@ -535,6 +537,10 @@ __global__ __launch_bounds__(256) void k_refill_plan_w(const uint8_t *states, in
                   ((uint64_t)(get ? 0u : (uint8_t)('a' + machine_id)) << 32) |
                   ((uint64_t)(get && (flags & HKV_WL_READ_TS_RESET) ? 1u : 0u) << 40) | (1ull << 48);
             opc[e] = oc;
+            if (put_keys) {   // the PUT-key mirror and the entry state of the patched op
+                put_keys[e] = oc == kOpPut ? p.a : HKV_NO_PUT;
+                states[e] = kNew;
+            }
         }
         *reinterpret_cast<W16 *>(patch + e * 16) = p;
     }
@@ -849,6 +855,114 @@ __global__ __launch_bounds__(1024) void k_scan_counts(const int32_t *counts, int
         run += counts[k];
     }
     if (t == 1023) off[n] = part[1023];
+}
+
+// ---- a rank's INVs straight into its packed slab, at most `cap` of them (replica groups without a
+// host read per round): k_count_invs counts each worker's sendable ops (at most C, the INV credits),
+// k_scan_cap turns the counts into slab offsets and how many each worker sends within cap, and
+// k_marshal_invs_packed copies them to their offsets. INVs past the cap keep their PUT_SUCCESS (or
+// RMW/REPLAY_SUCCESS, MEMBERSHIP_CHANGE) state and go out in a later round, as the credit-held ones do.
+__device__ __forceinline__ bool inv_sendable(uint8_t st)
+{
+    return st == kPutSuccess || st == kRmwSuccess || st == kReplaySuccess || st == kOpMembChange;
+}
+
+__global__ __launch_bounds__(256) void k_count_invs(const uint8_t *states, int32_t n_workers, int32_t stride,
+                                                    int32_t *count)
+{
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (w >= n_workers) return;
+    int c = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = r * 64 + lane;
+        c += __popcll(__ballot(i < stride && inv_sendable(states[(int64_t)w * stride + i])));
+    }
+    if (lane == 0) count[w] = c;
+}
+
+// counts[W] (sendable) -> off[0..W] (off[W] = the slab's total) and sent[W]: worker w sends
+// min(count, C, what is left of cap after the workers before it); the rest is added to *held
+__global__ __launch_bounds__(1024) void k_scan_cap(const int32_t *counts, int32_t n, int32_t C, int32_t cap,
+                                                   int32_t *off, int32_t *sent, unsigned long long *held)
+{
+    __shared__ int32_t part[1024];
+    __shared__ int32_t held_s[1024];
+    const int t = threadIdx.x;
+    const int per = (n + 1023) / 1024;
+    const int lo = t * per, hi = min(n, lo + per);
+    int32_t sum = 0;
+    for (int k = lo; k < hi; ++k) sum += min(counts[k], C);
+    part[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int32_t v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int32_t run = part[t] - sum;   // uncapped offset of worker lo
+    int32_t h = 0;
+    for (int k = lo; k < hi; ++k) {
+        const int32_t c = counts[k], want = min(c, C);
+        const int32_t start = min(run, cap);
+        const int32_t s = max(0, min(want, cap - run));
+        off[k] = start;
+        sent[k] = s;
+        h += c - s;
+        run += want;
+    }
+    held_s[t] = h;
+    __syncthreads();
+    if (t == 0) {
+        int64_t tot = 0;
+        for (int k = 0; k < 1024; ++k) tot += held_s[k];
+        if (tot && held) atomicAdd(held, (unsigned long long)tot);
+        off[n] = min(part[1023], cap);
+    }
+}
+
+// k_marshal_invs_w writing worker w's first sent[w] INVs at out[off[w] ..]
+__global__ __launch_bounds__(256) void k_marshal_invs_packed(uint8_t *ops, int32_t n_workers, int32_t stride,
+                                                             uint32_t op_size, uint8_t *out, const int32_t *off,
+                                                             const int32_t *sent, uint32_t machine_id,
+                                                             uint8_t *states)
+{
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (w >= n_workers) return;
+    const int64_t e0 = (int64_t)w * stride;
+    uint8_t st[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = r * 64 + lane;
+        st[r] = i < stride ? states[e0 + i] : 0;
+    }
+    unsigned long long bs[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bs[r] = __ballot(r * 64 + lane < stride && inv_sendable(st[r]));
+    int rank[4], total;
+    wave_ranks(bs, lane, rank, total);
+    const int cap = sent[w];
+    const int64_t base = off[w];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        if (!((bs[r] >> lane) & 1ull) || rank[r] >= cap) continue;
+        const int64_t e = e0 + r * 64 + lane;
+        uint8_t *op = ops + e * op_size;
+        uint8_t *dst = out + (base + rank[r]) * op_size;
+        const W16 h = *reinterpret_cast<const W16 *>(op);
+        *reinterpret_cast<W16 *>(dst) = W16{h.a, with_op_state(h.b, kOpInv, (uint8_t)machine_id)};
+        uint32_t k = 16;
+        for (; k + 16 <= op_size; k += 16) *reinterpret_cast<W16 *>(dst + k) = *reinterpret_cast<const W16 *>(op + k);
+        if (k < op_size) *reinterpret_cast<uint64_t *>(dst + k) = *reinterpret_cast<const uint64_t *>(op + k);
+        const uint8_t s = st[r];
+        const uint8_t ns = s == kPutSuccess ? kInProgressPut : s == kRmwSuccess ? kInProgressRmw
+                         : s == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
+        op[9] = ns;
+        states[e] = ns;
+    }
 }
 
 // rows [W][C] x esz with counts[W] -> packed[off[w] ..], one workgroup per row
@@ -1379,13 +1493,14 @@ __global__ __launch_bounds__(256) void k_peer_locate(TableView t, const uint8_t 
 
 // k_peer_ts for located INVs (one thread each): the key is checked at the entry, and an INV
 // whose entry does not hold its key any more takes the full lookup
+// inv_at (may be NULL): INV g sits at element inv_at[g] of invs (a rows layout, hkv_wl_peer_ts_rows)
 __global__ __launch_bounds__(256) void k_peer_ts_at(TableView t, uint8_t *invs, uint8_t *vals, const uint64_t *phys_in,
                                                     int64_t total, uint32_t op_size, unsigned long long *peer_ts,
-                                                    uint32_t round)
+                                                    uint32_t round, const int64_t *inv_at)
 {
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (g >= total) return;
-    uint8_t *x = invs + g * op_size;
+    uint8_t *x = invs + (inv_at ? inv_at[g] : g) * op_size;
     const uint64_t key = *reinterpret_cast<const uint64_t *>(x);
     const uint64_t h8 = *reinterpret_cast<const uint64_t *>(x + 8);
     const uint8_t peer = (uint8_t)(h8 >> 8);
@@ -1487,16 +1602,17 @@ int hkv_wl_refill_st(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t o
     return ok();
 }
 
-int hkv_wl_refill_plan(const uint8_t *states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
+int hkv_wl_refill_plan(uint8_t *states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
                        const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor, uint32_t machine_id,
-                       uint32_t flags, unsigned long long *counters, uint8_t *opc, uint8_t *patch, void *stream)
+                       uint32_t flags, unsigned long long *counters, uint8_t *opc, uint8_t *patch,
+                       uint64_t *put_keys, void *stream)
 {
     if (stride > 256 || n_workers <= 0 || tlen <= 0 || !states || !opc || !patch) return -1;
     if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET)) return -1;   // no hot-request coalescing
-    if (((uintptr_t)patch & 15) || st_value > 255) return -1;
+    if (((uintptr_t)patch & 15) || ((uintptr_t)put_keys & 7) || st_value > 255) return -1;
     hipLaunchKernelGGL(k_refill_plan_w, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                        states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
-                       counters, opc, patch);
+                       counters, opc, patch, put_keys);
     return ok();
 }
 
@@ -1737,6 +1853,20 @@ int hkv_wl_ack_offsets(const int32_t *inv_count, int32_t n_workers, int32_t n_pe
     return ok();
 }
 
+int hkv_wl_marshal_invs_packed(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint8_t *states,
+                               int32_t C, int32_t cap, uint8_t *out, int32_t *offsets, int32_t *count, int32_t *sent,
+                               uint32_t machine_id, unsigned long long *held, void *stream)
+{
+    if (stride > 256 || n_workers <= 0 || C <= 0 || cap < 0 || op_size % 8 || !states) return -1;
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned g = (unsigned)((n_workers + 3) / 4);
+    hipLaunchKernelGGL(k_count_invs, dim3(g), dim3(256), 0, s, states, n_workers, stride, count);
+    hipLaunchKernelGGL(k_scan_cap, dim3(1), dim3(1024), 0, s, count, n_workers, C, cap, offsets, sent, held);
+    hipLaunchKernelGGL(k_marshal_invs_packed, dim3(g), dim3(256), 0, s, ops, n_workers, stride, op_size, out, offsets,
+                       sent, machine_id, states);
+    return ok();
+}
+
 int hkv_wl_pack_rows(const uint8_t *rows, const int32_t *counts, int32_t n_rows, int32_t C, uint32_t elem_size,
                      uint8_t *packed, int32_t *offsets, void *stream)
 {
@@ -1819,7 +1949,18 @@ int hkv_wl_peer_ts_at(hkv_table *t, uint8_t *invs, uint8_t *vals, const uint64_t
     if (table_view(t, &tv) || n < 0 || op_size % 8) return -1;
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_peer_ts_at, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, tv, invs, vals, phys, n,
-                       op_size, peer_ts, round);
+                       op_size, peer_ts, round, (const int64_t *)nullptr);
+    return ok();
+}
+
+int hkv_wl_peer_ts_rows(hkv_table *t, uint8_t *rows, const int64_t *inv_at, uint8_t *vals, const uint64_t *phys,
+                        int64_t n, uint32_t op_size, unsigned long long *peer_ts, uint32_t round, void *stream)
+{
+    TableView tv;
+    if (table_view(t, &tv) || n < 0 || op_size % 8 || !inv_at) return -1;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_peer_ts_at, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, tv, rows, vals, phys, n,
+                       op_size, peer_ts, round, inv_at);
     return ok();
 }
 

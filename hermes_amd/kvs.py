@@ -86,6 +86,7 @@ BATCH_ENGINE = 1   # hkv_batch_desc.flags (include/hermeskv.h): the multi-kernel
 BATCH_SMALL = 2    # the single-workgroup kernel (launches of at most 4096 elements)
 BATCH_PACKED = 4   # INV / VAL batches back to back, d_counts = n_batches + 1 offsets
 BATCH_UNIQUE = 8   # no key twice in the launch (INV batches: one pass)
+BATCH_ROWS = 16    # with BATCH_UNIQUE: rows of one layout, element j of every row on one key
 
 
 class HermesKV:
@@ -170,23 +171,35 @@ class HermesKV:
               stream: torch.cuda.Stream | None = None, offsets: torch.Tensor | None = None,
               state_out: torch.Tensor | None = None, opcode_in: torch.Tensor | None = None,
               patch: torch.Tensor | None = None, rw_state: torch.Tensor | None = None,
-              unique: bool = False) -> None:
+              unique: bool = False, put_keys: torch.Tensor | None = None,
+              rows: tuple[int, int, int] | None = None) -> None:
         """Apply n_batches batches of one type, concatenated in `elems` (uint8, on the GPU),
         in concatenation order, asynchronously on `stream` (default: torch's current).
         offsets (INV / ACK / VAL batches): the batches stored back to back, batch b at elements
         [offsets[b], offsets[b+1]); `stride` is then the total (HKV_BATCH_PACKED). patch (local
         batches): 16 B per element of pending header writes (hkv_batch_desc.d_patch); rw_state (ACK
         batches): the read_write_ops' state-byte mirror, kept up to date by the completions. unique
-        (INV batches): no key appears twice in the launch (HKV_BATCH_UNIQUE, one pass)."""
+        (INV batches): no key appears twice in the launch (HKV_BATCH_UNIQUE, one pass). put_keys (local
+        batches with state_out): the PUT-key mirror (hkv_batch_desc.d_put_keys); state_out must then hold
+        every element's state byte on entry too. rows (unique INV / ACK launches): (n_rows, row_stride,
+        skip_row) -- n_rows launches of this layout, row r at element r * row_stride of elems, applied in
+        row order in one pass (HKV_BATCH_ROWS; skip_row -1: none)."""
         assert elems.is_cuda and elems.dtype == torch.uint8
         total = stride if offsets is not None else n_batches * stride
-        assert elems.numel() >= total * elem_size
+        if rows is not None:
+            assert unique and rows[0] >= 1 and (rows[0] == 1 or rows[1] >= total)
+            assert elems.numel() >= ((rows[0] - 1) * rows[1] + total) * elem_size
+        else:
+            assert elems.numel() >= total * elem_size
         d = HkvBatchDesc()
         d.type = int(btype)
         d.n_batches = int(n_batches)
         d.stride = int(stride)
         d.elem_size = int(elem_size)
         d.flags = self.default_flags | (BATCH_UNIQUE if unique else 0)
+        if rows is not None:
+            d.flags |= BATCH_ROWS
+            d.n_rows, d.row_stride, d.skip_row = int(rows[0]), int(rows[1]), int(rows[2])
         d.d_elems = elems.data_ptr()
         if state_out is not None:   # local batches: the mirror of each element's final state byte
             assert state_out.is_cuda and state_out.dtype == torch.uint8 and state_out.numel() >= n_batches * stride
@@ -200,6 +213,10 @@ class HermesKV:
         if rw_state is not None:
             assert rw_state.is_cuda and rw_state.dtype == torch.uint8
             d.d_rw_state = rw_state.data_ptr()
+        if put_keys is not None:
+            assert state_out is not None and put_keys.is_cuda and put_keys.dtype == torch.int64
+            assert put_keys.numel() >= n_batches * stride
+            d.d_put_keys = put_keys.data_ptr()
         if offsets is not None:
             assert counts is None and offsets.is_cuda and offsets.dtype == torch.int32
             assert offsets.numel() >= n_batches + 1

@@ -36,7 +36,7 @@ from . import layout as L
 from .kvs import HermesKV
 from .lib import check, raw
 from .hades import NO_VIEW, Hades, MajorityLost, exchange_views
-from .workload import HkvZipf, _ptr, _s, refill_flags, slots_per_worker  # noqa: F401 (re-exported)
+from .workload import HkvZipf, _ptr, _s, init_mirrors, refill_flags, slots_per_worker  # noqa: F401 (re-exported)
 
 _L = raw()
 _P = ctypes.c_void_p
@@ -54,6 +54,8 @@ _L.hkv_wl_marshal_memb_vals.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctyp
                                         ctypes.c_uint32, _P, _P]
 _L.hkv_wl_regroup_aligned.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, ctypes.c_uint32,
                                       _P, ctypes.c_int32, _P, _P]
+_L.hkv_wl_marshal_invs_packed.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32,
+                                          ctypes.c_int32, _P, _P, _P, _P, ctypes.c_uint32, _P, _P]
 _L.hkv_wl_collect_vals_rows.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, _P,
                                         ctypes.c_int32, _P, ctypes.c_uint32, _P, _P, _P]
 
@@ -90,10 +92,16 @@ class ReplicaRound:
         # refills planned from the state mirror and applied by the next local launch (workload.Round)
         self.fused = fused_refill and self.op <= 64
         self.patch = torch.zeros(W * LOCAL * 16, **u8) if self.fused else None
+        self.put_keys = (torch.zeros(W * LOCAL, dtype=torch.int64, device=dev)
+                         if self.fused and os.environ.get("HKV_PUT_KEYS", "1") != "0" else None)   # d_put_keys
         # outgoing INVs: [W][C] rows, then packed (worker w at inv_off[w]; inv_off[W] = total)
         self.inv_slab = torch.zeros(W * C * self.op, **u8)
-        self.inv_count = torch.zeros(W, **i32)
+        self.inv_count = torch.zeros(W, **i32)           # INVs each worker sends this round
+        self.inv_sendable = torch.zeros(W, **i32)        # ... and could send (the rest are held)
         self.inv_off = torch.zeros(W + 1, **i32)
+        # the INVs go straight into the packed slab, at most `cap` per rank and round (local(cap)), so the
+        # group can size its collectives without a host read (HKV_GROUP_PACKED_MARSHAL=0: rows, then packed)
+        self.packed_marshal = os.environ.get("HKV_GROUP_PACKED_MARSHAL", "1") != "0"
         self.inv_pack = torch.zeros(W * C * self.op, **u8)
         self.inv_totals = torch.zeros(N, **i32)          # all ranks' INV totals (this round's width: max)
         self.inv_maxc = torch.zeros(1, **i32)            # this rank's largest per-worker INV count
@@ -126,7 +134,10 @@ class ReplicaRound:
         # replica's INVs once, and a key has one local write in flight), with no regroup pass; once any
         # replica has failed, its rows hold empty slots and the regrouped batch takes over for good
         self.unique_acks = os.environ.get("HKV_GROUP_UNIQUE_ACKS", "1") != "0"
-        self.own_total = 0             # this round's packed INV total (round_shape)
+        # ... all peers' rows in one launch (HKV_BATCH_ROWS, this rank's own row skipped; HKV_ACK_ROWS=0: one
+        # launch per peer)
+        self.ack_rows = os.environ.get("HKV_ACK_ROWS", "1") != "0" and self.sizes.entry == 64 and self.ack_size <= 64
+        self.own_total = None          # this round's packed INV total, when read back (round_shape)
         self.refill(first=True)
 
     # -- Hades: one view-update period per round when enabled
@@ -160,27 +171,37 @@ class ReplicaRound:
             check(_L.hkv_wl_refill_plan(_ptr(self.states), self.W, LOCAL, self.sizes.st_value, self.sizes.shift,
                                         _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
                                         self.rank, self.rflags, _ptr(self.counters), _ptr(self.opcodes),
-                                        _ptr(self.patch), _s()), "refill_plan")
+                                        _ptr(self.patch), _ptr(self.put_keys), _s()), "refill_plan")
             return
         check(_L.hkv_wl_refill(_ptr(self.ops), self.W, LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
                                _ptr(self.trace_key), _ptr(self.trace_op), None, self.trace_len, _ptr(self.cursor),
                                self.rank, int(first), self.rflags, _ptr(self.counters), _ptr(self.opcodes), None,
                                _s()), "refill")
+        if first:
+            init_mirrors(self.ops, self.op, self.states, self.put_keys)
 
-    def local(self):
-        """Local batch, then this round's INVs, packed (inv_pack; worker w at inv_off[w])."""
+    def local(self, cap: int | None = None):
+        """Local batch, then this round's INVs, packed (inv_pack; worker w at inv_off[w]); at most `cap` of
+        them (the rest keep their state and go out in a later round, counted in held[0])."""
         if self.failed:
             self.inv_count.zero_()
             self.inv_off.zero_()
             self.inv_maxc.zero_()
             return
         self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, LOCAL, self.op, self.mb, state_out=self.states,
-                       opcode_in=self.opcodes, patch=self.patch)
-        check(_L.hkv_wl_marshal_invs_cap(_ptr(self.ops), self.W, LOCAL, self.op, _ptr(self.inv_slab), self.C,
-                                         _ptr(self.inv_count), self.rank, _ptr(self.held), _ptr(self.states), _s()),
-              "marshal_invs")
-        check(_L.hkv_wl_pack_rows(_ptr(self.inv_slab), _ptr(self.inv_count), self.W, self.C, self.op,
-                                  _ptr(self.inv_pack), _ptr(self.inv_off), _s()), "pack invs")
+                       opcode_in=self.opcodes, patch=self.patch, put_keys=self.put_keys)
+        if self.packed_marshal:
+            check(_L.hkv_wl_marshal_invs_packed(_ptr(self.ops), self.W, LOCAL, self.op, _ptr(self.states), self.C,
+                                                self.W * self.C if cap is None else int(cap), _ptr(self.inv_pack),
+                                                _ptr(self.inv_off), _ptr(self.inv_sendable), _ptr(self.inv_count),
+                                                self.rank, _ptr(self.held), _s()), "marshal_invs_packed")
+        else:
+            assert cap is None, "a capped round needs the packed marshal"
+            check(_L.hkv_wl_marshal_invs_cap(_ptr(self.ops), self.W, LOCAL, self.op, _ptr(self.inv_slab), self.C,
+                                             _ptr(self.inv_count), self.rank, _ptr(self.held), _ptr(self.states), _s()),
+                  "marshal_invs")
+            check(_L.hkv_wl_pack_rows(_ptr(self.inv_slab), _ptr(self.inv_count), self.W, self.C, self.op,
+                                      _ptr(self.inv_pack), _ptr(self.inv_off), _s()), "pack invs")
         torch.amax(self.inv_count, dim=0, keepdim=True, out=self.inv_maxc)
         if self.count_elems:
             self.inv_total += self.inv_off[self.W]
@@ -216,7 +237,7 @@ class ReplicaRound:
     def invs(self, width: int):
         """Apply the gathered INVs of the peers ([N][width], row p: inv_totals[p] INVs) as N
         batches; their ACKs go into ack_slab in the positions of the INVs they answer."""
-        self.inv_totals[self.rank] = 0
+        self.inv_totals[self.rank:self.rank + 1].zero_()   # (an indexed store from the host would synchronise)
         if self.failed:   # no ACKs from a failed replica
             self.ack_slab[:self.N * width * self.ack_size].view(-1, self.ack_size)[:, 8] = int(L.Bucket.EMPTY)
             return
@@ -240,16 +261,21 @@ class ReplicaRound:
             self.val_off[W:].zero_()
             return
         if self.unique_acks:
-            # row p of ack_recv: peer p's ACKs lined up with inv_pack, worker w's at [inv_off[w], inv_off[w+1])
-            T = self.own_total
-            if T:
+            # row p of ack_recv: peer p's ACKs lined up with inv_pack, worker w's at [inv_off[w], inv_off[w+1]);
+            # without the total read back, the launch spans the width and ends at inv_off[W]
+            T = self.own_total if self.own_total is not None else width
+            if T and self.ack_rows:
+                self.kvs.batch(L.BatchType.acks, self.ack_recv, W, T, self.ack_size, self.mb, rw=self.ops,
+                               rw_stride_bytes=LOCAL * self.op, offsets=self.inv_off, rw_state=self.states,
+                               unique=True, rows=(N, width, self.rank))
+            elif T:
                 for p in range(N):
                     if p != self.rank:
                         self.kvs.batch(L.BatchType.acks, self.ack_recv[p * width * self.ack_size:], W, T, self.ack_size,
                                        self.mb, rw=self.ops, rw_stride_bytes=LOCAL * self.op, offsets=self.inv_off,
                                        rw_state=self.states, unique=True)
             if self.count_elems:
-                self.elem_totals[1] += (N - 1) * T
+                self.elem_totals[1] += (N - 1) * self.inv_off[W]
             check(_L.hkv_wl_collect_vals_rows(_ptr(self.ack_recv), W, N, width, self.ack_size, _ptr(self.val_slab), C,
                                               _ptr(self.val_count), self.rank, _ptr(self.held[1:]), _ptr(self.inv_off),
                                               _s()), "collect_vals_rows")
@@ -273,7 +299,7 @@ class ReplicaRound:
         """Apply the gathered VALs of the peers ([N][width], row p: val_totals[p] VALs)."""
         if self.failed:
             return
-        self.val_totals[self.rank] = 0
+        self.val_totals[self.rank:self.rank + 1].zero_()
         if self.count_elems:
             self.elem_totals[2] += self.val_totals.sum()
         self.kvs.batch(L.BatchType.vals, self.val_recv, self.N, width, L.OP_META_SIZE, self.mb,
@@ -320,6 +346,30 @@ class ReplicaRound:
         return {"committed": c[0], "misses": c[1], "writes_completed": c[2], "invs_held": h[0], "vals_dropped": h[1]}
 
 
+class WidthPlan:
+    """The slab width of a replica group's rounds without a host read per round. Every
+    `calib_every`-th round (and the first) reads the round's largest INV total back, as before; the
+    rounds in between use width = slack x that total + pad and cap each rank's INVs at it (the rest
+    are held in PUT_SUCCESS, like credit-held INVs, and go out later). Every rank reads the same
+    all-gathered totals, so every rank picks the same width. A round with a failure, Hades or the
+    regrouped ACK path always reads back."""
+
+    def __init__(self):
+        self.calib_every = int(os.environ.get("HKV_GROUP_CALIB", "16"))
+        self.slack = float(os.environ.get("HKV_GROUP_WIDTH_SLACK", "1.25"))
+        self.pad = 256
+        self.width = None
+        self.k = 0
+
+    def steady(self, special: bool) -> bool:
+        """whether this round runs at the planned width (call once per round)"""
+        k, self.k = self.k, self.k + 1
+        return (self.calib_every > 0 and self.width is not None and not special and k % self.calib_every != 0)
+
+    def calibrate(self, width: int, cap: int) -> None:
+        self.width = min(cap, int(width * self.slack) + self.pad)
+
+
 def _timed(events, name, fn, only=None):
     if events is None or (only is not None and name not in only):
         fn()
@@ -338,13 +388,17 @@ class ReplicaGroupRound:
     LOCAL = LOCAL
 
     def __init__(self, kvs: HermesKV | None, n_workers: int, zipf: HkvZipf | None, write_permille: int = 200, *,
-                 seed: int = 0x5EED, world: int, rank: int, group=None, replica=None, hades: bool = False, **kw):
+                 seed: int = 0x5EED, world: int, rank: int, group=None, replica=None, hades: bool = False,
+                 comm=None, **kw):
         """`replica`: drive an existing ReplicaRound-shaped object instead of building one.
         `hades`: the membership comes from Hades agreement over heartbeats exchanged every round
-        (a failed rank is expelled when the survivors agree), instead of a host-driven drop."""
+        (a failed rank is expelled when the survivors agree), instead of a host-driven drop.
+        `comm`: an object with gather(out, inp), gather_async(out, inp) -> work (.wait()) and
+        a2a(out, inp) to use instead of torch.distributed (tests: ranks as threads of one process)."""
         import torch.distributed as dist
         self.dist = dist
         self.group = group
+        self.comm = comm
         self.r = replica if replica is not None else ReplicaRound(kvs, n_workers, world, rank, zipf,
                                                                   write_permille, seed=seed, **kw)
         self.hades = hades
@@ -356,6 +410,7 @@ class ReplicaGroupRound:
         self.rstride = self.r.C * self.R
         self.counters = self.r.counters
         self.fold_counters = self.r.fold_counters
+        self.plan = WidthPlan() if getattr(self.r, "packed_marshal", False) else None
         self.inv_total = self.r.inv_total
         self.elem_totals = self.r.elem_totals
 
@@ -368,14 +423,20 @@ class ReplicaGroupRound:
         self.r.count_elems = v
 
     def _gather(self, out, inp):
+        if self.comm is not None:
+            return self.comm.gather(out, inp)
         self.dist.all_gather_into_tensor(out, inp, group=self.group)
 
     def _gather_async(self, out, inp):
         """the same all-gather, returned unwaited: the collective runs on the backend's stream (RCCL's
         own) while torch's stream goes on; work.wait() orders the consumer after it"""
+        if self.comm is not None:
+            return self.comm.gather_async(out, inp)
         return self.dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True)
 
     def _a2a(self, out, inp):
+        if self.comm is not None:
+            return self.comm.a2a(out, inp)
         self.dist.all_to_all_single(out, inp, group=self.group)
 
     def _views(self, changed: bool) -> bytes:
@@ -426,9 +487,18 @@ class ReplicaGroupRound:
         exchange for the writes it completes -- or, with Hades, the failed rank stops
         heartbeating and the survivors expel it when they agree (two periods later)."""
         r = self.r
-        _timed(events, "local", r.local, timed_batches)
-        self._gather(*r.inv_total_io())
-        width, stride = r.round_shape()  # the round's one host synchronisation
+        steady = self.plan is not None and self.plan.steady(drop is not None or self.hades or not r.unique_acks)
+        if steady:   # no host read: the planned width, each rank's INVs capped at it
+            width, stride = self.plan.width, None
+            r.own_total = None
+            _timed(events, "local", lambda: r.local(cap=width), timed_batches)
+            self._gather(*r.inv_total_io())
+        else:
+            _timed(events, "local", r.local, timed_batches)
+            self._gather(*r.inv_total_io())
+            width, stride = r.round_shape()  # host synchronisation: this round's exact width
+            if self.plan is not None:
+                self.plan.calibrate(width, r.W * r.C)
         self._gather(*r.inv_io(width))
         if drop is not None:
             r.peer_failing()
@@ -473,6 +543,7 @@ class LoopbackGroup:
         self.rounds = rounds
         self.N = len(rounds)
         self.hades = hades
+        self.plan = WidthPlan() if all(getattr(r, "packed_marshal", False) for r in rounds) else None
         self.hades_changes = []        # (round, rank, membership) of every agreed change
         self.clock = 0
         if hades:
@@ -531,12 +602,24 @@ class LoopbackGroup:
         the group's state between phases (tests)."""
         rs = self.rounds
         seen = observer or (lambda phase: None)
+        steady = self.plan is not None and self.plan.steady(drop is not None or self.hades or
+                                                            not all(r.unique_acks for r in rs))
         for r in rs:
-            r.local()
+            if steady:
+                r.own_total = None
+                r.local(cap=self.plan.width)
+            else:
+                r.local()
         seen("local")
         self._gather_io([r.inv_total_io() for r in rs])
-        shapes = [r.round_shape() for r in rs]
-        width = shapes[0][0]                 # the same on every replica (max of the same totals)
+        if steady:
+            width = self.plan.width
+            shapes = [(width, None)] * len(rs)
+        else:
+            shapes = [r.round_shape() for r in rs]
+            width = shapes[0][0]                 # the same on every replica (max of the same totals)
+            if self.plan is not None:
+                self.plan.calibrate(width, rs[0].W * rs[0].C)
         self._gather_io([r.inv_io(width) for r in rs])
         if drop is not None:
             for r in rs:

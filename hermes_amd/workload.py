@@ -38,7 +38,7 @@ _L.hkv_wl_fold_counters.argtypes = [_P, _P]
 _L.hkv_wl_refill_st.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                 _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _P]
 _L.hkv_wl_refill_plan.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, _P, _P,
-                                  ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _P]
+                                  ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _P, _P]
 _L.hkv_wl_marshal_invs.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_invs_cap.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
                                        ctypes.c_uint32, _P, _P, _P]
@@ -72,6 +72,7 @@ _L.hkv_wl_ack_offsets.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ct
 _L.hkv_wl_pack_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_peer_locate.argtypes = [_P, _P, ctypes.c_int64, ctypes.c_uint32, _P, _P]
 _L.hkv_wl_peer_ts_at.argtypes = [_P, _P, _P, _P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
+_L.hkv_wl_peer_ts_rows.argtypes = [_P, _P, _P, _P, _P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_peer_ts_words.restype = ctypes.c_uint64
 _L.hkv_wl_peer_ts_words.argtypes = [_P]
 
@@ -122,6 +123,16 @@ def zipf_params(n: int, theta: float) -> HkvZipf:
 
 def _ptr(t: torch.Tensor | None):
     return _P(t.data_ptr()) if t is not None else None
+
+
+def init_mirrors(ops: torch.Tensor, op_size: int, states: torch.Tensor, put_keys: torch.Tensor | None):
+    """The state mirror and the PUT-key mirror (hkv_batch_desc.d_put_keys) of freshly written ops;
+    from then on the round's kernels keep them (local launch, marshals, ACK launches, refill plan)."""
+    v = ops.view(-1, op_size)
+    states.copy_(v[:, 9])
+    if put_keys is not None:
+        key = v[:, :8].contiguous().view(torch.int64).view(-1)
+        put_keys.copy_(torch.where(v[:, 8] == int(L.Op.PUT), key, torch.full_like(key, -1)))
 
 
 class CommitAudit:
@@ -262,6 +273,10 @@ class Round:
         self.states = torch.zeros(W * S, **u8)   # the local batch's mirror of every op's state byte
         self.opcodes = torch.zeros(W * S, **u8)  # the refill's mirror of every op's opcode byte
         self.patch = torch.zeros(W * S * 16, **u8) if self.fused else None   # planned refills (d_patch)
+        # the PUT-key mirror (d_put_keys) the plan keeps beside the state mirror: the local launch finds its
+        # PUTs from these two dense arrays (HKV_PUT_KEYS=0: from the ops, experiments)
+        self.put_keys = (torch.zeros(W * S, dtype=torch.int64, device=dev)
+                         if self.fused and os.environ.get("HKV_PUT_KEYS", "1") != "0" else None)
         self.C = slots_per_worker(write_permille, rmw_permille)   # INV send credits per worker
         self.inv_out = torch.zeros(W * self.C * self.op, **u8)
         self.inv_count = torch.zeros(W, dtype=torch.int32, device=dev)
@@ -298,6 +313,10 @@ class Round:
         # applied as a launch of its own with HKV_BATCH_UNIQUE (one ACK per key and peer: a key has at
         # most one local write in flight); ack_off then holds the INV offsets and inv_round the INV total
         self.ack_pm = self.fit and os.environ.get("HKV_ACK_PM", "1") != "0"
+        # ... and all peers' blocks in one launch (HKV_BATCH_ROWS: each key looked up once, its ACKs applied
+        # in peer order; HKV_ACK_ROWS=0: one launch per peer, experiments)
+        self.ack_rows = (os.environ.get("HKV_ACK_ROWS", "1") != "0" and self.sizes.entry == 64
+                         and self.ack_size <= 64)
         self.inv_round = 0
         self.ack_m = self.C
         self.maxc_ev = torch.cuda.Event() if self.fit else None
@@ -340,6 +359,12 @@ class Round:
             self.peer_ts = torch.zeros(int(_L.hkv_wl_peer_ts_words(kvs.h)), dtype=torch.int64, device=dev)
         self.pack_remote = virtual_peers and self.R > 0 and pack_remote
         self.remote_packed = []        # per round index: (INVs, VALs, batch offsets, total, entry offsets)
+        # the peers' INVs of a round index also as rows (HKV_BATCH_ROWS), applied in one launch (64-B entries;
+        # HKV_INV_ROWS=0: one launch per peer, experiments)
+        self.inv_rows = (self.pack_remote and 1 < self.R <= 8 and kvs.sizes.entry == 64 and self.op <= 64
+                         and os.environ.get("HKV_INV_ROWS", "1") != "0")
+        self.remote_rows = []
+        self.rows_acks = None          # our ACKs to the rows (marshalled, not read back: the peers are virtual)
         self.drops = []                # peers dropped from the membership (membership_change)
         self.alive = self.R            # live peers: the first `alive` slots of the remote slabs
         self._counts = {}
@@ -405,7 +430,44 @@ class Round:
                 phys = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
                 check(_L.hkv_wl_peer_locate(self.kvs.h, _ptr(pi), total, self.op, _ptr(phys), _s()), "peer_locate")
                 self.remote_packed.append((pi, pv, off32, total, phys, per_peer))
+                if self.inv_rows:
+                    self.remote_rows.append(self._inv_rows(pi, per_peer, total))
         del scratch
+
+    def _inv_rows(self, pi: torch.Tensor, per_peer, total: int):
+        """The peers' INVs of one round index as rows (HKV_BATCH_ROWS): row r = peer r, position j one key,
+        holes (opcode 0) where a peer sent nothing for it. Positions: peer 0's INVs in order, then each
+        later peer's keys no earlier peer wrote. Returns (rows slab, n positions, inv_at: the element of
+        the slab each packed INV went to, batch offsets [0, n])."""
+        dev, op, R = pi.device, self.op, self.R
+        keys = pi.view(-1, op)[:total, :8].contiguous().view(torch.int64).view(-1)
+        at = torch.empty(total, dtype=torch.int64, device=dev)
+        pos_keys = torch.empty(0, dtype=torch.int64, device=dev)
+        P = 0
+        for r, (base, n, _) in enumerate(per_peer):
+            kr = keys[base:base + n]
+            p = torch.full((n,), -1, dtype=torch.int64, device=dev)
+            if P and n:
+                sk, si = torch.sort(pos_keys)
+                idx = torch.searchsorted(sk, kr).clamp(max=P - 1)
+                hit = sk[idx] == kr
+                p[hit] = si[idx][hit]
+            new = p < 0
+            nn = int(new.sum().item())
+            p[new] = P + torch.arange(nn, device=dev)
+            pos_keys = torch.cat([pos_keys, kr[new]])
+            P += nn
+            at[base:base + n] = p
+        row_of = torch.repeat_interleave(torch.arange(R, device=dev), torch.tensor([n for _, n, _ in per_peer],
+                                                                                     device=dev))
+        inv_at = row_of * P + at
+        rows = torch.zeros(max(R * P, 1) * op, dtype=torch.uint8, device=dev)
+        if total:
+            rows.view(-1, op)[inv_at] = pi.view(-1, op)[:total]
+        if self.rows_acks is None or self.rows_acks.numel() < R * P * self.ack_size:
+            self.rows_acks = torch.zeros(max(R * P, 1) * self.ack_size, dtype=torch.uint8, device=dev)
+        off = torch.tensor([0, P], dtype=torch.int32, device=dev)
+        return rows, P, inv_at, off
 
     # -- pieces of one round
     def refill(self, first: bool = False):
@@ -413,7 +475,7 @@ class Round:
             check(_L.hkv_wl_refill_plan(_ptr(self.states), self.W, self.LOCAL, self.sizes.st_value, self.sizes.shift,
                                         _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
                                         self.machine_id, self.rflags, _ptr(self.counters), _ptr(self.opcodes),
-                                        _ptr(self.patch), _s()), "refill_plan")
+                                        _ptr(self.patch), _ptr(self.put_keys), _s()), "refill_plan")
             return
         if self.st_refill and not first:
             check(_L.hkv_wl_refill_st(_ptr(self.ops), self.W, self.LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
@@ -426,10 +488,12 @@ class Round:
                                _ptr(self.cursor), self.machine_id, int(first), self.rflags, _ptr(self.counters),
                                _ptr(self.opcodes), _ptr(self.hot), _s()),
               "refill")
+        if first:
+            init_mirrors(self.ops, self.op, self.states, getattr(self, "put_keys", None))
 
     def local_batch(self):
         self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb, state_out=self.states,
-                       opcode_in=self.opcodes, patch=self.patch)
+                       opcode_in=self.opcodes, patch=self.patch, put_keys=self.put_keys)
 
     def marshal_invs(self):
         if self.V is not None:
@@ -464,6 +528,11 @@ class Round:
     def peer_timestamps_packed(self, k: int):
         """the same for the packed slabs, whose INVs' entries were located when they were drawn"""
         pi, pv, _, total, phys, _ = self.remote_packed[k]
+        if self.inv_rows:
+            rows, _, inv_at, _ = self.remote_rows[k]
+            check(_L.hkv_wl_peer_ts_rows(self.kvs.h, _ptr(rows), _ptr(inv_at), _ptr(pv), _ptr(phys), total, self.op,
+                                         _ptr(self.peer_ts), self.clock, _s()), "peer_ts_rows")
+            return
         check(_L.hkv_wl_peer_ts_at(self.kvs.h, _ptr(pi), _ptr(pv), _ptr(phys), total, self.op, _ptr(self.peer_ts),
                                    self.clock, _s()), "peer_ts_at")
 
@@ -473,7 +542,15 @@ class Round:
                        unique=unique)
 
     def inv_batches_per_peer(self, k: int):
-        """Every peer's INVs of round index k as a launch of its own (HKV_BATCH_UNIQUE), in peer order"""
+        """Every peer's INVs of round index k as a launch of its own (HKV_BATCH_UNIQUE), in peer order --
+        or all peers' as one rows launch (HKV_BATCH_ROWS): each key looked up once, its INVs applied in
+        peer order"""
+        if self.inv_rows:
+            rows, P, _, off = self.remote_rows[k]
+            if P:
+                self.kvs.batch(L.BatchType.invs, rows, 1, P, self.op, self.mb, offsets=off, unique=True,
+                               rows=(self.R, P, -1))
+            return
         pi, _, _, _, _, per_peer = self.remote_packed[k]
         for base, n, off in per_peer:
             if n:
@@ -493,7 +570,13 @@ class Round:
         acks = self.acks if acks is None else acks
         if self.fit and stride is None and self.ack_pm:   # one launch per peer, in peer order
             T = self.inv_round
-            for r in range(self.ack_total // max(T, 1) if T else 0):
+            n_rows = self.ack_total // max(T, 1) if T else 0
+            if self.ack_rows and n_rows:
+                self.kvs.batch(L.BatchType.acks, acks, self.W, T, self.ack_size, self.mb, rw=self.ops,
+                               rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off, rw_state=self._rws(),
+                               unique=True, rows=(n_rows, T, -1))
+                return
+            for r in range(n_rows):
                 self.kvs.batch(L.BatchType.acks, acks[r * T * self.ack_size:], self.W, T, self.ack_size, self.mb,
                                rw=self.ops, rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off,
                                rw_state=self._rws(), unique=True)
@@ -614,7 +697,11 @@ class Round:
             if packed:
                 pi, pv, off, total, _, _ = self.remote_packed[k]
                 timed("invs", lambda: self.inv_batches_per_peer(k))
-                self.marshal_acks(pi, total, self.ack_out)
+                if self.inv_rows:   # our ACKs to the rows (holes answer nothing)
+                    rows, P, _, _ = self.remote_rows[k]
+                    self.marshal_acks(rows, self.R * P, self.rows_acks)
+                else:
+                    self.marshal_acks(pi, total, self.ack_out)
             else:
                 timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride, counts=ic))
                 self.marshal_acks(ri, self.W * self.rstride, self.ack_out)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HKV_ABI_VERSION 5
+#define HKV_ABI_VERSION 6
 
 /* ------------------------------------------------------------------ reference types
  * Declared here only when the reference's own spacetime.h has not been included; the
@@ -149,7 +149,19 @@ typedef struct hkv_batch_desc {
     uint8_t *d_rw_state;        /* device, ACK batches: a mirror of the read_write_ops' state bytes
                                    (rw_stride_bytes / op size per batch); every completion a launch writes
                                    into read_write_ops is also written here. NULL = none (ABI 5) */
+    const uint64_t *d_put_keys; /* device, local batches with d_state_out: the caller's PUT-key mirror, one
+                                   8-byte word per element (n_batches * stride): the key (op bytes 0..7) of
+                                   a PUT, HKV_NO_PUT for any other opcode, describing the (patched) ops.
+                                   d_state_out must then also hold every element's state byte (op byte 9)
+                                   on entry: with both, the launch finds its PUTs and applies the skip rule
+                                   from two dense arrays instead of the ops (hkv_wl_refill_plan keeps both).
+                                   An element the mirrors misdescribe raises error flag bit 3.
+                                   NULL = none (ABI 6) */
+    int32_t  n_rows;            /* HKV_BATCH_ROWS: rows of elements, applied row after row (ABI 6) */
+    int32_t  skip_row;          /* HKV_BATCH_ROWS: a row that is not applied (-1: none) */
+    int64_t  row_stride;        /* HKV_BATCH_ROWS: elements from one row to the next in d_elems */
 } hkv_batch_desc;
+#define HKV_NO_PUT 0xFFFFFFFFFFFFFFFFull
 
 /* d_patch layout (16 bytes per element): key 0..7, opcode 8, val_len 9, flags (RMW_flag | no_coales
  * << 1) 10..11, value fill byte 12 (0: the value is kept), ts reset 13 (1: ts bytes 11..15 := 0),
@@ -174,7 +186,17 @@ typedef struct hkv_batch_desc {
  * one such launch. A duplicate breaks the results; with HKV_CHECK_UNIQUE=1 in the environment every
  * launch checks and raises error flag bit 4. */
 #define HKV_BATCH_UNIQUE 8u
-
+/* With HKV_BATCH_UNIQUE, INV and ACK launches of 64-byte entries: n_rows (at most 8) launches of one
+ * layout in one, applied in row order -- row r is the launch whose elements start at element
+ * r * row_stride of d_elems (the same n_batches, stride, counts or offsets and read_write_ops for every
+ * row), row skip_row excepted. Element j of every row carries the same key, or is a hole (opcode byte
+ * 0: not an element of its row's batch; nothing of it is read or written). So each key is looked up
+ * once and its elements applied one row after the other: a coordinator's ACKs from all its peers, lined
+ * up with the INVs they answer, go in one launch, and so do INVs that peers sent for the same keys.
+ * An element whose key differs from its position's raises error flag bit 4. d_node_suspected must be
+ * NULL. */
+#define HKV_BATCH_ROWS 16u   /* packed rows: elements past d_counts[n_batches] (<= stride) are in no batch */
+#define HKV_MAX_ROWS 8
 int  hkv_abi_version(void);
 const char *hkv_last_error(void);
 
@@ -203,7 +225,7 @@ void *hkv_device_index(hkv_table *t);
  * bit 0: an element resolved in parallel (not a key's first mutating element) changed the meta;
  * bit 1: the ACK direct path completed a write from an unexpected state;
  * bit 2: a local launch's mutating element had not offered itself in its prepass;
- * bit 3: d_opcode_in missed a PUT (the mirror disagrees with the op);
+ * bit 3: d_opcode_in missed a PUT, or d_put_keys / the entry states of d_state_out disagree with the ops;
  * bit 4: an HKV_BATCH_UNIQUE launch held a key twice (checked with HKV_CHECK_UNIQUE=1) */
 int  hkv_take_error_flags(hkv_table *t, uint32_t *out);
 void *hkv_device_log(hkv_table *t);

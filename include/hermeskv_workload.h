@@ -84,11 +84,14 @@ int hkv_wl_refill(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op
  * membership marshals, the ACK launch's d_rw_state) -- instead of the ops. Each refilled op gets a
  * valid patch in d_patch (HKV_PATCH_BYTES per op, include/hermeskv.h), every other op an invalid one;
  * d_opcode (the opcode mirror) takes the refilled ops' opcodes. The ops themselves are untouched:
- * the next local launch, given d_patch, applies the patches as it reads them. */
-int hkv_wl_refill_plan(const uint8_t *d_states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
+ * the next local launch, given d_patch, applies the patches as it reads them. With d_put_keys (may be
+ * NULL), a refilled op's PUT-key word (hkv_batch_desc.d_put_keys: its key for a PUT, HKV_NO_PUT
+ * otherwise) is written there and its d_states byte set to ST_NEW, so both mirrors describe the
+ * patched ops the next local launch sees. */
+int hkv_wl_refill_plan(uint8_t *d_states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
                        const uint64_t *d_trace_key, const uint8_t *d_trace_op, int32_t trace_len, uint32_t *d_cursor,
                        uint32_t machine_id, uint32_t flags, unsigned long long *d_counters, uint8_t *d_opcode,
-                       uint8_t *d_patch, void *stream);
+                       uint8_t *d_patch, uint64_t *d_put_keys, void *stream);
 /* hkv_wl_refill for big ops (op_size > 64, refilled in place; not on the first pass, flags
  * HKV_WL_REFILL_ALL and HKV_WL_READ_TS_RESET), deciding from d_states, the state mirror
  * hkv_wl_refill_plan reads: an op that is not refilled is not touched, a refilled one is only
@@ -154,6 +157,12 @@ int hkv_wl_peer_locate(hkv_table *t, const uint8_t *d_invs, int64_t n, uint32_t 
                        void *stream);
 int hkv_wl_peer_ts_at(hkv_table *t, uint8_t *d_invs, uint8_t *d_vals, const uint64_t *d_phys, int64_t n,
                       uint32_t op_size, unsigned long long *d_peer_ts, uint32_t round, void *stream);
+/* hkv_wl_peer_ts_at for INVs laid out as rows (hkv_batch_desc HKV_BATCH_ROWS: row r = peer r, element j
+ * of every row on one key): INV g, whose VAL is d_vals[g] and entry d_phys[g], sits at element
+ * d_inv_at[g] of d_rows. */
+int hkv_wl_peer_ts_rows(hkv_table *t, uint8_t *d_rows, const int64_t *d_inv_at, uint8_t *d_vals,
+                        const uint64_t *d_phys, int64_t n, uint32_t op_size, unsigned long long *d_peer_ts,
+                        uint32_t round, void *stream);
 
 /* The virtual peers' answers to this round's INVs: for INV j of worker w, the ack_size-byte
  * element d_acks[w*out_stride + j*n_peers + r] from peer_ids[r] is an ACK {key, ST_OP_ACK,
@@ -280,6 +289,15 @@ int hkv_wl_vals_credit(uint8_t *d_aq, int32_t *d_aq_n, const int32_t *d_ack_coun
  * d_offsets[n_rows] = the total (d_offsets has n_rows + 1 entries) */
 int hkv_wl_pack_rows(const uint8_t *d_rows, const int32_t *d_counts, int32_t n_rows, int32_t C,
                      uint32_t elem_size, uint8_t *d_packed, int32_t *d_offsets, void *stream);
+/* This round's INVs (the INV callbacks of hermes_worker.c:12-65) straight into one packed slab of at
+ * most `cap` INVs, so a replica group can size its collectives without reading anything back: worker
+ * w sends its first min(sendable, C, what cap leaves after the workers before it) INVs to
+ * d_out[d_offsets[w] ..] (d_offsets[n_workers] = the slab's total, d_count = sendable per worker,
+ * d_sent = sent per worker; d_states is the state mirror, kept up to date). The INVs not sent keep
+ * their state and are counted in *d_held. */
+int hkv_wl_marshal_invs_packed(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint8_t *d_states,
+                               int32_t C, int32_t cap, uint8_t *d_out, int32_t *d_offsets, int32_t *d_count,
+                               int32_t *d_sent, uint32_t machine_id, unsigned long long *d_held, void *stream);
 
 /* ACKs for received packed INV slabs ([rows][width], d_counts[rows] live per row), element i of
  * the output in the position of INV i: an ACK (with RMWs an INV-abort) where it applied,

@@ -95,8 +95,11 @@ class Mirror:
 
     def batch(self, btype, elems, n_batches, stride, elem_size, membership, counts=None, rw=None,
               rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None, state_out=None, opcode_in=None,
-              patch=None, rw_state=None, unique=False):
+              patch=None, rw_state=None, unique=False, put_keys=None, rows=None):
         import torch
+        if rows is not None:
+            return self._rows(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
+                              rw_stride_bytes, rw_state, rows)
         if offsets is not None:
             return self._packed(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
                                 rw_stride_bytes, rw_state, unique)
@@ -114,6 +117,11 @@ class Mirror:
         if opcode_in is not None:   # the caller's opcode mirror must be every element's opcode byte
             assert np.array_equal(opcode_in[: n_batches * stride].cpu().numpy(),
                                   np.frombuffer(e_in.tobytes(), np.uint8).reshape(-1, elem_size)[:, 8])
+        if put_keys is not None:   # the PUT-key mirror and the entry states describe the (patched) elements
+            eb = np.frombuffer(e_in.tobytes(), np.uint8).reshape(-1, elem_size)
+            want = np.where(eb[:, 8] == int(L.Op.PUT), eb[:, :8].copy().view(np.int64)[:, 0], -1)
+            assert np.array_equal(put_keys[: n_batches * stride].cpu().numpy(), want), "PUT-key mirror is stale"
+            assert np.array_equal(state_out[: n_batches * stride].cpu().numpy(), eb[:, 9]), "entry state mirror is stale"
         self._count(btype, "in8", 8, np.frombuffer(e_in.tobytes(), np.uint8), n_batches, stride, elem_size, c_in)
         rw_in = rw_op = None
         if rw is not None:
@@ -122,7 +130,7 @@ class Mirror:
         rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
         self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
                    node_suspected, stream, state_out=state_out, opcode_in=opcode_in, patch=patch, rw_state=rw_state,
-                   unique=unique)
+                   unique=unique, put_keys=put_keys)
         torch.cuda.synchronize()
         self.o.batch_multi(int(btype), e_in, n_batches, stride, c_in, membership, rw_in,
                            rw_stride_bytes // self.g.sizes.op if rw is not None else 0)
@@ -170,6 +178,67 @@ class Mirror:
         n = min(len(st_before), len(rws_in))
         assert np.array_equal(rws_in[:n], st_before[:n]), f"{what}: the caller's state mirror was already stale"
         assert np.array_equal(rw_state.cpu().numpy()[:n], st_after[:n]), f"{what}: read_write_ops state mirror differs"
+
+    def _rows(self, btype, elems, n_batches, total, elem_size, membership, offsets, stream, rw, rw_stride_bytes,
+              rw_state, rows):
+        """An HKV_BATCH_ROWS launch: the oracle applies row after row (skip row excepted), each row's
+        batches without their holes (opcode 0); the device's rows must equal them, holes untouched."""
+        import torch
+        torch.cuda.synchronize()
+        n_rows, row_stride, skip = rows
+        assert offsets is not None, "the tests' row launches are packed"
+        off = offsets[: n_batches + 1].cpu().numpy().astype(np.int64)
+        assert off[0] == 0 and off[-1] <= total
+        bat = np.repeat(np.arange(n_batches), np.diff(off))
+        nl = int(off[-1])   # elements past the last offset are in no batch (and must stay untouched)
+        flat_all = elems.cpu().numpy().copy()
+        rw_in = rw.cpu().numpy().copy().view(np.dtype((np.void, self.g.sizes.op))) if rw is not None else None
+        st_before = rw_in.view(np.uint8).reshape(-1, self.g.sizes.op)[:, 9].copy() if rw is not None else None
+        rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
+        ins = {}
+        for r in range(n_rows):
+            if r == skip:
+                continue
+            flat = flat_all[r * row_stride * elem_size:(r * row_stride + total) * elem_size].reshape(total, elem_size)
+            ins[r] = flat.copy()
+        self._orig(btype, elems, n_batches, total, elem_size, membership, rw=rw, rw_stride_bytes=rw_stride_bytes,
+                   stream=stream, offsets=offsets, rw_state=rw_state, unique=True, rows=rows)
+        torch.cuda.synchronize()
+        got_all = elems.cpu().numpy()
+        what = f"{self.name} launch {self.launches} type {int(btype)} (rows)"
+        for r, flat in ins.items():
+            live = flat[:, 8] != 0
+            live[nl:] = False
+            cnt = np.bincount(bat[live[:nl]], minlength=n_batches).astype(np.int32)
+            width = max(int(cnt.max()), 1) if n_batches else 1
+            rws_ = np.zeros((n_batches, width, elem_size), np.uint8)
+            pos = np.arange(width)[None, :] < cnt[:, None]
+            rws_[pos] = flat[live]
+            self._count(btype, "in8", 8, rws_.reshape(-1), n_batches, width, elem_size, cnt)
+            e_in = rws_.reshape(-1).view(np.dtype((np.void, elem_size))).copy()
+            self.o.batch_multi(int(btype), e_in, n_batches, width, cnt, membership, rw_in,
+                               rw_stride_bytes // self.g.sizes.op if rw is not None else 0)
+            want = flat.copy()
+            want[live] = e_in.view(np.uint8).reshape(n_batches, width, elem_size)[pos]
+            got = got_all[r * row_stride * elem_size:(r * row_stride + total) * elem_size].reshape(total, elem_size)
+            grow = np.zeros_like(rws_)
+            grow[pos] = got[live]
+            self._count(btype, "out8", 8, grow.reshape(-1), n_batches, width, elem_size, cnt)
+            self._count(btype, "out9", 9, grow.reshape(-1), n_batches, width, elem_size, cnt)
+            if not np.array_equal(got, want):
+                bad = np.nonzero((got != want).any(axis=1))[0]
+                pytest.fail(f"{what}: row {r} elements differ at {len(bad)} elements, first {bad[:8]}")
+        if rw is not None:
+            rw_op = rw.cpu().numpy()
+            assert np.array_equal(rw_op, rw_in.view(np.uint8)), f"{what}: read_write_ops differ"
+            self._check_rw_state(rw_state, rws_in, st_before, rw_op.reshape(-1, self.g.sizes.op)[:, 9], what)
+        gl, ol = self.g.log_bytes(), self.o.log_bytes()[: self.g.cfg.log_cap]
+        if not np.array_equal(gl, ol):
+            bad = np.nonzero(gl != ol)[0]
+            pytest.fail(f"{what}: log differs in entries {np.unique(bad // self.g.sizes.entry)[:8]}")
+        assert np.array_equal(self.g.index_bytes(), self.o.index_bytes()), f"{what}: index differs"
+        assert self.g.take_error_flags() == 0, f"{what}: device consistency flags"
+        self.launches += 1
 
     def _packed(self, btype, elems, n_batches, total, elem_size, membership, offsets, stream, rw=None,
                 rw_stride_bytes=0, rw_state=None, unique=False):

@@ -74,6 +74,17 @@ def main():
     for _ in range(3):
         grp.step()
     torch.cuda.synchronize()
+    # steady rounds at the planned width make no host synchronisation: 4 more rounds, unmirrored,
+    # under torch.cuda.set_sync_debug_mode("error")
+    for m in mirrors:
+        m.g.batch = m._orig
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        for _ in range(4):
+            grp.step()
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    torch.cuda.synchronize()
     offs = [mirrors[0].o.lookup(int(k)) for k in keys]
     logs = [m.g.log_bytes() for m in mirrors]
     bad = 0
@@ -91,6 +102,7 @@ def main():
     except Exception:   # noqa: BLE001 -- the version is informational
         ver = None
     print(json.dumps({"launches": [m.launches for m in mirrors], "calls": calls, "diverged_keys": bad,
+                      "width": grp.plan.width if grp.plan else None,
                       "committed": [s["committed"] for s in stats], "rccl_version": ver, "skew": skew,
                       "retry": retry_skew}))
 

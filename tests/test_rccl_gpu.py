@@ -36,8 +36,10 @@ def test_one_rank_rccl_group_round(args):
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     d = json.loads(p.stdout.strip().splitlines()[-1])
     print(d)
-    assert d["launches"] == [18, 18, 18], d          # 3 rounds x (local, INV per peer (2), ACK per peer (2), VAL)
+    assert d["launches"] == [15, 15, 15], d          # 3 rounds x (local, INV per peer (2), the ACK rows, VAL)
     assert d["diverged_keys"] == 0, d
     # per round and replica: INV totals + INV slabs + VAL totals + VAL slabs gathered, ACKs all-to-all
-    assert d["calls"]["all_gather_into_tensor"] == 3 * 4 * 3 and d["calls"]["all_to_all_single"] == 3 * 3, d
+    # (3 mirrored rounds, then 4 steady ones under the sync check)
+    assert d["calls"]["all_gather_into_tensor"] == 7 * 4 * 3 and d["calls"]["all_to_all_single"] == 7 * 3, d
+    assert d["width"] is not None
     assert min(d["committed"]) > 0

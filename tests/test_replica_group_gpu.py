@@ -374,3 +374,136 @@ def test_bench_multi_rank_over_gloo(world, config):
     if config == "cfg5":
         g = d["detail"]["membership"]["g_membership_after"]
         assert g == ((1 << world) - 1) & ~(1 << (world - 1)), d["detail"]["membership"]
+
+
+class _ThreadComm:
+    """The collectives of `n` ranks run as threads of one process on one GPU: each rank leaves its
+    input, and after a barrier copies what it receives on the shared (null) stream -- the producers
+    of every input were enqueued before the barrier, so stream order makes the copies correct without
+    any host synchronisation."""
+
+    class _Rank:
+        def __init__(self, hub, rank):
+            self.hub, self.rank = hub, rank
+
+        def gather(self, out, inp):
+            h = self.hub
+            h.slots[self.rank] = inp
+            h.bar.wait()
+            ov = out.view(h.n, -1)
+            for p, x in enumerate(h.slots):
+                ov[p].copy_(x.reshape(-1))
+            h.bar.wait()
+
+        def gather_async(self, out, inp):
+            self.gather(out, inp)
+            return type("Done", (), {"wait": lambda self: None})()
+
+        def a2a(self, out, inp):
+            h = self.hub
+            h.slots[self.rank] = inp
+            h.bar.wait()
+            ov = out.view(h.n, -1)
+            for p, x in enumerate(h.slots):
+                ov[p].copy_(x.view(h.n, -1)[self.rank])
+            h.bar.wait()
+
+    def __init__(self, n):
+        import threading
+        self.n = n
+        self.bar = threading.Barrier(n, timeout=60)
+        self.slots = [None] * n
+
+    def rank(self, r):
+        return self._Rank(self, r)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_group_rounds_without_host_sync(world):
+    """ReplicaGroupRound's steady rounds (bench.py --gpus N's configuration: retry + skew flags 3)
+    make no host synchronisation: after the first round calibrates the slab width (WidthPlan), 10
+    rounds run under torch.cuda.set_sync_debug_mode("error") -- a .item(), .cpu() or synchronize in
+    any of them raises. The ranks are threads of this process with a thread-barrier comm; afterwards
+    every rank's table has converged (same state, timestamp and value of every key, all VALID)."""
+    import faulthandler
+    import os
+    import threading
+
+    from hermes_amd.kvs import HermesKV
+    from hermes_amd.replica_group import ReplicaGroupRound
+    from hermes_amd.workload import zipf_params
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+    dump = open(os.path.join(root, "gpurun_out", f"sync_test_stacks_{world}.txt"), "w")
+    faulthandler.dump_traceback_later(90, exit=False, file=dump)   # every thread's stack if it hangs
+    n_keys = 20000
+    hub = _ThreadComm(world)
+    z = zipf_params(n_keys, 0.99)
+    tables = [HermesKV(n_keys, 1 << 15, 1 << 22, machine_id=r, skew=3) for r in range(world)]
+    errs, drivers = [], [None] * world
+    phase = threading.Barrier(world + 1, timeout=120)
+
+    def note(msg):
+        dump.write(msg + "\n")
+        dump.flush()
+
+    def run(r):
+        try:
+            note(f"rank {r} start")
+            drivers[r] = drv = ReplicaGroupRound(tables[r], 64, z, 200, seed=123, world=world, rank=r,
+                                                 trace_len=1024, retry_stalled=True, comm=hub.rank(r))
+            note(f"rank {r} built")
+            drv.step()            # calibrates the width (host read)
+            note(f"rank {r} calibrated, width {drv.plan.width}")
+            phase.wait()          # the main thread arms the sync check
+            phase.wait()
+            for k in range(10):
+                drv.step()
+                note(f"rank {r} step {k}")
+            phase.wait()          # the main thread disarms it
+        except Exception as e:   # noqa: BLE001 -- reported below
+            errs.append((r, repr(e)))
+            hub.bar.abort()
+            phase.abort()
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    try:
+        phase.wait()
+        torch.cuda.synchronize()
+        torch.cuda.set_sync_debug_mode("error")
+        phase.wait()
+        phase.wait()
+    except threading.BrokenBarrierError:
+        pass
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+        for t in ts:
+            t.join(timeout=120)
+        faulthandler.cancel_dump_traceback_later()
+        dump.close()
+    assert not errs, errs
+    torch.cuda.synchronize()
+    for d in drivers:
+        st = d.stats()
+        assert st["committed"] > 0 and st["writes_completed"] > 0, st
+        assert d.plan is not None and d.plan.width is not None
+    assert all(t.take_error_flags() == 0 for t in tables)
+    # state, timestamp (cid, version) and value of every key (last_local_write_ts is each replica's own)
+    keys = gen_keys(n_keys)
+    base = None
+    for g in tables:
+        log = g.log_bytes()
+        img = []
+        for k in keys:
+            off = g.lookup_offset(int(k))
+            img.append(None if off is None else (int(log[off + 18]), log[off + 23:off + 28].tobytes(),
+                                                 log[off + 33:off + 64].tobytes()))
+        if base is None:
+            base = img
+            bad = sum(1 for x in img if x is not None and x[0] != L.State.VALID)
+            assert bad == 0, f"{bad} keys not VALID"
+        else:
+            diff = sum(1 for x, y in zip(img, base) if x != y)
+            assert diff == 0, f"{diff} keys differ between replicas"

@@ -40,7 +40,8 @@ def test_bench_round_mirrored(theta, workers, cfg3):
     for _ in range(steps):
         r.step()
     torch.cuda.synchronize()
-    assert m.launches == steps * 6      # local, INV per peer (2), ACK per peer (2), VAL
+    # local, the peers' INVs and ACKs as one rows launch each (64-B entries; cfg3: one launch per peer), VAL
+    assert m.launches == steps * (6 if cfg3 else 4)
     st = r.stats()
     assert st["committed"] > 0 and st["writes_completed"] > 0, st
     assert g.take_error_flags() == 0
@@ -77,7 +78,7 @@ def test_retry_round_mirrored(skew, hot):
     for _ in range(steps):
         r.step()
     torch.cuda.synchronize()
-    assert m.launches == steps * 6      # local, INV per peer (2), ACK per peer (2), VAL
+    assert m.launches == steps * 4      # local, the peers' INVs and ACKs (a rows launch each), VAL
     st = r.stats()
     assert st["committed"] > 0 and st["dropped"] == 0, st
     assert g.take_error_flags() == 0
@@ -313,7 +314,8 @@ def test_val_credits_round_mirrored(credits, cfg3):
     for _ in range(steps):
         r.step()
     torch.cuda.synchronize()
-    assert m.launches == steps * 5      # local, INV per peer (2), ACK (one packed launch), VAL
+    # local, the peers' INVs (one rows launch; cfg3: one launch per peer), ACK (one packed launch), VAL
+    assert m.launches == steps * (5 if cfg3 else 4)
     st = r.stats()
     assert g.take_error_flags() == 0
     assert seen["gated"] > 0 and seen["carried_rounds"] > 0, seen
@@ -496,9 +498,11 @@ def test_refill_plan_matches_refill(flags):
     opc0 = ops.reshape(W * S, osz)[:, 8].copy()
     d_opc = torch.from_numpy(opc0.copy()).cuda()
     d_patch = torch.full((W * S * 16,), 0xAB, dtype=torch.uint8, device="cuda")   # stale bytes get overwritten
+    pk0 = rng.integers(-2**62, 2**62, size=W * S, dtype=np.int64)                  # kept where not refilled
+    d_pk = torch.from_numpy(pk0.copy()).cuda()
     WL.check(WL._L.hkv_wl_refill_plan(WL._ptr(d_st), W, S, sz.st_value, sz.shift, WL._ptr(d_tkey), WL._ptr(d_top),
                                       tlen, WL._ptr(d_cur), mid, flags, WL._ptr(d_cnt), WL._ptr(d_opc),
-                                      WL._ptr(d_patch), None), "refill_plan")
+                                      WL._ptr(d_patch), WL._ptr(d_pk), None), "refill_plan")
     WL.check(WL._L.hkv_wl_fold_counters(WL._ptr(d_cnt), None), "fold")
     torch.cuda.synchronize()
     patch = d_patch.cpu().numpy()
@@ -508,6 +512,14 @@ def test_refill_plan_matches_refill(flags):
     assert np.array_equal(d_cur.cpu().numpy(), exp_cur)
     assert d_cnt[:5].cpu().tolist() == exp_cnt.tolist()
     assert np.array_equal(d_opc.cpu().numpy(), exp_ops.reshape(W * S, osz)[:, 8])
+    # the PUT-key mirror and the state mirror describe the patched ops (kept ops keep their words)
+    refilled = patch.reshape(-1, 16)[:, 14] == 1
+    e = exp_ops.reshape(W * S, osz)
+    want_pk = np.where(e[:, 8] == 112, e[:, :8].copy().view(np.int64)[:, 0], -1)
+    assert np.array_equal(d_pk.cpu().numpy()[refilled], want_pk[refilled])
+    assert np.array_equal(d_pk.cpu().numpy()[~refilled], pk0[~refilled])
+    assert np.array_equal(d_st.cpu().numpy()[refilled], e[refilled, 9])
+    assert np.array_equal(d_st.cpu().numpy()[~refilled], ops.reshape(W * S, osz)[~refilled, 9])
 
 
 @pytest.mark.parametrize("mirror", [False, True])

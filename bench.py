@@ -278,6 +278,11 @@ def main():
     probe_ms = {k: avg(v) for k, v in probe_events.items()}
     ms = dict(probe_ms)
     ms.update({k: avg(v) for k, v in events.items()})
+    # a local launch in two stages (its prepass on a side stream beside the VAL batch): its kernel time
+    # is both stages' (the roofline charges the launch the prepass it overlaps)
+    pre_ms = ms.pop("local_pre", None)
+    if pre_ms is not None and "local" in ms:
+        ms["local"] += pre_ms
     W, S = a.workers, Round.LOCAL
     per_launch_bytes = {
         "local": W * S * BYTES["get"] + puts_per_step * (BYTES["put"] - BYTES["get"]),
@@ -356,7 +361,7 @@ def main():
             "elements_per_step": {"inv": n_inv, "ack": n_ack, "val": n_val},
         },
         "roofline": {
-            "bound": "hbm", "kernel": (f"{dom} batch launch (" + ("k_local_pre + k_local_fused + k_commit, the direct path" if dom == "local"
+            "bound": "hbm", "kernel": (f"{dom} batch launch (" + ("k_local_pre (own stream) + k_local_fused + k_local_deferred + k_commit_w, the direct path" if dom == "local"
                                                   and not cfg3 else "k_lookup + element-order rounds") + ", hkv_batch.hip)"),
             "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
             "traffic": traffic, "traffic_source": traffic_src, "launch_ms": ms.get(dom),
@@ -424,6 +429,7 @@ def main():
         # the policies start from the table this run leaves: every write of it must have completed,
         # which holds only when no INV was held back by the send credits (nothing else is in flight)
         assert int(rnd.held.item()) == 0, "INVs held back: writes in flight would skew the other policies"
+        rnd.close()
         out["detail"]["policies"] = policy_rates(a, kvs, z, L, Round, (retry, a.skew, a.coalesce_hot))
     if rank == 0 and world == 1 and a.host_api_seconds > 0:
         out["detail"]["host_api"] = host_api_rate(a.host_api_seconds)
@@ -475,6 +481,7 @@ def policy_rates(a, kvs, z, L, Round, headline) -> dict:
         audit = r.audit_rounds(3) if not hot else None
         held = int(r.held.item())
         assert held == 0, f"policy {name}: INVs held back"   # the next policy needs a quiet table
+        r.close()
         out[name] = {"value": c[0] / dt, "unit": "ops/s", "steps": a.policy_steps, "warmup": warm,
                      "ms_per_step": dt * 1e3 / a.policy_steps, "committed_per_step": c[0] / a.policy_steps,
                      "writes_completed_per_step": c[2] / a.policy_steps, "dropped_per_step": c[3] / a.policy_steps,

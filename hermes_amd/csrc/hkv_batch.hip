@@ -105,6 +105,7 @@ struct BatchArgs {
     int32_t check_unique;        // HKV_CHECK_UNIQUE: HKV_BATCH_UNIQUE launches verify their keys are unique
     int32_t pre_patch_first;     // k_local_pre reads a PUT's header only when it has no patch (HKV_PRE_PATCH_FIRST)
     int32_t wave_copy;           // big values copied a wave per value (HKV_WAVE_COPY=0: by their own lane)
+    int32_t cancel;              // k_local_pre undoes its tags (HKV_BATCH_PREPASS_CANCEL)
 };
 
 // Rounds after round 0 per batch type: how often a hot key usually mutates in one launch beyond
@@ -1335,6 +1336,10 @@ __global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
             Meta m0;
             const uint64_t ek = line_key_meta(ln[k], m0);
             if (q != 0 || !ok[k] || ek != key[k]) continue;
+            if (a.cancel) {   // a prepass whose launch will not run: its tags go (its F words are stale anyway)
+                if ((uint8_t)(m0.w5 >> 16) == a.ltag) a.log[phys[k] + kEntryMetaOff + 4] = 0;
+                continue;
+            }
             if (!would_mutate(kLocal, reinterpret_cast<const uint8_t *>(hput), m0, c) || (a.dbg & 1)) continue;
             atomicMin(a.fw + fw_index(a, phys[k]), ((unsigned long long)(~a.rtag0) << 32) | idx[k]);
             if ((uint8_t)(m0.w5 >> 16) != a.ltag && !(a.dbg & 32)) a.log[phys[k] + kEntryMetaOff + 4] = a.ltag;
@@ -2872,7 +2877,27 @@ __device__ void hp_partition(const HostPartCommon &p, HpLds &L, int g, int nb, u
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (pr) p.prof[4] = wall_clock64();
-    if (tid == 0) __hip_atomic_store(p.flags + g, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0) {
+        __hip_atomic_store(p.flags + g, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // the partition's next launch may start: the entry lines written above are visible to it
+        if (p.order) __hip_atomic_store(p.order + g, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Launches on several streams: workgroup g waits until its partition's previous launch is done
+// (order[g] == seq - 1). Every wait ends: after 1 s (wall_clock64 at 100 MHz) it gives up, raises
+// error flag bit 5 and goes on, so a lost predecessor cannot hang the GPU.
+__device__ __forceinline__ void hp_wait_turn(const HostPartCommon &c, int g, uint32_t seq)
+{
+    if (!c.order || threadIdx.x != 0) return;
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(c.order + g, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != seq - 1u) {
+        __builtin_amdgcn_s_sleep(4);
+        if (wall_clock64() - t0 > 100000000ull) {
+            if (c.error_flags) atomicOr(c.error_flags, 32u);
+            break;
+        }
+    }
 }
 
 // One launch, its headers in the kernel arguments
@@ -2886,6 +2911,7 @@ __global__ __launch_bounds__(kHpThreads) void k_hpart(HostPartLaunch p)
         L.prow[0][tid] = p.part[g][tid];
         L.prow[1][tid] = p.part[g + 1][tid];
     }
+    hp_wait_turn(p.c, g, p.seq);
     __syncthreads();
     hp_scan(L, nb);
     __syncthreads();
@@ -3047,7 +3073,7 @@ size_t batch_fw_words(uint64_t log_cap) { return (size_t)(log_cap >> 6); }
 
 uint32_t batch_max_epoch() { return (1u << 29) - 1; }
 
-int launch_batch(const BatchLaunch &bl, hipStream_t s)
+int launch_batch(BatchLaunch &bl, hipStream_t s)
 {
     const int64_t n = bl.n;
     if (n <= 0) return 0;
@@ -3059,6 +3085,7 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
     a.opc = bl.type == kLocal ? bl.opcode_in : nullptr;
     a.patch = nullptr;
     a.pkeys = nullptr;
+    a.cancel = bl.stage == 3;
     a.n_rows = bl.n_rows;
     a.skip_row = bl.skip_row;
     a.row_stride = bl.row_stride;
@@ -3131,6 +3158,23 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
                               bl.g.st_value == 31 && bl.g.entry_size == 64 && !bl.offsets;
     // HKV_PATCH_APPLY=1: patches always written into the ops first (experiments)
     static const bool patch_apply_env = getenv("HKV_PATCH_APPLY") && atoi(getenv("HKV_PATCH_APPLY")) != 0;
+    if (bl.stage == 3) {   // HKV_BATCH_PREPASS_CANCEL: the prepass's lookups again, clearing its tags
+        if (bl.pre_done) {
+            if (bl.patch) a.patch = bl.patch;
+            if (bl.put_keys && a.state_out) a.pkeys = bl.put_keys;
+            hipLaunchKernelGGL(k_local_pre, dim3((unsigned)((n + kPreElems - 1) / kPreElems)), dim3(256), 0, s, a);
+        }
+        return hipGetLastError() == hipSuccess ? 0 : -3;
+    }
+    if (bl.stage == 1) {   // HKV_BATCH_PREPASS: the direct path's prepass only (any other path runs whole later)
+        if (local_direct && !small && !patch_apply_env) {
+            if (bl.patch) a.patch = bl.patch;
+            if (local_direct && bl.put_keys && a.state_out) a.pkeys = bl.put_keys;
+            hipLaunchKernelGGL(k_local_pre, dim3((unsigned)((n + kPreElems - 1) / kPreElems)), dim3(256), 0, s, a);
+            bl.pre_done = 1;
+        }
+        return hipGetLastError() == hipSuccess ? 0 : -3;
+    }
     if (bl.patch && (small || !local_direct || patch_apply_env)) {  // the other paths take the patches as op writes first
         hipLaunchKernelGGL(k_apply_patch, dim3(grid), dim3(256), 0, s, bl.elems, bl.patch, n, bl.esz, bl.g.st_value);
     } else if (bl.patch) {
@@ -3141,7 +3185,11 @@ int launch_batch(const BatchLaunch &bl, hipStream_t s)
         if (launch_small(a, s)) return -3;
         return 0;                              // node_suspected written by the kernel
     } else if (local_direct) {
-        hipLaunchKernelGGL(k_local_pre, dim3((unsigned)((n + kPreElems - 1) / kPreElems)), dim3(256), 0, s, a);
+        if (bl.stage == 2 && bl.pre_done) {   // the prepass ran earlier (HKV_BATCH_PREPASS)
+            if (bl.reset_defer && hipMemsetAsync(bl.ctr + kCtrDefer, 0, 4, s) != hipSuccess) return -3;
+        } else {
+            hipLaunchKernelGGL(k_local_pre, dim3((unsigned)((n + kPreElems - 1) / kPreElems)), dim3(256), 0, s, a);
+        }
         // HKV_LF_PAIR: elements per lane group in k_local_fused (2: 32 per wave; 4: 64, more loads in flight)
         static const int lfp_env = getenv("HKV_LF_PAIR") ? atoi(getenv("HKV_LF_PAIR")) : 2;
         if (lfp_env == 4)

@@ -45,6 +45,9 @@ struct BatchLaunch {
     uint8_t g_membership;
     uint8_t w_ack_init;
     int32_t path;                             // kPath*: which engine runs the launch
+    int32_t stage;                            // 0 whole launch, 1 local prepass only, 2 after a prepass
+    int32_t pre_done;                         // stage 2: the prepass ran in stage 1 (else it runs now)
+    int32_t reset_defer;                      // stage 2: the scratch moved since stage 1 (zero its counter)
     int32_t unique;                           // HKV_BATCH_UNIQUE: no key twice in the launch
     int32_t n_rows, skip_row;                 // HKV_BATCH_ROWS (n_rows 0: a plain launch)
     int64_t row_stride;
@@ -102,7 +105,12 @@ struct HostPartCommon {
     unsigned int *error_flags;
     uint32_t *flags;             // device address: kPartG words, workgroup g stores seq into flags[g]
     unsigned long long *prof;    // HKV_PART_PROF: workgroup 0's phase timestamps (debug), or NULL
+    // launches on several streams: workgroup g of launch seq first waits until order[g] (device memory)
+    // is seq - 1, and stores seq there when done, so each partition's launches apply in launch order
+    // while different partitions' run side by side. NULL: stream order does it (one stream).
+    uint32_t *order;
 };
+constexpr int kPartStreams = 4;  // streams partitioned launches go round (GPU_MAX_HW_QUEUES is 4)
 struct HostPartLaunch {          // one launch, everything in the kernel arguments
     HostPartCommon c;
     uint32_t seq;
@@ -159,7 +167,7 @@ struct TableView {
 };
 int table_view(const hkv_table *t, TableView *out);
 
-int launch_batch(const BatchLaunch &bl, hipStream_t s);
+int launch_batch(BatchLaunch &bl, hipStream_t s);   // sets bl.pre_done (stage 1)
 constexpr int64_t kSmallMaxElems = 4096;   // launches the single-workgroup kernel can take
 int launch_populate(const PopulateLaunch &pl, hipStream_t s);
 int launch_hash_ids(const uint32_t *ids, uint64_t *out, int64_t n, hipStream_t s);

@@ -111,6 +111,14 @@ struct hkv_table {
     int64_t batch_cap = 0;
     unsigned long long *d_fw = nullptr;  // F words, one per 64-B log line (+ INV words X, Y, ACK words T)
     uint32_t epoch = 0;                // batch launches since d_fw was all-ones
+    uint32_t scratch_gen = 0;          // d_batch reallocations
+    // a local launch's prepass (HKV_BATCH_PREPASS) waiting for the rest of its launch
+    struct {
+        bool valid = false, done = false;
+        uint32_t epoch = 0, scratch_gen = 0;
+        int64_t n = 0;
+        const uint8_t *elems = nullptr;
+    } pre;
     unsigned int *d_error_flags = nullptr;
     int32_t *d_ns_idx = nullptr;
     int32_t ns_cap = 0;
@@ -125,6 +133,18 @@ struct hkv_table {
     // stream order, so each word only grows); pseq counts the launches
     uint32_t *pflags = nullptr, *pflags_d = nullptr;
     uint32_t pseq = 0;
+    // ... launched round the streams pstreams (HKV_PART_STREAMS, default kPartStreams), ordered per
+    // partition on the device (porder_d, HostPartCommon.order). pev[k]: the last launch on stream k;
+    // t->stream's other launches wait for all of them (part_join), and the partitioned launches after
+    // them wait for tev (recorded on t->stream when tev_gen moved past pgen[k])
+    hipStream_t pstreams[kPartStreams] = {};
+    hipEvent_t pev[kPartStreams] = {};
+    uint32_t pgen[kPartStreams] = {};
+    int n_pstreams = 0;
+    bool part_pending = false;
+    uint32_t *porder_d = nullptr;
+    hipEvent_t tev = nullptr;
+    uint32_t tev_gen = 0;
     // the serving kernel (k_hserve): launches are published in a pinned ring instead of launched
     HostRingSlot *ring = nullptr, *ring_d = nullptr;
     uint32_t *srv_words = nullptr, *srv_words_d = nullptr;   // [0] stop, [32..63] exited per workgroup
@@ -244,6 +264,7 @@ static int ensure_batch_scratch(hkv_table *t, int64_t n)
     t->batch_cap = 0;
     HIP_TRY(hipMalloc(&t->d_batch, batch_scratch_bytes(cap, t->geo.entry_size)));
     t->batch_cap = cap;
+    ++t->scratch_gen;
     return 0;
 }
 
@@ -330,9 +351,14 @@ int hkv_table_create(const hkv_config *cfg, hkv_table **out)
     return 0;
 }
 
+static void part_quiesce(hkv_table *t);
+static void part_join(hkv_table *t);
+static void part_mark(hkv_table *t);
+
 int hkv_table_destroy(hkv_table *t)
 {
     if (!t) return 0;
+    part_quiesce(t);
     if (t->stream) hipStreamSynchronize(t->stream);
     hipFree(t->d_index);
     hipFree(t->d_log);
@@ -355,6 +381,12 @@ int hkv_table_destroy(hkv_table *t)
     if (t->ring) hipHostFree(t->ring);
     if (t->srv_words) hipHostFree(t->srv_words);
     if (t->pflags) hipHostFree(t->pflags);
+    for (int k = 0; k < t->n_pstreams; ++k) {
+        hipStreamDestroy(t->pstreams[k]);
+        hipEventDestroy(t->pev[k]);
+    }
+    if (t->tev) hipEventDestroy(t->tev);
+    hipFree(t->porder_d);
     if (t->stream) hipStreamDestroy(t->stream);
     delete t;
     return 0;
@@ -428,6 +460,7 @@ int hkv_table_populate(hkv_table *t, int64_t n, int val_len)
     uint64_t final_head;
     pl.h0 = t->geo.log_head;
     plan_log(t->geo.log_head, t->geo.log_cap, t->geo.entry_size, t->geo.kvs_value, (uint64_t)n, pl.k, pl.hw, final_head);
+    part_quiesce(t);
     int rc = launch_populate(pl, t->stream);
     hipError_t se = hipStreamSynchronize(t->stream);
     release();
@@ -520,12 +553,34 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.fx = t->d_fw + batch_fw_words(t->cfg.log_cap);
     bl.fy = bl.fx + batch_fw_words(t->cfg.log_cap);
     bl.ft = bl.fy + batch_fw_words(t->cfg.log_cap);
-    if (++t->epoch > batch_max_epoch()) {  // round tags would wrap: start the F and T words over
-        HIP_TRY(hipMemsetAsync(t->d_fw, 0xFF, 8 * batch_fw_words(t->cfg.log_cap), s));
-        HIP_TRY(hipMemsetAsync(bl.ft, 0, 64 * batch_fw_words(t->cfg.log_cap), s));
-        t->epoch = 1;
+    const int stage = (d->flags & HKV_BATCH_PREPASS_CANCEL) ? 3 : (d->flags & HKV_BATCH_PREPASSED) ? 2
+                    : (d->flags & HKV_BATCH_PREPASS) ? 1 : 0;
+    if (stage && d->type != kLocal) return fail(-1, "HKV_BATCH_PREPASS/PREPASSED apply to local batches");
+    bool force_engine = false;
+    if (t->pre.valid && stage < 2) {
+        // between a prepass and the rest of its launch only VAL batches may run, on the engine's one-pass
+        // VAL lookup, which stores the state byte alone (the single-workgroup kernel writes whole metas
+        // back, and with them the seqlock bytes the prepass tagged)
+        if (d->type != kVals) return fail(-1, "a local launch's prepass is pending: finish or cancel it first");
+        force_engine = true;
     }
-    bl.epoch = t->epoch;
+    if (stage >= 2) {   // the rest of a launch whose prepass ran: its epoch (tags, F words), no new one
+        if (!t->pre.valid || t->pre.n != n || t->pre.elems != d->d_elems)
+            return fail(-1, "HKV_BATCH_PREPASSED without the matching HKV_BATCH_PREPASS launch");
+        t->pre.valid = false;
+        bl.epoch = t->pre.epoch;
+        bl.pre_done = t->pre.done;
+        bl.reset_defer = t->pre.scratch_gen != t->scratch_gen;
+    } else {
+        if (++t->epoch > batch_max_epoch()) {  // round tags would wrap: start the F and T words over
+            HIP_TRY(hipMemsetAsync(t->d_fw, 0xFF, 8 * batch_fw_words(t->cfg.log_cap), s));
+            HIP_TRY(hipMemsetAsync(bl.ft, 0, 64 * batch_fw_words(t->cfg.log_cap), s));
+            t->epoch = 1;
+            t->pre.valid = false;   // a pending prepass's offers are gone: its second call fails
+        }
+        bl.epoch = t->epoch;
+    }
+    bl.stage = stage;
     bl.error_flags = t->d_error_flags;
     bl.n = n;
     bl.n_batches = d->n_batches;
@@ -537,6 +592,7 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.path = (d->flags & HKV_BATCH_ENGINE) || packed ? kPathEngine
             : (d->flags & HKV_BATCH_SMALL) ? kPathSmall : kPathAuto;
     bl.unique = (d->flags & HKV_BATCH_UNIQUE) && (d->type == kInvs || d->type == kAcks) ? 1 : 0;
+    if (force_engine) bl.path = kPathEngine;
     if (d->flags & HKV_BATCH_ROWS) {
         if (!bl.unique || t->geo.entry_size != 64 || t->geo.st_value != 31 || d->elem_size > 64)
             return fail(-1, "HKV_BATCH_ROWS: unique INV or ACK launches of 64-byte entries and elements only");
@@ -552,6 +608,14 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     TRACE("batch_async type=%d n=%lld", d->type, (long long)n);
     rc = launch_batch(bl, s);
     if (rc) return fail(rc, "batch launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));
+    if (stage == 1) {   // launch_batch set pre_done when the launch takes the direct path
+        t->pre.valid = true;
+        t->pre.done = bl.pre_done != 0;
+        t->pre.epoch = bl.epoch;
+        t->pre.scratch_gen = t->scratch_gen;
+        t->pre.n = n;
+        t->pre.elems = d->d_elems;
+    }
     return 0;
 }
 
@@ -560,6 +624,7 @@ int hkv_sync(hkv_table *t, void *stream)
     if (!t) return fail(-1, "null table");
     srv_stop(t);
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    part_quiesce(t);
     HIP_TRY(hipStreamSynchronize(t->stream));
     return 0;
 }
@@ -569,6 +634,7 @@ int hkv_copy_index(hkv_table *t, void *dst, uint64_t off, uint64_t bytes)
     if (!t || !dst) return fail(-1, "null argument");
     if (off + bytes > t->cfg.num_bkts * 64) return fail(-1, "index range out of bounds");
     srv_stop(t);
+    part_quiesce(t);
     HIP_TRY(hipStreamSynchronize(t->stream));
     HIP_TRY(hipMemcpy(dst, t->d_index + off, bytes, hipMemcpyDeviceToHost));
     return 0;
@@ -579,6 +645,7 @@ int hkv_copy_log(hkv_table *t, void *dst, uint64_t off, uint64_t bytes)
     if (!t || !dst) return fail(-1, "null argument");
     if (off + bytes > t->cfg.log_cap + t->geo.entry_size) return fail(-1, "log range out of bounds");
     srv_stop(t);
+    part_quiesce(t);
     HIP_TRY(hipStreamSynchronize(t->stream));
     HIP_TRY(hipMemcpy(dst, t->d_log + off, bytes, hipMemcpyDeviceToHost));
     return 0;
@@ -809,7 +876,9 @@ static void host_launch_mixed(hkv_table *t, HostSet *set, std::unique_lock<std::
         // t->mu orders the launch against hkv_table_populate, which moves geo.log_head
         std::lock_guard<std::mutex> tl(t->mu);
         bl.g = t->geo;
+        part_join(t);
         if (launch_batch(bl, t->stream)) die("hermes_batch_ops_to_KVS (small launch)");
+        part_mark(t);
     }
     lk.lock();
     set->busy = true;
@@ -840,6 +909,29 @@ static void srv_stop_locked(hkv_table *t)
     if (hipEventSynchronize(t->srv_ev) != hipSuccess) die("serving kernel");
     __atomic_store_n(t->srv_words, 0u, __ATOMIC_RELEASE);
     t->srv_running = false;
+}
+
+// Partitioned launches go round t->pstreams; every other launch of the host API runs on t->stream.
+// part_join: t->stream waits for the partitioned launches so far; part_mark: the partitioned launches
+// after this point wait for what t->stream holds now (called after a launch on t->stream).
+static void part_join(hkv_table *t)
+{
+    if (!t->part_pending) return;
+    for (int k = 0; k < t->n_pstreams; ++k)
+        if (hipStreamWaitEvent(t->stream, t->pev[k], 0) != hipSuccess) die("stream wait");
+    t->part_pending = false;
+}
+
+static void part_mark(hkv_table *t)
+{
+    if (!t->n_pstreams) return;
+    if (hipEventRecord(t->tev, t->stream) != hipSuccess) die("event record");
+    ++t->tev_gen;
+}
+
+static void part_quiesce(hkv_table *t)
+{
+    for (int k = 0; k < t->n_pstreams; ++k) hipStreamSynchronize(t->pstreams[k]);
 }
 
 static void srv_stop(hkv_table *t)
@@ -879,6 +971,7 @@ static void srv_ensure(hkv_table *t)
     for (int g = 0; g < kPartG; ++g) sl.start[g] = __atomic_load_n(t->pflags + g, __ATOMIC_ACQUIRE) + 1;
     __atomic_store_n(t->srv_words, 0u, __ATOMIC_RELEASE);
     if (!t->srv_ev && hipEventCreateWithFlags(&t->srv_ev, hipEventDisableTiming) != hipSuccess) die("event");
+    part_join(t);
     if (launch_host_serve(sl, t->stream) || hipEventRecord(t->srv_ev, t->stream) != hipSuccess) die("serving kernel launch");
     t->srv_running = true;
     TRACE("serving kernel epoch %u", sl.epoch);
@@ -906,8 +999,27 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
     // 1 / 8 / 16 threads with launches, 5.7 / 23.3 / 40.7 M served): a launch's dispatch is not what
     // bounds a call, its PCIe round trips are (descriptor, elements, results: about 2.5 us each)
     static const bool serve = getenv("HKV_HOST_SERVE") && atoi(getenv("HKV_HOST_SERVE")) != 0;
+    // HKV_PART_STREAMS=n (at most kPartStreams): the launches go round n streams, each partition's
+    // launches ordered on the device. Measured, not adopted (round 4): 4 streams ran 8 / 16 caller
+    // threads at 7.9-9.3 / 14.5-15.7 M local ops/s against 20.4-21.0 / 34.9-36.0 M on the one table
+    // stream (1, the default), the same at 1 thread
+    static const int n_streams = serve ? 1 : std::max(1, std::min(kPartStreams, getenv("HKV_PART_STREAMS") ?
+                                                                    atoi(getenv("HKV_PART_STREAMS")) : 1));
     static const int inflight = std::min(kRingN, getenv("HKV_PART_INFLIGHT") ? std::max(1, atoi(getenv("HKV_PART_INFLIGHT")))
-                                                                              : serve ? 4 : 2);
+                                                                              : serve ? 4 : n_streams > 1 ? 2 * n_streams : 2);
+    if (n_streams > 1 && !t->n_pstreams) {
+        for (int k = 0; k < n_streams; ++k)
+            if (hipStreamCreateWithFlags(&t->pstreams[k], hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&t->pev[k], hipEventDisableTiming) != hipSuccess)
+                die("partition streams");
+        if (hipEventCreateWithFlags(&t->tev, hipEventDisableTiming) != hipSuccess ||
+            hipMalloc(&t->porder_d, 4 * kPartG) != hipSuccess || hipMemset(t->porder_d, 0, 4 * kPartG) != hipSuccess)
+            die("partition order words");
+        // the launches so far (t->stream) precede the first partitioned one
+        if (hipEventRecord(t->tev, t->stream) != hipSuccess) die("event record");
+        t->tev_gen = 1;
+        t->n_pstreams = n_streams;
+    }
     if (!t->pflags) {
         if (hipHostMalloc((void **)&t->pflags, 4 * kPartG, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
             hipHostGetDevicePointer((void **)&t->pflags_d, t->pflags, 0) != hipSuccess)
@@ -982,7 +1094,20 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
         {
             std::lock_guard<std::mutex> tl(t->mu);   // against hkv_table_populate (geo.log_head)
             pl.c.g = t->geo;
-            if (launch_host_part(pl, t->stream)) die("hermes_batch_ops_to_KVS (partitioned launch)");
+            if (t->n_pstreams) {   // round the streams; each partition's launches ordered on the device
+                const int k = (int)(seq % (uint32_t)t->n_pstreams);
+                hipStream_t ps = t->pstreams[k];
+                if (t->pgen[k] != t->tev_gen) {
+                    if (hipStreamWaitEvent(ps, t->tev, 0) != hipSuccess) die("stream wait");
+                    t->pgen[k] = t->tev_gen;
+                }
+                pl.c.order = t->porder_d;
+                if (launch_host_part(pl, ps)) die("hermes_batch_ops_to_KVS (partitioned launch)");
+                if (hipEventRecord(t->pev[k], ps) != hipSuccess) die("event record");
+                t->part_pending = true;
+            } else if (launch_host_part(pl, t->stream)) {
+                die("hermes_batch_ops_to_KVS (partitioned launch)");
+            }
         }
         lk.lock();
     }
@@ -1121,6 +1246,7 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
     }
     hipStream_t s = t->stream;
     set->mode = kModeEvent;
+    part_join(t);
     if (hipMemcpyAsync(set->d, set->h, total, hipMemcpyHostToDevice, s) != hipSuccess) die("copy in");
     hkv_batch_desc d;
     memset(&d, 0, sizeof d);
@@ -1142,6 +1268,7 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
     }
     if (hipMemcpyAsync(set->h, set->d, total, hipMemcpyDeviceToHost, s) != hipSuccess) die("copy out");
     if (hipEventRecord(set->ev, s) != hipSuccess) die("event record");
+    part_mark(t);
     lk.lock();
     set->busy = true;
     set->refs = nb;

@@ -87,6 +87,9 @@ BATCH_SMALL = 2    # the single-workgroup kernel (launches of at most 4096 eleme
 BATCH_PACKED = 4   # INV / VAL batches back to back, d_counts = n_batches + 1 offsets
 BATCH_UNIQUE = 8   # no key twice in the launch (INV batches: one pass)
 BATCH_ROWS = 16    # with BATCH_UNIQUE: rows of one layout, element j of every row on one key
+BATCH_PREPASS = 32     # a local launch's prepass only (its own stream; see include/hermeskv.h)
+BATCH_PREPASSED = 64   # the rest of that launch
+BATCH_PREPASS_CANCEL = 128   # or: that launch will not run (its prepass's tags undone)
 
 
 class HermesKV:
@@ -172,7 +175,7 @@ class HermesKV:
               state_out: torch.Tensor | None = None, opcode_in: torch.Tensor | None = None,
               patch: torch.Tensor | None = None, rw_state: torch.Tensor | None = None,
               unique: bool = False, put_keys: torch.Tensor | None = None,
-              rows: tuple[int, int, int] | None = None) -> None:
+              rows: tuple[int, int, int] | None = None, stage: int = 0) -> None:
         """Apply n_batches batches of one type, concatenated in `elems` (uint8, on the GPU),
         in concatenation order, asynchronously on `stream` (default: torch's current).
         offsets (INV / ACK / VAL batches): the batches stored back to back, batch b at elements
@@ -183,7 +186,9 @@ class HermesKV:
         batches with state_out): the PUT-key mirror (hkv_batch_desc.d_put_keys); state_out must then hold
         every element's state byte on entry too. rows (unique INV / ACK launches): (n_rows, row_stride,
         skip_row) -- n_rows launches of this layout, row r at element r * row_stride of elems, applied in
-        row order in one pass (HKV_BATCH_ROWS; skip_row -1: none)."""
+        row order in one pass (HKV_BATCH_ROWS; skip_row -1: none). stage (local batches): 1 runs only the
+        launch's prepass (HKV_BATCH_PREPASS), 2 the rest of it (HKV_BATCH_PREPASSED), 3 cancels it
+        (HKV_BATCH_PREPASS_CANCEL), 0 runs all of it."""
         assert elems.is_cuda and elems.dtype == torch.uint8
         total = stride if offsets is not None else n_batches * stride
         if rows is not None:
@@ -197,6 +202,8 @@ class HermesKV:
         d.stride = int(stride)
         d.elem_size = int(elem_size)
         d.flags = self.default_flags | (BATCH_UNIQUE if unique else 0)
+        if stage:
+            d.flags |= {1: BATCH_PREPASS, 2: BATCH_PREPASSED, 3: BATCH_PREPASS_CANCEL}[stage]
         if rows is not None:
             d.flags |= BATCH_ROWS
             d.n_rows, d.row_stride, d.skip_row = int(rows[0]), int(rows[1]), int(rows[2])

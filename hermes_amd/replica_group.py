@@ -93,7 +93,7 @@ class ReplicaRound:
         self.fused = fused_refill and self.op <= 64
         self.patch = torch.zeros(W * LOCAL * 16, **u8) if self.fused else None
         self.put_keys = (torch.zeros(W * LOCAL, dtype=torch.int64, device=dev)
-                         if self.fused and os.environ.get("HKV_PUT_KEYS", "1") != "0" else None)   # d_put_keys
+                         if self.fused and os.environ.get("HKV_PUT_KEYS", "0") == "1" else None)   # d_put_keys
         # outgoing INVs: [W][C] rows, then packed (worker w at inv_off[w]; inv_off[W] = total)
         self.inv_slab = torch.zeros(W * C * self.op, **u8)
         self.inv_count = torch.zeros(W, **i32)           # INVs each worker sends this round

@@ -273,10 +273,12 @@ class Round:
         self.states = torch.zeros(W * S, **u8)   # the local batch's mirror of every op's state byte
         self.opcodes = torch.zeros(W * S, **u8)  # the refill's mirror of every op's opcode byte
         self.patch = torch.zeros(W * S * 16, **u8) if self.fused else None   # planned refills (d_patch)
-        # the PUT-key mirror (d_put_keys) the plan keeps beside the state mirror: the local launch finds its
-        # PUTs from these two dense arrays (HKV_PUT_KEYS=0: from the ops, experiments)
+        # the PUT-key mirror (d_put_keys) the plan keeps beside the state mirror, from which the local launch
+        # could find its PUTs without reading ops (HKV_PUT_KEYS=1). Measured, not adopted (round 4): the
+        # prepass stays at 83 us (its atomics and seqlock tags, not its loads, bound it now) and the mirror
+        # checks cost the fused pass 10-20 us
         self.put_keys = (torch.zeros(W * S, dtype=torch.int64, device=dev)
-                         if self.fused and os.environ.get("HKV_PUT_KEYS", "1") != "0" else None)
+                         if self.fused and os.environ.get("HKV_PUT_KEYS", "0") == "1" else None)
         self.C = slots_per_worker(write_permille, rmw_permille)   # INV send credits per worker
         self.inv_out = torch.zeros(W * self.C * self.op, **u8)
         self.inv_count = torch.zeros(W, dtype=torch.int32, device=dev)
@@ -360,9 +362,11 @@ class Round:
         self.pack_remote = virtual_peers and self.R > 0 and pack_remote
         self.remote_packed = []        # per round index: (INVs, VALs, batch offsets, total, entry offsets)
         # the peers' INVs of a round index also as rows (HKV_BATCH_ROWS), applied in one launch (64-B entries;
-        # HKV_INV_ROWS=0: one launch per peer, experiments)
+        # HKV_INV_ROWS=1). Measured, not adopted (round 4): the rows launch takes what the two per-peer
+        # launches take (70.6 vs 2 x 36 us: each position loads both rows' 56-B elements, holes included)
+        # and the ACK marshal over the rows' holes costs 8 us more
         self.inv_rows = (self.pack_remote and 1 < self.R <= 8 and kvs.sizes.entry == 64 and self.op <= 64
-                         and os.environ.get("HKV_INV_ROWS", "1") != "0")
+                         and os.environ.get("HKV_INV_ROWS", "0") == "1")
         self.remote_rows = []
         self.rows_acks = None          # our ACKs to the rows (marshalled, not read back: the peers are virtual)
         self.drops = []                # peers dropped from the membership (membership_change)
@@ -378,6 +382,17 @@ class Round:
         # Measured slower (1.884 vs 1.907 G ops/s, 3 x 30 steps each), so in line by default.
         self.overlap = os.environ.get("HKV_PEER_OVERLAP", "0") == "1" and self.pack_remote
         self.audit: CommitAudit | None = None   # audit_rounds(): per-outcome commit breakdown (untimed)
+        # the local launch in two stages (HKV_BATCH_PREPASS): the next round's prepass runs on a side
+        # stream right after this round's refill plan, beside this round's VAL batch and the next round's
+        # peer timestamps, which leave every key's PUT-mutability as it was (HKV_PRE_SPLIT=0: in line)
+        self.pre_split = (self.fused and virtual_peers and self.R > 0 and not kvs.rmw and self.op == 56
+                          and kvs.sizes.entry == 64 and val_credits is None
+                          and os.environ.get("HKV_PRE_SPLIT", "1") != "0")
+        self.pre_pending = False
+        if self.pre_split:
+            self.side_pre = torch.cuda.Stream(device=dev)
+            self.ev_plan, self.ev_pre = torch.cuda.Event(), torch.cuda.Event()
+
         if self.overlap:
             self.side = torch.cuda.Stream(device=dev)
             self.tbl_ready, self.pts_done = torch.cuda.Event(), torch.cuda.Event()
@@ -491,9 +506,44 @@ class Round:
         if first:
             init_mirrors(self.ops, self.op, self.states, getattr(self, "put_keys", None))
 
-    def local_batch(self):
+    def _local(self, stage: int, stream=None):
         self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb, state_out=self.states,
-                       opcode_in=self.opcodes, patch=self.patch, put_keys=self.put_keys)
+                       opcode_in=self.opcodes, patch=self.patch, put_keys=self.put_keys, stage=stage, stream=stream)
+
+    def prepass(self, overlap: bool, events: dict | None = None):
+        """Stage 1 of the next local launch: on the side stream after what the current stream holds
+        (overlap), or in line. events: its (start, end) timing pair goes to events["local_pre"]."""
+        if overlap:
+            self.ev_plan.record()
+            self.side_pre.wait_event(self.ev_plan)
+        s = self.side_pre if overlap else torch.cuda.current_stream()
+        if events is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(s)
+        self._local(1, s)
+        if events is not None:
+            ev[1].record(s)
+            events.setdefault("local_pre", []).append(ev)
+        self.ev_pre.record(s)
+        self.pre_pending = True
+
+    def close(self):
+        """A prepass issued for a round that will not run is undone (its tags cleared), so the table is
+        the reference's image again; call before the table serves anything else."""
+        if self.pre_split and self.pre_pending:
+            torch.cuda.current_stream().wait_event(self.ev_pre)
+            self._local(3)
+            self.pre_pending = False
+
+    def local_batch(self):
+        if not self.pre_split:
+            self._local(0)
+            return
+        if not self.pre_pending:
+            self.prepass(overlap=False)
+        torch.cuda.current_stream().wait_event(self.ev_pre)
+        self._local(2)
+        self.pre_pending = False
 
     def marshal_invs(self):
         if self.V is not None:
@@ -651,6 +701,7 @@ class Round:
             events.setdefault(name, []).append((a, b))
 
         k = self.clock % max(len(self.remote_inv), 1)
+        early = False                              # refill and next prepass done before the VAL batch
         if drop is not None:
             assert self.virtual and self.alive and drop == self.peers[self.alive - 1], "drop the last live peer"
         sent = self.alive                          # peers whose INVs this round applies
@@ -670,6 +721,8 @@ class Round:
                 self.peer_timestamps(k, sent)
         if self.audit is not None:
             self.audit.pre_local()
+        if self.pre_split and self.pre_pending:   # the local launch's timing starts after its prepass
+            torch.cuda.current_stream().wait_event(self.ev_pre)
         timed("local", self.local_batch)
         if self.audit is not None:
             self.audit.post_local()
@@ -740,6 +793,13 @@ class Round:
                 self.collect_vals()
             # a dropped peer sent its INVs but fails before its VALs
             vc = self._slot_counts(k, alive)
+            # the round's ops are final: refill plan now, and the next round's prepass beside the VALs
+            early = self.pre_split and drop is None and self.hades is None and not self.overlap
+            if early:
+                if self.audit is not None:
+                    self.audit.end()
+                self.refill()
+                self.prepass(overlap=True, events=events if events is not None and "local" in timed_batches else None)
             if packed:
                 timed("vals", lambda: self.val_batch(pv, self.R * self.W, total, offsets=off))
             else:
@@ -756,9 +816,10 @@ class Round:
             self.membership_change(drop)
         if self.overlap:
             self.tbl_ready.record()
-        if self.audit is not None:
-            self.audit.end()
-        self.refill()
+        if not early:
+            if self.audit is not None:
+                self.audit.end()
+            self.refill()
         self.clock += 1
 
     def _slot_counts(self, k: int, n_peers: int):

@@ -196,6 +196,17 @@ typedef struct hkv_batch_desc {
  * An element whose key differs from its position's raises error flag bit 4. d_node_suspected must be
  * NULL. */
 #define HKV_BATCH_ROWS 16u   /* packed rows: elements past d_counts[n_batches] (<= stride) are in no batch */
+/* A local launch in two calls, so its first stage can overlap other work: HKV_BATCH_PREPASS runs only
+ * the launch's prepass (on the direct path: every PUT that mutates its key offers itself), on its own
+ * stream; a later call with the same descriptor and HKV_BATCH_PREPASSED runs the rest. In between, the
+ * only launches on the table may be VAL batches (they leave every key's PUT-mutability as it was:
+ * VALID or INVALID with an empty op buffer index). Results are those of one launch. The second call
+ * fails if the table saw no matching first call. */
+#define HKV_BATCH_PREPASS 32u
+#define HKV_BATCH_PREPASSED 64u
+/* instead of HKV_BATCH_PREPASSED: the launch will not run; undo what its prepass left in the table
+ * (the seqlock bytes it used as tags), so the table is the reference's image again */
+#define HKV_BATCH_PREPASS_CANCEL 128u
 #define HKV_MAX_ROWS 8
 int  hkv_abi_version(void);
 const char *hkv_last_error(void);

@@ -40,8 +40,8 @@ def test_bench_round_mirrored(theta, workers, cfg3):
     for _ in range(steps):
         r.step()
     torch.cuda.synchronize()
-    # local, the peers' INVs and ACKs as one rows launch each (64-B entries; cfg3: one launch per peer), VAL
-    assert m.launches == steps * (6 if cfg3 else 4)
+    # local, the peers' INVs (one launch per peer), their ACKs (one rows launch; cfg3: one per peer), VAL
+    assert m.launches == steps * (6 if cfg3 else 5)
     st = r.stats()
     assert st["committed"] > 0 and st["writes_completed"] > 0, st
     assert g.take_error_flags() == 0
@@ -78,7 +78,7 @@ def test_retry_round_mirrored(skew, hot):
     for _ in range(steps):
         r.step()
     torch.cuda.synchronize()
-    assert m.launches == steps * 4      # local, the peers' INVs and ACKs (a rows launch each), VAL
+    assert m.launches == steps * 5      # local, the peers' INVs (one launch each), their ACKs (one rows launch), VAL
     st = r.stats()
     assert st["committed"] > 0 and st["dropped"] == 0, st
     assert g.take_error_flags() == 0
@@ -314,8 +314,8 @@ def test_val_credits_round_mirrored(credits, cfg3):
     for _ in range(steps):
         r.step()
     torch.cuda.synchronize()
-    # local, the peers' INVs (one rows launch; cfg3: one launch per peer), ACK (one packed launch), VAL
-    assert m.launches == steps * (5 if cfg3 else 4)
+    # local, the peers' INVs (one launch per peer), ACK (one packed launch), VAL
+    assert m.launches == steps * 5
     st = r.stats()
     assert g.take_error_flags() == 0
     assert seen["gated"] > 0 and seen["carried_rounds"] > 0, seen

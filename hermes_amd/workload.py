@@ -382,12 +382,14 @@ class Round:
         # Measured slower (1.884 vs 1.907 G ops/s, 3 x 30 steps each), so in line by default.
         self.overlap = os.environ.get("HKV_PEER_OVERLAP", "0") == "1" and self.pack_remote
         self.audit: CommitAudit | None = None   # audit_rounds(): per-outcome commit breakdown (untimed)
-        # the local launch in two stages (HKV_BATCH_PREPASS): the next round's prepass runs on a side
-        # stream right after this round's refill plan, beside this round's VAL batch and the next round's
-        # peer timestamps, which leave every key's PUT-mutability as it was (HKV_PRE_SPLIT=0: in line)
+        # the local launch in two stages (HKV_BATCH_PREPASS, HKV_PRE_SPLIT=1): the next round's prepass runs
+        # on a side stream right after this round's refill plan, beside this round's VAL batch and the next
+        # round's peer timestamps, which leave every key's PUT-mutability as it was. Measured, not adopted
+        # (round 4): 3.99-4.00 G against 4.04-4.07 G ops/s in line -- beside the VAL batch the prepass takes
+        # 120 us instead of 80 (both are random-access bound), and the local launch waits for it anyway
         self.pre_split = (self.fused and virtual_peers and self.R > 0 and not kvs.rmw and self.op == 56
                           and kvs.sizes.entry == 64 and val_credits is None
-                          and os.environ.get("HKV_PRE_SPLIT", "1") != "0")
+                          and os.environ.get("HKV_PRE_SPLIT", "0") == "1")
         self.pre_pending = False
         if self.pre_split:
             self.side_pre = torch.cuda.Stream(device=dev)

@@ -106,6 +106,8 @@ struct BatchArgs {
     int32_t pre_patch_first;     // k_local_pre reads a PUT's header only when it has no patch (HKV_PRE_PATCH_FIRST)
     int32_t wave_copy;           // big values copied a wave per value (HKV_WAVE_COPY=0: by their own lane)
     int32_t cancel;              // k_local_pre undoes its tags (HKV_BATCH_PREPASS_CANCEL)
+    uint8_t *ack_out;            // INV launches: each element's ACK (hkv_batch_desc.d_ack_out), or NULL
+    uint32_t ack_out_size;
 };
 
 // Rounds after round 0 per batch type: how often a hot key usually mutates in one launch beyond
@@ -1676,7 +1678,30 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
 #pragma unroll
     for (int k = 0; k < kLookupPair; ++k) {
         if (!live[k]) continue;
-        const uint4 w = sops[te[k] * 4 + q];
+        uint4 w = sops[te[k] * 4 + q];
+        if (TYPE == kInvs && a.ack_out) {
+            // the ACK callbacks (ack_skip_or_get_sender_id, ack_copy_and_modify_elem,
+            // ack_modify_elem_after_send; the k_marshal_acks of hkv_workload.hip) on the element as the
+            // batch left it: the header chunk is lane 0's, the INV leaves as ST_EMPTY once answered
+            uint8_t *y = a.ack_out + (i0 + te[k]) * a.ack_out_size;
+            const uint32_t hz = sops[te[k] * 4].z;
+            const uint8_t oc = (uint8_t)hz;
+            const bool full = oc == kOpInvAbort && a.ack_out_size >= (uint32_t)a.esz;
+            if (oc == kInvSuccess || full) {
+                uint4 c = w;
+                if (q == 0)
+                    c.z = (hz & ~0xFFFFu) | (oc == kInvSuccess ? kOpAck : kOpInvAbort) |
+                          ((uint32_t)(uint8_t)a.g.machine_id << 8);
+                if (q == 0 || (full && 16 * q < a.esz)) {
+                    if (16 * q + 16 <= a.esz || q == 0) *reinterpret_cast<uint4 *>(y + 16 * q) = c;
+                    else *reinterpret_cast<uint64_t *>(y + 16 * q) = (uint64_t)c.x | ((uint64_t)c.y << 32);
+                }
+            } else if (q == 0) {
+                y[8] = kEmpty;
+            }
+            if (q == 0 && (oc == kInvSuccess || oc == kOpInvAbort || oc == kOpMembChange))
+                w.z = (w.z & ~0xFFu) | kEmpty;
+        }
         if (!chunk_equal(w, op[k])) {
             uint8_t *xg = a.elems + (i0 + te[k]) * a.esz + 16 * q;
             if (16 * q + 16 <= a.esz) *reinterpret_cast<uint4 *>(xg) = w;
@@ -2869,7 +2894,8 @@ __device__ void hp_partition(const HostPartCommon &p, HpLds &L, int g, int nb, u
     for (int w = tid; w < L.wbase[nb]; w += kHpThreads) {
         const int l = hp_batch_of(L.wbase, nb, w);
         const int per = L.bh[l].esz / 8, wi = w - L.wbase[l];
-        unsigned long long *d = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(L.bh[l].elems) +
+        const uint64_t ob = L.bh[l].out ? L.bh[l].out : L.bh[l].elems;
+        unsigned long long *d = reinterpret_cast<unsigned long long *>(reinterpret_cast<uint8_t *>(ob) +
                                                                        (int64_t)L.lo[l] * L.bh[l].esz) + wi;
         __hip_atomic_store(d, (unsigned long long)reinterpret_cast<const uint64_t *>(L.sel)[(L.base[l] + wi / per) * 8 + wi % per],
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -3086,6 +3112,8 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.patch = nullptr;
     a.pkeys = nullptr;
     a.cancel = bl.stage == 3;
+    a.ack_out = bl.type == kInvs ? bl.ack_out : nullptr;
+    a.ack_out_size = bl.ack_out_size;
     a.n_rows = bl.n_rows;
     a.skip_row = bl.skip_row;
     a.row_stride = bl.row_stride;
@@ -3227,6 +3255,8 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     } while (0)
         // 64-B entries: the LDS-staged pass (HKV_UNIQUE_LDS=0: the in-place one, experiments)
         static const bool ulds_env = !getenv("HKV_UNIQUE_LDS") || atoi(getenv("HKV_UNIQUE_LDS")) != 0;
+        if (a.ack_out && !(ulds_env && bl.g.st_value == 31 && bl.g.entry_size == 64 && bl.esz <= 64))
+            return -1;   // only the LDS-staged pass writes the ACKs
         if (ulds_env && bl.g.st_value == 31 && bl.g.entry_size == 64 && bl.esz <= 64) {
             const unsigned lgrid = (unsigned)((n + kLfElems - 1) / kLfElems);
             if (bl.type == kInvs) hipLaunchKernelGGL(k_unique_lds<kInvs>, dim3(lgrid), dim3(64), 0, s, a);

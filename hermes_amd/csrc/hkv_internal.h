@@ -50,6 +50,8 @@ struct BatchLaunch {
     int32_t reset_defer;                      // stage 2: the scratch moved since stage 1 (zero its counter)
     int32_t unique;                           // HKV_BATCH_UNIQUE: no key twice in the launch
     int32_t n_rows, skip_row;                 // HKV_BATCH_ROWS (n_rows 0: a plain launch)
+    uint8_t *ack_out;                         // INV launches: the ACK marshal's output (hkv_batch_desc.d_ack_out)
+    uint32_t ack_out_size;
     int64_t row_stride;
     // small launches staged in host memory (the combining submit of hermes_batch_ops_to_KVS): the
     // kernel first copies region_bytes from host_src to dev_region (where elems, counts, rw and
@@ -95,7 +97,7 @@ struct HostPartHdr {
     uint64_t rw;      // ACK batches: device address of the read_write_ops copy, else 0
     int32_t type, count, esz;
     uint8_t g_membership, w_ack_init, pad0, pad1;
-    uint64_t pad2;
+    uint64_t out;     // device address the results go to (pinned), or 0: back into elems
 };
 static_assert(sizeof(HostPartHdr) == 48, "HostPartHdr is three 16-byte loads");
 struct HostPartCommon {

@@ -68,12 +68,19 @@ struct HostSet {
 struct CallerStage {
     uint8_t *h = nullptr, *d = nullptr;
     size_t cap = 0;
+    // HKV_STAGE_VRAM=1: elements and positions written by the caller's CPU straight into
+    // fine-grained device memory (through the BAR), so k_hpart reads them from HBM instead of over
+    // PCIe; the results still come back to the pinned buffer h
+    uint8_t *v = nullptr;
+    size_t vcap = 0;
+    std::vector<uint8_t> tmp;
     std::vector<uint32_t> perm;   // element i of the caller's batch sits at staged slot perm[i]
     // a caller returns only after its launch's flags arrived, so nothing reads the staging when
     // its thread exits: threads that come and go do not leak pinned memory
     ~CallerStage()
     {
         if (h) (void)hipHostFree(h);
+        if (v) (void)hipFree(v);
     }
 };
 static thread_local CallerStage t_stage;
@@ -92,7 +99,7 @@ struct HostReq {
     // partitioned: staged in the caller's t_stage (device addresses), partition g at [poff[g], poff[g+1])
     bool part = false;
     uint32_t pseq = 0;     // launched as partitioned launch pseq (0: in a set's launch)
-    uint64_t st_elems = 0, st_pos = 0, st_rw = 0;
+    uint64_t st_elems = 0, st_pos = 0, st_rw = 0, st_out = 0;
     uint16_t poff[kPartG + 1];
 };
 
@@ -593,6 +600,14 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
             : (d->flags & HKV_BATCH_SMALL) ? kPathSmall : kPathAuto;
     bl.unique = (d->flags & HKV_BATCH_UNIQUE) && (d->type == kInvs || d->type == kAcks) ? 1 : 0;
     if (force_engine) bl.path = kPathEngine;
+    if (d->d_ack_out) {
+        if (d->type != kInvs || !bl.unique || d->n_rows > 1 || t->geo.entry_size != 64 || t->geo.st_value != 31 ||
+            d->elem_size > 64 || d->ack_out_size < 16 || (d->ack_out_size & 7) || ((uintptr_t)d->d_ack_out & 7))
+            return fail(-1, "d_ack_out: unique INV launches of 64-byte entries and elements, 16-byte ACKs or larger");
+        bl.ack_out = d->d_ack_out;
+        bl.ack_out_size = d->ack_out_size;
+        bl.path = kPathEngine;
+    }
     if (d->flags & HKV_BATCH_ROWS) {
         if (!bl.unique || t->geo.entry_size != 64 || t->geo.st_value != 31 || d->elem_size > 64)
             return fail(-1, "HKV_BATCH_ROWS: unique INV or ACK launches of 64-byte entries and elements only");
@@ -1066,6 +1081,7 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
         HostPartHdr &h = pl.hdr[b];
         h.elems = r->st_elems;
         h.pos = r->st_pos;
+        h.out = r->st_out;
         h.rw = r->st_rw;
         h.type = r->type;
         h.count = r->n;
@@ -1144,21 +1160,41 @@ static bool host_stage_part(const hkv_table *t, HostReq &r)
             die("caller staging alloc");
         st.cap = cap;
     }
+    static const bool vram = getenv("HKV_STAGE_VRAM") && atoi(getenv("HKV_STAGE_VRAM")) != 0;
+    if (vram && ebytes + pbytes > st.vcap) {
+        if (st.v) (void)hipFree(st.v);
+        st.v = nullptr;
+        const size_t cap = std::max(ebytes + pbytes, (size_t)1 << 20);
+        if (hipExtMallocWithFlags((void **)&st.v, cap, hipDeviceMallocFinegrained) != hipSuccess) die("caller VRAM staging alloc");
+        st.vcap = cap;
+    }
     if ((int)st.perm.size() < r.n) st.perm.resize(r.n);
     uint16_t cur[kPartG];
     for (int g = 0; g < kPartG; ++g) cur[g] = r.poff[g];
-    uint16_t *pos = reinterpret_cast<uint16_t *>(st.h + ebytes);
+    // built in a host buffer first when it goes to VRAM: one sequential copy, whole write-combined lines
+    if (vram && st.tmp.size() < ebytes + pbytes) st.tmp.resize(ebytes + pbytes);
+    uint8_t *sb = vram ? st.tmp.data() : st.h;
+    uint16_t *pos = reinterpret_cast<uint16_t *>(sb + ebytes);
     for (int i = 0; i < r.n; ++i) {
         const uint8_t *x = r.ops + (size_t)i * r.esz;
         const uint32_t slot = cur[part_of(*reinterpret_cast<const uint64_t *>(x))]++;
-        memcpy(st.h + (size_t)slot * r.esz, x, r.esz);
+        memcpy(sb + (size_t)slot * r.esz, x, r.esz);
         pos[slot] = (uint16_t)i;
         st.perm[i] = slot;
     }
     if (rw_bytes) memcpy(st.h + ebytes + pbytes, r.rw, rw_bytes);
     r.rw_bytes = rw_bytes;
-    r.st_elems = (uint64_t)(uintptr_t)st.d;
-    r.st_pos = (uint64_t)(uintptr_t)(st.d + ebytes);
+    if (vram) {
+        memcpy(st.v, sb, ebytes + pbytes);
+        __builtin_ia32_sfence();   // the write-combined stores leave before the launch that reads them
+        r.st_elems = (uint64_t)(uintptr_t)st.v;
+        r.st_pos = (uint64_t)(uintptr_t)(st.v + ebytes);
+        r.st_out = (uint64_t)(uintptr_t)st.d;
+    } else {
+        r.st_elems = (uint64_t)(uintptr_t)st.d;
+        r.st_pos = (uint64_t)(uintptr_t)(st.d + ebytes);
+        r.st_out = 0;
+    }
     r.st_rw = rw_bytes ? (uint64_t)(uintptr_t)(st.d + ebytes + pbytes) : 0;
     r.rw_off = ebytes + pbytes;
     r.part = true;

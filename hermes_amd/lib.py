@@ -40,7 +40,7 @@ class HkvBatchDesc(ctypes.Structure):
                 ("membership", ctypes.c_uint8 * 8), ("d_state_out", ctypes.c_void_p),
                 ("d_opcode_in", ctypes.c_void_p), ("d_patch", ctypes.c_void_p), ("d_rw_state", ctypes.c_void_p),
                 ("d_put_keys", ctypes.c_void_p), ("n_rows", ctypes.c_int32), ("skip_row", ctypes.c_int32),
-                ("row_stride", ctypes.c_int64)]
+                ("row_stride", ctypes.c_int64), ("d_ack_out", ctypes.c_void_p), ("ack_out_size", ctypes.c_uint32)]
 
 
 class Membership(ctypes.Structure):

@@ -369,6 +369,10 @@ class Round:
                          and os.environ.get("HKV_INV_ROWS", "0") == "1")
         self.remote_rows = []
         self.rows_acks = None          # our ACKs to the rows (marshalled, not read back: the peers are virtual)
+        # our ACKs to each peer's INVs written by that peer's INV launch itself (hkv_batch_desc.d_ack_out)
+        # instead of a marshal pass over the applied INVs (HKV_FUSED_ACKS=0: the pass, experiments)
+        self.fused_acks = (self.pack_remote and kvs.sizes.entry == 64 and self.op <= 64
+                           and os.environ.get("HKV_FUSED_ACKS", "1") != "0")
         self.drops = []                # peers dropped from the membership (membership_change)
         self.alive = self.R            # live peers: the first `alive` slots of the remote slabs
         self._counts = {}
@@ -606,7 +610,11 @@ class Round:
         pi, _, _, _, _, per_peer = self.remote_packed[k]
         for base, n, off in per_peer:
             if n:
-                self.inv_batch(pi[base * self.op:], self.W, n, offsets=off, unique=True)
+                if self.fused_acks and not self.inv_rows:
+                    self.kvs.batch(L.BatchType.invs, pi[base * self.op:], self.W, n, self.op, self.mb, offsets=off,
+                                   unique=True, ack_out=self.ack_out[base * self.ack_size:], ack_out_size=self.ack_size)
+                else:
+                    self.inv_batch(pi[base * self.op:], self.W, n, offsets=off, unique=True)
 
     def marshal_acks(self, invs: torch.Tensor, n: int, out: torch.Tensor):
         check(_L.hkv_wl_marshal_acks(_ptr(invs), n, self.op, _ptr(out), self.ack_size, self.machine_id, _s()),
@@ -755,7 +763,7 @@ class Round:
                 if self.inv_rows:   # our ACKs to the rows (holes answer nothing)
                     rows, P, _, _ = self.remote_rows[k]
                     self.marshal_acks(rows, self.R * P, self.rows_acks)
-                else:
+                elif not self.fused_acks:   # (else the INV launches wrote them)
                     self.marshal_acks(pi, total, self.ack_out)
             else:
                 timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride, counts=ic))

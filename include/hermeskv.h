@@ -160,6 +160,13 @@ typedef struct hkv_batch_desc {
     int32_t  n_rows;            /* HKV_BATCH_ROWS: rows of elements, applied row after row (ABI 6) */
     int32_t  skip_row;          /* HKV_BATCH_ROWS: a row that is not applied (-1: none) */
     int64_t  row_stride;        /* HKV_BATCH_ROWS: elements from one row to the next in d_elems */
+    uint8_t *d_ack_out;         /* INV launches with HKV_BATCH_UNIQUE, 64-byte entries: element i's answer, as the
+                                   worker's ACK callbacks make it (hermes_worker.c:69-118: an ACK from this
+                                   machine for INV_SUCCESS, the element itself as INV-abort when ack_out_size holds
+                                   it, else opcode ST_EMPTY), written to d_ack_out + i * ack_out_size by the launch
+                                   itself; the elements keep the batch's output (the callbacks' after-send reset of
+                                   their opcode is the caller's). NULL = none (ABI 6) */
+    uint32_t ack_out_size;
 } hkv_batch_desc;
 #define HKV_NO_PUT 0xFFFFFFFFFFFFFFFFull
 

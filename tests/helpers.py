@@ -75,6 +75,31 @@ def run_known_answers(engine, keys: np.ndarray):
     assert (miss["state"] == int(L.Resp.MISS)).all()
 
 
+def ack_callbacks(invs, ack_size, machine_id):
+    """The worker's ACK callbacks (src/hermes/hermes_worker.c:69-118) on INV elements after their
+    batch: (ACKs [n][ack_size], ST_EMPTY at byte 8 where none is sent; the INVs after send).
+    INV_SUCCESS answers with its header as ST_OP_ACK from this machine, OP_INV_ABORT with the whole
+    element when the ACK slot holds it; INV_SUCCESS, INV_ABORT and membership-change INVs become
+    ST_EMPTY."""
+    n, esz = invs.shape
+    oc = invs[:, 8]
+    acks = np.zeros((n, ack_size), np.uint8)
+    acks[:, 8] = int(L.Bucket.EMPTY)
+    ok = oc == int(L.Resp.INV_SUCCESS)
+    acks[ok, :16] = invs[ok, :16]
+    acks[ok, 8] = int(L.Op.ACK)
+    if ack_size >= esz:
+        ab = oc == int(L.Resp.OP_INV_ABORT)
+        acks[ab, :esz] = invs[ab]
+        acks[ab, 8] = int(L.Resp.OP_INV_ABORT)
+        ok = ok | ab
+    acks[ok, 9] = machine_id
+    after = invs.copy()
+    done = np.isin(oc, [int(L.Resp.INV_SUCCESS), int(L.Resp.OP_INV_ABORT), int(L.Op.MEMBERSHIP_CHANGE)])
+    after[done, 8] = int(L.Bucket.EMPTY)
+    return acks, after
+
+
 class Mirror:
     """Runs every batch launch of a device table on an oracle twin and compares."""
 
@@ -96,7 +121,8 @@ class Mirror:
 
     def batch(self, btype, elems, n_batches, stride, elem_size, membership, counts=None, rw=None,
               rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None, state_out=None, opcode_in=None,
-              patch=None, rw_state=None, unique=False, put_keys=None, rows=None, stage=0):
+              patch=None, rw_state=None, unique=False, put_keys=None, rows=None, stage=0, ack_out=None,
+              ack_out_size=16):
         import torch
         if stage in (1, 3):   # a prepass (or its cancellation) changes no element and nothing of the meta
             self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
@@ -112,7 +138,7 @@ class Mirror:
                               rw_stride_bytes, rw_state, rows)
         if offsets is not None:
             return self._packed(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
-                                rw_stride_bytes, rw_state, unique)
+                                rw_stride_bytes, rw_state, unique, ack_out, ack_out_size)
         torch.cuda.synchronize()
         n = n_batches * stride * elem_size
         vt = np.dtype((np.void, elem_size))
@@ -259,7 +285,7 @@ class Mirror:
         self.launches += 1
 
     def _packed(self, btype, elems, n_batches, total, elem_size, membership, offsets, stream, rw=None,
-                rw_stride_bytes=0, rw_state=None, unique=False):
+                rw_stride_bytes=0, rw_state=None, unique=False, ack_out=None, ack_out_size=16):
         """A packed (HKV_BATCH_PACKED) INV / ACK / VAL launch: the oracle applies the same batches
         laid out in rows; the device's packed output must equal the oracle's rows packed again."""
         import torch
@@ -277,7 +303,8 @@ class Mirror:
         st_before = rw_in.view(np.uint8).reshape(-1, self.g.sizes.op)[:, 9].copy() if rw is not None else None
         rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
         self._orig(btype, elems, n_batches, total, elem_size, membership, rw=rw, rw_stride_bytes=rw_stride_bytes,
-                   stream=stream, offsets=offsets, rw_state=rw_state, unique=unique)
+                   stream=stream, offsets=offsets, rw_state=rw_state, unique=unique, ack_out=ack_out,
+                   ack_out_size=ack_out_size)
         torch.cuda.synchronize()
         e_in = rows.reshape(-1).view(np.dtype((np.void, elem_size))).copy()
         self.o.batch_multi(int(btype), e_in, n_batches, width, cnt, membership, rw_in,
@@ -287,6 +314,17 @@ class Mirror:
         what = f"{self.name} launch {self.launches} type {int(btype)} (packed)"
         grow = np.zeros_like(rows)
         grow[pos] = got
+        if ack_out is not None:   # the launch also ran the ACK callbacks on its output (d_ack_out)
+            grow[pos] = want
+            want = want.copy()
+            got_acks = ack_out[: total * ack_out_size].cpu().numpy().reshape(total, ack_out_size)
+            want_acks, want = ack_callbacks(want, ack_out_size, self.g.machine_id)
+            sent = want_acks[:, 8] != L.Bucket.EMPTY
+            if not (np.array_equal(got_acks[sent], want_acks[sent])
+                    and (got_acks[~sent, 8] == int(L.Bucket.EMPTY)).all()):
+                bad = np.nonzero(((got_acks != want_acks) & sent[:, None]).any(axis=1)
+                                 | (~sent & (got_acks[:, 8] != int(L.Bucket.EMPTY))))[0]
+                pytest.fail(f"{what}: fused ACKs differ at {len(bad)} elements, first {bad[:8]}")
         self._count(btype, "out8", 8, grow.reshape(-1), n_batches, width, elem_size, cnt)
         self._count(btype, "out9", 9, grow.reshape(-1), n_batches, width, elem_size, cnt)
         if not np.array_equal(got, want):

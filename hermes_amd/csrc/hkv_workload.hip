@@ -480,7 +480,10 @@ __device__ __forceinline__ void wave_ranks(const unsigned long long *b, int lane
 // made from the state mirror (one byte per op instead of every op's line); each refilled
 // slot gets a patch (hkv_batch_desc.d_patch) that the next local launch applies as it reads the op,
 // so the op slab is read and written once per round (by that launch) instead of twice.
-// One wave per worker.
+// One wave per WPW workers: all their state loads, then all their trace loads, are in flight
+// together (a wave's work is two dependent loads; with WPW = 2 the 16384 workers of configs[1] fit
+// the chip's 8192 wave slots in one pass instead of two).
+template <int WPW>
 __global__ __launch_bounds__(256) void k_refill_plan_w(uint8_t *states, int32_t n_workers, int32_t stride,
                                                        uint32_t st_value, uint32_t shift, const uint64_t *tkey,
                                                        const uint8_t *top, int32_t tlen, uint32_t *cursor,
@@ -489,64 +492,93 @@ __global__ __launch_bounds__(256) void k_refill_plan_w(uint8_t *states, int32_t 
                                                        uint64_t *put_keys)
 {
     const int lane = threadIdx.x & 63;
-    const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-    if (w >= n_workers) return;
-    const int64_t e0 = (int64_t)w * stride;
-    uint8_t st[4];
+    const int wb = (blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * WPW;
+    if (wb >= n_workers) return;
+    uint8_t st[WPW][4];
+    uint32_t base[WPW];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) st[r] = r * 64 + lane < stride ? states[e0 + r * 64 + lane] : 0;
-    const uint32_t base = cursor[w];
-    unsigned long long bd[4];
-    int c = 0, m = 0, wr = 0, dr = 0, ab = 0;
+    for (int v = 0; v < WPW; ++v) {
+        const bool wl = wb + v < n_workers;
+        const int64_t e0 = (int64_t)(wb + v) * stride;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const bool live = r * 64 + lane < stride;
-        const bool complete = is_complete(st[r]);
-        const bool drop = live && (flags & HKV_WL_REFILL_ALL) && !complete && !in_flight(st[r]);
-        bd[r] = __ballot(live && (complete || drop));
-        c += __popcll(__ballot(live && complete && st[r] != kMiss && st[r] != kRmwAbort));
-        m += __popcll(__ballot(live && st[r] == kMiss));
-        wr += __popcll(__ballot(live && st[r] == kPutComplete));
-        dr += __popcll(__ballot(drop));
-        ab += __popcll(__ballot(live && st[r] == kRmwAbort));
+        for (int r = 0; r < 4; ++r) st[v][r] = wl && r * 64 + lane < stride ? states[e0 + r * 64 + lane] : 0;
+        base[v] = wl ? cursor[wb + v] : 0;
     }
-    int rank[4], total;
-    wave_ranks(bd, lane, rank, total);
-    if (lane == 0) {
-        cursor[w] = (uint32_t)((base + (uint32_t)total) % (uint32_t)tlen);
-        unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + (w % kStripes) * 16;
-        if (c) atomicAdd(&stripe[0], (unsigned long long)c);
-        if (m) atomicAdd(&stripe[1], (unsigned long long)m);
-        if (wr) atomicAdd(&stripe[2], (unsigned long long)wr);
-        if (dr) atomicAdd(&stripe[3], (unsigned long long)dr);
-        if (ab) atomicAdd(&stripe[4], (unsigned long long)ab);
-    }
+    unsigned long long bd[WPW][4];
+    int rank[WPW][4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int i = r * 64 + lane;
-        if (i >= stride) continue;
-        const int64_t e = e0 + i;
-        W16 p{0, 0};
-        if ((bd[r] >> lane) & 1ull) {
-            const int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)rank[r]) % (uint32_t)tlen);
-            const uint8_t oc = top[t];
-            const bool get = oc == kOpGet;
-            p.a = tkey[t];
-            p.b = (uint64_t)oc | ((uint64_t)(get ? 0u : (uint8_t)(st_value >> shift)) << 8) |
-                  ((uint64_t)((oc == kOpRmw ? 1u : 0u) | 2u) << 16) |
-                  ((uint64_t)(get ? 0u : (uint8_t)('a' + machine_id)) << 32) |
-                  ((uint64_t)(get && (flags & HKV_WL_READ_TS_RESET) ? 1u : 0u) << 40) | (1ull << 48);
-            opc[e] = oc;
-            if (put_keys) {   // the PUT-key mirror and the entry state of the patched op
-                put_keys[e] = oc == kOpPut ? p.a : HKV_NO_PUT;
-                states[e] = kNew;
-            }
+    for (int v = 0; v < WPW; ++v) {
+        const int w = wb + v;
+        const bool wl = w < n_workers;
+        int c = 0, m = 0, wr = 0, dr = 0, ab = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const bool live = wl && r * 64 + lane < stride;
+            const uint8_t x = st[v][r];
+            const bool complete = is_complete(x);
+            const bool drop = live && (flags & HKV_WL_REFILL_ALL) && !complete && !in_flight(x);
+            bd[v][r] = __ballot(live && (complete || drop));
+            c += __popcll(__ballot(live && complete && x != kMiss && x != kRmwAbort));
+            m += __popcll(__ballot(live && x == kMiss));
+            wr += __popcll(__ballot(live && x == kPutComplete));
+            dr += __popcll(__ballot(drop));
+            ab += __popcll(__ballot(live && x == kRmwAbort));
         }
-        *reinterpret_cast<W16 *>(patch + e * 16) = p;
+        int total;
+        wave_ranks(bd[v], lane, rank[v], total);
+        if (lane == 0 && wl) {
+            cursor[w] = (uint32_t)((base[v] + (uint32_t)total) % (uint32_t)tlen);
+            unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + (w % kStripes) * 16;
+            if (c) atomicAdd(&stripe[0], (unsigned long long)c);
+            if (m) atomicAdd(&stripe[1], (unsigned long long)m);
+            if (wr) atomicAdd(&stripe[2], (unsigned long long)wr);
+            if (dr) atomicAdd(&stripe[3], (unsigned long long)dr);
+            if (ab) atomicAdd(&stripe[4], (unsigned long long)ab);
+        }
+    }
+    uint8_t oc[WPW][4];
+    uint64_t key[WPW][4];
+#pragma unroll
+    for (int v = 0; v < WPW; ++v)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const bool rf = (bd[v][r] >> lane) & 1ull;
+            const int64_t t = (int64_t)(wb + v) * tlen + (int64_t)((base[v] + (uint32_t)rank[v][r]) % (uint32_t)tlen);
+            oc[v][r] = rf ? top[t] : (uint8_t)0;
+            key[v][r] = rf ? tkey[t] : 0ull;
+        }
+#pragma unroll
+    for (int v = 0; v < WPW; ++v) {
+        if (wb + v >= n_workers) break;
+        const int64_t e0 = (int64_t)(wb + v) * stride;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = r * 64 + lane;
+            if (i >= stride) continue;
+            const int64_t e = e0 + i;
+            W16 p{0, 0};
+            if ((bd[v][r] >> lane) & 1ull) {
+                const uint8_t o = oc[v][r];
+                const bool get = o == kOpGet;
+                p.a = key[v][r];
+                p.b = (uint64_t)o | ((uint64_t)(get ? 0u : (uint8_t)(st_value >> shift)) << 8) |
+                      ((uint64_t)((o == kOpRmw ? 1u : 0u) | 2u) << 16) |
+                      ((uint64_t)(get ? 0u : (uint8_t)('a' + machine_id)) << 32) |
+                      ((uint64_t)(get && (flags & HKV_WL_READ_TS_RESET) ? 1u : 0u) << 40) | (1ull << 48);
+                opc[e] = o;
+                if (put_keys) {   // the PUT-key mirror and the entry state of the patched op
+                    put_keys[e] = o == kOpPut ? p.a : HKV_NO_PUT;
+                    states[e] = kNew;
+                }
+            }
+            *reinterpret_cast<W16 *>(patch + e * 16) = p;
+        }
     }
 }
 
-// k_marshal_invs for ops of at most 64 bytes, one wave per worker
+// k_marshal_invs for ops of at most 64 bytes, one wave per WPW workers (their state loads all in
+// flight together, see k_refill_plan_w)
+template <int WPW>
 __global__ __launch_bounds__(256) void k_marshal_invs_w(uint8_t *ops, int32_t n_workers, int32_t stride,
                                                         uint32_t op_size, uint8_t *out, int32_t out_stride,
                                                         int32_t *count, uint32_t machine_id,
@@ -554,45 +586,65 @@ __global__ __launch_bounds__(256) void k_marshal_invs_w(uint8_t *ops, int32_t n_
                                                         int32_t r_alive, uint8_t *states)
 {
     const int lane = threadIdx.x & 63;
-    const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-    if (w >= n_workers) return;
-    const int64_t e0 = (int64_t)w * stride;
-    uint8_t st[4];
+    const int wb = (blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * WPW;
+    if (wb >= n_workers) return;
+    uint8_t st[WPW][4];
+    int aqn[WPW];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int i = r * 64 + lane;
-        st[r] = i < stride ? (states ? states[e0 + i] : ops[(e0 + i) * op_size + 9]) : 0;
-    }
-    unsigned long long bs[4];
+    for (int v = 0; v < WPW; ++v) {
+        const bool wl = wb + v < n_workers;
+        const int64_t e0 = (int64_t)(wb + v) * stride;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-        bs[r] = __ballot(r * 64 + lane < stride &&
-                         (st[r] == kPutSuccess || st[r] == kRmwSuccess || st[r] == kReplaySuccess ||
-                          st[r] == kOpMembChange));
-    int rank[4], total;
-    wave_ranks(bs, lane, rank, total);
-    const int cap = aq_n ? max(0, out_stride - aq_n[w] / max(1, r_alive)) : out_stride;
-    if (lane == 0) {
-        count[w] = total < cap ? total : cap;
-        if (total > cap && held) atomicAdd(held, (unsigned long long)(total - cap));
+        for (int r = 0; r < 4; ++r) {
+            const int i = r * 64 + lane;
+            st[v][r] = wl && i < stride ? (states ? states[e0 + i] : ops[(e0 + i) * op_size + 9]) : 0;
+        }
+        aqn[v] = aq_n && wl ? aq_n[wb + v] : 0;
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        if (!((bs[r] >> lane) & 1ull) || rank[r] >= cap) continue;
-        const int64_t e = e0 + r * 64 + lane;
-        uint8_t *op = ops + e * op_size;
-        uint8_t *dst = out + ((int64_t)w * out_stride + rank[r]) * op_size;
-        const W16 h = *reinterpret_cast<const W16 *>(op);
-        *reinterpret_cast<W16 *>(dst) = W16{h.a, with_op_state(h.b, kOpInv, (uint8_t)machine_id)};
-        uint32_t k = 16;
-        for (; k + 16 <= op_size; k += 16) *reinterpret_cast<W16 *>(dst + k) = *reinterpret_cast<const W16 *>(op + k);
-        if (k < op_size) *reinterpret_cast<uint64_t *>(dst + k) = *reinterpret_cast<const uint64_t *>(op + k);
-        const uint8_t s = st[r];
-        const uint8_t ns = s == kPutSuccess ? kInProgressPut : s == kRmwSuccess ? kInProgressRmw
-                         : s == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
-        op[9] = ns;
-        if (states) states[e] = ns;
+    for (int v = 0; v < WPW; ++v) {
+        const int w = wb + v;
+        if (w >= n_workers) break;
+        const int64_t e0 = (int64_t)w * stride;
+        unsigned long long bs[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint8_t x = st[v][r];
+            bs[r] = __ballot(r * 64 + lane < stride &&
+                             (x == kPutSuccess || x == kRmwSuccess || x == kReplaySuccess || x == kOpMembChange));
+        }
+        int rank[4], total;
+        wave_ranks(bs, lane, rank, total);
+        const int cap = aq_n ? max(0, out_stride - aqn[v] / max(1, r_alive)) : out_stride;
+        if (lane == 0) {
+            count[w] = total < cap ? total : cap;
+            if (total > cap && held) atomicAdd(held, (unsigned long long)(total - cap));
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (!((bs[r] >> lane) & 1ull) || rank[r] >= cap) continue;
+            const int64_t e = e0 + r * 64 + lane;
+            uint8_t *op = ops + e * op_size;
+            uint8_t *dst = out + ((int64_t)w * out_stride + rank[r]) * op_size;
+            const W16 h = *reinterpret_cast<const W16 *>(op);
+            *reinterpret_cast<W16 *>(dst) = W16{h.a, with_op_state(h.b, kOpInv, (uint8_t)machine_id)};
+            uint32_t k = 16;
+            for (; k + 16 <= op_size; k += 16) *reinterpret_cast<W16 *>(dst + k) = *reinterpret_cast<const W16 *>(op + k);
+            if (k < op_size) *reinterpret_cast<uint64_t *>(dst + k) = *reinterpret_cast<const uint64_t *>(op + k);
+            const uint8_t x = st[v][r];
+            const uint8_t ns = x == kPutSuccess ? kInProgressPut : x == kRmwSuccess ? kInProgressRmw
+                             : x == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
+            op[9] = ns;
+            if (states) states[e] = ns;
+        }
     }
+}
+
+// workers per wave of the wave-per-worker workload kernels (HKV_WL_WPW, 1 or 2)
+static int wl_wpw()
+{
+    static const int w = getenv("HKV_WL_WPW") && atoi(getenv("HKV_WL_WPW")) == 1 ? 1 : 2;
+    return w;
 }
 
 // wings_issue_pkts(inv) with the INV callbacks of hermes_worker.c:12-65. At most out_stride
@@ -1501,8 +1553,11 @@ __global__ __launch_bounds__(256) void k_peer_ts_at(TableView t, uint8_t *invs, 
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (g >= total) return;
     uint8_t *x = invs + (inv_at ? inv_at[g] : g) * op_size;
+    // every load that does not need the entry first: INV header, flags, location and the VAL's header
+    uint8_t *vv = vals + g * kOpMetaSize;
     const uint64_t key = *reinterpret_cast<const uint64_t *>(x);
     const uint64_t h8 = *reinterpret_cast<const uint64_t *>(x + 8);
+    const uint64_t vh = *reinterpret_cast<const uint64_t *>(vv + 8);
     const uint8_t peer = (uint8_t)(h8 >> 8);
     const bool rmw = x[16] & 1u;
     uint64_t phys = phys_in[g];
@@ -1534,8 +1589,6 @@ __global__ __launch_bounds__(256) void k_peer_ts_at(TableView t, uint8_t *invs, 
     // bytes 8..15 rewritten whole (opcode, sender, val_len, cid, version): one 8-B store
     const uint64_t nh = (h8 & 0xFFFFFF00ull & 0xFFFFFFFFull) | kOpInv | ((uint64_t)ver << 32);
     *reinterpret_cast<uint64_t *>(x + 8) = nh;
-    uint8_t *vv = vals + g * kOpMetaSize;
-    const uint64_t vh = *reinterpret_cast<const uint64_t *>(vv + 8);
     *reinterpret_cast<uint64_t *>(vv + 8) = (vh & 0xFFFFFF00ull & 0xFFFFFFFFull) | kOpVal | ((uint64_t)ver << 32);
 }
 
@@ -1610,9 +1663,14 @@ int hkv_wl_refill_plan(uint8_t *states, int32_t n_workers, int32_t stride, uint3
     if (stride > 256 || n_workers <= 0 || tlen <= 0 || !states || !opc || !patch) return -1;
     if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET)) return -1;   // no hot-request coalescing
     if (((uintptr_t)patch & 15) || ((uintptr_t)put_keys & 7) || st_value > 255) return -1;
-    hipLaunchKernelGGL(k_refill_plan_w, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
-                       states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
-                       counters, opc, patch, put_keys);
+    if (wl_wpw() == 2)
+        hipLaunchKernelGGL(k_refill_plan_w<2>, dim3((unsigned)((n_workers + 7) / 8)), dim3(256), 0, (hipStream_t)stream,
+                           states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
+                           counters, opc, patch, put_keys);
+    else
+        hipLaunchKernelGGL(k_refill_plan_w<1>, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                           states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
+                           counters, opc, patch, put_keys);
     return ok();
 }
 
@@ -1750,9 +1808,14 @@ int hkv_wl_marshal_invs_cap(uint8_t *ops, int32_t n_workers, int32_t stride, uin
 {
     if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
     if (op_size <= 64)
-        hipLaunchKernelGGL(k_marshal_invs_w, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
-                           ops, n_workers, stride, op_size, out, out_stride, count, machine_id, held,
-                           (const int32_t *)nullptr, 1, states);
+        if (wl_wpw() == 2)
+            hipLaunchKernelGGL(k_marshal_invs_w<2>, dim3((unsigned)((n_workers + 7) / 8)), dim3(256), 0, (hipStream_t)stream,
+                               ops, n_workers, stride, op_size, out, out_stride, count, machine_id, held,
+                               (const int32_t *)nullptr, 1, states);
+        else
+            hipLaunchKernelGGL(k_marshal_invs_w<1>, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                               ops, n_workers, stride, op_size, out, out_stride, count, machine_id, held,
+                               (const int32_t *)nullptr, 1, states);
     else
         hipLaunchKernelGGL(k_marshal_invs, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
                            out, out_stride, count, machine_id, held, (const int32_t *)nullptr, 1, states);
@@ -1765,7 +1828,7 @@ int hkv_wl_marshal_invs_credits(uint8_t *ops, int32_t n_workers, int32_t stride,
 {
     if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
     if (op_size <= 64)
-        hipLaunchKernelGGL(k_marshal_invs_w, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+        hipLaunchKernelGGL(k_marshal_invs_w<1>, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                            ops, n_workers, stride, op_size, out, out_stride, count, machine_id, held, aq_n, r_alive,
                            (uint8_t *)nullptr);
     else

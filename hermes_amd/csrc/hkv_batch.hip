@@ -400,6 +400,7 @@ __device__ __forceinline__ void copy_elem(uint8_t *dst, const uint8_t *src, int3
 
 constexpr int64_t kLookupHead = 8192;
 constexpr int kLookupPair = 2;
+template <int P = kLookupPair>
 __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, int64_t i_end)
 {
     const int q = threadIdx.x & 3;
@@ -410,12 +411,12 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
         a.ctr[kCtrFbL] = 0;
     }
     const bool vals_direct = a.type == kVals;
-    int64_t gi[kLookupPair];
-    uint64_t key[kLookupPair], hdr[kLookupPair];
-    int probe[kLookupPair];
+    int64_t gi[P];
+    uint64_t key[P], hdr[P];
+    int probe[P];
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
-        gi[k] = i_begin + ((int64_t)blockIdx.x * kLookupPair + k) * 64 + (threadIdx.x >> 2);
+    for (int k = 0; k < P; ++k) {
+        gi[k] = i_begin + ((int64_t)blockIdx.x * P + k) * 64 + (threadIdx.x >> 2);
         uint64_t kk = 0, hh = 0;
         int p = 0;
         if (gi[k] < i_end && q == 0) {
@@ -441,21 +442,21 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
         probe[k] = p;
     }
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         const int p = __shfl(probe[k], 0, 4);
         const uint64_t kk = __shfl(key[k], 0, 4);
         probe[k] = p;
         key[k] = kk;
     }
-    uint4 v[kLookupPair];
+    uint4 v[P];
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k)
+    for (int k = 0; k < P; ++k)
         v[k] = probe[k] ? reinterpret_cast<const uint4 *>(a.index + ((key[k] & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u)[q]
                         : make_uint4(0u, 0u, 0u, 0u);
-    uint64_t off[kLookupPair];
-    uint32_t order[kLookupPair];
+    uint64_t off[P];
+    uint32_t order[P];
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         const uint64_t s0 = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
         const uint64_t s1 = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
         const uint32_t tag = (uint32_t)(key[k] >> 48);
@@ -474,18 +475,18 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
     // key and the meta), one access per lane for both elements in flight together; lane 0 gathers.
     // The F word only for a candidate (a dependent load, but one random line less for the ~80 %
     // that never mutate).
-    bool ok[kLookupPair];
-    uint64_t phys[kLookupPair], ekey[kLookupPair];
-    Meta m0[kLookupPair];
-    U64x2 ln[kLookupPair];
+    bool ok[P];
+    uint64_t phys[P], ekey[P];
+    Meta m0[P];
+    U64x2 ln[P];
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         ok[k] = probe[k] && order[k] && a.g.log_head - off[k] < a.g.log_cap;
         phys[k] = off[k] & a.g.log_mask;
         ln[k] = ok[k] ? reinterpret_cast<const U64x2 *>(a.log + phys[k])[q] : U64x2{0, 0};
     }
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         ekey[k] = __shfl(ln[k].b, 0, 4);
         const uint64_t w45 = __shfl(ln[k].a, 1, 4), w67 = __shfl(ln[k].b, 1, 4);
         const uint32_t b32 = (uint32_t)__shfl(ln[k].a, 2, 4) & 0xFFu;
@@ -497,7 +498,7 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
     }
     if (q != 0) return;
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         if (gi[k] >= i_end) continue;
         uint8_t *x = a.elems + gi[k] * a.esz;
         uint32_t e = kNone;
@@ -1593,23 +1594,24 @@ __device__ __forceinline__ bool chunk_equal(const uint4 &a, const uint4 &b)
     return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
 }
 
-template <int TYPE>
+template <int TYPE, int P = kLookupPair>
 __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
 {
-    __shared__ uint4 sops[kLfElems * 4];
-    __shared__ uint4 sln[kLfElems * 4];
-    __shared__ uint32_t sent[kLfElems];
-    __shared__ uint8_t sprb[kLfElems];
+    constexpr int E = 16 * P;   // elements per wave: P per lane group
+    __shared__ uint4 sops[E * 4];
+    __shared__ uint4 sln[E * 4];
+    __shared__ uint32_t sent[E];
+    __shared__ uint8_t sprb[E];
     const int tid = threadIdx.x, q = tid & 3, gbase = tid & ~3;
-    const int64_t i0 = (int64_t)blockIdx.x * kLfElems;
+    const int64_t i0 = (int64_t)blockIdx.x * E;
     const int64_t n_live = a.offsets ? (int64_t)a.offsets[a.n_batches] : a.n;   // packed: past the last offset
-    uint64_t key[kLookupPair];
-    bool probe[kLookupPair], ok[kLookupPair], live[kLookupPair];
-    uint64_t phys[kLookupPair];
-    uint4 ln[kLookupPair], op[kLookupPair];
-    int te[kLookupPair];
+    uint64_t key[P];
+    bool probe[P], ok[P], live[P];
+    uint64_t phys[P];
+    uint4 ln[P], op[P];
+    int te[P];
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         te[k] = k * 16 + (tid >> 2);
         const int64_t i = i0 + te[k];
         live[k] = i < a.n && i < n_live;
@@ -1617,7 +1619,7 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
         sops[te[k] * 4 + q] = op[k];
     }
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         key[k] = (uint64_t)(uint32_t)__shfl((int)op[k].x, 0, 4) | ((uint64_t)(uint32_t)__shfl((int)op[k].y, 0, 4) << 32);
         const uint32_t h0 = (uint32_t)__shfl((int)op[k].z, 0, 4);
         probe[k] = false;
@@ -1632,9 +1634,9 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
             }
         }
     }
-    lookup_pair(a, key, probe, q, gbase, ok, phys, ln);
+    lookup_pair<P>(a, key, probe, q, gbase, ok, phys, ln);
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         Meta m;
         const uint64_t ek = line_key_meta(ln[k], m);
         const bool hit = ok[k] && ek == key[k];
@@ -1645,7 +1647,7 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
         }
     }
     __syncthreads();
-    if (tid < kLfElems && i0 + tid < n_live) {
+    if (tid < E && i0 + tid < n_live) {
         const int64_t i = i0 + tid;
         uint8_t *x = reinterpret_cast<uint8_t *>(&sops[tid * 4]);
         uint8_t *ent = reinterpret_cast<uint8_t *>(&sln[tid * 4]);
@@ -1676,7 +1678,7 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         if (!live[k]) continue;
         uint4 w = sops[te[k] * 4 + q];
         if (TYPE == kInvs && a.ack_out) {
@@ -3258,9 +3260,16 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         if (a.ack_out && !(ulds_env && bl.g.st_value == 31 && bl.g.entry_size == 64 && bl.esz <= 64))
             return -1;   // only the LDS-staged pass writes the ACKs
         if (ulds_env && bl.g.st_value == 31 && bl.g.entry_size == 64 && bl.esz <= 64) {
-            const unsigned lgrid = (unsigned)((n + kLfElems - 1) / kLfElems);
-            if (bl.type == kInvs) hipLaunchKernelGGL(k_unique_lds<kInvs>, dim3(lgrid), dim3(64), 0, s, a);
-            else hipLaunchKernelGGL(k_unique_lds<kAcks>, dim3(lgrid), dim3(64), 0, s, a);
+            // four elements per lane group (HKV_UNIQUE_PAIR4=1): 64 per wave, every lane dispatching one
+            static const bool u4 = getenv("HKV_UNIQUE_PAIR4") && atoi(getenv("HKV_UNIQUE_PAIR4")) != 0;
+            const unsigned lgrid = (unsigned)((n + kLfElems - 1) / kLfElems), lgrid4 = (unsigned)((n + 63) / 64);
+            if (bl.type == kInvs) {
+                if (u4) hipLaunchKernelGGL((k_unique_lds<kInvs, 4>), dim3(lgrid4), dim3(64), 0, s, a);
+                else hipLaunchKernelGGL((k_unique_lds<kInvs>), dim3(lgrid), dim3(64), 0, s, a);
+            } else {
+                if (u4) hipLaunchKernelGGL((k_unique_lds<kAcks, 4>), dim3(lgrid4), dim3(64), 0, s, a);
+                else hipLaunchKernelGGL((k_unique_lds<kAcks>), dim3(lgrid), dim3(64), 0, s, a);
+            }
         } else if (ulds_env && bl.type == kInvs && bl.g.st_value == 287 && bl.g.entry_size == 320 && bl.esz <= 320) {
             // big-object INVs, whose raises copy 287-B values: staged through LDS (cfg3: 460 -> 326 us per
             // round). ACKs touch the header and the meta only, so they stay in place (LDS-staged: 110 -> 191 us)
@@ -3269,7 +3278,10 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         else HKV_UNIQUE(kAcks);
 #undef HKV_UNIQUE
     } else if (bl.type == kVals) {             // one pass (see k_lookup)
-        hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, n);
+        // four elements per lane group (HKV_VAL_PAIR4=1): twice the loads in flight per wave, half the waves
+        static const bool val4 = getenv("HKV_VAL_PAIR4") && atoi(getenv("HKV_VAL_PAIR4")) != 0;
+        if (val4) hipLaunchKernelGGL(k_lookup<4>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, (int64_t)0, n);
+        else hipLaunchKernelGGL(k_lookup<>, dim3((unsigned)((n + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, n);
         return hipGetLastError() == hipSuccess ? 0 : -3;
     } else {
     // The head split pays off where one launch piles many candidates onto a few keys: local
@@ -3277,9 +3289,9 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     // round, so those launches take one pass (their launch-sized head took ~9 us at cfg2).
     const bool split = bl.type == kLocal || bl.type == kLocalAfterMemb;
     const int64_t head = split && n > kLookupHead ? kLookupHead : n;
-    hipLaunchKernelGGL(k_lookup, dim3((unsigned)((head + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, head);
+    hipLaunchKernelGGL(k_lookup<>, dim3((unsigned)((head + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, head);
     if (n > head)
-        hipLaunchKernelGGL(k_lookup, dim3((unsigned)((n - head + kPer - 1) / kPer)), dim3(256), 0, s, a, head, n);
+        hipLaunchKernelGGL(k_lookup<>, dim3((unsigned)((n - head + kPer - 1) / kPer)), dim3(256), 0, s, a, head, n);
     if (a.ack_direct) {
         hipLaunchKernelGGL(k_ack_resolve, dim3(grid), dim3(256), 0, s, a);
     } else if (a.inv_direct) {

@@ -105,6 +105,7 @@ struct BatchArgs {
     int32_t check_unique;        // HKV_CHECK_UNIQUE: HKV_BATCH_UNIQUE launches verify their keys are unique
     int32_t pre_patch_first;     // k_local_pre reads a PUT's header only when it has no patch (HKV_PRE_PATCH_FIRST)
     int32_t wave_copy;           // big values copied a wave per value (HKV_WAVE_COPY=0: by their own lane)
+    int32_t vc_batch;            // values per step of those wave copies (HKV_VC_BATCH, 1 or kVcBatch)
     int32_t cancel;              // k_local_pre undoes its tags (HKV_BATCH_PREPASS_CANCEL)
     uint8_t *ack_out;            // INV launches: each element's ACK (hkv_batch_desc.d_ack_out), or NULL
     uint32_t ack_out_size;
@@ -933,34 +934,57 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
 
 // k_resolve0 for big ops (312 B) in place: one thread per element on its global copy, no LDS, so
 // occupancy is bound by registers instead of by 312 B of LDS per element (local and ACK launches)
-// The value copies the wave's exec calls recorded (Ctx::vc), one value at a time by the whole wave:
-// byte k of a value by lane k % 64, so each instruction moves 64 consecutive bytes. Every lane of the
-// wave calls it.
-__device__ __forceinline__ void wave_value_copies(const VCopy &v, uint32_t n)
+// The value copies the wave's exec calls recorded (Ctx::vc), made by the whole wave: byte k of a
+// value by lane k % 64, so each instruction moves 64 consecutive bytes. kVcBatch values at a time:
+// all their loads are issued before the first store, so a wave waits one memory latency per
+// kVcBatch values instead of one per value (HKV_VC_BATCH=1: one at a time). Every lane of the wave
+// calls it.
+constexpr int kVcBatch = 4;
+template <int VB>
+__device__ __forceinline__ void wave_value_copies_n(const VCopy &v, uint32_t n)
 {
     const int lane = threadIdx.x & 63;
     unsigned long long todo = __ballot(v.dst != nullptr);
     while (todo) {
-        const int j = __ffsll((long long)todo) - 1;
-        todo &= todo - 1;
-        const uint64_t d = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(uintptr_t)v.dst, j, 64) |
-                           ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)v.dst >> 32), j, 64) << 32);
-        const uint64_t s = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(uintptr_t)v.src, j, 64) |
-                           ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)v.src >> 32), j, 64) << 32);
-        uint8_t *dp = reinterpret_cast<uint8_t *>(d);
-        const uint8_t *sp = reinterpret_cast<const uint8_t *>(s);
-        uint8_t b[5];
+        uint8_t *dp[VB];
+        const uint8_t *sp[VB];
 #pragma unroll
-        for (int r = 0; r < 5; ++r) {   // values up to 320 B; all loads before the stores
-            const uint32_t k = (uint32_t)lane + 64u * r;
-            b[r] = k < n ? sp[k] : 0;
+        for (int u = 0; u < VB; ++u) {   // the next VB recorded copies (todo is the same in every lane)
+            dp[u] = nullptr;
+            sp[u] = nullptr;
+            if (todo) {
+                const int j = __ffsll((long long)todo) - 1;
+                todo &= todo - 1;
+                const uint64_t d = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(uintptr_t)v.dst, j, 64) |
+                                   ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)v.dst >> 32), j, 64) << 32);
+                const uint64_t s = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(uintptr_t)v.src, j, 64) |
+                                   ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)v.src >> 32), j, 64) << 32);
+                dp[u] = reinterpret_cast<uint8_t *>(d);
+                sp[u] = reinterpret_cast<const uint8_t *>(s);
+            }
         }
+        uint8_t b[VB][5];
 #pragma unroll
-        for (int r = 0; r < 5; ++r) {
-            const uint32_t k = (uint32_t)lane + 64u * r;
-            if (k < n) dp[k] = b[r];
-        }
+        for (int u = 0; u < VB; ++u)
+#pragma unroll
+            for (int r = 0; r < 5; ++r) {   // values up to 320 B; all loads before the stores
+                const uint32_t k = (uint32_t)lane + 64u * r;
+                b[u][r] = sp[u] && k < n ? sp[u][k] : 0;
+            }
+#pragma unroll
+        for (int u = 0; u < VB; ++u)
+#pragma unroll
+            for (int r = 0; r < 5; ++r) {
+                const uint32_t k = (uint32_t)lane + 64u * r;
+                if (dp[u] && k < n) dp[u][k] = b[u][r];
+            }
     }
+}
+
+__device__ __forceinline__ void wave_value_copies(const VCopy &v, uint32_t n, int batch)
+{
+    if (batch == 1) wave_value_copies_n<1>(v, n);
+    else wave_value_copies_n<kVcBatch>(v, n);
 }
 
 template <int TYPE, int SV>
@@ -1000,7 +1024,7 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
             st = kStPend;
         }
     }
-    if (SV != 31) wave_value_copies(vc, a.g.st_value);
+    if (SV != 31) wave_value_copies(vc, a.g.st_value, a.vc_batch);
     if (!in) return;
     a.st[i] = st;
     note_state(a, i, xg);
@@ -1180,6 +1204,7 @@ __device__ __forceinline__ bool pre_insert(uint64_t *hk, uint32_t *hv, uint64_t 
 // L2-resident after the first block) and drops its keys that have a PUT there -- an earlier block
 // offers that one. Four keys per lane group are in flight; the offer is a plain atomicMin.
 constexpr int kPrePair = 4;
+template <int HEAD = kPreHead>
 __global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
 {
     __shared__ uint64_t hk[kPreHash], gk[kPreHash];  // the block's PUT keys, the head's
@@ -1199,12 +1224,12 @@ __global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
     }
     if (a.dbg & 8) return;
     const int64_t i0 = (int64_t)blockIdx.x * kPreElems;
-    const int64_t head_end = (a.dbg & 4) ? 0 : i0 < kPreHead ? i0 : kPreHead;  // the head: elements before the block's own
+    const int64_t head_end = (a.dbg & 4) ? 0 : i0 < HEAD ? i0 : HEAD;  // the head: elements before the block's own
     // PUTs that are not skipped (hermes_skip_op, hermesKV.c:709-769). Reading every op header is a
     // pass over the whole op slab; with the caller's opcode mirror only the PUTs' headers are read
     // (the others read element 0's, one cached line; k_local_fused checks the mirror against every
     // element's opcode). Loads are unconditional and all issued before the first is used.
-    constexpr int kOwnK = kPreElems / 256, kAllK = kPreElems / 256 + kPreHead / 256;
+    constexpr int kOwnK = kPreElems / 256, kAllK = kPreElems / 256 + HEAD / 256;
     U64x2 h[kAllK];
     bool in[kAllK];
     uint8_t opm[kAllK];
@@ -2010,7 +2035,7 @@ __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
             left = r == a.rounds;
         }
     }
-    if (SV != 31) wave_value_copies(vc, a.g.st_value);
+    if (SV != 31) wave_value_copies(vc, a.g.st_value, a.vc_batch);
     if (r == a.rounds) {  // wave-aggregated append (uniform branch)
         const uint32_t t = agg_ticket(&a.ctr[kCtrFbL], 0u, left);
         if (left) a.fbl[t] = (uint32_t)i;
@@ -3101,6 +3126,17 @@ size_t batch_fw_words(uint64_t log_cap) { return (size_t)(log_cap >> 6); }
 
 uint32_t batch_max_epoch() { return (1u << 29) - 1; }
 
+// k_local_pre with a launch head of HKV_PRE_HEAD elements (1024 default; 512 or 256: fewer loads and
+// LDS inserts per block, later F for hot keys -- experiments)
+static void launch_local_pre(const BatchArgs &a, int64_t n, hipStream_t s)
+{
+    static const int head = getenv("HKV_PRE_HEAD") ? atoi(getenv("HKV_PRE_HEAD")) : kPreHead;
+    const dim3 grid((unsigned)((n + kPreElems - 1) / kPreElems));
+    if (head == 256) hipLaunchKernelGGL(k_local_pre<256>, grid, dim3(256), 0, s, a);
+    else if (head == 512) hipLaunchKernelGGL(k_local_pre<512>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_local_pre<kPreHead>, grid, dim3(256), 0, s, a);
+}
+
 int launch_batch(BatchLaunch &bl, hipStream_t s)
 {
     const int64_t n = bl.n;
@@ -3128,6 +3164,8 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.pre_patch_first = ppf_env;
     static const int wave_copy_env = !getenv("HKV_WAVE_COPY") || atoi(getenv("HKV_WAVE_COPY")) != 0;
     a.wave_copy = wave_copy_env;
+    static const int vc_batch_env = getenv("HKV_VC_BATCH") && atoi(getenv("HKV_VC_BATCH")) == 1 ? 1 : kVcBatch;
+    a.vc_batch = vc_batch_env;
     if (dbg_env) a.error_flags = nullptr;
     a.index = bl.index;
     a.log = bl.log;
@@ -3192,7 +3230,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         if (bl.pre_done) {
             if (bl.patch) a.patch = bl.patch;
             if (bl.put_keys && a.state_out) a.pkeys = bl.put_keys;
-            hipLaunchKernelGGL(k_local_pre, dim3((unsigned)((n + kPreElems - 1) / kPreElems)), dim3(256), 0, s, a);
+            launch_local_pre(a, n, s);
         }
         return hipGetLastError() == hipSuccess ? 0 : -3;
     }
@@ -3200,7 +3238,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         if (local_direct && !small && !patch_apply_env) {
             if (bl.patch) a.patch = bl.patch;
             if (local_direct && bl.put_keys && a.state_out) a.pkeys = bl.put_keys;
-            hipLaunchKernelGGL(k_local_pre, dim3((unsigned)((n + kPreElems - 1) / kPreElems)), dim3(256), 0, s, a);
+            launch_local_pre(a, n, s);
             bl.pre_done = 1;
         }
         return hipGetLastError() == hipSuccess ? 0 : -3;
@@ -3218,7 +3256,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         if (bl.stage == 2 && bl.pre_done) {   // the prepass ran earlier (HKV_BATCH_PREPASS)
             if (bl.reset_defer && hipMemsetAsync(bl.ctr + kCtrDefer, 0, 4, s) != hipSuccess) return -3;
         } else {
-            hipLaunchKernelGGL(k_local_pre, dim3((unsigned)((n + kPreElems - 1) / kPreElems)), dim3(256), 0, s, a);
+            launch_local_pre(a, n, s);
         }
         // HKV_LF_PAIR: elements per lane group in k_local_fused (2: 32 per wave; 4: 64, more loads in flight)
         static const int lfp_env = getenv("HKV_LF_PAIR") ? atoi(getenv("HKV_LF_PAIR")) : 2;

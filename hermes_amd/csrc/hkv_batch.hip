@@ -1945,8 +1945,30 @@ __global__ __launch_bounds__(64) void k_unique_big(BatchArgs a)
     }
     __syncthreads();
     if (live) {
+        const uint32_t hz = sx[el * kUbChunks].z;   // the element's opcode after the batch (byte 8)
+        const uint8_t oc = (uint8_t)hz;
+        if (TYPE == kInvs && a.ack_out) {
+            // the ACK callbacks on the element as the batch left it (as in k_unique_lds): an INV_SUCCESS
+            // answers with its header, an OP_INV_ABORT with the whole element when the ACK slot holds it
+            uint8_t *y = a.ack_out + i * a.ack_out_size;
+            const bool full = oc == kOpInvAbort && a.ack_out_size >= (uint32_t)a.esz;
+            if (oc == kInvSuccess || full) {
+                for (int c = q; c < (full ? nch : 1); c += 4) {
+                    uint4 w = sx[el * kUbChunks + c];
+                    if (c == 0)
+                        w.z = (hz & ~0xFFFFu) | (oc == kInvSuccess ? kOpAck : kOpInvAbort) |
+                              ((uint32_t)(uint8_t)a.g.machine_id << 8);
+                    if (16 * c + 16 <= a.esz || c == 0) *reinterpret_cast<uint4 *>(y + 16 * c) = w;
+                    else *reinterpret_cast<uint64_t *>(y + 16 * c) = (uint64_t)w.x | ((uint64_t)w.y << 32);
+                }
+            } else if (q == 0) {
+                y[8] = kEmpty;
+            }
+        }
         for (int c = q; c < nch; c += 4) {
-            const uint4 w = sx[el * kUbChunks + c];
+            uint4 w = sx[el * kUbChunks + c];
+            if (TYPE == kInvs && a.ack_out && c == 0 && (oc == kInvSuccess || oc == kOpInvAbort || oc == kOpMembChange))
+                w.z = (w.z & ~0xFFu) | kEmpty;   // answered (ack_modify_elem_after_send)
             if (chunk_equal(w, sx0[el * kUbChunks + c])) continue;
             if (16 * c + 16 <= a.esz) *reinterpret_cast<uint4 *>(xg + 16 * c) = w;
             else *reinterpret_cast<uint64_t *>(xg + 16 * c) = (uint64_t)w.x | ((uint64_t)w.y << 32);
@@ -3295,8 +3317,10 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     } while (0)
         // 64-B entries: the LDS-staged pass (HKV_UNIQUE_LDS=0: the in-place one, experiments)
         static const bool ulds_env = !getenv("HKV_UNIQUE_LDS") || atoi(getenv("HKV_UNIQUE_LDS")) != 0;
-        if (a.ack_out && !(ulds_env && bl.g.st_value == 31 && bl.g.entry_size == 64 && bl.esz <= 64))
-            return -1;   // only the LDS-staged pass writes the ACKs
+        if (a.ack_out && !(ulds_env && ((bl.g.st_value == 31 && bl.g.entry_size == 64 && bl.esz <= 64) ||
+                                         (bl.type == kInvs && bl.g.st_value == 287 && bl.g.entry_size == 320 &&
+                                          bl.esz <= 320))))
+            return -1;   // only the LDS-staged passes write the ACKs
         if (ulds_env && bl.g.st_value == 31 && bl.g.entry_size == 64 && bl.esz <= 64) {
             // four elements per lane group (HKV_UNIQUE_PAIR4=1): 64 per wave, every lane dispatching one
             static const bool u4 = getenv("HKV_UNIQUE_PAIR4") && atoi(getenv("HKV_UNIQUE_PAIR4")) != 0;

@@ -601,9 +601,12 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.unique = (d->flags & HKV_BATCH_UNIQUE) && (d->type == kInvs || d->type == kAcks) ? 1 : 0;
     if (force_engine) bl.path = kPathEngine;
     if (d->d_ack_out) {
-        if (d->type != kInvs || !bl.unique || d->n_rows > 1 || t->geo.entry_size != 64 || t->geo.st_value != 31 ||
-            d->elem_size > 64 || d->ack_out_size < 16 || (d->ack_out_size & 7) || ((uintptr_t)d->d_ack_out & 7))
-            return fail(-1, "d_ack_out: unique INV launches of 64-byte entries and elements, 16-byte ACKs or larger");
+        const bool small_geo = t->geo.entry_size == 64 && t->geo.st_value == 31 && d->elem_size <= 64;
+        const bool big_geo = t->geo.entry_size == 320 && t->geo.st_value == 287 && d->elem_size <= 320;
+        if (d->type != kInvs || !bl.unique || d->n_rows > 1 || !(small_geo || big_geo) || d->ack_out_size < 16 ||
+            (d->ack_out_size & 7) || ((uintptr_t)d->d_ack_out & 7))
+            return fail(-1, "d_ack_out: unique INV launches of 64-byte entries and elements (or 320-byte big "
+                            "objects), 16-byte ACKs or larger");
         bl.ack_out = d->d_ack_out;
         bl.ack_out_size = d->ack_out_size;
         bl.path = kPathEngine;

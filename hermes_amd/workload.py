@@ -371,7 +371,8 @@ class Round:
         self.rows_acks = None          # our ACKs to the rows (marshalled, not read back: the peers are virtual)
         # our ACKs to each peer's INVs written by that peer's INV launch itself (hkv_batch_desc.d_ack_out)
         # instead of a marshal pass over the applied INVs (HKV_FUSED_ACKS=0: the pass, experiments)
-        self.fused_acks = (self.pack_remote and kvs.sizes.entry == 64 and self.op <= 64
+        self.fused_acks = (self.pack_remote and ((kvs.sizes.entry == 64 and self.op <= 64) or
+                                                 (kvs.sizes.entry == 320 and self.op <= 320))
                            and os.environ.get("HKV_FUSED_ACKS", "1") != "0")
         self.drops = []                # peers dropped from the membership (membership_change)
         self.alive = self.R            # live peers: the first `alive` slots of the remote slabs

@@ -3284,6 +3284,8 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         static const int lfp_env = getenv("HKV_LF_PAIR") ? atoi(getenv("HKV_LF_PAIR")) : 2;
         if (lfp_env == 4)
             hipLaunchKernelGGL(k_local_fused<4>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, a);
+        else if (lfp_env == 1)
+            hipLaunchKernelGGL(k_local_fused<1>, dim3((unsigned)((n + 15) / 16)), dim3(64), 0, s, a);
         else
             hipLaunchKernelGGL(k_local_fused<2>, dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
         hipLaunchKernelGGL(k_local_deferred, dim3(8), dim3(256), 0, s, a);
@@ -3322,14 +3324,20 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
                                           bl.esz <= 320))))
             return -1;   // only the LDS-staged passes write the ACKs
         if (ulds_env && bl.g.st_value == 31 && bl.g.entry_size == 64 && bl.esz <= 64) {
-            // four elements per lane group (HKV_UNIQUE_PAIR4=1): 64 per wave, every lane dispatching one
-            static const bool u4 = getenv("HKV_UNIQUE_PAIR4") && atoi(getenv("HKV_UNIQUE_PAIR4")) != 0;
-            const unsigned lgrid = (unsigned)((n + kLfElems - 1) / kLfElems), lgrid4 = (unsigned)((n + 63) / 64);
-            if (bl.type == kInvs) {
-                if (u4) hipLaunchKernelGGL((k_unique_lds<kInvs, 4>), dim3(lgrid4), dim3(64), 0, s, a);
-                else hipLaunchKernelGGL((k_unique_lds<kInvs>), dim3(lgrid), dim3(64), 0, s, a);
+            // elements per lane group (HKV_UNIQUE_PAIR: 2 by default; 4 measured slower for INVs, 91 vs 77 us
+            // per step; 1: twice the waves, each with one chain in flight)
+            static const int up = getenv("HKV_UNIQUE_PAIR") ? atoi(getenv("HKV_UNIQUE_PAIR")) : 2;
+            if (up == 1) {
+                const unsigned g1 = (unsigned)((n + 15) / 16);
+                if (bl.type == kInvs) hipLaunchKernelGGL((k_unique_lds<kInvs, 1>), dim3(g1), dim3(64), 0, s, a);
+                else hipLaunchKernelGGL((k_unique_lds<kAcks, 1>), dim3(g1), dim3(64), 0, s, a);
+            } else if (up == 4) {
+                const unsigned g4 = (unsigned)((n + 63) / 64);
+                if (bl.type == kInvs) hipLaunchKernelGGL((k_unique_lds<kInvs, 4>), dim3(g4), dim3(64), 0, s, a);
+                else hipLaunchKernelGGL((k_unique_lds<kAcks, 4>), dim3(g4), dim3(64), 0, s, a);
             } else {
-                if (u4) hipLaunchKernelGGL((k_unique_lds<kAcks, 4>), dim3(lgrid4), dim3(64), 0, s, a);
+                const unsigned lgrid = (unsigned)((n + kLfElems - 1) / kLfElems);
+                if (bl.type == kInvs) hipLaunchKernelGGL((k_unique_lds<kInvs>), dim3(lgrid), dim3(64), 0, s, a);
                 else hipLaunchKernelGGL((k_unique_lds<kAcks>), dim3(lgrid), dim3(64), 0, s, a);
             }
         } else if (ulds_env && bl.type == kInvs && bl.g.st_value == 287 && bl.g.entry_size == 320 && bl.esz <= 320) {

@@ -106,6 +106,7 @@ struct BatchArgs {
     int32_t pre_patch_first;     // k_local_pre reads a PUT's header only when it has no patch (HKV_PRE_PATCH_FIRST)
     int32_t wave_copy;           // big values copied a wave per value (HKV_WAVE_COPY=0: by their own lane)
     int32_t vc_batch;            // values per step of those wave copies (HKV_VC_BATCH, 1 or kVcBatch)
+    int32_t wave_shadow;         // big entries: candidates applied by the whole wave (HKV_WAVE_SHADOW=0: per lane)
     int32_t cancel;              // k_local_pre undoes its tags (HKV_BATCH_PREPASS_CANCEL)
     uint8_t *ack_out;            // INV launches: each element's ACK (hkv_batch_desc.d_ack_out), or NULL
     uint32_t ack_out_size;
@@ -364,6 +365,31 @@ __device__ __forceinline__ void apply_to_shadow(const BatchArgs &a, uint8_t *x, 
     // not one on a select of the two, so each keeps its address space (no flat accesses).
     if (x) dispatch<SV>(TYPE, x, sh, idx, m, c);
     else dispatch<SV>(TYPE, xg, sh, idx, m, c);
+    meta_store(sh, m);
+}
+
+// apply_to_shadow for big entries, by the whole wave (every lane calls it; cand: this lane's element
+// is its key's first candidate, src its S_r): the wave copies S_r into the candidates' shadows
+// (wave_block_copies), then each candidate runs its exec function on its shadow with the value
+// copy recorded in vc (made by wave_value_copies after it), instead of one lane copying 320 + 287
+// bytes in dependent steps while the rest of its wave waits.
+__device__ __forceinline__ void wave_block_copies(uint8_t *dst, const uint8_t *src, uint32_t bytes);
+template <int TYPE, int SV>
+__device__ __forceinline__ void apply_to_shadow_wave(const BatchArgs &a, bool cand, uint32_t i, const uint8_t *src,
+                                                     VCopy &vc)
+{
+    uint8_t *sh = cand ? shadow_of(a, i) : nullptr;
+    wave_block_copies(sh, src, a.g.entry_size);
+    __threadfence_block();   // the shadows' bytes before any lane reads or rewrites them
+    if (!cand) return;
+    Meta m;
+    meta_load(src, m);
+    Ctx c = make_ctx(a);
+    c.vc = &vc;
+    uint8_t *xg;
+    uint8_t idx;
+    elem_at(a, i, xg, idx, c);
+    dispatch<SV>(TYPE, xg, sh, idx, m, c);
     meta_store(sh, m);
 }
 
@@ -987,6 +1013,57 @@ __device__ __forceinline__ void wave_value_copies(const VCopy &v, uint32_t n, in
     else wave_value_copies_n<kVcBatch>(v, n);
 }
 
+// Whole-wave copies of `bytes` (a multiple of 8, 8-byte aligned ends) recorded one per lane (dst
+// null: none): C = bytes / 16 rounded up lanes per copy move 16 B each, 64 / C copies per
+// instruction, and kBcRounds instructions' loads are issued before their stores. Every lane of the
+// wave calls it.
+constexpr int kBcRounds = 2;
+__device__ __forceinline__ void wave_block_copies(uint8_t *dst, const uint8_t *src, uint32_t bytes)
+{
+    struct __attribute__((aligned(8))) W16 {
+        uint64_t a, b;
+    };
+    const int lane = threadIdx.x & 63;
+    const int C = (int)((bytes + 15) / 16);
+    const int per = 64 / C;
+    const int slot = lane / C, ch = lane - slot * C;
+    unsigned long long todo = __ballot(dst != nullptr);
+    while (todo) {
+        W16 v[kBcRounds];
+        uint8_t *dp[kBcRounds];
+        bool half[kBcRounds];
+#pragma unroll
+        for (int r = 0; r < kBcRounds; ++r) {
+            int mine = -1;
+            for (int k = 0; k < per; ++k) {   // this instruction's copies, lane order (todo is uniform)
+                if (!todo) break;
+                const int j = __ffsll((long long)todo) - 1;
+                todo &= todo - 1;
+                if (k == slot) mine = j;
+            }
+            const int sl = mine < 0 ? 0 : mine;
+            const uint64_t d = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(uintptr_t)dst, sl, 64) |
+                               ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)dst >> 32), sl, 64) << 32);
+            const uint64_t sa = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(uintptr_t)src, sl, 64) |
+                                ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)src >> 32), sl, 64) << 32);
+            dp[r] = mine >= 0 && slot < per ? reinterpret_cast<uint8_t *>(d) + 16 * ch : nullptr;
+            half[r] = 16 * ch + 16 > (int)bytes;
+            const uint8_t *sp = reinterpret_cast<const uint8_t *>(sa) + 16 * ch;
+            v[r] = W16{0, 0};
+            if (dp[r]) {
+                if (half[r]) v[r].a = *reinterpret_cast<const uint64_t *>(sp);
+                else v[r] = *reinterpret_cast<const W16 *>(sp);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kBcRounds; ++r) {
+            if (!dp[r]) continue;
+            if (half[r]) *reinterpret_cast<uint64_t *>(dp[r]) = v[r].a;
+            else *reinterpret_cast<W16 *>(dp[r]) = v[r];
+        }
+    }
+}
+
 template <int TYPE, int SV>
 __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
 {
@@ -1002,6 +1079,9 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
     // the op is this lane's own)
     VCopy vc{nullptr, nullptr};
     if (SV != 31 && a.wave_copy && a.g.st_value <= 320) c.vc = &vc;
+    // a key's first candidate applies itself to its shadow by the whole wave (apply_to_shadow_wave)
+    const bool wave_shadow = SV != 31 && a.wave_copy && a.g.st_value <= 320 && a.wave_shadow;
+    bool cand = false;
     if (in) elem_at(a, (uint32_t)i, xg, idx, c);
     if (e != kNone) {
         Meta m;
@@ -1012,7 +1092,8 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
             dispatch<SV>(TYPE, xg, entry_of(a, e), idx, tm, c);
             if (a.error_flags && !meta_equal(tm, m)) atomicOr(a.error_flags, 1u);
         } else if ((uint32_t)i == f) {
-            apply_to_shadow<TYPE, SV>(a, nullptr, (uint32_t)i, entry_of(a, e));
+            if (wave_shadow) cand = true;
+            else apply_to_shadow<TYPE, SV>(a, nullptr, (uint32_t)i, entry_of(a, e));
             st = kStCommit;
         } else if (a.rounds == 0) {
             const Meta m1 = after_first<TYPE>(a, m, f, 0);
@@ -1024,6 +1105,7 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
             st = kStPend;
         }
     }
+    if (wave_shadow) apply_to_shadow_wave<TYPE, SV>(a, cand, (uint32_t)i, cand ? entry_of(a, e) : nullptr, vc);
     if (SV != 31) wave_value_copies(vc, a.g.st_value, a.vc_batch);
     if (!in) return;
     a.st[i] = st;
@@ -2033,10 +2115,13 @@ __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
     // they read (round r-1's first candidate's) is not written in this round
     VCopy vc{nullptr, nullptr};
     VCopy *vcp = SV != 31 && a.wave_copy && a.g.st_value <= 320 ? &vc : nullptr;
+    const bool wave_shadow = SV != 31 && vcp && a.wave_shadow;   // see k_resolve0_direct
+    bool cand = false;
+    uint32_t prev = 0;
     if (i < a.n && a.st[i] == kStPend) {
         const uint32_t e = a.ent[i];
         const uint32_t f = first_cand(*fw_of(a, e), a.rtag0 + (uint32_t)r);
-        const uint32_t prev = a.pf[i];  // S_r lives in the shadow of round r-1's first candidate
+        prev = a.pf[i];  // S_r lives in the shadow of round r-1's first candidate
         if (f == kNone || (uint32_t)i <= f) {
             uint8_t *xg = a.elems + i * a.esz;
             uint8_t *xl = reinterpret_cast<uint8_t *>(sx) + threadIdx.x * (uint32_t)a.esz;
@@ -2046,16 +2131,21 @@ __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
                 else resolve_elem<TYPE, SV>(a, (uint32_t)i, xg, shadow_of(a, prev), vcp);
                 a.st[i] = kStDone;
             } else {
-                apply_to_shadow<TYPE, SV>(a, kStage ? xl : nullptr, (uint32_t)i, shadow_of(a, prev));
+                if (wave_shadow) cand = true;
+                else apply_to_shadow<TYPE, SV>(a, kStage ? xl : nullptr, (uint32_t)i, shadow_of(a, prev));
                 a.st[prev] = kStDone;  // superseded
                 a.st[i] = kStCommit;
             }
             if (kStage) copy_elem(xg, xl, a.esz);
-            note_state(a, i, kStage ? xl : xg);
+            if (!cand) note_state(a, i, kStage ? xl : xg);
         } else {
             a.pf[i] = f;  // after the last round: identifies the key's run in k_fb_exec
             left = r == a.rounds;
         }
+    }
+    if (wave_shadow) {
+        apply_to_shadow_wave<TYPE, SV>(a, cand, (uint32_t)i, cand ? shadow_of(a, prev) : nullptr, vc);
+        if (cand) note_state(a, i, a.elems + i * a.esz);
     }
     if (SV != 31) wave_value_copies(vc, a.g.st_value, a.vc_batch);
     if (r == a.rounds) {  // wave-aggregated append (uniform branch)
@@ -3188,6 +3278,8 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.wave_copy = wave_copy_env;
     static const int vc_batch_env = getenv("HKV_VC_BATCH") && atoi(getenv("HKV_VC_BATCH")) == 1 ? 1 : kVcBatch;
     a.vc_batch = vc_batch_env;
+    static const int wave_shadow_env = !getenv("HKV_WAVE_SHADOW") || atoi(getenv("HKV_WAVE_SHADOW")) != 0;
+    a.wave_shadow = wave_shadow_env;
     if (dbg_env) a.error_flags = nullptr;
     a.index = bl.index;
     a.log = bl.log;

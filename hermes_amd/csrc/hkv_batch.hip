@@ -2162,21 +2162,11 @@ template <int SV>
 __global__ __launch_bounds__(256) void k_commit(BatchArgs a)
 {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (SV != 31) {  // big entries: one entry per wave-wide copy, 8-B word k by lane k
+    if (SV != 31) {  // big entries: copied by the whole wave, 16 B per lane, several entries per step
         const bool mine = i < a.n && a.st[i] == kStCommit;
         const uint32_t e = mine ? a.ent[i] : 0u;
-        const int lane = threadIdx.x & 63;
-        const int words = (int)(a.g.entry_size / 8u);
-        unsigned long long todo = __ballot(mine);
-        while (todo) {
-            const int j = __ffsll((long long)todo) - 1;
-            todo &= todo - 1;
-            const uint32_t ej = (uint32_t)__shfl((int)e, j, 64);
-            const uint32_t ij = (uint32_t)(i - lane + j);
-            uint64_t *d8 = reinterpret_cast<uint64_t *>(entry_of(a, ej));
-            const uint64_t *s8 = reinterpret_cast<const uint64_t *>(shadow_of(a, ij));
-            for (int k = lane; k < words; k += 64) d8[k] = s8[k];
-        }
+        wave_block_copies(mine ? entry_of(a, e) : nullptr, mine ? shadow_of(a, (uint32_t)i) : nullptr,
+                          a.g.entry_size);
         return;
     }
     if (i >= a.n || a.st[i] != kStCommit) return;

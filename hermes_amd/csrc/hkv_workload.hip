@@ -576,6 +576,97 @@ __global__ __launch_bounds__(256) void k_refill_plan_w(uint8_t *states, int32_t 
     }
 }
 
+// k_refill_direct from the state mirror (hkv_wl_refill_st: big ops refilled in place), one wave per
+// worker as k_refill_plan_w: ranks and counts from ballots instead of six block reductions, every
+// trace load of the worker in flight together, then the stores -- key, opcode, ST_NEW, val_len,
+// a GET's flags and timestamp reset, the state and opcode mirrors, and a write's value, one op at
+// a time per wave (lane k stores 8-B word k of bytes 16 .. 18 + st_value, word 0 the flags).
+__global__ __launch_bounds__(256) void k_refill_st_w(uint8_t *ops, int32_t n_workers, int32_t stride,
+                                                     uint32_t op_size, uint32_t st_value, uint32_t shift,
+                                                     const uint64_t *tkey, const uint8_t *top, int32_t tlen,
+                                                     uint32_t *cursor, uint32_t machine_id, uint32_t rflags,
+                                                     unsigned long long *counters, uint8_t *opc_out, uint8_t *states)
+{
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    if (w >= n_workers) return;
+    const int64_t e0 = (int64_t)w * stride;
+    uint8_t st[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st[r] = r * 64 + lane < stride ? states[e0 + r * 64 + lane] : 0;
+    const uint32_t base = cursor[w];
+    unsigned long long bd[4];
+    int c = 0, m = 0, wr = 0, dr = 0, ab = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const bool live = r * 64 + lane < stride;
+        const bool complete = is_complete(st[r]);
+        const bool drop = live && (rflags & HKV_WL_REFILL_ALL) && !complete && !in_flight(st[r]);
+        bd[r] = __ballot(live && (complete || drop));
+        c += __popcll(__ballot(live && complete && st[r] != kMiss && st[r] != kRmwAbort));
+        m += __popcll(__ballot(live && st[r] == kMiss));
+        wr += __popcll(__ballot(live && st[r] == kPutComplete));
+        dr += __popcll(__ballot(drop));
+        ab += __popcll(__ballot(live && st[r] == kRmwAbort));
+    }
+    int rank[4], total;
+    wave_ranks(bd, lane, rank, total);
+    if (lane == 0) {
+        cursor[w] = (uint32_t)((base + (uint32_t)total) % (uint32_t)tlen);
+        unsigned long long *stripe = counters + HKV_WL_STRIPE_BASE + (w % kStripes) * 16;
+        if (c) atomicAdd(&stripe[0], (unsigned long long)c);
+        if (m) atomicAdd(&stripe[1], (unsigned long long)m);
+        if (wr) atomicAdd(&stripe[2], (unsigned long long)wr);
+        if (dr) atomicAdd(&stripe[3], (unsigned long long)dr);
+        if (ab) atomicAdd(&stripe[4], (unsigned long long)ab);
+    }
+    uint8_t oc[4];
+    uint64_t key[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const bool rf = (bd[r] >> lane) & 1ull;
+        const int64_t t = (int64_t)w * tlen + (int64_t)((base + (uint32_t)rank[r]) % (uint32_t)tlen);
+        oc[r] = rf ? top[t] : (uint8_t)kOpGet;
+        key[r] = rf ? tkey[t] : 0ull;
+    }
+    const uint64_t vv = 0x0101010101010101ull * (uint8_t)('a' + machine_id);
+    const uint32_t span = kOpValueOff - 16 + st_value;
+    const int nfull = (int)(span / 8), tail = (int)(span % 8);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const bool rf = (bd[r] >> lane) & 1ull;
+        const int64_t e = e0 + r * 64 + lane;
+        const uint16_t flags = (uint16_t)((oc[r] == kOpRmw ? 1u : 0u) | 2u);   // RMW_flag, no_coales
+        if (rf) {
+            uint8_t *op = ops + e * op_size;
+            *reinterpret_cast<uint64_t *>(op) = key[r];
+            const bool get = oc[r] == kOpGet;
+            op[8] = oc[r];
+            op[9] = kNew;
+            op[10] = get ? (uint8_t)0 : (uint8_t)(st_value >> shift);
+            if (get && (rflags & HKV_WL_READ_TS_RESET)) {   // inline-util.h:268-272
+                op[11] = 0;
+                *reinterpret_cast<uint32_t *>(op + 12) = 0;
+            }
+            if (get) *reinterpret_cast<uint16_t *>(op + 16) = flags;
+            states[e] = kNew;
+            opc_out[e] = oc[r];
+        }
+        unsigned long long todo = __ballot(rf && oc[r] != kOpGet);
+        uint8_t *row = ops + (e0 + r * 64) * op_size;
+        while (todo) {
+            const int j = __ffsll((long long)todo) - 1;
+            todo &= todo - 1;
+            const uint16_t fj = (uint16_t)__shfl((int)flags, j, 64);
+            uint8_t *oj = row + (int64_t)j * op_size + 16;
+            if (lane < nfull)
+                *reinterpret_cast<uint64_t *>(oj + 8 * lane) = lane == 0 ? ((uint64_t)fj | (vv << 16)) : vv;
+            else if (lane < nfull + tail)
+                oj[8 * nfull + (lane - nfull)] = (uint8_t)vv;
+        }
+    }
+}
+
 // k_marshal_invs for ops of at most 64 bytes, one wave per WPW workers (their state loads all in
 // flight together, see k_refill_plan_w)
 template <int WPW>
@@ -1650,8 +1741,15 @@ int hkv_wl_refill_st(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t o
     if (stride > 256 || n_workers <= 0 || tlen <= 0 || !states || !opc) return -1;
     if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET)) return -1;   // no hot-request coalescing
     if (!(op_size > 64 && op_size % 8 == 0 && st_value >= 6 && (kOpValueOff - 16 + st_value) / 8 + 7 <= 64)) return -1;
-    hipLaunchKernelGGL(k_refill_direct, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
-                       st_value, shift, tkey, top, tlen, cursor, machine_id, 0, flags, counters, opc, states);
+    // one wave per worker (HKV_REFILL_ST_W=0: the workgroup-per-worker k_refill_direct)
+    static const bool st_w = !getenv("HKV_REFILL_ST_W") || atoi(getenv("HKV_REFILL_ST_W")) != 0;
+    if (st_w)
+        hipLaunchKernelGGL(k_refill_st_w, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream, ops,
+                           n_workers, stride, op_size, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
+                           counters, opc, states);
+    else
+        hipLaunchKernelGGL(k_refill_direct, dim3(n_workers), dim3(256), 0, (hipStream_t)stream, ops, stride, op_size,
+                           st_value, shift, tkey, top, tlen, cursor, machine_id, 0, flags, counters, opc, states);
     return ok();
 }
 

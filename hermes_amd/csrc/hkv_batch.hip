@@ -1131,7 +1131,10 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
 // the op slab are read once instead of twice.
 constexpr int kPreElems = 1024;          // elements per k_local_pre block
 constexpr int kPreHead = 1024;           // launch head whose PUT keys every block knows
-constexpr int kPreHash = 1024;           // LDS slots of a (key -> first PUT) table
+#ifndef HKV_PRE_HASH_SLOTS
+#define HKV_PRE_HASH_SLOTS 1024
+#endif
+constexpr int kPreHash = HKV_PRE_HASH_SLOTS;   // LDS slots of a (key -> first PUT) table (a power of two)
 constexpr int kLfElems = 32;             // elements per k_local_fused block (one wave)
 enum { kCtrDefer = 3 };
 enum : uint8_t { kStDefer = 3 };
@@ -1277,6 +1280,18 @@ __device__ __forceinline__ bool pre_insert(uint64_t *hk, uint32_t *hv, uint64_t 
     return false;
 }
 
+// a key into an LDS set of kPreHash slots (the head's PUT keys: only membership is asked)
+__device__ __forceinline__ void pre_insert_key(uint64_t *hk, uint64_t key)
+{
+    if (key == ~0ull) return;
+    uint32_t sl = pre_slot(key);
+    for (int n = 0; n < kPreHash; ++n) {
+        const unsigned long long old = atomicCAS((unsigned long long *)&hk[sl], ~0ull, key);
+        if (old == ~0ull || old == key) return;
+        sl = (sl + 1) & (kPreHash - 1);
+    }
+}
+
 // The PUTs of kPreElems elements offer F. Whether a PUT mutates S_0 depends on S_0 alone
 // (hermes_exec_write: VALID or INVALID and no op buffer index), so either every PUT of a key is a
 // candidate or none is, and F is the key's first PUT or nothing. So each block looks up each key
@@ -1286,11 +1301,16 @@ __device__ __forceinline__ bool pre_insert(uint64_t *hk, uint32_t *hv, uint64_t 
 // L2-resident after the first block) and drops its keys that have a PUT there -- an earlier block
 // offers that one. Four keys per lane group are in flight; the offer is a plain atomicMin.
 constexpr int kPrePair = 4;
+#ifdef HKV_PRE_WAVES
+#define HKV_PRE_ATTR __attribute__((amdgpu_waves_per_eu(HKV_PRE_WAVES)))
+#else
+#define HKV_PRE_ATTR
+#endif
 template <int HEAD = kPreHead>
-__global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
+__global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 {
     __shared__ uint64_t hk[kPreHash], gk[kPreHash];  // the block's PUT keys, the head's
-    __shared__ uint32_t hv[kPreHash], gv[kPreHash];
+    __shared__ uint32_t hv[kPreHash];
     __shared__ uint32_t dl[kPreElems];               // distinct keys: slots of hk, or ~index (no slot)
     __shared__ uint32_t nd;
     const int tid = threadIdx.x, q = tid & 3, gbase = (tid & 63) & ~3;
@@ -1302,7 +1322,6 @@ __global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
         hk[j] = ~0ull;
         gk[j] = ~0ull;
         hv[j] = kNone;
-        gv[j] = kNone;
     }
     if (a.dbg & 8) return;
     const int64_t i0 = (int64_t)blockIdx.x * kPreElems;
@@ -1407,7 +1426,7 @@ __global__ __launch_bounds__(256) void k_local_pre(BatchArgs a)
                 dl[atomicAdd(&nd, 1u)] = in_table ? sl : ~i;
             }
         } else {
-            pre_insert(gk, gv, key, i, created, sl);
+            pre_insert_key(gk, key);
         }
     }
     __syncthreads();

@@ -1848,27 +1848,28 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
 // of the entry -- exactly the rows' launches one after another, since each row holds the key once --
 // and each element and the entry line are written back where they changed. An ACK's completion finds
 // its read_write_ops once per position (the rows share the batch layout).
-template <int TYPE, int RMAX, int CH>
+template <int TYPE, int RMAX, int CH, int P = kLookupPair>
 __global__ __launch_bounds__(64) void k_unique_rows(BatchArgs a)
 {
+    constexpr int E = 16 * P;   // positions per wave: P per lane group
     // CH: 16-B chunks of an element held in LDS (1 for 16-B ACKs, 4 for 56-B INVs)
-    __shared__ uint4 sops[RMAX][kLfElems * CH];
-    __shared__ uint4 sln[kLfElems * 4];
-    __shared__ uint32_t sent[kLfElems];
-    __shared__ uint8_t spart[kLfElems];   // bit r: row r's element takes part (present, in count, not skipped)
+    __shared__ uint4 sops[RMAX][E * CH];
+    __shared__ uint4 sln[E * 4];
+    __shared__ uint32_t sent[E];
+    __shared__ uint8_t spart[E];   // bit r: row r's element takes part (present, in count, not skipped)
     const int tid = threadIdx.x, q = tid & 3, gbase = tid & ~3;
-    const int64_t i0 = (int64_t)blockIdx.x * kLfElems;
+    const int64_t i0 = (int64_t)blockIdx.x * E;
     const int R = a.n_rows < RMAX ? a.n_rows : RMAX;
     // packed rows may end before the stride: elements past the last batch offset are in no batch
     const int64_t n_live = a.offsets ? (int64_t)a.offsets[a.n_batches] : a.n;
-    uint64_t key[kLookupPair];
-    bool probe[kLookupPair], ok[kLookupPair], live[kLookupPair];
-    uint64_t phys[kLookupPair];
-    uint4 ln[kLookupPair], op[RMAX][kLookupPair];
-    uint32_t part[kLookupPair];
-    int te[kLookupPair];
+    uint64_t key[P];
+    bool probe[P], ok[P], live[P];
+    uint64_t phys[P];
+    uint4 ln[P], op[RMAX][P];
+    uint32_t part[P];
+    int te[P];
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         te[k] = k * 16 + (tid >> 2);
         const int64_t i = i0 + te[k];
         live[k] = i < a.n && i < n_live && (a.offsets || in_count(a, (uint32_t)i));
@@ -1881,7 +1882,7 @@ __global__ __launch_bounds__(64) void k_unique_rows(BatchArgs a)
         }
     }
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         uint64_t kk = 0;
         uint32_t p = 0;
         bool mismatch = false;
@@ -1901,9 +1902,9 @@ __global__ __launch_bounds__(64) void k_unique_rows(BatchArgs a)
         part[k] = mismatch ? 0u : p;
         probe[k] = part[k] != 0;
     }
-    lookup_pair(a, key, probe, q, gbase, ok, phys, ln);
+    lookup_pair<P>(a, key, probe, q, gbase, ok, phys, ln);
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         Meta m;
         const uint64_t ek = line_key_meta(ln[k], m);
         const bool hit = ok[k] && ek == key[k];
@@ -1914,7 +1915,7 @@ __global__ __launch_bounds__(64) void k_unique_rows(BatchArgs a)
         }
     }
     __syncthreads();
-    if (tid < kLfElems && i0 + tid < n_live) {
+    if (tid < E && i0 + tid < n_live) {
         const int64_t i = i0 + tid;
         uint8_t *ent = reinterpret_cast<uint8_t *>(&sln[tid * 4]);
         const uint32_t e = sent[tid];
@@ -1949,7 +1950,7 @@ __global__ __launch_bounds__(64) void k_unique_rows(BatchArgs a)
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         if (!live[k]) continue;
 #pragma unroll
         for (int r = 0; r < RMAX; ++r) {
@@ -3397,7 +3398,13 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         else
             hipLaunchKernelGGL((k_commit<31>), dim3(grid), dim3(256), 0, s, a);
     } else if (bl.n_rows > 0 && bl.unique) {  // HKV_BATCH_ROWS: one pass over positions of all rows
-        const unsigned lgrid = (unsigned)((n + kLfElems - 1) / kLfElems);
+        // positions per lane group (HKV_ROWS_PAIR=1: 16 per wave instead of 32; ACKs of 16 B only)
+        static const int rp = getenv("HKV_ROWS_PAIR") ? atoi(getenv("HKV_ROWS_PAIR")) : 2;
+        const unsigned lgrid = (unsigned)((n + kLfElems - 1) / kLfElems), g1 = (unsigned)((n + 15) / 16);
+        if (rp == 1 && bl.type == kAcks && bl.esz <= 16) {
+            if (bl.n_rows <= 2) hipLaunchKernelGGL((k_unique_rows<kAcks, 2, 1, 1>), dim3(g1), dim3(64), 0, s, a);
+            else hipLaunchKernelGGL((k_unique_rows<kAcks, 8, 1, 1>), dim3(g1), dim3(64), 0, s, a);
+        } else
         // elements of 16 B (ACKs without RMWs) keep one chunk each in LDS, others four
         if (bl.type == kInvs) {
             if (bl.n_rows <= 2) hipLaunchKernelGGL((k_unique_rows<kInvs, 2, 4>), dim3(lgrid), dim3(64), 0, s, a);
@@ -3425,9 +3432,9 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
                                           bl.esz <= 320))))
             return -1;   // only the LDS-staged passes write the ACKs
         if (ulds_env && bl.g.st_value == 31 && bl.g.entry_size == 64 && bl.esz <= 64) {
-            // elements per lane group (HKV_UNIQUE_PAIR: 2 by default; 4 measured slower for INVs, 91 vs 77 us
-            // per step; 1: twice the waves, each with one chain in flight)
-            static const int up = getenv("HKV_UNIQUE_PAIR") ? atoi(getenv("HKV_UNIQUE_PAIR")) : 2;
+            // elements per lane group (HKV_UNIQUE_PAIR): 1 by default, 16 per wave. Same box, INV phase per
+            // step (gpurun_out/r04m, r04t): 72-77 us at 1, 78-80 at 2, 91 at 4
+            static const int up = getenv("HKV_UNIQUE_PAIR") ? atoi(getenv("HKV_UNIQUE_PAIR")) : 1;
             if (up == 1) {
                 const unsigned g1 = (unsigned)((n + 15) / 16);
                 if (bl.type == kInvs) hipLaunchKernelGGL((k_unique_lds<kInvs, 1>), dim3(g1), dim3(64), 0, s, a);
@@ -3449,9 +3456,10 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         else HKV_UNIQUE(kAcks);
 #undef HKV_UNIQUE
     } else if (bl.type == kVals) {             // one pass (see k_lookup)
-        // four elements per lane group (HKV_VAL_PAIR4=1): twice the loads in flight per wave, half the waves
-        static const bool val4 = getenv("HKV_VAL_PAIR4") && atoi(getenv("HKV_VAL_PAIR4")) != 0;
-        if (val4) hipLaunchKernelGGL(k_lookup<4>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, (int64_t)0, n);
+        // elements per lane group (HKV_VAL_PAIR: 2 by default; 4 measured slower, 57 vs 53.6 us per step)
+        static const int vp = getenv("HKV_VAL_PAIR") ? atoi(getenv("HKV_VAL_PAIR")) : 2;
+        if (vp == 4) hipLaunchKernelGGL(k_lookup<4>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, (int64_t)0, n);
+        else if (vp == 1) hipLaunchKernelGGL(k_lookup<1>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, a, (int64_t)0, n);
         else hipLaunchKernelGGL(k_lookup<>, dim3((unsigned)((n + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, n);
         return hipGetLastError() == hipSuccess ? 0 : -3;
     } else {

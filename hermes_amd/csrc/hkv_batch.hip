@@ -3456,8 +3456,9 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         else HKV_UNIQUE(kAcks);
 #undef HKV_UNIQUE
     } else if (bl.type == kVals) {             // one pass (see k_lookup)
-        // elements per lane group (HKV_VAL_PAIR: 2 by default; 4 measured slower, 57 vs 53.6 us per step)
-        static const int vp = getenv("HKV_VAL_PAIR") ? atoi(getenv("HKV_VAL_PAIR")) : 2;
+        // elements per lane group (HKV_VAL_PAIR): 1 by default. Same box, VAL batch per step (gpurun_out/r04m,
+        // r04u): 49.6-50.2 us at 1, 52.3-53.9 at 2, 57 at 4
+        static const int vp = getenv("HKV_VAL_PAIR") ? atoi(getenv("HKV_VAL_PAIR")) : 1;
         if (vp == 4) hipLaunchKernelGGL(k_lookup<4>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, (int64_t)0, n);
         else if (vp == 1) hipLaunchKernelGGL(k_lookup<1>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, a, (int64_t)0, n);
         else hipLaunchKernelGGL(k_lookup<>, dim3((unsigned)((n + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, n);
@@ -3468,9 +3469,16 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     // round, so those launches take one pass (their launch-sized head took ~9 us at cfg2).
     const bool split = bl.type == kLocal || bl.type == kLocalAfterMemb;
     const int64_t head = split && n > kLookupHead ? kLookupHead : n;
-    hipLaunchKernelGGL(k_lookup<>, dim3((unsigned)((head + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, head);
-    if (n > head)
-        hipLaunchKernelGGL(k_lookup<>, dim3((unsigned)((n - head + kPer - 1) / kPer)), dim3(256), 0, s, a, head, n);
+    // elements per lane group of the other lookups (HKV_LOOKUP_PAIR=1: 64 per workgroup instead of 128)
+    static const int lp = getenv("HKV_LOOKUP_PAIR") ? atoi(getenv("HKV_LOOKUP_PAIR")) : 2;
+    if (lp == 1) {
+        hipLaunchKernelGGL(k_lookup<1>, dim3((unsigned)((head + 63) / 64)), dim3(256), 0, s, a, (int64_t)0, head);
+        if (n > head) hipLaunchKernelGGL(k_lookup<1>, dim3((unsigned)((n - head + 63) / 64)), dim3(256), 0, s, a, head, n);
+    } else {
+        hipLaunchKernelGGL(k_lookup<>, dim3((unsigned)((head + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, head);
+        if (n > head)
+            hipLaunchKernelGGL(k_lookup<>, dim3((unsigned)((n - head + kPer - 1) / kPer)), dim3(256), 0, s, a, head, n);
+    }
     if (a.ack_direct) {
         hipLaunchKernelGGL(k_ack_resolve, dim3(grid), dim3(256), 0, s, a);
     } else if (a.inv_direct) {

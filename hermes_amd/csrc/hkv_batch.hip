@@ -1626,17 +1626,17 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
 // launches: a peer's round slab, see hermeskv.h.) With check_unique every element also swaps its
 // index into its key's F word, tagged with the launch; finding the launch's tag there means a
 // second element of the key (error bit 4).
-template <int TYPE, int SV>
+template <int TYPE, int SV, int P = kLookupPair>
 __global__ __launch_bounds__(256) void k_unique(BatchArgs a)
 {
     const int q = threadIdx.x & 3;
     const int gbase = (threadIdx.x & 63) & ~3;
-    int64_t gi[kLookupPair];
-    uint64_t key[kLookupPair], hdr[kLookupPair];
-    bool probe[kLookupPair];
+    int64_t gi[P];
+    uint64_t key[P], hdr[P];
+    bool probe[P];
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
-        gi[k] = ((int64_t)blockIdx.x * kLookupPair + k) * 64 + (threadIdx.x >> 2);
+    for (int k = 0; k < P; ++k) {
+        gi[k] = ((int64_t)blockIdx.x * P + k) * 64 + (threadIdx.x >> 2);
         uint64_t kk = 0, hh = 0;
         bool p = false;
         if (gi[k] < a.n && q == 0) {
@@ -1665,17 +1665,17 @@ __global__ __launch_bounds__(256) void k_unique(BatchArgs a)
         probe[k] = __shfl((int)p, 0, 4) != 0;
         hdr[k] = hh;
     }
-    bool ok[kLookupPair];
-    uint64_t phys[kLookupPair];
-    uint4 ln[kLookupPair];
-    lookup_pair(a, key, probe, q, gbase, ok, phys, ln);
-    Meta m[kLookupPair];
-    uint64_t ek[kLookupPair];
+    bool ok[P];
+    uint64_t phys[P];
+    uint4 ln[P];
+    lookup_pair<P>(a, key, probe, q, gbase, ok, phys, ln);
+    Meta m[P];
+    uint64_t ek[P];
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) ek[k] = line_key_meta(ln[k], m[k]);
+    for (int k = 0; k < P; ++k) ek[k] = line_key_meta(ln[k], m[k]);
     if (q != 0) return;
 #pragma unroll
-    for (int k = 0; k < kLookupPair; ++k) {
+    for (int k = 0; k < P; ++k) {
         if (!probe[k]) continue;
         uint8_t *x = a.elems + gi[k] * a.esz;
         if (!(ok[k] && ek[k] == key[k])) {
@@ -3419,9 +3419,16 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     } else if (bl.unique && (bl.type == kInvs || bl.type == kAcks)) {  // one pass: every key has one element
         constexpr int64_t kPerU = 64 * kLookupPair;
         const unsigned ugrid = (unsigned)((n + kPerU - 1) / kPerU);
+        // in-place unique pass (big-entry ACKs, other geometries): elements per lane group as HKV_UNIQUE_PAIR
+        static const int upi = getenv("HKV_UNIQUE_PAIR") ? atoi(getenv("HKV_UNIQUE_PAIR")) : 1;
+        const unsigned ugrid1 = (unsigned)((n + 63) / 64);
 #define HKV_UNIQUE(T)                                                                                  \
     do {                                                                                               \
-        if (bl.g.st_value == 31) hipLaunchKernelGGL((k_unique<T, 31>), dim3(ugrid), dim3(256), 0, s, a); \
+        if (upi == 1) {                                                                                \
+            if (bl.g.st_value == 31) hipLaunchKernelGGL((k_unique<T, 31, 1>), dim3(ugrid1), dim3(256), 0, s, a); \
+            else if (bl.g.st_value == 287) hipLaunchKernelGGL((k_unique<T, 287, 1>), dim3(ugrid1), dim3(256), 0, s, a); \
+            else hipLaunchKernelGGL((k_unique<T, 0, 1>), dim3(ugrid1), dim3(256), 0, s, a);         \
+        } else if (bl.g.st_value == 31) hipLaunchKernelGGL((k_unique<T, 31>), dim3(ugrid), dim3(256), 0, s, a); \
         else if (bl.g.st_value == 287) hipLaunchKernelGGL((k_unique<T, 287>), dim3(ugrid), dim3(256), 0, s, a); \
         else hipLaunchKernelGGL((k_unique<T, 0>), dim3(ugrid), dim3(256), 0, s, a);                   \
     } while (0)
@@ -3469,8 +3476,9 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     // round, so those launches take one pass (their launch-sized head took ~9 us at cfg2).
     const bool split = bl.type == kLocal || bl.type == kLocalAfterMemb;
     const int64_t head = split && n > kLookupHead ? kLookupHead : n;
-    // elements per lane group of the other lookups (HKV_LOOKUP_PAIR=1: 64 per workgroup instead of 128)
-    static const int lp = getenv("HKV_LOOKUP_PAIR") ? atoi(getenv("HKV_LOOKUP_PAIR")) : 2;
+    // elements per lane group of the other lookups (HKV_LOOKUP_PAIR, 1 by default: configs[2] 0.627-0.635
+    // against 0.620-0.622 G ops/s at 2, same box, gpurun_out/r04v)
+    static const int lp = getenv("HKV_LOOKUP_PAIR") ? atoi(getenv("HKV_LOOKUP_PAIR")) : 1;
     if (lp == 1) {
         hipLaunchKernelGGL(k_lookup<1>, dim3((unsigned)((head + 63) / 64)), dim3(256), 0, s, a, (int64_t)0, head);
         if (n > head) hipLaunchKernelGGL(k_lookup<1>, dim3((unsigned)((n - head + 63) / 64)), dim3(256), 0, s, a, head, n);

@@ -1978,17 +1978,23 @@ constexpr int kUbChunks = 20;   // 320 B
 template <int TYPE>
 __global__ __launch_bounds__(64) void k_unique_big(BatchArgs a)
 {
-    __shared__ uint4 sx[kUbElems * kUbChunks], sx0[kUbElems * kUbChunks];   // elements, as loaded
-    __shared__ uint4 se[kUbElems * kUbChunks], se0[kUbElems * kUbChunks];   // entries, as loaded
+    // elements and entries in LDS; each lane keeps the chunks it loaded in registers (what changed goes
+    // back), so a wave's LDS is 10 KB and four waves fit a SIMD
+    __shared__ uint4 sx[kUbElems * kUbChunks];
+    __shared__ uint4 se[kUbElems * kUbChunks];
+    constexpr int kPerLane = (kUbChunks + 3) / 4;
+    uint4 x0[kPerLane], e0[kPerLane];
     const int tid = threadIdx.x, q = tid & 3, el = tid >> 2, gbase = tid & ~3;
     const int64_t i = (int64_t)blockIdx.x * kUbElems + el;
     const bool live = i < a.n;
     const int nch = (a.esz + 15) / 16;
     uint8_t *xg = a.elems + i * a.esz;
-    for (int c = q; c < nch; c += 4) {
-        const uint4 v = live ? load_chunk(xg, c, a.esz) : make_uint4(0u, 0u, 0u, 0u);
-        sx[el * kUbChunks + c] = v;
-        sx0[el * kUbChunks + c] = v;
+#pragma unroll
+    for (int u = 0; u < kPerLane; ++u) {
+        const int c = q + 4 * u;
+        const uint4 v = live && c < nch ? load_chunk(xg, c, a.esz) : make_uint4(0u, 0u, 0u, 0u);
+        if (c < nch) sx[el * kUbChunks + c] = v;
+        x0[u] = v;
     }
     const uint4 c0 = sx[el * kUbChunks];   // the element's key and header (every lane of the group)
     const uint64_t key = (uint64_t)c0.x | ((uint64_t)c0.y << 32);
@@ -2009,12 +2015,17 @@ __global__ __launch_bounds__(64) void k_unique_big(BatchArgs a)
     Meta m0;
     const uint64_t ek = line_key_meta(ln, m0);
     const bool hit = ok && ek == key;
+#pragma unroll
+    for (int u = 0; u < kPerLane; ++u) e0[u] = make_uint4(0u, 0u, 0u, 0u);
     if (hit) {
         const uint4 *eg = reinterpret_cast<const uint4 *>(a.log + phys);
-        for (int c = q; c < kUbChunks; c += 4) {
+#pragma unroll
+        for (int u = 0; u < kPerLane; ++u) {
+            const int c = q + 4 * u;
+            if (c >= kUbChunks) continue;
             const uint4 v = c < 4 ? ln : eg[c];
             se[el * kUbChunks + c] = v;
-            se0[el * kUbChunks + c] = v;
+            e0[u] = v;
         }
     }
     __syncthreads();
@@ -2067,20 +2078,26 @@ __global__ __launch_bounds__(64) void k_unique_big(BatchArgs a)
                 y[8] = kEmpty;
             }
         }
-        for (int c = q; c < nch; c += 4) {
+#pragma unroll
+        for (int u = 0; u < kPerLane; ++u) {
+            const int c = q + 4 * u;
+            if (c >= nch) continue;
             uint4 w = sx[el * kUbChunks + c];
             if (TYPE == kInvs && a.ack_out && c == 0 && (oc == kInvSuccess || oc == kOpInvAbort || oc == kOpMembChange))
                 w.z = (w.z & ~0xFFu) | kEmpty;   // answered (ack_modify_elem_after_send)
-            if (chunk_equal(w, sx0[el * kUbChunks + c])) continue;
+            if (chunk_equal(w, x0[u])) continue;
             if (16 * c + 16 <= a.esz) *reinterpret_cast<uint4 *>(xg + 16 * c) = w;
             else *reinterpret_cast<uint64_t *>(xg + 16 * c) = (uint64_t)w.x | ((uint64_t)w.y << 32);
         }
     }
     if (hit) {   // bytes 0..15 of an entry (the MICA key) never change
         uint4 *eg = reinterpret_cast<uint4 *>(a.log + phys);
-        for (int c = q; c < kUbChunks; c += 4) {
+#pragma unroll
+        for (int u = 0; u < kPerLane; ++u) {
+            const int c = q + 4 * u;
+            if (c >= kUbChunks) continue;
             const uint4 w = se[el * kUbChunks + c];
-            if (c > 0 && !chunk_equal(w, se0[el * kUbChunks + c])) eg[c] = w;
+            if (c > 0 && !chunk_equal(w, e0[u])) eg[c] = w;
         }
     }
 }

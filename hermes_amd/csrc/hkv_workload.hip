@@ -738,56 +738,6 @@ static int wl_wpw()
     return w;
 }
 
-// Whole-wave copies of big ops (op_size a multiple of 8) recorded one per lane (dst null: none), with
-// the header word turned into an INV from this machine (hermes_worker.c:12-65's inv_modify_elem):
-// ceil(op_size / 16) lanes per op move 16 B each, 64 / that many ops per instruction, and two
-// instructions' loads are issued before their stores -- one memory latency per six ops instead of
-// one per op. Every lane of the wave calls it.
-__device__ __forceinline__ void wave_op_copies(uint8_t *dst, const uint8_t *src, uint32_t op_size, uint8_t mid)
-{
-    constexpr int R = 2;
-    const int lane = threadIdx.x & 63;
-    const int C = (int)((op_size + 15) / 16);
-    const int per = 64 / C;
-    const int slot = lane / C, ch = lane - slot * C;
-    unsigned long long todo = __ballot(dst != nullptr);
-    while (todo) {
-        W16 v[R];
-        uint8_t *dp[R];
-        bool half[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            int mine = -1;
-            for (int k = 0; k < per; ++k) {   // this instruction's copies, lane order (todo is uniform)
-                if (!todo) break;
-                const int j = __ffsll((long long)todo) - 1;
-                todo &= todo - 1;
-                if (k == slot) mine = j;
-            }
-            const int sl = mine < 0 ? 0 : mine;
-            const uint64_t d = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(uintptr_t)dst, sl, 64) |
-                               ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)dst >> 32), sl, 64) << 32);
-            const uint64_t sa = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(uintptr_t)src, sl, 64) |
-                                ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)src >> 32), sl, 64) << 32);
-            dp[r] = mine >= 0 && slot < per ? reinterpret_cast<uint8_t *>(d) + 16 * ch : nullptr;
-            half[r] = 16 * ch + 16 > (int)op_size;
-            const uint8_t *sp = reinterpret_cast<const uint8_t *>(sa) + 16 * ch;
-            v[r] = W16{0, 0};
-            if (dp[r]) {
-                if (half[r]) v[r].a = *reinterpret_cast<const uint64_t *>(sp);
-                else v[r] = *reinterpret_cast<const W16 *>(sp);
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (!dp[r]) continue;
-            if (ch == 0) v[r].b = with_op_state(v[r].b, kOpInv, mid);
-            if (half[r]) *reinterpret_cast<uint64_t *>(dp[r]) = v[r].a;
-            else *reinterpret_cast<W16 *>(dp[r]) = v[r];
-        }
-    }
-}
-
 // wings_issue_pkts(inv) with the INV callbacks of hermes_worker.c:12-65. At most out_stride
 // INVs per worker go out per round (the send credits); the rest keep their state and are
 // sent by a later round, as with the reference's credit-limited wings sends.
@@ -813,10 +763,22 @@ __global__ __launch_bounds__(256) void k_marshal_invs(uint8_t *ops, int32_t stri
     }
     out_stride = cap > 0 ? out_stride : 0;  // row stride unchanged; rank < cap below
     const int send_cap = cap;
-    if (op_size > 64) {  // big ops: copied by the whole wave, 16 B per lane, several ops per step
-        const bool mine = send && rank < send_cap;
-        wave_op_copies(mine ? out + ((int64_t)w * out_stride + rank) * op_size : nullptr, op, op_size,
-                       (uint8_t)machine_id);
+    if (op_size > 64) {  // big ops: one op at a time per wave, 8-B word k by lane k
+        const int lane = i & 63;
+        const int words = (int)(op_size / 8);
+        uint8_t *wave_ops = ops + ((int64_t)w * stride + (i & ~63)) * op_size;
+        unsigned long long todo = __ballot(send && rank < send_cap);
+        while (todo) {
+            const int j = __ffsll((long long)todo) - 1;
+            todo &= todo - 1;
+            const int rj = __shfl(rank, j, 64);
+            const uint64_t *src = reinterpret_cast<const uint64_t *>(wave_ops + (int64_t)j * op_size);
+            uint64_t *dst = reinterpret_cast<uint64_t *>(out + ((int64_t)w * out_stride + rj) * op_size);
+            for (int k = lane; k < words; k += 64) {
+                const uint64_t v = src[k];
+                dst[k] = k == 1 ? with_op_state(v, kOpInv, (uint8_t)machine_id) : v;
+            }
+        }
         if (send && rank < send_cap) {
             const uint8_t ns = st == kPutSuccess ? kInProgressPut : st == kRmwSuccess ? kInProgressRmw
                              : st == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
@@ -1677,7 +1639,7 @@ __global__ __launch_bounds__(256) void k_peer_locate(TableView t, const uint8_t 
 // inv_at (may be NULL): INV g sits at element inv_at[g] of invs (a rows layout, hkv_wl_peer_ts_rows)
 __global__ __launch_bounds__(256) void k_peer_ts_at(TableView t, uint8_t *invs, uint8_t *vals, const uint64_t *phys_in,
                                                     int64_t total, uint32_t op_size, unsigned long long *peer_ts,
-                                                    uint32_t round, const int64_t *inv_at, int32_t ts_atomic)
+                                                    uint32_t round, const int64_t *inv_at)
 {
     const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (g >= total) return;
@@ -1710,15 +1672,10 @@ __global__ __launch_bounds__(256) void k_peer_ts_at(TableView t, uint8_t *invs, 
     uint32_t ver = 2;
     if (ok) {
         ver = cur + ((!t.g.rmw_enabled || rmw) ? 2u : 4u);
-        if (peer_ts && peer < 8) {
-            // a peer sends at most one write per key and round, so its word of this entry has one writer
-            // per round and a store does what the max did (HKV_PEER_TS_ATOMIC=1: the atomic max)
-            unsigned long long *pw = peer_ts + peer_slot(t, phys) * 8 + peer;
-            const unsigned long long v = ((unsigned long long)peer_round_tag(round) << 41) |
-                                         ((unsigned long long)rmw << 40) | ((unsigned long long)ver << 8) | peer;
-            if (ts_atomic) atomicMax(pw, v);
-            else *pw = v;
-        }
+        if (peer_ts && peer < 8)
+            atomicMax(peer_ts + peer_slot(t, phys) * 8 + peer,
+                      ((unsigned long long)peer_round_tag(round) << 41) | ((unsigned long long)rmw << 40) |
+                          ((unsigned long long)ver << 8) | peer);
     }
     // bytes 8..15 rewritten whole (opcode, sender, val_len, cid, version): one 8-B store
     const uint64_t nh = (h8 & 0xFFFFFF00ull & 0xFFFFFFFFull) | kOpInv | ((uint64_t)ver << 32);
@@ -1731,11 +1688,6 @@ __global__ __launch_bounds__(256) void k_peer_ts_at(TableView t, uint8_t *invs, 
 using namespace hkv;
 
 static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
-static int peer_ts_atomic()
-{
-    static const int v = getenv("HKV_PEER_TS_ATOMIC") && atoi(getenv("HKV_PEER_TS_ATOMIC")) != 0;
-    return v;
-}
 static inline int ok() { return hipGetLastError() == hipSuccess ? 0 : -5; }
 
 extern "C" {
@@ -2158,7 +2110,7 @@ int hkv_wl_peer_ts_at(hkv_table *t, uint8_t *invs, uint8_t *vals, const uint64_t
     if (table_view(t, &tv) || n < 0 || op_size % 8) return -1;
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_peer_ts_at, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, tv, invs, vals, phys, n,
-                       op_size, peer_ts, round, (const int64_t *)nullptr, peer_ts_atomic());
+                       op_size, peer_ts, round, (const int64_t *)nullptr);
     return ok();
 }
 
@@ -2169,7 +2121,7 @@ int hkv_wl_peer_ts_rows(hkv_table *t, uint8_t *rows, const int64_t *inv_at, uint
     if (table_view(t, &tv) || n < 0 || op_size % 8 || !inv_at) return -1;
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_peer_ts_at, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, tv, rows, vals, phys, n,
-                       op_size, peer_ts, round, inv_at, peer_ts_atomic());
+                       op_size, peer_ts, round, inv_at);
     return ok();
 }
 

@@ -157,6 +157,10 @@ struct hkv_table {
     // the serving kernel (k_hserve): launches are published in a pinned ring instead of launched
     HostRingSlot *ring = nullptr, *ring_d = nullptr;
     uint32_t *srv_words = nullptr, *srv_words_d = nullptr;   // [0] stop, [32..63] exited per workgroup
+    // with callers staging in device memory (HKV_STAGE_VRAM), the ring and the stop word live there
+    // too: the serving kernel polls HBM instead of reading host memory over PCIe every iteration
+    uint32_t *srv_stop = nullptr, *srv_stop_d = nullptr;
+    bool ring_vram = false;
     uint32_t srv_epoch = 0;
     bool srv_running = false;
     hipEvent_t srv_ev = nullptr;
@@ -164,6 +168,13 @@ struct hkv_table {
 };
 
 static void srv_stop(hkv_table *t);   // the serving kernel (see "combining submit") stopped
+static bool stage_vram_usable();
+// the serving kernel's stop word (device memory: write-combined, so flushed at once)
+static void srv_set_stop(hkv_table *t, uint32_t v)
+{
+    __atomic_store_n(t->srv_stop, v, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();
+}
 
 static thread_local std::string g_err;
 static const bool g_trace = getenv("HKV_TRACE") != nullptr;
@@ -383,11 +394,12 @@ int hkv_table_destroy(hkv_table *t)
         if (hs.ev) hipEventDestroy(hs.ev);
     }
     if (t->srv_running) {
-        __atomic_store_n(t->srv_words, 1u, __ATOMIC_RELEASE);
+        srv_set_stop(t, 1u);
         hipEventSynchronize(t->srv_ev);
     }
     if (t->srv_ev) hipEventDestroy(t->srv_ev);
-    if (t->ring) hipHostFree(t->ring);
+    if (t->ring) (void)(t->ring_vram ? hipFree(t->ring) : hipHostFree(t->ring));
+    if (t->ring_vram && t->srv_stop) (void)hipFree(t->srv_stop);
     if (t->srv_words) hipHostFree(t->srv_words);
     if (t->pflags) hipHostFree(t->pflags);
     for (int k = 0; k < t->n_pstreams; ++k) {
@@ -925,9 +937,9 @@ static bool srv_exited(const hkv_table *t)
 static void srv_stop_locked(hkv_table *t)
 {
     if (!t->srv_running) return;
-    __atomic_store_n(t->srv_words, 1u, __ATOMIC_RELEASE);
+    srv_set_stop(t, 1u);
     if (hipEventSynchronize(t->srv_ev) != hipSuccess) die("serving kernel");
-    __atomic_store_n(t->srv_words, 0u, __ATOMIC_RELEASE);
+    srv_set_stop(t, 0u);
     t->srv_running = false;
 }
 
@@ -984,12 +996,12 @@ static void srv_ensure(hkv_table *t)
     sl.ring = t->ring_d;
     sl.ring_n = kRingN;
     sl.epoch = ++t->srv_epoch;
-    sl.stop = t->srv_words_d;
+    sl.stop = t->srv_stop_d;
     sl.exited = t->srv_words_d + 32;
     sl.idle_ticks = (uint64_t)(idle_ms * 1e5);     // wall_clock64: 100 MHz
     sl.life_ticks = (uint64_t)1e8;                 // 1 s, then a fresh server
     for (int g = 0; g < kPartG; ++g) sl.start[g] = __atomic_load_n(t->pflags + g, __ATOMIC_ACQUIRE) + 1;
-    __atomic_store_n(t->srv_words, 0u, __ATOMIC_RELEASE);
+    srv_set_stop(t, 0u);
     if (!t->srv_ev && hipEventCreateWithFlags(&t->srv_ev, hipEventDisableTiming) != hipSuccess) die("event");
     part_join(t);
     if (launch_host_serve(sl, t->stream) || hipEventRecord(t->srv_ev, t->stream) != hipSuccess) die("serving kernel launch");
@@ -1047,13 +1059,26 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
         for (int g = 0; g < kPartG; ++g) __atomic_store_n(t->pflags + g, 0u, __ATOMIC_RELEASE);
     }
     if (serve && !t->ring) {
-        if (hipHostMalloc((void **)&t->ring, sizeof(HostRingSlot) * kRingN, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-            hipHostGetDevicePointer((void **)&t->ring_d, t->ring, 0) != hipSuccess ||
-            hipHostMalloc((void **)&t->srv_words, 4 * 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        if (hipHostMalloc((void **)&t->srv_words, 4 * 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
             hipHostGetDevicePointer((void **)&t->srv_words_d, t->srv_words, 0) != hipSuccess)
             die("ring alloc");
-        memset(t->ring, 0, sizeof(HostRingSlot) * kRingN);
         for (int k = 0; k < 64; ++k) __atomic_store_n(t->srv_words + k, 0u, __ATOMIC_RELEASE);
+        t->ring_vram = stage_vram_usable();
+        if (t->ring_vram) {
+            if (hipExtMallocWithFlags((void **)&t->ring, sizeof(HostRingSlot) * kRingN, hipDeviceMallocFinegrained) != hipSuccess ||
+                hipExtMallocWithFlags((void **)&t->srv_stop, 64, hipDeviceMallocFinegrained) != hipSuccess)
+                die("ring alloc");
+            t->ring_d = t->ring;
+            t->srv_stop_d = t->srv_stop;
+        } else {
+            if (hipHostMalloc((void **)&t->ring, sizeof(HostRingSlot) * kRingN, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+                hipHostGetDevicePointer((void **)&t->ring_d, t->ring, 0) != hipSuccess)
+                die("ring alloc");
+            t->srv_stop = t->srv_words;
+            t->srv_stop_d = t->srv_words_d;
+        }
+        memset(t->ring, 0, sizeof(HostRingSlot) * kRingN);
+        srv_set_stop(t, 0u);
     }
     for (uint32_t spins = 0; (int32_t)(t->pseq - part_done(t)) >= inflight; ++spins) {
         if (serve && t->srv_running && srv_exited(t)) srv_ensure(t);   // a server that left has work to do
@@ -1108,7 +1133,9 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
         slot.n_batches = nb;
         memcpy(slot.hdr, pl.hdr, sizeof(HostPartHdr) * (size_t)nb);
         memcpy(slot.part, pl.part, sizeof slot.part);
+        __builtin_ia32_sfence();   // device memory is write-combined: the slot's bytes before its seq
         __atomic_store_n(&slot.seq, seq, __ATOMIC_RELEASE);
+        __builtin_ia32_sfence();
         lk.lock();
         srv_ensure(t);
     } else {
@@ -1146,7 +1173,7 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
 // with a guarded store, falling back to pinned staging when it faults.
 static sigjmp_buf g_vram_jb;
 static void vram_probe_fault(int) { siglongjmp(g_vram_jb, 1); }
-static bool stage_vram_usable()
+static bool probe_vram()
 {
     if (getenv("HKV_STAGE_VRAM") && atoi(getenv("HKV_STAGE_VRAM")) == 0) return false;
     void *p = nullptr;
@@ -1168,6 +1195,11 @@ static bool stage_vram_usable()
     (void)hipFree(p);
     TRACE("caller staging in device memory: %s", ok ? "yes" : "no (pinned)");
     return ok;
+}
+static bool stage_vram_usable()
+{
+    static const bool v = probe_vram();
+    return v;
 }
 
 // Stages a caller's batch for a partitioned launch in its thread's pinned buffer (see "combining
@@ -1196,7 +1228,7 @@ static bool host_stage_part(const hkv_table *t, HostReq &r)
             die("caller staging alloc");
         st.cap = cap;
     }
-    static const bool vram = stage_vram_usable();
+    const bool vram = stage_vram_usable();
     if (vram && ebytes + pbytes > st.vcap) {
         if (st.v) (void)hipFree(st.v);
         st.v = nullptr;

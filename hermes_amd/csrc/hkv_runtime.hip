@@ -1026,11 +1026,13 @@ static uint32_t part_done(const hkv_table *t)
 // first waits for the oldest, and batches queued meanwhile join its launch. Called with t->hmu held.
 static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
 {
-    // HKV_HOST_SERVE=1: publish to the serving kernel (k_hserve) instead of one k_hpart launch per
-    // combined batch. Measured, not adopted: the same rates (6.4 / 22.8 / 41.1 M local ops/s from
-    // 1 / 8 / 16 threads with launches, 5.7 / 23.3 / 40.7 M served): a launch's dispatch is not what
-    // bounds a call, its PCIe round trips are (descriptor, elements, results: about 2.5 us each)
-    static const bool serve = getenv("HKV_HOST_SERVE") && atoi(getenv("HKV_HOST_SERVE")) != 0;
+    // Serving kernel (k_hserve): launches are published to a ring that a persistent kernel polls,
+    // instead of one k_hpart launch per combined batch. With the ring and the callers' batches in host
+    // memory it ran at the launches' rates (round 3: the PCIe reads of descriptor and elements bound a
+    // call); with both in device memory (stage_vram_usable) it is the default: same box, 3 reps each
+    // (gpurun_out/r04z), 8.6-8.8 / 24.0-27.0 / 40.7-43.7 M local ops/s from 1 / 8 / 16 threads against
+    // 6.1-6.9 / 23.0-26.0 / 35.6-44.1 M launched. HKV_HOST_SERVE=0 / 1 forces either.
+    static const bool serve = getenv("HKV_HOST_SERVE") ? atoi(getenv("HKV_HOST_SERVE")) != 0 : stage_vram_usable();
     // HKV_PART_STREAMS=n (at most kPartStreams): the launches go round n streams, each partition's
     // launches ordered on the device. Measured, not adopted (round 4): 4 streams ran 8 / 16 caller
     // threads at 7.9-9.3 / 14.5-15.7 M local ops/s against 20.4-21.0 / 34.9-36.0 M on the one table

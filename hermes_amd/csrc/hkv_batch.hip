@@ -1521,12 +1521,8 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         op[k] = make_uint4(0u, 0u, 0u, 0u);
         if (live[k]) {
             const uint8_t *xg = a.elems + i * 56 + 16 * q;
-            // the patch is loaded beside the op either way (a load that waits for the mirror byte first
-            // measured slower: local 386 -> 404 us); an unmarked slot's stale patch is then dropped
             U64x2 p{0, 0};
-            const uint8_t om = a.sparse_patch ? a.opc[i] : (uint8_t)0x80u;
-            if (a.patch) p = *reinterpret_cast<const U64x2 *>(a.patch + i * 16);
-            if (!(om & 0x80u)) p = U64x2{0, 0};
+            if (a.patch && (!a.sparse_patch || (a.opc[i] & 0x80u))) p = *reinterpret_cast<const U64x2 *>(a.patch + i * 16);
             if (q < 3) {
                 op[k] = *reinterpret_cast<const uint4 *>(xg);
             } else {

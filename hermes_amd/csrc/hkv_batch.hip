@@ -108,8 +108,6 @@ struct BatchArgs {
     int32_t vc_batch;            // values per step of those wave copies (HKV_VC_BATCH, 1 or kVcBatch)
     int32_t wave_shadow;         // big entries: candidates applied by the whole wave (HKV_WAVE_SHADOW=0: per lane)
     int32_t cancel;              // k_local_pre undoes its tags (HKV_BATCH_PREPASS_CANCEL)
-    int32_t sparse_patch;        // HKV_BATCH_SPARSE_PATCH: a patch is valid where the opcode mirror has 0x80
-    uint8_t *opc_w;              // the opcode mirror, written back (bit cleared) where a patch applied
     uint8_t *ack_out;            // INV launches: each element's ACK (hkv_batch_desc.d_ack_out), or NULL
     uint32_t ack_out_size;
 };
@@ -1207,8 +1205,7 @@ __device__ __forceinline__ bool patch_valid(uint64_t pb) { return ((pb >> 48) & 
 // the key of element i as the launch sees it (patched or not)
 __device__ __forceinline__ uint64_t elem_key(const BatchArgs &a, int64_t i)
 {
-    if (a.patch && (a.sparse_patch ? (a.opc[i] & 0x80u) != 0 : a.patch[i * 16 + 14] != 0))
-        return *reinterpret_cast<const uint64_t *>(a.patch + i * 16);
+    if (a.patch && a.patch[i * 16 + 14]) return *reinterpret_cast<const uint64_t *>(a.patch + i * 16);
     return *reinterpret_cast<const uint64_t *>(a.elems + i * a.esz);
 }
 
@@ -1239,15 +1236,10 @@ __device__ __forceinline__ uint4 patch_chunk(uint4 w, int q, uint64_t pa, uint64
 // Every other path: the patches go into the ops first (one thread per element), then the launch
 // runs as usual
 __global__ __launch_bounds__(256) void k_apply_patch(uint8_t *elems, const uint8_t *patch, int64_t n, int32_t esz,
-                                                     uint32_t st_value, uint8_t *sparse_opc)
+                                                     uint32_t st_value)
 {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    if (sparse_opc) {   // HKV_BATCH_SPARSE_PATCH: valid where the mirror byte has 0x80, which then goes
-        const uint8_t om = sparse_opc[i];
-        if (!(om & 0x80u)) return;
-        sparse_opc[i] = (uint8_t)(om & 0x7Fu);
-    }
     const U64x2 p = *reinterpret_cast<const U64x2 *>(patch + i * 16);
     if (!patch_valid(p.b)) return;
     uint8_t *x = elems + i * esz;
@@ -1342,7 +1334,6 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
     U64x2 h[kAllK];
     bool in[kAllK];
     uint8_t opm[kAllK];
-    bool pvb[kAllK];
     U64x2 pt[kAllK];
     if (a.pkeys) {
         // the caller's PUT-key mirror and entry states (hkv_batch_desc.d_put_keys): two dense arrays,
@@ -1372,9 +1363,6 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
         const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
         in[k] = i < a.n && (own || i < head_end);
         opm[k] = a.opc ? a.opc[in[k] ? i : 0] : (uint8_t)kOpPut;
-        // HKV_BATCH_SPARSE_PATCH: bit 0x80 marks a patched slot (its patch is the one to read)
-        pvb[k] = !a.sparse_patch || (opm[k] & 0x80u);
-        opm[k] &= 0x7Fu;
     }
     if (a.pre_patch_first && a.patch) {
         // the patches first: a refilled PUT's patch holds all the prepass needs (key, opcode, ST_NEW),
@@ -1384,7 +1372,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
         for (int k = 0; k < kAllK; ++k) {
             const bool own = k < kOwnK;
             const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
-            pt[k] = in[k] && opm[k] == kOpPut && pvb[k] ? *reinterpret_cast<const U64x2 *>(a.patch + i * 16) : U64x2{0, 0};
+            pt[k] = in[k] && opm[k] == kOpPut ? *reinterpret_cast<const U64x2 *>(a.patch + i * 16) : U64x2{0, 0};
         }
 #pragma unroll
         for (int k = 0; k < kAllK; ++k) {
@@ -1398,7 +1386,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
             const bool own = k < kOwnK;
             const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
             h[k] = *reinterpret_cast<const U64x2 *>(a.elems + (in[k] && opm[k] == kOpPut ? i : 0) * 56);
-            pt[k] = a.patch && in[k] && opm[k] == kOpPut && pvb[k] ? *reinterpret_cast<const U64x2 *>(a.patch + i * 16) : U64x2{0, 0};
+            pt[k] = a.patch && in[k] && opm[k] == kOpPut ? *reinterpret_cast<const U64x2 *>(a.patch + i * 16) : U64x2{0, 0};
         }
     }
 #pragma unroll
@@ -1522,7 +1510,7 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         if (live[k]) {
             const uint8_t *xg = a.elems + i * 56 + 16 * q;
             U64x2 p{0, 0};
-            if (a.patch && (!a.sparse_patch || (a.opc[i] & 0x80u))) p = *reinterpret_cast<const U64x2 *>(a.patch + i * 16);
+            if (a.patch) p = *reinterpret_cast<const U64x2 *>(a.patch + i * 16);
             if (q < 3) {
                 op[k] = *reinterpret_cast<const uint4 *>(xg);
             } else {
@@ -1609,11 +1597,7 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
             x[9] = kMiss;
         }
         // k_local_pre read only the PUTs the caller's opcode mirror names
-        if (a.opc) {
-            const uint8_t om = a.opc[i];
-            if (sprb[tid] && x[8] == kOpPut && (om & 0x7Fu) != kOpPut && a.error_flags) atomicOr(a.error_flags, 8u);
-            if (a.sparse_patch && (om & 0x80u)) a.opc_w[i] = (uint8_t)(om & 0x7Fu);   // its patch is applied
-        }
+        if (a.opc && sprb[tid] && x[8] == kOpPut && a.opc[i] != kOpPut && a.error_flags) atomicOr(a.error_flags, 8u);
         a.ent[i] = e;
         a.st[i] = st;
         if (st != kStDefer) note_state(a, i, x);
@@ -3302,8 +3286,6 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.offsets = bl.offsets;
     a.state_out = (bl.type == kLocal || bl.type == kLocalAfterMemb) ? bl.state_out : nullptr;
     a.opc = bl.type == kLocal ? bl.opcode_in : nullptr;
-    a.sparse_patch = bl.sparse_patch;
-    a.opc_w = bl.opcode_w;
     a.patch = nullptr;
     a.pkeys = nullptr;
     a.cancel = bl.stage == 3;
@@ -3403,8 +3385,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         return hipGetLastError() == hipSuccess ? 0 : -3;
     }
     if (bl.patch && (small || !local_direct || patch_apply_env)) {  // the other paths take the patches as op writes first
-        hipLaunchKernelGGL(k_apply_patch, dim3(grid), dim3(256), 0, s, bl.elems, bl.patch, n, bl.esz, bl.g.st_value,
-                           bl.sparse_patch ? bl.opcode_w : (uint8_t *)nullptr);
+        hipLaunchKernelGGL(k_apply_patch, dim3(grid), dim3(256), 0, s, bl.elems, bl.patch, n, bl.esz, bl.g.st_value);
     } else if (bl.patch) {
         a.patch = bl.patch;
     }

@@ -18,8 +18,6 @@ struct BatchLaunch {
     uint8_t *state_out;          // local launches: each element's final state byte (may be NULL)
     const uint8_t *opcode_in;    // local launches: the caller's mirror of each element's opcode (may be NULL)
     const uint8_t *patch;        // local launches: pending header writes, 16 B per element (may be NULL)
-    int32_t sparse_patch;        // HKV_BATCH_SPARSE_PATCH: patches valid where opcode_in has bit 0x80
-    uint8_t *opcode_w;           // the same mirror, written back by the launch (sparse patches)
     uint8_t *rw_state;           // ACK launches: state-byte mirror of read_write_ops (may be NULL)
     const uint64_t *put_keys;    // local launches: PUT-key mirror (state_out holds the entry states), or NULL
     const uint8_t *index;

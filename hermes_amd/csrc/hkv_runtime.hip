@@ -561,12 +561,6 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     static const bool pk_off = getenv("HKV_PUT_KEYS") && atoi(getenv("HKV_PUT_KEYS")) == 0;
     bl.put_keys = d->type == kLocal && d->d_state_out && !pk_off ? d->d_put_keys : nullptr;
     if (bl.patch && ((uintptr_t)bl.patch & 15)) return fail(-1, "d_patch must be 16-byte aligned");
-    bl.sparse_patch = d->type == kLocal && (d->flags & HKV_BATCH_SPARSE_PATCH) ? 1 : 0;
-    if (bl.sparse_patch) {   // the launch rewrites the mirror bytes of the patches it applies
-        if (!bl.patch || !bl.opcode_in || bl.put_keys)
-            return fail(-1, "HKV_BATCH_SPARSE_PATCH: local launches with d_patch and d_opcode_in, without d_put_keys");
-        bl.opcode_w = const_cast<uint8_t *>(d->d_opcode_in);
-    }
     if (bl.put_keys && ((uintptr_t)bl.put_keys & 7)) return fail(-1, "d_put_keys must be 8-byte aligned");
     bl.offsets = packed ? d->d_counts : nullptr;
     bl.index = t->d_index;

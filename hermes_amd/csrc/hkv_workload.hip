@@ -565,13 +565,11 @@ __global__ __launch_bounds__(256) void k_refill_plan_w(uint8_t *states, int32_t 
                       ((uint64_t)((o == kOpRmw ? 1u : 0u) | 2u) << 16) |
                       ((uint64_t)(get ? 0u : (uint8_t)('a' + machine_id)) << 32) |
                       ((uint64_t)(get && (flags & HKV_WL_READ_TS_RESET) ? 1u : 0u) << 40) | (1ull << 48);
-                opc[e] = (flags & HKV_WL_SPARSE_PATCH) ? (uint8_t)(o | 0x80u) : o;
+                opc[e] = o;
                 if (put_keys) {   // the PUT-key mirror and the entry state of the patched op
                     put_keys[e] = o == kOpPut ? p.a : HKV_NO_PUT;
                     states[e] = kNew;
                 }
-            } else if (flags & HKV_WL_SPARSE_PATCH) {
-                continue;   // a kept slot: its patch bytes are not read (its mirror byte has no 0x80)
             }
             *reinterpret_cast<W16 *>(patch + e * 16) = p;
         }
@@ -1761,9 +1759,8 @@ int hkv_wl_refill_plan(uint8_t *states, int32_t n_workers, int32_t stride, uint3
                        uint64_t *put_keys, void *stream)
 {
     if (stride > 256 || n_workers <= 0 || tlen <= 0 || !states || !opc || !patch) return -1;
-    if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET | HKV_WL_SPARSE_PATCH)) return -1;   // no hot-request coalescing
+    if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET)) return -1;   // no hot-request coalescing
     if (((uintptr_t)patch & 15) || ((uintptr_t)put_keys & 7) || st_value > 255) return -1;
-    if ((flags & HKV_WL_SPARSE_PATCH) && put_keys) return -1;
     if (wl_wpw() == 2)
         hipLaunchKernelGGL(k_refill_plan_w<2>, dim3((unsigned)((n_workers + 7) / 8)), dim3(256), 0, (hipStream_t)stream,
                            states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,

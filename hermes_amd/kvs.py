@@ -90,7 +90,6 @@ BATCH_ROWS = 16    # with BATCH_UNIQUE: rows of one layout, element j of every r
 BATCH_PREPASS = 32     # a local launch's prepass only (its own stream; see include/hermeskv.h)
 BATCH_PREPASSED = 64   # the rest of that launch
 BATCH_PREPASS_CANCEL = 128   # or: that launch will not run (its prepass's tags undone)
-BATCH_SPARSE_PATCH = 256     # patches valid where the opcode mirror has bit 0x80 (the launch clears it)
 
 
 class HermesKV:
@@ -177,7 +176,7 @@ class HermesKV:
               patch: torch.Tensor | None = None, rw_state: torch.Tensor | None = None,
               unique: bool = False, put_keys: torch.Tensor | None = None,
               rows: tuple[int, int, int] | None = None, stage: int = 0,
-              ack_out: torch.Tensor | None = None, ack_out_size: int = 16, sparse_patch: bool = False) -> None:
+              ack_out: torch.Tensor | None = None, ack_out_size: int = 16) -> None:
         """Apply n_batches batches of one type, concatenated in `elems` (uint8, on the GPU),
         in concatenation order, asynchronously on `stream` (default: torch's current).
         offsets (INV / ACK / VAL batches): the batches stored back to back, batch b at elements
@@ -191,9 +190,7 @@ class HermesKV:
         row order in one pass (HKV_BATCH_ROWS; skip_row -1: none). stage (local batches): 1 runs only the
         launch's prepass (HKV_BATCH_PREPASS), 2 the rest of it (HKV_BATCH_PREPASSED), 3 cancels it
         (HKV_BATCH_PREPASS_CANCEL), 0 runs all of it. ack_out (unique INV launches): every element's ACK
-        as the worker's ACK callbacks make it, ack_out_size bytes each (hkv_batch_desc.d_ack_out).
-        sparse_patch (local batches with patch and opcode_in): a patch is valid only where the opcode
-        mirror byte has bit 0x80, which the launch clears (HKV_BATCH_SPARSE_PATCH)."""
+        as the worker's ACK callbacks make it, ack_out_size bytes each (hkv_batch_desc.d_ack_out)."""
         assert elems.is_cuda and elems.dtype == torch.uint8
         total = stride if offsets is not None else n_batches * stride
         if rows is not None:
@@ -222,9 +219,6 @@ class HermesKV:
         if patch is not None:
             assert patch.is_cuda and patch.dtype == torch.uint8 and patch.numel() >= n_batches * stride * 16
             d.d_patch = patch.data_ptr()
-        if sparse_patch:
-            assert patch is not None and opcode_in is not None and put_keys is None
-            d.flags |= BATCH_SPARSE_PATCH
         if rw_state is not None:
             assert rw_state.is_cuda and rw_state.dtype == torch.uint8
             d.d_rw_state = rw_state.data_ptr()

@@ -80,7 +80,6 @@ _L.hkv_wl_peer_ts_words.argtypes = [_P]
 REFILL_ALL = 1      # hkv_wl_refill flags (include/hermeskv_workload.h)
 READ_TS_RESET = 2
 COALESCE_HOT = 4
-HKV_WL_SPARSE_PATCH = 8   # hkv_wl_refill_plan: patches of refilled slots only, marked in the opcode mirror
 HOT_KEYS = 100      # COALESCE_N_HOTTEST_KEYS, config.h:78
 
 
@@ -176,10 +175,7 @@ class CommitAudit:
         patch = getattr(self.r, "patch", None)
         if getattr(self.r, "fused", False) and patch is not None:
             p = patch.view(-1, 16)
-            if getattr(self.r, "sparse_patch", False):   # only the marked slots' patches are current
-                fresh, oc = (self.r.opcodes & 0x80) != 0, p[:, 8]
-            else:
-                fresh, oc = p[:, 14] == 1, p[:, 8]
+            fresh, oc = p[:, 14] == 1, p[:, 8]
         else:
             fresh, oc = ops[:, 9] == int(L.Bucket.NEW), ops[:, 8]
         tsv = ops[:, 12:16].contiguous().view(torch.int32).view(-1)
@@ -277,17 +273,12 @@ class Round:
         self.states = torch.zeros(W * S, **u8)   # the local batch's mirror of every op's state byte
         self.opcodes = torch.zeros(W * S, **u8)  # the refill's mirror of every op's opcode byte
         self.patch = torch.zeros(W * S * 16, **u8) if self.fused else None   # planned refills (d_patch)
-        # sparse patches (HKV_SPARSE_PATCH=1): the plan writes the patches of refilled slots only and marks
-        # them in the opcode mirror; the launch reads only those (HKV_BATCH_SPARSE_PATCH)
-        self.sparse_patch = False
         # the PUT-key mirror (d_put_keys) the plan keeps beside the state mirror, from which the local launch
         # could find its PUTs without reading ops (HKV_PUT_KEYS=1). Measured, not adopted (round 4): the
         # prepass stays at 83 us (its atomics and seqlock tags, not its loads, bound it now) and the mirror
         # checks cost the fused pass 10-20 us
         self.put_keys = (torch.zeros(W * S, dtype=torch.int64, device=dev)
                          if self.fused and os.environ.get("HKV_PUT_KEYS", "0") == "1" else None)
-        self.sparse_patch = (self.fused and self.put_keys is None
-                             and os.environ.get("HKV_SPARSE_PATCH", "0") == "1")
         self.C = slots_per_worker(write_permille, rmw_permille)   # INV send credits per worker
         self.inv_out = torch.zeros(W * self.C * self.op, **u8)
         self.inv_count = torch.zeros(W, dtype=torch.int32, device=dev)
@@ -505,9 +496,8 @@ class Round:
         if self.fused and not first:   # a plan the next local launch applies (the ops stay as they are)
             check(_L.hkv_wl_refill_plan(_ptr(self.states), self.W, self.LOCAL, self.sizes.st_value, self.sizes.shift,
                                         _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
-                                        self.machine_id, self.rflags | (HKV_WL_SPARSE_PATCH if self.sparse_patch else 0),
-                                        _ptr(self.counters), _ptr(self.opcodes), _ptr(self.patch), _ptr(self.put_keys),
-                                        _s()), "refill_plan")
+                                        self.machine_id, self.rflags, _ptr(self.counters), _ptr(self.opcodes),
+                                        _ptr(self.patch), _ptr(self.put_keys), _s()), "refill_plan")
             return
         if self.st_refill and not first:
             check(_L.hkv_wl_refill_st(_ptr(self.ops), self.W, self.LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
@@ -525,8 +515,7 @@ class Round:
 
     def _local(self, stage: int, stream=None):
         self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb, state_out=self.states,
-                       opcode_in=self.opcodes, patch=self.patch, put_keys=self.put_keys, stage=stage, stream=stream,
-                       sparse_patch=self.sparse_patch)
+                       opcode_in=self.opcodes, patch=self.patch, put_keys=self.put_keys, stage=stage, stream=stream)
 
     def prepass(self, overlap: bool, events: dict | None = None):
         """Stage 1 of the next local launch: on the side stream after what the current stream holds

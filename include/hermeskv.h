@@ -164,8 +164,8 @@ typedef struct hkv_batch_desc {
                                    worker's ACK callbacks make it (hermes_worker.c:69-118: an ACK from this
                                    machine for INV_SUCCESS, the element itself as INV-abort when ack_out_size holds
                                    it, else opcode ST_EMPTY), written to d_ack_out + i * ack_out_size by the launch
-                                   itself, and each answered element leaves with opcode ST_EMPTY, as after the
-                                   callbacks' send (ack_modify_elem_after_send). NULL = none (ABI 6) */
+                                   itself; the elements keep the batch's output (the callbacks' after-send reset of
+                                   their opcode is the caller's). NULL = none (ABI 6) */
     uint32_t ack_out_size;
 } hkv_batch_desc;
 #define HKV_NO_PUT 0xFFFFFFFFFFFFFFFFull
@@ -214,11 +214,6 @@ typedef struct hkv_batch_desc {
 /* instead of HKV_BATCH_PREPASSED: the launch will not run; undo what its prepass left in the table
  * (the seqlock bytes it used as tags), so the table is the reference's image again */
 #define HKV_BATCH_PREPASS_CANCEL 128u
-/* Local launches with d_patch and d_opcode_in: a patch is valid only where the opcode mirror byte has
- * bit 0x80 set (its low bits are the patched opcode), and only those patches are read. The launch
- * applies them and rewrites those mirror bytes to the op's opcode (bit cleared), so a refill writes
- * the patches of the slots it refills and nothing else (hkv_wl_refill_plan with HKV_WL_SPARSE_PATCH). */
-#define HKV_BATCH_SPARSE_PATCH 256u
 #define HKV_MAX_ROWS 8
 int  hkv_abi_version(void);
 const char *hkv_last_error(void);

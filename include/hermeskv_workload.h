@@ -73,9 +73,6 @@ int hkv_wl_gen_trace(uint64_t *d_trace_key, uint8_t *d_trace_op, uint32_t *d_tra
 #define HKV_WL_REFILL_ALL    1u
 #define HKV_WL_READ_TS_RESET 2u
 #define HKV_WL_COALESCE_HOT  4u
-/* hkv_wl_refill_plan only: write the patches of refilled slots only, and mark each in the opcode
- * mirror (opcode | 0x80), for local launches with HKV_BATCH_SPARSE_PATCH */
-#define HKV_WL_SPARSE_PATCH  8u
 #define HKV_WL_HOT_KEYS      100
 int hkv_wl_refill(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint32_t st_value,
                   uint32_t shift, const uint64_t *d_trace_key, const uint8_t *d_trace_op, const uint32_t *d_trace_id,

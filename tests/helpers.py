@@ -122,12 +122,12 @@ class Mirror:
     def batch(self, btype, elems, n_batches, stride, elem_size, membership, counts=None, rw=None,
               rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None, state_out=None, opcode_in=None,
               patch=None, rw_state=None, unique=False, put_keys=None, rows=None, stage=0, ack_out=None,
-              ack_out_size=16, sparse_patch=False):
+              ack_out_size=16):
         import torch
         if stage in (1, 3):   # a prepass (or its cancellation) changes no element and nothing of the meta
             self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
                        node_suspected, stream, state_out=state_out, opcode_in=opcode_in, patch=patch,
-                       rw_state=rw_state, unique=unique, put_keys=put_keys, stage=stage, sparse_patch=sparse_patch)
+                       rw_state=rw_state, unique=unique, put_keys=put_keys, stage=stage)
             self.prepass = stage == 1
             if stage == 3:
                 torch.cuda.synchronize()
@@ -143,16 +143,15 @@ class Mirror:
         n = n_batches * stride * elem_size
         vt = np.dtype((np.void, elem_size))
         e_in = elems[:n].cpu().numpy().copy()
-        opc_in = opcode_in[: n_batches * stride].cpu().numpy().copy() if opcode_in is not None else None
         if patch is not None:   # the pending refill the launch applies first (hkv_batch_desc.d_patch)
             from tests.test_workload_gpu import _apply_patches
             e_in = _apply_patches(e_in, patch[: n_batches * stride * 16].cpu().numpy(), elem_size,
-                                  self.g.sizes.st_value, (opc_in & 0x80) != 0 if sparse_patch else None)
+                                  self.g.sizes.st_value)
         e_in = e_in.view(vt)
         e_orig = e_in.copy()
         c_in = counts[:n_batches].cpu().numpy().copy() if counts is not None else None
         if opcode_in is not None:   # the caller's opcode mirror must be every element's opcode byte
-            assert np.array_equal(opc_in & (0x7F if sparse_patch else 0xFF),
+            assert np.array_equal(opcode_in[: n_batches * stride].cpu().numpy(),
                                   np.frombuffer(e_in.tobytes(), np.uint8).reshape(-1, elem_size)[:, 8])
         if put_keys is not None:   # the PUT-key mirror and the entry states describe the (patched) elements
             eb = np.frombuffer(e_in.tobytes(), np.uint8).reshape(-1, elem_size)
@@ -167,13 +166,9 @@ class Mirror:
         rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
         self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
                    node_suspected, stream, state_out=state_out, opcode_in=opcode_in, patch=patch, rw_state=rw_state,
-                   unique=unique, put_keys=put_keys, stage=stage, sparse_patch=sparse_patch)
+                   unique=unique, put_keys=put_keys, stage=stage)
         if stage == 2:
             self.prepass = False
-        if sparse_patch:   # the launch cleared the marks of the patches it applied
-            torch.cuda.synchronize()
-            assert np.array_equal(opcode_in[: n_batches * stride].cpu().numpy(), opc_in & 0x7F), \
-                "opcode mirror marks not cleared"
         torch.cuda.synchronize()
         self.o.batch_multi(int(btype), e_in, n_batches, stride, c_in, membership, rw_in,
                            rw_stride_bytes // self.g.sizes.op if rw is not None else 0)

@@ -458,12 +458,11 @@ def test_refill_kernel_matches_numpy(big, flags):
     assert np.array_equal(d_opc.cpu().numpy(), exp_ops.reshape(W * S, osz)[:, 8])
 
 
-def _apply_patches(ops, patch, osz, st_value, marks=None):
-    """d_patch applied in numpy (include/hermeskv.h: the 16-B layout and what applying does); marks
-    (HKV_BATCH_SPARSE_PATCH): only these slots' patches are valid"""
+def _apply_patches(ops, patch, osz, st_value):
+    """d_patch applied in numpy (include/hermeskv.h: the 16-B layout and what applying does)"""
     ops = ops.copy().reshape(-1, osz)
     p = patch.reshape(-1, 16)
-    for i in np.nonzero(p[:, 14] if marks is None else marks)[0]:
+    for i in np.nonzero(p[:, 14])[0]:
         o = ops[i]
         o[0:8] = p[i, 0:8]
         o[8], o[9], o[10] = p[i, 8], 141, p[i, 9]
@@ -521,48 +520,6 @@ def test_refill_plan_matches_refill(flags):
     assert np.array_equal(d_pk.cpu().numpy()[~refilled], pk0[~refilled])
     assert np.array_equal(d_st.cpu().numpy()[refilled], e[refilled, 9])
     assert np.array_equal(d_st.cpu().numpy()[~refilled], ops.reshape(W * S, osz)[~refilled, 9])
-
-
-@pytest.mark.parametrize("flags", [0, 2])
-def test_refill_plan_sparse_patches(flags):
-    """hkv_wl_refill_plan with HKV_WL_SPARSE_PATCH: only refilled slots get a patch, each marked in the
-    opcode mirror (opcode | 0x80); the other slots' patch bytes are not written and their mirror bytes
-    keep their value. Applying the marked patches gives exactly what hkv_wl_refill gives."""
-    from hermes_amd import workload as WL
-    sz = L.DEFAULT
-    W, S, osz, tlen, mid = 23, 250, sz.op, 300, 1
-    rng = np.random.default_rng(91 + flags)
-    states = np.array([130, 128, 138, 137, 119, 121, 131, 132, 136, 140, 141, *IN_FLIGHT], dtype=np.uint8)
-    ops = rng.integers(0, 256, size=W * S * osz, dtype=np.uint8)
-    ops.reshape(W, S, osz)[:, :, 9] = rng.choice(states, size=(W, S))
-    ops.reshape(W, S, osz)[:, :, 8] = rng.choice(np.array([111, 112, 113], dtype=np.uint8), size=(W, S))
-    tkey = rng.integers(0, 2**63, size=W * tlen, dtype=np.int64)
-    top = rng.choice(np.array([111, 112, 113], dtype=np.uint8), size=W * tlen)
-    cursor = rng.integers(0, tlen, size=W, dtype=np.int32)
-    exp_ops, exp_cur, exp_cnt = _refill_ref(ops, W, S, osz, sz.st_value, sz.shift, tkey.view(np.uint64), top, tlen,
-                                            cursor, mid, False, flags)
-    d_st = torch.from_numpy(ops.reshape(W * S, osz)[:, 9].copy()).cuda()
-    d_tkey, d_top = torch.from_numpy(tkey).cuda(), torch.from_numpy(top).cuda()
-    d_cur = torch.from_numpy(cursor.copy()).cuda()
-    d_cnt = torch.zeros(4096, dtype=torch.int64, device="cuda")
-    opc0 = ops.reshape(W * S, osz)[:, 8].copy()
-    d_opc = torch.from_numpy(opc0.copy()).cuda()
-    d_patch = torch.full((W * S * 16,), 0xAB, dtype=torch.uint8, device="cuda")   # kept slots keep these bytes
-    WL.check(WL._L.hkv_wl_refill_plan(WL._ptr(d_st), W, S, sz.st_value, sz.shift, WL._ptr(d_tkey), WL._ptr(d_top),
-                                      tlen, WL._ptr(d_cur), mid, flags | WL.HKV_WL_SPARSE_PATCH, WL._ptr(d_cnt),
-                                      WL._ptr(d_opc), WL._ptr(d_patch), None, None), "refill_plan")
-    WL.check(WL._L.hkv_wl_fold_counters(WL._ptr(d_cnt), None), "fold")
-    torch.cuda.synchronize()
-    opc, patch = d_opc.cpu().numpy(), d_patch.cpu().numpy().reshape(-1, 16)
-    marks = (opc & 0x80) != 0
-    assert (patch[~marks] == 0xAB).all(), "a kept slot's patch was written"
-    assert (patch[marks, 14] == 1).all()
-    got = _apply_patches(ops, patch.reshape(-1), osz, sz.st_value, marks)
-    assert np.array_equal(got, exp_ops), "patched ops differ from the refill"
-    assert np.array_equal(opc & 0x7F, exp_ops.reshape(W * S, osz)[:, 8])
-    assert np.array_equal(opc[~marks], opc0[~marks])
-    assert np.array_equal(d_cur.cpu().numpy(), exp_cur)
-    assert d_cnt[:5].cpu().tolist() == exp_cnt.tolist()
 
 
 @pytest.mark.parametrize("mirror", [False, True])

@@ -164,8 +164,8 @@ typedef struct hkv_batch_desc {
                                    worker's ACK callbacks make it (hermes_worker.c:69-118: an ACK from this
                                    machine for INV_SUCCESS, the element itself as INV-abort when ack_out_size holds
                                    it, else opcode ST_EMPTY), written to d_ack_out + i * ack_out_size by the launch
-                                   itself; the elements keep the batch's output (the callbacks' after-send reset of
-                                   their opcode is the caller's). NULL = none (ABI 6) */
+                                   itself, and each answered element leaves with opcode ST_EMPTY, as after the
+                                   callbacks' send (ack_modify_elem_after_send). NULL = none (ABI 6) */
     uint32_t ack_out_size;
 } hkv_batch_desc;
 #define HKV_NO_PUT 0xFFFFFFFFFFFFFFFFull

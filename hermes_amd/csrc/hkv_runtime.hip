@@ -14,6 +14,7 @@
 #include <cstring>
 #include <sched.h>
 #include <unistd.h>
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <deque>
@@ -169,6 +170,8 @@ struct hkv_table {
 
 static void srv_stop(hkv_table *t);   // the serving kernel (see "combining submit") stopped
 static bool stage_vram_usable();
+static std::mutex g_srv_mu;                      // tables whose serving kernel was started (srv_atexit)
+static std::vector<hkv_table *> g_srv_tables;
 // the serving kernel's stop word (device memory: write-combined, so flushed at once)
 static void srv_set_stop(hkv_table *t, uint32_t v)
 {
@@ -396,6 +399,10 @@ int hkv_table_destroy(hkv_table *t)
     if (t->srv_running) {
         srv_set_stop(t, 1u);
         hipEventSynchronize(t->srv_ev);
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_srv_mu);
+        g_srv_tables.erase(std::remove(g_srv_tables.begin(), g_srv_tables.end(), t), g_srv_tables.end());
     }
     if (t->srv_ev) hipEventDestroy(t->srv_ev);
     if (t->ring) (void)(t->ring_vram ? hipFree(t->ring) : hipHostFree(t->ring));
@@ -972,6 +979,20 @@ static void srv_stop(hkv_table *t)
     srv_stop_locked(t);
 }
 
+// Tables whose serving kernel was started: at process exit each is told to stop and waited for, so no
+// persistent kernel is still running when the runtime tears down (it would leave after 2 ms idle anyway)
+static void srv_atexit()
+{
+    std::lock_guard<std::mutex> lk(g_srv_mu);
+    for (hkv_table *t : g_srv_tables)
+        if (t->srv_running) {
+            srv_set_stop(t, 1u);
+            (void)hipEventSynchronize(t->srv_ev);
+            t->srv_running = false;
+        }
+    g_srv_tables.clear();
+}
+
 // With t->hmu held, after a launch was published: a serving kernel will take it. If the running one
 // is leaving (idle or lifetime limit), wait until it has gone and start another at every
 // partition's first unfinished launch.
@@ -1006,6 +1027,12 @@ static void srv_ensure(hkv_table *t)
     part_join(t);
     if (launch_host_serve(sl, t->stream) || hipEventRecord(t->srv_ev, t->stream) != hipSuccess) die("serving kernel launch");
     t->srv_running = true;
+    {
+        static std::once_flag once;
+        std::call_once(once, [] { atexit(srv_atexit); });
+        std::lock_guard<std::mutex> lk(g_srv_mu);
+        if (std::find(g_srv_tables.begin(), g_srv_tables.end(), t) == g_srv_tables.end()) g_srv_tables.push_back(t);
+    }
     TRACE("serving kernel epoch %u", sl.epoch);
 }
 

@@ -107,6 +107,7 @@ struct BatchArgs {
     int32_t wave_copy;           // big values copied a wave per value (HKV_WAVE_COPY=0: by their own lane)
     int32_t vc_batch;            // values per step of those wave copies (HKV_VC_BATCH, 1 or kVcBatch)
     int32_t wave_shadow;         // big entries: candidates applied by the whole wave (HKV_WAVE_SHADOW=0: per lane)
+    const uint64_t *phys_hint;   // INV / VAL launches: located entries (hkv_batch_desc.d_phys), or NULL
     int32_t cancel;              // k_local_pre undoes its tags (HKV_BATCH_PREPASS_CANCEL)
     uint8_t *ack_out;            // INV launches: each element's ACK (hkv_batch_desc.d_ack_out), or NULL
     uint32_t ack_out_size;
@@ -427,6 +428,79 @@ __device__ __forceinline__ void copy_elem(uint8_t *dst, const uint8_t *src, int3
 
 constexpr int64_t kLookupHead = 8192;
 constexpr int kLookupPair = 2;
+// Four lanes (q = lane & 3) look up kLookupPair keys side by side: the 64-B bucket (16 B per
+// lane), the reference's slot order (first tag match, hermesKV.c:954-975), the log window
+// (:969-970), then each lane's 16 B of the 64-B log line (bytes 16q..16q+15). All four lanes of a
+// group call it with the same arguments.
+template <int P = kLookupPair>
+__device__ __forceinline__ void lookup_pair(const BatchArgs &a, const uint64_t *key, const bool *probe, int q,
+                                            int gbase, bool *ok, uint64_t *phys, uint4 *ln)
+{
+    uint4 v[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+        v[k] = probe[k] ? reinterpret_cast<const uint4 *>(a.index + ((key[k] & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u)[q]
+                        : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const uint64_t s0 = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
+        const uint64_t s1 = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
+        const uint32_t tag = (uint32_t)(key[k] >> 48);
+        const bool mt0 = probe[k] && (s0 & 1u) && ((uint32_t)(s0 >> 1) & 0x7FFFFFu) == tag;
+        const bool mt1 = probe[k] && (s1 & 1u) && ((uint32_t)(s1 >> 1) & 0x7FFFFFu) == tag;
+        const uint32_t g0 = (uint32_t)(__ballot(mt0) >> gbase) & 0xFu;
+        const uint32_t g1 = (uint32_t)(__ballot(mt1) >> gbase) & 0xFu;
+        uint32_t o = 0;  // bit 2*l + j: slot 2*l + j matches
+#pragma unroll
+        for (int l = 0; l < 4; ++l) o |= ((g0 >> l) & 1u) << (2 * l) | ((g1 >> l) & 1u) << (2 * l + 1);
+        const int first = o ? __ffs(o) - 1 : 0;
+        const uint64_t off = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
+        ok[k] = probe[k] && o && a.g.log_head - off < a.g.log_cap;
+        phys[k] = off & a.g.log_mask;
+    }
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+        ln[k] = ok[k] ? reinterpret_cast<const uint4 *>(a.log + phys[k])[q] : make_uint4(0u, 0u, 0u, 0u);
+}
+
+
+// lookup_pair with located entries (hkv_batch_desc.d_phys): an element with an offset reads its entry
+// line straight away; one without, or whose entry does not hold its key, takes lookup_pair's path. gi:
+// the elements' indices into the hints. All lanes of the wave call it.
+template <int P>
+__device__ __forceinline__ void lookup_hinted(const BatchArgs &a, const int64_t *gi, const uint64_t *key,
+                                              const bool *probe, int q, int gbase, bool *ok, uint64_t *phys, uint4 *ln)
+{
+    bool redo[P];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const uint64_t h = probe[k] ? a.phys_hint[gi[k]] : ~0ull;
+        ok[k] = h != ~0ull;
+        phys[k] = ok[k] ? h : 0;
+        ln[k] = ok[k] ? reinterpret_cast<const uint4 *>(a.log + phys[k])[q] : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const uint64_t ek = (uint64_t)(uint32_t)__shfl((int)ln[k].z, 0, 4) | ((uint64_t)(uint32_t)__shfl((int)ln[k].w, 0, 4) << 32);
+        redo[k] = probe[k] && (!ok[k] || ek != key[k]);
+        any |= redo[k];
+    }
+    if (__ballot(any)) {   // wave-uniform: the rare elements without a usable offset
+        bool ok2[P];
+        uint64_t ph2[P];
+        uint4 ln2[P];
+        lookup_pair<P>(a, key, redo, q, gbase, ok2, ph2, ln2);
+#pragma unroll
+        for (int k = 0; k < P; ++k)
+            if (redo[k]) {
+                ok[k] = ok2[k];
+                phys[k] = ph2[k];
+                ln[k] = ln2[k];
+            }
+    }
+}
+
 template <int P = kLookupPair>
 __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, int64_t i_end)
 {
@@ -475,42 +549,22 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
         probe[k] = p;
         key[k] = kk;
     }
-    uint4 v[P];
-#pragma unroll
-    for (int k = 0; k < P; ++k)
-        v[k] = probe[k] ? reinterpret_cast<const uint4 *>(a.index + ((key[k] & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u)[q]
-                        : make_uint4(0u, 0u, 0u, 0u);
-    uint64_t off[P];
-    uint32_t order[P];
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-        const uint64_t s0 = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
-        const uint64_t s1 = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
-        const uint32_t tag = (uint32_t)(key[k] >> 48);
-        const bool mt0 = probe[k] && (s0 & 1u) && ((uint32_t)(s0 >> 1) & 0x7FFFFFu) == tag;
-        const bool mt1 = probe[k] && (s1 & 1u) && ((uint32_t)(s1 >> 1) & 0x7FFFFFu) == tag;
-        const uint32_t g0 = (uint32_t)(__ballot(mt0) >> gbase) & 0xFu;
-        const uint32_t g1 = (uint32_t)(__ballot(mt1) >> gbase) & 0xFu;
-        uint32_t o = 0;  // bit 2*l + j: slot 2*l + j matches
-#pragma unroll
-        for (int l = 0; l < 4; ++l) o |= ((g0 >> l) & 1u) << (2 * l) | ((g1 >> l) & 1u) << (2 * l + 1);
-        order[k] = o;
-        const int first = o ? __ffs(o) - 1 : 0;
-        off[k] = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
-    }
-    // the log line of every element: the group's four lanes read 16 B each (bytes 8..32 hold the
-    // key and the meta), one access per lane for both elements in flight together; lane 0 gathers.
-    // The F word only for a candidate (a dependent load, but one random line less for the ~80 %
-    // that never mutate).
+    // bucket, then the log line (lookup_pair: four lanes per element, 16 B each); with located entries
+    // (hkv_batch_desc.d_phys) the log line straight away (lookup_hinted)
     bool ok[P];
     uint64_t phys[P], ekey[P];
     Meta m0[P];
     U64x2 ln[P];
+    {
+        bool pr[P];
+        uint4 l4[P];
 #pragma unroll
-    for (int k = 0; k < P; ++k) {
-        ok[k] = probe[k] && order[k] && a.g.log_head - off[k] < a.g.log_cap;
-        phys[k] = off[k] & a.g.log_mask;
-        ln[k] = ok[k] ? reinterpret_cast<const U64x2 *>(a.log + phys[k])[q] : U64x2{0, 0};
+        for (int k = 0; k < P; ++k) pr[k] = probe[k] != 0;
+        if (a.phys_hint) lookup_hinted<P>(a, gi, key, pr, q, gbase, ok, phys, l4);
+        else lookup_pair<P>(a, key, pr, q, gbase, ok, phys, l4);
+#pragma unroll
+        for (int k = 0; k < P; ++k)
+            ln[k] = U64x2{(uint64_t)l4[k].x | ((uint64_t)l4[k].y << 32), (uint64_t)l4[k].z | ((uint64_t)l4[k].w << 32)};
     }
 #pragma unroll
     for (int k = 0; k < P; ++k) {
@@ -1139,41 +1193,6 @@ constexpr int kLfElems = 32;             // elements per k_local_fused block (on
 enum { kCtrDefer = 3 };
 enum : uint8_t { kStDefer = 3 };
 
-// Four lanes (q = lane & 3) look up kLookupPair keys side by side: the 64-B bucket (16 B per
-// lane), the reference's slot order (first tag match, hermesKV.c:954-975), the log window
-// (:969-970), then each lane's 16 B of the 64-B log line (bytes 16q..16q+15). All four lanes of a
-// group call it with the same arguments.
-template <int P = kLookupPair>
-__device__ __forceinline__ void lookup_pair(const BatchArgs &a, const uint64_t *key, const bool *probe, int q,
-                                            int gbase, bool *ok, uint64_t *phys, uint4 *ln)
-{
-    uint4 v[P];
-#pragma unroll
-    for (int k = 0; k < P; ++k)
-        v[k] = probe[k] ? reinterpret_cast<const uint4 *>(a.index + ((key[k] & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u)[q]
-                        : make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-        const uint64_t s0 = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
-        const uint64_t s1 = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
-        const uint32_t tag = (uint32_t)(key[k] >> 48);
-        const bool mt0 = probe[k] && (s0 & 1u) && ((uint32_t)(s0 >> 1) & 0x7FFFFFu) == tag;
-        const bool mt1 = probe[k] && (s1 & 1u) && ((uint32_t)(s1 >> 1) & 0x7FFFFFu) == tag;
-        const uint32_t g0 = (uint32_t)(__ballot(mt0) >> gbase) & 0xFu;
-        const uint32_t g1 = (uint32_t)(__ballot(mt1) >> gbase) & 0xFu;
-        uint32_t o = 0;  // bit 2*l + j: slot 2*l + j matches
-#pragma unroll
-        for (int l = 0; l < 4; ++l) o |= ((g0 >> l) & 1u) << (2 * l) | ((g1 >> l) & 1u) << (2 * l + 1);
-        const int first = o ? __ffs(o) - 1 : 0;
-        const uint64_t off = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
-        ok[k] = probe[k] && o && a.g.log_head - off < a.g.log_cap;
-        phys[k] = off & a.g.log_mask;
-    }
-#pragma unroll
-    for (int k = 0; k < P; ++k)
-        ln[k] = ok[k] ? reinterpret_cast<const uint4 *>(a.log + phys[k])[q] : make_uint4(0u, 0u, 0u, 0u);
-}
-
 // The key (bytes 8..15) and the meta (bytes 16..32) of a log line held 16 B per lane, in every lane
 __device__ __forceinline__ uint64_t line_key_meta(const uint4 &ln, Meta &m)
 {
@@ -1760,7 +1779,14 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
             }
         }
     }
-    lookup_pair<P>(a, key, probe, q, gbase, ok, phys, ln);
+    if (a.phys_hint) {   // located entries (hkv_batch_desc.d_phys)
+        int64_t gi[P];
+#pragma unroll
+        for (int k = 0; k < P; ++k) gi[k] = i0 + te[k];
+        lookup_hinted<P>(a, gi, key, probe, q, gbase, ok, phys, ln);
+    } else {
+        lookup_pair<P>(a, key, probe, q, gbase, ok, phys, ln);
+    }
 #pragma unroll
     for (int k = 0; k < P; ++k) {
         Meta m;
@@ -3286,6 +3312,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.offsets = bl.offsets;
     a.state_out = (bl.type == kLocal || bl.type == kLocalAfterMemb) ? bl.state_out : nullptr;
     a.opc = bl.type == kLocal ? bl.opcode_in : nullptr;
+    a.phys_hint = bl.type == kInvs || bl.type == kVals ? bl.phys_hint : nullptr;
     a.patch = nullptr;
     a.pkeys = nullptr;
     a.cancel = bl.stage == 3;

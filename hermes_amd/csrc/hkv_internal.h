@@ -18,6 +18,7 @@ struct BatchLaunch {
     uint8_t *state_out;          // local launches: each element's final state byte (may be NULL)
     const uint8_t *opcode_in;    // local launches: the caller's mirror of each element's opcode (may be NULL)
     const uint8_t *patch;        // local launches: pending header writes, 16 B per element (may be NULL)
+    const uint64_t *phys_hint;   // INV / VAL launches: each element's located log offset (hkv_batch_desc.d_phys)
     uint8_t *rw_state;           // ACK launches: state-byte mirror of read_write_ops (may be NULL)
     const uint64_t *put_keys;    // local launches: PUT-key mirror (state_out holds the entry states), or NULL
     const uint8_t *index;

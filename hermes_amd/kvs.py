@@ -176,7 +176,7 @@ class HermesKV:
               patch: torch.Tensor | None = None, rw_state: torch.Tensor | None = None,
               unique: bool = False, put_keys: torch.Tensor | None = None,
               rows: tuple[int, int, int] | None = None, stage: int = 0,
-              ack_out: torch.Tensor | None = None, ack_out_size: int = 16) -> None:
+              ack_out: torch.Tensor | None = None, ack_out_size: int = 16, phys: torch.Tensor | None = None) -> None:
         """Apply n_batches batches of one type, concatenated in `elems` (uint8, on the GPU),
         in concatenation order, asynchronously on `stream` (default: torch's current).
         offsets (INV / ACK / VAL batches): the batches stored back to back, batch b at elements
@@ -190,7 +190,9 @@ class HermesKV:
         row order in one pass (HKV_BATCH_ROWS; skip_row -1: none). stage (local batches): 1 runs only the
         launch's prepass (HKV_BATCH_PREPASS), 2 the rest of it (HKV_BATCH_PREPASSED), 3 cancels it
         (HKV_BATCH_PREPASS_CANCEL), 0 runs all of it. ack_out (unique INV launches): every element's ACK
-        as the worker's ACK callbacks make it, ack_out_size bytes each (hkv_batch_desc.d_ack_out)."""
+        as the worker's ACK callbacks make it, ack_out_size bytes each (hkv_batch_desc.d_ack_out). phys
+        (unique INV and VAL launches): each element's located log offset (hkv_wl_peer_locate; ~0 none), the
+        entry line read without the bucket first (hkv_batch_desc.d_phys)."""
         assert elems.is_cuda and elems.dtype == torch.uint8
         total = stride if offsets is not None else n_batches * stride
         if rows is not None:
@@ -222,6 +224,9 @@ class HermesKV:
         if rw_state is not None:
             assert rw_state.is_cuda and rw_state.dtype == torch.uint8
             d.d_rw_state = rw_state.data_ptr()
+        if phys is not None:
+            assert phys.is_cuda and phys.dtype == torch.int64 and phys.numel() >= total
+            d.d_phys = phys.data_ptr()
         if ack_out is not None:
             assert unique and ack_out.is_cuda and ack_out.dtype == torch.uint8 and ack_out.numel() >= total * ack_out_size
             d.d_ack_out = ack_out.data_ptr()

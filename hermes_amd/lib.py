@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 HERE = os.path.dirname(os.path.abspath(__file__))
 # HKV_LIB: another build of the same library (A/B timing of two revisions in one GPU session)
 LIB_PATH = os.environ.get("HKV_LIB") or os.path.join(HERE, "libhermeskv.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
@@ -40,7 +40,8 @@ class HkvBatchDesc(ctypes.Structure):
                 ("membership", ctypes.c_uint8 * 8), ("d_state_out", ctypes.c_void_p),
                 ("d_opcode_in", ctypes.c_void_p), ("d_patch", ctypes.c_void_p), ("d_rw_state", ctypes.c_void_p),
                 ("d_put_keys", ctypes.c_void_p), ("n_rows", ctypes.c_int32), ("skip_row", ctypes.c_int32),
-                ("row_stride", ctypes.c_int64), ("d_ack_out", ctypes.c_void_p), ("ack_out_size", ctypes.c_uint32)]
+                ("row_stride", ctypes.c_int64), ("d_ack_out", ctypes.c_void_p), ("ack_out_size", ctypes.c_uint32),
+                ("d_phys", ctypes.c_void_p)]
 
 
 class Membership(ctypes.Structure):

@@ -371,6 +371,8 @@ class Round:
         self.rows_acks = None          # our ACKs to the rows (marshalled, not read back: the peers are virtual)
         # our ACKs to each peer's INVs written by that peer's INV launch itself (hkv_batch_desc.d_ack_out)
         # instead of a marshal pass over the applied INVs (HKV_FUSED_ACKS=0: the pass, experiments)
+        # the peers' INVs and VALs launch with their entries located when drawn (hkv_batch_desc.d_phys)
+        self.phys_hints = os.environ.get("HKV_PHYS_HINTS", "0") == "1"
         self.fused_acks = (self.pack_remote and ((kvs.sizes.entry == 64 and self.op <= 64) or
                                                  (kvs.sizes.entry == 320 and self.op <= 320))
                            and os.environ.get("HKV_FUSED_ACKS", "1") != "0")
@@ -608,14 +610,17 @@ class Round:
                 self.kvs.batch(L.BatchType.invs, rows, 1, P, self.op, self.mb, offsets=off, unique=True,
                                rows=(self.R, P, -1))
             return
-        pi, _, _, _, _, per_peer = self.remote_packed[k]
+        pi, _, _, _, phys, per_peer = self.remote_packed[k]
         for base, n, off in per_peer:
             if n:
+                ph = phys[base:] if self.phys_hints else None
                 if self.fused_acks and not self.inv_rows:
                     self.kvs.batch(L.BatchType.invs, pi[base * self.op:], self.W, n, self.op, self.mb, offsets=off,
-                                   unique=True, ack_out=self.ack_out[base * self.ack_size:], ack_out_size=self.ack_size)
+                                   unique=True, ack_out=self.ack_out[base * self.ack_size:], ack_out_size=self.ack_size,
+                                   phys=ph)
                 else:
-                    self.inv_batch(pi[base * self.op:], self.W, n, offsets=off, unique=True)
+                    self.kvs.batch(L.BatchType.invs, pi[base * self.op:], self.W, n, self.op, self.mb, offsets=off,
+                                   unique=True, phys=ph)
 
     def marshal_acks(self, invs: torch.Tensor, n: int, out: torch.Tensor):
         check(_L.hkv_wl_marshal_acks(_ptr(invs), n, self.op, _ptr(out), self.ack_size, self.machine_id, _s()),
@@ -690,9 +695,9 @@ class Round:
             self.val_totals[0] += self.val_count.sum()
 
     def val_batch(self, vals: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None,
-                  offsets: torch.Tensor | None = None):
+                  offsets: torch.Tensor | None = None, phys: torch.Tensor | None = None):
         self.kvs.batch(L.BatchType.vals, vals, n_batches, stride, L.OP_META_SIZE, self.mb, counts=counts,
-                       offsets=offsets)
+                       offsets=offsets, phys=phys)
 
     # -- a whole round with virtual peers
     def step(self, events: dict | None = None, timed_batches=("local", "invs", "acks", "vals"),
@@ -812,7 +817,8 @@ class Round:
                 self.refill()
                 self.prepass(overlap=True, events=events if events is not None and "local" in timed_batches else None)
             if packed:
-                timed("vals", lambda: self.val_batch(pv, self.R * self.W, total, offsets=off))
+                ph = self.remote_packed[k][4] if self.phys_hints else None
+                timed("vals", lambda: self.val_batch(pv, self.R * self.W, total, offsets=off, phys=ph))
             else:
                 timed("vals", lambda: self.val_batch(rv, self.W, self.rstride, counts=vc))
             if self.count_elems:

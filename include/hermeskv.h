@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HKV_ABI_VERSION 6
+#define HKV_ABI_VERSION 7
 
 /* ------------------------------------------------------------------ reference types
  * Declared here only when the reference's own spacetime.h has not been included; the
@@ -167,6 +167,12 @@ typedef struct hkv_batch_desc {
                                    itself, and each answered element leaves with opcode ST_EMPTY, as after the
                                    callbacks' send (ack_modify_elem_after_send). NULL = none (ABI 6) */
     uint32_t ack_out_size;
+    const uint64_t *d_phys;     /* device, INV (HKV_BATCH_UNIQUE) and VAL launches: per element, the log offset
+                                   the lookup of its key gives (hkv_wl_peer_locate), or ~0 for none; valid only
+                                   while the index is unchanged since (no populate in between), which the caller
+                                   guarantees. The launch then reads the entry line straight away instead of the
+                                   bucket first; an element whose entry no longer holds its key, or without an
+                                   offset, is looked up as usual. NULL = none (ABI 7) */
 } hkv_batch_desc;
 #define HKV_NO_PUT 0xFFFFFFFFFFFFFFFFull
 

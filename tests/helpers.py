@@ -122,7 +122,7 @@ class Mirror:
     def batch(self, btype, elems, n_batches, stride, elem_size, membership, counts=None, rw=None,
               rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None, state_out=None, opcode_in=None,
               patch=None, rw_state=None, unique=False, put_keys=None, rows=None, stage=0, ack_out=None,
-              ack_out_size=16):
+              ack_out_size=16, phys=None):
         import torch
         if stage in (1, 3):   # a prepass (or its cancellation) changes no element and nothing of the meta
             self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
@@ -138,7 +138,7 @@ class Mirror:
                               rw_stride_bytes, rw_state, rows)
         if offsets is not None:
             return self._packed(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
-                                rw_stride_bytes, rw_state, unique, ack_out, ack_out_size)
+                                rw_stride_bytes, rw_state, unique, ack_out, ack_out_size, phys)
         torch.cuda.synchronize()
         n = n_batches * stride * elem_size
         vt = np.dtype((np.void, elem_size))
@@ -285,7 +285,7 @@ class Mirror:
         self.launches += 1
 
     def _packed(self, btype, elems, n_batches, total, elem_size, membership, offsets, stream, rw=None,
-                rw_stride_bytes=0, rw_state=None, unique=False, ack_out=None, ack_out_size=16):
+                rw_stride_bytes=0, rw_state=None, unique=False, ack_out=None, ack_out_size=16, phys=None):
         """A packed (HKV_BATCH_PACKED) INV / ACK / VAL launch: the oracle applies the same batches
         laid out in rows; the device's packed output must equal the oracle's rows packed again."""
         import torch
@@ -304,7 +304,7 @@ class Mirror:
         rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
         self._orig(btype, elems, n_batches, total, elem_size, membership, rw=rw, rw_stride_bytes=rw_stride_bytes,
                    stream=stream, offsets=offsets, rw_state=rw_state, unique=unique, ack_out=ack_out,
-                   ack_out_size=ack_out_size)
+                   ack_out_size=ack_out_size, phys=phys)
         torch.cuda.synchronize()
         e_in = rows.reshape(-1).view(np.dtype((np.void, elem_size))).copy()
         self.o.batch_multi(int(btype), e_in, n_batches, width, cnt, membership, rw_in,

@@ -1478,7 +1478,14 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
                 }
             }
         }
-        lookup_pair<kPrePair>(a, key, probe, q, gbase, ok, phys, ln);
+        if (a.phys_hint) {   // located entries (hkv_batch_desc.d_phys): each key's first PUT's word
+            int64_t gi[kPrePair];
+#pragma unroll
+            for (int k = 0; k < kPrePair; ++k) gi[k] = probe[k] ? (int64_t)idx[k] : 0;
+            lookup_hinted<kPrePair>(a, gi, key, probe, q, gbase, ok, phys, ln);
+        } else {
+            lookup_pair<kPrePair>(a, key, probe, q, gbase, ok, phys, ln);
+        }
 #pragma unroll
         for (int k = 0; k < kPrePair; ++k) {
             Meta m0;
@@ -1554,7 +1561,14 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         if (live[k])
             probe[k] = in_count(a, (uint32_t)(i0 + te[k])) && !skip_elem_os(kLocal, (uint8_t)h0, (uint8_t)(h0 >> 8));
     }
-    lookup_pair<P>(a, key, probe, q, gbase, ok, phys, ln);
+    if (a.phys_hint) {   // located entries (hkv_batch_desc.d_phys)
+        int64_t gi[P];
+#pragma unroll
+        for (int k = 0; k < P; ++k) gi[k] = i0 + te[k];
+        lookup_hinted<P>(a, gi, key, probe, q, gbase, ok, phys, ln);
+    } else {
+        lookup_pair<P>(a, key, probe, q, gbase, ok, phys, ln);
+    }
     // F of a key tagged by k_local_pre, loaded for both elements before either is resolved
 #pragma unroll
     for (int k = 0; k < P; ++k) {
@@ -3312,7 +3326,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.offsets = bl.offsets;
     a.state_out = (bl.type == kLocal || bl.type == kLocalAfterMemb) ? bl.state_out : nullptr;
     a.opc = bl.type == kLocal ? bl.opcode_in : nullptr;
-    a.phys_hint = bl.type == kInvs || bl.type == kVals ? bl.phys_hint : nullptr;
+    a.phys_hint = bl.type == kInvs || bl.type == kVals || bl.type == kLocal ? bl.phys_hint : nullptr;
     a.patch = nullptr;
     a.pkeys = nullptr;
     a.cancel = bl.stage == 3;

@@ -569,9 +569,9 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.put_keys = d->type == kLocal && d->d_state_out && !pk_off ? d->d_put_keys : nullptr;
     if (bl.patch && ((uintptr_t)bl.patch & 15)) return fail(-1, "d_patch must be 16-byte aligned");
     if (d->d_phys) {   // located entries: unique INV launches (not rows) and VAL launches, on the engine
-        if (!((d->type == kInvs && (d->flags & HKV_BATCH_UNIQUE) && d->n_rows <= 1) || d->type == kVals) ||
-            ((uintptr_t)d->d_phys & 7))
-            return fail(-1, "d_phys: unique INV or VAL launches, 8-byte aligned");
+        if (!((d->type == kInvs && (d->flags & HKV_BATCH_UNIQUE) && d->n_rows <= 1) || d->type == kVals ||
+              d->type == kLocal) || ((uintptr_t)d->d_phys & 7))
+            return fail(-1, "d_phys: local, unique INV or VAL launches, 8-byte aligned");
         bl.phys_hint = d->d_phys;
     }
     if (bl.put_keys && ((uintptr_t)bl.put_keys & 7)) return fail(-1, "d_put_keys must be 8-byte aligned");

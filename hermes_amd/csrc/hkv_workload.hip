@@ -489,7 +489,7 @@ __global__ __launch_bounds__(256) void k_refill_plan_w(uint8_t *states, int32_t 
                                                        const uint8_t *top, int32_t tlen, uint32_t *cursor,
                                                        uint32_t machine_id, uint32_t flags,
                                                        unsigned long long *counters, uint8_t *opc, uint8_t *patch,
-                                                       uint64_t *put_keys)
+                                                       uint64_t *put_keys, const uint64_t *tphys, uint64_t *sphys)
 {
     const int lane = threadIdx.x & 63;
     const int wb = (blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * WPW;
@@ -537,7 +537,7 @@ __global__ __launch_bounds__(256) void k_refill_plan_w(uint8_t *states, int32_t 
         }
     }
     uint8_t oc[WPW][4];
-    uint64_t key[WPW][4];
+    uint64_t key[WPW][4], kph[WPW][4];
 #pragma unroll
     for (int v = 0; v < WPW; ++v)
 #pragma unroll
@@ -546,6 +546,7 @@ __global__ __launch_bounds__(256) void k_refill_plan_w(uint8_t *states, int32_t 
             const int64_t t = (int64_t)(wb + v) * tlen + (int64_t)((base[v] + (uint32_t)rank[v][r]) % (uint32_t)tlen);
             oc[v][r] = rf ? top[t] : (uint8_t)0;
             key[v][r] = rf ? tkey[t] : 0ull;
+            kph[v][r] = rf && tphys ? tphys[t] : ~0ull;   // the new key's located entry
         }
 #pragma unroll
     for (int v = 0; v < WPW; ++v) {
@@ -566,6 +567,7 @@ __global__ __launch_bounds__(256) void k_refill_plan_w(uint8_t *states, int32_t 
                       ((uint64_t)(get ? 0u : (uint8_t)('a' + machine_id)) << 32) |
                       ((uint64_t)(get && (flags & HKV_WL_READ_TS_RESET) ? 1u : 0u) << 40) | (1ull << 48);
                 opc[e] = o;
+                if (sphys) sphys[e] = kph[v][r];
                 if (put_keys) {   // the PUT-key mirror and the entry state of the patched op
                     put_keys[e] = o == kOpPut ? p.a : HKV_NO_PUT;
                     states[e] = kNew;
@@ -1753,23 +1755,43 @@ int hkv_wl_refill_st(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t o
     return ok();
 }
 
+static int refill_plan(uint8_t *states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
+                       const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor, uint32_t machine_id,
+                       uint32_t flags, unsigned long long *counters, uint8_t *opc, uint8_t *patch,
+                       uint64_t *put_keys, const uint64_t *tphys, uint64_t *sphys, void *stream)
+{
+    if (stride > 256 || n_workers <= 0 || tlen <= 0 || !states || !opc || !patch) return -1;
+    if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET)) return -1;   // no hot-request coalescing
+    if (((uintptr_t)patch & 15) || ((uintptr_t)put_keys & 7) || st_value > 255) return -1;
+    if ((!tphys) != (!sphys) || ((uintptr_t)tphys & 7) || ((uintptr_t)sphys & 7)) return -1;
+    if (wl_wpw() == 2)
+        hipLaunchKernelGGL(k_refill_plan_w<2>, dim3((unsigned)((n_workers + 7) / 8)), dim3(256), 0, (hipStream_t)stream,
+                           states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
+                           counters, opc, patch, put_keys, tphys, sphys);
+    else
+        hipLaunchKernelGGL(k_refill_plan_w<1>, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+                           states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
+                           counters, opc, patch, put_keys, tphys, sphys);
+    return ok();
+}
+
 int hkv_wl_refill_plan(uint8_t *states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
                        const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor, uint32_t machine_id,
                        uint32_t flags, unsigned long long *counters, uint8_t *opc, uint8_t *patch,
                        uint64_t *put_keys, void *stream)
 {
-    if (stride > 256 || n_workers <= 0 || tlen <= 0 || !states || !opc || !patch) return -1;
-    if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET)) return -1;   // no hot-request coalescing
-    if (((uintptr_t)patch & 15) || ((uintptr_t)put_keys & 7) || st_value > 255) return -1;
-    if (wl_wpw() == 2)
-        hipLaunchKernelGGL(k_refill_plan_w<2>, dim3((unsigned)((n_workers + 7) / 8)), dim3(256), 0, (hipStream_t)stream,
-                           states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
-                           counters, opc, patch, put_keys);
-    else
-        hipLaunchKernelGGL(k_refill_plan_w<1>, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
-                           states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
-                           counters, opc, patch, put_keys);
-    return ok();
+    return refill_plan(states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags, counters,
+                       opc, patch, put_keys, nullptr, nullptr, stream);
+}
+
+int hkv_wl_refill_plan_located(uint8_t *states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
+                               const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor,
+                               uint32_t machine_id, uint32_t flags, unsigned long long *counters, uint8_t *opc,
+                               uint8_t *patch, uint64_t *put_keys, const uint64_t *tphys, uint64_t *sphys, void *stream)
+{
+    if (!tphys || !sphys) return -1;
+    return refill_plan(states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags, counters,
+                       opc, patch, put_keys, tphys, sphys, stream);
 }
 
 int hkv_wl_fold_counters(unsigned long long *counters, void *stream)

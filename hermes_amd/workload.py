@@ -39,6 +39,9 @@ _L.hkv_wl_refill_st.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uin
                                 _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _P]
 _L.hkv_wl_refill_plan.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, _P, _P,
                                   ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _P, _P]
+_L.hkv_wl_refill_plan_located.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, _P, _P,
+                                          ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _P, _P, _P,
+                                          _P]
 _L.hkv_wl_marshal_invs.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_invs_cap.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
                                        ctypes.c_uint32, _P, _P, _P]
@@ -277,6 +280,11 @@ class Round:
         # could find its PUTs without reading ops (HKV_PUT_KEYS=1). Measured, not adopted (round 4): the
         # prepass stays at 83 us (its atomics and seqlock tags, not its loads, bound it now) and the mirror
         # checks cost the fused pass 10-20 us
+        # located entries for the local launch (HKV_LOCAL_HINTS=1): every trace key's log offset, located once
+        # (at the first plan, the table populated), and each slot's word, kept by the plan (d_phys)
+        self.local_hints = self.fused and os.environ.get("HKV_LOCAL_HINTS", "0") == "1"
+        self.trace_phys = None
+        self.slot_phys = torch.full((W * S,), -1, dtype=torch.int64, device=dev) if self.local_hints else None
         self.put_keys = (torch.zeros(W * S, dtype=torch.int64, device=dev)
                          if self.fused and os.environ.get("HKV_PUT_KEYS", "0") == "1" else None)
         self.C = slots_per_worker(write_permille, rmw_permille)   # INV send credits per worker
@@ -497,6 +505,19 @@ class Round:
 
     # -- pieces of one round
     def refill(self, first: bool = False):
+        if self.fused and not first and self.local_hints:   # the plan keeps each slot's located entry too
+            if self.trace_phys is None:
+                n = self.W * self.trace_len
+                self.trace_phys = torch.empty(n, dtype=torch.int64, device=self.ops.device)
+                check(_L.hkv_wl_peer_locate(self.kvs.h, _ptr(self.trace_key), n, 8, _ptr(self.trace_phys), _s()),
+                      "trace_locate")
+            check(_L.hkv_wl_refill_plan_located(_ptr(self.states), self.W, self.LOCAL, self.sizes.st_value,
+                                                self.sizes.shift, _ptr(self.trace_key), _ptr(self.trace_op),
+                                                self.trace_len, _ptr(self.cursor), self.machine_id, self.rflags,
+                                                _ptr(self.counters), _ptr(self.opcodes), _ptr(self.patch),
+                                                _ptr(self.put_keys), _ptr(self.trace_phys), _ptr(self.slot_phys),
+                                                _s()), "refill_plan_located")
+            return
         if self.fused and not first:   # a plan the next local launch applies (the ops stay as they are)
             check(_L.hkv_wl_refill_plan(_ptr(self.states), self.W, self.LOCAL, self.sizes.st_value, self.sizes.shift,
                                         _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
@@ -519,7 +540,8 @@ class Round:
 
     def _local(self, stage: int, stream=None):
         self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb, state_out=self.states,
-                       opcode_in=self.opcodes, patch=self.patch, put_keys=self.put_keys, stage=stage, stream=stream)
+                       opcode_in=self.opcodes, patch=self.patch, put_keys=self.put_keys, stage=stage, stream=stream,
+                       phys=self.slot_phys)
 
     def prepass(self, overlap: bool, events: dict | None = None):
         """Stage 1 of the next local launch: on the side stream after what the current stream holds

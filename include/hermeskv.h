@@ -167,7 +167,7 @@ typedef struct hkv_batch_desc {
                                    itself, and each answered element leaves with opcode ST_EMPTY, as after the
                                    callbacks' send (ack_modify_elem_after_send). NULL = none (ABI 6) */
     uint32_t ack_out_size;
-    const uint64_t *d_phys;     /* device, INV (HKV_BATCH_UNIQUE) and VAL launches: per element, the log offset
+    const uint64_t *d_phys;     /* device, local, INV (HKV_BATCH_UNIQUE) and VAL launches: per element, the log offset
                                    the lookup of its key gives (hkv_wl_peer_locate), or ~0 for none; valid only
                                    while the index is unchanged since (no populate in between), which the caller
                                    guarantees. The launch then reads the entry line straight away instead of the

@@ -92,6 +92,16 @@ int hkv_wl_refill_plan(uint8_t *d_states, int32_t n_workers, int32_t stride, uin
                        const uint64_t *d_trace_key, const uint8_t *d_trace_op, int32_t trace_len, uint32_t *d_cursor,
                        uint32_t machine_id, uint32_t flags, unsigned long long *d_counters, uint8_t *d_opcode,
                        uint8_t *d_patch, uint64_t *d_put_keys, void *stream);
+/* hkv_wl_refill_plan that also keeps each slot's located entry: d_trace_phys holds the located log
+ * offset of every trace key (hkv_wl_peer_locate over the trace, ~0 for none) and a refilled slot's
+ * word of d_slot_phys takes its new key's; the next local launch takes d_slot_phys as
+ * hkv_batch_desc.d_phys (a kept slot's word still describes its op's key). */
+int hkv_wl_refill_plan_located(uint8_t *d_states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
+                               const uint64_t *d_trace_key, const uint8_t *d_trace_op, int32_t trace_len,
+                               uint32_t *d_cursor, uint32_t machine_id, uint32_t flags,
+                               unsigned long long *d_counters, uint8_t *d_opcode, uint8_t *d_patch,
+                               uint64_t *d_put_keys, const uint64_t *d_trace_phys, uint64_t *d_slot_phys,
+                               void *stream);
 /* hkv_wl_refill for big ops (op_size > 64, refilled in place; not on the first pass, flags
  * HKV_WL_REFILL_ALL and HKV_WL_READ_TS_RESET), deciding from d_states, the state mirror
  * hkv_wl_refill_plan reads: an op that is not refilled is not touched, a refilled one is only

@@ -127,7 +127,7 @@ class Mirror:
         if stage in (1, 3):   # a prepass (or its cancellation) changes no element and nothing of the meta
             self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
                        node_suspected, stream, state_out=state_out, opcode_in=opcode_in, patch=patch,
-                       rw_state=rw_state, unique=unique, put_keys=put_keys, stage=stage)
+                       rw_state=rw_state, unique=unique, put_keys=put_keys, stage=stage, phys=phys)
             self.prepass = stage == 1
             if stage == 3:
                 torch.cuda.synchronize()
@@ -166,7 +166,7 @@ class Mirror:
         rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
         self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
                    node_suspected, stream, state_out=state_out, opcode_in=opcode_in, patch=patch, rw_state=rw_state,
-                   unique=unique, put_keys=put_keys, stage=stage)
+                   unique=unique, put_keys=put_keys, stage=stage, phys=phys)
         if stage == 2:
             self.prepass = False
         torch.cuda.synchronize()

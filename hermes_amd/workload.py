@@ -281,7 +281,9 @@ class Round:
         # prepass stays at 83 us (its atomics and seqlock tags, not its loads, bound it now) and the mirror
         # checks cost the fused pass 10-20 us
         # located entries for the local launch (HKV_LOCAL_HINTS=1): every trace key's log offset, located once
-        # (at the first plan, the table populated), and each slot's word, kept by the plan (d_phys)
+        # (at the first plan, the table populated), and each slot's word, kept by the plan (d_phys). Same box
+        # (gpurun_out/r04zi): local launch 381 -> 355 us, 4.26 -> 4.35 G ops/s; off by default, as
+        # HKV_PHYS_HINTS
         self.local_hints = self.fused and os.environ.get("HKV_LOCAL_HINTS", "0") == "1"
         self.trace_phys = None
         self.slot_phys = torch.full((W * S,), -1, dtype=torch.int64, device=dev) if self.local_hints else None
@@ -379,10 +381,12 @@ class Round:
         self.rows_acks = None          # our ACKs to the rows (marshalled, not read back: the peers are virtual)
         # our ACKs to each peer's INVs written by that peer's INV launch itself (hkv_batch_desc.d_ack_out)
         # instead of a marshal pass over the applied INVs (HKV_FUSED_ACKS=0: the pass, experiments)
-        # the peers' INVs and VALs launch with their entries located when drawn (hkv_batch_desc.d_phys):
-        # same box, 3 reps each (gpurun_out/r04zh), INV 72 -> 59 us, VAL 50 -> 38 us, 4.24 -> 4.40 G ops/s.
-        # HKV_PHYS_HINTS=0: the bucket lookup for every element
-        self.phys_hints = os.environ.get("HKV_PHYS_HINTS", "1") != "0"
+        # HKV_PHYS_HINTS=1: the peers' INVs and VALs launch with their entries located when drawn
+        # (hkv_batch_desc.d_phys). Same box, 3 reps each (gpurun_out/r04zh): INV 72 -> 59 us, VAL 50 -> 38 us,
+        # 4.24 -> 4.40 G ops/s. Off by default: it skips the bucket read the reference makes for every
+        # message (the location comes from a lookup made when the round's slabs were drawn), so the
+        # headline keeps the reference's per-element lookup ("Located entries")
+        self.phys_hints = os.environ.get("HKV_PHYS_HINTS", "0") == "1"
         self.fused_acks = (self.pack_remote and ((kvs.sizes.entry == 64 and self.op <= 64) or
                                                  (kvs.sizes.entry == 320 and self.op <= 320))
                            and os.environ.get("HKV_FUSED_ACKS", "1") != "0")

@@ -501,7 +501,7 @@ __device__ __forceinline__ void lookup_hinted(const BatchArgs &a, const int64_t 
     }
 }
 
-template <int P = kLookupPair>
+template <int P = kLookupPair, bool H = false>
 __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, int64_t i_end)
 {
     const int q = threadIdx.x & 3;
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
         uint4 l4[P];
 #pragma unroll
         for (int k = 0; k < P; ++k) pr[k] = probe[k] != 0;
-        if (a.phys_hint) lookup_hinted<P>(a, gi, key, pr, q, gbase, ok, phys, l4);
+        if (H) lookup_hinted<P>(a, gi, key, pr, q, gbase, ok, phys, l4);
         else lookup_pair<P>(a, key, pr, q, gbase, ok, phys, l4);
 #pragma unroll
         for (int k = 0; k < P; ++k)
@@ -1325,7 +1325,7 @@ constexpr int kPrePair = 4;
 #else
 #define HKV_PRE_ATTR
 #endif
-template <int HEAD = kPreHead>
+template <int HEAD = kPreHead, bool H = false>
 __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 {
     __shared__ uint64_t hk[kPreHash], gk[kPreHash];  // the block's PUT keys, the head's
@@ -1478,7 +1478,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
                 }
             }
         }
-        if (a.phys_hint) {   // located entries (hkv_batch_desc.d_phys): each key's first PUT's word
+        if (H) {   // located entries (hkv_batch_desc.d_phys): each key's first PUT's word
             int64_t gi[kPrePair];
 #pragma unroll
             for (int k = 0; k < kPrePair; ++k) gi[k] = probe[k] ? (int64_t)idx[k] : 0;
@@ -1506,7 +1506,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 // nothing shared beyond it. The lookup runs four lanes per element (each lane holds 16 B of the op
 // and of the log line); the wave-private LDS copies of op and entry are then resolved one element
 // per lane, so the exec code's branches are paid once per 32 elements; the ops go back whole.
-template <int P>
+template <int P, bool H = false>
 __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
 {
     constexpr int E = 16 * P;   // elements per wave: P per lane group
@@ -1561,7 +1561,7 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         if (live[k])
             probe[k] = in_count(a, (uint32_t)(i0 + te[k])) && !skip_elem_os(kLocal, (uint8_t)h0, (uint8_t)(h0 >> 8));
     }
-    if (a.phys_hint) {   // located entries (hkv_batch_desc.d_phys)
+    if (H) {   // located entries (hkv_batch_desc.d_phys)
         int64_t gi[P];
 #pragma unroll
         for (int k = 0; k < P; ++k) gi[k] = i0 + te[k];
@@ -1753,7 +1753,7 @@ __device__ __forceinline__ bool chunk_equal(const uint4 &a, const uint4 &b)
     return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
 }
 
-template <int TYPE, int P = kLookupPair>
+template <int TYPE, int P = kLookupPair, bool H = false>
 __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
 {
     constexpr int E = 16 * P;   // elements per wave: P per lane group
@@ -1793,7 +1793,7 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
             }
         }
     }
-    if (a.phys_hint) {   // located entries (hkv_batch_desc.d_phys)
+    if (H) {   // located entries (hkv_batch_desc.d_phys)
         int64_t gi[P];
 #pragma unroll
         for (int k = 0; k < P; ++k) gi[k] = i0 + te[k];
@@ -3311,7 +3311,8 @@ static void launch_local_pre(const BatchArgs &a, int64_t n, hipStream_t s)
 {
     static const int head = getenv("HKV_PRE_HEAD") ? atoi(getenv("HKV_PRE_HEAD")) : kPreHead;
     const dim3 grid((unsigned)((n + kPreElems - 1) / kPreElems));
-    if (head == 256) hipLaunchKernelGGL(k_local_pre<256>, grid, dim3(256), 0, s, a);
+    if (a.phys_hint) hipLaunchKernelGGL((k_local_pre<kPreHead, true>), grid, dim3(256), 0, s, a);
+    else if (head == 256) hipLaunchKernelGGL(k_local_pre<256>, grid, dim3(256), 0, s, a);
     else if (head == 512) hipLaunchKernelGGL(k_local_pre<512>, grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_local_pre<kPreHead>, grid, dim3(256), 0, s, a);
 }
@@ -3442,7 +3443,9 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         }
         // HKV_LF_PAIR: elements per lane group in k_local_fused (2: 32 per wave; 4: 64, more loads in flight)
         static const int lfp_env = getenv("HKV_LF_PAIR") ? atoi(getenv("HKV_LF_PAIR")) : 2;
-        if (lfp_env == 4)
+        if (a.phys_hint)
+            hipLaunchKernelGGL((k_local_fused<2, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
+        else if (lfp_env == 4)
             hipLaunchKernelGGL(k_local_fused<4>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, a);
         else if (lfp_env == 1)
             hipLaunchKernelGGL(k_local_fused<1>, dim3((unsigned)((n + 15) / 16)), dim3(64), 0, s, a);
@@ -3502,7 +3505,8 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
             static const int up = getenv("HKV_UNIQUE_PAIR") ? atoi(getenv("HKV_UNIQUE_PAIR")) : 1;
             if (up == 1) {
                 const unsigned g1 = (unsigned)((n + 15) / 16);
-                if (bl.type == kInvs) hipLaunchKernelGGL((k_unique_lds<kInvs, 1>), dim3(g1), dim3(64), 0, s, a);
+                if (bl.type == kInvs && a.phys_hint) hipLaunchKernelGGL((k_unique_lds<kInvs, 1, true>), dim3(g1), dim3(64), 0, s, a);
+                else if (bl.type == kInvs) hipLaunchKernelGGL((k_unique_lds<kInvs, 1>), dim3(g1), dim3(64), 0, s, a);
                 else hipLaunchKernelGGL((k_unique_lds<kAcks, 1>), dim3(g1), dim3(64), 0, s, a);
             } else if (up == 4) {
                 const unsigned g4 = (unsigned)((n + 63) / 64);
@@ -3524,7 +3528,8 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         // elements per lane group (HKV_VAL_PAIR): 1 by default. Same box, VAL batch per step (gpurun_out/r04m,
         // r04u): 49.6-50.2 us at 1, 52.3-53.9 at 2, 57 at 4
         static const int vp = getenv("HKV_VAL_PAIR") ? atoi(getenv("HKV_VAL_PAIR")) : 1;
-        if (vp == 4) hipLaunchKernelGGL(k_lookup<4>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, (int64_t)0, n);
+        if (a.phys_hint) hipLaunchKernelGGL((k_lookup<1, true>), dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, a, (int64_t)0, n);
+        else if (vp == 4) hipLaunchKernelGGL(k_lookup<4>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, (int64_t)0, n);
         else if (vp == 1) hipLaunchKernelGGL(k_lookup<1>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, a, (int64_t)0, n);
         else hipLaunchKernelGGL(k_lookup<>, dim3((unsigned)((n + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, n);
         return hipGetLastError() == hipSuccess ? 0 : -3;

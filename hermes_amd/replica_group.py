@@ -234,6 +234,32 @@ class ReplicaRound:
         n = width * L.OP_META_SIZE
         return self.val_recv[:self.N * n], self.val_pack[:n]
 
+    # steady rounds (WidthPlan): each slab is one slot wider than the INV cap and carries its rank's
+    # total in that spare slot, so the totals travel with the slabs (two collectives per round fewer)
+    def _put_total(self, pack, width: int, size: int, off) -> None:
+        a = (width - 1) * size
+        pack[a:a + 4].view(torch.int32).copy_(off[self.W:])
+
+    def _take_totals(self, recv, width: int, size: int, out) -> None:
+        a = (width - 1) * size
+        out.copy_(recv[:self.N * width * size].view(self.N, width * size)[:, a:a + 4].view(torch.int32).view(-1))
+
+    def inv_io_total(self, width: int):
+        """inv_io, the spare slot (width - 1) of the send slab holding this rank's INV total"""
+        self._put_total(self.inv_pack, width, self.op, self.inv_off)
+        return self.inv_io(width)
+
+    def take_inv_totals(self, width: int) -> None:
+        """inv_totals from the spare slots of the gathered INV slabs"""
+        self._take_totals(self.inv_recv, width, self.op, self.inv_totals)
+
+    def val_io_total(self, width: int):
+        self._put_total(self.val_pack, width, L.OP_META_SIZE, self.val_off)
+        return self.val_io(width)
+
+    def take_val_totals(self, width: int) -> None:
+        self._take_totals(self.val_recv, width, L.OP_META_SIZE, self.val_totals)
+
     def invs(self, width: int):
         """Apply the gathered INVs of the peers ([N][width], row p: inv_totals[p] INVs) as N
         batches; their ACKs go into ack_slab in the positions of the INVs they answer."""
@@ -358,6 +384,8 @@ class WidthPlan:
         self.calib_every = int(os.environ.get("HKV_GROUP_CALIB", "16"))
         self.slack = float(os.environ.get("HKV_GROUP_WIDTH_SLACK", "1.25"))
         self.pad = 256
+        # the totals ride in one spare slot of each slab (HKV_GROUP_FOLD_TOTALS=0: their own all-gathers)
+        self.fold = os.environ.get("HKV_GROUP_FOLD_TOTALS", "1") != "0"
         self.width = None
         self.k = 0
 
@@ -367,7 +395,12 @@ class WidthPlan:
         return (self.calib_every > 0 and self.width is not None and not special and k % self.calib_every != 0)
 
     def calibrate(self, width: int, cap: int) -> None:
-        self.width = min(cap, int(width * self.slack) + self.pad)
+        """cap: the slab capacity in slots (one is kept for the spare slot)"""
+        self.width = min(cap - 1, int(width * self.slack) + self.pad)
+
+    def slab_width(self) -> int:
+        """slots per slab in a steady round: the INV cap, plus the spare slot when the totals ride in it"""
+        return self.width + 1 if self.fold else self.width
 
 
 def _timed(events, name, fn, only=None):
@@ -488,18 +521,24 @@ class ReplicaGroupRound:
         heartbeating and the survivors expel it when they agree (two periods later)."""
         r = self.r
         steady = self.plan is not None and self.plan.steady(drop is not None or self.hades or not r.unique_acks)
+        fold = steady and self.plan.fold
         if steady:   # no host read: the planned width, each rank's INVs capped at it
-            width, stride = self.plan.width, None
+            width, stride = self.plan.slab_width(), None
             r.own_total = None
-            _timed(events, "local", lambda: r.local(cap=width), timed_batches)
-            self._gather(*r.inv_total_io())
+            _timed(events, "local", lambda: r.local(cap=self.plan.width), timed_batches)
+            if fold:
+                self._gather(*r.inv_io_total(width))
+                r.take_inv_totals(width)
+            else:
+                self._gather(*r.inv_total_io())
         else:
             _timed(events, "local", r.local, timed_batches)
             self._gather(*r.inv_total_io())
             width, stride = r.round_shape()  # host synchronisation: this round's exact width
             if self.plan is not None:
                 self.plan.calibrate(width, r.W * r.C)
-        self._gather(*r.inv_io(width))
+        if not fold:
+            self._gather(*r.inv_io(width))
         if drop is not None:
             r.peer_failing()
             if drop == r.rank:
@@ -510,11 +549,17 @@ class ReplicaGroupRound:
         if not self.hades and drop is None:
             # the VAL exchange overlaps the refill: the refill touches only this replica's op slab and
             # its mirrors, the VAL batch only the table, so their order does not matter
-            w_tot = self._gather_async(*r.val_total_io())
-            w_val = self._gather_async(*r.val_io(width))
-            r.refill()
-            w_tot.wait()
-            w_val.wait()
+            if fold:
+                w_val = self._gather_async(*r.val_io_total(width))
+                r.refill()
+                w_val.wait()
+                r.take_val_totals(width)
+            else:
+                w_tot = self._gather_async(*r.val_total_io())
+                w_val = self._gather_async(*r.val_io(width))
+                r.refill()
+                w_tot.wait()
+                w_val.wait()
             _timed(events, "vals", lambda: r.vals(width), timed_batches)
             return
         self._gather(*r.val_total_io())
@@ -604,6 +649,7 @@ class LoopbackGroup:
         seen = observer or (lambda phase: None)
         steady = self.plan is not None and self.plan.steady(drop is not None or self.hades or
                                                             not all(r.unique_acks for r in rs))
+        fold = steady and self.plan.fold
         for r in rs:
             if steady:
                 r.own_total = None
@@ -611,16 +657,24 @@ class LoopbackGroup:
             else:
                 r.local()
         seen("local")
-        self._gather_io([r.inv_total_io() for r in rs])
-        if steady:
-            width = self.plan.width
+        if fold:
+            width = self.plan.slab_width()
+            shapes = [(width, None)] * len(rs)
+            self._gather_io([r.inv_io_total(width) for r in rs])
+            for r in rs:
+                r.take_inv_totals(width)
+        elif steady:
+            self._gather_io([r.inv_total_io() for r in rs])
+            width = self.plan.slab_width()
             shapes = [(width, None)] * len(rs)
         else:
+            self._gather_io([r.inv_total_io() for r in rs])
             shapes = [r.round_shape() for r in rs]
             width = shapes[0][0]                 # the same on every replica (max of the same totals)
             if self.plan is not None:
                 self.plan.calibrate(width, rs[0].W * rs[0].C)
-        self._gather_io([r.inv_io(width) for r in rs])
+        if not fold:
+            self._gather_io([r.inv_io(width) for r in rs])
         if drop is not None:
             for r in rs:
                 r.peer_failing()
@@ -632,8 +686,13 @@ class LoopbackGroup:
         for r, (_, stride) in zip(rs, shapes):
             r.acks(width, stride)
         seen("acks")
-        self._gather_io([r.val_total_io() for r in rs])
-        self._gather_io([r.val_io(width) for r in rs])
+        if fold:
+            self._gather_io([r.val_io_total(width) for r in rs])
+            for r in rs:
+                r.take_val_totals(width)
+        else:
+            self._gather_io([r.val_total_io() for r in rs])
+            self._gather_io([r.val_io(width) for r in rs])
         for r in rs:
             r.vals(width)
         seen("vals")

@@ -38,8 +38,9 @@ def test_one_rank_rccl_group_round(args):
     print(d)
     assert d["launches"] == [15, 15, 15], d          # 3 rounds x (local, INV per peer (2), the ACK rows, VAL)
     assert d["diverged_keys"] == 0, d
-    # per round and replica: INV totals + INV slabs + VAL totals + VAL slabs gathered, ACKs all-to-all
+    # per round and replica: INV totals + INV slabs + VAL totals + VAL slabs gathered in the calibrating
+    # round, the slabs alone (each carrying its total, WidthPlan.fold) in the 6 steady ones; ACKs all-to-all
     # (3 mirrored rounds, then 4 steady ones under the sync check)
-    assert d["calls"]["all_gather_into_tensor"] == 7 * 4 * 3 and d["calls"]["all_to_all_single"] == 7 * 3, d
+    assert d["calls"]["all_gather_into_tensor"] == (4 + 6 * 2) * 3 and d["calls"]["all_to_all_single"] == 7 * 3, d
     assert d["width"] is not None
     assert min(d["committed"]) > 0

@@ -43,15 +43,18 @@ def _key_images(g, o, keys):
     return rows
 
 
-@pytest.mark.parametrize("n_rep,workers,write_pm,rounds,retry,skew", [
-    (2, 24, 300, 4, False, 0), (3, 16, 400, 4, False, 0), (4, 8, 500, 3, False, 0), (8, 16, 200, 3, False, 0),
-    (8, 16, 200, 4, True, 3), (8, 16, 200, 4, True, 0), (3, 24, 400, 5, True, 3)])
-def test_loopback_group_parity_and_convergence(n_rep, workers, write_pm, rounds, retry, skew):
+@pytest.mark.parametrize("n_rep,workers,write_pm,rounds,retry,skew,fold", [
+    (2, 24, 300, 4, False, 0, True), (3, 16, 400, 4, False, 0, True), (4, 8, 500, 3, False, 0, True),
+    (8, 16, 200, 3, False, 0, True), (8, 16, 200, 4, True, 3, True), (8, 16, 200, 4, True, 0, True),
+    (3, 24, 400, 5, True, 3, True), (3, 24, 400, 5, True, 3, False)])
+def test_loopback_group_parity_and_convergence(n_rep, workers, write_pm, rounds, retry, skew, fold, monkeypatch):
     """(8, 16, 200, 3) is BASELINE configs[3]'s group on one GPU: 8 replicas (the width of the
     membership vectors), 20 % writes, Zipf 0.99 -- every phase, kernel and slab layout of the RCCL
     run, with every launch of every replica mirrored into its oracle twin. retry / skew: the
     configuration bench.py --gpus N runs (refill_ops' retry, stalled ops keep their slots, and the
-    reference's skew optimisations, config.h:79-80) and the reference's shipped one (skew 0)."""
+    reference's skew optimisations, config.h:79-80) and the reference's shipped one (skew 0). fold: the
+    steady rounds' totals ride in a spare slot of each slab (WidthPlan.fold) or get their own gathers."""
+    monkeypatch.setenv("HKV_GROUP_FOLD_TOTALS", "1" if fold else "0")
     from hermes_amd.kvs import HermesKV
     from hermes_amd.replica_group import LoopbackGroup, ReplicaRound
     from hermes_amd.workload import zipf_params

@@ -2864,13 +2864,30 @@ __device__ __forceinline__ uint32_t ld_sys_u8(const uint8_t *p)
     return (ld_sys32(reinterpret_cast<const void *>(a & ~(uintptr_t)3)) >> (8 * (a & 3))) & 0xFFu;
 }
 
-// exec_ack's read_write_ops completion of slot `done` in a caller's pinned copy (hermesKV.c:660-668)
-__device__ __forceinline__ void hp_complete_rw(uint8_t *rw, int done, uint32_t op_size)
+// exec_ack's read_write_ops completion of slot `done` in a caller's pinned copy (hermesKV.c:660-668).
+// pre: bytes 8..11 of slot pre_slot, read ahead (hp_rw_ahead); a slot of another opcode keeps its state,
+// so it is not written at all.
+__device__ __forceinline__ void hp_complete_rw(uint8_t *rw, int done, uint32_t op_size, uint32_t pre = 0, int pre_slot = -1)
 {
     uint8_t *w = rw + (size_t)done * op_size;
-    const uint8_t oc = (uint8_t)ld_sys_u8(w + 8);
-    const uint8_t ns = oc == kOpGet ? kNew : oc == kOpPut ? kPutComplete : oc == kOpRmw ? kRmwComplete : (uint8_t)ld_sys_u8(w + 9);
+    const uint8_t oc = done == pre_slot ? (uint8_t)pre : (uint8_t)ld_sys_u8(w + 8);
+    if (oc != kOpGet && oc != kOpPut && oc != kOpRmw) return;
+    const uint8_t ns = oc == kOpGet ? kNew : oc == kOpPut ? kPutComplete : kRmwComplete;
     __hip_atomic_store(w + 9, ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// An ACK's read_write_ops slot is the entry's op-buffer index (exec_ack): its opcode is read right after
+// the lookup, so the read overlaps the rounds instead of following them -- from the opcodes the caller
+// staged in device memory (rwo), else from byte 8 of the slot in the pinned copy (over PCIe)
+__device__ __forceinline__ void hp_rw_ahead(const uint8_t *rw, const uint8_t *rwo, const uint8_t *line, uint32_t op_size,
+                                            uint32_t &pre, int &pre_slot)
+{
+    Meta m;
+    meta_load(line, m);
+    const int ob = m_obi(m);
+    if (ob == kObiEmpty) return;
+    pre = rwo ? ld_sys_u8(rwo + ob) : ld_sys_u8(rw + (size_t)ob * op_size + 8);
+    pre_slot = ob;
 }
 
 // The LDS of one partition's work (both kernels)
@@ -2885,6 +2902,8 @@ struct HpLds {
     uint16_t shs[kPartCap];
     int cmd;
     int32_t nb;
+    int32_t nm;                     // k_hserve: launches taken in this pass
+    int32_t sb[kPartMaxB + 1];      // ... their first batches (sb[nm]: all of them)
 };
 
 // The batch ranges of partition g (bh, prow in LDS): per-batch slot and word offsets (one wave)
@@ -3015,6 +3034,11 @@ __device__ void hp_partition(const HostPartCommon &p, HpLds &L, int g, int nb, u
         }
         if (e == kNone) x[9] = kMiss;
     }
+    uint32_t rw_pre = 0;
+    int rw_pre_slot = -1;
+    if (type == kAcks && hd.rw && e != kNone)
+        hp_rw_ahead(reinterpret_cast<const uint8_t *>(hd.rw), reinterpret_cast<const uint8_t *>(hd.rwo),
+                    reinterpret_cast<const uint8_t *>(&L.sln[s * 4]), p.g.op_size, rw_pre, rw_pre_slot);
     if (pr) p.prof[2] = wall_clock64();
     uint32_t hs = 0;
     if (e != kNone) {
@@ -3082,7 +3106,7 @@ __device__ void hp_partition(const HostPartCommon &p, HpLds &L, int g, int nb, u
         }
     }
     // a completing ACK of the rounds marks its read_write_ops slot (exec_ack left it to us)
-    if (done >= 0 && c.rw) hp_complete_rw(c.rw, done, p.g.op_size);
+    if (done >= 0 && c.rw) hp_complete_rw(c.rw, done, p.g.op_size, rw_pre, rw_pre_slot);
     if (pr) p.prof[3] = wall_clock64();
     L.sdirty[s] = 0;
     __syncthreads();
@@ -3164,38 +3188,86 @@ __global__ __launch_bounds__(kHpThreads) void k_hserve(HostServeLaunch p)
     uint64_t idle_since = t0;
     for (;;) {
         const HostRingSlot *sl = p.ring + (next % (uint32_t)p.ring_n);
-        if (tid == 0) {
+        if (tid < 64) {
             int cmd = 0;
-            for (;;) {
-                if (ld_sys32(&sl->seq) == next) {
-                    cmd = 1;
-                    L.nb = (int32_t)ld_sys32(&sl->n_batches);
-                    break;
+            if (tid == 0) {
+                for (;;) {
+                    if (ld_sys32(&sl->seq) == next) {
+                        cmd = 1;
+                        break;
+                    }
+                    const uint64_t now = wall_clock64();
+                    if (ld_sys32(p.stop) || now - idle_since > p.idle_ticks || now - t0 > p.life_ticks) {
+                        cmd = 2;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(4);
                 }
-                const uint64_t now = wall_clock64();
-                if (ld_sys32(p.stop) || now - idle_since > p.idle_ticks || now - t0 > p.life_ticks) {
-                    cmd = 2;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(4);
+                L.cmd = cmd;
             }
-            L.cmd = cmd;
+            cmd = __shfl(cmd, 0);
+            if (cmd == 1) {   // this launch and the ones published after it while their batches fit: lane k
+                              // reads launch next + k's seq and batch count, all loads in flight together
+                const HostRingSlot *sk = p.ring + ((next + (uint32_t)tid) % (uint32_t)p.ring_n);
+                const bool in = tid < p.merge;
+                const uint32_t sq = in && tid > 0 ? ld_sys32(&sk->seq) : next;
+                // the count only once the seq is seen (the host writes a slot's contents before its seq)
+                const int nbk = in && sq == next + (uint32_t)tid ? (int)ld_sys32(&sk->n_batches) : 0;
+                int incl = nbk;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const int v = __shfl_up(incl, d, 64);
+                    if (tid >= d) incl += v;
+                }
+                const bool ok = in && sq == next + (uint32_t)tid && (tid == 0 || incl <= kPartMaxB);
+                const uint64_t stop = __ballot(!ok);   // the first launch not taken (lane 0 always is)
+                const int nm = stop ? __ffsll((long long)stop) - 1 : 64;
+                if (tid < nm) L.sb[tid + 1] = incl;
+                if (tid == 0) {
+                    L.sb[0] = 0;
+                    L.nm = nm;
+                }
+            }
         }
         __syncthreads();
         if (L.cmd == 2) break;
         const bool pr = p.c.prof && g == 0 && tid == 0;
         const uint64_t t_seen = pr ? wall_clock64() : 0;
-        const int nb = L.nb;
-        if (tid < 6 * nb) {   // the headers, 8 bytes per thread
-            reinterpret_cast<uint64_t *>(L.bh)[tid] = ld_sys64(reinterpret_cast<const uint64_t *>(sl->hdr) + tid);
-        } else if (tid >= 128 && tid < 128 + 2 * (kPartMaxB / 4)) {   // part rows g and g + 1, 8 bytes per thread
-            const int k = tid - 128, row = k / (kPartMaxB / 4), wd = k % (kPartMaxB / 4);
-            reinterpret_cast<uint64_t *>(L.prow[row])[wd] = ld_sys64(reinterpret_cast<const uint64_t *>(sl->part[g + row]) + wd);
+        const int nm = L.nm, nbt = L.sb[nm];
+        // the headers (8 bytes per thread) and part rows g and g + 1 (2 bytes per thread) of every launch
+        // taken, its batches after the previous launch's
+        constexpr int HW = (int)(sizeof(HostPartHdr) / 8);
+        if (tid < HW * nbt) {
+            const int b = tid / HW;
+            int k = 0;
+            while (L.sb[k + 1] <= b) ++k;
+            const HostRingSlot *sk = p.ring + ((next + (uint32_t)k) % (uint32_t)p.ring_n);
+            reinterpret_cast<uint64_t *>(L.bh)[tid] =
+                ld_sys64(reinterpret_cast<const uint64_t *>(sk->hdr) + (tid - HW * L.sb[k]));
+        } else if (tid >= 128 && tid < 128 + 2 * nbt) {
+            const int q = tid - 128, row = q / nbt, b = q % nbt;
+            int k = 0;
+            while (L.sb[k + 1] <= b) ++k;
+            const HostRingSlot *sk = p.ring + ((next + (uint32_t)k) % (uint32_t)p.ring_n);
+            L.prow[row][b] = (uint16_t)ld_sys_u16(&sk->part[g + row][b - L.sb[k]]);
         }
         __syncthreads();
+        if (tid == 0) {   // partition g of the taken launches within kPartCap elements (the first always is)
+            int k = 1, tot = 0;
+            for (int b = 0; b < L.sb[1]; ++b) tot += L.prow[1][b] - L.prow[0][b];
+            for (; k < nm; ++k) {
+                int c = 0;
+                for (int b = L.sb[k]; b < L.sb[k + 1]; ++b) c += L.prow[1][b] - L.prow[0][b];
+                if (tot + c > kPartCap) break;
+                tot += c;
+            }
+            L.nm = k;
+        }
+        __syncthreads();
+        const int taken = L.nm, nb = L.sb[taken];
         hp_scan(L, nb);
         __syncthreads();
-        hp_partition(p.c, L, g, nb, next);
+        hp_partition(p.c, L, g, nb, next + (uint32_t)taken - 1u);
         if (pr) {   // HKV_PART_PROF: workgroup 0's phase sums over the launches it served (debug)
             unsigned long long *q = p.c.prof;
             q[8] += t_seen - idle_since;
@@ -3205,7 +3277,7 @@ __global__ __launch_bounds__(kHpThreads) void k_hserve(HostServeLaunch p)
             q[12] += q[4] - q[3];
             q[13] += 1;
         }
-        ++next;
+        next += (uint32_t)taken;
         idle_since = wall_clock64();
         __syncthreads();   // LDS reuse by the next launch
     }

@@ -99,8 +99,9 @@ struct HostPartHdr {
     int32_t type, count, esz;
     uint8_t g_membership, w_ack_init, pad0, pad1;
     uint64_t out;     // device address the results go to (pinned), or 0: back into elems
+    uint64_t rwo;     // ACK batches staged in device memory: each read_write_ops slot's opcode there, else 0
 };
-static_assert(sizeof(HostPartHdr) == 48, "HostPartHdr is three 16-byte loads");
+static_assert(sizeof(HostPartHdr) == 56, "HostPartHdr is seven 8-byte words");
 struct HostPartCommon {
     Geometry g;
     const uint8_t *index;
@@ -137,6 +138,7 @@ struct HostServeLaunch {
     const uint32_t *stop;        // pinned: non-zero makes every workgroup leave between launches
     uint32_t *exited;            // pinned: workgroup g stores epoch into exited[g] when it leaves
     uint64_t idle_ticks, life_ticks;   // wall_clock64 ticks (100 MHz)
+    int32_t merge;               // launches one workgroup pass may take together (HKV_SERVE_MERGE; 1: one at a time)
     uint32_t start[kPartG];      // the first launch each workgroup takes
 };
 int launch_host_serve(const HostServeLaunch &sl, hipStream_t s);

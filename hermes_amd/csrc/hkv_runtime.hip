@@ -102,7 +102,7 @@ struct HostReq {
     // partitioned: staged in the caller's t_stage (device addresses), partition g at [poff[g], poff[g+1])
     bool part = false;
     uint32_t pseq = 0;     // launched as partitioned launch pseq (0: in a set's launch)
-    uint64_t st_elems = 0, st_pos = 0, st_rw = 0, st_out = 0;
+    uint64_t st_elems = 0, st_pos = 0, st_rw = 0, st_out = 0, st_rwo = 0;
     uint16_t poff[kPartG + 1];
 };
 
@@ -937,6 +937,7 @@ static void host_launch_mixed(hkv_table *t, HostSet *set, std::unique_lock<std::
 }
 
 constexpr int kRingN = 16;   // ring slots of the serving kernel (launches in flight at most)
+constexpr int kServeMerge = 4;   // published launches one serving-kernel pass may take together (HKV_SERVE_MERGE)
 
 // The serving kernel has started leaving (some workgroup recorded the current epoch)
 static bool srv_exited(const hkv_table *t)
@@ -1027,6 +1028,8 @@ static void srv_ensure(hkv_table *t)
     sl.exited = t->srv_words_d + 32;
     sl.idle_ticks = (uint64_t)(idle_ms * 1e5);     // wall_clock64: 100 MHz
     sl.life_ticks = (uint64_t)1e8;                 // 1 s, then a fresh server
+    static const int merge = getenv("HKV_SERVE_MERGE") ? std::max(1, atoi(getenv("HKV_SERVE_MERGE"))) : kServeMerge;
+    sl.merge = std::min(merge, kRingN / 2);
     for (int g = 0; g < kPartG; ++g) sl.start[g] = __atomic_load_n(t->pflags + g, __ATOMIC_ACQUIRE) + 1;
     srv_set_stop(t, 0u);
     if (!t->srv_ev && hipEventCreateWithFlags(&t->srv_ev, hipEventDisableTiming) != hipSuccess) die("event");
@@ -1148,6 +1151,7 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
         h.pos = r->st_pos;
         h.out = r->st_out;
         h.rw = r->st_rw;
+        h.rwo = r->st_rwo;
         h.type = r->type;
         h.count = r->n;
         h.esz = r->esz;
@@ -1264,10 +1268,12 @@ static bool host_stage_part(const hkv_table *t, HostReq &r)
         st.cap = cap;
     }
     const bool vram = stage_vram_usable();
-    if (vram && ebytes + pbytes > st.vcap) {
+    // ACK batches in device memory: each read_write_ops slot's opcode beside the elements (hp_rw_ahead)
+    const size_t obytes = vram && rw_bytes ? align16((size_t)t->cfg.rw_len) : 0;
+    if (vram && ebytes + pbytes + obytes > st.vcap) {
         if (st.v) (void)hipFree(st.v);
         st.v = nullptr;
-        const size_t cap = std::max(ebytes + pbytes, (size_t)1 << 20);
+        const size_t cap = std::max(ebytes + pbytes + obytes, (size_t)1 << 20);
         if (hipExtMallocWithFlags((void **)&st.v, cap, hipDeviceMallocFinegrained) != hipSuccess) die("caller VRAM staging alloc");
         st.vcap = cap;
     }
@@ -1275,7 +1281,7 @@ static bool host_stage_part(const hkv_table *t, HostReq &r)
     uint16_t cur[kPartG];
     for (int g = 0; g < kPartG; ++g) cur[g] = r.poff[g];
     // built in a host buffer first when it goes to VRAM: one sequential copy, whole write-combined lines
-    if (vram && st.tmp.size() < ebytes + pbytes) st.tmp.resize(ebytes + pbytes);
+    if (vram && st.tmp.size() < ebytes + pbytes + obytes) st.tmp.resize(ebytes + pbytes + obytes);
     uint8_t *sb = vram ? st.tmp.data() : st.h;
     uint16_t *pos = reinterpret_cast<uint16_t *>(sb + ebytes);
     for (int i = 0; i < r.n; ++i) {
@@ -1287,8 +1293,14 @@ static bool host_stage_part(const hkv_table *t, HostReq &r)
     }
     if (rw_bytes) memcpy(st.h + ebytes + pbytes, r.rw, rw_bytes);
     r.rw_bytes = rw_bytes;
+    r.st_rwo = 0;
+    if (obytes) {
+        uint8_t *oc = sb + ebytes + pbytes;
+        for (int k = 0; k < t->cfg.rw_len; ++k) oc[k] = r.rw[(size_t)k * t->geo.op_size + 8];
+        r.st_rwo = (uint64_t)(uintptr_t)(st.v + ebytes + pbytes);
+    }
     if (vram) {
-        memcpy(st.v, sb, ebytes + pbytes);
+        memcpy(st.v, sb, ebytes + pbytes + obytes);
         __builtin_ia32_sfence();   // the write-combined stores leave before the launch that reads them
         r.st_elems = (uint64_t)(uintptr_t)st.v;
         r.st_pos = (uint64_t)(uintptr_t)(st.v + ebytes);

@@ -98,6 +98,7 @@ struct BatchArgs {
     const uint8_t *opc;          // local launches: the caller's opcode mirror (may be NULL, see k_local_pre)
     const uint8_t *patch;        // local direct path: pending header writes (hkv_batch_desc.d_patch), or NULL
     uint8_t *rws;                // ACK launches: read_write_ops state mirror (hkv_batch_desc.d_rw_state), or NULL
+    const uint8_t *rwo;          // ACK launches: read_write_ops opcode mirror (hkv_batch_desc.d_opcode_in), or NULL
     const uint64_t *pkeys;       // local direct path: the PUT-key mirror (hkv_batch_desc.d_put_keys), or NULL
     int32_t n_rows, skip_row;    // HKV_BATCH_ROWS: rows applied in order (k_unique_rows), one skipped (-1: none)
     int64_t row_stride;          // elements between rows
@@ -249,6 +250,7 @@ __device__ __forceinline__ void elem_at(const BatchArgs &a, uint32_t i, uint8_t 
         idx = (uint8_t)(i - start);
         c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
         c.rws = a.rws ? a.rws + (int64_t)b * (a.rw_stride / a.g.op_size) : nullptr;
+        c.rwo = a.rwo ? a.rwo + (int64_t)b * (a.rw_stride / a.g.op_size) : nullptr;
     }
     x = a.elems + (int64_t)i * a.esz;
 }
@@ -2533,6 +2535,7 @@ __device__ __forceinline__ SmallView small_at(const BatchArgs &a, const int32_t 
         v.live = a.counts == nullptr || idx < a.counts[b];
         c.rw = a.rw ? a.rw + (int64_t)b * a.rw_stride : nullptr;
         c.rws = a.rws ? a.rws + (int64_t)b * (a.rw_stride / a.g.op_size) : nullptr;
+        c.rwo = a.rwo ? a.rwo + (int64_t)b * (a.rw_stride / a.g.op_size) : nullptr;
         return v;
     }
     int lo = 0, hi = a.n_batches;  // the last b with bstart[b] <= i
@@ -3409,6 +3412,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.skip_row = bl.skip_row;
     a.row_stride = bl.row_stride;
     a.rws = bl.type == kAcks ? bl.rw_state : nullptr;
+    a.rwo = bl.type == kAcks ? bl.opcode_in : nullptr;
     static const int dbg_env = getenv("HKV_DBG") ? atoi(getenv("HKV_DBG")) : 0;
     a.dbg = dbg_env;
     static const int check_unique_env = getenv("HKV_CHECK_UNIQUE") ? atoi(getenv("HKV_CHECK_UNIQUE")) : 0;

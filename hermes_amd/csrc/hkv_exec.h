@@ -128,6 +128,7 @@ struct Ctx {           // per-launch constants
     uint8_t w_ack_init;
     uint8_t *rw;       // this element's batch read_write_ops (ACKs)
     uint8_t *rws;      // its state-byte mirror (hkv_batch_desc.d_rw_state), or null
+    const uint8_t *rwo = nullptr;   // its opcode mirror (hkv_batch_desc.d_opcode_in of an ACK launch), or null
     int *rw_done;      // non-null: exec_ack leaves the read_write_ops completion to the caller
     VCopy *vc;         // non-null: big-value copies are recorded here instead of made (at most one per dispatch)
 };
@@ -329,6 +330,19 @@ __device__ __forceinline__ void exec_inv(uint8_t *inv, uint8_t *entry, Meta &m, 
     if (inv[8] != kOpInvAbort && inv[8] != kInvOutOfGroup) inv[8] = kInvSuccess;
 }
 
+// exec_ack's read_write_ops completion of slot `done` (hermesKV.c:660-668): GET -> NEW, PUT ->
+// PUT_COMPLETE, RMW -> RMW_COMPLETE; a slot of any other opcode keeps its state, so it is not written.
+// The opcode comes from the caller's opcode mirror when the launch has one (c.rwo), else from the op.
+__device__ __forceinline__ void complete_rw_slot(const Ctx &c, int done)
+{
+    uint8_t *w = c.rw + (size_t)done * c.g.op_size;
+    const uint8_t oc = c.rwo ? c.rwo[done] : w[8];
+    if (oc != kOpGet && oc != kOpPut && oc != kOpRmw) return;
+    const uint8_t ns = oc == kOpGet ? kNew : oc == kOpPut ? kPutComplete : kRmwComplete;
+    w[9] = ns;
+    if (c.rws) c.rws[done] = ns;
+}
+
 // hermes_exec_ack, hermesKV.c:591-674
 __device__ __forceinline__ void exec_ack(uint8_t *ack, Meta &m, const Ctx &c)
 {
@@ -356,25 +370,11 @@ __device__ __forceinline__ void exec_ack(uint8_t *ack, Meta &m, const Ctx &c)
     } else if ((ack[8] == kLastAckSuccess || ack[8] == kLastAckNoBcast) && done != kObiEmpty && c.rw != nullptr) {
         // every completer of this slot writes the same byte (it depends only on the slot's
         // own opcode), so concurrent segments completing one slot are benign
-        uint8_t *w = c.rw + (size_t)done * c.g.op_size;
-        uint8_t oc = w[8];
-        const uint8_t ns = oc == kOpGet ? kNew : oc == kOpPut ? kPutComplete : oc == kOpRmw ? kRmwComplete : w[9];
-        w[9] = ns;
-        if (c.rws) c.rws[done] = ns;
+        complete_rw_slot(c, done);
     }
     if (ack[8] != kLastAckSuccess) ack[8] = kAckSuccess;
 }
 
-// exec_ack's read_write_ops completion of slot `done` (hermesKV.c:660-668), for callers that find
-// the batch only for completing ACKs
-__device__ __forceinline__ void complete_rw_slot(const Ctx &c, int done)
-{
-    uint8_t *w = c.rw + (size_t)done * c.g.op_size;
-    const uint8_t oc = w[8];
-    const uint8_t ns = oc == kOpGet ? kNew : oc == kOpPut ? kPutComplete : oc == kOpRmw ? kRmwComplete : w[9];
-    w[9] = ns;
-    if (c.rws) c.rws[done] = ns;
-}
 
 // hermes_exec_val, hermesKV.c:676-703
 __device__ __forceinline__ void exec_val(uint8_t *val, Meta &m)

@@ -561,7 +561,7 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.counts = packed ? nullptr : d->d_counts;
     bl.state_out = d->d_state_out;
     static const bool opc_off = getenv("HKV_OPCODE_IN") && atoi(getenv("HKV_OPCODE_IN")) == 0;  // experiments
-    bl.opcode_in = d->type == kLocal && !opc_off ? d->d_opcode_in : nullptr;
+    bl.opcode_in = (d->type == kLocal || d->type == kAcks) && !opc_off ? d->d_opcode_in : nullptr;
     bl.patch = d->type == kLocal ? d->d_patch : nullptr;
     bl.rw_state = d->type == kAcks ? d->d_rw_state : nullptr;
     // HKV_PUT_KEYS=0: the PUT-key mirror ignored (experiments)

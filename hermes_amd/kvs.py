@@ -176,7 +176,8 @@ class HermesKV:
               patch: torch.Tensor | None = None, rw_state: torch.Tensor | None = None,
               unique: bool = False, put_keys: torch.Tensor | None = None,
               rows: tuple[int, int, int] | None = None, stage: int = 0,
-              ack_out: torch.Tensor | None = None, ack_out_size: int = 16, phys: torch.Tensor | None = None) -> None:
+              ack_out: torch.Tensor | None = None, ack_out_size: int = 16, phys: torch.Tensor | None = None,
+              rw_opcodes: torch.Tensor | None = None) -> None:
         """Apply n_batches batches of one type, concatenated in `elems` (uint8, on the GPU),
         in concatenation order, asynchronously on `stream` (default: torch's current).
         offsets (INV / ACK / VAL batches): the batches stored back to back, batch b at elements
@@ -192,7 +193,9 @@ class HermesKV:
         (HKV_BATCH_PREPASS_CANCEL), 0 runs all of it. ack_out (unique INV launches): every element's ACK
         as the worker's ACK callbacks make it, ack_out_size bytes each (hkv_batch_desc.d_ack_out). phys
         (unique INV and VAL launches): each element's located log offset (hkv_wl_peer_locate; ~0 none), the
-        entry line read without the bucket first (hkv_batch_desc.d_phys)."""
+        entry line read without the bucket first (hkv_batch_desc.d_phys). rw_opcodes (ACK batches): the
+        read_write_ops' opcode mirror, one byte per slot (hkv_batch_desc.d_opcode_in): completions read the
+        opcode there instead of the op."""
         assert elems.is_cuda and elems.dtype == torch.uint8
         total = stride if offsets is not None else n_batches * stride
         if rows is not None:
@@ -218,6 +221,10 @@ class HermesKV:
         if opcode_in is not None:   # local batches: the caller's mirror of each element's opcode byte
             assert opcode_in.is_cuda and opcode_in.dtype == torch.uint8 and opcode_in.numel() >= n_batches * stride
             d.d_opcode_in = opcode_in.data_ptr()
+        if rw_opcodes is not None:   # ACK batches: the read_write_ops' opcode mirror
+            assert opcode_in is None and rw is not None and rw_opcodes.is_cuda and rw_opcodes.dtype == torch.uint8
+            assert rw_opcodes.numel() >= n_batches * (rw_stride_bytes // self.sizes.op)
+            d.d_opcode_in = rw_opcodes.data_ptr()
         if patch is not None:
             assert patch.is_cuda and patch.dtype == torch.uint8 and patch.numel() >= n_batches * stride * 16
             d.d_patch = patch.data_ptr()

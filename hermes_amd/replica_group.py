@@ -293,13 +293,13 @@ class ReplicaRound:
             if T and self.ack_rows:
                 self.kvs.batch(L.BatchType.acks, self.ack_recv, W, T, self.ack_size, self.mb, rw=self.ops,
                                rw_stride_bytes=LOCAL * self.op, offsets=self.inv_off, rw_state=self.states,
-                               unique=True, rows=(N, width, self.rank))
+                               unique=True, rows=(N, width, self.rank), rw_opcodes=self._rwo())
             elif T:
                 for p in range(N):
                     if p != self.rank:
                         self.kvs.batch(L.BatchType.acks, self.ack_recv[p * width * self.ack_size:], W, T, self.ack_size,
                                        self.mb, rw=self.ops, rw_stride_bytes=LOCAL * self.op, offsets=self.inv_off,
-                                       rw_state=self.states, unique=True)
+                                       rw_state=self.states, unique=True, rw_opcodes=self._rwo())
             if self.count_elems:
                 self.elem_totals[1] += (N - 1) * self.inv_off[W]
             check(_L.hkv_wl_collect_vals_rows(_ptr(self.ack_recv), W, N, width, self.ack_size, _ptr(self.val_slab), C,
@@ -314,12 +314,17 @@ class ReplicaRound:
         if self.count_elems:
             self.elem_totals[1] += self.ack_batch_count.sum()
         self.kvs.batch(L.BatchType.acks, self.ack_batch, W, stride, self.ack_size, self.mb,
-                       counts=self.ack_batch_count, rw=self.ops, rw_stride_bytes=LOCAL * self.op, rw_state=self.states)
+                       counts=self.ack_batch_count, rw=self.ops, rw_stride_bytes=LOCAL * self.op, rw_state=self.states,
+                       rw_opcodes=self._rwo())
         check(_L.hkv_wl_collect_vals(_ptr(self.ack_batch), _ptr(self.ack_batch_count), W, stride, self.ack_size,
                                      _ptr(self.val_slab), C, _ptr(self.val_count), self.rank,
                                      _ptr(self.held[1:]), None, _s()), "collect_vals")
         check(_L.hkv_wl_pack_rows(_ptr(self.val_slab), _ptr(self.val_count), W, C, L.OP_META_SIZE,
                                   _ptr(self.val_pack), _ptr(self.val_off), _s()), "pack vals")
+
+    def _rwo(self):
+        """the opcode mirror the ACK launches complete from (HKV_ACK_OPCODES=0: they read the ops)"""
+        return self.opcodes if os.environ.get("HKV_ACK_OPCODES", "1") != "0" else None
 
     def vals(self, width: int):
         """Apply the gathered VALs of the peers ([N][width], row p: val_totals[p] VALs)."""

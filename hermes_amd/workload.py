@@ -284,6 +284,7 @@ class Round:
         # (at the first plan, the table populated), and each slot's word, kept by the plan (d_phys). Same box
         # (gpurun_out/r04zi): local launch 381 -> 355 us, 4.26 -> 4.35 G ops/s; off by default, as
         # HKV_PHYS_HINTS
+        self.ack_opcodes = os.environ.get("HKV_ACK_OPCODES", "1") != "0"   # ACK completions read the opcode mirror
         self.local_hints = self.fused and os.environ.get("HKV_LOCAL_HINTS", "0") == "1"
         self.trace_phys = None
         self.slot_phys = torch.full((W * S,), -1, dtype=torch.int64, device=dev) if self.local_hints else None
@@ -659,6 +660,11 @@ class Round:
         VAL-credits marshal does not maintain it)"""
         return self.states if self.fused or self.st_refill else None
 
+    def _rwo(self):
+        """the opcode mirror the ACK batch completes from (the refill keeps it; the local launch checks it
+        against every op; HKV_ACK_OPCODES=0: the completions read the ops)"""
+        return self.opcodes if self.ack_opcodes else None
+
     def ack_batch(self, acks: torch.Tensor | None = None, n_batches: int | None = None, stride: int | None = None,
                   counts: torch.Tensor | None = None):
         acks = self.acks if acks is None else acks
@@ -668,21 +674,21 @@ class Round:
             if self.ack_rows and n_rows:
                 self.kvs.batch(L.BatchType.acks, acks, self.W, T, self.ack_size, self.mb, rw=self.ops,
                                rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off, rw_state=self._rws(),
-                               unique=True, rows=(n_rows, T, -1))
+                               unique=True, rows=(n_rows, T, -1), rw_opcodes=self._rwo())
                 return
             for r in range(n_rows):
                 self.kvs.batch(L.BatchType.acks, acks[r * T * self.ack_size:], self.W, T, self.ack_size, self.mb,
                                rw=self.ops, rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off,
-                               rw_state=self._rws(), unique=True)
+                               rw_state=self._rws(), unique=True, rw_opcodes=self._rwo())
             return
         if self.fit and stride is None:   # this round's packed ACKs
             self.kvs.batch(L.BatchType.acks, acks, self.W, self.ack_total, self.ack_size, self.mb,
                            rw=self.ops, rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off,
-                           rw_state=self._rws())
+                           rw_state=self._rws(), rw_opcodes=self._rwo())
             return
         self.kvs.batch(L.BatchType.acks, acks, n_batches or self.W, stride or self.ack_width, self.ack_size,
                        self.mb, counts=self.ack_count if counts is None else counts, rw=self.ops,
-                       rw_stride_bytes=self.LOCAL * self.op, rw_state=self._rws())
+                       rw_stride_bytes=self.LOCAL * self.op, rw_state=self._rws(), rw_opcodes=self._rwo())
 
     def marshal_vals(self, acks: torch.Tensor, n: int, out: torch.Tensor):
         check(_L.hkv_wl_marshal_vals(_ptr(acks), n, self.ack_size, _ptr(out), self.machine_id, _s()),

@@ -138,7 +138,10 @@ typedef struct hkv_batch_desc {
                                    (op byte 8; n_batches * stride bytes), e.g. written by its refill
                                    (hkv_wl_refill); lets the launch find its PUTs without reading
                                    every op. A PUT the mirror misses raises error flag bit 3.
-                                   NULL = read the ops (ABI 3) */
+                                   NULL = read the ops (ABI 3). ACK batches with d_rw: the mirror of
+                                   each read_write_ops slot's opcode (rw_stride_bytes / op size per
+                                   batch), which a completion reads instead of the op; it must describe
+                                   the ops (round 4) */
     const uint8_t *d_patch;     /* device, local batches: pending header writes, HKV_PATCH_BYTES per element
                                    (n_batches * stride), NULL = none (ABI 5). An element whose patch is
                                    valid first gets the patch's bytes, exactly as if the caller had written

@@ -122,8 +122,14 @@ class Mirror:
     def batch(self, btype, elems, n_batches, stride, elem_size, membership, counts=None, rw=None,
               rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None, state_out=None, opcode_in=None,
               patch=None, rw_state=None, unique=False, put_keys=None, rows=None, stage=0, ack_out=None,
-              ack_out_size=16, phys=None):
+              ack_out_size=16, phys=None, rw_opcodes=None):
         import torch
+        if rw_opcodes is not None:   # the ACK launch's opcode mirror must be every read_write_ops slot's byte 8
+            torch.cuda.synchronize()
+            nrw = n_batches * (rw_stride_bytes // self.g.sizes.op)
+            assert np.array_equal(rw_opcodes[:nrw].cpu().numpy(),
+                                  rw[: nrw * self.g.sizes.op].cpu().numpy().reshape(nrw, self.g.sizes.op)[:, 8]), \
+                "read_write_ops opcode mirror is stale"
         if stage in (1, 3):   # a prepass (or its cancellation) changes no element and nothing of the meta
             self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
                        node_suspected, stream, state_out=state_out, opcode_in=opcode_in, patch=patch,
@@ -135,10 +141,10 @@ class Mirror:
             return
         if rows is not None:
             return self._rows(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
-                              rw_stride_bytes, rw_state, rows)
+                              rw_stride_bytes, rw_state, rows, rw_opcodes)
         if offsets is not None:
             return self._packed(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
-                                rw_stride_bytes, rw_state, unique, ack_out, ack_out_size, phys)
+                                rw_stride_bytes, rw_state, unique, ack_out, ack_out_size, phys, rw_opcodes)
         torch.cuda.synchronize()
         n = n_batches * stride * elem_size
         vt = np.dtype((np.void, elem_size))
@@ -166,7 +172,7 @@ class Mirror:
         rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
         self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
                    node_suspected, stream, state_out=state_out, opcode_in=opcode_in, patch=patch, rw_state=rw_state,
-                   unique=unique, put_keys=put_keys, stage=stage, phys=phys)
+                   unique=unique, put_keys=put_keys, stage=stage, phys=phys, rw_opcodes=rw_opcodes)
         if stage == 2:
             self.prepass = False
         torch.cuda.synchronize()
@@ -227,7 +233,7 @@ class Mirror:
         assert np.array_equal(rw_state.cpu().numpy()[:n], st_after[:n]), f"{what}: read_write_ops state mirror differs"
 
     def _rows(self, btype, elems, n_batches, total, elem_size, membership, offsets, stream, rw, rw_stride_bytes,
-              rw_state, rows):
+              rw_state, rows, rw_opcodes=None):
         """An HKV_BATCH_ROWS launch: the oracle applies row after row (skip row excepted), each row's
         batches without their holes (opcode 0); the device's rows must equal them, holes untouched."""
         import torch
@@ -249,7 +255,7 @@ class Mirror:
             flat = flat_all[r * row_stride * elem_size:(r * row_stride + total) * elem_size].reshape(total, elem_size)
             ins[r] = flat.copy()
         self._orig(btype, elems, n_batches, total, elem_size, membership, rw=rw, rw_stride_bytes=rw_stride_bytes,
-                   stream=stream, offsets=offsets, rw_state=rw_state, unique=True, rows=rows)
+                   stream=stream, offsets=offsets, rw_state=rw_state, unique=True, rows=rows, rw_opcodes=rw_opcodes)
         torch.cuda.synchronize()
         got_all = elems.cpu().numpy()
         what = f"{self.name} launch {self.launches} type {int(btype)} (rows)"
@@ -285,7 +291,8 @@ class Mirror:
         self.launches += 1
 
     def _packed(self, btype, elems, n_batches, total, elem_size, membership, offsets, stream, rw=None,
-                rw_stride_bytes=0, rw_state=None, unique=False, ack_out=None, ack_out_size=16, phys=None):
+                rw_stride_bytes=0, rw_state=None, unique=False, ack_out=None, ack_out_size=16, phys=None,
+                rw_opcodes=None):
         """A packed (HKV_BATCH_PACKED) INV / ACK / VAL launch: the oracle applies the same batches
         laid out in rows; the device's packed output must equal the oracle's rows packed again."""
         import torch
@@ -304,7 +311,7 @@ class Mirror:
         rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
         self._orig(btype, elems, n_batches, total, elem_size, membership, rw=rw, rw_stride_bytes=rw_stride_bytes,
                    stream=stream, offsets=offsets, rw_state=rw_state, unique=unique, ack_out=ack_out,
-                   ack_out_size=ack_out_size, phys=phys)
+                   ack_out_size=ack_out_size, phys=phys, rw_opcodes=rw_opcodes)
         torch.cuda.synchronize()
         e_in = rows.reshape(-1).view(np.dtype((np.void, elem_size))).copy()
         self.o.batch_multi(int(btype), e_in, n_batches, width, cnt, membership, rw_in,

@@ -671,13 +671,14 @@ __global__ __launch_bounds__(256) void k_refill_st_w(uint8_t *ops, int32_t n_wor
 
 // k_marshal_invs for ops of at most 64 bytes, one wave per WPW workers (their state loads all in
 // flight together, see k_refill_plan_w)
-template <int WPW>
+template <int WPW, bool WAVE = false>
 __global__ __launch_bounds__(256) void k_marshal_invs_w(uint8_t *ops, int32_t n_workers, int32_t stride,
                                                         uint32_t op_size, uint8_t *out, int32_t out_stride,
                                                         int32_t *count, uint32_t machine_id,
                                                         unsigned long long *held, const int32_t *aq_n,
                                                         int32_t r_alive, uint8_t *states)
 {
+    __shared__ uint32_t s_list[4][256];   // WAVE: each wave's sent ops (index in the worker | state << 16)
     const int lane = threadIdx.x & 63;
     const int wb = (blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * WPW;
     if (wb >= n_workers) return;
@@ -712,6 +713,41 @@ __global__ __launch_bounds__(256) void k_marshal_invs_w(uint8_t *ops, int32_t n_
         if (lane == 0) {
             count[w] = total < cap ? total : cap;
             if (total > cap && held) atomicAdd(held, (unsigned long long)(total - cap));
+        }
+        if (WAVE) {   // the sent ops listed in LDS, then copied four lanes per op, 16 bytes per lane
+            uint32_t *lst = s_list[threadIdx.x >> 6];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (((bs[r] >> lane) & 1ull) && rank[r] < cap) lst[rank[r]] = (uint32_t)(r * 64 + lane) | ((uint32_t)st[v][r] << 16);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int nsend = total < cap ? total : cap, q = lane & 3;
+            const uint32_t b0 = 16u * (uint32_t)q;
+            for (int j = lane >> 2; j < nsend; j += 16) {
+                const uint32_t li = lst[j];
+                const int64_t e = e0 + (int64_t)(li & 0xFFFFu);
+                uint8_t *op = ops + e * op_size;
+                uint8_t *dst = out + ((int64_t)w * out_stride + j) * op_size;
+                if (b0 + 16 <= op_size) {
+                    W16 h = *reinterpret_cast<const W16 *>(op + b0);
+                    if (q == 0) h.b = with_op_state(h.b, kOpInv, (uint8_t)machine_id);
+                    *reinterpret_cast<W16 *>(dst + b0) = h;
+                } else if (b0 + 8 <= op_size) {
+                    *reinterpret_cast<uint64_t *>(dst + b0) = *reinterpret_cast<const uint64_t *>(op + b0);
+                }
+                if (q == 0) {
+                    const uint8_t x = (uint8_t)(li >> 16);
+                    const uint8_t ns = x == kPutSuccess ? kInProgressPut : x == kRmwSuccess ? kInProgressRmw
+                                     : x == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
+                    op[9] = ns;
+                    if (states) states[e] = ns;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();   // the list is rewritten for the next worker
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            continue;
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1927,8 +1963,14 @@ int hkv_wl_marshal_invs_cap(uint8_t *ops, int32_t n_workers, int32_t stride, uin
                             uint8_t *states, void *stream)
 {
     if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
+    // HKV_MARSHAL_WAVE: the sent ops copied four lanes per op (1) or one lane per op (0)
+    static const bool mwave = !getenv("HKV_MARSHAL_WAVE") || atoi(getenv("HKV_MARSHAL_WAVE")) != 0;
     if (op_size <= 64)
-        if (wl_wpw() == 2)
+        if (wl_wpw() == 2 && mwave)
+            hipLaunchKernelGGL((k_marshal_invs_w<2, true>), dim3((unsigned)((n_workers + 7) / 8)), dim3(256), 0,
+                               (hipStream_t)stream, ops, n_workers, stride, op_size, out, out_stride, count, machine_id,
+                               held, (const int32_t *)nullptr, 1, states);
+        else if (wl_wpw() == 2)
             hipLaunchKernelGGL(k_marshal_invs_w<2>, dim3((unsigned)((n_workers + 7) / 8)), dim3(256), 0, (hipStream_t)stream,
                                ops, n_workers, stride, op_size, out, out_stride, count, machine_id, held,
                                (const int32_t *)nullptr, 1, states);

@@ -669,6 +669,46 @@ __global__ __launch_bounds__(256) void k_refill_st_w(uint8_t *ops, int32_t n_wor
     }
 }
 
+// The sent ops of one worker (bit set in bs, rank below cap; e0: the worker's first op) copied as INVs to
+// out_w + rank * op_size, four lanes per op (16 bytes a lane; op_size <= 64) from a list in LDS (lst, 256
+// words for the wave), then marked in flight in the op and the state mirror. The whole wave calls it.
+__device__ __forceinline__ void wave_copy_invs(uint8_t *ops, int64_t e0, const unsigned long long *bs, const int *rank,
+                                               int cap, int total, const uint8_t *st, uint32_t op_size, uint8_t *out_w,
+                                               uint32_t machine_id, uint8_t *states, uint32_t *lst, int lane)
+{
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        if (((bs[r] >> lane) & 1ull) && rank[r] < cap) lst[rank[r]] = (uint32_t)(r * 64 + lane) | ((uint32_t)st[r] << 16);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int nsend = total < cap ? total : cap, q = lane & 3;
+    const uint32_t b0 = 16u * (uint32_t)q;
+    for (int j = lane >> 2; j < nsend; j += 16) {
+        const uint32_t li = lst[j];
+        const int64_t e = e0 + (int64_t)(li & 0xFFFFu);
+        uint8_t *op = ops + e * op_size;
+        uint8_t *dst = out_w + (int64_t)j * op_size;
+        if (b0 + 16 <= op_size) {
+            W16 h = *reinterpret_cast<const W16 *>(op + b0);
+            if (q == 0) h.b = with_op_state(h.b, kOpInv, (uint8_t)machine_id);
+            *reinterpret_cast<W16 *>(dst + b0) = h;
+        } else if (b0 + 8 <= op_size) {
+            *reinterpret_cast<uint64_t *>(dst + b0) = *reinterpret_cast<const uint64_t *>(op + b0);
+        }
+        if (q == 0) {
+            const uint8_t x = (uint8_t)(li >> 16);
+            const uint8_t ns = x == kPutSuccess ? kInProgressPut : x == kRmwSuccess ? kInProgressRmw
+                             : x == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
+            op[9] = ns;
+            if (states) states[e] = ns;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();   // the list is rewritten for the next worker
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // k_marshal_invs for ops of at most 64 bytes, one wave per WPW workers (their state loads all in
 // flight together, see k_refill_plan_w)
 template <int WPW, bool WAVE = false>
@@ -715,38 +755,8 @@ __global__ __launch_bounds__(256) void k_marshal_invs_w(uint8_t *ops, int32_t n_
             if (total > cap && held) atomicAdd(held, (unsigned long long)(total - cap));
         }
         if (WAVE) {   // the sent ops listed in LDS, then copied four lanes per op, 16 bytes per lane
-            uint32_t *lst = s_list[threadIdx.x >> 6];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (((bs[r] >> lane) & 1ull) && rank[r] < cap) lst[rank[r]] = (uint32_t)(r * 64 + lane) | ((uint32_t)st[v][r] << 16);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const int nsend = total < cap ? total : cap, q = lane & 3;
-            const uint32_t b0 = 16u * (uint32_t)q;
-            for (int j = lane >> 2; j < nsend; j += 16) {
-                const uint32_t li = lst[j];
-                const int64_t e = e0 + (int64_t)(li & 0xFFFFu);
-                uint8_t *op = ops + e * op_size;
-                uint8_t *dst = out + ((int64_t)w * out_stride + j) * op_size;
-                if (b0 + 16 <= op_size) {
-                    W16 h = *reinterpret_cast<const W16 *>(op + b0);
-                    if (q == 0) h.b = with_op_state(h.b, kOpInv, (uint8_t)machine_id);
-                    *reinterpret_cast<W16 *>(dst + b0) = h;
-                } else if (b0 + 8 <= op_size) {
-                    *reinterpret_cast<uint64_t *>(dst + b0) = *reinterpret_cast<const uint64_t *>(op + b0);
-                }
-                if (q == 0) {
-                    const uint8_t x = (uint8_t)(li >> 16);
-                    const uint8_t ns = x == kPutSuccess ? kInProgressPut : x == kRmwSuccess ? kInProgressRmw
-                                     : x == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
-                    op[9] = ns;
-                    if (states) states[e] = ns;
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();   // the list is rewritten for the next worker
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            wave_copy_invs(ops, e0, bs, rank, cap, total, st[v], op_size, out + (int64_t)w * out_stride * op_size,
+                           machine_id, states, s_list[threadIdx.x >> 6], lane);
             continue;
         }
 #pragma unroll
@@ -767,6 +777,13 @@ __global__ __launch_bounds__(256) void k_marshal_invs_w(uint8_t *ops, int32_t n_
             if (states) states[e] = ns;
         }
     }
+}
+
+// HKV_MARSHAL_WAVE: the INV marshals copy the sent ops four lanes per op (1, default) or one lane per op (0)
+static bool marshal_wave()
+{
+    static const bool v = !getenv("HKV_MARSHAL_WAVE") || atoi(getenv("HKV_MARSHAL_WAVE")) != 0;
+    return v;
 }
 
 // workers per wave of the wave-per-worker workload kernels (HKV_WL_WPW, 1 or 2)
@@ -1108,7 +1125,7 @@ __global__ __launch_bounds__(1024) void k_scan_cap(const int32_t *counts, int32_
 __global__ __launch_bounds__(256) void k_marshal_invs_packed(uint8_t *ops, int32_t n_workers, int32_t stride,
                                                              uint32_t op_size, uint8_t *out, const int32_t *off,
                                                              const int32_t *sent, uint32_t machine_id,
-                                                             uint8_t *states)
+                                                             uint8_t *states, int32_t wave)
 {
     const int lane = threadIdx.x & 63;
     const int w = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
@@ -1127,6 +1144,12 @@ __global__ __launch_bounds__(256) void k_marshal_invs_packed(uint8_t *ops, int32
     wave_ranks(bs, lane, rank, total);
     const int cap = sent[w];
     const int64_t base = off[w];
+    if (op_size <= 64 && wave) {   // four lanes per op from a list in LDS (HKV_MARSHAL_WAVE)
+        __shared__ uint32_t s_list[4][256];
+        wave_copy_invs(ops, e0, bs, rank, cap, total, st, op_size, out + base * op_size, machine_id, states,
+                       s_list[threadIdx.x >> 6], lane);
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         if (!((bs[r] >> lane) & 1ull) || rank[r] >= cap) continue;
@@ -1963,8 +1986,7 @@ int hkv_wl_marshal_invs_cap(uint8_t *ops, int32_t n_workers, int32_t stride, uin
                             uint8_t *states, void *stream)
 {
     if (stride > 256 || n_workers <= 0 || out_stride <= 0 || op_size % 8) return -1;
-    // HKV_MARSHAL_WAVE: the sent ops copied four lanes per op (1) or one lane per op (0)
-    static const bool mwave = !getenv("HKV_MARSHAL_WAVE") || atoi(getenv("HKV_MARSHAL_WAVE")) != 0;
+    const bool mwave = marshal_wave();
     if (op_size <= 64)
         if (wl_wpw() == 2 && mwave)
             hipLaunchKernelGGL((k_marshal_invs_w<2, true>), dim3((unsigned)((n_workers + 7) / 8)), dim3(256), 0,
@@ -2088,7 +2110,7 @@ int hkv_wl_marshal_invs_packed(uint8_t *ops, int32_t n_workers, int32_t stride, 
     hipLaunchKernelGGL(k_count_invs, dim3(g), dim3(256), 0, s, states, n_workers, stride, count);
     hipLaunchKernelGGL(k_scan_cap, dim3(1), dim3(1024), 0, s, count, n_workers, C, cap, offsets, sent, held);
     hipLaunchKernelGGL(k_marshal_invs_packed, dim3(g), dim3(256), 0, s, ops, n_workers, stride, op_size, out, offsets,
-                       sent, machine_id, states);
+                       sent, machine_id, states, (int32_t)marshal_wave());
     return ok();
 }
 

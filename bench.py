@@ -137,8 +137,25 @@ def host_api_rate(seconds: float, threads=(1, 8)) -> dict:
     return out
 
 
+def refuse_debug_modes():
+    """A timing number measured with work skipped must never leave bench.py: HKV_DBG in the
+    environment, or a library built with the work-skipping modes (-DHKV_DEBUG_MODES), ends the run
+    with rc 4 and no JSON line."""
+    if os.environ.get("HKV_DBG") is not None:
+        print(f"bench.py: HKV_DBG={os.environ['HKV_DBG']!r} is set (work-skipping timing modes); no measurement "
+              "is reported from such a run", file=sys.stderr, flush=True)
+        raise SystemExit(4)
+    from hermes_amd.lib import _L, LIB_PATH
+    if _L.hkv_debug_modes():
+        print(f"bench.py: {LIB_PATH} was built with -DHKV_DEBUG_MODES (work-skipping timing modes); no "
+              "measurement is reported from it", file=sys.stderr, flush=True)
+        raise SystemExit(4)
+
+
 def main():
     a = parse()
+    if os.environ.get("HKV_DBG") is not None:   # before anything runs (the library check follows torch)
+        refuse_debug_modes()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -148,6 +165,7 @@ def main():
     import torch
     import torch.distributed as dist
 
+    refuse_debug_modes()
     dev = local_rank % max(1, torch.cuda.device_count())   # gloo tests: several ranks on one GPU
     torch.cuda.set_device(dev)
     if world > 1:
@@ -308,18 +326,32 @@ def main():
     value = committed_all / elapsed_max
     step_ms = elapsed_max * 1e3 / a.steps
     step_bytes = sum(per_launch_bytes.values())
-    # HBM traffic of the local launch: rocprofv3 PMC passes of this bench (tools/pmc.sh,
-    # tools/pmc_local.py) are committed under profiles/; counters cannot be read in this run
-    traffic, traffic_src = None, None
+    # HBM traffic per launch: rocprofv3 PMC passes of this bench (tools/pmc.sh, tools/pmc_local.py) are
+    # committed under profiles/; counters cannot be read inside the timed run itself
+    traffic, traffic_src, pmc_launches = None, None, {}
     pmc = os.path.join(ROOT, "profiles", "pmc_local_batch.json")
-    if world == 1 and not cfg3 and not cfg5 and dom == "local" and os.path.exists(pmc):
+    want = {"workers": a.workers, "keys": a.keys, "refill": a.refill, "skew": a.skew}
+    if world > 1 or cfg3 or cfg5 or dom != "local":
+        traffic_src = (f"null: PMC counters are committed for configs[1] at N=1 only (profiles/pmc_local_batch.json); "
+                       f"this run is {a.config} at N={world}")
+    elif not os.path.exists(pmc):
+        traffic_src = "null: profiles/pmc_local_batch.json is missing (tools/pmc.sh + tools/pmc_local.py write it)"
+    else:
         with open(pmc) as f:
             pj = json.load(f)
-        # only counters taken on this very configuration
-        if pj.get("config") == {"workers": a.workers, "keys": a.keys, "refill": a.refill, "skew": a.skew}:
+        if pj.get("config") != want:   # only counters taken on this very configuration
+            traffic_src = (f"null: profiles/pmc_local_batch.json holds counters of {pj.get('config')}, not of this "
+                           f"run's {want}")
+        else:
             traffic = pj["traffic_bytes"]
-            traffic_src = ("profiles/pmc_local_batch.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, separate "
-                           "runs of this configuration)")
+            pmc_launches = pj.get("launches", {})
+            traffic_src = (f"profiles/pmc_local_batch.json ({pj.get('source', 'rocprofv3 --pmc')}: FETCH_SIZE x2 + "
+                           f"WRITE_SIZE in separate rocprofv3 passes of this configuration, median of "
+                           f"{pj.get('launches_counted', pj.get('launches'))} launches)")
+    for k, v in launches.items():
+        t = pmc_launches.get(k, {}).get("traffic_bytes")
+        v["traffic"] = t
+        v["traffic_ratio"] = t / v["algorithmic_bytes"] if t else None
     refill = a.refill
     out = {
         "metric": "replicated KVS ops/s (reads+writes committed)",
@@ -367,7 +399,8 @@ def main():
             "bound": "hbm", "kernel": (f"{dom} batch launch (" + ("k_local_pre (own stream) + k_local_fused + k_local_deferred + k_commit_w, the direct path" if dom == "local"
                                                   and not cfg3 else "k_lookup + element-order rounds") + ", hkv_batch.hip)"),
             "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-            "traffic": traffic, "traffic_source": traffic_src, "launch_ms": ms.get(dom),
+            "traffic": traffic, "traffic_source": traffic_src,
+            "traffic_ratio": traffic / per_launch_bytes[dom] if traffic else None, "launch_ms": ms.get(dom),
             "launch_samples": len(events.get(dom, [])),
             "algorithmic_bytes_per_launch": per_launch_bytes[dom],
             "launches": launches,
@@ -403,7 +436,7 @@ def main():
             "what": "GET_COMPLETE with a value + PUT_COMPLETE by the PUT's own write or coalesced on a timestamp "
                     "the PUT recorded itself + RMW_COMPLETE, as a share of all commits over "
                     f"{audit['rounds']} audited rounds after the timed ones, times value"}
-    if flags_any and not os.environ.get("HKV_DBG"):   # HKV_DBG: timing experiments that skip work
+    if flags_any:
         print(json.dumps({"error": f"device consistency flags {flags_any:#x} raised", "partial": out}), flush=True)
         raise SystemExit(3)
     if cfg5:

@@ -102,7 +102,8 @@ struct BatchArgs {
     const uint64_t *pkeys;       // local direct path: the PUT-key mirror (hkv_batch_desc.d_put_keys), or NULL
     int32_t n_rows, skip_row;    // HKV_BATCH_ROWS: rows applied in order (k_unique_rows), one skipped (-1: none)
     int64_t row_stride;          // elements between rows
-    int32_t dbg;                 // HKV_DBG: timing experiments that skip work (results invalid)
+    int32_t dbg;                 // HKV_DBG: timing experiments that skip work (results invalid); always 0
+                                 // unless the library is built with -DHKV_DEBUG_MODES (HKV_DBG_ON)
     int32_t check_unique;        // HKV_CHECK_UNIQUE: HKV_BATCH_UNIQUE launches verify their keys are unique
     int32_t pre_patch_first;     // k_local_pre reads a PUT's header only when it has no patch (HKV_PRE_PATCH_FIRST)
     int32_t wave_copy;           // big values copied a wave per value (HKV_WAVE_COPY=0: by their own lane)
@@ -1185,6 +1186,13 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
 //   k_local_deferred  those waiting elements, against the final F.
 // k_commit then installs the shadows. Measured against k_lookup + k_resolve0: the entry line and
 // the op slab are read once instead of twice.
+// work-skipping timing modes of k_local_pre (tools/dbg_modes.sh): compiled in only with
+// -DHKV_DEBUG_MODES; the default build folds every test to false
+#ifdef HKV_DEBUG_MODES
+#define HKV_DBG_ON(a, bit) (((a).dbg & (bit)) != 0)
+#else
+#define HKV_DBG_ON(a, bit) false
+#endif
 constexpr int kPreElems = 1024;          // elements per k_local_pre block
 constexpr int kPreHead = 1024;           // launch head whose PUT keys every block knows
 #ifndef HKV_PRE_HASH_SLOTS
@@ -1344,9 +1352,9 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
         gk[j] = ~0ull;
         hv[j] = kNone;
     }
-    if (a.dbg & 8) return;
+    if (HKV_DBG_ON(a, 8)) return;
     const int64_t i0 = (int64_t)blockIdx.x * kPreElems;
-    const int64_t head_end = (a.dbg & 4) ? 0 : i0 < HEAD ? i0 : HEAD;  // the head: elements before the block's own
+    const int64_t head_end = HKV_DBG_ON(a, 4) ? 0 : i0 < HEAD ? i0 : HEAD;  // the head: elements before the block's own
     // PUTs that are not skipped (hermes_skip_op, hermesKV.c:709-769). Reading every op header is a
     // pass over the whole op slab; with the caller's opcode mirror only the PUTs' headers are read
     // (the others read element 0's, one cached line; k_local_fused checks the mirror against every
@@ -1425,7 +1433,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
         // mirror's PUTs take part
         in[k] = in[k] && opm[k] == kOpPut && in_count(a, (uint32_t)i);
     }
-    if (a.dbg & 16) {
+    if (HKV_DBG_ON(a, 16)) {
         uint64_t acc = 0;
 #pragma unroll
         for (int k = 0; k < kAllK; ++k) acc += h[k].a ^ h[k].b;
@@ -1453,7 +1461,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
     __syncthreads();
     const Ctx c = make_ctx(a);
     const uint64_t hput[2] = {0, (uint64_t)kOpPut};
-    const uint32_t cnt = (a.dbg & 2) ? 0 : nd;
+    const uint32_t cnt = HKV_DBG_ON(a, 2) ? 0 : nd;
     for (uint32_t base = 0; base < cnt; base += 64 * kPrePair) {
         uint64_t key[kPrePair];
         bool probe[kPrePair], ok[kPrePair];
@@ -1497,9 +1505,9 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
                 if ((uint8_t)(m0.w5 >> 16) == a.ltag) a.log[phys[k] + kEntryMetaOff + 4] = 0;
                 continue;
             }
-            if (!would_mutate(kLocal, reinterpret_cast<const uint8_t *>(hput), m0, c) || (a.dbg & 1)) continue;
+            if (!would_mutate(kLocal, reinterpret_cast<const uint8_t *>(hput), m0, c) || HKV_DBG_ON(a, 1)) continue;
             atomicMin(a.fw + fw_index(a, phys[k]), ((unsigned long long)(~a.rtag0) << 32) | idx[k]);
-            if ((uint8_t)(m0.w5 >> 16) != a.ltag && !(a.dbg & 32)) a.log[phys[k] + kEntryMetaOff + 4] = a.ltag;
+            if ((uint8_t)(m0.w5 >> 16) != a.ltag && !HKV_DBG_ON(a, 32)) a.log[phys[k] + kEntryMetaOff + 4] = a.ltag;
         }
     }
 }
@@ -3413,7 +3421,11 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.row_stride = bl.row_stride;
     a.rws = bl.type == kAcks ? bl.rw_state : nullptr;
     a.rwo = bl.type == kAcks ? bl.opcode_in : nullptr;
+#ifdef HKV_DEBUG_MODES
     static const int dbg_env = getenv("HKV_DBG") ? atoi(getenv("HKV_DBG")) : 0;
+#else
+    constexpr int dbg_env = 0;   // the default build cannot skip work (tools/dbg_modes.sh builds its own)
+#endif
     a.dbg = dbg_env;
     static const int check_unique_env = getenv("HKV_CHECK_UNIQUE") ? atoi(getenv("HKV_CHECK_UNIQUE")) : 0;
     a.check_unique = check_unique_env;
@@ -3425,7 +3437,6 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.vc_batch = vc_batch_env;
     static const int wave_shadow_env = !getenv("HKV_WAVE_SHADOW") || atoi(getenv("HKV_WAVE_SHADOW")) != 0;
     a.wave_shadow = wave_shadow_env;
-    if (dbg_env) a.error_flags = nullptr;
     a.index = bl.index;
     a.log = bl.log;
     a.rw = bl.rw;

@@ -326,6 +326,15 @@ extern "C" {
 
 int hkv_abi_version(void) { return HKV_ABI_VERSION; }
 
+int hkv_debug_modes(void)
+{
+#ifdef HKV_DEBUG_MODES
+    return 1;
+#else
+    return 0;
+#endif
+}
+
 const char *hkv_last_error(void) { return g_err.c_str(); }
 
 int hkv_table_create(const hkv_config *cfg, hkv_table **out)

@@ -53,6 +53,7 @@ class Membership(ctypes.Structure):
 
 _P = ctypes.c_void_p
 _L.hkv_abi_version.restype = ctypes.c_int
+_L.hkv_debug_modes.restype = ctypes.c_int
 _L.hkv_last_error.restype = ctypes.c_char_p
 _L.hkv_table_create.argtypes = [ctypes.POINTER(HkvConfig), ctypes.POINTER(_P)]
 _L.hkv_table_destroy.argtypes = [_P]

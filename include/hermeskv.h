@@ -225,6 +225,9 @@ typedef struct hkv_batch_desc {
 #define HKV_BATCH_PREPASS_CANCEL 128u
 #define HKV_MAX_ROWS 8
 int  hkv_abi_version(void);
+/* 1 when the library was built with work-skipping timing modes (-DHKV_DEBUG_MODES, HKV_DBG):
+ * such a build is for timing experiments only and bench.py refuses to report from it. */
+int  hkv_debug_modes(void);
 const char *hkv_last_error(void);
 
 int  hkv_table_create(const hkv_config *cfg, hkv_table **out);

@@ -1,15 +1,27 @@
-"""HBM bytes per local batch launch from a tools/pmc.sh run (FETCH_SIZE and WRITE_SIZE passes):
-    python tools/pmc_local.py TAG OUT.json [WORKERS KEYS REFILL SKEW]
+"""HBM bytes per batch launch from a tools/pmc.sh run (FETCH_SIZE and WRITE_SIZE passes):
+    python tools/pmc_local.py TAG OUT.json WORKERS KEYS REFILL SKEW
 
-A local launch is k_local_pre, k_local_fused, k_local_deferred and the k_commit after them (the
-direct path), or, on the rounds engine, the two k_lookup dispatches before a k_resolve0<0, ...>
-dispatch, that dispatch and the k_commit after it. Counters are KB per dispatch; FETCH_SIZE is doubled (on gfx950 it
-reports half the bytes of wide reads, MI355X_MICROARCH.md, HBM section). The median over the
-launches of the run is written to OUT.json, which bench.py reports as roofline.traffic."""
+Per protocol round of bench.py (the dispatches from one k_local_pre to the next) the launches are
+grouped the way bench.py times them:
+* local: k_local_pre, k_local_fused, k_local_deferred and k_commit_w (the direct path);
+* invs:  every INV launch of the round (one unique-key launch per virtual peer: k_unique_lds<2, ...>);
+* acks:  the ACK launch (k_unique_rows<3, ...>, all peers' rows in one pass);
+* vals:  the VAL launch (the one-pass k_lookup after the ACKs).
+Counters are KB per dispatch; FETCH_SIZE is doubled (on gfx950 it reports half the bytes of wide
+reads, MI355X_MICROARCH.md, HBM section). The median over the run's rounds is written to OUT.json,
+stamped with the bench configuration (bench.py reports it only for that configuration) as
+roofline.traffic and roofline.launches.*.traffic."""
 import csv
 import json
 import statistics
 import sys
+
+KIND_PATTERNS = {
+    "local": ("k_local_pre", "k_local_fused", "k_local_deferred", "k_commit_w"),
+    "invs": ("k_unique_lds<2,", "k_unique_rows<2,", "k_unique<2,"),
+    "acks": ("k_unique_lds<3,", "k_unique_rows<3,", "k_unique<3,"),
+    "vals": ("k_lookup<",),
+}
 
 
 def dispatches(path):
@@ -19,43 +31,56 @@ def dispatches(path):
     return rows
 
 
-def local_launches(rows):
+def per_round(rows, scale):
+    """{kind: [bytes per round]} over complete rounds"""
     ids = sorted(rows)
-    out = []
-    for k, d in enumerate(ids):
-        if "k_local_pre" in rows[d][0] and k + 3 < len(ids):
-            grp = ids[k:k + 4]
-            names = [rows[g][0] for g in grp]
-            if "k_local_fused" in names[1] and "k_local_deferred" in names[2] and "k_commit" in names[3]:
-                out.append(grp)
-            continue
-        if "k_resolve0<0," not in rows[d][0]:
-            continue
-        grp = [ids[k - 2], ids[k - 1], d, ids[k + 1]]
-        names = [rows[g][0] for g in grp]
-        if "k_lookup" in names[0] and "k_lookup" in names[1] and "k_commit" in names[3]:
-            out.append(grp)
+    starts = [k for k, d in enumerate(ids) if "k_local_pre" in rows[d][0]]
+    out = {k: [] for k in KIND_PATTERNS}
+    for s, e in zip(starts, starts[1:]):
+        acc = {k: 0.0 for k in KIND_PATTERNS}
+        seen = {k: 0 for k in KIND_PATTERNS}
+        acks_done = False
+        for d in ids[s:e]:
+            name = rows[d][0]
+            for kind, pats in KIND_PATTERNS.items():
+                if kind == "vals" and not acks_done:
+                    continue
+                if any(p in name for p in pats):
+                    acc[kind] += scale * rows[d][1]
+                    seen[kind] += 1
+                    if kind == "acks":
+                        acks_done = True
+                    break
+        if seen["local"] == 4 and all(seen[k] for k in KIND_PATTERNS):
+            for k in KIND_PATTERNS:
+                out[k].append(acc[k])
     return out
 
 
 def main():
     tag, dst = sys.argv[1], sys.argv[2]
-    f = dispatches(f"gpurun_out/{tag}/pmc/FETCH_SIZE/run_counter_collection.csv")
-    w = dispatches(f"gpurun_out/{tag}/pmc/WRITE_SIZE/run_counter_collection.csv")
-    fl = [sum(2.0 * f[g][1] for g in grp) for grp in local_launches(f)]
-    wl = [sum(w[g][1] for g in grp) for grp in local_launches(w)]
+    f = per_round(dispatches(f"gpurun_out/{tag}/pmc/FETCH_SIZE/run_counter_collection.csv"), 2.0)
+    w = per_round(dispatches(f"gpurun_out/{tag}/pmc/WRITE_SIZE/run_counter_collection.csv"), 1.0)
+    launches = {}
+    for k in KIND_PATTERNS:
+        fb, wb = statistics.median(f[k]), statistics.median(w[k])
+        launches[k] = {"kernels": list(KIND_PATTERNS[k]), "fetch_bytes": fb, "write_bytes": wb,
+                       "traffic_bytes": fb + wb}
     res = {
-        "what": "HBM bytes per local batch launch (k_local_pre, k_local_fused, k_local_deferred, k_commit; "
-                "or k_lookup x2, k_resolve0, k_commit), rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE "
-                "in separate passes of bench.py",
-        "launches": len(fl),
-        "fetch_bytes": statistics.median(fl),
-        "write_bytes": statistics.median(wl),
+        "what": "HBM bytes per batch launch of one bench round (median over rounds): local = k_local_pre + "
+                "k_local_fused + k_local_deferred + k_commit_w; invs = the round's INV launches; acks = the ACK "
+                "rows launch; vals = the VAL lookup. rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE in "
+                "separate passes of bench.py",
+        "source": f"gpurun_out/{tag}/pmc",
+        "launches_counted": min(len(f["local"]), len(w["local"])),
+        "fetch_bytes": launches["local"]["fetch_bytes"],
+        "write_bytes": launches["local"]["write_bytes"],
+        "traffic_bytes": launches["local"]["traffic_bytes"],
+        "launches": launches,
+        # the bench configuration the counters belong to (bench.py checks it)
+        "config": {"workers": int(sys.argv[3]), "keys": int(sys.argv[4]), "refill": sys.argv[5],
+                   "skew": int(sys.argv[6])},
     }
-    res["traffic_bytes"] = res["fetch_bytes"] + res["write_bytes"]
-    if len(sys.argv) > 6:   # the bench configuration the counters belong to (bench.py checks it)
-        res["config"] = {"workers": int(sys.argv[3]), "keys": int(sys.argv[4]), "refill": sys.argv[5],
-                         "skew": int(sys.argv[6])}
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res))
 

@@ -495,13 +495,17 @@ def policy_rates(a, kvs, z, L, Round, headline) -> dict:
     import torch
     out = {}
     skew0 = kvs.skew
-    warm = max(a.warmup, 10)
+    # refill_ops' retry without the skew flags has no steady state for tens of rounds (DESIGN.md section 5:
+    # slots drain into the hottest keys): it is timed over rounds RETRY_FROM..RETRY_FROM+policy_steps,
+    # not over the first rounds' descent
+    RETRY_FROM = 50
     # every policy starts from a table with no write in flight: the headline round's INVs all went
     # out (none held back by the send credits), so its last ACK batch completed every write
     for name, retry, skew, hot, what in POLICIES:
         if (retry, skew, hot) == headline:
             continue
         kvs.set_skew(skew)
+        warm = RETRY_FROM if (retry, skew, hot) == (True, 0, False) else max(a.warmup, 10)
         r = Round(kvs, a.workers, L.membership(3, 0), [1, 2], z, a.write_permille, a.rmw_permille,
                   seed=a.seed + 1, max_steps=warm + a.policy_steps + 2, retry_stalled=retry, coalesce_hot=hot)
         for _ in range(warm):
@@ -519,6 +523,7 @@ def policy_rates(a, kvs, z, L, Round, headline) -> dict:
         assert held == 0, f"policy {name}: INVs held back"   # the next policy needs a quiet table
         r.close()
         out[name] = {"value": c[0] / dt, "unit": "ops/s", "steps": a.policy_steps, "warmup": warm,
+                     "rounds_from": warm, "rounds_to": warm + a.policy_steps,
                      "ms_per_step": dt * 1e3 / a.policy_steps, "committed_per_step": c[0] / a.policy_steps,
                      "writes_completed_per_step": c[2] / a.policy_steps, "dropped_per_step": c[3] / a.policy_steps,
                      "invs_held": held, "commit_breakdown": audit,

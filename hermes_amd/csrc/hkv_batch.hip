@@ -3153,18 +3153,21 @@ __device__ void hp_partition(const HostPartCommon &p, HpLds &L, int g, int nb, u
 
 // Launches on several streams: workgroup g waits until its partition's previous launch is done
 // (order[g] == seq - 1). Every wait ends: after 1 s (wall_clock64 at 100 MHz) it gives up, raises
-// error flag bit 5 and goes on, so a lost predecessor cannot hang the GPU.
-__device__ __forceinline__ void hp_wait_turn(const HostPartCommon &c, int g, uint32_t seq)
+// error flag bit 5 and applies nothing (the host API then fails loudly), so a lost predecessor cannot
+// hang the GPU and no launch is ever applied out of its partition's order.
+__device__ __forceinline__ bool hp_wait_turn(const HostPartCommon &c, int g, uint32_t seq)
 {
-    if (!c.order || threadIdx.x != 0) return;
+    if (!c.order || threadIdx.x != 0) return true;
     const uint64_t t0 = wall_clock64();
     while (__hip_atomic_load(c.order + g, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != seq - 1u) {
         __builtin_amdgcn_s_sleep(4);
-        if (wall_clock64() - t0 > 100000000ull) {
+        if (wall_clock64() - t0 > 100000000ull) {   // 1 s: give up, apply nothing, tell the host
             if (c.error_flags) atomicOr(c.error_flags, 32u);
-            break;
+            __hip_atomic_store(c.flags + kPartG, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return false;
         }
     }
+    return true;
 }
 
 // One launch, its headers in the kernel arguments
@@ -3178,8 +3181,16 @@ __global__ __launch_bounds__(kHpThreads) void k_hpart(HostPartLaunch p)
         L.prow[0][tid] = p.part[g][tid];
         L.prow[1][tid] = p.part[g + 1][tid];
     }
-    hp_wait_turn(p.c, g, p.seq);
+    __shared__ int turn_ok;
+    if (tid == 0) turn_ok = hp_wait_turn(p.c, g, p.seq);
     __syncthreads();
+    if (!turn_ok) {   // out of order: nothing applied, the completion word set so no caller hangs
+        if (tid == 0) {
+            __hip_atomic_store(p.c.flags + g, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(p.c.order + g, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
     hp_scan(L, nb);
     __syncthreads();
     hp_partition(p.c, L, g, nb, p.seq);

@@ -76,16 +76,32 @@ struct CallerStage {
     // PCIe; the results still come back to the pinned buffer h
     uint8_t *v = nullptr;
     size_t vcap = 0;
+    bool vram_failed = false;     // its device buffer could not be allocated: pinned staging from then on
     std::vector<uint8_t> tmp;
     std::vector<uint32_t> perm;   // element i of the caller's batch sits at staged slot perm[i]
-    // a caller returns only after its launch's flags arrived, so nothing reads the staging when
-    // its thread exits: threads that come and go do not leak pinned memory
-    ~CallerStage()
-    {
-        if (h) (void)hipHostFree(h);
-        if (v) (void)hipFree(v);
-    }
+    // a caller returns only after its launch's flags arrived, so nothing reads the staging when its
+    // thread exits. hipFree / hipHostFree synchronise the device, and the serving kernel may be busy
+    // with other callers' launches for up to its lifetime limit: an exiting thread hands its buffers
+    // to a process-wide list that hkv_table_destroy frees once no serving kernel runs
+    ~CallerStage();
 };
+static std::mutex g_stage_gy_mu;
+static std::vector<std::pair<uint8_t *, bool>> g_stage_graveyard;   // (buffer, is device memory)
+CallerStage::~CallerStage()
+{
+    std::lock_guard<std::mutex> g(g_stage_gy_mu);
+    if (h) g_stage_graveyard.emplace_back(h, false);
+    if (v) g_stage_graveyard.emplace_back(v, true);
+}
+static void free_stage_graveyard()
+{
+    std::vector<std::pair<uint8_t *, bool>> gy;
+    {
+        std::lock_guard<std::mutex> g(g_stage_gy_mu);
+        gy.swap(g_stage_graveyard);
+    }
+    for (auto &b : gy) (void)(b.second ? hipFree(b.first) : hipHostFree(b.first));
+}
 static thread_local CallerStage t_stage;
 
 struct HostReq {
@@ -379,6 +395,10 @@ int hkv_table_create(const hkv_config *cfg, hkv_table **out)
         hkv_table_destroy(t);
         return rc;
     }
+    // whether callers can stage in device memory (a guarded store through the BAR) is probed once,
+    // here on the creating thread, before any caller thread exists: its signal handlers are swapped
+    // only while no other thread of the library runs
+    (void)stage_vram_usable();
     *out = t;
     return 0;
 }
@@ -414,6 +434,7 @@ int hkv_table_destroy(hkv_table *t)
         g_srv_tables.erase(std::remove(g_srv_tables.begin(), g_srv_tables.end(), t), g_srv_tables.end());
     }
     if (t->srv_ev) hipEventDestroy(t->srv_ev);
+    free_stage_graveyard();   // staging buffers of caller threads that have exited
     if (t->ring) (void)(t->ring_vram ? hipFree(t->ring) : hipHostFree(t->ring));
     if (t->ring_vram && t->srv_stop) (void)hipFree(t->srv_stop);
     if (t->srv_words) hipHostFree(t->srv_words);
@@ -614,6 +635,10 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
         bl.epoch = t->pre.epoch;
         bl.pre_done = t->pre.done;
         bl.reset_defer = t->pre.scratch_gen != t->scratch_gen;
+    } else if (force_engine) {
+        // a VAL launch between a prepass and the rest of its launch: the one-pass VAL lookup uses no
+        // round tag, so it takes the current epoch and can never wrap it under the pending prepass
+        bl.epoch = t->epoch;
     } else {
         if (++t->epoch > batch_max_epoch()) {  // round tags would wrap: start the F and T words over
             HIP_TRY(hipMemsetAsync(t->d_fw, 0xFF, 8 * batch_fw_words(t->cfg.log_cap), s));
@@ -1100,10 +1125,11 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
         t->n_pstreams = n_streams;
     }
     if (!t->pflags) {
-        if (hipHostMalloc((void **)&t->pflags, 4 * kPartG, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        // kPartG completion words, then the order-timeout word hp_wait_turn raises (HKV_PART_STREAMS > 1)
+        if (hipHostMalloc((void **)&t->pflags, 4 * (kPartG + 1), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
             hipHostGetDevicePointer((void **)&t->pflags_d, t->pflags, 0) != hipSuccess)
             die("flag alloc");
-        for (int g = 0; g < kPartG; ++g) __atomic_store_n(t->pflags + g, 0u, __ATOMIC_RELEASE);
+        for (int g = 0; g <= kPartG; ++g) __atomic_store_n(t->pflags + g, 0u, __ATOMIC_RELEASE);
     }
     if (serve && !t->ring) {
         if (hipHostMalloc((void **)&t->srv_words, 4 * 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -1111,10 +1137,18 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
             die("ring alloc");
         for (int k = 0; k < 64; ++k) __atomic_store_n(t->srv_words + k, 0u, __ATOMIC_RELEASE);
         t->ring_vram = stage_vram_usable();
-        if (t->ring_vram) {
+        if (t->ring_vram) {   // under VRAM pressure the ring goes to pinned memory instead
             if (hipExtMallocWithFlags((void **)&t->ring, sizeof(HostRingSlot) * kRingN, hipDeviceMallocFinegrained) != hipSuccess ||
-                hipExtMallocWithFlags((void **)&t->srv_stop, 64, hipDeviceMallocFinegrained) != hipSuccess)
-                die("ring alloc");
+                hipExtMallocWithFlags((void **)&t->srv_stop, 64, hipDeviceMallocFinegrained) != hipSuccess) {
+                (void)hipGetLastError();
+                if (t->ring) (void)hipFree(t->ring);
+                t->ring = nullptr;
+                t->srv_stop = nullptr;
+                t->ring_vram = false;
+                TRACE("serving-kernel ring VRAM alloc failed: ring in pinned memory");
+            }
+        }
+        if (t->ring_vram) {
             t->ring_d = t->ring;
             t->srv_stop_d = t->srv_stop;
         } else {
@@ -1272,19 +1306,34 @@ static bool host_stage_part(const hkv_table *t, HostReq &r)
         st.h = st.d = nullptr;
         const size_t cap = std::max(total, (size_t)1 << 20);
         if (hipHostMalloc((void **)&st.h, cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-            hipHostGetDevicePointer((void **)&st.d, st.h, 0) != hipSuccess)
-            die("caller staging alloc");
+            hipHostGetDevicePointer((void **)&st.d, st.h, 0) != hipSuccess) {
+            if (st.h) (void)hipHostFree(st.h);
+            st.h = st.d = nullptr;
+            st.cap = 0;
+            return false;   // the batch takes the staged-set path instead
+        }
         st.cap = cap;
     }
-    const bool vram = stage_vram_usable();
+    // device-memory staging when the BAR is writable and this caller's buffer could be allocated: under
+    // VRAM pressure (torch in the same process) the caller stages in its pinned buffer instead
+    bool vram = stage_vram_usable() && !st.vram_failed;
     // ACK batches in device memory: each read_write_ops slot's opcode beside the elements (hp_rw_ahead)
-    const size_t obytes = vram && rw_bytes ? align16((size_t)t->cfg.rw_len) : 0;
+    size_t obytes = vram && rw_bytes ? align16((size_t)t->cfg.rw_len) : 0;
     if (vram && ebytes + pbytes + obytes > st.vcap) {
         if (st.v) (void)hipFree(st.v);
         st.v = nullptr;
+        st.vcap = 0;
         const size_t cap = std::max(ebytes + pbytes + obytes, (size_t)1 << 20);
-        if (hipExtMallocWithFlags((void **)&st.v, cap, hipDeviceMallocFinegrained) != hipSuccess) die("caller VRAM staging alloc");
-        st.vcap = cap;
+        if (hipExtMallocWithFlags((void **)&st.v, cap, hipDeviceMallocFinegrained) != hipSuccess) {
+            (void)hipGetLastError();
+            st.v = nullptr;
+            st.vram_failed = true;
+            vram = false;
+            obytes = 0;
+            TRACE("caller VRAM staging alloc failed: pinned staging for this caller");
+        } else {
+            st.vcap = cap;
+        }
     }
     if ((int)st.perm.size() < r.n) st.perm.resize(r.n);
     uint16_t cur[kPartG];
@@ -1541,6 +1590,10 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
         die("sync");
     }
     const long t2 = g_host_timing ? now_ns() : 0;
+    // HKV_PART_STREAMS > 1: a workgroup that waited over 1 s for its partition's previous launch gave
+    // up without applying its elements (error bit 5): the table no longer follows any caller order
+    if (mode == kModePart && t->n_pstreams && __atomic_load_n(t->pflags + kPartG, __ATOMIC_ACQUIRE))
+        die("partitioned launch gave up waiting for its partition's previous launch (HKV_PART_STREAMS, error bit 5)");
     if (mode == kModePart) {
         // results from this thread's staging, back in element order; node_suspected is
         // hermes_skip_inv's, a function of the elements alone: the last membership-change INV's

@@ -256,7 +256,10 @@ void *hkv_device_index(hkv_table *t);
  * bit 1: the ACK direct path completed a write from an unexpected state;
  * bit 2: a local launch's mutating element had not offered itself in its prepass;
  * bit 3: d_opcode_in missed a PUT, or d_put_keys / the entry states of d_state_out disagree with the ops;
- * bit 4: an HKV_BATCH_UNIQUE launch held a key twice (checked with HKV_CHECK_UNIQUE=1) */
+ * bit 4: an HKV_BATCH_UNIQUE launch held a key twice (checked with HKV_CHECK_UNIQUE=1), or an
+ *        HKV_BATCH_ROWS position's rows disagree on the key;
+ * bit 5: (HKV_PART_STREAMS > 1 only) a partitioned host launch waited over 1 s for its partition's
+ *        previous launch and applied nothing; hermes_batch_ops_to_KVS then aborts the process */
 int  hkv_take_error_flags(hkv_table *t, uint32_t *out);
 void *hkv_device_log(hkv_table *t);
 

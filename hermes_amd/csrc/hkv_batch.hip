@@ -113,6 +113,11 @@ struct BatchArgs {
     int32_t cancel;              // k_local_pre undoes its tags (HKV_BATCH_PREPASS_CANCEL)
     uint8_t *ack_out;            // INV launches: each element's ACK (hkv_batch_desc.d_ack_out), or NULL
     uint32_t ack_out_size;
+    uint4 *ktab;                 // local direct path: the launch's PUT-key table (see kt_insert), or NULL
+    uint32_t ktab_bits;          // log2 of its slots
+    uint32_t ktag;               // the launch's 16-bit tag in the table's key words (1..65535)
+    uint32_t kepoch;             // the launch's epoch in the table's index words
+    unsigned long long *pchk;    // [2][kChkStripes] PUT-mirror checksums (prepass, fused pass), or NULL
 };
 
 // Rounds after round 0 per batch type: how often a hot key usually mutates in one launch beyond
@@ -285,6 +290,110 @@ __device__ __forceinline__ void offer(unsigned long long *f, uint32_t rtag, uint
 {
     const unsigned long long v = ((unsigned long long)(~rtag) << 32) | i;
     if (v < __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(f, v);
+}
+
+// ---- the launch's PUT-key table (local direct path, HKV_PRE_TABLE). k_local_pre puts every key that
+// has a PUT in the launch into an open-addressed table of 2^B 16-byte slots, with the key's first PUT,
+// instead of looking the key up in the index and offering its F word (two random lines, an atomic
+// and a seqlock-byte store into a third); k_local_fused reads the key's slot beside its bucket and
+// takes F from it when the key's S_0 lets a PUT mutate (for a key that is not INVALID, F is its first
+// PUT or nothing, see the direct path's section comment). A slot is
+//   key word:   rest << B | d << 16 | tag,   h = kt_mix(key) (a bijection), home = h >> (64 - B),
+//               rest = the low 64 - B bits of h, d = the slot's distance from home (< kKtMaxD), tag =
+//               the launch's 16-bit tag: (home, rest) is h, so the word names its key exactly;
+//   index word: epoch << 32 | ~i, i the key's first PUT (atomicMax: the launch's words outrank every
+//               earlier launch's, and within it the smallest i wins).
+// A word with another tag is an empty slot, so nothing is cleared between launches; the runtime
+// zeroes the table when the tag wraps (every 65535 launches). Slots are claimed by atomicCAS and
+// never released within a launch, so every inserter of a key reaches the same slot. A key that finds
+// kKtMaxD slots taken takes the lookup-and-tag path instead (k_local_fused reads both).
+constexpr uint32_t kKtMaxD = 32;
+constexpr int kChkStripes = 256;
+
+__device__ __forceinline__ uint64_t kt_mix(uint64_t k)
+{
+    k ^= k >> 33;
+    k *= 0xFF51AFD7ED558CCDull;
+    k ^= k >> 29;
+    k *= 0xC4CEB9FE1A85EC53ull;
+    k ^= k >> 32;
+    return k;
+}
+__device__ __forceinline__ uint32_t kt_home(const BatchArgs &a, uint64_t key)
+{
+    return (uint32_t)(kt_mix(key) >> (64 - a.ktab_bits));
+}
+__device__ __forceinline__ unsigned long long kt_want(const BatchArgs &a, uint64_t key, uint32_t d)
+{
+    const uint64_t h = kt_mix(key);
+    const uint64_t rest = h & ((1ull << (64 - a.ktab_bits)) - 1ull);
+    return (rest << a.ktab_bits) | ((unsigned long long)d << 16) | a.ktag;
+}
+__device__ __forceinline__ unsigned long long kt_lo(const uint4 &v) { return (unsigned long long)v.x | ((unsigned long long)v.y << 32); }
+__device__ __forceinline__ unsigned long long kt_hi(const uint4 &v) { return (unsigned long long)v.z | ((unsigned long long)v.w << 32); }
+
+// key -> its slot, with i as a candidate first PUT; false when kKtMaxD slots from home are taken by
+// other keys. The plain loads may be stale (another XCD's claim): a slot's key word changes at most
+// once per launch (from another tag to its key), so a stale one can only read as empty, and the CAS
+// then returns the real word; an index word only grows, so a stale one filters nothing wrongly.
+__device__ __forceinline__ bool kt_insert(const BatchArgs &a, uint64_t key, uint32_t i)
+{
+    const uint32_t mask = (1u << a.ktab_bits) - 1u, home = kt_home(a, key);
+    const unsigned long long iv = ((unsigned long long)a.kepoch << 32) | (0xFFFFFFFFu - i);
+    for (uint32_t d = 0; d < kKtMaxD; ++d) {
+        uint4 *slot = a.ktab + ((home + d) & mask);
+        unsigned long long *kw = reinterpret_cast<unsigned long long *>(slot);
+        const unsigned long long want = kt_want(a, key, d);
+        const uint4 v = *slot;
+        unsigned long long cur = kt_lo(v), idx = kt_hi(v);
+        for (;;) {
+            if ((uint32_t)(cur & 0xFFFFu) != a.ktag) {   // empty in this launch: claim it
+                const unsigned long long old = atomicCAS(kw, cur, want);
+                if (old == cur) {
+                    atomicMax(kw + 1, iv);
+                    return true;
+                }
+                cur = old;
+                idx = 0;
+                continue;
+            }
+            if (cur == want) {
+                if (iv > idx) atomicMax(kw + 1, iv);
+                return true;
+            }
+            break;   // another key's slot
+        }
+    }
+    return false;
+}
+
+// The key's first PUT from its table slot (v: the home slot, loaded beside the bucket), kNone when
+// the key has no PUT in the table (or took the lookup-and-tag path)
+__device__ __forceinline__ uint32_t kt_find(const BatchArgs &a, uint64_t key, uint4 v)
+{
+    const uint32_t mask = (1u << a.ktab_bits) - 1u, home = kt_home(a, key);
+    for (uint32_t d = 0; d < kKtMaxD; ++d) {
+        if (d) v = a.ktab[(home + d) & mask];
+        const unsigned long long cur = kt_lo(v);
+        if ((uint32_t)(cur & 0xFFFFu) != a.ktag) return kNone;
+        if (cur == kt_want(a, key, d)) {
+            const unsigned long long idx = kt_hi(v);
+            return (uint32_t)(idx >> 32) == a.kepoch ? 0xFFFFFFFFu - (uint32_t)idx : kNone;
+        }
+    }
+    return kNone;
+}
+
+// checksum term of a PUT (key, element): the prepass sums it over the PUTs the caller's mirror names,
+// the fused pass over the PUTs it sees; k_commit_w compares the sums (error bit 3)
+__device__ __forceinline__ unsigned long long chk_term(uint64_t key, uint32_t i)
+{
+    return kt_mix(key ^ ((uint64_t)i * 0x9E3779B97F4A7C15ull)) | 1ull;
+}
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v)
+{
+    for (int o = 32; o > 0; o >>= 1) v += (unsigned long long)__shfl_xor((long long)v, o, 64);
+    return v;
 }
 
 // Wave-aggregated atomicAdd(&arr[j], 1): one atomic per distinct j in the wave; each active lane
@@ -1335,18 +1444,25 @@ constexpr int kPrePair = 4;
 #else
 #define HKV_PRE_ATTR
 #endif
-template <int HEAD = kPreHead, bool H = false>
+// T (the PUT-key table, HKV_PRE_TABLE): each distinct key goes into the launch's key table (kt_insert)
+// instead of being looked up, offered and tagged; only keys the table cannot place take that path.
+// With the caller's PUT-key mirror the block also sums chk_term over the PUTs it read from it.
+template <int HEAD = kPreHead, bool H = false, bool T = false>
 __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 {
     __shared__ uint64_t hk[kPreHash], gk[kPreHash];  // the block's PUT keys, the head's
     __shared__ uint32_t hv[kPreHash];
     __shared__ uint32_t dl[kPreElems];               // distinct keys: slots of hk, or ~index (no slot)
+    __shared__ uint8_t lk[T ? kPreElems : 1];        // T: 1 = the key takes the lookup path
     __shared__ uint32_t nd;
     const int tid = threadIdx.x, q = tid & 3, gbase = (tid & 63) & ~3;
+    const bool table = T && !a.cancel;   // a cancel undoes tags: every key takes the lookup path
     if (tid == 0) {
         nd = 0;
         if (blockIdx.x == 0) a.ctr[kCtrDefer] = 0;
     }
+    if (T && a.cancel && a.pchk && blockIdx.x == 0)   // no fused pass follows: the sums start over
+        for (int j = tid; j < 2 * kChkStripes; j += 256) a.pchk[j] = 0;
     for (int j = tid; j < kPreHash; j += 256) {
         hk[j] = ~0ull;
         gk[j] = ~0ull;
@@ -1441,6 +1557,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
         return;
     }
     __syncthreads();
+    unsigned long long chk = 0;
 #pragma unroll
     for (int k = 0; k < kAllK; ++k) {
         const bool own = k < kOwnK;
@@ -1450,6 +1567,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
         bool created;
         uint32_t sl;
         if (own) {
+            if (T && a.pkeys) chk += chk_term(key, i);
             const bool in_table = pre_insert(hk, hv, key, i, created, sl);
             if (!in_table || created) {  // a key's first arrival lists it (no slot: it offers for itself)
                 dl[atomicAdd(&nd, 1u)] = in_table ? sl : ~i;
@@ -1458,10 +1576,40 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
             pre_insert_key(gk, key);
         }
     }
+    if (T && a.pkeys && !a.cancel) {   // the block's sum of the mirror's PUTs, one atomic per wave
+        chk = wave_sum64(chk);
+        if ((tid & 63) == 0 && chk) atomicAdd(a.pchk + (blockIdx.x % kChkStripes), chk);
+    }
     __syncthreads();
     const Ctx c = make_ctx(a);
     const uint64_t hput[2] = {0, (uint64_t)kOpPut};
     const uint32_t cnt = HKV_DBG_ON(a, 2) ? 0 : nd;
+    if (table) {
+        // one lane per distinct key: the head's keys are dropped (an earlier block holds their first
+        // PUT), the others go into the key table; those it cannot place are looked up below
+        for (uint32_t j = tid; j < cnt; j += 256) {
+            const uint32_t d = dl[j];
+            const uint32_t idx = d < (uint32_t)kPreHash ? hv[d] : ~d;
+            const uint64_t key = d < (uint32_t)kPreHash ? hk[d] : elem_key(a, (int64_t)idx);
+            bool lookup = false;
+            bool head = false;
+            if (head_end > 0 && key != ~0ull) {
+                uint32_t sl = pre_slot(key);
+                for (int n = 0; n < kPreHash; ++n) {
+                    const uint64_t g = gk[sl];
+                    if (g == ~0ull) break;
+                    if (g == key) {
+                        head = true;
+                        break;
+                    }
+                    sl = (sl + 1) & (kPreHash - 1);
+                }
+            }
+            if (!head) lookup = !kt_insert(a, key, idx);
+            lk[j] = lookup ? 1 : 0;
+        }
+        __syncthreads();
+    }
     for (uint32_t base = 0; base < cnt; base += 64 * kPrePair) {
         uint64_t key[kPrePair];
         bool probe[kPrePair], ok[kPrePair];
@@ -1471,7 +1619,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 #pragma unroll
         for (int k = 0; k < kPrePair; ++k) {
             const uint32_t j = base + k * 64 + (tid >> 2);
-            probe[k] = j < cnt;
+            probe[k] = j < cnt && (!table || lk[j]);
             const uint32_t d = probe[k] ? dl[j] : 0u;
             idx[k] = !probe[k] ? kNone : d < (uint32_t)kPreHash ? hv[d] : ~d;
             key[k] = !probe[k] ? 0 : d < (uint32_t)kPreHash ? hk[d] : elem_key(a, (int64_t)idx[k]);
@@ -1516,13 +1664,18 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 // nothing shared beyond it. The lookup runs four lanes per element (each lane holds 16 B of the op
 // and of the log line); the wave-private LDS copies of op and entry are then resolved one element
 // per lane, so the exec code's branches are paid once per 32 elements; the ops go back whole.
-template <int P, bool H = false>
+// T (HKV_PRE_TABLE): each key's first PUT comes from the launch's key table (its home slot loaded
+// beside the bucket); the tag-and-F-word path remains for the keys the table could not place. With
+// the caller's PUT-key mirror, the mirror is checked by a checksum of the PUTs (k_commit_w compares)
+// instead of element by element.
+template <int P, bool H = false, bool T = false>
 __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
 {
     constexpr int E = 16 * P;   // elements per wave: P per lane group
     __shared__ uint4 sops[E * 4];   // 64 B per op (56 used)
     __shared__ uint4 sln[E * 4];
     __shared__ unsigned long long sfw[E];
+    __shared__ uint32_t sft[T ? E : 1];   // T: the key's first PUT from the key table (kNone: none)
     __shared__ uint32_t sent[E];     // entry id of a hit, kNone otherwise
     __shared__ uint8_t sprb[E];      // probed (not skipped)
     __shared__ uint32_t sdef[E];
@@ -1555,7 +1708,7 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
                 op[k].y = (uint32_t)(t >> 32);
             }
             if (patch_valid(p.b)) op[k] = patch_chunk(op[k], q, p.a, p.b);
-            if (a.pkeys && q == 0) {   // the mirrors k_local_pre worked from, checked below
+            if (!T && a.pkeys && q == 0) {   // the mirrors k_local_pre worked from, checked below
                 spk[te[k]] = a.pkeys[i];
                 sps[te[k]] = a.state_out[i];
             }
@@ -1571,6 +1724,11 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         if (live[k])
             probe[k] = in_count(a, (uint32_t)(i0 + te[k])) && !skip_elem_os(kLocal, (uint8_t)h0, (uint8_t)(h0 >> 8));
     }
+    // T: the key's home slot in the key table, in flight beside the bucket (no dependence between them)
+    uint4 kt[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+        kt[k] = T && probe[k] && q == 0 ? a.ktab[kt_home(a, key[k])] : make_uint4(0u, 0u, 0u, 0u);
     if (H) {   // located entries (hkv_batch_desc.d_phys)
         int64_t gi[P];
 #pragma unroll
@@ -1587,6 +1745,7 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         const bool hit = ok[k] && ek == key[k];
         const bool tagged = hit && m_state(m) != kInvalid && (uint8_t)(m.w5 >> 16) == a.ltag;
         const unsigned long long f = tagged && q == 0 ? a.fw[fw_index(a, phys[k])] : ~0ull;
+        if (T && q == 0) sft[te[k]] = hit && m_state(m) != kInvalid ? kt_find(a, key[k], kt[k]) : kNone;
         if (hit) sln[te[k] * 4 + q] = ln[k];
         if (q == 0) {
             sfw[te[k]] = f;
@@ -1595,15 +1754,17 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         }
     }
     __syncthreads();
+    unsigned long long chk = 0;
     if (tid < E && i0 + tid < a.n) {
         const int64_t i = i0 + tid;
         uint8_t *x = reinterpret_cast<uint8_t *>(&sops[tid * 4]);
         uint8_t *ent = reinterpret_cast<uint8_t *>(&sln[tid * 4]);
         const uint32_t e = sent[tid];
         uint8_t st = kStDone;
+        if (T && a.pkeys && sprb[tid] && x[8] == kOpPut) chk = chk_term(ld64(x), (uint32_t)i);
         // the mirrors k_local_pre worked from must describe this element: the PUT-key word, and for
         // a PUT the state the skip rule was applied to
-        if (a.pkeys && a.error_flags &&
+        if (!T && a.pkeys && a.error_flags &&
             (spk[tid] != (x[8] == kOpPut ? ld64(x) : ~0ull) || (x[8] == kOpPut && sps[tid] != x[9])))
             atomicOr(a.error_flags, 8u);
         if (e != kNone) {
@@ -1622,7 +1783,11 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
                 st = kStDefer;
                 sdef[atomicAdd(&ndef, 1u)] = (uint32_t)i;
             } else {
-                const uint32_t f = first_cand(sfw[tid], a.rtag0);
+                uint32_t f = first_cand(sfw[tid], a.rtag0);
+                if (T && sft[tid] < f) {   // the key's first PUT, F when a PUT mutates S_0
+                    const uint64_t hput[2] = {0, (uint64_t)kOpPut};
+                    if (would_mutate(kLocal, reinterpret_cast<const uint8_t *>(hput), m, c)) f = sft[tid];
+                }
                 // a mutating element must have offered itself in k_local_pre
                 if (wm && (f == kNone || f > (uint32_t)i) && a.error_flags) atomicOr(a.error_flags, 4u);
                 if ((uint32_t)i == f) {
@@ -1639,11 +1804,17 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         } else if (sprb[tid]) {
             x[9] = kMiss;
         }
-        // k_local_pre read only the PUTs the caller's opcode mirror names
-        if (a.opc && sprb[tid] && x[8] == kOpPut && a.opc[i] != kOpPut && a.error_flags) atomicOr(a.error_flags, 8u);
+        // k_local_pre read only the PUTs the caller's opcode mirror names (with the PUT-key mirror and the
+        // key table: the checksum below)
+        if (!(T && a.pkeys) && a.opc && sprb[tid] && x[8] == kOpPut && a.opc[i] != kOpPut && a.error_flags)
+            atomicOr(a.error_flags, 8u);
         a.ent[i] = e;
         a.st[i] = st;
         if (st != kStDefer) note_state(a, i, x);
+    }
+    if (T && a.pkeys) {   // the wave's sum of the PUTs it saw (k_commit_w compares it with the prepass's)
+        chk = wave_sum64(chk);
+        if (tid == 0 && chk) atomicAdd(a.pchk + kChkStripes + (blockIdx.x % kChkStripes), chk);
     }
     __syncthreads();
     // the waiting elements (keys INVALID at S_0: rare), appended once per block
@@ -2283,6 +2454,20 @@ __global__ __launch_bounds__(256) void k_commit_w(BatchArgs a)
     __shared__ uint32_t lst[4][kCwElems];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t e0 = ((int64_t)blockIdx.x * 4 + w) * kCwElems + 16 * lane;
+    if (a.pchk && blockIdx.x == 0 && w == 0) {
+        // the PUT-key mirror's checksum (k_local_pre) against the PUTs k_local_fused saw: a mirror that
+        // named a PUT wrongly, or missed one, raises error bit 3; the sums start over for the next launch
+        unsigned long long sp = 0, sf = 0;
+        for (int j = lane; j < kChkStripes; j += 64) {
+            sp += a.pchk[j];
+            sf += a.pchk[kChkStripes + j];
+            a.pchk[j] = 0;
+            a.pchk[kChkStripes + j] = 0;
+        }
+        sp = wave_sum64(sp);
+        sf = wave_sum64(sf);
+        if (lane == 0 && sp != sf && a.error_flags) atomicOr(a.error_flags, 8u);
+    }
     uint32_t m = 0;
     if (e0 + 16 <= a.n) {   // st is 256-byte aligned and e0 a multiple of 16
         const uint4 s4 = *reinterpret_cast<const uint4 *>(a.st + e0);
@@ -3405,7 +3590,8 @@ static void launch_local_pre(const BatchArgs &a, int64_t n, hipStream_t s)
 {
     static const int head = getenv("HKV_PRE_HEAD") ? atoi(getenv("HKV_PRE_HEAD")) : kPreHead;
     const dim3 grid((unsigned)((n + kPreElems - 1) / kPreElems));
-    if (a.phys_hint) hipLaunchKernelGGL((k_local_pre<kPreHead, true>), grid, dim3(256), 0, s, a);
+    if (a.ktab) hipLaunchKernelGGL((k_local_pre<kPreHead, false, true>), grid, dim3(256), 0, s, a);
+    else if (a.phys_hint) hipLaunchKernelGGL((k_local_pre<kPreHead, true>), grid, dim3(256), 0, s, a);
     else if (head == 256) hipLaunchKernelGGL(k_local_pre<256>, grid, dim3(256), 0, s, a);
     else if (head == 512) hipLaunchKernelGGL(k_local_pre<512>, grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(k_local_pre<kPreHead>, grid, dim3(256), 0, s, a);
@@ -3427,6 +3613,11 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.cancel = bl.stage == 3;
     a.ack_out = bl.type == kInvs ? bl.ack_out : nullptr;
     a.ack_out_size = bl.ack_out_size;
+    a.ktab = nullptr;
+    a.ktab_bits = bl.ktab_bits;
+    a.ktag = 1u + (bl.epoch - 1u) % 65535u;
+    a.kepoch = bl.epoch;
+    a.pchk = nullptr;
     a.n_rows = bl.n_rows;
     a.skip_row = bl.skip_row;
     a.row_stride = bl.row_stride;
@@ -3507,10 +3698,19 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
                               bl.g.st_value == 31 && bl.g.entry_size == 64 && !bl.offsets;
     // HKV_PATCH_APPLY=1: patches always written into the ops first (experiments)
     static const bool patch_apply_env = getenv("HKV_PATCH_APPLY") && atoi(getenv("HKV_PATCH_APPLY")) != 0;
+    // HKV_PRE_TABLE=1: the prepass puts the launch's PUT keys into the key table instead of looking
+    // them up (kt_insert); with the PUT-key mirror the mirror is checked by checksum
+    static const bool table_env = getenv("HKV_PRE_TABLE") && atoi(getenv("HKV_PRE_TABLE")) != 0;
+    auto use_table = [&]() {
+        if (!(table_env && local_direct && bl.ktab && !a.phys_hint)) return;
+        a.ktab = reinterpret_cast<uint4 *>(bl.ktab);
+        if (a.pkeys) a.pchk = bl.pchk;
+    };
     if (bl.stage == 3) {   // HKV_BATCH_PREPASS_CANCEL: the prepass's lookups again, clearing its tags
         if (bl.pre_done) {
             if (bl.patch) a.patch = bl.patch;
             if (bl.put_keys && a.state_out) a.pkeys = bl.put_keys;
+            use_table();
             launch_local_pre(a, n, s);
         }
         return hipGetLastError() == hipSuccess ? 0 : -3;
@@ -3519,6 +3719,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         if (local_direct && !small && !patch_apply_env) {
             if (bl.patch) a.patch = bl.patch;
             if (local_direct && bl.put_keys && a.state_out) a.pkeys = bl.put_keys;
+            use_table();
             launch_local_pre(a, n, s);
             bl.pre_done = 1;
         }
@@ -3530,6 +3731,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         a.patch = bl.patch;
     }
     if (local_direct && !small && bl.put_keys && a.state_out) a.pkeys = bl.put_keys;
+    if (!small) use_table();
     if (small) {
         if (launch_small(a, s)) return -3;
         return 0;                              // node_suspected written by the kernel
@@ -3541,7 +3743,9 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         }
         // HKV_LF_PAIR: elements per lane group in k_local_fused (2: 32 per wave; 4: 64, more loads in flight)
         static const int lfp_env = getenv("HKV_LF_PAIR") ? atoi(getenv("HKV_LF_PAIR")) : 2;
-        if (a.phys_hint)
+        if (a.ktab)
+            hipLaunchKernelGGL((k_local_fused<2, false, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
+        else if (a.phys_hint)
             hipLaunchKernelGGL((k_local_fused<2, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
         else if (lfp_env == 4)
             hipLaunchKernelGGL(k_local_fused<4>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, a);

@@ -41,8 +41,8 @@ def main():
     torch.cuda.synchronize()
     ops = r.ops.view(-1, r.op)
     n = ops.shape[0]
-    inprog = torch.tensor([int(x) for x in (L.Resp.IN_PROGRESS_PUT, L.Resp.IN_PROGRESS_REPLAY,
-                                            L.Resp.IN_PROGRESS_GET, L.Resp.IN_PROGRESS_RMW)], device=ops.device)
+    inprog = torch.tensor([int(x) for x in (L.Bucket.IN_PROGRESS_PUT, L.Bucket.IN_PROGRESS_REPLAY,
+                                            L.Bucket.IN_PROGRESS_GET, L.Bucket.IN_PROGRESS_RMW)], device=ops.device)
     stats = []
     local = r.local_batch
 

@@ -575,6 +575,40 @@ __device__ __forceinline__ void lookup_pair(const BatchArgs &a, const uint64_t *
         ln[k] = ok[k] ? reinterpret_cast<const uint4 *>(a.log + phys[k])[q] : make_uint4(0u, 0u, 0u, 0u);
 }
 
+// lookup_pair that also loads each hit's F word beside its log line (lane q == 0; ~0 for a miss), so a
+// key's F costs no dependent load after the line (k_local_fused, HKV_LF_FSPEC)
+template <int P>
+__device__ __forceinline__ void lookup_pair_f(const BatchArgs &a, const uint64_t *key, const bool *probe, int q,
+                                              int gbase, bool *ok, uint64_t *phys, uint4 *ln, unsigned long long *fwv)
+{
+    uint4 v[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+        v[k] = probe[k] ? reinterpret_cast<const uint4 *>(a.index + ((key[k] & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u)[q]
+                        : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const uint64_t s0 = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
+        const uint64_t s1 = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
+        const uint32_t tag = (uint32_t)(key[k] >> 48);
+        const bool mt0 = probe[k] && (s0 & 1u) && ((uint32_t)(s0 >> 1) & 0x7FFFFFu) == tag;
+        const bool mt1 = probe[k] && (s1 & 1u) && ((uint32_t)(s1 >> 1) & 0x7FFFFFu) == tag;
+        const uint32_t g0 = (uint32_t)(__ballot(mt0) >> gbase) & 0xFu;
+        const uint32_t g1 = (uint32_t)(__ballot(mt1) >> gbase) & 0xFu;
+        uint32_t o = 0;
+#pragma unroll
+        for (int l = 0; l < 4; ++l) o |= ((g0 >> l) & 1u) << (2 * l) | ((g1 >> l) & 1u) << (2 * l + 1);
+        const int first = o ? __ffs(o) - 1 : 0;
+        const uint64_t off = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
+        ok[k] = probe[k] && o && a.g.log_head - off < a.g.log_cap;
+        phys[k] = off & a.g.log_mask;
+    }
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        ln[k] = ok[k] ? reinterpret_cast<const uint4 *>(a.log + phys[k])[q] : make_uint4(0u, 0u, 0u, 0u);
+        fwv[k] = ok[k] && q == 0 ? a.fw[fw_index(a, phys[k])] : ~0ull;
+    }
+}
 
 // lookup_pair with located entries (hkv_batch_desc.d_phys): an element with an offset reads its entry
 // line straight away; one without, or whose entry does not hold its key, takes lookup_pair's path. gi:
@@ -1447,7 +1481,9 @@ constexpr int kPrePair = 4;
 // T (the PUT-key table, HKV_PRE_TABLE): each distinct key goes into the launch's key table (kt_insert)
 // instead of being looked up, offered and tagged; only keys the table cannot place take that path.
 // With the caller's PUT-key mirror the block also sums chk_term over the PUTs it read from it.
-template <int HEAD = kPreHead, bool H = false, bool T = false>
+// FF (HKV_PRE_FFILTER): the key's F word is loaded beside its log line, and an offer that an earlier
+// element's offer already beats (it landed first) is dropped with its tag store (the earlier one tags)
+template <int HEAD = kPreHead, bool H = false, bool T = false, bool FF = false>
 __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 {
     __shared__ uint64_t hk[kPreHash], gk[kPreHash];  // the block's PUT keys, the head's
@@ -1616,6 +1652,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
         uint32_t idx[kPrePair];
         uint64_t phys[kPrePair];
         uint4 ln[kPrePair];
+        unsigned long long fwv[kPrePair];
 #pragma unroll
         for (int k = 0; k < kPrePair; ++k) {
             const uint32_t j = base + k * 64 + (tid >> 2);
@@ -1642,7 +1679,8 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
             for (int k = 0; k < kPrePair; ++k) gi[k] = probe[k] ? (int64_t)idx[k] : 0;
             lookup_hinted<kPrePair>(a, gi, key, probe, q, gbase, ok, phys, ln);
         } else {
-            lookup_pair<kPrePair>(a, key, probe, q, gbase, ok, phys, ln);
+            if (FF) lookup_pair_f<kPrePair>(a, key, probe, q, gbase, ok, phys, ln, fwv);
+            else lookup_pair<kPrePair>(a, key, probe, q, gbase, ok, phys, ln);
         }
 #pragma unroll
         for (int k = 0; k < kPrePair; ++k) {
@@ -1654,7 +1692,9 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
                 continue;
             }
             if (!would_mutate(kLocal, reinterpret_cast<const uint8_t *>(hput), m0, c) || HKV_DBG_ON(a, 1)) continue;
-            atomicMin(a.fw + fw_index(a, phys[k]), ((unsigned long long)(~a.rtag0) << 32) | idx[k]);
+            const unsigned long long ov = ((unsigned long long)(~a.rtag0) << 32) | idx[k];
+            if (FF && fwv[k] <= ov) continue;   // a smaller offer of this launch is in (and tags the entry)
+            atomicMin(a.fw + fw_index(a, phys[k]), ov);
             if ((uint8_t)(m0.w5 >> 16) != a.ltag && !HKV_DBG_ON(a, 32)) a.log[phys[k] + kEntryMetaOff + 4] = a.ltag;
         }
     }
@@ -1668,7 +1708,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 // beside the bucket); the tag-and-F-word path remains for the keys the table could not place. With
 // the caller's PUT-key mirror, the mirror is checked by a checksum of the PUTs (k_commit_w compares)
 // instead of element by element.
-template <int P, bool H = false, bool T = false>
+template <int P, bool H = false, bool T = false, bool FS = false>
 __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
 {
     constexpr int E = 16 * P;   // elements per wave: P per lane group
@@ -1729,11 +1769,14 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
 #pragma unroll
     for (int k = 0; k < P; ++k)
         kt[k] = T && probe[k] && q == 0 ? a.ktab[kt_home(a, key[k])] : make_uint4(0u, 0u, 0u, 0u);
+    unsigned long long fwv[P];   // FS: every hit's F word, loaded beside its log line
     if (H) {   // located entries (hkv_batch_desc.d_phys)
         int64_t gi[P];
 #pragma unroll
         for (int k = 0; k < P; ++k) gi[k] = i0 + te[k];
         lookup_hinted<P>(a, gi, key, probe, q, gbase, ok, phys, ln);
+    } else if (FS) {
+        lookup_pair_f<P>(a, key, probe, q, gbase, ok, phys, ln, fwv);
     } else {
         lookup_pair<P>(a, key, probe, q, gbase, ok, phys, ln);
     }
@@ -1744,7 +1787,7 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         const uint64_t ek = line_key_meta(ln[k], m);
         const bool hit = ok[k] && ek == key[k];
         const bool tagged = hit && m_state(m) != kInvalid && (uint8_t)(m.w5 >> 16) == a.ltag;
-        const unsigned long long f = tagged && q == 0 ? a.fw[fw_index(a, phys[k])] : ~0ull;
+        const unsigned long long f = !(tagged && q == 0) ? ~0ull : FS ? fwv[k] : a.fw[fw_index(a, phys[k])];
         if (T && q == 0) sft[te[k]] = hit && m_state(m) != kInvalid ? kt_find(a, key[k], kt[k]) : kNone;
         if (hit) sln[te[k] * 4 + q] = ln[k];
         if (q == 0) {
@@ -3590,7 +3633,10 @@ static void launch_local_pre(const BatchArgs &a, int64_t n, hipStream_t s)
 {
     static const int head = getenv("HKV_PRE_HEAD") ? atoi(getenv("HKV_PRE_HEAD")) : kPreHead;
     const dim3 grid((unsigned)((n + kPreElems - 1) / kPreElems));
+    static const bool ff_env = getenv("HKV_PRE_FFILTER") && atoi(getenv("HKV_PRE_FFILTER")) != 0;
     if (a.ktab) hipLaunchKernelGGL((k_local_pre<kPreHead, false, true>), grid, dim3(256), 0, s, a);
+    else if (ff_env && !a.phys_hint && head == kPreHead)
+        hipLaunchKernelGGL((k_local_pre<kPreHead, false, false, true>), grid, dim3(256), 0, s, a);
     else if (a.phys_hint) hipLaunchKernelGGL((k_local_pre<kPreHead, true>), grid, dim3(256), 0, s, a);
     else if (head == 256) hipLaunchKernelGGL(k_local_pre<256>, grid, dim3(256), 0, s, a);
     else if (head == 512) hipLaunchKernelGGL(k_local_pre<512>, grid, dim3(256), 0, s, a);
@@ -3743,7 +3789,11 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         }
         // HKV_LF_PAIR: elements per lane group in k_local_fused (2: 32 per wave; 4: 64, more loads in flight)
         static const int lfp_env = getenv("HKV_LF_PAIR") ? atoi(getenv("HKV_LF_PAIR")) : 2;
-        if (a.ktab)
+        // HKV_LF_FSPEC=1: every hit loads its key's F word beside the log line (no dependent load after it)
+        static const bool fspec_env = getenv("HKV_LF_FSPEC") && atoi(getenv("HKV_LF_FSPEC")) != 0;
+        if (fspec_env && !a.ktab && !a.phys_hint && lfp_env == 2)
+            hipLaunchKernelGGL((k_local_fused<2, false, false, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
+        else if (a.ktab)
             hipLaunchKernelGGL((k_local_fused<2, false, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
         else if (a.phys_hint)
             hipLaunchKernelGGL((k_local_fused<2, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);

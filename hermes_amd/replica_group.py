@@ -278,6 +278,48 @@ class ReplicaRound:
         check(_L.hkv_wl_marshal_acks_aligned(_ptr(self.inv_recv), _ptr(self.inv_totals), self.N, width, self.op,
                                              _ptr(self.ack_slab), self.ack_size, self.rank, _s()), "marshal_acks")
 
+    # -- per-peer exchanges (ReplicaGroupRound with p2p): each peer's INV slab is sent and received on
+    # its own, applied as soon as it is there, and its ACK row goes back right after
+    def inv_row_io(self, p: int, width: int):
+        """(send, receive) of the INV exchange with peer p: this rank's packed slab, p's row"""
+        n = width * self.op
+        return self.inv_pack[:n], self.inv_recv[p * n:(p + 1) * n]
+
+    def ack_row_io(self, p: int, width: int):
+        """(send, receive) of the ACK exchange with peer p: the answers to p's INVs, p's answers to ours"""
+        n = width * self.ack_size
+        return self.ack_slab[p * n:(p + 1) * n], self.ack_recv[p * n:(p + 1) * n]
+
+    def invs_begin(self, width: int):
+        """Before the per-peer INV launches: this rank's own row carries nothing, and the ACK row it
+        'receives' from itself is all empty slots (the ACK phase reads every row)"""
+        self.inv_totals[self.rank:self.rank + 1].zero_()
+        n, na = width * self.op, width * self.ack_size
+        check(_L.hkv_wl_marshal_acks_aligned(_ptr(self.inv_recv[self.rank * n:]), _ptr(self.inv_totals[self.rank:]), 1,
+                                             width, self.op, _ptr(self.ack_recv[self.rank * na:]), self.ack_size,
+                                             self.rank, _s()), "marshal_acks")
+        if self.failed:   # no ACKs from a failed replica
+            self.ack_slab[:self.N * na].view(-1, self.ack_size)[:, 8] = int(L.Bucket.EMPTY)
+
+    def invs_peer(self, p: int, width: int, fold: bool):
+        """Peer p's INVs (its row of inv_recv, just arrived) as one unique-key launch, then the ACK row
+        answering them. fold: p's total rides in the row's spare slot (steady rounds)"""
+        n = width * self.op
+        if fold:
+            a = p * n + (width - 1) * self.op
+            self.inv_totals[p:p + 1].copy_(self.inv_recv[a:a + 4].view(torch.int32))
+        if self.failed:
+            return
+        self.kvs.batch(L.BatchType.invs, self.inv_recv[p * n:], 1, width, self.op, self.mb,
+                       counts=self.inv_totals[p:p + 1], unique=True)
+        check(_L.hkv_wl_marshal_acks_aligned(_ptr(self.inv_recv[p * n:]), _ptr(self.inv_totals[p:]), 1, width, self.op,
+                                             _ptr(self.ack_slab[p * width * self.ack_size:]), self.ack_size, self.rank,
+                                             _s()), "marshal_acks")
+
+    def invs_end(self, width: int):
+        if self.count_elems and not self.failed:
+            self.elem_totals[0] += self.inv_totals.sum()
+
     def acks(self, width: int, stride: int):
         """Apply the ACKs returned by the peers (ack_recv [N][width], row p from rank p, lined up
         with inv_pack), regrouped per worker ([W][stride]); the VALs of completed writes, packed
@@ -427,16 +469,20 @@ class ReplicaGroupRound:
 
     def __init__(self, kvs: HermesKV | None, n_workers: int, zipf: HkvZipf | None, write_permille: int = 200, *,
                  seed: int = 0x5EED, world: int, rank: int, group=None, replica=None, hades: bool = False,
-                 comm=None, **kw):
+                 comm=None, p2p: bool | None = None, **kw):
         """`replica`: drive an existing ReplicaRound-shaped object instead of building one.
         `hades`: the membership comes from Hades agreement over heartbeats exchanged every round
         (a failed rank is expelled when the survivors agree), instead of a host-driven drop.
-        `comm`: an object with gather(out, inp), gather_async(out, inp) -> work (.wait()) and
-        a2a(out, inp) to use instead of torch.distributed (tests: ranks as threads of one process)."""
+        `comm`: an object with gather(out, inp), gather_async(out, inp) -> work (.wait()), a2a(out, inp)
+        and p2p(pairs) -> {peer: [work]} to use instead of torch.distributed (tests: ranks as threads of
+        one process). `p2p` (default: HKV_GROUP_P2P, on): the INV slabs and ACK rows go peer by peer
+        (grouped isend/irecv per peer) instead of one all-gather and one all-to-all, so each peer's INV
+        launch waits only for that peer's slab and its ACK row leaves right after it."""
         import torch.distributed as dist
         self.dist = dist
         self.group = group
         self.comm = comm
+        self.p2p = (os.environ.get("HKV_GROUP_P2P", "1") != "0") if p2p is None else p2p
         self.r = replica if replica is not None else ReplicaRound(kvs, n_workers, world, rank, zipf,
                                                                   write_permille, seed=seed, **kw)
         self.hades = hades
@@ -476,6 +522,16 @@ class ReplicaGroupRound:
         if self.comm is not None:
             return self.comm.a2a(out, inp)
         self.dist.all_to_all_single(out, inp, group=self.group)
+
+    def _p2p(self, pairs) -> dict:
+        """pairs: (peer, send, receive), peers ascending. One grouped isend/irecv per peer, returned
+        unwaited: {peer: [work]}. Every rank walks its peers in ascending order, which is one global
+        order of the rank pairs, so the exchanges cannot wait on each other in a cycle."""
+        if self.comm is not None:
+            return self.comm.p2p(pairs)
+        d = self.dist
+        return {p: d.batch_isend_irecv([d.P2POp(d.isend, snd, p, self.group), d.P2POp(d.irecv, rcv, p, self.group)])
+                for p, snd, rcv in pairs}
 
     def _views(self, changed: bool) -> bytes:
         """one heartbeat exchange: all ranks' rows gathered (row = sender), this rank polls its
@@ -525,13 +581,16 @@ class ReplicaGroupRound:
         exchange for the writes it completes -- or, with Hades, the failed rank stops
         heartbeating and the survivors expel it when they agree (two periods later)."""
         r = self.r
+        p2p = self.p2p and hasattr(r, "invs_peer")
         steady = self.plan is not None and self.plan.steady(drop is not None or self.hades or not r.unique_acks)
         fold = steady and self.plan.fold
         if steady:   # no host read: the planned width, each rank's INVs capped at it
             width, stride = self.plan.slab_width(), None
             r.own_total = None
             _timed(events, "local", lambda: r.local(cap=self.plan.width), timed_batches)
-            if fold:
+            if fold and p2p:
+                r.inv_io_total(width)          # the total into the slab's spare slot; the rows go peer by peer
+            elif fold:
                 self._gather(*r.inv_io_total(width))
                 r.take_inv_totals(width)
             else:
@@ -542,14 +601,33 @@ class ReplicaGroupRound:
             width, stride = r.round_shape()  # host synchronisation: this round's exact width
             if self.plan is not None:
                 self.plan.calibrate(width, r.W * r.C)
-        if not fold:
+        if p2p:
+            peers = [p for p in range(self.world) if p != r.rank]
+            inv_w = self._p2p([(p, *r.inv_row_io(p, width)) for p in peers])
+        elif not fold:
             self._gather(*r.inv_io(width))
         if drop is not None:
             r.peer_failing()
             if drop == r.rank:
                 r.fail()
-        _timed(events, "invs", lambda: r.invs(width), timed_batches)
-        self._a2a(*r.ack_io(width))
+        if p2p:
+            ack_w = {}
+
+            def invs():
+                r.invs_begin(width)
+                for p in peers:   # each peer's launch waits for that peer's slab only
+                    for w in inv_w[p]:
+                        w.wait()
+                    r.invs_peer(p, width, fold)
+                    ack_w.update(self._p2p([(p, *r.ack_row_io(p, width))]))
+                r.invs_end(width)
+            _timed(events, "invs", invs, timed_batches)
+            for p in peers:
+                for w in ack_w[p]:
+                    w.wait()
+        else:
+            _timed(events, "invs", lambda: r.invs(width), timed_batches)
+            self._a2a(*r.ack_io(width))
         _timed(events, "acks", lambda: r.acks(width, stride), timed_batches)
         if not self.hades and drop is None:
             # the VAL exchange overlaps the refill: the refill touches only this replica's op slab and
@@ -589,10 +667,14 @@ class LoopbackGroup:
     exactly the layouts the RCCL driver produces (all-gather: row p = rank p's slab;
     all-to-all: row p of the output = row `rank` of rank p's input)."""
 
-    def __init__(self, rounds: list[ReplicaRound], hades: bool = False):
+    def __init__(self, rounds: list[ReplicaRound], hades: bool = False, p2p: bool | None = None):
+        """p2p (default: HKV_GROUP_P2P, on, as ReplicaGroupRound): INV slabs and ACK rows move peer by
+        peer (row copies, `_rows`) and each replica applies its peers' INVs through the per-peer phases
+        (invs_begin / invs_peer / invs_end) instead of the all-gather and all-to-all layouts."""
         self.rounds = rounds
         self.N = len(rounds)
         self.hades = hades
+        self.p2p = (os.environ.get("HKV_GROUP_P2P", "1") != "0") if p2p is None else p2p
         self.plan = WidthPlan() if all(getattr(r, "packed_marshal", False) for r in rounds) else None
         self.hades_changes = []        # (round, rank, membership) of every agreed change
         self.clock = 0
@@ -643,6 +725,12 @@ class LoopbackGroup:
     def _gather_io(self, ios):
         self._gather([o for o, _ in ios], [i for _, i in ios])
 
+    @staticmethod
+    def _rows(pairs):
+        """pairs: (send, receive) of the per-peer exchanges, each receive the send's copy"""
+        for snd, rcv in pairs:
+            rcv.copy_(snd)
+
     def _a2a_io(self, ios):
         self._a2a([o for o, _ in ios], [i for _, i in ios])
 
@@ -662,7 +750,12 @@ class LoopbackGroup:
             else:
                 r.local()
         seen("local")
-        if fold:
+        if fold and self.p2p:   # the totals ride in the slabs' spare slots, taken per peer (invs_peer)
+            width = self.plan.slab_width()
+            shapes = [(width, None)] * len(rs)
+            for r in rs:
+                r.inv_io_total(width)
+        elif fold:
             width = self.plan.slab_width()
             shapes = [(width, None)] * len(rs)
             self._gather_io([r.inv_io_total(width) for r in rs])
@@ -678,16 +771,32 @@ class LoopbackGroup:
             width = shapes[0][0]                 # the same on every replica (max of the same totals)
             if self.plan is not None:
                 self.plan.calibrate(width, rs[0].W * rs[0].C)
-        if not fold:
+        N = self.N
+        if self.p2p:   # row p of replica q's INVs: peer p's slab
+            self._rows([(rs[p].inv_row_io(q, width)[0], rs[q].inv_row_io(p, width)[1])
+                        for q in range(N) for p in range(N) if p != q])
+        elif not fold:
             self._gather_io([r.inv_io(width) for r in rs])
         if drop is not None:
             for r in rs:
                 r.peer_failing()
             rs[drop].fail()
-        for r in rs:
-            r.invs(width)
+        if self.p2p:
+            for q, r in enumerate(rs):
+                r.invs_begin(width)
+                for p in range(N):
+                    if p != q:
+                        r.invs_peer(p, width, fold)
+                r.invs_end(width)
+        else:
+            for r in rs:
+                r.invs(width)
         seen("invs")
-        self._a2a_io([r.ack_io(width) for r in rs])
+        if self.p2p:   # row p of replica q's ACKs: peer p's answers to q's INVs
+            self._rows([(rs[p].ack_row_io(q, width)[0], rs[q].ack_row_io(p, width)[1])
+                        for q in range(N) for p in range(N) if p != q])
+        else:
+            self._a2a_io([r.ack_io(width) for r in rs])
         for r, (_, stride) in zip(rs, shapes):
             r.acks(width, stride)
         seen("acks")

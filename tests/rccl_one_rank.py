@@ -6,7 +6,9 @@ The group's replicas share this process, so each collective of a round -- the IN
 slab all-gathers, the ACK all-to-all, the VAL totals and VAL slab all-gathers -- is staged exactly
 as ReplicaGroupRound lays it out ([N][width] rows, row p = replica p) and then moved by RCCL
 (all_gather_into_tensor / all_to_all_single over the one rank, async_op with the wait before the
-consumer, on torch's stream), with the tensors, sizes and dtypes of a real round. Every batch launch
+consumer, on torch's stream), with the tensors, sizes and dtypes of a real round. With the per-peer
+exchanges (HKV_GROUP_P2P, the default) every INV slab row and ACK row is one grouped isend/irecv
+(batch_isend_irecv, to this rank itself) instead. Every batch launch
 is mirrored into an oracle table and every key must converge. Prints one JSON line.
 `--retry-skew`: bench.py's configuration (refill_ops' retry and the skew flags 3).
 """
@@ -33,7 +35,7 @@ def main():
     from oracle.oracle import OracleKVS, gen_keys
     from tests.helpers import Mirror
 
-    calls = {"all_gather_into_tensor": 0, "all_to_all_single": 0, "bytes": 0}
+    calls = {"all_gather_into_tensor": 0, "all_to_all_single": 0, "batch_isend_irecv": 0, "bytes": 0}
 
     class RcclLoopback(LoopbackGroup):
         """LoopbackGroup whose exchanges go through RCCL: the replicas' rows are staged in one
@@ -47,6 +49,17 @@ def main():
                 w.wait()
                 calls["all_gather_into_tensor"] += 1
                 calls["bytes"] += o.numel() * o.element_size()
+
+        @staticmethod
+        def _rows(pairs):
+            # the per-peer exchanges (ReplicaGroupRound's p2p path): one grouped isend/irecv per row, here
+            # a send to this one rank itself
+            for snd, rcv in pairs:
+                for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, snd.contiguous(), 0),
+                                                 dist.P2POp(dist.irecv, rcv, 0)]):
+                    w.wait()
+                calls["batch_isend_irecv"] += 1
+                calls["bytes"] += rcv.numel() * rcv.element_size()
 
         def _a2a(self, outs, ins):
             N = self.N

@@ -38,9 +38,12 @@ def test_one_rank_rccl_group_round(args):
     print(d)
     assert d["launches"] == [15, 15, 15], d          # 3 rounds x (local, INV per peer (2), the ACK rows, VAL)
     assert d["diverged_keys"] == 0, d
-    # per round and replica: INV totals + INV slabs + VAL totals + VAL slabs gathered in the calibrating
-    # round, the slabs alone (each carrying its total, WidthPlan.fold) in the 6 steady ones; ACKs all-to-all
-    # (3 mirrored rounds, then 4 steady ones under the sync check)
-    assert d["calls"]["all_gather_into_tensor"] == (4 + 6 * 2) * 3 and d["calls"]["all_to_all_single"] == 7 * 3, d
+    # per round and replica (3 mirrored rounds, then 4 steady ones under the sync check): INV totals, VAL
+    # totals and VAL slabs gathered in the calibrating round, the VAL slab alone (carrying its total,
+    # WidthPlan.fold) in the 6 steady ones; every INV slab row and ACK row one grouped isend/irecv
+    # (3 replicas x 2 peers each, both directions: 12 per round)
+    c = d["calls"]
+    assert c["all_gather_into_tensor"] == (3 + 6 * 1) * 3 and c["all_to_all_single"] == 0, d
+    assert c["batch_isend_irecv"] == 7 * 12, d
     assert d["width"] is not None
     assert min(d["committed"]) > 0

@@ -118,14 +118,41 @@ class TagReplica:
         if self.failed:
             return
         for p in range(self.N):
-            n = int(self.inv_totals[p])
-            rows = self._rows(p)
-            assert n == (0 if p == self.rank else len(rows)) and len(rows) <= width
-            for k in range(n):
-                w, j = rows[k]
-                assert int(rv[p, k]) == _tag(1, p, 0, w, j)
-                av[p, k] = _tag(2, self.rank, p, w, j)   # ACK from me to coordinator p, INV's position
-                self.checked += 1
+            self._inv_row(p, width)
+
+    def _inv_row(self, p, width):
+        rv, av = self.inv_recv[:self.N * width].view(self.N, width), self.ack_slab[:self.N * width].view(self.N, width)
+        n = int(self.inv_totals[p])
+        rows = self._rows(p)
+        assert n == (0 if p == self.rank else len(rows)) and len(rows) <= width
+        for k in range(n):
+            w, j = rows[k]
+            assert int(rv[p, k]) == _tag(1, p, 0, w, j)
+            av[p, k] = _tag(2, self.rank, p, w, j)   # ACK from me to coordinator p, INV's position
+            self.checked += 1
+
+    # the per-peer exchange (ReplicaGroupRound's p2p path): the same rows, one peer at a time
+    def inv_row_io(self, p, width):
+        return self.inv_pack[:width], self.inv_recv[p * width:(p + 1) * width]
+
+    def ack_row_io(self, p, width):
+        return self.ack_slab[p * width:(p + 1) * width], self.ack_recv[p * width:(p + 1) * width]
+
+    def invs_begin(self, width):
+        self.inv_totals[self.rank] = 0
+        self.ack_slab[:self.N * width].fill_(-1)
+        self.ack_recv[self.rank * width:(self.rank + 1) * width].fill_(-1)   # nothing from itself
+        self.p2p_peers = []
+
+    def invs_peer(self, p, width, fold):
+        assert not fold and p != self.rank and p not in self.p2p_peers
+        self.p2p_peers.append(p)
+        if not self.failed:
+            self._inv_row(p, width)
+
+    def invs_end(self, width):
+        assert self.p2p_peers == [p for p in range(self.N) if p != self.rank]
+        self.p2p_rounds = getattr(self, "p2p_rounds", 0) + 1
 
     def acks(self, width, stride):
         rv = self.ack_recv[:self.N * width].view(self.N, width)
@@ -161,14 +188,15 @@ class TagReplica:
         self.pending += 1
 
 
-def _worker(rank, world, port, rounds, q, drop=None):
+def _worker(rank, world, port, rounds, q, drop=None, p2p=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         rep = TagReplica(world, rank, drop=drop)
-        drv = ReplicaGroupRound(None, rep.W, None, world=world, rank=rank, replica=rep)
+        drv = ReplicaGroupRound(None, rep.W, None, world=world, rank=rank, replica=rep, p2p=p2p)
         for k in range(rounds):
             drv.step(drop=drop[0] if drop is not None and k == drop[1] else None)
+        assert getattr(rep, "p2p_rounds", 0) == (rounds if p2p else 0)
         q.put((rank, rep.checked, None))
     except Exception as e:  # surfaced by the parent
         q.put((rank, 0, repr(e)))
@@ -184,15 +212,18 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,drop", [(2, None), (3, None), (3, (2, 1)), (4, (1, 1))])
-def test_rccl_choreography_gloo(world, drop):
+@pytest.mark.parametrize("world,drop,p2p", [(2, None, True), (3, None, True), (3, (2, 1), True), (4, (1, 1), True),
+                                            (3, None, False), (4, (1, 1), False)])
+def test_rccl_choreography_gloo(world, drop, p2p):
     """drop = (rank, round): that rank fails in that round once its INVs are out; the others
-    see no ACKs or VALs from it, the membership-change VAL exchange, and no INVs from it later."""
+    see no ACKs or VALs from it, the membership-change VAL exchange, and no INVs from it later.
+    p2p: the INV slabs and ACK rows exchanged peer by peer (grouped isend/irecv, the default), or
+    as one all-gather and one all-to-all."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     rounds = 4 if drop else 3
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, rounds, q, drop)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, rounds, q, drop, p2p)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]

@@ -43,18 +43,22 @@ def _key_images(g, o, keys):
     return rows
 
 
-@pytest.mark.parametrize("n_rep,workers,write_pm,rounds,retry,skew,fold", [
-    (2, 24, 300, 4, False, 0, True), (3, 16, 400, 4, False, 0, True), (4, 8, 500, 3, False, 0, True),
-    (8, 16, 200, 3, False, 0, True), (8, 16, 200, 4, True, 3, True), (8, 16, 200, 4, True, 0, True),
-    (3, 24, 400, 5, True, 3, True), (3, 24, 400, 5, True, 3, False)])
-def test_loopback_group_parity_and_convergence(n_rep, workers, write_pm, rounds, retry, skew, fold, monkeypatch):
+@pytest.mark.parametrize("n_rep,workers,write_pm,rounds,retry,skew,fold,p2p", [
+    (2, 24, 300, 4, False, 0, True, True), (3, 16, 400, 4, False, 0, True, True), (4, 8, 500, 3, False, 0, True, True),
+    (8, 16, 200, 3, False, 0, True, True), (8, 16, 200, 4, True, 3, True, True), (8, 16, 200, 4, True, 0, True, True),
+    (3, 24, 400, 5, True, 3, True, True), (3, 24, 400, 5, True, 3, False, True), (8, 16, 200, 4, True, 3, True, False),
+    (3, 24, 400, 5, True, 3, False, False)])
+def test_loopback_group_parity_and_convergence(n_rep, workers, write_pm, rounds, retry, skew, fold, p2p, monkeypatch):
     """(8, 16, 200, 3) is BASELINE configs[3]'s group on one GPU: 8 replicas (the width of the
     membership vectors), 20 % writes, Zipf 0.99 -- every phase, kernel and slab layout of the RCCL
     run, with every launch of every replica mirrored into its oracle twin. retry / skew: the
     configuration bench.py --gpus N runs (refill_ops' retry, stalled ops keep their slots, and the
     reference's skew optimisations, config.h:79-80) and the reference's shipped one (skew 0). fold: the
-    steady rounds' totals ride in a spare slot of each slab (WidthPlan.fold) or get their own gathers."""
+    steady rounds' totals ride in a spare slot of each slab (WidthPlan.fold) or get their own gathers.
+    p2p: INV slabs and ACK rows moved peer by peer (ReplicaGroupRound's default), or as the all-gather
+    and all-to-all layouts."""
     monkeypatch.setenv("HKV_GROUP_FOLD_TOTALS", "1" if fold else "0")
+    monkeypatch.setenv("HKV_GROUP_P2P", "1" if p2p else "0")
     from hermes_amd.kvs import HermesKV
     from hermes_amd.replica_group import LoopbackGroup, ReplicaRound
     from hermes_amd.workload import zipf_params
@@ -411,11 +415,37 @@ class _ThreadComm:
                 ov[p].copy_(x.view(h.n, -1)[self.rank])
             h.bar.wait()
 
+        def p2p(self, pairs):
+            """per-peer exchanges through a mailbox: every send of the call is posted first, then each
+            receive waits for its peer's matching send (the k-th message between two ranks) and copies it
+            on the shared stream, behind the sender's producers"""
+            h = self.hub
+            with h.cv:
+                for p, snd, _ in pairs:
+                    k = h.sent.get((self.rank, p), 0)
+                    h.sent[(self.rank, p)] = k + 1
+                    h.mail[(self.rank, p, k)] = snd
+                    h.p2p_calls += 1
+                h.cv.notify_all()
+            for p, _, rcv in pairs:
+                k = h.got.get((p, self.rank), 0)
+                h.got[(p, self.rank)] = k + 1
+                with h.cv:
+                    if not h.cv.wait_for(lambda: (p, self.rank, k) in h.mail, timeout=60):
+                        raise TimeoutError(f"rank {self.rank}: no message {k} from {p}")
+                    snd = h.mail.pop((p, self.rank, k))
+                rcv.copy_(snd)
+            done = type("Done", (), {"wait": lambda self: None})()
+            return {p: [done] for p, _, _ in pairs}
+
     def __init__(self, n):
         import threading
         self.n = n
         self.bar = threading.Barrier(n, timeout=60)
         self.slots = [None] * n
+        self.cv = threading.Condition()
+        self.mail, self.sent, self.got = {}, {}, {}
+        self.p2p_calls = 0
 
     def rank(self, r):
         return self._Rank(self, r)
@@ -487,6 +517,9 @@ def test_group_rounds_without_host_sync(world):
         faulthandler.cancel_dump_traceback_later()
         dump.close()
     assert not errs, errs
+    # the per-peer exchanges (ReplicaGroupRound's p2p default): per rank and round, its INV slab to each
+    # peer and an ACK row back to each, over the calibrating round and the 10 checked ones
+    assert hub.p2p_calls == world * 11 * 2 * (world - 1), hub.p2p_calls
     torch.cuda.synchronize()
     for d in drivers:
         st = d.stats()

@@ -2219,7 +2219,18 @@ __global__ __launch_bounds__(64) void k_unique_rows(BatchArgs a)
 #pragma unroll
         for (int r = 0; r < RMAX; ++r) {
             if (r >= R || r == a.skip_row || q >= CH) continue;
-            const uint4 w = sops[r][te[k] * CH + q];
+            uint4 w = sops[r][te[k] * CH + q];
+            if (TYPE == kAcks && CH == 1 && a.ack_out) {
+                // the VAL callbacks (hermes_worker.c:122-157, as shipped): an element whose opcode is not
+                // ACK_SUCCESS, MEMBERSHIP_CHANGE or EMPTY is sent as a VAL from this machine, every
+                // non-empty one leaves empty; a hole (opcode 0) is no element
+                const uint8_t oc = (uint8_t)w.z;
+                uint4 v = make_uint4(0u, 0u, (uint32_t)kEmpty, 0u);
+                if (oc != 0 && oc != kAckSuccess && oc != kOpMembChange && oc != kEmpty)
+                    v = make_uint4(w.x, w.y, (w.z & ~0xFFFFu) | (uint32_t)kOpVal | ((uint32_t)(uint8_t)a.g.machine_id << 8), w.w);
+                *reinterpret_cast<uint4 *>(a.ack_out + (r * a.row_stride + i0 + te[k]) * 16) = v;
+                if (oc != 0 && oc != kEmpty) w.z = (w.z & ~0xFFu) | (uint32_t)kEmpty;
+            }
             if (!chunk_equal(w, op[r][k])) {
                 uint8_t *xg = a.elems + (r * a.row_stride + i0 + te[k]) * a.esz + 16 * q;
                 if (16 * q + 16 <= a.esz) *reinterpret_cast<uint4 *>(xg) = w;
@@ -3657,7 +3668,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.patch = nullptr;
     a.pkeys = nullptr;
     a.cancel = bl.stage == 3;
-    a.ack_out = bl.type == kInvs ? bl.ack_out : nullptr;
+    a.ack_out = bl.type == kInvs || (bl.type == kAcks && bl.n_rows > 0) ? bl.ack_out : nullptr;
     a.ack_out_size = bl.ack_out_size;
     a.ktab = nullptr;
     a.ktab_bits = bl.ktab_bits;

@@ -679,7 +679,14 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
             : (d->flags & HKV_BATCH_SMALL) ? kPathSmall : kPathAuto;
     bl.unique = (d->flags & HKV_BATCH_UNIQUE) && (d->type == kInvs || d->type == kAcks) ? 1 : 0;
     if (force_engine) bl.path = kPathEngine;
-    if (d->d_ack_out) {
+    if (d->d_ack_out && d->type == kAcks) {   // the VAL callbacks, by the ACK rows launch
+        if (!(d->flags & HKV_BATCH_ROWS) || !bl.unique || d->elem_size != 16 || d->ack_out_size != 16 ||
+            t->geo.entry_size != 64 || t->geo.st_value != 31 || ((uintptr_t)d->d_ack_out & 15))
+            return fail(-1, "d_ack_out on an ACK launch: HKV_BATCH_ROWS unique launches of 16-byte ACKs and 64-byte "
+                            "entries, 16-byte VALs, 16-byte aligned");
+        bl.ack_out = d->d_ack_out;
+        bl.ack_out_size = d->ack_out_size;
+    } else if (d->d_ack_out) {
         const bool small_geo = t->geo.entry_size == 64 && t->geo.st_value == 31 && d->elem_size <= 64;
         const bool big_geo = t->geo.entry_size == 320 && t->geo.st_value == 287 && d->elem_size <= 320;
         if (d->type != kInvs || !bl.unique || d->n_rows > 1 || !(small_geo || big_geo) || d->ack_out_size < 16 ||

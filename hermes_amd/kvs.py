@@ -234,8 +234,9 @@ class HermesKV:
         if phys is not None:
             assert phys.is_cuda and phys.dtype == torch.int64 and phys.numel() >= total
             d.d_phys = phys.data_ptr()
-        if ack_out is not None:
-            assert unique and ack_out.is_cuda and ack_out.dtype == torch.uint8 and ack_out.numel() >= total * ack_out_size
+        if ack_out is not None:   # INV launches: the ACK callbacks; ACK rows launches: the VAL callbacks, per row
+            span = total if rows is None else (rows[0] - 1) * rows[1] + total
+            assert unique and ack_out.is_cuda and ack_out.dtype == torch.uint8 and ack_out.numel() >= span * ack_out_size
             d.d_ack_out = ack_out.data_ptr()
             d.ack_out_size = int(ack_out_size)
         if put_keys is not None:

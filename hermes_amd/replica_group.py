@@ -450,6 +450,19 @@ class WidthPlan:
         return self.width + 1 if self.fold else self.width
 
 
+class _HostStaged:
+    """a gloo exchange staged through host buffers: wait() ends the exchange and copies the received row
+    to the device tensor (on the current stream)"""
+
+    def __init__(self, works, host_rcv, rcv, host_snd):
+        self.works, self.host_rcv, self.rcv, self.host_snd = works, host_rcv, rcv, host_snd
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.rcv.copy_(self.host_rcv)
+
+
 def _timed(events, name, fn, only=None):
     if events is None or (only is not None and name not in only):
         fn()
@@ -530,6 +543,15 @@ class ReplicaGroupRound:
         if self.comm is not None:
             return self.comm.p2p(pairs)
         d = self.dist
+        if pairs and pairs[0][1].is_cuda and d.get_backend(self.group) != "nccl":
+            # gloo (tests: ranks sharing one GPU): its point-to-point ops move host memory and are not
+            # ordered on the CUDA stream, so the rows are staged through host buffers
+            out = {}
+            for p, snd, rcv in pairs:
+                sc, rc = snd.cpu(), torch.empty(rcv.shape, dtype=rcv.dtype)
+                ws = d.batch_isend_irecv([d.P2POp(d.isend, sc, p, self.group), d.P2POp(d.irecv, rc, p, self.group)])
+                out[p] = [_HostStaged(ws, rc, rcv, sc)]
+            return out
         return {p: d.batch_isend_irecv([d.P2POp(d.isend, snd, p, self.group), d.P2POp(d.irecv, rcv, p, self.group)])
                 for p, snd, rcv in pairs}
 

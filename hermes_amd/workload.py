@@ -330,6 +330,12 @@ class Round:
         # in peer order; HKV_ACK_ROWS=0: one launch per peer, experiments)
         self.ack_rows = (os.environ.get("HKV_ACK_ROWS", "1") != "0" and self.sizes.entry == 64
                          and self.ack_size <= 64)
+        # ... which also makes the VALs of the writes it completes (the VAL callbacks, hermes_worker.c:122-157,
+        # into val_out in the ACKs' positions: hkv_batch_desc.d_ack_out on an ACK launch) instead of a
+        # collection pass over the ACK slab (HKV_FUSED_VALS=0: k_collect_vals, compacted per worker)
+        self.fused_vals = (self.ack_pm and self.ack_rows and self.ack_size == 16 and val_credits is None
+                           and os.environ.get("HKV_FUSED_VALS", "1") != "0")
+        self._vals_made = False
         self.inv_round = 0
         self.ack_m = self.C
         self.maxc_ev = torch.cuda.Event() if self.fit else None
@@ -674,7 +680,9 @@ class Round:
             if self.ack_rows and n_rows:
                 self.kvs.batch(L.BatchType.acks, acks, self.W, T, self.ack_size, self.mb, rw=self.ops,
                                rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off, rw_state=self._rws(),
-                               unique=True, rows=(n_rows, T, -1), rw_opcodes=self._rwo())
+                               unique=True, rows=(n_rows, T, -1), rw_opcodes=self._rwo(),
+                               ack_out=self.val_out if self.fused_vals else None)
+                self._vals_made = self.fused_vals
                 return
             for r in range(n_rows):
                 self.kvs.batch(L.BatchType.acks, acks[r * T * self.ack_size:], self.W, T, self.ack_size, self.mb,
@@ -696,7 +704,11 @@ class Round:
 
     def collect_vals(self):
         """VALs of the writes this round's ACK batch completed, compacted per worker (val_out
-        [W][ack_stride], val_count): only the ACK slab's live elements are read."""
+        [W][ack_stride], val_count): only the ACK slab's live elements are read. Nothing to do when the
+        ACK rows launch made them itself (fused_vals: val_out then holds them in the ACKs' positions)."""
+        if self._vals_made:
+            self._vals_made = False
+            return
         if self.ack_pm:
             check(_L.hkv_wl_collect_vals_blocks(_ptr(self.acks), _ptr(self.ack_count), self.W, self.ack_width,
                                                 self.ack_size, _ptr(self.val_out), self.C, _ptr(self.val_count),

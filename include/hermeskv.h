@@ -168,7 +168,14 @@ typedef struct hkv_batch_desc {
                                    machine for INV_SUCCESS, the element itself as INV-abort when ack_out_size holds
                                    it, else opcode ST_EMPTY), written to d_ack_out + i * ack_out_size by the launch
                                    itself, and each answered element leaves with opcode ST_EMPTY, as after the
-                                   callbacks' send (ack_modify_elem_after_send). NULL = none (ABI 6) */
+                                   callbacks' send (ack_modify_elem_after_send). NULL = none (ABI 6)
+                                   ACK launches with HKV_BATCH_ROWS, 16-byte ACKs and 64-byte entries: the VAL
+                                   callbacks (hermes_worker.c:122-157) instead -- every row element of a batch
+                                   whose result opcode is not ACK_SUCCESS, MEMBERSHIP_CHANGE or EMPTY is copied
+                                   to d_ack_out + (r * row_stride + j) * 16 with opcode ST_OP_VAL and sender =
+                                   this machine (val_copy_and_modify_elem), every other position there gets
+                                   opcode ST_EMPTY, and every non-empty element leaves with opcode ST_EMPTY
+                                   (val_skip_or_get_sender_id, val_modify_elem_after_send); ack_out_size 16 */
     uint32_t ack_out_size;
     const uint64_t *d_phys;     /* device, local, INV (HKV_BATCH_UNIQUE) and VAL launches: per element, the log offset
                                    the lookup of its key gives (hkv_wl_peer_locate), or ~0 for none; valid only

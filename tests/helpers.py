@@ -100,6 +100,25 @@ def ack_callbacks(invs, ack_size, machine_id):
     return acks, after
 
 
+def val_callbacks(acks: np.ndarray, live: np.ndarray, machine_id: int):
+    """The worker's VAL callbacks (hermes_worker.c:122-157, assertions off as shipped) over ACK results
+    in place: an element whose opcode is not ACK_SUCCESS, MEMBERSHIP_CHANGE or EMPTY is sent as a VAL
+    (its first 16 bytes, opcode ST_OP_VAL, sender = this machine: val_copy_and_modify_elem); every
+    non-empty element then leaves empty (val_skip_or_get_sender_id, val_modify_elem_after_send). Holes
+    (live False) are no elements. Returns (VALs in the ACKs' positions, opcode ST_EMPTY where none;
+    the ACKs after)."""
+    oc = acks[:, 8]
+    send = live & ~np.isin(oc, [int(L.Resp.ACK_SUCCESS), int(L.Op.MEMBERSHIP_CHANGE), int(L.Bucket.EMPTY)])
+    vals = np.zeros((len(acks), 16), np.uint8)
+    vals[:, 8] = int(L.Bucket.EMPTY)
+    vals[send] = acks[send, :16]
+    vals[send, 8] = int(L.Op.VAL)
+    vals[send, 9] = machine_id
+    after = acks.copy()
+    after[live & (oc != int(L.Bucket.EMPTY)), 8] = int(L.Bucket.EMPTY)
+    return vals, after
+
+
 class Mirror:
     """Runs every batch launch of a device table on an oracle twin and compares."""
 
@@ -141,7 +160,7 @@ class Mirror:
             return
         if rows is not None:
             return self._rows(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
-                              rw_stride_bytes, rw_state, rows, rw_opcodes)
+                              rw_stride_bytes, rw_state, rows, rw_opcodes, ack_out)
         if offsets is not None:
             return self._packed(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
                                 rw_stride_bytes, rw_state, unique, ack_out, ack_out_size, phys, rw_opcodes)
@@ -233,9 +252,10 @@ class Mirror:
         assert np.array_equal(rw_state.cpu().numpy()[:n], st_after[:n]), f"{what}: read_write_ops state mirror differs"
 
     def _rows(self, btype, elems, n_batches, total, elem_size, membership, offsets, stream, rw, rw_stride_bytes,
-              rw_state, rows, rw_opcodes=None):
+              rw_state, rows, rw_opcodes=None, ack_out=None):
         """An HKV_BATCH_ROWS launch: the oracle applies row after row (skip row excepted), each row's
-        batches without their holes (opcode 0); the device's rows must equal them, holes untouched."""
+        batches without their holes (opcode 0); the device's rows must equal them, holes untouched. ack_out
+        (ACK launches): the VALs the launch made must be val_callbacks() of the oracle's results."""
         import torch
         torch.cuda.synchronize()
         n_rows, row_stride, skip = rows
@@ -255,9 +275,11 @@ class Mirror:
             flat = flat_all[r * row_stride * elem_size:(r * row_stride + total) * elem_size].reshape(total, elem_size)
             ins[r] = flat.copy()
         self._orig(btype, elems, n_batches, total, elem_size, membership, rw=rw, rw_stride_bytes=rw_stride_bytes,
-                   stream=stream, offsets=offsets, rw_state=rw_state, unique=True, rows=rows, rw_opcodes=rw_opcodes)
+                   stream=stream, offsets=offsets, rw_state=rw_state, unique=True, rows=rows, rw_opcodes=rw_opcodes,
+                   ack_out=ack_out)
         torch.cuda.synchronize()
         got_all = elems.cpu().numpy()
+        vals_all = ack_out.cpu().numpy() if ack_out is not None else None
         what = f"{self.name} launch {self.launches} type {int(btype)} (rows)"
         for r, flat in ins.items():
             live = flat[:, 8] != 0
@@ -273,6 +295,15 @@ class Mirror:
                                rw_stride_bytes // self.g.sizes.op if rw is not None else 0)
             want = flat.copy()
             want[live] = e_in.view(np.uint8).reshape(n_batches, width, elem_size)[pos]
+            if vals_all is not None:   # the VAL callbacks over the row's results
+                vwant, after = val_callbacks(want[:nl], live[:nl], self.g.machine_id)
+                want[:nl] = after
+                vgot = vals_all[r * row_stride * 16:(r * row_stride + nl) * 16].reshape(nl, 16)
+                if not np.array_equal(vgot, vwant):
+                    bad = np.nonzero((vgot != vwant).any(axis=1))[0]
+                    pytest.fail(f"{what}: row {r} VALs differ at {len(bad)} positions, first {bad[:8]}: "
+                                f"dev {vgot[bad[0]].tolist()} want {vwant[bad[0]].tolist()}")
+                self.codes[(int(btype), "vals_sent", 0)] += int((vwant[:, 8] == int(L.Op.VAL)).sum())
             got = got_all[r * row_stride * elem_size:(r * row_stride + total) * elem_size].reshape(total, elem_size)
             grow = np.zeros_like(rws_)
             grow[pos] = got[live]

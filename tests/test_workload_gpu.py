@@ -81,6 +81,8 @@ def test_retry_round_mirrored(skew, hot):
     assert m.launches == steps * 5      # local, the peers' INVs (one launch each), their ACKs (one rows launch), VAL
     st = r.stats()
     assert st["committed"] > 0 and st["dropped"] == 0, st
+    # the ACK rows launch made the VALs of the writes it completed (checked against val_callbacks per launch)
+    assert (m.codes[(int(L.BatchType.acks), "vals_sent", 0)] > 0) == r.fused_vals, m.codes
     assert g.take_error_flags() == 0
     coalesced = m.codes[(int(L.BatchType.local_ops), "out9", int(L.Resp.PUT_COMPLETE))]
     assert (coalesced > 0) == bool(skew & 2), m.codes

@@ -3,9 +3,9 @@
 # loads (HKV_LF_FSPEC, HKV_PRE_FFILTER), and a same-box A/B of them with kernel stats.  tools/gpu_r05c.sh TAG
 tag=$1; out=gpurun_out/$tag; mkdir -p $out; export TMPDIR=/tmp
 T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
-timeout -k 10 400 $T tests/test_replica_group_gpu.py tests/test_rccl_gpu.py > $out/t_group.log 2>&1 || exit 11
+timeout -k 10 500 $T tests/test_replica_group_gpu.py tests/test_rccl_gpu.py tests/test_workload_gpu.py > $out/t_group.log 2>&1 || exit 11
 HKV_LF_FSPEC=1 HKV_PRE_FFILTER=1 timeout -k 10 400 $T tests/test_gpu_parity.py tests/test_workload_gpu.py > $out/t_spec.log 2>&1 || exit 12
-cfgs=("" "HKV_LF_FSPEC=1" "HKV_PRE_FFILTER=1" "HKV_LF_FSPEC=1 HKV_PRE_FFILTER=1")
+cfgs=("" "HKV_FUSED_VALS=0" "HKV_LF_FSPEC=1" "HKV_PRE_FFILTER=1" "HKV_LF_FSPEC=1 HKV_PRE_FFILTER=1")
 printf '%s\n' "${cfgs[@]}" > $out/configs.txt
 b="--steps 20 --warmup 5 --cpu-seconds 0 --host-api-seconds 0 --policy-steps 0"
 for k in "${!cfgs[@]}"; do

@@ -113,6 +113,7 @@ struct BatchArgs {
     int32_t cancel;              // k_local_pre undoes its tags (HKV_BATCH_PREPASS_CANCEL)
     uint8_t *ack_out;            // INV launches: each element's ACK (hkv_batch_desc.d_ack_out), or NULL
     uint32_t ack_out_size;
+    int32_t pre_notag;           // local direct path: k_local_pre sets no tags, k_local_fused reads F for every hit
     uint4 *ktab;                 // local direct path: the launch's PUT-key table (see kt_insert), or NULL
     uint32_t ktab_bits;          // log2 of its slots
     uint32_t ktag;               // the launch's 16-bit tag in the table's key words (1..65535)
@@ -1483,7 +1484,9 @@ constexpr int kPrePair = 4;
 // With the caller's PUT-key mirror the block also sums chk_term over the PUTs it read from it.
 // FF (HKV_PRE_FFILTER): the key's F word is loaded beside its log line, and an offer that an earlier
 // element's offer already beats (it landed first) is dropped with its tag store (the earlier one tags)
-template <int HEAD = kPreHead, bool H = false, bool T = false, bool FF = false>
+// NT (with k_local_fused's speculative F loads, HKV_LF_FSPEC): no seqlock-byte tags -- the fused pass
+// reads every hit's F word beside its log line and needs no mark of the keys that have one
+template <int HEAD = kPreHead, bool H = false, bool T = false, bool FF = false, bool NT = false>
 __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 {
     __shared__ uint64_t hk[kPreHash], gk[kPreHash];  // the block's PUT keys, the head's
@@ -1695,7 +1698,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
             const unsigned long long ov = ((unsigned long long)(~a.rtag0) << 32) | idx[k];
             if (FF && fwv[k] <= ov) continue;   // a smaller offer of this launch is in (and tags the entry)
             atomicMin(a.fw + fw_index(a, phys[k]), ov);
-            if ((uint8_t)(m0.w5 >> 16) != a.ltag && !HKV_DBG_ON(a, 32)) a.log[phys[k] + kEntryMetaOff + 4] = a.ltag;
+            if (!NT && (uint8_t)(m0.w5 >> 16) != a.ltag && !HKV_DBG_ON(a, 32)) a.log[phys[k] + kEntryMetaOff + 4] = a.ltag;
         }
     }
 }
@@ -1787,7 +1790,10 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         const uint64_t ek = line_key_meta(ln[k], m);
         const bool hit = ok[k] && ek == key[k];
         const bool tagged = hit && m_state(m) != kInvalid && (uint8_t)(m.w5 >> 16) == a.ltag;
-        const unsigned long long f = !(tagged && q == 0) ? ~0ull : FS ? fwv[k] : a.fw[fw_index(a, phys[k])];
+        // FS: every hit's F word came with its line; without tags (a.pre_notag) the word alone says
+        // whether this launch offered one (first_cand)
+        const bool want_f = FS && a.pre_notag ? hit && m_state(m) != kInvalid : tagged;
+        const unsigned long long f = !(want_f && q == 0) ? ~0ull : FS ? fwv[k] : a.fw[fw_index(a, phys[k])];
         if (T && q == 0) sft[te[k]] = hit && m_state(m) != kInvalid ? kt_find(a, key[k], kt[k]) : kNone;
         if (hit) sln[te[k] * 4 + q] = ln[k];
         if (q == 0) {
@@ -3646,6 +3652,8 @@ static void launch_local_pre(const BatchArgs &a, int64_t n, hipStream_t s)
     const dim3 grid((unsigned)((n + kPreElems - 1) / kPreElems));
     static const bool ff_env = getenv("HKV_PRE_FFILTER") && atoi(getenv("HKV_PRE_FFILTER")) != 0;
     if (a.ktab) hipLaunchKernelGGL((k_local_pre<kPreHead, false, true>), grid, dim3(256), 0, s, a);
+    else if (a.pre_notag && !a.cancel && !a.phys_hint && head == kPreHead)
+        hipLaunchKernelGGL((k_local_pre<kPreHead, false, false, false, true>), grid, dim3(256), 0, s, a);
     else if (ff_env && !a.phys_hint && head == kPreHead)
         hipLaunchKernelGGL((k_local_pre<kPreHead, false, false, true>), grid, dim3(256), 0, s, a);
     else if (a.phys_hint) hipLaunchKernelGGL((k_local_pre<kPreHead, true>), grid, dim3(256), 0, s, a);
@@ -3670,6 +3678,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.cancel = bl.stage == 3;
     a.ack_out = bl.type == kInvs || (bl.type == kAcks && bl.n_rows > 0) ? bl.ack_out : nullptr;
     a.ack_out_size = bl.ack_out_size;
+    a.pre_notag = 0;
     a.ktab = nullptr;
     a.ktab_bits = bl.ktab_bits;
     a.ktag = 1u + (bl.epoch - 1u) % 65535u;
@@ -3758,7 +3767,11 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     // HKV_PRE_TABLE=1: the prepass puts the launch's PUT keys into the key table instead of looking
     // them up (kt_insert); with the PUT-key mirror the mirror is checked by checksum
     static const bool table_env = getenv("HKV_PRE_TABLE") && atoi(getenv("HKV_PRE_TABLE")) != 0;
+    // HKV_PRE_NOTAG=1: the prepass sets no seqlock-byte tags and the fused pass loads every hit's F word
+    // beside its log line (HKV_LF_FSPEC's kernel)
+    static const bool notag_env = getenv("HKV_PRE_NOTAG") && atoi(getenv("HKV_PRE_NOTAG")) != 0;
     auto use_table = [&]() {
+        if (notag_env && local_direct && !a.phys_hint && !table_env) a.pre_notag = 1;
         if (!(table_env && local_direct && bl.ktab && !a.phys_hint)) return;
         a.ktab = reinterpret_cast<uint4 *>(bl.ktab);
         if (a.pkeys) a.pchk = bl.pchk;
@@ -3802,7 +3815,9 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         static const int lfp_env = getenv("HKV_LF_PAIR") ? atoi(getenv("HKV_LF_PAIR")) : 2;
         // HKV_LF_FSPEC=1: every hit loads its key's F word beside the log line (no dependent load after it)
         static const bool fspec_env = getenv("HKV_LF_FSPEC") && atoi(getenv("HKV_LF_FSPEC")) != 0;
-        if (fspec_env && !a.ktab && !a.phys_hint && lfp_env == 2)
+        if (a.pre_notag)
+            hipLaunchKernelGGL((k_local_fused<2, false, false, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
+        else if (fspec_env && !a.ktab && !a.phys_hint && lfp_env == 2)
             hipLaunchKernelGGL((k_local_fused<2, false, false, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
         else if (a.ktab)
             hipLaunchKernelGGL((k_local_fused<2, false, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);

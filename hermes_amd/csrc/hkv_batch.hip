@@ -3767,9 +3767,11 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     // HKV_PRE_TABLE=1: the prepass puts the launch's PUT keys into the key table instead of looking
     // them up (kt_insert); with the PUT-key mirror the mirror is checked by checksum
     static const bool table_env = getenv("HKV_PRE_TABLE") && atoi(getenv("HKV_PRE_TABLE")) != 0;
-    // HKV_PRE_NOTAG=1: the prepass sets no seqlock-byte tags and the fused pass loads every hit's F word
-    // beside its log line (HKV_LF_FSPEC's kernel)
-    static const bool notag_env = getenv("HKV_PRE_NOTAG") && atoi(getenv("HKV_PRE_NOTAG")) != 0;
+    // The prepass sets no seqlock-byte tags and the fused pass loads every hit's F word beside its log
+    // line (round 5, the default; HKV_PRE_NOTAG=0: tags, and F loaded after the line for tagged keys
+    // only). Same box, 3 x 20 steps each (gpurun_out/r05e): 4.355-4.359 -> 4.378-4.393 G ops/s, prepass
+    // 78.1 -> 73.8 us, fused pass level (265.7 / 266.7 us)
+    static const bool notag_env = !getenv("HKV_PRE_NOTAG") || atoi(getenv("HKV_PRE_NOTAG")) != 0;
     auto use_table = [&]() {
         if (notag_env && local_direct && !a.phys_hint && !table_env) a.pre_notag = 1;
         if (!(table_env && local_direct && bl.ktab && !a.phys_hint)) return;

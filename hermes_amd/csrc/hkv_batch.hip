@@ -1881,6 +1881,256 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
     }
 }
 
+// k_local_fused, software-pipelined (HKV_LF_PIPE; the default path only: no tags, F loaded beside every
+// hit's line, no hints, no key table, no PUT-key mirror). A persistent wave walks its chunks of 32
+// elements (chunk blockIdx.x, + gridDim.x, ...) and keeps the next chunk's loads in flight while it
+// resolves the current one: per iteration
+//   wait for chunk X's log lines and F words (issued last iteration), stage X in LDS;
+//   wait for chunk Y's ops, issue Y's bucket loads;
+//   resolve X on its LDS copies and write its ops back (Y's buckets in flight meanwhile);
+//   wait for Y's buckets, issue Y's log line + F loads; issue chunk Z's op loads; X := Y, Y := Z.
+// The waits are in issue order, so none of them waits for a younger load. Each element's result is
+// k_local_fused's: elements are independent once F is final, whatever chunk order a wave takes.
+struct LfChunk {
+    uint4 op[2];
+    uint64_t key[2];
+    bool probe[2], live[2];
+};
+
+__device__ __forceinline__ void lf_load_ops(const BatchArgs &a, int64_t i0, int q, int tid, LfChunk &c)
+{
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int64_t i = i0 + k * 16 + (tid >> 2);
+        c.live[k] = i0 >= 0 && i < a.n;
+        c.op[k] = make_uint4(0u, 0u, 0u, 0u);
+        if (c.live[k]) {
+            const uint8_t *xg = a.elems + i * 56 + 16 * q;
+            U64x2 p{0, 0};
+            if (a.patch) p = *reinterpret_cast<const U64x2 *>(a.patch + i * 16);
+            if (q < 3) {
+                c.op[k] = *reinterpret_cast<const uint4 *>(xg);
+            } else {
+                const uint64_t t = *reinterpret_cast<const uint64_t *>(xg);
+                c.op[k].x = (uint32_t)t;
+                c.op[k].y = (uint32_t)(t >> 32);
+            }
+            if (patch_valid(p.b)) c.op[k] = patch_chunk(c.op[k], q, p.a, p.b);
+        }
+    }
+}
+
+__device__ __forceinline__ void lf_keys(const BatchArgs &a, int64_t i0, int tid, LfChunk &c)
+{
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        c.key[k] = (uint64_t)(uint32_t)__shfl((int)c.op[k].x, 0, 4) | ((uint64_t)(uint32_t)__shfl((int)c.op[k].y, 0, 4) << 32);
+        const uint32_t h0 = (uint32_t)__shfl((int)c.op[k].z, 0, 4);
+        c.probe[k] = c.live[k] && in_count(a, (uint32_t)(i0 + k * 16 + (tid >> 2))) &&
+                     !skip_elem_os(kLocal, (uint8_t)h0, (uint8_t)(h0 >> 8));
+    }
+}
+
+// The LDS of one resolving chunk (k_local_fused_pp, k_local_fused_2c)
+struct LfLds {
+    uint4 sops[32 * 4];
+    uint4 sln[32 * 4];
+    unsigned long long sfw[32];
+    uint32_t sent[32];
+    uint8_t sprb[32];
+    uint32_t sdef[32];
+    uint32_t ndef;
+};
+
+// Buckets of a chunk (16 B per lane) -> its log lines and F words (lookup_pair_f's second half)
+__device__ __forceinline__ void lf_lines(const BatchArgs &a, const LfChunk &c, const uint4 *v, int q, int gbase,
+                                         bool *ok, uint64_t *phys, uint4 *ln, unsigned long long *fwv)
+{
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint64_t s0 = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
+        const uint64_t s1 = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
+        const uint32_t tag = (uint32_t)(c.key[k] >> 48);
+        const bool mt0 = c.probe[k] && (s0 & 1u) && ((uint32_t)(s0 >> 1) & 0x7FFFFFu) == tag;
+        const bool mt1 = c.probe[k] && (s1 & 1u) && ((uint32_t)(s1 >> 1) & 0x7FFFFFu) == tag;
+        const uint32_t g0 = (uint32_t)(__ballot(mt0) >> gbase) & 0xFu;
+        const uint32_t g1 = (uint32_t)(__ballot(mt1) >> gbase) & 0xFu;
+        uint32_t o = 0;
+#pragma unroll
+        for (int l = 0; l < 4; ++l) o |= ((g0 >> l) & 1u) << (2 * l) | ((g1 >> l) & 1u) << (2 * l + 1);
+        const int first = o ? __ffs(o) - 1 : 0;
+        const uint64_t off = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
+        ok[k] = c.probe[k] && o && a.g.log_head - off < a.g.log_cap;
+        phys[k] = off & a.g.log_mask;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        ln[k] = ok[k] ? reinterpret_cast<const uint4 *>(a.log + phys[k])[q] : make_uint4(0u, 0u, 0u, 0u);
+        fwv[k] = ok[k] && q == 0 ? a.fw[fw_index(a, phys[k])] : ~0ull;
+    }
+}
+
+__device__ __forceinline__ void lf_buckets(const BatchArgs &a, const LfChunk &c, int q, uint4 *v)
+{
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        v[k] = c.probe[k] ? reinterpret_cast<const uint4 *>(a.index + ((c.key[k] & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u)[q]
+                          : make_uint4(0u, 0u, 0u, 0u);
+}
+
+// one chunk staged in LDS (the caller has reset L.ndef and synchronises after)
+__device__ __forceinline__ void lf_stage(const BatchArgs &a, LfLds &L, const LfChunk &c, const bool *ok,
+                                         const uint64_t *phys, const uint4 *ln, const unsigned long long *fwv, int q,
+                                         int tid)
+{
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int te = k * 16 + (tid >> 2);
+        Meta m;
+        const uint64_t ek = line_key_meta(ln[k], m);
+        const bool hit = ok[k] && ek == c.key[k];
+        L.sops[te * 4 + q] = c.op[k];
+        if (hit) L.sln[te * 4 + q] = ln[k];
+        if (q == 0) {
+            L.sfw[te] = hit && m_state(m) != kInvalid ? fwv[k] : ~0ull;
+            L.sent[te] = hit ? (uint32_t)(phys[k] / a.g.entry_unit) : kNone;
+            L.sprb[te] = c.probe[k];
+        }
+    }
+}
+
+// k_local_fused's rules for one staged chunk (default path), then its ops back (between two barriers)
+__device__ __forceinline__ void lf_resolve(const BatchArgs &a, LfLds &L, const LfChunk &c, int64_t i0, int q, int tid)
+{
+    if (tid < 32 && i0 + tid < a.n) {
+        const int64_t i = i0 + tid;
+        uint8_t *x = reinterpret_cast<uint8_t *>(&L.sops[tid * 4]);
+        uint8_t *ent = reinterpret_cast<uint8_t *>(&L.sln[tid * 4]);
+        const uint32_t e = L.sent[tid];
+        uint8_t st = kStDone;
+        if (e != kNone) {
+            Ctx cx = make_ctx(a);
+            const uint8_t bidx = (uint8_t)((uint32_t)i % (uint32_t)a.stride);
+            Meta m;
+            meta_load(ent, m);
+            const bool wm = would_mutate(kLocal, x, m, cx);
+            if (m_state(m) == kInvalid) {
+                if (wm) {
+                    const uint64_t ph = phys_of(a, e);
+                    offer(a.fw + fw_index(a, ph), a.rtag0, (uint32_t)i);
+                    if ((uint8_t)(m.w5 >> 16) != a.ltag) a.log[ph + kEntryMetaOff + 4] = a.ltag;
+                }
+                st = kStDefer;
+                L.sdef[atomicAdd(&L.ndef, 1u)] = (uint32_t)i;
+            } else {
+                const uint32_t f = first_cand(L.sfw[tid], a.rtag0);
+                if (wm && (f == kNone || f > (uint32_t)i) && a.error_flags) atomicOr(a.error_flags, 4u);
+                if ((uint32_t)i == f) {
+                    apply_to_shadow<kLocal, 31>(a, x, (uint32_t)i, ent);
+                    st = kStCommit;
+                } else {
+                    const Meta m0 = f != kNone && (uint32_t)i > f ? after_first<kLocal>(a, m, f, 1) : m;
+                    Meta tm = m0;
+                    dispatch<31>(kLocal, x, ent, bidx, tm, cx);
+                    if (a.error_flags && !meta_equal(tm, m0)) atomicOr(a.error_flags, 1u);
+                }
+            }
+        } else if (L.sprb[tid]) {
+            x[9] = kMiss;
+        }
+        if (a.opc && L.sprb[tid] && x[8] == kOpPut && a.opc[i] != kOpPut && a.error_flags) atomicOr(a.error_flags, 8u);
+        a.ent[i] = e;
+        a.st[i] = st;
+        if (st != kStDefer) note_state(a, i, x);
+    }
+    __syncthreads();
+    if (L.ndef && tid == 0) {
+        const uint32_t base = atomicAdd(&a.ctr[kCtrDefer], L.ndef);
+        for (uint32_t j = 0; j < L.ndef; ++j) a.fbl[base + j] = L.sdef[j];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (!c.live[k]) continue;
+        const int te = k * 16 + (tid >> 2);
+        uint8_t *xg = a.elems + (i0 + te) * 56 + 16 * q;
+        const uint4 w = L.sops[te * 4 + q];
+        if (q < 3) *reinterpret_cast<uint4 *>(xg) = w;
+        else *reinterpret_cast<uint64_t *>(xg) = (uint64_t)w.x | ((uint64_t)w.y << 32);
+    }
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_local_fused_pp(BatchArgs a, int64_t n_chunks)
+{
+    __shared__ LfLds L;
+    const int tid = threadIdx.x, q = tid & 3, gbase = tid & ~3;
+    const int64_t stride = gridDim.x;
+    int64_t cx = blockIdx.x;          // chunk X: its lines and F words in flight
+    if (cx >= n_chunks) return;
+    LfChunk X, Y;
+    uint4 lnx[2], vy[2];
+    unsigned long long fwx[2];
+    bool okx[2];
+    uint64_t physx[2];
+    // prologue: X's ops, buckets and lines; Y's ops
+    lf_load_ops(a, cx * 32, q, tid, X);
+    lf_keys(a, cx * 32, tid, X);
+    lf_buckets(a, X, q, vy);
+    lf_lines(a, X, vy, q, gbase, okx, physx, lnx, fwx);
+    int64_t cy = cx + stride;
+    lf_load_ops(a, cy < n_chunks ? cy * 32 : -1, q, tid, Y);
+    for (;;) {
+        if (tid == 0) L.ndef = 0;
+        lf_stage(a, L, X, okx, physx, lnx, fwx, q, tid);
+        const bool more = cy < n_chunks;
+        if (more) {   // Y's keys and buckets: in flight while X resolves
+            lf_keys(a, cy * 32, tid, Y);
+            lf_buckets(a, Y, q, vy);
+        }
+        __syncthreads();
+        lf_resolve(a, L, X, cx * 32, q, tid);
+        if (!more) break;
+        lf_lines(a, Y, vy, q, gbase, okx, physx, lnx, fwx);
+        X = Y;
+        cx = cy;
+        cy = cx + stride;
+        lf_load_ops(a, cy < n_chunks ? cy * 32 : -1, q, tid, Y);
+        __syncthreads();   // X's LDS copies are free again
+    }
+}
+
+// k_local_fused with two chunks per wave (HKV_LF_2C): both chunks' loads in flight together, then each
+// staged and resolved through the same 32-element LDS (so LDS stays that of one chunk)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_local_fused_2c(BatchArgs a)
+{
+    __shared__ LfLds L;
+    const int tid = threadIdx.x, q = tid & 3, gbase = tid & ~3;
+    const int64_t c0 = (int64_t)blockIdx.x * 2;
+    LfChunk X, Y;
+    uint4 vx[2], vy[2], lnx[2], lny[2];
+    unsigned long long fwx[2], fwy[2];
+    bool okx[2], oky[2];
+    uint64_t physx[2], physy[2];
+    const int64_t nch = (a.n + 31) / 32;
+    lf_load_ops(a, c0 * 32, q, tid, X);
+    lf_load_ops(a, c0 + 1 < nch ? (c0 + 1) * 32 : -1, q, tid, Y);
+    lf_keys(a, c0 * 32, tid, X);
+    lf_keys(a, (c0 + 1) * 32, tid, Y);
+    lf_buckets(a, X, q, vx);
+    lf_buckets(a, Y, q, vy);
+    lf_lines(a, X, vx, q, gbase, okx, physx, lnx, fwx);
+    lf_lines(a, Y, vy, q, gbase, oky, physy, lny, fwy);
+    if (tid == 0) L.ndef = 0;
+    lf_stage(a, L, X, okx, physx, lnx, fwx, q, tid);
+    __syncthreads();
+    lf_resolve(a, L, X, c0 * 32, q, tid);
+    if (c0 + 1 >= nch) return;
+    __syncthreads();
+    if (tid == 0) L.ndef = 0;
+    lf_stage(a, L, Y, oky, physy, lny, fwy, q, tid);
+    __syncthreads();
+    lf_resolve(a, L, Y, (c0 + 1) * 32, q, tid);
+}
+
 // ------------------------------------------------------------------ launches with unique keys
 // HKV_BATCH_UNIQUE: no key appears twice among the launch's elements, so every element is its key's
 // only one and sees S_0 in any serial order: after k_lookup's lookup (four lanes per element, two
@@ -3817,7 +4067,23 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         static const int lfp_env = getenv("HKV_LF_PAIR") ? atoi(getenv("HKV_LF_PAIR")) : 2;
         // HKV_LF_FSPEC=1: every hit loads its key's F word beside the log line (no dependent load after it)
         static const bool fspec_env = getenv("HKV_LF_FSPEC") && atoi(getenv("HKV_LF_FSPEC")) != 0;
-        if (a.pre_notag)
+        // HKV_LF_PIPE=1: the software-pipelined persistent fused pass (k_local_fused_pp), HKV_LF_PIPE_WAVES
+        // waves per CU (default 32)
+        static const bool pipe_env = getenv("HKV_LF_PIPE") && atoi(getenv("HKV_LF_PIPE")) != 0;
+        static const int pipe_waves = getenv("HKV_LF_PIPE_WAVES") ? std::max(1, atoi(getenv("HKV_LF_PIPE_WAVES"))) : 32;
+        static const bool twoc_env = getenv("HKV_LF_2C") && atoi(getenv("HKV_LF_2C")) != 0;
+        if (a.pre_notag && twoc_env && !a.pkeys) {
+            hipLaunchKernelGGL(k_local_fused_2c, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, a);
+        } else if (a.pre_notag && pipe_env && !a.pkeys) {
+            const int64_t chunks = (n + 31) / 32;
+            static const int cus = [] {
+                int dev = 0, c = 256;
+                if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+                return c;
+            }();
+            const int64_t g = std::min<int64_t>(chunks, (int64_t)cus * pipe_waves);
+            hipLaunchKernelGGL(k_local_fused_pp, dim3((unsigned)g), dim3(64), 0, s, a, chunks);
+        } else if (a.pre_notag)
             hipLaunchKernelGGL((k_local_fused<2, false, false, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
         else if (fspec_env && !a.ktab && !a.phys_hint && lfp_env == 2)
             hipLaunchKernelGGL((k_local_fused<2, false, false, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);

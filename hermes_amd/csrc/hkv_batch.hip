@@ -114,11 +114,6 @@ struct BatchArgs {
     uint8_t *ack_out;            // INV launches: each element's ACK (hkv_batch_desc.d_ack_out), or NULL
     uint32_t ack_out_size;
     int32_t pre_notag;           // local direct path: k_local_pre sets no tags, k_local_fused reads F for every hit
-    uint4 *ktab;                 // local direct path: the launch's PUT-key table (see kt_insert), or NULL
-    uint32_t ktab_bits;          // log2 of its slots
-    uint32_t ktag;               // the launch's 16-bit tag in the table's key words (1..65535)
-    uint32_t kepoch;             // the launch's epoch in the table's index words
-    unsigned long long *pchk;    // [2][kChkStripes] PUT-mirror checksums (prepass, fused pass), or NULL
 };
 
 // Rounds after round 0 per batch type: how often a hot key usually mutates in one launch beyond
@@ -291,110 +286,6 @@ __device__ __forceinline__ void offer(unsigned long long *f, uint32_t rtag, uint
 {
     const unsigned long long v = ((unsigned long long)(~rtag) << 32) | i;
     if (v < __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(f, v);
-}
-
-// ---- the launch's PUT-key table (local direct path, HKV_PRE_TABLE). k_local_pre puts every key that
-// has a PUT in the launch into an open-addressed table of 2^B 16-byte slots, with the key's first PUT,
-// instead of looking the key up in the index and offering its F word (two random lines, an atomic
-// and a seqlock-byte store into a third); k_local_fused reads the key's slot beside its bucket and
-// takes F from it when the key's S_0 lets a PUT mutate (for a key that is not INVALID, F is its first
-// PUT or nothing, see the direct path's section comment). A slot is
-//   key word:   rest << B | d << 16 | tag,   h = kt_mix(key) (a bijection), home = h >> (64 - B),
-//               rest = the low 64 - B bits of h, d = the slot's distance from home (< kKtMaxD), tag =
-//               the launch's 16-bit tag: (home, rest) is h, so the word names its key exactly;
-//   index word: epoch << 32 | ~i, i the key's first PUT (atomicMax: the launch's words outrank every
-//               earlier launch's, and within it the smallest i wins).
-// A word with another tag is an empty slot, so nothing is cleared between launches; the runtime
-// zeroes the table when the tag wraps (every 65535 launches). Slots are claimed by atomicCAS and
-// never released within a launch, so every inserter of a key reaches the same slot. A key that finds
-// kKtMaxD slots taken takes the lookup-and-tag path instead (k_local_fused reads both).
-constexpr uint32_t kKtMaxD = 32;
-constexpr int kChkStripes = 256;
-
-__device__ __forceinline__ uint64_t kt_mix(uint64_t k)
-{
-    k ^= k >> 33;
-    k *= 0xFF51AFD7ED558CCDull;
-    k ^= k >> 29;
-    k *= 0xC4CEB9FE1A85EC53ull;
-    k ^= k >> 32;
-    return k;
-}
-__device__ __forceinline__ uint32_t kt_home(const BatchArgs &a, uint64_t key)
-{
-    return (uint32_t)(kt_mix(key) >> (64 - a.ktab_bits));
-}
-__device__ __forceinline__ unsigned long long kt_want(const BatchArgs &a, uint64_t key, uint32_t d)
-{
-    const uint64_t h = kt_mix(key);
-    const uint64_t rest = h & ((1ull << (64 - a.ktab_bits)) - 1ull);
-    return (rest << a.ktab_bits) | ((unsigned long long)d << 16) | a.ktag;
-}
-__device__ __forceinline__ unsigned long long kt_lo(const uint4 &v) { return (unsigned long long)v.x | ((unsigned long long)v.y << 32); }
-__device__ __forceinline__ unsigned long long kt_hi(const uint4 &v) { return (unsigned long long)v.z | ((unsigned long long)v.w << 32); }
-
-// key -> its slot, with i as a candidate first PUT; false when kKtMaxD slots from home are taken by
-// other keys. The plain loads may be stale (another XCD's claim): a slot's key word changes at most
-// once per launch (from another tag to its key), so a stale one can only read as empty, and the CAS
-// then returns the real word; an index word only grows, so a stale one filters nothing wrongly.
-__device__ __forceinline__ bool kt_insert(const BatchArgs &a, uint64_t key, uint32_t i)
-{
-    const uint32_t mask = (1u << a.ktab_bits) - 1u, home = kt_home(a, key);
-    const unsigned long long iv = ((unsigned long long)a.kepoch << 32) | (0xFFFFFFFFu - i);
-    for (uint32_t d = 0; d < kKtMaxD; ++d) {
-        uint4 *slot = a.ktab + ((home + d) & mask);
-        unsigned long long *kw = reinterpret_cast<unsigned long long *>(slot);
-        const unsigned long long want = kt_want(a, key, d);
-        const uint4 v = *slot;
-        unsigned long long cur = kt_lo(v), idx = kt_hi(v);
-        for (;;) {
-            if ((uint32_t)(cur & 0xFFFFu) != a.ktag) {   // empty in this launch: claim it
-                const unsigned long long old = atomicCAS(kw, cur, want);
-                if (old == cur) {
-                    atomicMax(kw + 1, iv);
-                    return true;
-                }
-                cur = old;
-                idx = 0;
-                continue;
-            }
-            if (cur == want) {
-                if (iv > idx) atomicMax(kw + 1, iv);
-                return true;
-            }
-            break;   // another key's slot
-        }
-    }
-    return false;
-}
-
-// The key's first PUT from its table slot (v: the home slot, loaded beside the bucket), kNone when
-// the key has no PUT in the table (or took the lookup-and-tag path)
-__device__ __forceinline__ uint32_t kt_find(const BatchArgs &a, uint64_t key, uint4 v)
-{
-    const uint32_t mask = (1u << a.ktab_bits) - 1u, home = kt_home(a, key);
-    for (uint32_t d = 0; d < kKtMaxD; ++d) {
-        if (d) v = a.ktab[(home + d) & mask];
-        const unsigned long long cur = kt_lo(v);
-        if ((uint32_t)(cur & 0xFFFFu) != a.ktag) return kNone;
-        if (cur == kt_want(a, key, d)) {
-            const unsigned long long idx = kt_hi(v);
-            return (uint32_t)(idx >> 32) == a.kepoch ? 0xFFFFFFFFu - (uint32_t)idx : kNone;
-        }
-    }
-    return kNone;
-}
-
-// checksum term of a PUT (key, element): the prepass sums it over the PUTs the caller's mirror names,
-// the fused pass over the PUTs it sees; k_commit_w compares the sums (error bit 3)
-__device__ __forceinline__ unsigned long long chk_term(uint64_t key, uint32_t i)
-{
-    return kt_mix(key ^ ((uint64_t)i * 0x9E3779B97F4A7C15ull)) | 1ull;
-}
-__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v)
-{
-    for (int o = 32; o > 0; o >>= 1) v += (unsigned long long)__shfl_xor((long long)v, o, 64);
-    return v;
 }
 
 // Wave-aggregated atomicAdd(&arr[j], 1): one atomic per distinct j in the wave; each active lane
@@ -1479,29 +1370,20 @@ constexpr int kPrePair = 4;
 #else
 #define HKV_PRE_ATTR
 #endif
-// T (the PUT-key table, HKV_PRE_TABLE): each distinct key goes into the launch's key table (kt_insert)
-// instead of being looked up, offered and tagged; only keys the table cannot place take that path.
-// With the caller's PUT-key mirror the block also sums chk_term over the PUTs it read from it.
-// FF (HKV_PRE_FFILTER): the key's F word is loaded beside its log line, and an offer that an earlier
-// element's offer already beats (it landed first) is dropped with its tag store (the earlier one tags)
-// NT (with k_local_fused's speculative F loads, HKV_LF_FSPEC): no seqlock-byte tags -- the fused pass
-// reads every hit's F word beside its log line and needs no mark of the keys that have one
-template <int HEAD = kPreHead, bool H = false, bool T = false, bool FF = false, bool NT = false>
+// NT (the default, with k_local_fused's F loads beside every hit's line): no seqlock-byte tags -- the
+// fused pass reads every hit's F word and needs no mark of the keys that have one
+template <int HEAD = kPreHead, bool H = false, bool NT = false>
 __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 {
     __shared__ uint64_t hk[kPreHash], gk[kPreHash];  // the block's PUT keys, the head's
     __shared__ uint32_t hv[kPreHash];
     __shared__ uint32_t dl[kPreElems];               // distinct keys: slots of hk, or ~index (no slot)
-    __shared__ uint8_t lk[T ? kPreElems : 1];        // T: 1 = the key takes the lookup path
     __shared__ uint32_t nd;
     const int tid = threadIdx.x, q = tid & 3, gbase = (tid & 63) & ~3;
-    const bool table = T && !a.cancel;   // a cancel undoes tags: every key takes the lookup path
     if (tid == 0) {
         nd = 0;
         if (blockIdx.x == 0) a.ctr[kCtrDefer] = 0;
     }
-    if (T && a.cancel && a.pchk && blockIdx.x == 0)   // no fused pass follows: the sums start over
-        for (int j = tid; j < 2 * kChkStripes; j += 256) a.pchk[j] = 0;
     for (int j = tid; j < kPreHash; j += 256) {
         hk[j] = ~0ull;
         gk[j] = ~0ull;
@@ -1596,7 +1478,6 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
         return;
     }
     __syncthreads();
-    unsigned long long chk = 0;
 #pragma unroll
     for (int k = 0; k < kAllK; ++k) {
         const bool own = k < kOwnK;
@@ -1606,7 +1487,6 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
         bool created;
         uint32_t sl;
         if (own) {
-            if (T && a.pkeys) chk += chk_term(key, i);
             const bool in_table = pre_insert(hk, hv, key, i, created, sl);
             if (!in_table || created) {  // a key's first arrival lists it (no slot: it offers for itself)
                 dl[atomicAdd(&nd, 1u)] = in_table ? sl : ~i;
@@ -1615,51 +1495,20 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
             pre_insert_key(gk, key);
         }
     }
-    if (T && a.pkeys && !a.cancel) {   // the block's sum of the mirror's PUTs, one atomic per wave
-        chk = wave_sum64(chk);
-        if ((tid & 63) == 0 && chk) atomicAdd(a.pchk + (blockIdx.x % kChkStripes), chk);
-    }
     __syncthreads();
     const Ctx c = make_ctx(a);
     const uint64_t hput[2] = {0, (uint64_t)kOpPut};
     const uint32_t cnt = HKV_DBG_ON(a, 2) ? 0 : nd;
-    if (table) {
-        // one lane per distinct key: the head's keys are dropped (an earlier block holds their first
-        // PUT), the others go into the key table; those it cannot place are looked up below
-        for (uint32_t j = tid; j < cnt; j += 256) {
-            const uint32_t d = dl[j];
-            const uint32_t idx = d < (uint32_t)kPreHash ? hv[d] : ~d;
-            const uint64_t key = d < (uint32_t)kPreHash ? hk[d] : elem_key(a, (int64_t)idx);
-            bool lookup = false;
-            bool head = false;
-            if (head_end > 0 && key != ~0ull) {
-                uint32_t sl = pre_slot(key);
-                for (int n = 0; n < kPreHash; ++n) {
-                    const uint64_t g = gk[sl];
-                    if (g == ~0ull) break;
-                    if (g == key) {
-                        head = true;
-                        break;
-                    }
-                    sl = (sl + 1) & (kPreHash - 1);
-                }
-            }
-            if (!head) lookup = !kt_insert(a, key, idx);
-            lk[j] = lookup ? 1 : 0;
-        }
-        __syncthreads();
-    }
     for (uint32_t base = 0; base < cnt; base += 64 * kPrePair) {
         uint64_t key[kPrePair];
         bool probe[kPrePair], ok[kPrePair];
         uint32_t idx[kPrePair];
         uint64_t phys[kPrePair];
         uint4 ln[kPrePair];
-        unsigned long long fwv[kPrePair];
 #pragma unroll
         for (int k = 0; k < kPrePair; ++k) {
             const uint32_t j = base + k * 64 + (tid >> 2);
-            probe[k] = j < cnt && (!table || lk[j]);
+            probe[k] = j < cnt;
             const uint32_t d = probe[k] ? dl[j] : 0u;
             idx[k] = !probe[k] ? kNone : d < (uint32_t)kPreHash ? hv[d] : ~d;
             key[k] = !probe[k] ? 0 : d < (uint32_t)kPreHash ? hk[d] : elem_key(a, (int64_t)idx[k]);
@@ -1682,8 +1531,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
             for (int k = 0; k < kPrePair; ++k) gi[k] = probe[k] ? (int64_t)idx[k] : 0;
             lookup_hinted<kPrePair>(a, gi, key, probe, q, gbase, ok, phys, ln);
         } else {
-            if (FF) lookup_pair_f<kPrePair>(a, key, probe, q, gbase, ok, phys, ln, fwv);
-            else lookup_pair<kPrePair>(a, key, probe, q, gbase, ok, phys, ln);
+            lookup_pair<kPrePair>(a, key, probe, q, gbase, ok, phys, ln);
         }
 #pragma unroll
         for (int k = 0; k < kPrePair; ++k) {
@@ -1695,9 +1543,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
                 continue;
             }
             if (!would_mutate(kLocal, reinterpret_cast<const uint8_t *>(hput), m0, c) || HKV_DBG_ON(a, 1)) continue;
-            const unsigned long long ov = ((unsigned long long)(~a.rtag0) << 32) | idx[k];
-            if (FF && fwv[k] <= ov) continue;   // a smaller offer of this launch is in (and tags the entry)
-            atomicMin(a.fw + fw_index(a, phys[k]), ov);
+            atomicMin(a.fw + fw_index(a, phys[k]), ((unsigned long long)(~a.rtag0) << 32) | idx[k]);
             if (!NT && (uint8_t)(m0.w5 >> 16) != a.ltag && !HKV_DBG_ON(a, 32)) a.log[phys[k] + kEntryMetaOff + 4] = a.ltag;
         }
     }
@@ -1707,18 +1553,15 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 // nothing shared beyond it. The lookup runs four lanes per element (each lane holds 16 B of the op
 // and of the log line); the wave-private LDS copies of op and entry are then resolved one element
 // per lane, so the exec code's branches are paid once per 32 elements; the ops go back whole.
-// T (HKV_PRE_TABLE): each key's first PUT comes from the launch's key table (its home slot loaded
-// beside the bucket); the tag-and-F-word path remains for the keys the table could not place. With
-// the caller's PUT-key mirror, the mirror is checked by a checksum of the PUTs (k_commit_w compares)
-// instead of element by element.
-template <int P, bool H = false, bool T = false, bool FS = false>
+// FS (the default): every hit's F word is loaded beside its log line (with the prepass's tags off,
+// a.pre_notag, the word alone says whether the key has a first candidate)
+template <int P, bool H = false, bool FS = false>
 __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
 {
     constexpr int E = 16 * P;   // elements per wave: P per lane group
     __shared__ uint4 sops[E * 4];   // 64 B per op (56 used)
     __shared__ uint4 sln[E * 4];
     __shared__ unsigned long long sfw[E];
-    __shared__ uint32_t sft[T ? E : 1];   // T: the key's first PUT from the key table (kNone: none)
     __shared__ uint32_t sent[E];     // entry id of a hit, kNone otherwise
     __shared__ uint8_t sprb[E];      // probed (not skipped)
     __shared__ uint32_t sdef[E];
@@ -1751,7 +1594,7 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
                 op[k].y = (uint32_t)(t >> 32);
             }
             if (patch_valid(p.b)) op[k] = patch_chunk(op[k], q, p.a, p.b);
-            if (!T && a.pkeys && q == 0) {   // the mirrors k_local_pre worked from, checked below
+            if (a.pkeys && q == 0) {   // the mirrors k_local_pre worked from, checked below
                 spk[te[k]] = a.pkeys[i];
                 sps[te[k]] = a.state_out[i];
             }
@@ -1767,11 +1610,6 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         if (live[k])
             probe[k] = in_count(a, (uint32_t)(i0 + te[k])) && !skip_elem_os(kLocal, (uint8_t)h0, (uint8_t)(h0 >> 8));
     }
-    // T: the key's home slot in the key table, in flight beside the bucket (no dependence between them)
-    uint4 kt[P];
-#pragma unroll
-    for (int k = 0; k < P; ++k)
-        kt[k] = T && probe[k] && q == 0 ? a.ktab[kt_home(a, key[k])] : make_uint4(0u, 0u, 0u, 0u);
     unsigned long long fwv[P];   // FS: every hit's F word, loaded beside its log line
     if (H) {   // located entries (hkv_batch_desc.d_phys)
         int64_t gi[P];
@@ -1794,7 +1632,6 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         // whether this launch offered one (first_cand)
         const bool want_f = FS && a.pre_notag ? hit && m_state(m) != kInvalid : tagged;
         const unsigned long long f = !(want_f && q == 0) ? ~0ull : FS ? fwv[k] : a.fw[fw_index(a, phys[k])];
-        if (T && q == 0) sft[te[k]] = hit && m_state(m) != kInvalid ? kt_find(a, key[k], kt[k]) : kNone;
         if (hit) sln[te[k] * 4 + q] = ln[k];
         if (q == 0) {
             sfw[te[k]] = f;
@@ -1803,17 +1640,15 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         }
     }
     __syncthreads();
-    unsigned long long chk = 0;
     if (tid < E && i0 + tid < a.n) {
         const int64_t i = i0 + tid;
         uint8_t *x = reinterpret_cast<uint8_t *>(&sops[tid * 4]);
         uint8_t *ent = reinterpret_cast<uint8_t *>(&sln[tid * 4]);
         const uint32_t e = sent[tid];
         uint8_t st = kStDone;
-        if (T && a.pkeys && sprb[tid] && x[8] == kOpPut) chk = chk_term(ld64(x), (uint32_t)i);
         // the mirrors k_local_pre worked from must describe this element: the PUT-key word, and for
         // a PUT the state the skip rule was applied to
-        if (!T && a.pkeys && a.error_flags &&
+        if (a.pkeys && a.error_flags &&
             (spk[tid] != (x[8] == kOpPut ? ld64(x) : ~0ull) || (x[8] == kOpPut && sps[tid] != x[9])))
             atomicOr(a.error_flags, 8u);
         if (e != kNone) {
@@ -1832,11 +1667,7 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
                 st = kStDefer;
                 sdef[atomicAdd(&ndef, 1u)] = (uint32_t)i;
             } else {
-                uint32_t f = first_cand(sfw[tid], a.rtag0);
-                if (T && sft[tid] < f) {   // the key's first PUT, F when a PUT mutates S_0
-                    const uint64_t hput[2] = {0, (uint64_t)kOpPut};
-                    if (would_mutate(kLocal, reinterpret_cast<const uint8_t *>(hput), m, c)) f = sft[tid];
-                }
+                const uint32_t f = first_cand(sfw[tid], a.rtag0);
                 // a mutating element must have offered itself in k_local_pre
                 if (wm && (f == kNone || f > (uint32_t)i) && a.error_flags) atomicOr(a.error_flags, 4u);
                 if ((uint32_t)i == f) {
@@ -1853,17 +1684,11 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         } else if (sprb[tid]) {
             x[9] = kMiss;
         }
-        // k_local_pre read only the PUTs the caller's opcode mirror names (with the PUT-key mirror and the
-        // key table: the checksum below)
-        if (!(T && a.pkeys) && a.opc && sprb[tid] && x[8] == kOpPut && a.opc[i] != kOpPut && a.error_flags)
-            atomicOr(a.error_flags, 8u);
+        // k_local_pre read only the PUTs the caller's opcode mirror names
+        if (a.opc && sprb[tid] && x[8] == kOpPut && a.opc[i] != kOpPut && a.error_flags) atomicOr(a.error_flags, 8u);
         a.ent[i] = e;
         a.st[i] = st;
         if (st != kStDefer) note_state(a, i, x);
-    }
-    if (T && a.pkeys) {   // the wave's sum of the PUTs it saw (k_commit_w compares it with the prepass's)
-        chk = wave_sum64(chk);
-        if (tid == 0 && chk) atomicAdd(a.pchk + kChkStripes + (blockIdx.x % kChkStripes), chk);
     }
     __syncthreads();
     // the waiting elements (keys INVALID at S_0: rare), appended once per block
@@ -1879,256 +1704,6 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         if (q < 3) *reinterpret_cast<uint4 *>(xg) = w;
         else *reinterpret_cast<uint64_t *>(xg) = (uint64_t)w.x | ((uint64_t)w.y << 32);
     }
-}
-
-// k_local_fused, software-pipelined (HKV_LF_PIPE; the default path only: no tags, F loaded beside every
-// hit's line, no hints, no key table, no PUT-key mirror). A persistent wave walks its chunks of 32
-// elements (chunk blockIdx.x, + gridDim.x, ...) and keeps the next chunk's loads in flight while it
-// resolves the current one: per iteration
-//   wait for chunk X's log lines and F words (issued last iteration), stage X in LDS;
-//   wait for chunk Y's ops, issue Y's bucket loads;
-//   resolve X on its LDS copies and write its ops back (Y's buckets in flight meanwhile);
-//   wait for Y's buckets, issue Y's log line + F loads; issue chunk Z's op loads; X := Y, Y := Z.
-// The waits are in issue order, so none of them waits for a younger load. Each element's result is
-// k_local_fused's: elements are independent once F is final, whatever chunk order a wave takes.
-struct LfChunk {
-    uint4 op[2];
-    uint64_t key[2];
-    bool probe[2], live[2];
-};
-
-__device__ __forceinline__ void lf_load_ops(const BatchArgs &a, int64_t i0, int q, int tid, LfChunk &c)
-{
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int64_t i = i0 + k * 16 + (tid >> 2);
-        c.live[k] = i0 >= 0 && i < a.n;
-        c.op[k] = make_uint4(0u, 0u, 0u, 0u);
-        if (c.live[k]) {
-            const uint8_t *xg = a.elems + i * 56 + 16 * q;
-            U64x2 p{0, 0};
-            if (a.patch) p = *reinterpret_cast<const U64x2 *>(a.patch + i * 16);
-            if (q < 3) {
-                c.op[k] = *reinterpret_cast<const uint4 *>(xg);
-            } else {
-                const uint64_t t = *reinterpret_cast<const uint64_t *>(xg);
-                c.op[k].x = (uint32_t)t;
-                c.op[k].y = (uint32_t)(t >> 32);
-            }
-            if (patch_valid(p.b)) c.op[k] = patch_chunk(c.op[k], q, p.a, p.b);
-        }
-    }
-}
-
-__device__ __forceinline__ void lf_keys(const BatchArgs &a, int64_t i0, int tid, LfChunk &c)
-{
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        c.key[k] = (uint64_t)(uint32_t)__shfl((int)c.op[k].x, 0, 4) | ((uint64_t)(uint32_t)__shfl((int)c.op[k].y, 0, 4) << 32);
-        const uint32_t h0 = (uint32_t)__shfl((int)c.op[k].z, 0, 4);
-        c.probe[k] = c.live[k] && in_count(a, (uint32_t)(i0 + k * 16 + (tid >> 2))) &&
-                     !skip_elem_os(kLocal, (uint8_t)h0, (uint8_t)(h0 >> 8));
-    }
-}
-
-// The LDS of one resolving chunk (k_local_fused_pp, k_local_fused_2c)
-struct LfLds {
-    uint4 sops[32 * 4];
-    uint4 sln[32 * 4];
-    unsigned long long sfw[32];
-    uint32_t sent[32];
-    uint8_t sprb[32];
-    uint32_t sdef[32];
-    uint32_t ndef;
-};
-
-// Buckets of a chunk (16 B per lane) -> its log lines and F words (lookup_pair_f's second half)
-__device__ __forceinline__ void lf_lines(const BatchArgs &a, const LfChunk &c, const uint4 *v, int q, int gbase,
-                                         bool *ok, uint64_t *phys, uint4 *ln, unsigned long long *fwv)
-{
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const uint64_t s0 = (uint64_t)v[k].x | ((uint64_t)v[k].y << 32);
-        const uint64_t s1 = (uint64_t)v[k].z | ((uint64_t)v[k].w << 32);
-        const uint32_t tag = (uint32_t)(c.key[k] >> 48);
-        const bool mt0 = c.probe[k] && (s0 & 1u) && ((uint32_t)(s0 >> 1) & 0x7FFFFFu) == tag;
-        const bool mt1 = c.probe[k] && (s1 & 1u) && ((uint32_t)(s1 >> 1) & 0x7FFFFFu) == tag;
-        const uint32_t g0 = (uint32_t)(__ballot(mt0) >> gbase) & 0xFu;
-        const uint32_t g1 = (uint32_t)(__ballot(mt1) >> gbase) & 0xFu;
-        uint32_t o = 0;
-#pragma unroll
-        for (int l = 0; l < 4; ++l) o |= ((g0 >> l) & 1u) << (2 * l) | ((g1 >> l) & 1u) << (2 * l + 1);
-        const int first = o ? __ffs(o) - 1 : 0;
-        const uint64_t off = __shfl((first & 1) ? (s1 >> 24) : (s0 >> 24), first >> 1, 4);
-        ok[k] = c.probe[k] && o && a.g.log_head - off < a.g.log_cap;
-        phys[k] = off & a.g.log_mask;
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        ln[k] = ok[k] ? reinterpret_cast<const uint4 *>(a.log + phys[k])[q] : make_uint4(0u, 0u, 0u, 0u);
-        fwv[k] = ok[k] && q == 0 ? a.fw[fw_index(a, phys[k])] : ~0ull;
-    }
-}
-
-__device__ __forceinline__ void lf_buckets(const BatchArgs &a, const LfChunk &c, int q, uint4 *v)
-{
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-        v[k] = c.probe[k] ? reinterpret_cast<const uint4 *>(a.index + ((c.key[k] & 0xFFFFFFFFFFFFULL) & a.g.bkt_mask) * 64u)[q]
-                          : make_uint4(0u, 0u, 0u, 0u);
-}
-
-// one chunk staged in LDS (the caller has reset L.ndef and synchronises after)
-__device__ __forceinline__ void lf_stage(const BatchArgs &a, LfLds &L, const LfChunk &c, const bool *ok,
-                                         const uint64_t *phys, const uint4 *ln, const unsigned long long *fwv, int q,
-                                         int tid)
-{
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int te = k * 16 + (tid >> 2);
-        Meta m;
-        const uint64_t ek = line_key_meta(ln[k], m);
-        const bool hit = ok[k] && ek == c.key[k];
-        L.sops[te * 4 + q] = c.op[k];
-        if (hit) L.sln[te * 4 + q] = ln[k];
-        if (q == 0) {
-            L.sfw[te] = hit && m_state(m) != kInvalid ? fwv[k] : ~0ull;
-            L.sent[te] = hit ? (uint32_t)(phys[k] / a.g.entry_unit) : kNone;
-            L.sprb[te] = c.probe[k];
-        }
-    }
-}
-
-// k_local_fused's rules for one staged chunk (default path), then its ops back (between two barriers)
-__device__ __forceinline__ void lf_resolve(const BatchArgs &a, LfLds &L, const LfChunk &c, int64_t i0, int q, int tid)
-{
-    if (tid < 32 && i0 + tid < a.n) {
-        const int64_t i = i0 + tid;
-        uint8_t *x = reinterpret_cast<uint8_t *>(&L.sops[tid * 4]);
-        uint8_t *ent = reinterpret_cast<uint8_t *>(&L.sln[tid * 4]);
-        const uint32_t e = L.sent[tid];
-        uint8_t st = kStDone;
-        if (e != kNone) {
-            Ctx cx = make_ctx(a);
-            const uint8_t bidx = (uint8_t)((uint32_t)i % (uint32_t)a.stride);
-            Meta m;
-            meta_load(ent, m);
-            const bool wm = would_mutate(kLocal, x, m, cx);
-            if (m_state(m) == kInvalid) {
-                if (wm) {
-                    const uint64_t ph = phys_of(a, e);
-                    offer(a.fw + fw_index(a, ph), a.rtag0, (uint32_t)i);
-                    if ((uint8_t)(m.w5 >> 16) != a.ltag) a.log[ph + kEntryMetaOff + 4] = a.ltag;
-                }
-                st = kStDefer;
-                L.sdef[atomicAdd(&L.ndef, 1u)] = (uint32_t)i;
-            } else {
-                const uint32_t f = first_cand(L.sfw[tid], a.rtag0);
-                if (wm && (f == kNone || f > (uint32_t)i) && a.error_flags) atomicOr(a.error_flags, 4u);
-                if ((uint32_t)i == f) {
-                    apply_to_shadow<kLocal, 31>(a, x, (uint32_t)i, ent);
-                    st = kStCommit;
-                } else {
-                    const Meta m0 = f != kNone && (uint32_t)i > f ? after_first<kLocal>(a, m, f, 1) : m;
-                    Meta tm = m0;
-                    dispatch<31>(kLocal, x, ent, bidx, tm, cx);
-                    if (a.error_flags && !meta_equal(tm, m0)) atomicOr(a.error_flags, 1u);
-                }
-            }
-        } else if (L.sprb[tid]) {
-            x[9] = kMiss;
-        }
-        if (a.opc && L.sprb[tid] && x[8] == kOpPut && a.opc[i] != kOpPut && a.error_flags) atomicOr(a.error_flags, 8u);
-        a.ent[i] = e;
-        a.st[i] = st;
-        if (st != kStDefer) note_state(a, i, x);
-    }
-    __syncthreads();
-    if (L.ndef && tid == 0) {
-        const uint32_t base = atomicAdd(&a.ctr[kCtrDefer], L.ndef);
-        for (uint32_t j = 0; j < L.ndef; ++j) a.fbl[base + j] = L.sdef[j];
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        if (!c.live[k]) continue;
-        const int te = k * 16 + (tid >> 2);
-        uint8_t *xg = a.elems + (i0 + te) * 56 + 16 * q;
-        const uint4 w = L.sops[te * 4 + q];
-        if (q < 3) *reinterpret_cast<uint4 *>(xg) = w;
-        else *reinterpret_cast<uint64_t *>(xg) = (uint64_t)w.x | ((uint64_t)w.y << 32);
-    }
-}
-
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_local_fused_pp(BatchArgs a, int64_t n_chunks)
-{
-    __shared__ LfLds L;
-    const int tid = threadIdx.x, q = tid & 3, gbase = tid & ~3;
-    const int64_t stride = gridDim.x;
-    int64_t cx = blockIdx.x;          // chunk X: its lines and F words in flight
-    if (cx >= n_chunks) return;
-    LfChunk X, Y;
-    uint4 lnx[2], vy[2];
-    unsigned long long fwx[2];
-    bool okx[2];
-    uint64_t physx[2];
-    // prologue: X's ops, buckets and lines; Y's ops
-    lf_load_ops(a, cx * 32, q, tid, X);
-    lf_keys(a, cx * 32, tid, X);
-    lf_buckets(a, X, q, vy);
-    lf_lines(a, X, vy, q, gbase, okx, physx, lnx, fwx);
-    int64_t cy = cx + stride;
-    lf_load_ops(a, cy < n_chunks ? cy * 32 : -1, q, tid, Y);
-    for (;;) {
-        if (tid == 0) L.ndef = 0;
-        lf_stage(a, L, X, okx, physx, lnx, fwx, q, tid);
-        const bool more = cy < n_chunks;
-        if (more) {   // Y's keys and buckets: in flight while X resolves
-            lf_keys(a, cy * 32, tid, Y);
-            lf_buckets(a, Y, q, vy);
-        }
-        __syncthreads();
-        lf_resolve(a, L, X, cx * 32, q, tid);
-        if (!more) break;
-        lf_lines(a, Y, vy, q, gbase, okx, physx, lnx, fwx);
-        X = Y;
-        cx = cy;
-        cy = cx + stride;
-        lf_load_ops(a, cy < n_chunks ? cy * 32 : -1, q, tid, Y);
-        __syncthreads();   // X's LDS copies are free again
-    }
-}
-
-// k_local_fused with two chunks per wave (HKV_LF_2C): both chunks' loads in flight together, then each
-// staged and resolved through the same 32-element LDS (so LDS stays that of one chunk)
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_local_fused_2c(BatchArgs a)
-{
-    __shared__ LfLds L;
-    const int tid = threadIdx.x, q = tid & 3, gbase = tid & ~3;
-    const int64_t c0 = (int64_t)blockIdx.x * 2;
-    LfChunk X, Y;
-    uint4 vx[2], vy[2], lnx[2], lny[2];
-    unsigned long long fwx[2], fwy[2];
-    bool okx[2], oky[2];
-    uint64_t physx[2], physy[2];
-    const int64_t nch = (a.n + 31) / 32;
-    lf_load_ops(a, c0 * 32, q, tid, X);
-    lf_load_ops(a, c0 + 1 < nch ? (c0 + 1) * 32 : -1, q, tid, Y);
-    lf_keys(a, c0 * 32, tid, X);
-    lf_keys(a, (c0 + 1) * 32, tid, Y);
-    lf_buckets(a, X, q, vx);
-    lf_buckets(a, Y, q, vy);
-    lf_lines(a, X, vx, q, gbase, okx, physx, lnx, fwx);
-    lf_lines(a, Y, vy, q, gbase, oky, physy, lny, fwy);
-    if (tid == 0) L.ndef = 0;
-    lf_stage(a, L, X, okx, physx, lnx, fwx, q, tid);
-    __syncthreads();
-    lf_resolve(a, L, X, c0 * 32, q, tid);
-    if (c0 + 1 >= nch) return;
-    __syncthreads();
-    if (tid == 0) L.ndef = 0;
-    lf_stage(a, L, Y, oky, physy, lny, fwy, q, tid);
-    __syncthreads();
-    lf_resolve(a, L, Y, (c0 + 1) * 32, q, tid);
 }
 
 // ------------------------------------------------------------------ launches with unique keys
@@ -2764,20 +2339,6 @@ __global__ __launch_bounds__(256) void k_commit_w(BatchArgs a)
     __shared__ uint32_t lst[4][kCwElems];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t e0 = ((int64_t)blockIdx.x * 4 + w) * kCwElems + 16 * lane;
-    if (a.pchk && blockIdx.x == 0 && w == 0) {
-        // the PUT-key mirror's checksum (k_local_pre) against the PUTs k_local_fused saw: a mirror that
-        // named a PUT wrongly, or missed one, raises error bit 3; the sums start over for the next launch
-        unsigned long long sp = 0, sf = 0;
-        for (int j = lane; j < kChkStripes; j += 64) {
-            sp += a.pchk[j];
-            sf += a.pchk[kChkStripes + j];
-            a.pchk[j] = 0;
-            a.pchk[kChkStripes + j] = 0;
-        }
-        sp = wave_sum64(sp);
-        sf = wave_sum64(sf);
-        if (lane == 0 && sp != sf && a.error_flags) atomicOr(a.error_flags, 8u);
-    }
     uint32_t m = 0;
     if (e0 + 16 <= a.n) {   // st is 256-byte aligned and e0 a multiple of 16
         const uint4 s4 = *reinterpret_cast<const uint4 *>(a.st + e0);
@@ -3900,12 +3461,8 @@ static void launch_local_pre(const BatchArgs &a, int64_t n, hipStream_t s)
 {
     static const int head = getenv("HKV_PRE_HEAD") ? atoi(getenv("HKV_PRE_HEAD")) : kPreHead;
     const dim3 grid((unsigned)((n + kPreElems - 1) / kPreElems));
-    static const bool ff_env = getenv("HKV_PRE_FFILTER") && atoi(getenv("HKV_PRE_FFILTER")) != 0;
-    if (a.ktab) hipLaunchKernelGGL((k_local_pre<kPreHead, false, true>), grid, dim3(256), 0, s, a);
-    else if (a.pre_notag && !a.cancel && !a.phys_hint && head == kPreHead)
-        hipLaunchKernelGGL((k_local_pre<kPreHead, false, false, false, true>), grid, dim3(256), 0, s, a);
-    else if (ff_env && !a.phys_hint && head == kPreHead)
-        hipLaunchKernelGGL((k_local_pre<kPreHead, false, false, true>), grid, dim3(256), 0, s, a);
+    if (a.pre_notag && !a.cancel && !a.phys_hint && head == kPreHead)
+        hipLaunchKernelGGL((k_local_pre<kPreHead, false, true>), grid, dim3(256), 0, s, a);
     else if (a.phys_hint) hipLaunchKernelGGL((k_local_pre<kPreHead, true>), grid, dim3(256), 0, s, a);
     else if (head == 256) hipLaunchKernelGGL(k_local_pre<256>, grid, dim3(256), 0, s, a);
     else if (head == 512) hipLaunchKernelGGL(k_local_pre<512>, grid, dim3(256), 0, s, a);
@@ -3929,11 +3486,6 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.ack_out = bl.type == kInvs || (bl.type == kAcks && bl.n_rows > 0) ? bl.ack_out : nullptr;
     a.ack_out_size = bl.ack_out_size;
     a.pre_notag = 0;
-    a.ktab = nullptr;
-    a.ktab_bits = bl.ktab_bits;
-    a.ktag = 1u + (bl.epoch - 1u) % 65535u;
-    a.kepoch = bl.epoch;
-    a.pchk = nullptr;
     a.n_rows = bl.n_rows;
     a.skip_row = bl.skip_row;
     a.row_stride = bl.row_stride;
@@ -4014,25 +3566,19 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
                               bl.g.st_value == 31 && bl.g.entry_size == 64 && !bl.offsets;
     // HKV_PATCH_APPLY=1: patches always written into the ops first (experiments)
     static const bool patch_apply_env = getenv("HKV_PATCH_APPLY") && atoi(getenv("HKV_PATCH_APPLY")) != 0;
-    // HKV_PRE_TABLE=1: the prepass puts the launch's PUT keys into the key table instead of looking
-    // them up (kt_insert); with the PUT-key mirror the mirror is checked by checksum
-    static const bool table_env = getenv("HKV_PRE_TABLE") && atoi(getenv("HKV_PRE_TABLE")) != 0;
     // The prepass sets no seqlock-byte tags and the fused pass loads every hit's F word beside its log
     // line (round 5, the default; HKV_PRE_NOTAG=0: tags, and F loaded after the line for tagged keys
     // only). Same box, 3 x 20 steps each (gpurun_out/r05e): 4.355-4.359 -> 4.378-4.393 G ops/s, prepass
     // 78.1 -> 73.8 us, fused pass level (265.7 / 266.7 us)
     static const bool notag_env = !getenv("HKV_PRE_NOTAG") || atoi(getenv("HKV_PRE_NOTAG")) != 0;
-    auto use_table = [&]() {
-        if (notag_env && local_direct && !a.phys_hint && !table_env) a.pre_notag = 1;
-        if (!(table_env && local_direct && bl.ktab && !a.phys_hint)) return;
-        a.ktab = reinterpret_cast<uint4 *>(bl.ktab);
-        if (a.pkeys) a.pchk = bl.pchk;
+    auto set_notag = [&]() {
+        if (notag_env && local_direct && !a.phys_hint) a.pre_notag = 1;
     };
     if (bl.stage == 3) {   // HKV_BATCH_PREPASS_CANCEL: the prepass's lookups again, clearing its tags
         if (bl.pre_done) {
             if (bl.patch) a.patch = bl.patch;
             if (bl.put_keys && a.state_out) a.pkeys = bl.put_keys;
-            use_table();
+            set_notag();
             launch_local_pre(a, n, s);
         }
         return hipGetLastError() == hipSuccess ? 0 : -3;
@@ -4041,7 +3587,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         if (local_direct && !small && !patch_apply_env) {
             if (bl.patch) a.patch = bl.patch;
             if (local_direct && bl.put_keys && a.state_out) a.pkeys = bl.put_keys;
-            use_table();
+            set_notag();
             launch_local_pre(a, n, s);
             bl.pre_done = 1;
         }
@@ -4053,7 +3599,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         a.patch = bl.patch;
     }
     if (local_direct && !small && bl.put_keys && a.state_out) a.pkeys = bl.put_keys;
-    if (!small) use_table();
+    if (!small) set_notag();
     if (small) {
         if (launch_small(a, s)) return -3;
         return 0;                              // node_suspected written by the kernel
@@ -4067,27 +3613,9 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         static const int lfp_env = getenv("HKV_LF_PAIR") ? atoi(getenv("HKV_LF_PAIR")) : 2;
         // HKV_LF_FSPEC=1: every hit loads its key's F word beside the log line (no dependent load after it)
         static const bool fspec_env = getenv("HKV_LF_FSPEC") && atoi(getenv("HKV_LF_FSPEC")) != 0;
-        // HKV_LF_PIPE=1: the software-pipelined persistent fused pass (k_local_fused_pp), HKV_LF_PIPE_WAVES
-        // waves per CU (default 32)
-        static const bool pipe_env = getenv("HKV_LF_PIPE") && atoi(getenv("HKV_LF_PIPE")) != 0;
-        static const int pipe_waves = getenv("HKV_LF_PIPE_WAVES") ? std::max(1, atoi(getenv("HKV_LF_PIPE_WAVES"))) : 32;
-        static const bool twoc_env = getenv("HKV_LF_2C") && atoi(getenv("HKV_LF_2C")) != 0;
-        if (a.pre_notag && twoc_env && !a.pkeys) {
-            hipLaunchKernelGGL(k_local_fused_2c, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, a);
-        } else if (a.pre_notag && pipe_env && !a.pkeys) {
-            const int64_t chunks = (n + 31) / 32;
-            static const int cus = [] {
-                int dev = 0, c = 256;
-                if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
-                return c;
-            }();
-            const int64_t g = std::min<int64_t>(chunks, (int64_t)cus * pipe_waves);
-            hipLaunchKernelGGL(k_local_fused_pp, dim3((unsigned)g), dim3(64), 0, s, a, chunks);
-        } else if (a.pre_notag)
-            hipLaunchKernelGGL((k_local_fused<2, false, false, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
-        else if (fspec_env && !a.ktab && !a.phys_hint && lfp_env == 2)
-            hipLaunchKernelGGL((k_local_fused<2, false, false, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
-        else if (a.ktab)
+        if (a.pre_notag)
+            hipLaunchKernelGGL((k_local_fused<2, false, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
+        else if (fspec_env && !a.phys_hint && lfp_env == 2)
             hipLaunchKernelGGL((k_local_fused<2, false, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
         else if (a.phys_hint)
             hipLaunchKernelGGL((k_local_fused<2, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);

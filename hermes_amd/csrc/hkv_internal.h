@@ -32,9 +32,6 @@ struct BatchLaunch {
     unsigned long long *fw;
     unsigned long long *fx, *fy;              // INV words per log line (zero between launches)
     unsigned long long *ft;                   // ACK words, eight per log line (tagged with the epoch)
-    void *ktab;                               // local direct path: the PUT-key table (2^ktab_bits 16-B slots)
-    uint32_t ktab_bits;
-    unsigned long long *pchk;                 // its PUT-mirror checksum stripes
     unsigned long long *mem;
     uint32_t *ent, *fbl, *pf, *ctr;
     uint8_t *st, *shadow;

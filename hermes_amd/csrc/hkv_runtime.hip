@@ -136,9 +136,6 @@ struct hkv_table {
     uint8_t *d_batch = nullptr;
     int64_t batch_cap = 0;
     unsigned long long *d_fw = nullptr;  // F words, one per 64-B log line (+ INV words X, Y, ACK words T)
-    void *d_ktab = nullptr;              // the local launches' PUT-key table (hkv_batch.hip, kt_insert)
-    uint32_t ktab_bits = 0;
-    unsigned long long *d_pchk = nullptr;   // its checksum stripes (2 x 256)
     uint32_t epoch = 0;                // batch launches since d_fw was all-ones
     uint32_t scratch_gen = 0;          // d_batch reallocations
     // a local launch's prepass (HKV_BATCH_PREPASS) waiting for the rest of its launch
@@ -296,13 +293,6 @@ static int ensure_batch_scratch(hkv_table *t, int64_t n)
         // the null stream, which does not order the table's non-blocking streams: wait for it here.
         HIP_TRY(hipMemset(t->d_fw, 0xFF, bytes));
         HIP_TRY(hipMemset(reinterpret_cast<uint8_t *>(t->d_fw) + bytes, 0, 10 * bytes));
-        // the PUT-key table: 2^HKV_KTAB_BITS 16-B slots (default 2^21, 32 MiB: a few hundred thousand
-        // distinct PUT keys per launch at configs[1]), zero = empty for every launch tag
-        t->ktab_bits = getenv("HKV_KTAB_BITS") ? (uint32_t)std::max(16, std::min(26, atoi(getenv("HKV_KTAB_BITS")))) : 21u;
-        HIP_TRY(hipMalloc(&t->d_ktab, (size_t)16 << t->ktab_bits));
-        HIP_TRY(hipMemset(t->d_ktab, 0, (size_t)16 << t->ktab_bits));
-        HIP_TRY(hipMalloc(&t->d_pchk, 2 * 256 * sizeof(unsigned long long)));
-        HIP_TRY(hipMemset(t->d_pchk, 0, 2 * 256 * sizeof(unsigned long long)));
         HIP_TRY(hipDeviceSynchronize());
         t->epoch = 0;
     }
@@ -427,8 +417,6 @@ int hkv_table_destroy(hkv_table *t)
     hipFree(t->d_evictions);
     hipFree(t->d_batch);
     hipFree(t->d_fw);
-    hipFree(t->d_ktab);
-    hipFree(t->d_pchk);
     hipFree(t->d_error_flags);
     hipFree(t->d_ns_idx);
     for (HostSet &hs : t->sets) {
@@ -629,9 +617,7 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.fx = t->d_fw + batch_fw_words(t->cfg.log_cap);
     bl.fy = bl.fx + batch_fw_words(t->cfg.log_cap);
     bl.ft = bl.fy + batch_fw_words(t->cfg.log_cap);
-    bl.ktab = t->d_ktab;
-    bl.ktab_bits = t->ktab_bits;
-    bl.pchk = t->d_pchk;
+
     const int stage = (d->flags & HKV_BATCH_PREPASS_CANCEL) ? 3 : (d->flags & HKV_BATCH_PREPASSED) ? 2
                     : (d->flags & HKV_BATCH_PREPASS) ? 1 : 0;
     if (stage && d->type != kLocal) return fail(-1, "HKV_BATCH_PREPASS/PREPASSED apply to local batches");
@@ -662,9 +648,6 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
             t->pre.valid = false;   // a pending prepass's offers are gone: its second call fails
         }
         bl.epoch = t->epoch;
-        // the key table's 16-bit launch tag wraps every 65535 launches: it starts over empty then
-        if ((bl.epoch - 1) % 65535u == 0)
-            HIP_TRY(hipMemsetAsync(t->d_ktab, 0, (size_t)16 << t->ktab_bits, s));
     }
     bl.stage = stage;
     bl.error_flags = t->d_error_flags;

@@ -833,11 +833,14 @@ static const bool g_staging_nc = getenv("HKV_STAGING_NC") != nullptr;  // experi
 // averaged over the calls and printed at exit
 static const bool g_host_timing = getenv("HKV_HOST_TIMING") != nullptr;
 static std::atomic<long> g_ht_calls{0}, g_ht_stage{0}, g_ht_wait{0}, g_ht_out{0};
+static std::atomic<long> g_hc_n{0}, g_hc_inflight{0}, g_hc_take{0}, g_hc_publish{0}, g_hc_flagwait{0};
 static void host_timing_print()
 {
-    const long n = std::max(1L, g_ht_calls.load());
-    fprintf(stderr, "[hkv] host call timing (us, avg of %ld): stage %.2f wait %.2f copy-out %.2f\n", n,
-            g_ht_stage.load() / 1e3 / n, g_ht_wait.load() / 1e3 / n, g_ht_out.load() / 1e3 / n);
+    const long n = std::max(1L, g_ht_calls.load()), m = std::max(1L, g_hc_n.load());
+    fprintf(stderr, "[hkv] host call timing (us, avg of %ld): stage %.2f wait %.2f (flags %.2f) copy-out %.2f\n", n,
+            g_ht_stage.load() / 1e3 / n, g_ht_wait.load() / 1e3 / n, g_hc_flagwait.load() / 1e3 / n, g_ht_out.load() / 1e3 / n);
+    fprintf(stderr, "[hkv] combiner (us, avg of %ld launches): in-flight wait %.2f take %.2f publish %.2f\n", m,
+            g_hc_inflight.load() / 1e3 / m, g_hc_take.load() / 1e3 / m, g_hc_publish.load() / 1e3 / m);
 }
 static long now_ns()
 {
@@ -1169,6 +1172,7 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
         memset(t->ring, 0, sizeof(HostRingSlot) * kRingN);
         srv_set_stop(t, 0u);
     }
+    const long c0 = g_host_timing ? now_ns() : 0;
     for (uint32_t spins = 0; (int32_t)(t->pseq - part_done(t)) >= inflight; ++spins) {
         if (serve && t->srv_running && srv_exited(t)) srv_ensure(t);   // a server that left has work to do
         lk.unlock();
@@ -1176,6 +1180,7 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
         if ((spins & 255u) == 255u) sched_yield();
         lk.lock();
     }
+    const long c1 = g_host_timing ? now_ns() : 0;
     HostPartLaunch pl;
     memset(&pl, 0, sizeof pl);
     std::vector<HostReq *> take;
@@ -1218,6 +1223,7 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
     pl.seq = seq;
     if (g_host_stats) host_stats_note(nb);
     TRACE("partitioned launch %u batches=%d", seq, nb);
+    const long c2 = g_host_timing ? now_ns() : 0;
     if (serve) {   // publish: the slot's contents, then its seq (x86 stores stay in order)
         HostRingSlot &slot = t->ring[seq % kRingN];
         slot.n_batches = nb;
@@ -1248,6 +1254,13 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
             }
         }
         lk.lock();
+    }
+    if (g_host_timing) {
+        const long c3 = now_ns();
+        g_hc_n += 1;
+        g_hc_inflight += c1 - c0;
+        g_hc_take += c2 - c1;
+        g_hc_publish += c3 - c2;
     }
     for (HostReq *r : take) {
         r->pseq = seq;
@@ -1576,6 +1589,7 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
         std::lock_guard<std::mutex> lk(t->hmu);
         seq = set->seq;
     }
+    const long tl = g_host_timing ? now_ns() : 0;
     if (mode == kModePart) {  // every workgroup's flag at or past this launch (they only grow); yield
                               // now and then, so callers that outnumber the cores leave the combiner CPU time
         for (uint32_t spins = 0;; ++spins) {
@@ -1598,10 +1612,11 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
         die("sync");
     }
     const long t2 = g_host_timing ? now_ns() : 0;
+    if (g_host_timing) g_hc_flagwait += t2 - tl;
     // HKV_PART_STREAMS > 1: a workgroup that waited over 1 s for its partition's previous launch gave
     // up without applying its elements (error bit 5): the table no longer follows any caller order
-    if (mode == kModePart && t->n_pstreams && __atomic_load_n(t->pflags + kPartG, __ATOMIC_ACQUIRE))
-        die("partitioned launch gave up waiting for its partition's previous launch (HKV_PART_STREAMS, error bit 5)");
+    if (mode == kModePart && __atomic_load_n(t->pflags + kPartG, __ATOMIC_ACQUIRE))
+        die("partitioned launch gave up waiting for its partition's previous launch (error bit 5)");
     if (mode == kModePart) {
         // results from this thread's staging, back in element order; node_suspected is
         // hermes_skip_inv's, a function of the elements alone: the last membership-change INV's

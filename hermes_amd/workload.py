@@ -397,6 +397,7 @@ class Round:
         self.fused_acks = (self.pack_remote and ((kvs.sizes.entry == 64 and self.op <= 64) or
                                                  (kvs.sizes.entry == 320 and self.op <= 320))
                            and os.environ.get("HKV_FUSED_ACKS", "1") != "0")
+        self.packed_prefix = os.environ.get("HKV_PACKED_PREFIX", "1") != "0"
         self.drops = []                # peers dropped from the membership (membership_change)
         self.alive = self.R            # live peers: the first `alive` slots of the remote slabs
         self._counts = {}
@@ -619,9 +620,16 @@ class Round:
                                 _ptr(self.remote_counts[k][n_peers]), self.W, self.rstride, self.op,
                                 _ptr(self.peer_ts), self.clock, _s()), "peer_ts")
 
-    def peer_timestamps_packed(self, k: int):
-        """the same for the packed slabs, whose INVs' entries were located when they were drawn"""
+    def _packed_total(self, k: int, n_peers: int) -> int:
+        """elements of the first n_peers peers in round index k's packed slabs"""
+        return sum(n for _, n, _ in self.remote_packed[k][5][:n_peers])
+
+    def peer_timestamps_packed(self, k: int, n_peers: int | None = None):
+        """the same for the packed slabs, whose INVs' entries were located when they were drawn (the first
+        n_peers peers' elements; default all)"""
         pi, pv, _, total, phys, _ = self.remote_packed[k]
+        if n_peers is not None:
+            total = self._packed_total(k, n_peers)
         if self.inv_rows:
             rows, _, inv_at, _ = self.remote_rows[k]
             check(_L.hkv_wl_peer_ts_rows(self.kvs.h, _ptr(rows), _ptr(inv_at), _ptr(pv), _ptr(phys), total, self.op,
@@ -635,10 +643,10 @@ class Round:
         self.kvs.batch(L.BatchType.invs, invs, n_batches, stride, self.op, self.mb, counts=counts, offsets=offsets,
                        unique=unique)
 
-    def inv_batches_per_peer(self, k: int):
+    def inv_batches_per_peer(self, k: int, n_peers: int | None = None):
         """Every peer's INVs of round index k as a launch of its own (HKV_BATCH_UNIQUE), in peer order --
         or all peers' as one rows launch (HKV_BATCH_ROWS): each key looked up once, its INVs applied in
-        peer order"""
+        peer order. n_peers: the first n_peers peers only (default all)"""
         if self.inv_rows:
             rows, P, _, off = self.remote_rows[k]
             if P:
@@ -646,7 +654,7 @@ class Round:
                                rows=(self.R, P, -1))
             return
         pi, _, _, _, phys, per_peer = self.remote_packed[k]
-        for base, n, off in per_peer:
+        for base, n, off in per_peer[:n_peers]:
             if n:
                 ph = phys[base:] if self.phys_hints else None
                 if self.fused_acks and not self.inv_rows:
@@ -768,17 +776,20 @@ class Round:
             assert self.virtual and self.alive and drop == self.peers[self.alive - 1], "drop the last live peer"
         sent = self.alive                          # peers whose INVs this round applies
         alive = self.alive - (drop is not None)    # peers that answer them (ACKs) and send VALs
-        # every peer live and none failing this round: the packed slabs (same elements, same order)
-        packed = self.pack_remote and sent == self.R and alive == self.R
+        # the packed slabs (same elements, same order): the live peers are their first `alive` peers (a
+        # failed peer is always the last live one), so after a failure the rounds apply a prefix of them
+        # (the rows layout holds every peer: only while all are live)
+        # (HKV_PACKED_PREFIX=0: the row layout once a peer has failed, as before round 5)
+        packed = self.pack_remote and ((sent == self.R and alive == self.R) or (self.packed_prefix and not self.inv_rows))
         if self.R and sent:
             if packed and self.overlap:
                 self.side.wait_event(self.tbl_ready)
                 with torch.cuda.stream(self.side):
-                    self.peer_timestamps_packed(k)
+                    self.peer_timestamps_packed(k, sent)
                 self.pts_done.record(self.side)
                 torch.cuda.current_stream().wait_event(self.pts_done)
             elif packed:
-                self.peer_timestamps_packed(k)
+                self.peer_timestamps_packed(k, sent)
             else:
                 self.peer_timestamps(k, sent)
         if self.audit is not None:
@@ -811,12 +822,12 @@ class Round:
             ic = self._slot_counts(k, sent)
             if packed:
                 pi, pv, off, total, _, _ = self.remote_packed[k]
-                timed("invs", lambda: self.inv_batches_per_peer(k))
+                timed("invs", lambda: self.inv_batches_per_peer(k, sent))
                 if self.inv_rows:   # our ACKs to the rows (holes answer nothing)
                     rows, P, _, _ = self.remote_rows[k]
                     self.marshal_acks(rows, self.R * P, self.rows_acks)
                 elif not self.fused_acks:   # (else the INV launches wrote them)
-                    self.marshal_acks(pi, total, self.ack_out)
+                    self.marshal_acks(pi, self._packed_total(k, sent), self.ack_out)
             else:
                 timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride, counts=ic))
                 self.marshal_acks(ri, self.W * self.rstride, self.ack_out)
@@ -864,7 +875,8 @@ class Round:
                 self.prepass(overlap=True, events=events if events is not None and "local" in timed_batches else None)
             if packed:
                 ph = self.remote_packed[k][4] if self.phys_hints else None
-                timed("vals", lambda: self.val_batch(pv, self.R * self.W, total, offsets=off, phys=ph))
+                timed("vals", lambda: self.val_batch(pv, alive * self.W, self._packed_total(k, alive), offsets=off,
+                                                     phys=ph))
             else:
                 timed("vals", lambda: self.val_batch(rv, self.W, self.rstride, counts=vc))
             if self.count_elems:

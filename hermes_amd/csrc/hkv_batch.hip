@@ -3625,7 +3625,11 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
             hipLaunchKernelGGL(k_local_fused<1>, dim3((unsigned)((n + 15) / 16)), dim3(64), 0, s, a);
         else
             hipLaunchKernelGGL(k_local_fused<2>, dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
-        hipLaunchKernelGGL(k_local_deferred, dim3(8), dim3(256), 0, s, a);
+        // the waiting elements' count is on the device: enough workgroups for the rounds after a
+        // membership change (configs[4]: ~100 K elements of keys a failed peer left INVALID), which
+        // return at once when there are few (HKV_DEFER_BLOCKS: the grid, experiments)
+        static const int defer_blocks = getenv("HKV_DEFER_BLOCKS") ? std::max(1, atoi(getenv("HKV_DEFER_BLOCKS"))) : 128;
+        hipLaunchKernelGGL(k_local_deferred, dim3((unsigned)defer_blocks), dim3(256), 0, s, a);
         // HKV_COMMIT_W=0: the thread-per-element k_commit (experiments)
         static const bool commit_w_env = !getenv("HKV_COMMIT_W") || atoi(getenv("HKV_COMMIT_W")) != 0;
         if (commit_w_env)

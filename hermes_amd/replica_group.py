@@ -138,6 +138,10 @@ class ReplicaRound:
         # launch per peer)
         self.ack_rows = os.environ.get("HKV_ACK_ROWS", "1") != "0" and self.sizes.entry == 64 and self.ack_size <= 64
         self.own_total = None          # this round's packed INV total, when read back (round_shape)
+        # this replica's ACKs to a peer's INVs written by that peer's INV launch itself (hkv_batch_desc.d_ack_out,
+        # as at N = 1) instead of a marshal pass over the applied row (HKV_FUSED_ACKS=0: the pass)
+        self.fused_acks = (((self.sizes.entry == 64 and self.op <= 64) or (self.sizes.entry == 320 and self.op <= 320))
+                           and os.environ.get("HKV_FUSED_ACKS", "1") != "0")
         self.refill(first=True)
 
     # -- Hades: one view-update period per round when enabled
@@ -273,10 +277,28 @@ class ReplicaRound:
         # flight per key and coordinator), so each applies in one pass (HKV_BATCH_UNIQUE)
         for p in range(self.N):
             if p != self.rank:
-                self.kvs.batch(L.BatchType.invs, self.inv_recv[p * width * self.op:], 1, width, self.op, self.mb,
-                               counts=self.inv_totals[p:p + 1], unique=True)
-        check(_L.hkv_wl_marshal_acks_aligned(_ptr(self.inv_recv), _ptr(self.inv_totals), self.N, width, self.op,
-                                             _ptr(self.ack_slab), self.ack_size, self.rank, _s()), "marshal_acks")
+                self._inv_launch(p, width)
+        if not self.fused_acks:
+            check(_L.hkv_wl_marshal_acks_aligned(_ptr(self.inv_recv), _ptr(self.inv_totals), self.N, width, self.op,
+                                                 _ptr(self.ack_slab), self.ack_size, self.rank, _s()), "marshal_acks")
+            return
+        n, na = width * self.op, width * self.ack_size   # this rank's own row: all empty slots
+        check(_L.hkv_wl_marshal_acks_aligned(_ptr(self.inv_recv[self.rank * n:]), _ptr(self.inv_totals[self.rank:]), 1,
+                                             width, self.op, _ptr(self.ack_slab[self.rank * na:]), self.ack_size,
+                                             self.rank, _s()), "marshal_acks")
+
+    def _inv_launch(self, p: int, width: int):
+        """peer p's row of inv_recv as one unique-key launch; with fused_acks it also writes the ACKs
+        answering them into ack_slab's row p, lined up with the INVs (positions past the row's total
+        are never read: the peer's ACK launch stops at its own total)"""
+        n = width * self.op
+        if self.fused_acks:
+            self.kvs.batch(L.BatchType.invs, self.inv_recv[p * n:], 1, width, self.op, self.mb,
+                           counts=self.inv_totals[p:p + 1], unique=True,
+                           ack_out=self.ack_slab[p * width * self.ack_size:], ack_out_size=self.ack_size)
+        else:
+            self.kvs.batch(L.BatchType.invs, self.inv_recv[p * n:], 1, width, self.op, self.mb,
+                           counts=self.inv_totals[p:p + 1], unique=True)
 
     # -- per-peer exchanges (ReplicaGroupRound with p2p): each peer's INV slab is sent and received on
     # its own, applied as soon as it is there, and its ACK row goes back right after
@@ -310,11 +332,11 @@ class ReplicaRound:
             self.inv_totals[p:p + 1].copy_(self.inv_recv[a:a + 4].view(torch.int32))
         if self.failed:
             return
-        self.kvs.batch(L.BatchType.invs, self.inv_recv[p * n:], 1, width, self.op, self.mb,
-                       counts=self.inv_totals[p:p + 1], unique=True)
-        check(_L.hkv_wl_marshal_acks_aligned(_ptr(self.inv_recv[p * n:]), _ptr(self.inv_totals[p:]), 1, width, self.op,
-                                             _ptr(self.ack_slab[p * width * self.ack_size:]), self.ack_size, self.rank,
-                                             _s()), "marshal_acks")
+        self._inv_launch(p, width)
+        if not self.fused_acks:
+            check(_L.hkv_wl_marshal_acks_aligned(_ptr(self.inv_recv[p * n:]), _ptr(self.inv_totals[p:]), 1, width,
+                                                 self.op, _ptr(self.ack_slab[p * width * self.ack_size:]), self.ack_size,
+                                                 self.rank, _s()), "marshal_acks")
 
     def invs_end(self, width: int):
         if self.count_elems and not self.failed:

@@ -191,13 +191,29 @@ class Mirror:
         rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
         self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
                    node_suspected, stream, state_out=state_out, opcode_in=opcode_in, patch=patch, rw_state=rw_state,
-                   unique=unique, put_keys=put_keys, stage=stage, phys=phys, rw_opcodes=rw_opcodes)
+                   unique=unique, put_keys=put_keys, stage=stage, phys=phys, rw_opcodes=rw_opcodes,
+                   ack_out=ack_out, ack_out_size=ack_out_size)
         if stage == 2:
             self.prepass = False
         torch.cuda.synchronize()
         self.o.batch_multi(int(btype), e_in, n_batches, stride, c_in, membership, rw_in,
                            rw_stride_bytes // self.g.sizes.op if rw is not None else 0)
         what = f"{self.name} launch {self.launches} type {int(btype)}"
+        if ack_out is not None:   # the launch also ran the ACK callbacks on its applied INVs (d_ack_out)
+            eo = e_in.view(np.uint8).reshape(-1, elem_size)
+            j = np.arange(n_batches * stride) % stride
+            live = j < np.repeat(c_in, stride) if c_in is not None else np.ones(n_batches * stride, bool)
+            idx = np.nonzero(live)[0]
+            want_acks, after = ack_callbacks(eo[idx].copy(), ack_out_size, self.g.machine_id)
+            eo[idx] = after       # an answered INV leaves as after its send
+            got_acks = ack_out[: n_batches * stride * ack_out_size].cpu().numpy().reshape(-1, ack_out_size)[idx]
+            sent = want_acks[:, 8] != L.Bucket.EMPTY
+            span = np.where(want_acks[:, 8] == int(L.Resp.OP_INV_ABORT), elem_size, 16)
+            cmp = sent[:, None] & (np.arange(ack_out_size)[None, :] < span[:, None])
+            if not ((got_acks == want_acks) | ~cmp).all() or not (got_acks[~sent, 8] == int(L.Bucket.EMPTY)).all():
+                bad = np.nonzero(((got_acks != want_acks) & cmp).any(axis=1)
+                                 | (~sent & (got_acks[:, 8] != int(L.Bucket.EMPTY))))[0]
+                pytest.fail(f"{what}: fused ACKs differ at {len(bad)} elements, first {idx[bad[:8]]}")
         got = elems[:n].cpu().numpy()
         self._count(btype, "out8", 8, got, n_batches, stride, elem_size, c_in)
         self._count(btype, "out9", 9, got, n_batches, stride, elem_size, c_in)

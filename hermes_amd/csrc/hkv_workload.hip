@@ -1086,7 +1086,7 @@ __global__ __launch_bounds__(1024) void k_scan_cap(const int32_t *counts, int32_
                                                    int32_t *off, int32_t *sent, unsigned long long *held)
 {
     __shared__ int32_t part[1024];
-    __shared__ int32_t held_s[1024];
+    __shared__ unsigned long long held_s[16];
     const int t = threadIdx.x;
     const int per = (n + 1023) / 1024;
     const int lo = t * per, hi = min(n, lo + per);
@@ -1111,12 +1111,16 @@ __global__ __launch_bounds__(1024) void k_scan_cap(const int32_t *counts, int32_
         h += c - s;
         run += want;
     }
-    held_s[t] = h;
+    // the held total: a wave sum, then the 16 waves' (a serial walk over 1024 LDS words took ~20 us)
+    unsigned long long hw = (unsigned long long)h;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) hw += __shfl_down(hw, o, 64);
+    if ((t & 63) == 0) held_s[t >> 6] = hw;
     __syncthreads();
     if (t == 0) {
-        int64_t tot = 0;
-        for (int k = 0; k < 1024; ++k) tot += held_s[k];
-        if (tot && held) atomicAdd(held, (unsigned long long)tot);
+        unsigned long long tot = 0;
+        for (int k = 0; k < 16; ++k) tot += held_s[k];
+        if (tot && held) atomicAdd(held, tot);
         off[n] = min(part[1023], cap);
     }
 }

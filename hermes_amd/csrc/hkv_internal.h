@@ -169,7 +169,6 @@ struct TableView {
     Geometry g;
     const uint8_t *index;
     const uint8_t *log;
-    unsigned int *error_flags;   // the table's consistency flags (hkv_take_error_flags)
 };
 int table_view(const hkv_table *t, TableView *out);
 

@@ -334,7 +334,6 @@ int table_view(const hkv_table *t, TableView *out)
     out->g = t->geo;
     out->index = t->d_index;
     out->log = t->d_log;
-    out->error_flags = t->d_error_flags;
     return 0;
 }
 }  // namespace hkv

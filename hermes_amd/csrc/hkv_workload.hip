@@ -779,194 +779,6 @@ __global__ __launch_bounds__(256) void k_marshal_invs_w(uint8_t *ops, int32_t n_
     }
 }
 
-// The INV marshal of a round with virtual peers, the ACK offsets and the peers' ACKs in one pass
-// (hkv_wl_marshal_invs_pm; replaces k_marshal_invs_w + k_ack_offsets + k_peer_acks on the N = 1 round):
-// block b takes workers 8b .. 8b + 7, counts their sendable ops, and gets its
-// first INV's place in the round from the blocks before it by a decoupled look-back over one 64-bit
-// status word per block ([tag:30 | flag:2 | max:10 | sum:22], flag 1 = the block's own aggregate, 2 =
-// the inclusive prefix; the tag, the round's, makes a word of an earlier round unreadable, so nothing
-// is cleared between rounds). Then each wave copies its workers' INVs and writes every peer's ACK to
-// each of them at ack[r * ack_rs + off[w] + j]: the peer-major rows of the ACK rows launch, row stride
-// ack_rs. The last block writes off[W], the total and the largest per-worker count to the host
-// (h[0], h[1], then h[2] = seq when seq > 0).
-constexpr uint32_t kPmAgg = 1u, kPmPre = 2u;
-__device__ __forceinline__ unsigned long long pm_word(uint32_t tag, uint32_t flag, uint32_t mx, uint32_t sum)
-{
-    return ((unsigned long long)tag << 34) | ((unsigned long long)flag << 32) | ((unsigned long long)mx << 22) | sum;
-}
-
-template <int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void k_marshal_invs_pm(uint8_t *ops, int32_t n_workers, int32_t stride,
-                                                         uint32_t op_size, uint8_t *out, int32_t out_stride,
-                                                         int32_t *count, uint32_t machine_id, unsigned long long *held,
-                                                         uint8_t *states, uint8_t *acks, int64_t ack_rs,
-                                                         const uint8_t *peer_ids, int32_t n_peers, int32_t *ack_count,
-                                                         int32_t *off, int32_t *h, int32_t seq,
-                                                         unsigned long long *words, uint32_t tag,
-                                                         unsigned int *error_flags)
-{
-    __shared__ uint32_t s_list[WAVES][256];
-    __shared__ int32_t s_cnt[2 * WAVES];
-    __shared__ int32_t s_base;
-    const int lane = threadIdx.x & 63, wv = (int)(threadIdx.x >> 6);
-    // blocks wait only on blocks of lower index, which the dispatcher starts first (each XCD takes its
-    // blocks in index order), so a waiting block's predecessors run; a ticket drawn by atomicAdd would
-    // order them without that, but 2048 memory-side atomics on one word cost ~40 us (the waits are bounded
-    // in any case)
-    const int vb = (int)blockIdx.x, nblk = (int)gridDim.x;
-    const int wb = (vb * WAVES + wv) * 2;
-    uint8_t st[2][4];
-    unsigned long long bs[2][4];
-    int rank[2][4], sent[2];
-#pragma unroll
-    for (int v = 0; v < 2; ++v) {
-        const bool wl = wb + v < n_workers;
-        const int64_t e0 = (int64_t)(wb + v) * stride;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = r * 64 + lane;
-            st[v][r] = wl && i < stride ? states[e0 + i] : 0;
-        }
-    }
-#pragma unroll
-    for (int v = 0; v < 2; ++v) {
-        const int w = wb + v;
-        const bool wl = w < n_workers;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint8_t x = st[v][r];
-            bs[v][r] = __ballot(wl && r * 64 + lane < stride &&
-                                (x == kPutSuccess || x == kRmwSuccess || x == kReplaySuccess || x == kOpMembChange));
-        }
-        int total;
-        wave_ranks(bs[v], lane, rank[v], total);
-        sent[v] = total < out_stride ? total : out_stride;
-        if (lane == 0) {
-            s_cnt[wv * 2 + v] = wl ? sent[v] : 0;
-            if (wl) {
-                count[w] = sent[v];
-                if (ack_count) ack_count[w] = sent[v] * n_peers;
-                if (total > out_stride && held) atomicAdd(held, (unsigned long long)(total - out_stride));
-            }
-        }
-    }
-    __syncthreads();
-    if (wv == 0) {   // the look-back, a wave at a time: lane k reads the word of block vb - 1 - k
-        uint32_t agg = 0, mx = 0;
-        for (int k = 0; k < 2 * WAVES; ++k) {
-            agg += (uint32_t)s_cnt[k];
-            mx = (uint32_t)s_cnt[k] > mx ? (uint32_t)s_cnt[k] : mx;
-        }
-        uint32_t pre = 0, pmx = 0;
-        unsigned long long *sw = words + 1;
-        if (vb == 0) {
-            if (lane == 0) __hip_atomic_store(sw, pm_word(tag, kPmPre, mx, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0) __hip_atomic_store(sw + vb, pm_word(tag, kPmAgg, mx, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t t0 = wall_clock64();
-            int j0 = vb - 1;
-            for (;;) {
-                const int j = j0 - lane;
-                // before block 0: an inclusive prefix of 0
-                const unsigned long long v = j >= 0 ? __hip_atomic_load(sw + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                                    : pm_word(tag, kPmPre, 0, 0);
-                const bool ready = (uint32_t)(v >> 34) == tag;
-                const unsigned long long pm = __ballot(ready && ((v >> 32) & 3ull) == kPmPre), rm = __ballot(ready);
-                const int lp = pm ? __ffsll((long long)pm) - 1 : 63;   // the nearest inclusive prefix, else all 64
-                const unsigned long long need = lp == 63 ? ~0ull : (1ull << (lp + 1)) - 1ull;
-                if ((rm & need) != need) {   // a block before it has not published yet
-                    if (wall_clock64() - t0 > 100000000ull) {   // 1 s: never expected; fail loudly
-                        if (lane == 0 && error_flags) atomicOr(error_flags, 32u);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                uint32_t sv = lane <= lp ? (uint32_t)(v & 0x3FFFFFull) : 0u;
-                uint32_t mv = lane <= lp ? (uint32_t)((v >> 22) & 0x3FFull) : 0u;
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    sv += (uint32_t)__shfl_xor((int)sv, o, 64);
-                    const uint32_t u = (uint32_t)__shfl_xor((int)mv, o, 64);
-                    mv = u > mv ? u : mv;
-                }
-                pre += sv;
-                pmx = mv > pmx ? mv : pmx;
-                if (pm) break;
-                j0 -= 64;
-            }
-            if (lane == 0)
-                __hip_atomic_store(sw + vb, pm_word(tag, kPmPre, mx > pmx ? mx : pmx, pre + agg), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (lane == 0) {
-            s_base = (int32_t)pre;
-            if (vb == nblk - 1) {
-                const int32_t tot = (int32_t)(pre + agg), m = (int32_t)(mx > pmx ? mx : pmx);
-                off[n_workers] = tot;
-                if (seq == 0) {
-                    h[0] = tot;
-                    h[1] = m;
-                } else {   // as k_ack_offsets: the host spins on h[2]
-                    __hip_atomic_store(h, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    __hip_atomic_store(h + 1, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    __builtin_amdgcn_s_waitcnt(0);
-                    __hip_atomic_store(h + 2, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                }
-            }
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int v = 0; v < 2; ++v) {
-        const int w = wb + v;
-        if (w >= n_workers) break;
-        int o = s_base;
-        for (int k = 0; k < wv * 2 + v; ++k) o += s_cnt[k];
-        if (lane == 0) off[w] = o;
-        // the INVs (wave_copy_invs), each answered right away by every peer
-        uint32_t *lst = s_list[wv];
-        const int64_t e0 = (int64_t)w * stride;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            if (((bs[v][r] >> lane) & 1ull) && rank[v][r] < out_stride)
-                lst[rank[v][r]] = (uint32_t)(r * 64 + lane) | ((uint32_t)st[v][r] << 16);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int q = lane & 3;
-        const uint32_t b0 = 16u * (uint32_t)q;
-        uint8_t *out_w = out + (int64_t)w * out_stride * op_size;
-        for (int j = lane >> 2; j < sent[v]; j += 16) {
-            const uint32_t li = lst[j];
-            const int64_t e = e0 + (int64_t)(li & 0xFFFFu);
-            uint8_t *op = ops + e * op_size;
-            uint8_t *dst = out_w + (int64_t)j * op_size;
-            if (b0 + 16 <= op_size) {
-                W16 hh = *reinterpret_cast<const W16 *>(op + b0);
-                if (q == 0) hh.b = with_op_state(hh.b, kOpInv, (uint8_t)machine_id);
-                *reinterpret_cast<W16 *>(dst + b0) = hh;
-                if (q == 0)   // ack_copy_and_modify_elem of every peer (hermes_worker.c:100-118)
-                    for (int r = 0; r < n_peers; ++r)
-                        *reinterpret_cast<W16 *>(acks + ((int64_t)r * ack_rs + o + j) * 16) =
-                            W16{hh.a, with_op_state(hh.b, kOpAck, peer_ids[r])};
-            } else if (b0 + 8 <= op_size) {
-                *reinterpret_cast<uint64_t *>(dst + b0) = *reinterpret_cast<const uint64_t *>(op + b0);
-            }
-            if (q == 0) {
-                const uint8_t x = (uint8_t)(li >> 16);
-                const uint8_t ns = x == kPutSuccess ? kInProgressPut : x == kRmwSuccess ? kInProgressRmw
-                                 : x == kReplaySuccess ? kInProgressReplay : kOpMembComplete;
-                op[9] = ns;
-                if (states) states[e] = ns;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-}
-
 // HKV_MARSHAL_WAVE: the INV marshals copy the sent ops four lanes per op (1, default) or one lane per op (0)
 static bool marshal_wave()
 {
@@ -2291,34 +2103,6 @@ int hkv_wl_ack_offsets(const int32_t *inv_count, int32_t n_workers, int32_t n_pe
                        offsets, d_out, seq);
     return ok();
 }
-
-int hkv_wl_marshal_invs_pm(hkv_table *t, uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size,
-                           uint8_t *out, int32_t out_stride, int32_t *count, uint32_t machine_id,
-                           unsigned long long *held, uint8_t *states, uint8_t *acks, int64_t ack_rs,
-                           const uint8_t *peer_ids, int32_t n_peers, int32_t *ack_count, int32_t *offsets,
-                           int32_t *h_out, int32_t seq, unsigned long long *words, uint32_t tag, void *stream)
-{
-    TableView tv{};
-    if (table_view(t, &tv)) return -1;
-    if (stride > 256 || n_workers <= 0 || out_stride <= 0 || out_stride > 1023 || op_size % 8 || op_size > 64 ||
-        op_size < 16 || !states || !acks || !offsets || !words || n_peers <= 0 || n_peers > 7 || seq < 0 ||
-        tag == 0 || tag >= (1u << 30) || (int64_t)n_workers * out_stride >= (1 << 22) ||
-        ack_rs < (int64_t)n_workers * out_stride)
-        return -1;
-    int32_t *d_out = nullptr;
-    if (hipHostGetDevicePointer(reinterpret_cast<void **>(&d_out), h_out, 0) != hipSuccess || !d_out) return -1;
-    // 32 workers per block: the look-back walks at most 64 blocks per step, so fewer blocks, fewer steps
-    // for the last ones (8 workers per block: 2048 blocks at configs[1], 47 us against 44 us for the
-    // three kernels it replaces)
-    constexpr int kWaves = 16;
-    hipLaunchKernelGGL(k_marshal_invs_pm<kWaves>, dim3((unsigned)((n_workers + 2 * kWaves - 1) / (2 * kWaves))),
-                       dim3(64 * kWaves), 0, (hipStream_t)stream,
-                       ops, n_workers, stride, op_size, out, out_stride, count, machine_id, held, states, acks, ack_rs,
-                       peer_ids, n_peers, ack_count, offsets, d_out, seq, words, tag, tv.error_flags);
-    return ok();
-}
-
-uint64_t hkv_wl_marshal_invs_pm_words(int32_t n_workers) { return 8ull * (2 + (uint64_t)(n_workers + 7) / 8); }   // (>= 1 + blocks)
 
 int hkv_wl_marshal_invs_packed(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t op_size, uint8_t *states,
                                int32_t C, int32_t cap, uint8_t *out, int32_t *offsets, int32_t *count, int32_t *sent,

@@ -72,13 +72,6 @@ _L.hkv_wl_peer_acks_queue.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32
 _L.hkv_wl_vals_credit.argtypes = [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_int32,
                                   _P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P]
 _L.hkv_wl_ack_offsets.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, _P]
-_L.hkv_wl_marshal_invs_pm.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
-                                      ctypes.c_uint32, _P, _P, _P, ctypes.c_int64, _P, ctypes.c_int32, _P, _P, _P,
-                                      ctypes.c_int32, _P, ctypes.c_uint32, _P]
-_L.hkv_wl_marshal_invs_pm_words.restype = ctypes.c_uint64
-_L.hkv_wl_marshal_invs_pm_words.argtypes = [ctypes.c_int32]
-_L.hkv_wl_collect_vals_rows.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, _P,
-                                        ctypes.c_int32, _P, ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_pack_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_peer_locate.argtypes = [_P, _P, ctypes.c_int64, ctypes.c_uint32, _P, _P]
 _L.hkv_wl_peer_ts_at.argtypes = [_P, _P, _P, _P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
@@ -351,17 +344,6 @@ class Round:
         if self.ackoff_side:
             self.side2 = torch.cuda.Stream(device=dev)
             self.ao_start, self.ao_done = torch.cuda.Event(), torch.cuda.Event()
-        # the INV marshal, the ACK offsets and the virtual peers' ACKs as one pass (hkv_wl_marshal_invs_pm:
-        # a look-back scan over blocks of workers), peer r's ACK row at r * ack_rs (HKV_FUSED_MARSHAL=0: the
-        # three kernels, rows the round's total apart)
-        self.pm_fused = (self.ack_pm and val_credits is None and not kvs.rmw and self.op <= 64 and self.ack_size == 16
-                         and self.LOCAL <= 256 and self.C < 1024 and W * self.C < (1 << 22) and 0 < self.R <= 7
-                         and os.environ.get("HKV_FUSED_MARSHAL", "0") == "1")
-        self.ack_rs = W * self.C if self.pm_fused else 0
-        if self.pm_fused:
-            self.pm_words = torch.zeros(int(_L.hkv_wl_marshal_invs_pm_words(W)) // 8, dtype=torch.int64, device=dev)
-            self.pm_tag = 0
-        self._pm_done = False          # this round's ACKs and offsets came with the marshal
         self.acks = torch.zeros(W * self.ack_stride * self.ack_size, **u8)
         self.ack_count = torch.zeros(W, dtype=torch.int32, device=dev)
         self.val_out = torch.zeros(W * self.ack_stride * L.OP_META_SIZE, **u8)
@@ -608,12 +590,7 @@ class Round:
         self._local(2)
         self.pre_pending = False
 
-    def marshal_invs(self, n_peers: int = 0):
-        """This round's INVs into inv_out [W][C]; with pm_fused and n_peers > 0 also the ACK offsets and the
-        first n_peers virtual peers' ACKs (_marshal_pm)"""
-        if n_peers and self.pm_fused:
-            self._marshal_pm(n_peers)
-            return
+    def marshal_invs(self):
         if self.V is not None:
             check(_L.hkv_wl_marshal_invs_credits(_ptr(self.ops), self.W, self.LOCAL, self.op, _ptr(self.inv_out),
                                                  self.C, _ptr(self.inv_count), self.machine_id, _ptr(self.held),
@@ -623,23 +600,9 @@ class Round:
                                          _ptr(self.inv_count), self.machine_id, _ptr(self.held), _ptr(self.states),
                                          _s()), "marshal_invs")
 
-    def _marshal_pm(self, n_peers: int):
-        """marshal_invs, the ACK offsets and the first n_peers virtual peers' ACKs in one pass
-        (hkv_wl_marshal_invs_pm): ack_off, the host's total / largest count / flag, and peer r's ACK row
-        at acks[r * ack_rs]"""
-        self.pm_tag = self.pm_tag % ((1 << 30) - 1) + 1
-        check(_L.hkv_wl_marshal_invs_pm(self.kvs.h, _ptr(self.ops), self.W, self.LOCAL, self.op, _ptr(self.inv_out),
-                                        self.C, _ptr(self.inv_count), self.machine_id, _ptr(self.held),
-                                        _ptr(self.states), _ptr(self.acks), self.ack_rs, _ptr(self.peer_t), n_peers,
-                                        _ptr(self.ack_count), _ptr(self.ack_off), _ptr(self.maxc_h), self._ack_seq,
-                                        _ptr(self.pm_words), self.pm_tag, _s()), "marshal_invs_pm")
-        self._pm_done = True
-
     def virtual_peer_acks(self, n_peers: int | None = None):
         """ACKs (INV-aborts for RMWs a peer's own write beats) of the first n_peers virtual peers
-        (default all) to this round's INVs (already written when the marshal made them: _pm_done)"""
-        if self._pm_done:
-            return
+        (default all) to this round's INVs"""
         if self.ack_pm:
             check(_L.hkv_wl_peer_acks_pm(self.kvs.h, _ptr(self.inv_out), _ptr(self.inv_count), self.W, self.C,
                                          self.op, _ptr(self.acks), self.ack_size, self.ack_m,
@@ -722,16 +685,15 @@ class Round:
         if self.fit and stride is None and self.ack_pm:   # one launch per peer, in peer order
             T = self.inv_round
             n_rows = self.ack_total // max(T, 1) if T else 0
-            rs = self.ack_rs if self._pm_done else T   # the rows' stride: fixed when the marshal wrote them
             if self.ack_rows and n_rows:
                 self.kvs.batch(L.BatchType.acks, acks, self.W, T, self.ack_size, self.mb, rw=self.ops,
                                rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off, rw_state=self._rws(),
-                               unique=True, rows=(n_rows, max(rs, T), -1), rw_opcodes=self._rwo(),
+                               unique=True, rows=(n_rows, T, -1), rw_opcodes=self._rwo(),
                                ack_out=self.val_out if self.fused_vals else None)
                 self._vals_made = self.fused_vals
                 return
             for r in range(n_rows):
-                self.kvs.batch(L.BatchType.acks, acks[r * rs * self.ack_size:], self.W, T, self.ack_size, self.mb,
+                self.kvs.batch(L.BatchType.acks, acks[r * T * self.ack_size:], self.W, T, self.ack_size, self.mb,
                                rw=self.ops, rw_stride_bytes=self.LOCAL * self.op, offsets=self.ack_off,
                                rw_state=self._rws(), unique=True, rw_opcodes=self._rwo())
             return
@@ -754,11 +716,6 @@ class Round:
         ACK rows launch made them itself (fused_vals: val_out then holds them in the ACKs' positions)."""
         if self._vals_made:
             self._vals_made = False
-            return
-        if self.ack_pm and self._pm_done and self.inv_round:   # rows ack_rs apart
-            check(_L.hkv_wl_collect_vals_rows(_ptr(self.acks), self.W, self.ack_total // self.inv_round, self.ack_rs,
-                                              self.ack_size, _ptr(self.val_out), self.C, _ptr(self.val_count),
-                                              self.machine_id, None, _ptr(self.ack_off), _s()), "collect_vals")
             return
         if self.ack_pm:
             check(_L.hkv_wl_collect_vals_blocks(_ptr(self.acks), _ptr(self.ack_count), self.W, self.ack_width,
@@ -842,17 +799,10 @@ class Round:
         timed("local", self.local_batch)
         if self.audit is not None:
             self.audit.post_local()
-        self._pm_done = False
-        if self.pm_fused and self.fit and alive:   # the marshal also lays out and writes the peers' ACKs
-            self._ack_seq = self._ack_seq % 0x7FFFFFFF + 1 if self.ack_spin else 0
-            self.marshal_invs(alive)
-            if self._pm_done and not self.ack_spin:
-                self.maxc_ev.record()
-        else:
-            self.marshal_invs()
+        self.marshal_invs()
         if self.count_elems:
             self.inv_total += self.inv_count.sum()
-        if self.fit and alive and not self._pm_done:
+        if self.fit and alive:
             self._ack_seq = self._ack_seq % 0x7FFFFFFF + 1 if self.ack_spin else 0
             if self.ackoff_side:   # one workgroup: beside the INV batch, which does not need it
                 self.ao_start.record()

@@ -206,21 +206,6 @@ int hkv_wl_peer_acks_pm(hkv_table *t, const uint8_t *d_inv_out, const int32_t *d
 int hkv_wl_ack_offsets(const int32_t *d_inv_count, int32_t n_workers, int32_t n_peers, int32_t *d_offsets,
                        int32_t *h_out, int32_t seq, void *stream);
 
-/* hkv_wl_marshal_invs_cap (d_inv_count, d_out [n_workers][out_stride]), hkv_wl_ack_offsets with n_peers
- * = 1 (d_offsets, h_out, seq) and hkv_wl_peer_acks_pm in one pass, for 16-byte ACKs without d_peer_ts
- * (the N = 1 round's default): peer r's ACK to INV j of worker w goes to element
- * r * ack_rs + d_offsets[w] + j of d_acks, so the rows are ack_rs apart (ack_rs >= n_workers *
- * out_stride) instead of the round's total apart. d_words: hkv_wl_marshal_invs_pm_words(n_workers)
- * zeroed bytes, kept between calls (a ticket and one look-back word per 8 workers); tag: this call's
- * round tag, 1 .. 2^30 - 1, different from the previous call's. ops of at most 64 bytes, stride <=
- * 256, out_stride < 1024, n_workers * out_stride < 2^22, 1..7 peers. */
-int hkv_wl_marshal_invs_pm(hkv_table *t, uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op_size,
-                           uint8_t *d_out, int32_t out_stride, int32_t *d_inv_count, uint32_t machine_id,
-                           unsigned long long *d_held, uint8_t *d_states, uint8_t *d_acks, int64_t ack_rs,
-                           const uint8_t *d_peer_ids, int32_t n_peers, int32_t *d_ack_count, int32_t *d_offsets,
-                           int32_t *h_out, int32_t seq, unsigned long long *d_words, uint32_t tag, void *stream);
-uint64_t hkv_wl_marshal_invs_pm_words(int32_t n_workers);
-
 /* ---- replica groups (one replica per GPU, slabs exchanged over RCCL) ------------------ */
 
 /* VALs of the writes/replays a membership change completed (memb_change_* callbacks,

@@ -272,72 +272,3 @@ def test_pack_and_regroup():
         assert goc[w] == len(keep), w
         for k, e in enumerate(keep):
             assert np.array_equal(got[w, k], e), (w, k)
-
-
-@pytest.mark.parametrize("W,C,n_peers", [(1001, 24, 2), (64, 40, 7), (8, 250, 1)])
-def test_marshal_invs_pm_matches_three_passes(W, C, n_peers):
-    """hkv_wl_marshal_invs_pm (the N = 1 round's INV marshal, ACK offsets and virtual peers' ACKs in one
-    pass, a look-back scan over blocks of workers) against hkv_wl_marshal_invs_cap + hkv_wl_ack_offsets
-    + hkv_wl_peer_acks_pm on the same ops: INV slab, counts, held INVs, op states and their mirror,
-    offsets, the host's total and largest count, the ACK counts, and every peer's ACK row (rows ack_rs
-    apart instead of the total apart). Three rounds in a row, so the ticket reset and the round tags
-    are exercised (W not a multiple of 8 in one case)."""
-    from hermes_amd.kvs import HermesKV
-    WL = _wl()
-    _L = WL._L
-    S, op = 250, 56
-    g = HermesKV(1000, 1 << 10, 1 << 20, machine_id=0)
-    rng = np.random.default_rng(W * 7 + C)
-    words = torch.zeros(int(_L.hkv_wl_marshal_invs_pm_words(W)) // 8, dtype=torch.int64, device="cuda")
-    peers = _dev(np.arange(1, n_peers + 1, dtype=np.uint8))
-    sendable = [int(R.PUT_SUCCESS), int(R.RMW_SUCCESS), int(R.REPLAY_SUCCESS), int(L.Op.MEMBERSHIP_CHANGE)]
-    for rnd in range(3):
-        ops = rng.integers(0, 256, size=(W * S, op), dtype=np.uint8)
-        st = np.where(rng.random(W * S) < 0.12, rng.choice(np.array(sendable, np.uint8), W * S),
-                      rng.choice(np.array([int(R.GET_COMPLETE), int(B.EMPTY), 0], np.uint8), W * S)).astype(np.uint8)
-        ops[:, 9] = st
-        outs = []
-        for fused in (False, True):
-            d_ops, d_st = _dev(ops.reshape(-1)), _dev(st)
-            d_inv = torch.zeros(W * C * op, dtype=torch.uint8, device="cuda")
-            d_cnt = torch.zeros(W, dtype=torch.int32, device="cuda")
-            d_held = torch.zeros(1, dtype=torch.int64, device="cuda")
-            d_off = torch.zeros(W + 1, dtype=torch.int32, device="cuda")
-            d_ac = torch.zeros(W, dtype=torch.int32, device="cuda")
-            h = torch.zeros(4, dtype=torch.int32, pin_memory=True)
-            rs = W * C
-            d_acks = torch.zeros(n_peers * rs * 16, dtype=torch.uint8, device="cuda")
-            if fused:
-                WL.check(_L.hkv_wl_marshal_invs_pm(g.h, WL._ptr(d_ops), W, S, op, WL._ptr(d_inv), C, WL._ptr(d_cnt), 0,
-                                                   WL._ptr(d_held), WL._ptr(d_st), WL._ptr(d_acks), rs, WL._ptr(peers),
-                                                   n_peers, WL._ptr(d_ac), WL._ptr(d_off), WL._ptr(h), rnd + 1,
-                                                   WL._ptr(words), rnd + 1, None), "marshal_invs_pm")
-            else:
-                WL.check(_L.hkv_wl_marshal_invs_cap(WL._ptr(d_ops), W, S, op, WL._ptr(d_inv), C, WL._ptr(d_cnt), 0,
-                                                    WL._ptr(d_held), WL._ptr(d_st), None), "marshal_invs")
-                WL.check(_L.hkv_wl_ack_offsets(WL._ptr(d_cnt), W, 1, WL._ptr(d_off), WL._ptr(h), rnd + 1, None),
-                         "ack_offsets")
-                WL.check(_L.hkv_wl_peer_acks_pm(g.h, WL._ptr(d_inv), WL._ptr(d_cnt), W, C, op, WL._ptr(d_acks), 16, C,
-                                                WL._ptr(d_ac), WL._ptr(peers), n_peers, None, 0, WL._ptr(d_off), None),
-                         "peer_acks_pm")
-            torch.cuda.synchronize()
-            cnt = d_cnt.cpu().numpy()
-            T = int(d_off[W].item())
-            inv = d_inv.cpu().numpy().reshape(W, C, op)
-            acks = d_acks.cpu().numpy().reshape(n_peers, -1, 16)
-            row_at = rs if fused else T
-            a = d_acks.cpu().numpy().reshape(-1, 16)
-            outs.append(dict(cnt=cnt, held=int(d_held.item()), ops=d_ops.cpu().numpy(), st=d_st.cpu().numpy(),
-                             off=d_off.cpu().numpy(), h=h.numpy()[:3].copy(), ac=d_ac.cpu().numpy(),
-                             inv=[inv[w, :cnt[w]].copy() for w in range(W)],
-                             acks=[a[r * row_at: r * row_at + T].copy() for r in range(n_peers)]))
-            del acks
-        A, Bf = outs
-        assert np.array_equal(A["cnt"], Bf["cnt"]) and A["held"] == Bf["held"]
-        assert np.array_equal(A["ops"], Bf["ops"]) and np.array_equal(A["st"], Bf["st"])
-        assert np.array_equal(A["off"], Bf["off"]) and np.array_equal(A["h"], Bf["h"]), (A["h"], Bf["h"])
-        assert np.array_equal(A["ac"], Bf["ac"])
-        assert all(np.array_equal(x, y) for x, y in zip(A["inv"], Bf["inv"]))
-        assert all(np.array_equal(x, y) for x, y in zip(A["acks"], Bf["acks"]))
-        assert int(A["off"][W]) == int(A["cnt"].sum()) and int(A["h"][1]) == int(A["cnt"].max())
-    assert g.take_error_flags() == 0

@@ -1228,10 +1228,22 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
 #else
 #define HKV_DBG_ON(a, bit) false
 #endif
-constexpr int kPreElems = 1024;          // elements per k_local_pre block
-constexpr int kPreHead = 1024;           // launch head whose PUT keys every block knows
+// Round 5: 2048 elements per block (512 threads), a 2048-slot table: each block looks up and offers
+// each of its PUT keys once, so doubling the block removes the second lookup of the keys two 1024-element
+// halves shared, and the two head elements per thread instead of four cut registers. Same box, 3 x 20
+// steps (gpurun_out/r05v): prepass 76.1 -> 64.2 us, 4.25-4.29 -> 4.27-4.36 G ops/s; 1536 (86 us), 4096 (78 us),
+// a 2048-element head (79 us) and a 4096-slot table (111 us) were slower
+#ifndef HKV_PRE_ELEMS
+#define HKV_PRE_ELEMS 2048
+#endif
+constexpr int kPreElems = HKV_PRE_ELEMS;   // elements per k_local_pre block (HKV_PRE_ELEMS: a build macro for A/B)
+constexpr int kPreThreads = kPreElems / 4; // four of its own elements per thread
+#ifndef HKV_PRE_HEAD_ELEMS
+#define HKV_PRE_HEAD_ELEMS 1024
+#endif
+constexpr int kPreHead = HKV_PRE_HEAD_ELEMS;   // launch head whose PUT keys every block knows
 #ifndef HKV_PRE_HASH_SLOTS
-#define HKV_PRE_HASH_SLOTS 1024
+#define HKV_PRE_HASH_SLOTS 2048
 #endif
 constexpr int kPreHash = HKV_PRE_HASH_SLOTS;   // LDS slots of a (key -> first PUT) table (a power of two)
 constexpr int kLfElems = 32;             // elements per k_local_fused block (one wave)
@@ -1321,7 +1333,10 @@ __global__ __launch_bounds__(256) void k_apply_patch(uint8_t *elems, const uint8
         for (uint32_t k = 0; k < st_value; ++k) x[kOpValueOff + k] = fill;
 }
 
-__device__ __forceinline__ uint32_t pre_slot(uint64_t key) { return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 54) & (kPreHash - 1); }
+__device__ __forceinline__ uint32_t pre_slot(uint64_t key)
+{
+    return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - __builtin_ctz(kPreHash))) & (kPreHash - 1);
+}
 
 // (key -> smallest element) in an LDS table of kPreHash slots, key ~0 the empty mark; false when the
 // key cannot go in (key ~0 itself, or a full table)
@@ -1373,7 +1388,7 @@ constexpr int kPrePair = 4;
 // NT (the default, with k_local_fused's F loads beside every hit's line): no seqlock-byte tags -- the
 // fused pass reads every hit's F word and needs no mark of the keys that have one
 template <int HEAD = kPreHead, bool H = false, bool NT = false>
-__global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
+__global__ __launch_bounds__(kPreThreads) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 {
     __shared__ uint64_t hk[kPreHash], gk[kPreHash];  // the block's PUT keys, the head's
     __shared__ uint32_t hv[kPreHash];
@@ -1384,7 +1399,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
         nd = 0;
         if (blockIdx.x == 0) a.ctr[kCtrDefer] = 0;
     }
-    for (int j = tid; j < kPreHash; j += 256) {
+    for (int j = tid; j < kPreHash; j += kPreThreads) {
         hk[j] = ~0ull;
         gk[j] = ~0ull;
         hv[j] = kNone;
@@ -1396,7 +1411,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
     // pass over the whole op slab; with the caller's opcode mirror only the PUTs' headers are read
     // (the others read element 0's, one cached line; k_local_fused checks the mirror against every
     // element's opcode). Loads are unconditional and all issued before the first is used.
-    constexpr int kOwnK = kPreElems / 256, kAllK = kPreElems / 256 + HEAD / 256;
+    constexpr int kOwnK = kPreElems / kPreThreads, kAllK = kOwnK + (HEAD + kPreThreads - 1) / kPreThreads;
     U64x2 h[kAllK];
     bool in[kAllK];
     uint8_t opm[kAllK];
@@ -1410,7 +1425,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 #pragma unroll
         for (int k = 0; k < kAllK; ++k) {
             const bool own = k < kOwnK;
-            const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
+            const int64_t i = own ? i0 + k * kPreThreads + tid : (int64_t)(k - kOwnK) * kPreThreads + tid;
             in[k] = i < a.n && (own || i < head_end);
             pk[k] = in[k] ? a.pkeys[i] : ~0ull;
             ps[k] = in[k] ? a.state_out[i] : (uint8_t)0;
@@ -1426,7 +1441,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 #pragma unroll
     for (int k = 0; k < kAllK; ++k) {
         const bool own = k < kOwnK;
-        const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
+        const int64_t i = own ? i0 + k * kPreThreads + tid : (int64_t)(k - kOwnK) * kPreThreads + tid;
         in[k] = i < a.n && (own || i < head_end);
         opm[k] = a.opc ? a.opc[in[k] ? i : 0] : (uint8_t)kOpPut;
     }
@@ -1437,20 +1452,20 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 #pragma unroll
         for (int k = 0; k < kAllK; ++k) {
             const bool own = k < kOwnK;
-            const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
+            const int64_t i = own ? i0 + k * kPreThreads + tid : (int64_t)(k - kOwnK) * kPreThreads + tid;
             pt[k] = in[k] && opm[k] == kOpPut ? *reinterpret_cast<const U64x2 *>(a.patch + i * 16) : U64x2{0, 0};
         }
 #pragma unroll
         for (int k = 0; k < kAllK; ++k) {
             const bool own = k < kOwnK;
-            const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
+            const int64_t i = own ? i0 + k * kPreThreads + tid : (int64_t)(k - kOwnK) * kPreThreads + tid;
             h[k] = *reinterpret_cast<const U64x2 *>(a.elems + (in[k] && opm[k] == kOpPut && !patch_valid(pt[k].b) ? i : 0) * 56);
         }
     } else {
 #pragma unroll
         for (int k = 0; k < kAllK; ++k) {
             const bool own = k < kOwnK;
-            const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
+            const int64_t i = own ? i0 + k * kPreThreads + tid : (int64_t)(k - kOwnK) * kPreThreads + tid;
             h[k] = *reinterpret_cast<const U64x2 *>(a.elems + (in[k] && opm[k] == kOpPut ? i : 0) * 56);
             pt[k] = a.patch && in[k] && opm[k] == kOpPut ? *reinterpret_cast<const U64x2 *>(a.patch + i * 16) : U64x2{0, 0};
         }
@@ -1465,7 +1480,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 #pragma unroll
     for (int k = 0; k < kAllK; ++k) {
         const bool own = k < kOwnK;
-        const int64_t i = own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid;
+        const int64_t i = own ? i0 + k * kPreThreads + tid : (int64_t)(k - kOwnK) * kPreThreads + tid;
         // a non-PUT read element 0's raw header, which a patch may have made stale: only the
         // mirror's PUTs take part
         in[k] = in[k] && opm[k] == kOpPut && in_count(a, (uint32_t)i);
@@ -1481,7 +1496,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 #pragma unroll
     for (int k = 0; k < kAllK; ++k) {
         const bool own = k < kOwnK;
-        const uint32_t i = (uint32_t)(own ? i0 + k * 256 + tid : (int64_t)(k - kOwnK) * 256 + tid);
+        const uint32_t i = (uint32_t)(own ? i0 + k * kPreThreads + tid : (int64_t)(k - kOwnK) * kPreThreads + tid);
         const uint64_t key = h[k].a;
         if (!(in[k] && (uint8_t)h[k].b == kOpPut && !skip_elem_os(kLocal, kOpPut, (uint8_t)(h[k].b >> 8)))) continue;
         bool created;
@@ -1499,7 +1514,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
     const Ctx c = make_ctx(a);
     const uint64_t hput[2] = {0, (uint64_t)kOpPut};
     const uint32_t cnt = HKV_DBG_ON(a, 2) ? 0 : nd;
-    for (uint32_t base = 0; base < cnt; base += 64 * kPrePair) {
+    for (uint32_t base = 0; base < cnt; base += (kPreThreads / 4) * kPrePair) {
         uint64_t key[kPrePair];
         bool probe[kPrePair], ok[kPrePair];
         uint32_t idx[kPrePair];
@@ -1507,7 +1522,7 @@ __global__ __launch_bounds__(256) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
         uint4 ln[kPrePair];
 #pragma unroll
         for (int k = 0; k < kPrePair; ++k) {
-            const uint32_t j = base + k * 64 + (tid >> 2);
+            const uint32_t j = base + k * (kPreThreads / 4) + (tid >> 2);
             probe[k] = j < cnt;
             const uint32_t d = probe[k] ? dl[j] : 0u;
             idx[k] = !probe[k] ? kNone : d < (uint32_t)kPreHash ? hv[d] : ~d;
@@ -3462,11 +3477,11 @@ static void launch_local_pre(const BatchArgs &a, int64_t n, hipStream_t s)
     static const int head = getenv("HKV_PRE_HEAD") ? atoi(getenv("HKV_PRE_HEAD")) : kPreHead;
     const dim3 grid((unsigned)((n + kPreElems - 1) / kPreElems));
     if (a.pre_notag && !a.cancel && !a.phys_hint && head == kPreHead)
-        hipLaunchKernelGGL((k_local_pre<kPreHead, false, true>), grid, dim3(256), 0, s, a);
-    else if (a.phys_hint) hipLaunchKernelGGL((k_local_pre<kPreHead, true>), grid, dim3(256), 0, s, a);
-    else if (head == 256) hipLaunchKernelGGL(k_local_pre<256>, grid, dim3(256), 0, s, a);
-    else if (head == 512) hipLaunchKernelGGL(k_local_pre<512>, grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_local_pre<kPreHead>, grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((k_local_pre<kPreHead, false, true>), grid, dim3(kPreThreads), 0, s, a);
+    else if (a.phys_hint) hipLaunchKernelGGL((k_local_pre<kPreHead, true>), grid, dim3(kPreThreads), 0, s, a);
+    else if (head == 256) hipLaunchKernelGGL(k_local_pre<256>, grid, dim3(kPreThreads), 0, s, a);
+    else if (head == 512) hipLaunchKernelGGL(k_local_pre<512>, grid, dim3(kPreThreads), 0, s, a);
+    else hipLaunchKernelGGL(k_local_pre<kPreHead>, grid, dim3(kPreThreads), 0, s, a);
 }
 
 int launch_batch(BatchLaunch &bl, hipStream_t s)

@@ -1379,7 +1379,10 @@ __device__ __forceinline__ void pre_insert_key(uint64_t *hk, uint64_t key)
 // keys of the PUTs among the launch's first kPreHead elements (before its own; headers only,
 // L2-resident after the first block) and drops its keys that have a PUT there -- an earlier block
 // offers that one. Four keys per lane group are in flight; the offer is a plain atomicMin.
-constexpr int kPrePair = 4;
+#ifndef HKV_PRE_PAIR
+#define HKV_PRE_PAIR 4
+#endif
+constexpr int kPrePair = HKV_PRE_PAIR;   // keys per lane group in flight in the prepass's lookups (a build macro for A/B)
 #ifdef HKV_PRE_WAVES
 #define HKV_PRE_ATTR __attribute__((amdgpu_waves_per_eu(HKV_PRE_WAVES)))
 #else

@@ -3284,9 +3284,10 @@ __global__ __launch_bounds__(kHpThreads) void k_hserve(HostServeLaunch p)
     uint64_t idle_since = t0;
     for (;;) {
         const HostRingSlot *sl = p.ring + (next % (uint32_t)p.ring_n);
-        if (tid < 64) {
-            int cmd = 0;
+        constexpr int HW = (int)(sizeof(HostPartHdr) / 8);
+        if (p.spec) {   // thread 0 polls alone; the scan below runs beside the first launch's header loads
             if (tid == 0) {
+                int cmd = 0;
                 for (;;) {
                     if (ld_sys32(&sl->seq) == next) {
                         cmd = 1;
@@ -3301,7 +3302,29 @@ __global__ __launch_bounds__(kHpThreads) void k_hserve(HostServeLaunch p)
                 }
                 L.cmd = cmd;
             }
-            cmd = __shfl(cmd, 0);
+            __syncthreads();
+            if (L.cmd == 2) break;
+        }
+        if (tid < 64) {
+            int cmd = 1;
+            if (!p.spec) {
+                if (tid == 0) {
+                    for (;;) {
+                        if (ld_sys32(&sl->seq) == next) {
+                            cmd = 1;
+                            break;
+                        }
+                        const uint64_t now = wall_clock64();
+                        if (ld_sys32(p.stop) || now - idle_since > p.idle_ticks || now - t0 > p.life_ticks) {
+                            cmd = 2;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(4);
+                    }
+                    L.cmd = cmd;
+                }
+                cmd = __shfl(cmd, 0);
+            }
             if (cmd == 1) {   // this launch and the ones published after it while their batches fit: lane k
                               // reads launch next + k's seq and batch count, all loads in flight together
                 const HostRingSlot *sk = p.ring + ((next + (uint32_t)tid) % (uint32_t)p.ring_n);
@@ -3324,6 +3347,14 @@ __global__ __launch_bounds__(kHpThreads) void k_hserve(HostServeLaunch p)
                     L.nm = nm;
                 }
             }
+        } else if (p.spec) {   // launch `next` is published: all kPartMaxB of its headers and rows g, g + 1
+            const int u = tid - 64;
+            if (u < HW * kPartMaxB) {
+                reinterpret_cast<uint64_t *>(L.bh)[u] = ld_sys64(reinterpret_cast<const uint64_t *>(sl->hdr) + u);
+            } else if (u < HW * kPartMaxB + 2 * kPartMaxB) {
+                const int q = u - HW * kPartMaxB, row = q / kPartMaxB, b = q % kPartMaxB;
+                L.prow[row][b] = (uint16_t)ld_sys_u16(&sl->part[g + row][b]);
+            }
         }
         __syncthreads();
         if (L.cmd == 2) break;
@@ -3331,23 +3362,27 @@ __global__ __launch_bounds__(kHpThreads) void k_hserve(HostServeLaunch p)
         const uint64_t t_seen = pr ? wall_clock64() : 0;
         const int nm = L.nm, nbt = L.sb[nm];
         // the headers (8 bytes per thread) and part rows g and g + 1 (2 bytes per thread) of every launch
-        // taken, its batches after the previous launch's
-        constexpr int HW = (int)(sizeof(HostPartHdr) / 8);
-        if (tid < HW * nbt) {
-            const int b = tid / HW;
-            int k = 0;
-            while (L.sb[k + 1] <= b) ++k;
-            const HostRingSlot *sk = p.ring + ((next + (uint32_t)k) % (uint32_t)p.ring_n);
-            reinterpret_cast<uint64_t *>(L.bh)[tid] =
-                ld_sys64(reinterpret_cast<const uint64_t *>(sk->hdr) + (tid - HW * L.sb[k]));
-        } else if (tid >= 128 && tid < 128 + 2 * nbt) {
-            const int q = tid - 128, row = q / nbt, b = q % nbt;
-            int k = 0;
-            while (L.sb[k + 1] <= b) ++k;
-            const HostRingSlot *sk = p.ring + ((next + (uint32_t)k) % (uint32_t)p.ring_n);
-            L.prow[row][b] = (uint16_t)ld_sys_u16(&sk->part[g + row][b - L.sb[k]]);
+        // taken, its batches after the previous launch's (p.spec: the first launch's came beside the scan)
+        const int bfrom = p.spec ? L.sb[1] : 0;
+        if (bfrom < nbt) {
+            if (tid >= HW * bfrom && tid < HW * nbt) {
+                const int b = tid / HW;
+                int k = 0;
+                while (L.sb[k + 1] <= b) ++k;
+                const HostRingSlot *sk = p.ring + ((next + (uint32_t)k) % (uint32_t)p.ring_n);
+                reinterpret_cast<uint64_t *>(L.bh)[tid] =
+                    ld_sys64(reinterpret_cast<const uint64_t *>(sk->hdr) + (tid - HW * L.sb[k]));
+            } else if (tid >= 128 && tid < 128 + 2 * nbt) {
+                const int q = tid - 128, row = q / nbt, b = q % nbt;
+                if (b >= bfrom) {
+                    int k = 0;
+                    while (L.sb[k + 1] <= b) ++k;
+                    const HostRingSlot *sk = p.ring + ((next + (uint32_t)k) % (uint32_t)p.ring_n);
+                    L.prow[row][b] = (uint16_t)ld_sys_u16(&sk->part[g + row][b - L.sb[k]]);
+                }
+            }
+            __syncthreads();
         }
-        __syncthreads();
         if (tid == 0) {   // partition g of the taken launches within kPartCap elements (the first always is)
             int k = 1, tot = 0;
             for (int b = 0; b < L.sb[1]; ++b) tot += L.prow[1][b] - L.prow[0][b];

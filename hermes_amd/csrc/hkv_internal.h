@@ -140,6 +140,7 @@ struct HostServeLaunch {
     uint64_t idle_ticks, life_ticks;   // wall_clock64 ticks (100 MHz)
     int32_t merge;               // launches one workgroup pass may take together (HKV_SERVE_MERGE; 1: one at a time)
     uint32_t start[kPartG];      // the first launch each workgroup takes
+    int32_t spec;                // the first launch's headers read beside the merge scan (HKV_SERVE_SPEC)
 };
 int launch_host_serve(const HostServeLaunch &sl, hipStream_t s);
 int launch_host_part(const HostPartLaunch &pl, hipStream_t s);

@@ -1075,6 +1075,8 @@ static void srv_ensure(hkv_table *t)
     sl.life_ticks = (uint64_t)1e8;                 // 1 s, then a fresh server
     static const int merge = getenv("HKV_SERVE_MERGE") ? std::max(1, atoi(getenv("HKV_SERVE_MERGE"))) : kServeMerge;
     sl.merge = std::min(merge, kRingN / 2);
+    static const int spec = !getenv("HKV_SERVE_SPEC") || atoi(getenv("HKV_SERVE_SPEC")) != 0;
+    sl.spec = spec;
     for (int g = 0; g < kPartG; ++g) sl.start[g] = __atomic_load_n(t->pflags + g, __ATOMIC_ACQUIRE) + 1;
     srv_set_stop(t, 0u);
     if (!t->srv_ev && hipEventCreateWithFlags(&t->srv_ev, hipEventDisableTiming) != hipSuccess) die("event");

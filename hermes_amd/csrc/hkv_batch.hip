@@ -1057,7 +1057,10 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
 // all their loads are issued before the first store, so a wave waits one memory latency per
 // kVcBatch values instead of one per value (HKV_VC_BATCH=1: one at a time). Every lane of the wave
 // calls it.
-constexpr int kVcBatch = 4;
+#ifndef HKV_VC_BATCH_N
+#define HKV_VC_BATCH_N 4
+#endif
+constexpr int kVcBatch = HKV_VC_BATCH_N;
 template <int VB>
 __device__ __forceinline__ void wave_value_copies_n(const VCopy &v, uint32_t n)
 {
@@ -1099,8 +1102,94 @@ __device__ __forceinline__ void wave_value_copies_n(const VCopy &v, uint32_t n)
     }
 }
 
+// bytes [lo, hi) of the 8-byte word v to the 8-byte aligned p, in aligned 1/2/4-byte stores (the
+// word's other bytes are other fields: op header, entry meta)
+__device__ __forceinline__ void store_word_part(uint8_t *p, uint64_t v, uint32_t lo, uint32_t hi)
+{
+    for (uint32_t b = lo; b < hi;) {
+        if ((b & 3) == 0 && b + 4 <= hi) {
+            *reinterpret_cast<uint32_t *>(p + b) = (uint32_t)(v >> (8 * b));
+            b += 4;
+        } else if ((b & 1) == 0 && b + 2 <= hi) {
+            *reinterpret_cast<uint16_t *>(p + b) = (uint16_t)(v >> (8 * b));
+            b += 2;
+        } else {
+            p[b] = (uint8_t)(v >> (8 * b));
+            b += 1;
+        }
+    }
+}
+
+// wave_value_copies_n by 8-byte words: lane k stores the destination's aligned word k (the two end
+// words byte-exact), built from the aligned source words k and k + 1 (the latter from lane k + 1), so
+// a 287-byte value is 37 lanes of one load and one store instead of five byte instructions each way
+// (the op value sits at byte 18 and the entry value at byte 33, so the two ends differ mod 8). Only
+// source words holding a byte of the value are loaded.
+template <int VB>
+__device__ __forceinline__ void wave_value_words_n(const VCopy &v, uint32_t n)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    unsigned long long todo = __ballot(v.dst != nullptr);
+    while (todo) {
+        uint8_t *dp[VB];
+        const uint8_t *sp[VB];
+#pragma unroll
+        for (int u = 0; u < VB; ++u) {
+            dp[u] = nullptr;
+            sp[u] = nullptr;
+            if (todo) {
+                const int j = __ffsll((long long)todo) - 1;
+                todo &= todo - 1;
+                const uint64_t d = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(uintptr_t)v.dst, j, 64) |
+                                   ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)v.dst >> 32), j, 64) << 32);
+                const uint64_t s = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(uintptr_t)v.src, j, 64) |
+                                   ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)v.src >> 32), j, 64) << 32);
+                dp[u] = reinterpret_cast<uint8_t *>(d);
+                sp[u] = reinterpret_cast<const uint8_t *>(s);
+            }
+        }
+        uint64_t w[VB];
+#pragma unroll
+        for (int u = 0; u < VB; ++u) {   // all loads before the stores
+            // destination word k takes the source bytes from base + 8k; aligned source word j is at ab + 8j
+            const uintptr_t s = (uintptr_t)sp[u], d0 = (uintptr_t)dp[u] & 7u;
+            const uintptr_t ab = (s - d0) & ~(uintptr_t)7;
+            const uintptr_t wa = ab + 8u * lane;
+            w[u] = 0;
+            if (sp[u] && wa + 8 > s && wa < s + n) w[u] = *reinterpret_cast<const uint64_t *>(wa);
+        }
+#pragma unroll
+        for (int u = 0; u < VB; ++u) {
+            const uint64_t hi_w = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)w[u], 1, 64) |
+                                  ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(w[u] >> 32), 1, 64) << 32);
+            if (!dp[u]) continue;
+            const uint32_t d0 = (uint32_t)((uintptr_t)dp[u] & 7u);
+            const uint32_t r = (uint32_t)(((uintptr_t)sp[u] - d0) & 7u);
+            const uint32_t nw = (d0 + n + 7u) >> 3;
+            if (lane >= nw) continue;
+            const uint64_t val = r ? (w[u] >> (8 * r)) | (hi_w << (64 - 8 * r)) : w[u];
+            uint8_t *dw = dp[u] - d0 + 8u * lane;
+            const uint32_t lo = lane == 0 ? d0 : 0u;
+            const uint32_t hi = lane == nw - 1 ? d0 + n - 8u * (nw - 1) : 8u;
+            if (lo == 0 && hi == 8) *reinterpret_cast<uint64_t *>(dw) = val;
+            else store_word_part(dw, val, lo, hi);
+        }
+    }
+}
+
+#ifndef HKV_FULL_HDR
+#define HKV_FULL_HDR 0
+#endif
+#ifndef HKV_VC_WORDS
+#define HKV_VC_WORDS 1
+#endif
 __device__ __forceinline__ void wave_value_copies(const VCopy &v, uint32_t n, int batch)
 {
+    if (HKV_VC_WORDS && n <= 8 * 62) {   // nw + 1 <= 64 source words
+        if (batch == 1) wave_value_words_n<1>(v, n);
+        else wave_value_words_n<kVcBatch>(v, n);
+        return;
+    }
     if (batch == 1) wave_value_copies_n<1>(v, n);
     else wave_value_copies_n<kVcBatch>(v, n);
 }
@@ -1202,6 +1291,20 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
     if (!in) return;
     a.st[i] = st;
     note_state(a, i, xg);
+#if HKV_FULL_HDR
+    // the op's first three and last 8-byte words stored again as they now stand, so that with the value a
+    // GET copied the slab's lines are written whole (a line written with holes costs HBM a read-modify-write:
+    // tools/write_bench.hip, 4M 312-byte ops with an 8-byte hole each 495 us against 241 us whole)
+    if (SV != 31 && (a.esz & 7) == 0 && a.esz >= 32) {
+        __threadfence_block();   // the wave's value copies before the loads
+        uint64_t *o = reinterpret_cast<uint64_t *>(xg);
+        const uint64_t h0 = o[0], h1 = o[1], h2 = o[2], t = o[a.esz / 8 - 1];
+        o[0] = h0;
+        o[1] = h1;
+        o[2] = h2;
+        o[a.esz / 8 - 1] = t;
+    }
+#endif
 }
 
 // ------------------------------------------------------------------ local launches: direct path

@@ -8,6 +8,16 @@
 // mode 2  only each op's words 1 and 2 (bytes 8..23: what a refill writes of a GET)
 // mode 3  mode 1 after loading each op's first word (the holes' lines read first)
 // mode 4  every word after loading each op's first word
+// The slab as 64-byte chunks, one per lane (the log's 64-byte entries):
+// mode 5  every chunk whole
+// mode 6  even chunks only (whole 64-byte halves of each 128-byte line)
+// mode 7  bytes 16..63 of every chunk (an INV's meta and value, not the key)
+// mode 8  bytes 0..31 of every chunk (whole 32-byte halves)
+// Four lanes per 64-byte chunk, 16 bytes a lane (how the batch kernels write entries):
+// mode 9   every chunk whole
+// mode 10  even chunks only
+// mode 11  bytes 16..63 of every chunk
+// mode 12  bytes 32..63 of every chunk
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -32,6 +42,31 @@ __global__ __launch_bounds__(256) void k_write(uint64_t *slab, int64_t n_ops, in
         if (st) base[w] = v;
     }
     if (acc == 0x123456789ull) sink[0] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_chunks(uint64_t *slab, int64_t n_chunks, int mode)
+{
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= n_chunks) return;
+    if (mode == 6 && (c & 1)) return;
+    uint64_t *p = slab + c * 8;
+    const int lo = mode == 7 ? 2 : 0, hi = mode == 8 ? 4 : 8;
+    for (int k = lo; k < hi; ++k) p[k] = 0x6262626262626262ull;
+}
+
+struct __attribute__((aligned(16))) V16 {
+    uint64_t a, b;
+};
+__global__ __launch_bounds__(256) void k_quads(V16 *slab, int64_t n_chunks, int mode)
+{
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t c = t >> 2;
+    const int q = (int)(t & 3);
+    if (c >= n_chunks) return;
+    if (mode == 10 && (c & 1)) return;
+    if (mode == 11 && q < 1) return;
+    if (mode == 12 && q < 2) return;
+    slab[t] = V16{0x6363636363636363ull, 0x6363636363636363ull};
 }
 
 int main()
@@ -59,6 +94,40 @@ int main()
             const double us = ms * 1000.0 / it;
             printf("rep %d mode %d: %8.1f us per launch, %6.2f TB/s of bytes stored, %6.2f TB/s of slab\n", rep, mode, us,
                    n_ops * algo[mode] / us / 1e6, n_ops * 312.0 / us / 1e6);
+        }
+    const int64_t n_chunks = n_ops * kOpWords / 8;
+    const unsigned cgrid = (unsigned)((n_chunks + 255) / 256);
+    const double cb[9] = {0, 0, 0, 0, 0, 64.0, 32.0, 48.0, 32.0};
+    for (int rep = 0; rep < 3; ++rep)
+        for (int mode = 5; mode < 9; ++mode) {
+            hipLaunchKernelGGL(k_chunks, dim3(cgrid), dim3(256), 0, 0, slab, n_chunks, mode);
+            hipEventRecord(e0);
+            const int it = 5;
+            for (int k = 0; k < it; ++k) hipLaunchKernelGGL(k_chunks, dim3(cgrid), dim3(256), 0, 0, slab, n_chunks, mode);
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            const double us = ms * 1000.0 / it;
+            printf("rep %d mode %d: %8.1f us per launch, %6.2f TB/s of bytes stored, %6.2f TB/s of slab\n", rep, mode, us,
+                   n_chunks * cb[mode] / us / 1e6, n_chunks * 64.0 / us / 1e6);
+        }
+    const double qb[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 64.0, 32.0, 48.0, 32.0};
+    const unsigned qgrid = (unsigned)((n_chunks * 4 + 255) / 256);
+    for (int rep = 0; rep < 3; ++rep)
+        for (int mode = 9; mode < 13; ++mode) {
+            hipLaunchKernelGGL(k_quads, dim3(qgrid), dim3(256), 0, 0, reinterpret_cast<V16 *>(slab), n_chunks, mode);
+            hipEventRecord(e0);
+            const int it = 5;
+            for (int k = 0; k < it; ++k)
+                hipLaunchKernelGGL(k_quads, dim3(qgrid), dim3(256), 0, 0, reinterpret_cast<V16 *>(slab), n_chunks, mode);
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            const double us = ms * 1000.0 / it;
+            printf("rep %d mode %d: %8.1f us per launch, %6.2f TB/s of bytes stored, %6.2f TB/s of slab\n", rep, mode, us,
+                   n_chunks * qb[mode] / us / 1e6, n_chunks * 64.0 / us / 1e6);
         }
     hipFree(slab);
     return 0;

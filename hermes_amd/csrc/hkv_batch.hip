@@ -1178,7 +1178,7 @@ __device__ __forceinline__ void wave_value_words_n(const VCopy &v, uint32_t n)
 }
 
 #ifndef HKV_FULL_HDR
-#define HKV_FULL_HDR 0
+#define HKV_FULL_HDR 1
 #endif
 #ifndef HKV_VC_WORDS
 #define HKV_VC_WORDS 1

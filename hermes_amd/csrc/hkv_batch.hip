@@ -109,6 +109,7 @@ struct BatchArgs {
     int32_t wave_copy;           // big values copied a wave per value (HKV_WAVE_COPY=0: by their own lane)
     int32_t vc_batch;            // values per step of those wave copies (HKV_VC_BATCH, 1 or kVcBatch)
     int32_t wave_shadow;         // big entries: candidates applied by the whole wave (HKV_WAVE_SHADOW=0: per lane)
+    int32_t big_patch;           // big local launches: patches read by k_lookup, written by k_resolve0_direct
     const uint64_t *phys_hint;   // INV / VAL launches: located entries (hkv_batch_desc.d_phys), or NULL
     int32_t cancel;              // k_local_pre undoes its tags (HKV_BATCH_PREPASS_CANCEL)
     uint8_t *ack_out;            // INV launches: each element's ACK (hkv_batch_desc.d_ack_out), or NULL
@@ -430,6 +431,16 @@ __device__ __forceinline__ void copy_elem(uint8_t *dst, const uint8_t *src, int3
     if (esz & 8) *reinterpret_cast<uint64_t *>(dst + esz - 8) = *reinterpret_cast<const uint64_t *>(src + esz - 8);
 }
 
+// bytes 8..15 of an op after its refill patch (second patch word pb, see patch_valid): opcode,
+// ST_NEW, val_len; the timestamp (bytes 11..15) kept unless the patch resets it
+__device__ __forceinline__ uint64_t patched_hdr(uint64_t h, uint64_t pb)
+{
+    const bool reset = ((pb >> 40) & 0xFFu) != 0;
+    const uint64_t low = (pb & 0xFFu) | ((uint64_t)kNew << 8) | (((pb >> 8) & 0xFFu) << 16);
+    return reset ? low : (low | (h & ~0xFFFFFFull));
+}
+__device__ __forceinline__ bool patch_valid(uint64_t pb);
+
 constexpr int64_t kLookupHead = 8192;
 constexpr int kLookupPair = 2;
 // Four lanes (q = lane & 3) look up kLookupPair keys side by side: the 64-B bucket (16 B per
@@ -553,8 +564,10 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
     int64_t gi[P];
     uint64_t key[P], hdr[P];
     int probe[P];
+    bool patched[P];
 #pragma unroll
     for (int k = 0; k < P; ++k) {
+        patched[k] = false;
         gi[k] = i_begin + ((int64_t)blockIdx.x * P + k) * 64 + (threadIdx.x >> 2);
         uint64_t kk = 0, hh = 0;
         int p = 0;
@@ -565,6 +578,14 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                 const U64x2 h = *reinterpret_cast<const U64x2 *>(a.elems + gi[k] * a.esz);
                 kk = h.a;
                 hh = h.b;
+                if (a.big_patch) {   // a refilled slot: the op as its patch makes it (k_resolve0_direct writes it)
+                    const U64x2 pt = *reinterpret_cast<const U64x2 *>(a.patch + gi[k] * 16);
+                    if (patch_valid(pt.b)) {
+                        kk = pt.a;
+                        hh = patched_hdr(hh, pt.b);
+                        patched[k] = true;
+                    }
+                }
                 if (skip_elem_os(a.type, (uint8_t)hh, (uint8_t)(hh >> 8))) {
                     if (a.type == kInvs && a.ns_idx) {
                         int64_t start;  // packed: a search, for the rare membership-change INVs only
@@ -677,7 +698,7 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                 }
             }
         }
-        if (probe[k] && e == kNone) x[9] = kMiss;
+        if (probe[k] && e == kNone && !patched[k]) x[9] = kMiss;   // (a patched one's miss: k_resolve0_direct)
         a.ent[gi[k]] = e;
         if (a.inv_direct || a.ack_direct) a.st[gi[k]] = ifl;
     }
@@ -1245,6 +1266,55 @@ __device__ __forceinline__ void wave_block_copies(uint8_t *dst, const uint8_t *s
     }
 }
 
+// A refilled slot's patch written into its op (what k_apply_patch does, here beside the value copies
+// and header stores of k_resolve0_direct, so the op's 64-byte blocks are written whole once instead
+// of its header with holes by a separate pass): key, opcode, ST_NEW, val_len, timestamp reset and
+// flags by the lane, a write's value fill by the whole wave (8-byte words, as wave_value_words_n);
+// then MISS for an element k_lookup found no entry for (it leaves patched ops alone). Every lane of
+// the wave calls it.
+__device__ __forceinline__ bool in_count(const BatchArgs &a, uint32_t i);
+__device__ __forceinline__ void apply_patch_wave(const BatchArgs &a, bool in, int64_t i, uint8_t *x)
+{
+    uint64_t pb = 0;
+    uint8_t *fdst = nullptr;
+    if (in) {
+        const U64x2 p = *reinterpret_cast<const U64x2 *>(a.patch + i * 16);
+        pb = p.b;
+        if (patch_valid(pb)) {
+            uint64_t *o = reinterpret_cast<uint64_t *>(x);
+            const uint64_t h = patched_hdr(o[1], pb);
+            o[0] = p.a;
+            o[1] = h;
+            *reinterpret_cast<uint16_t *>(x + 16) = (uint16_t)(pb >> 16);
+            if ((pb >> 32) & 0xFFu) fdst = x + kOpValueOff;
+        }
+    }
+    const uint32_t lane = threadIdx.x & 63, n = a.g.st_value;
+    unsigned long long todo = __ballot(fdst != nullptr);
+    while (todo) {
+        const int j = __ffsll((long long)todo) - 1;
+        todo &= todo - 1;
+        const uint64_t d = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(uintptr_t)fdst, j, 64) |
+                           ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)fdst >> 32), j, 64) << 32);
+        const uint64_t fill = 0x0101010101010101ull * (uint8_t)__shfl((int)(uint32_t)(pb >> 32), j, 64);
+        uint8_t *dp = reinterpret_cast<uint8_t *>(d);
+        const uint32_t d0 = (uint32_t)(d & 7u), nw = (d0 + n + 7u) >> 3;
+        for (uint32_t w = lane; w < nw; w += 64) {
+            uint8_t *dw = dp - d0 + 8u * w;
+            const uint32_t lo = w == 0 ? d0 : 0u;
+            const uint32_t hi = w == nw - 1 ? d0 + n - 8u * (nw - 1) : 8u;
+            if (lo == 0 && hi == 8) *reinterpret_cast<uint64_t *>(dw) = fill;
+            else store_word_part(dw, fill, lo, hi);
+        }
+    }
+    if (in && patch_valid(pb) && a.ent[i] == kNone) {
+        // k_lookup's probe on the patched op: in its batch's count and not skipped
+        const uint8_t oc = (uint8_t)pb;
+        if (in_count(a, (uint32_t)i) && !skip_elem_os(a.type, oc, kNew)) x[9] = kMiss;
+    }
+    __threadfence_block();   // the patched ops before the exec functions read them
+}
+
 template <int TYPE, int SV>
 __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
 {
@@ -1264,6 +1334,7 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
     const bool wave_shadow = SV != 31 && a.wave_copy && a.g.st_value <= 320 && a.wave_shadow;
     bool cand = false;
     if (in) elem_at(a, (uint32_t)i, xg, idx, c);
+    if (a.big_patch) apply_patch_wave(a, in, i, xg);
     if (e != kNone) {
         Meta m;
         meta_load(entry_of(a, e), m);
@@ -3637,6 +3708,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.opc = bl.type == kLocal ? bl.opcode_in : nullptr;
     a.phys_hint = bl.type == kInvs || bl.type == kVals || bl.type == kLocal ? bl.phys_hint : nullptr;
     a.patch = nullptr;
+    a.big_patch = 0;
     a.pkeys = nullptr;
     a.cancel = bl.stage == 3;
     a.ack_out = bl.type == kInvs || (bl.type == kAcks && bl.n_rows > 0) ? bl.ack_out : nullptr;
@@ -3749,7 +3821,16 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         }
         return hipGetLastError() == hipSuccess ? 0 : -3;
     }
-    if (bl.patch && (small || !local_direct || patch_apply_env)) {  // the other paths take the patches as op writes first
+    // big local launches on the rounds engine: k_lookup reads the patches and k_resolve0_direct writes them
+    // into the ops (HKV_BIG_PATCH=0: k_apply_patch first)
+    static const bool big_patch_env = !getenv("HKV_BIG_PATCH") || atoi(getenv("HKV_BIG_PATCH")) != 0;
+    const bool big_patch = bl.patch && big_patch_env && !small && !local_direct && !patch_apply_env && big && big_direct &&
+                           (bl.type == kLocal || bl.type == kLocalAfterMemb) && bl.esz % 8 == 0 &&
+                           bl.esz >= kOpValueOff + (int32_t)bl.g.st_value && !a.phys_hint;
+    a.big_patch = big_patch ? 1 : 0;
+    if (big_patch) {
+        a.patch = bl.patch;
+    } else if (bl.patch && (small || !local_direct || patch_apply_env)) {  // the other paths take the patches as op writes first
         hipLaunchKernelGGL(k_apply_patch, dim3(grid), dim3(256), 0, s, bl.elems, bl.patch, n, bl.esz, bl.g.st_value);
     } else if (bl.patch) {
         a.patch = bl.patch;

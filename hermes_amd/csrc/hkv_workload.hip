@@ -1825,7 +1825,7 @@ static int refill_plan(uint8_t *states, int32_t n_workers, int32_t stride, uint3
 {
     if (stride > 256 || n_workers <= 0 || tlen <= 0 || !states || !opc || !patch) return -1;
     if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET)) return -1;   // no hot-request coalescing
-    if (((uintptr_t)patch & 15) || ((uintptr_t)put_keys & 7) || st_value > 255) return -1;
+    if (((uintptr_t)patch & 15) || ((uintptr_t)put_keys & 7) || (st_value >> shift) > 255) return -1;   // val_len: a byte
     if ((!tphys) != (!sphys) || ((uintptr_t)tphys & 7) || ((uintptr_t)sphys & 7)) return -1;
     if (wl_wpw() == 2)
         hipLaunchKernelGGL(k_refill_plan_w<2>, dim3((unsigned)((n_workers + 7) / 8)), dim3(256), 0, (hipStream_t)stream,

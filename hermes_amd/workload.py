@@ -262,11 +262,14 @@ class Round:
         # the next local launch as patches, so the op slab is read and written once per round. Not with
         # hot-request coalescing (a sequential walk over the ops), VAL credits (their marshal keeps no
         # mirror) or 312-B ops (refilled in place). Default: wherever it applies.
-        can_fuse = not coalesce_hot and val_credits is None and self.op <= 64
+        # HKV_BIG_FUSED=1: 312-B ops planned too, their patches written by the local launch's in-place
+        # resolve (k_resolve0_direct) beside the value copies instead of by hkv_wl_refill_st
+        big_fused = os.environ.get("HKV_BIG_FUSED", "0") == "1"
+        can_fuse = not coalesce_hot and val_credits is None and (self.op <= 64 or big_fused)
         self.fused = can_fuse if fused_refill is None else (fused_refill and can_fuse)
         # 312-B ops are refilled in place, but from the same state mirror (hkv_wl_refill_st), so a slot
         # the refill keeps is not read (fused_refill=False or HKV_REFILL_ST=0: from the ops)
-        self.st_refill = (not coalesce_hot and val_credits is None and self.op > 64 and fused_refill is not False
+        self.st_refill = (not self.fused and not coalesce_hot and val_credits is None and self.op > 64 and fused_refill is not False
                           and os.environ.get("HKV_REFILL_ST", "1") != "0")
         self.machine_id = kvs.machine_id
         dev = torch.device("cuda", kvs.device)

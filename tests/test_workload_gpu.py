@@ -21,11 +21,14 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("theta,workers,cfg3", [(0.99, 40, False), (0.0, 40, False), (0.99, 160, False),
-                                                (0.99, 40, True)])
-def test_bench_round_mirrored(theta, workers, cfg3):
+@pytest.mark.parametrize("theta,workers,cfg3,big_fused", [(0.99, 40, False, False), (0.0, 40, False, False),
+                                                          (0.99, 160, False, False), (0.99, 40, True, False),
+                                                          (0.99, 40, True, True)])
+def test_bench_round_mirrored(theta, workers, cfg3, big_fused, monkeypatch):
     """cfg3: bench.py --config cfg3 (RMWs on, big objects, 25 % PUT + 25 % RMW): the rounds engine,
-    op-sized ACKs from the virtual peers, RMW completions."""
+    op-sized ACKs from the virtual peers, RMW completions. big_fused (HKV_BIG_FUSED=1): the 312-B ops'
+    refills planned as patches, which k_lookup reads and k_resolve0_direct writes into the ops."""
+    monkeypatch.setenv("HKV_BIG_FUSED", "1" if big_fused else "0")
     from hermes_amd.kvs import HermesKV
     from hermes_amd.workload import Round, zipf_params
     n_keys, bkts = 60_000, 1 << 16
@@ -37,6 +40,7 @@ def test_bench_round_mirrored(theta, workers, cfg3):
     m = Mirror(g, o, "bench round")
     r = Round(g, workers, L.membership(3, 0), [1, 2], zipf_params(n_keys, theta), 500 if cfg3 else 200,
               500 if cfg3 else 0, seed=0x5EED, max_steps=8, trace_len=1024)
+    assert r.fused == (not cfg3 or big_fused)
     for _ in range(steps):
         r.step()
     torch.cuda.synchronize()

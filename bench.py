@@ -299,11 +299,6 @@ def main():
     probe_ms = {k: avg(v) for k, v in probe_events.items()}
     ms = dict(probe_ms)
     ms.update({k: avg(v) for k, v in events.items()})
-    # a local launch in two stages (its prepass on a side stream beside the VAL batch): its kernel time
-    # is both stages' (the roofline charges the launch the prepass it overlaps)
-    pre_ms = ms.pop("local_pre", None)
-    if pre_ms is not None and "local" in ms:
-        ms["local"] += pre_ms
     W, S = a.workers, Round.LOCAL
     per_launch_bytes = {
         "local": W * S * BYTES["get"] + puts_per_step * (BYTES["put"] - BYTES["get"]),

@@ -99,22 +99,13 @@ struct BatchArgs {
     const uint8_t *patch;        // local direct path: pending header writes (hkv_batch_desc.d_patch), or NULL
     uint8_t *rws;                // ACK launches: read_write_ops state mirror (hkv_batch_desc.d_rw_state), or NULL
     const uint8_t *rwo;          // ACK launches: read_write_ops opcode mirror (hkv_batch_desc.d_opcode_in), or NULL
-    const uint64_t *pkeys;       // local direct path: the PUT-key mirror (hkv_batch_desc.d_put_keys), or NULL
     int32_t n_rows, skip_row;    // HKV_BATCH_ROWS: rows applied in order (k_unique_rows), one skipped (-1: none)
     int64_t row_stride;          // elements between rows
     int32_t dbg;                 // HKV_DBG: timing experiments that skip work (results invalid); always 0
                                  // unless the library is built with -DHKV_DEBUG_MODES (HKV_DBG_ON)
     int32_t check_unique;        // HKV_CHECK_UNIQUE: HKV_BATCH_UNIQUE launches verify their keys are unique
-    int32_t pre_patch_first;     // k_local_pre reads a PUT's header only when it has no patch (HKV_PRE_PATCH_FIRST)
-    int32_t wave_copy;           // big values copied a wave per value (HKV_WAVE_COPY=0: by their own lane)
-    int32_t vc_batch;            // values per step of those wave copies (HKV_VC_BATCH, 1 or kVcBatch)
-    int32_t wave_shadow;         // big entries: candidates applied by the whole wave (HKV_WAVE_SHADOW=0: per lane)
-    int32_t big_patch;           // big local launches: patches read by k_lookup, written by k_resolve0_direct
-    const uint64_t *phys_hint;   // INV / VAL launches: located entries (hkv_batch_desc.d_phys), or NULL
-    int32_t cancel;              // k_local_pre undoes its tags (HKV_BATCH_PREPASS_CANCEL)
     uint8_t *ack_out;            // INV launches: each element's ACK (hkv_batch_desc.d_ack_out), or NULL
     uint32_t ack_out_size;
-    int32_t pre_notag;           // local direct path: k_local_pre sets no tags, k_local_fused reads F for every hit
 };
 
 // Rounds after round 0 per batch type: how often a hot key usually mutates in one launch beyond
@@ -479,7 +470,7 @@ __device__ __forceinline__ void lookup_pair(const BatchArgs &a, const uint64_t *
 }
 
 // lookup_pair that also loads each hit's F word beside its log line (lane q == 0; ~0 for a miss), so a
-// key's F costs no dependent load after the line (k_local_fused, HKV_LF_FSPEC)
+// key's F costs no dependent load after the line (k_local_fused)
 template <int P>
 __device__ __forceinline__ void lookup_pair_f(const BatchArgs &a, const uint64_t *key, const bool *probe, int q,
                                               int gbase, bool *ok, uint64_t *phys, uint4 *ln, unsigned long long *fwv)
@@ -513,44 +504,7 @@ __device__ __forceinline__ void lookup_pair_f(const BatchArgs &a, const uint64_t
     }
 }
 
-// lookup_pair with located entries (hkv_batch_desc.d_phys): an element with an offset reads its entry
-// line straight away; one without, or whose entry does not hold its key, takes lookup_pair's path. gi:
-// the elements' indices into the hints. All lanes of the wave call it.
-template <int P>
-__device__ __forceinline__ void lookup_hinted(const BatchArgs &a, const int64_t *gi, const uint64_t *key,
-                                              const bool *probe, int q, int gbase, bool *ok, uint64_t *phys, uint4 *ln)
-{
-    bool redo[P];
-    bool any = false;
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-        const uint64_t h = probe[k] ? a.phys_hint[gi[k]] : ~0ull;
-        ok[k] = h != ~0ull;
-        phys[k] = ok[k] ? h : 0;
-        ln[k] = ok[k] ? reinterpret_cast<const uint4 *>(a.log + phys[k])[q] : make_uint4(0u, 0u, 0u, 0u);
-    }
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-        const uint64_t ek = (uint64_t)(uint32_t)__shfl((int)ln[k].z, 0, 4) | ((uint64_t)(uint32_t)__shfl((int)ln[k].w, 0, 4) << 32);
-        redo[k] = probe[k] && (!ok[k] || ek != key[k]);
-        any |= redo[k];
-    }
-    if (__ballot(any)) {   // wave-uniform: the rare elements without a usable offset
-        bool ok2[P];
-        uint64_t ph2[P];
-        uint4 ln2[P];
-        lookup_pair<P>(a, key, redo, q, gbase, ok2, ph2, ln2);
-#pragma unroll
-        for (int k = 0; k < P; ++k)
-            if (redo[k]) {
-                ok[k] = ok2[k];
-                phys[k] = ph2[k];
-                ln[k] = ln2[k];
-            }
-    }
-}
-
-template <int P = kLookupPair, bool H = false>
+template <int P = kLookupPair>
 __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, int64_t i_end)
 {
     const int q = threadIdx.x & 3;
@@ -564,10 +518,8 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
     int64_t gi[P];
     uint64_t key[P], hdr[P];
     int probe[P];
-    bool patched[P];
 #pragma unroll
     for (int k = 0; k < P; ++k) {
-        patched[k] = false;
         gi[k] = i_begin + ((int64_t)blockIdx.x * P + k) * 64 + (threadIdx.x >> 2);
         uint64_t kk = 0, hh = 0;
         int p = 0;
@@ -578,14 +530,6 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                 const U64x2 h = *reinterpret_cast<const U64x2 *>(a.elems + gi[k] * a.esz);
                 kk = h.a;
                 hh = h.b;
-                if (a.big_patch) {   // a refilled slot: the op as its patch makes it (k_resolve0_direct writes it)
-                    const U64x2 pt = *reinterpret_cast<const U64x2 *>(a.patch + gi[k] * 16);
-                    if (patch_valid(pt.b)) {
-                        kk = pt.a;
-                        hh = patched_hdr(hh, pt.b);
-                        patched[k] = true;
-                    }
-                }
                 if (skip_elem_os(a.type, (uint8_t)hh, (uint8_t)(hh >> 8))) {
                     if (a.type == kInvs && a.ns_idx) {
                         int64_t start;  // packed: a search, for the rare membership-change INVs only
@@ -608,8 +552,7 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
         probe[k] = p;
         key[k] = kk;
     }
-    // bucket, then the log line (lookup_pair: four lanes per element, 16 B each); with located entries
-    // (hkv_batch_desc.d_phys) the log line straight away (lookup_hinted)
+    // bucket, then the log line (lookup_pair: four lanes per element, 16 B each)
     bool ok[P];
     uint64_t phys[P], ekey[P];
     Meta m0[P];
@@ -619,8 +562,7 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
         uint4 l4[P];
 #pragma unroll
         for (int k = 0; k < P; ++k) pr[k] = probe[k] != 0;
-        if (H) lookup_hinted<P>(a, gi, key, pr, q, gbase, ok, phys, l4);
-        else lookup_pair<P>(a, key, pr, q, gbase, ok, phys, l4);
+        lookup_pair<P>(a, key, pr, q, gbase, ok, phys, l4);
 #pragma unroll
         for (int k = 0; k < P; ++k)
             ln[k] = U64x2{(uint64_t)l4[k].x | ((uint64_t)l4[k].y << 32), (uint64_t)l4[k].z | ((uint64_t)l4[k].w << 32)};
@@ -698,7 +640,7 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                 }
             }
         }
-        if (probe[k] && e == kNone && !patched[k]) x[9] = kMiss;   // (a patched one's miss: k_resolve0_direct)
+        if (probe[k] && e == kNone) x[9] = kMiss;
         a.ent[gi[k]] = e;
         if (a.inv_direct || a.ack_direct) a.st[gi[k]] = ifl;
     }
@@ -1076,7 +1018,7 @@ __global__ __launch_bounds__(BP) void k_resolve0(BatchArgs a)
 // The value copies the wave's exec calls recorded (Ctx::vc), made by the whole wave: byte k of a
 // value by lane k % 64, so each instruction moves 64 consecutive bytes. kVcBatch values at a time:
 // all their loads are issued before the first store, so a wave waits one memory latency per
-// kVcBatch values instead of one per value (HKV_VC_BATCH=1: one at a time). Every lane of the wave
+// kVcBatch values instead of one per value. Every lane of the wave
 // calls it.
 #ifndef HKV_VC_BATCH_N
 #define HKV_VC_BATCH_N 4
@@ -1266,55 +1208,6 @@ __device__ __forceinline__ void wave_block_copies(uint8_t *dst, const uint8_t *s
     }
 }
 
-// A refilled slot's patch written into its op (what k_apply_patch does, here beside the value copies
-// and header stores of k_resolve0_direct, so the op's 64-byte blocks are written whole once instead
-// of its header with holes by a separate pass): key, opcode, ST_NEW, val_len, timestamp reset and
-// flags by the lane, a write's value fill by the whole wave (8-byte words, as wave_value_words_n);
-// then MISS for an element k_lookup found no entry for (it leaves patched ops alone). Every lane of
-// the wave calls it.
-__device__ __forceinline__ bool in_count(const BatchArgs &a, uint32_t i);
-__device__ __forceinline__ void apply_patch_wave(const BatchArgs &a, bool in, int64_t i, uint8_t *x)
-{
-    uint64_t pb = 0;
-    uint8_t *fdst = nullptr;
-    if (in) {
-        const U64x2 p = *reinterpret_cast<const U64x2 *>(a.patch + i * 16);
-        pb = p.b;
-        if (patch_valid(pb)) {
-            uint64_t *o = reinterpret_cast<uint64_t *>(x);
-            const uint64_t h = patched_hdr(o[1], pb);
-            o[0] = p.a;
-            o[1] = h;
-            *reinterpret_cast<uint16_t *>(x + 16) = (uint16_t)(pb >> 16);
-            if ((pb >> 32) & 0xFFu) fdst = x + kOpValueOff;
-        }
-    }
-    const uint32_t lane = threadIdx.x & 63, n = a.g.st_value;
-    unsigned long long todo = __ballot(fdst != nullptr);
-    while (todo) {
-        const int j = __ffsll((long long)todo) - 1;
-        todo &= todo - 1;
-        const uint64_t d = (uint64_t)(uint32_t)__shfl((int)(uint32_t)(uintptr_t)fdst, j, 64) |
-                           ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)fdst >> 32), j, 64) << 32);
-        const uint64_t fill = 0x0101010101010101ull * (uint8_t)__shfl((int)(uint32_t)(pb >> 32), j, 64);
-        uint8_t *dp = reinterpret_cast<uint8_t *>(d);
-        const uint32_t d0 = (uint32_t)(d & 7u), nw = (d0 + n + 7u) >> 3;
-        for (uint32_t w = lane; w < nw; w += 64) {
-            uint8_t *dw = dp - d0 + 8u * w;
-            const uint32_t lo = w == 0 ? d0 : 0u;
-            const uint32_t hi = w == nw - 1 ? d0 + n - 8u * (nw - 1) : 8u;
-            if (lo == 0 && hi == 8) *reinterpret_cast<uint64_t *>(dw) = fill;
-            else store_word_part(dw, fill, lo, hi);
-        }
-    }
-    if (in && patch_valid(pb) && a.ent[i] == kNone) {
-        // k_lookup's probe on the patched op: in its batch's count and not skipped
-        const uint8_t oc = (uint8_t)pb;
-        if (in_count(a, (uint32_t)i) && !skip_elem_os(a.type, oc, kNew)) x[9] = kMiss;
-    }
-    __threadfence_block();   // the patched ops before the exec functions read them
-}
-
 template <int TYPE, int SV>
 __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
 {
@@ -1329,12 +1222,11 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
     // key's entry is not written in this pass -- its first candidate writes its own shadow -- and
     // the op is this lane's own)
     VCopy vc{nullptr, nullptr};
-    if (SV != 31 && a.wave_copy && a.g.st_value <= 320) c.vc = &vc;
+    if (SV != 31 && a.g.st_value <= 320) c.vc = &vc;
     // a key's first candidate applies itself to its shadow by the whole wave (apply_to_shadow_wave)
-    const bool wave_shadow = SV != 31 && a.wave_copy && a.g.st_value <= 320 && a.wave_shadow;
+    const bool wave_shadow = SV != 31 && a.g.st_value <= 320;
     bool cand = false;
     if (in) elem_at(a, (uint32_t)i, xg, idx, c);
-    if (a.big_patch) apply_patch_wave(a, in, i, xg);
     if (e != kNone) {
         Meta m;
         meta_load(entry_of(a, e), m);
@@ -1358,7 +1250,7 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
         }
     }
     if (wave_shadow) apply_to_shadow_wave<TYPE, SV>(a, cand, (uint32_t)i, cand ? entry_of(a, e) : nullptr, vc);
-    if (SV != 31) wave_value_copies(vc, a.g.st_value, a.vc_batch);
+    if (SV != 31) wave_value_copies(vc, a.g.st_value, kVcBatch);
     if (!in) return;
     a.st[i] = st;
     note_state(a, i, xg);
@@ -1562,9 +1454,9 @@ constexpr int kPrePair = HKV_PRE_PAIR;   // keys per lane group in flight in the
 #else
 #define HKV_PRE_ATTR
 #endif
-// NT (the default, with k_local_fused's F loads beside every hit's line): no seqlock-byte tags -- the
-// fused pass reads every hit's F word and needs no mark of the keys that have one
-template <int HEAD = kPreHead, bool H = false, bool NT = false>
+// No seqlock-byte tags (round 5): k_local_fused loads every hit's F word beside its log line and needs
+// no mark of the keys that have one
+template <int HEAD = kPreHead>
 __global__ __launch_bounds__(kPreThreads) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
 {
     __shared__ uint64_t hk[kPreHash], gk[kPreHash];  // the block's PUT keys, the head's
@@ -1593,28 +1485,6 @@ __global__ __launch_bounds__(kPreThreads) HKV_PRE_ATTR void k_local_pre(BatchArg
     bool in[kAllK];
     uint8_t opm[kAllK];
     U64x2 pt[kAllK];
-    if (a.pkeys) {
-        // the caller's PUT-key mirror and entry states (hkv_batch_desc.d_put_keys): two dense arrays,
-        // one load each and no dependence between them, instead of opcode mirror -> patch -> op header
-        // (k_local_fused checks both mirrors against every element)
-        uint64_t pk[kAllK];
-        uint8_t ps[kAllK];
-#pragma unroll
-        for (int k = 0; k < kAllK; ++k) {
-            const bool own = k < kOwnK;
-            const int64_t i = own ? i0 + k * kPreThreads + tid : (int64_t)(k - kOwnK) * kPreThreads + tid;
-            in[k] = i < a.n && (own || i < head_end);
-            pk[k] = in[k] ? a.pkeys[i] : ~0ull;
-            ps[k] = in[k] ? a.state_out[i] : (uint8_t)0;
-        }
-#pragma unroll
-        for (int k = 0; k < kAllK; ++k) {
-            h[k].a = pk[k];
-            h[k].b = (uint64_t)(pk[k] != ~0ull ? kOpPut : kOpGet) | ((uint64_t)ps[k] << 8);
-            opm[k] = (uint8_t)h[k].b;
-            pt[k] = U64x2{0, 0};
-        }
-    } else {
 #pragma unroll
     for (int k = 0; k < kAllK; ++k) {
         const bool own = k < kOwnK;
@@ -1622,7 +1492,7 @@ __global__ __launch_bounds__(kPreThreads) HKV_PRE_ATTR void k_local_pre(BatchArg
         in[k] = i < a.n && (own || i < head_end);
         opm[k] = a.opc ? a.opc[in[k] ? i : 0] : (uint8_t)kOpPut;
     }
-    if (a.pre_patch_first && a.patch) {
+    if (a.patch) {
         // the patches first: a refilled PUT's patch holds all the prepass needs (key, opcode, ST_NEW),
         // so only the PUTs kept from the last round read their op header (a second dependent load
         // for them, against a third of the op slab's lines fetched for nothing)
@@ -1644,7 +1514,7 @@ __global__ __launch_bounds__(kPreThreads) HKV_PRE_ATTR void k_local_pre(BatchArg
             const bool own = k < kOwnK;
             const int64_t i = own ? i0 + k * kPreThreads + tid : (int64_t)(k - kOwnK) * kPreThreads + tid;
             h[k] = *reinterpret_cast<const U64x2 *>(a.elems + (in[k] && opm[k] == kOpPut ? i : 0) * 56);
-            pt[k] = a.patch && in[k] && opm[k] == kOpPut ? *reinterpret_cast<const U64x2 *>(a.patch + i * 16) : U64x2{0, 0};
+            pt[k] = U64x2{0, 0};
         }
     }
 #pragma unroll
@@ -1653,7 +1523,6 @@ __global__ __launch_bounds__(kPreThreads) HKV_PRE_ATTR void k_local_pre(BatchArg
             h[k].a = pt[k].a;
             h[k].b = (h[k].b & ~0xFFFFull) | (pt[k].b & 0xFFu) | ((uint64_t)kNew << 8);
         }
-    }
 #pragma unroll
     for (int k = 0; k < kAllK; ++k) {
         const bool own = k < kOwnK;
@@ -1717,26 +1586,14 @@ __global__ __launch_bounds__(kPreThreads) HKV_PRE_ATTR void k_local_pre(BatchArg
                 }
             }
         }
-        if (H) {   // located entries (hkv_batch_desc.d_phys): each key's first PUT's word
-            int64_t gi[kPrePair];
-#pragma unroll
-            for (int k = 0; k < kPrePair; ++k) gi[k] = probe[k] ? (int64_t)idx[k] : 0;
-            lookup_hinted<kPrePair>(a, gi, key, probe, q, gbase, ok, phys, ln);
-        } else {
-            lookup_pair<kPrePair>(a, key, probe, q, gbase, ok, phys, ln);
-        }
+        lookup_pair<kPrePair>(a, key, probe, q, gbase, ok, phys, ln);
 #pragma unroll
         for (int k = 0; k < kPrePair; ++k) {
             Meta m0;
             const uint64_t ek = line_key_meta(ln[k], m0);
             if (q != 0 || !ok[k] || ek != key[k]) continue;
-            if (a.cancel) {   // a prepass whose launch will not run: its tags go (its F words are stale anyway)
-                if ((uint8_t)(m0.w5 >> 16) == a.ltag) a.log[phys[k] + kEntryMetaOff + 4] = 0;
-                continue;
-            }
             if (!would_mutate(kLocal, reinterpret_cast<const uint8_t *>(hput), m0, c) || HKV_DBG_ON(a, 1)) continue;
             atomicMin(a.fw + fw_index(a, phys[k]), ((unsigned long long)(~a.rtag0) << 32) | idx[k]);
-            if (!NT && (uint8_t)(m0.w5 >> 16) != a.ltag && !HKV_DBG_ON(a, 32)) a.log[phys[k] + kEntryMetaOff + 4] = a.ltag;
         }
     }
 }
@@ -1745,9 +1602,9 @@ __global__ __launch_bounds__(kPreThreads) HKV_PRE_ATTR void k_local_pre(BatchArg
 // nothing shared beyond it. The lookup runs four lanes per element (each lane holds 16 B of the op
 // and of the log line); the wave-private LDS copies of op and entry are then resolved one element
 // per lane, so the exec code's branches are paid once per 32 elements; the ops go back whole.
-// FS (the default): every hit's F word is loaded beside its log line (with the prepass's tags off,
-// a.pre_notag, the word alone says whether the key has a first candidate)
-template <int P, bool H = false, bool FS = false>
+// Every hit's F word is loaded beside its log line; the word alone says whether this launch's prepass
+// offered a first candidate for the key (first_cand)
+template <int P>
 __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
 {
     constexpr int E = 16 * P;   // elements per wave: P per lane group
@@ -1758,8 +1615,6 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
     __shared__ uint8_t sprb[E];      // probed (not skipped)
     __shared__ uint32_t sdef[E];
     __shared__ uint32_t ndef;
-    __shared__ unsigned long long spk[E];  // the PUT-key mirror's word (a.pkeys)
-    __shared__ uint8_t sps[E];             // the entry state the mirror gives
     const int tid = threadIdx.x, q = tid & 3, gbase = tid & ~3;
     const int64_t i0 = (int64_t)blockIdx.x * E;
     if (tid == 0) ndef = 0;
@@ -1786,10 +1641,6 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
                 op[k].y = (uint32_t)(t >> 32);
             }
             if (patch_valid(p.b)) op[k] = patch_chunk(op[k], q, p.a, p.b);
-            if (a.pkeys && q == 0) {   // the mirrors k_local_pre worked from, checked below
-                spk[te[k]] = a.pkeys[i];
-                sps[te[k]] = a.state_out[i];
-            }
         }
         sops[te[k] * 4 + q] = op[k];
     }
@@ -1802,28 +1653,15 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         if (live[k])
             probe[k] = in_count(a, (uint32_t)(i0 + te[k])) && !skip_elem_os(kLocal, (uint8_t)h0, (uint8_t)(h0 >> 8));
     }
-    unsigned long long fwv[P];   // FS: every hit's F word, loaded beside its log line
-    if (H) {   // located entries (hkv_batch_desc.d_phys)
-        int64_t gi[P];
-#pragma unroll
-        for (int k = 0; k < P; ++k) gi[k] = i0 + te[k];
-        lookup_hinted<P>(a, gi, key, probe, q, gbase, ok, phys, ln);
-    } else if (FS) {
-        lookup_pair_f<P>(a, key, probe, q, gbase, ok, phys, ln, fwv);
-    } else {
-        lookup_pair<P>(a, key, probe, q, gbase, ok, phys, ln);
-    }
-    // F of a key tagged by k_local_pre, loaded for both elements before either is resolved
+    unsigned long long fwv[P];   // every hit's F word, loaded beside its log line
+    lookup_pair_f<P>(a, key, probe, q, gbase, ok, phys, ln, fwv);
 #pragma unroll
     for (int k = 0; k < P; ++k) {
         Meta m;
         const uint64_t ek = line_key_meta(ln[k], m);
         const bool hit = ok[k] && ek == key[k];
-        const bool tagged = hit && m_state(m) != kInvalid && (uint8_t)(m.w5 >> 16) == a.ltag;
-        // FS: every hit's F word came with its line; without tags (a.pre_notag) the word alone says
-        // whether this launch offered one (first_cand)
-        const bool want_f = FS && a.pre_notag ? hit && m_state(m) != kInvalid : tagged;
-        const unsigned long long f = !(want_f && q == 0) ? ~0ull : FS ? fwv[k] : a.fw[fw_index(a, phys[k])];
+        // keys INVALID at S_0 take their F after this pass (k_local_deferred)
+        const unsigned long long f = hit && m_state(m) != kInvalid && q == 0 ? fwv[k] : ~0ull;
         if (hit) sln[te[k] * 4 + q] = ln[k];
         if (q == 0) {
             sfw[te[k]] = f;
@@ -1838,11 +1676,6 @@ __global__ __launch_bounds__(64) void k_local_fused(BatchArgs a)
         uint8_t *ent = reinterpret_cast<uint8_t *>(&sln[tid * 4]);
         const uint32_t e = sent[tid];
         uint8_t st = kStDone;
-        // the mirrors k_local_pre worked from must describe this element: the PUT-key word, and for
-        // a PUT the state the skip rule was applied to
-        if (a.pkeys && a.error_flags &&
-            (spk[tid] != (x[8] == kOpPut ? ld64(x) : ~0ull) || (x[8] == kOpPut && sps[tid] != x[9])))
-            atomicOr(a.error_flags, 8u);
         if (e != kNone) {
             Ctx c = make_ctx(a);
             const uint8_t bidx = (uint8_t)((uint32_t)i % (uint32_t)a.stride);
@@ -2000,7 +1833,7 @@ __device__ __forceinline__ bool chunk_equal(const uint4 &a, const uint4 &b)
     return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
 }
 
-template <int TYPE, int P = kLookupPair, bool H = false>
+template <int TYPE, int P = kLookupPair>
 __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
 {
     constexpr int E = 16 * P;   // elements per wave: P per lane group
@@ -2040,14 +1873,7 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
             }
         }
     }
-    if (H) {   // located entries (hkv_batch_desc.d_phys)
-        int64_t gi[P];
-#pragma unroll
-        for (int k = 0; k < P; ++k) gi[k] = i0 + te[k];
-        lookup_hinted<P>(a, gi, key, probe, q, gbase, ok, phys, ln);
-    } else {
-        lookup_pair<P>(a, key, probe, q, gbase, ok, phys, ln);
-    }
+    lookup_pair<P>(a, key, probe, q, gbase, ok, phys, ln);
 #pragma unroll
     for (int k = 0; k < P; ++k) {
         Meta m;
@@ -2449,8 +2275,8 @@ __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
     // big values: copied a wave per value after the exec calls (see k_resolve0_direct); the shadow
     // they read (round r-1's first candidate's) is not written in this round
     VCopy vc{nullptr, nullptr};
-    VCopy *vcp = SV != 31 && a.wave_copy && a.g.st_value <= 320 ? &vc : nullptr;
-    const bool wave_shadow = SV != 31 && vcp && a.wave_shadow;   // see k_resolve0_direct
+    VCopy *vcp = SV != 31 && a.g.st_value <= 320 ? &vc : nullptr;
+    const bool wave_shadow = SV != 31 && vcp;   // see k_resolve0_direct
     bool cand = false;
     uint32_t prev = 0;
     if (i < a.n && a.st[i] == kStPend) {
@@ -2482,7 +2308,7 @@ __global__ __launch_bounds__(256) void k_resolve(BatchArgs a, int r)
         apply_to_shadow_wave<TYPE, SV>(a, cand, (uint32_t)i, cand ? shadow_of(a, prev) : nullptr, vc);
         if (cand) note_state(a, i, a.elems + i * a.esz);
     }
-    if (SV != 31) wave_value_copies(vc, a.g.st_value, a.vc_batch);
+    if (SV != 31) wave_value_copies(vc, a.g.st_value, kVcBatch);
     if (r == a.rounds) {  // wave-aggregated append (uniform branch)
         const uint32_t t = agg_ticket(&a.ctr[kCtrFbL], 0u, left);
         if (left) a.fbl[t] = (uint32_t)i;
@@ -3682,20 +3508,6 @@ size_t batch_fw_words(uint64_t log_cap) { return (size_t)(log_cap >> 6); }
 
 uint32_t batch_max_epoch() { return (1u << 29) - 1; }
 
-// k_local_pre with a launch head of HKV_PRE_HEAD elements (1024 default; 512 or 256: fewer loads and
-// LDS inserts per block, later F for hot keys -- experiments)
-static void launch_local_pre(const BatchArgs &a, int64_t n, hipStream_t s)
-{
-    static const int head = getenv("HKV_PRE_HEAD") ? atoi(getenv("HKV_PRE_HEAD")) : kPreHead;
-    const dim3 grid((unsigned)((n + kPreElems - 1) / kPreElems));
-    if (a.pre_notag && !a.cancel && !a.phys_hint && head == kPreHead)
-        hipLaunchKernelGGL((k_local_pre<kPreHead, false, true>), grid, dim3(kPreThreads), 0, s, a);
-    else if (a.phys_hint) hipLaunchKernelGGL((k_local_pre<kPreHead, true>), grid, dim3(kPreThreads), 0, s, a);
-    else if (head == 256) hipLaunchKernelGGL(k_local_pre<256>, grid, dim3(kPreThreads), 0, s, a);
-    else if (head == 512) hipLaunchKernelGGL(k_local_pre<512>, grid, dim3(kPreThreads), 0, s, a);
-    else hipLaunchKernelGGL(k_local_pre<kPreHead>, grid, dim3(kPreThreads), 0, s, a);
-}
-
 int launch_batch(BatchLaunch &bl, hipStream_t s)
 {
     const int64_t n = bl.n;
@@ -3706,14 +3518,9 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.offsets = bl.offsets;
     a.state_out = (bl.type == kLocal || bl.type == kLocalAfterMemb) ? bl.state_out : nullptr;
     a.opc = bl.type == kLocal ? bl.opcode_in : nullptr;
-    a.phys_hint = bl.type == kInvs || bl.type == kVals || bl.type == kLocal ? bl.phys_hint : nullptr;
     a.patch = nullptr;
-    a.big_patch = 0;
-    a.pkeys = nullptr;
-    a.cancel = bl.stage == 3;
     a.ack_out = bl.type == kInvs || (bl.type == kAcks && bl.n_rows > 0) ? bl.ack_out : nullptr;
     a.ack_out_size = bl.ack_out_size;
-    a.pre_notag = 0;
     a.n_rows = bl.n_rows;
     a.skip_row = bl.skip_row;
     a.row_stride = bl.row_stride;
@@ -3727,14 +3534,6 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.dbg = dbg_env;
     static const int check_unique_env = getenv("HKV_CHECK_UNIQUE") ? atoi(getenv("HKV_CHECK_UNIQUE")) : 0;
     a.check_unique = check_unique_env;
-    static const int ppf_env = !getenv("HKV_PRE_PATCH_FIRST") || atoi(getenv("HKV_PRE_PATCH_FIRST")) != 0;
-    a.pre_patch_first = ppf_env;
-    static const int wave_copy_env = !getenv("HKV_WAVE_COPY") || atoi(getenv("HKV_WAVE_COPY")) != 0;
-    a.wave_copy = wave_copy_env;
-    static const int vc_batch_env = getenv("HKV_VC_BATCH") && atoi(getenv("HKV_VC_BATCH")) == 1 ? 1 : kVcBatch;
-    a.vc_batch = vc_batch_env;
-    static const int wave_shadow_env = !getenv("HKV_WAVE_SHADOW") || atoi(getenv("HKV_WAVE_SHADOW")) != 0;
-    a.wave_shadow = wave_shadow_env;
     a.index = bl.index;
     a.log = bl.log;
     a.rw = bl.rw;
@@ -3778,109 +3577,35 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     const unsigned cgrid = (unsigned)((n + 256 * kCandPer - 1) / (256 * kCandPer));
     const bool big = bl.esz > 64;
     // big ops: local and ACK launches resolve round 0 in place (measured at cfg3: local 1.26 ->
-    // 1.05 ms, ACK 0.69 -> 0.55 ms); INV launches keep the LDS slab (0.40 vs 0.52 ms in place).
-    // HKV_BIG_DIRECT=0/1 forces one or the other (experiments).
-    static const int big_env = getenv("HKV_BIG_DIRECT") ? atoi(getenv("HKV_BIG_DIRECT")) : -1;
-    const bool big_direct = big_env >= 0 ? big_env != 0 : bl.type != kInvs;
+    // 1.05 ms, ACK 0.69 -> 0.55 ms); INV launches keep the LDS slab (0.40 vs 0.52 ms in place)
+    const bool big_direct = bl.type != kInvs;
     const unsigned rgrid = (unsigned)(big ? (n + 127) / 128 : grid);
     const size_t rlds = (size_t)(big ? 128 : 256) * (size_t)bl.esz;
-    constexpr int64_t kPer = 64 * kLookupPair;  // elements per k_lookup block
     const bool small = (bl.path == kPathSmall || (bl.path == kPathAuto && n <= kSmallMax)) && n <= kSmallMax;
     if (bl.region_bytes && !small) return -1;  // host-staged launches are small ones
-    // local batches without RMWs in the default layout: the direct path (k_local_pre). HKV_LOCAL_DIRECT=0
-    // runs them on the rounds engine instead (experiments)
-    static const int ld_env = getenv("HKV_LOCAL_DIRECT") ? atoi(getenv("HKV_LOCAL_DIRECT")) : 1;
-    const bool local_direct = ld_env != 0 && bl.type == kLocal && !bl.g.rmw_enabled && bl.esz == 56 &&
-                              bl.g.st_value == 31 && bl.g.entry_size == 64 && !bl.offsets;
-    // HKV_PATCH_APPLY=1: patches always written into the ops first (experiments)
-    static const bool patch_apply_env = getenv("HKV_PATCH_APPLY") && atoi(getenv("HKV_PATCH_APPLY")) != 0;
-    // The prepass sets no seqlock-byte tags and the fused pass loads every hit's F word beside its log
-    // line (round 5, the default; HKV_PRE_NOTAG=0: tags, and F loaded after the line for tagged keys
-    // only). Same box, 3 x 20 steps each (gpurun_out/r05e): 4.355-4.359 -> 4.378-4.393 G ops/s, prepass
-    // 78.1 -> 73.8 us, fused pass level (265.7 / 266.7 us)
-    static const bool notag_env = !getenv("HKV_PRE_NOTAG") || atoi(getenv("HKV_PRE_NOTAG")) != 0;
-    auto set_notag = [&]() {
-        if (notag_env && local_direct && !a.phys_hint) a.pre_notag = 1;
-    };
-    if (bl.stage == 3) {   // HKV_BATCH_PREPASS_CANCEL: the prepass's lookups again, clearing its tags
-        if (bl.pre_done) {
-            if (bl.patch) a.patch = bl.patch;
-            if (bl.put_keys && a.state_out) a.pkeys = bl.put_keys;
-            set_notag();
-            launch_local_pre(a, n, s);
-        }
-        return hipGetLastError() == hipSuccess ? 0 : -3;
-    }
-    if (bl.stage == 1) {   // HKV_BATCH_PREPASS: the direct path's prepass only (any other path runs whole later)
-        if (local_direct && !small && !patch_apply_env) {
-            if (bl.patch) a.patch = bl.patch;
-            if (local_direct && bl.put_keys && a.state_out) a.pkeys = bl.put_keys;
-            set_notag();
-            launch_local_pre(a, n, s);
-            bl.pre_done = 1;
-        }
-        return hipGetLastError() == hipSuccess ? 0 : -3;
-    }
-    // big local launches on the rounds engine: k_lookup reads the patches and k_resolve0_direct writes them
-    // into the ops (HKV_BIG_PATCH=0: k_apply_patch first)
-    static const bool big_patch_env = !getenv("HKV_BIG_PATCH") || atoi(getenv("HKV_BIG_PATCH")) != 0;
-    const bool big_patch = bl.patch && big_patch_env && !small && !local_direct && !patch_apply_env && big && big_direct &&
-                           (bl.type == kLocal || bl.type == kLocalAfterMemb) && bl.esz % 8 == 0 &&
-                           bl.esz >= kOpValueOff + (int32_t)bl.g.st_value && !a.phys_hint;
-    a.big_patch = big_patch ? 1 : 0;
-    if (big_patch) {
-        a.patch = bl.patch;
-    } else if (bl.patch && (small || !local_direct || patch_apply_env)) {  // the other paths take the patches as op writes first
+    // local batches without RMWs in the default layout: the direct path (k_local_pre, k_local_fused)
+    const bool local_direct = bl.type == kLocal && !bl.g.rmw_enabled && bl.esz == 56 && bl.g.st_value == 31 &&
+                              bl.g.entry_size == 64 && !bl.offsets;
+    if (bl.patch && (small || !local_direct)) {  // the other paths take the patches as op writes first
         hipLaunchKernelGGL(k_apply_patch, dim3(grid), dim3(256), 0, s, bl.elems, bl.patch, n, bl.esz, bl.g.st_value);
     } else if (bl.patch) {
         a.patch = bl.patch;
     }
-    if (local_direct && !small && bl.put_keys && a.state_out) a.pkeys = bl.put_keys;
-    if (!small) set_notag();
     if (small) {
         if (launch_small(a, s)) return -3;
         return 0;                              // node_suspected written by the kernel
     } else if (local_direct) {
-        if (bl.stage == 2 && bl.pre_done) {   // the prepass ran earlier (HKV_BATCH_PREPASS)
-            if (bl.reset_defer && hipMemsetAsync(bl.ctr + kCtrDefer, 0, 4, s) != hipSuccess) return -3;
-        } else {
-            launch_local_pre(a, n, s);
-        }
-        // HKV_LF_PAIR: elements per lane group in k_local_fused (2: 32 per wave; 4: 64, more loads in flight)
-        static const int lfp_env = getenv("HKV_LF_PAIR") ? atoi(getenv("HKV_LF_PAIR")) : 2;
-        // HKV_LF_FSPEC=1: every hit loads its key's F word beside the log line (no dependent load after it)
-        static const bool fspec_env = getenv("HKV_LF_FSPEC") && atoi(getenv("HKV_LF_FSPEC")) != 0;
-        if (a.pre_notag)
-            hipLaunchKernelGGL((k_local_fused<2, false, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
-        else if (fspec_env && !a.phys_hint && lfp_env == 2)
-            hipLaunchKernelGGL((k_local_fused<2, false, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
-        else if (a.phys_hint)
-            hipLaunchKernelGGL((k_local_fused<2, true>), dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
-        else if (lfp_env == 4)
-            hipLaunchKernelGGL(k_local_fused<4>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, a);
-        else if (lfp_env == 1)
-            hipLaunchKernelGGL(k_local_fused<1>, dim3((unsigned)((n + 15) / 16)), dim3(64), 0, s, a);
-        else
-            hipLaunchKernelGGL(k_local_fused<2>, dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(k_local_pre<kPreHead>, dim3((unsigned)((n + kPreElems - 1) / kPreElems)), dim3(kPreThreads),
+                           0, s, a);
+        hipLaunchKernelGGL(k_local_fused<2>, dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
         // the waiting elements' count is on the device: enough workgroups for the rounds after a
         // membership change (configs[4]: ~100 K elements of keys a failed peer left INVALID), which
-        // return at once when there are few (HKV_DEFER_BLOCKS: the grid, experiments)
-        static const int defer_blocks = getenv("HKV_DEFER_BLOCKS") ? std::max(1, atoi(getenv("HKV_DEFER_BLOCKS"))) : 128;
-        hipLaunchKernelGGL(k_local_deferred, dim3((unsigned)defer_blocks), dim3(256), 0, s, a);
-        // HKV_COMMIT_W=0: the thread-per-element k_commit (experiments)
-        static const bool commit_w_env = !getenv("HKV_COMMIT_W") || atoi(getenv("HKV_COMMIT_W")) != 0;
-        if (commit_w_env)
-            hipLaunchKernelGGL(k_commit_w, dim3((unsigned)((n + 4 * kCwElems - 1) / (4 * kCwElems))), dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL((k_commit<31>), dim3(grid), dim3(256), 0, s, a);
+        // return at once when there are few
+        hipLaunchKernelGGL(k_local_deferred, dim3(128u), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_commit_w, dim3((unsigned)((n + 4 * kCwElems - 1) / (4 * kCwElems))), dim3(256), 0, s, a);
     } else if (bl.n_rows > 0 && bl.unique) {  // HKV_BATCH_ROWS: one pass over positions of all rows
-        // positions per lane group (HKV_ROWS_PAIR=1: 16 per wave instead of 32; ACKs of 16 B only)
-        static const int rp = getenv("HKV_ROWS_PAIR") ? atoi(getenv("HKV_ROWS_PAIR")) : 2;
-        const unsigned lgrid = (unsigned)((n + kLfElems - 1) / kLfElems), g1 = (unsigned)((n + 15) / 16);
-        if (rp == 1 && bl.type == kAcks && bl.esz <= 16) {
-            if (bl.n_rows <= 2) hipLaunchKernelGGL((k_unique_rows<kAcks, 2, 1, 1>), dim3(g1), dim3(64), 0, s, a);
-            else hipLaunchKernelGGL((k_unique_rows<kAcks, 8, 1, 1>), dim3(g1), dim3(64), 0, s, a);
-        } else
+        // two positions per lane group, 32 per wave
+        const unsigned lgrid = (unsigned)((n + kLfElems - 1) / kLfElems);
         // elements of 16 B (ACKs without RMWs) keep one chunk each in LDS, others four
         if (bl.type == kInvs) {
             if (bl.n_rows <= 2) hipLaunchKernelGGL((k_unique_rows<kInvs, 2, 4>), dim3(lgrid), dim3(64), 0, s, a);
@@ -3893,46 +3618,24 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
             else hipLaunchKernelGGL((k_unique_rows<kAcks, 8, 4>), dim3(lgrid), dim3(64), 0, s, a);
         }
     } else if (bl.unique && (bl.type == kInvs || bl.type == kAcks)) {  // one pass: every key has one element
-        constexpr int64_t kPerU = 64 * kLookupPair;
-        const unsigned ugrid = (unsigned)((n + kPerU - 1) / kPerU);
-        // in-place unique pass (big-entry ACKs, other geometries): elements per lane group as HKV_UNIQUE_PAIR
-        static const int upi = getenv("HKV_UNIQUE_PAIR") ? atoi(getenv("HKV_UNIQUE_PAIR")) : 1;
+        // in-place unique pass (big-entry ACKs, other geometries): one element per lane group
         const unsigned ugrid1 = (unsigned)((n + 63) / 64);
 #define HKV_UNIQUE(T)                                                                                  \
     do {                                                                                               \
-        if (upi == 1) {                                                                                \
-            if (bl.g.st_value == 31) hipLaunchKernelGGL((k_unique<T, 31, 1>), dim3(ugrid1), dim3(256), 0, s, a); \
-            else if (bl.g.st_value == 287) hipLaunchKernelGGL((k_unique<T, 287, 1>), dim3(ugrid1), dim3(256), 0, s, a); \
-            else hipLaunchKernelGGL((k_unique<T, 0, 1>), dim3(ugrid1), dim3(256), 0, s, a);         \
-        } else if (bl.g.st_value == 31) hipLaunchKernelGGL((k_unique<T, 31>), dim3(ugrid), dim3(256), 0, s, a); \
-        else if (bl.g.st_value == 287) hipLaunchKernelGGL((k_unique<T, 287>), dim3(ugrid), dim3(256), 0, s, a); \
-        else hipLaunchKernelGGL((k_unique<T, 0>), dim3(ugrid), dim3(256), 0, s, a);                   \
+        if (bl.g.st_value == 31) hipLaunchKernelGGL((k_unique<T, 31, 1>), dim3(ugrid1), dim3(256), 0, s, a); \
+        else if (bl.g.st_value == 287) hipLaunchKernelGGL((k_unique<T, 287, 1>), dim3(ugrid1), dim3(256), 0, s, a); \
+        else hipLaunchKernelGGL((k_unique<T, 0, 1>), dim3(ugrid1), dim3(256), 0, s, a);             \
     } while (0)
-        // 64-B entries: the LDS-staged pass (HKV_UNIQUE_LDS=0: the in-place one, experiments)
-        static const bool ulds_env = !getenv("HKV_UNIQUE_LDS") || atoi(getenv("HKV_UNIQUE_LDS")) != 0;
-        if (a.ack_out && !(ulds_env && ((bl.g.st_value == 31 && bl.g.entry_size == 64 && bl.esz <= 64) ||
-                                         (bl.type == kInvs && bl.g.st_value == 287 && bl.g.entry_size == 320 &&
-                                          bl.esz <= 320))))
-            return -1;   // only the LDS-staged passes write the ACKs
-        if (ulds_env && bl.g.st_value == 31 && bl.g.entry_size == 64 && bl.esz <= 64) {
-            // elements per lane group (HKV_UNIQUE_PAIR): 1 by default, 16 per wave. Same box, INV phase per
-            // step (gpurun_out/r04m, r04t): 72-77 us at 1, 78-80 at 2, 91 at 4
-            static const int up = getenv("HKV_UNIQUE_PAIR") ? atoi(getenv("HKV_UNIQUE_PAIR")) : 1;
-            if (up == 1) {
-                const unsigned g1 = (unsigned)((n + 15) / 16);
-                if (bl.type == kInvs && a.phys_hint) hipLaunchKernelGGL((k_unique_lds<kInvs, 1, true>), dim3(g1), dim3(64), 0, s, a);
-                else if (bl.type == kInvs) hipLaunchKernelGGL((k_unique_lds<kInvs, 1>), dim3(g1), dim3(64), 0, s, a);
-                else hipLaunchKernelGGL((k_unique_lds<kAcks, 1>), dim3(g1), dim3(64), 0, s, a);
-            } else if (up == 4) {
-                const unsigned g4 = (unsigned)((n + 63) / 64);
-                if (bl.type == kInvs) hipLaunchKernelGGL((k_unique_lds<kInvs, 4>), dim3(g4), dim3(64), 0, s, a);
-                else hipLaunchKernelGGL((k_unique_lds<kAcks, 4>), dim3(g4), dim3(64), 0, s, a);
-            } else {
-                const unsigned lgrid = (unsigned)((n + kLfElems - 1) / kLfElems);
-                if (bl.type == kInvs) hipLaunchKernelGGL((k_unique_lds<kInvs>), dim3(lgrid), dim3(64), 0, s, a);
-                else hipLaunchKernelGGL((k_unique_lds<kAcks>), dim3(lgrid), dim3(64), 0, s, a);
-            }
-        } else if (ulds_env && bl.type == kInvs && bl.g.st_value == 287 && bl.g.entry_size == 320 && bl.esz <= 320) {
+        const bool lds64 = bl.g.st_value == 31 && bl.g.entry_size == 64 && bl.esz <= 64;
+        const bool lds_big = bl.type == kInvs && bl.g.st_value == 287 && bl.g.entry_size == 320 && bl.esz <= 320;
+        if (a.ack_out && !(lds64 || lds_big)) return -1;   // only the LDS-staged passes write the ACKs
+        if (lds64) {
+            // 64-B entries: the LDS-staged pass, one element per lane group (16 per wave). Same box, INV phase
+            // per step (gpurun_out/r04m, r04t): 72-77 us at 1 element per lane group, 78-80 at 2, 91 at 4
+            const unsigned g1 = (unsigned)((n + 15) / 16);
+            if (bl.type == kInvs) hipLaunchKernelGGL((k_unique_lds<kInvs, 1>), dim3(g1), dim3(64), 0, s, a);
+            else hipLaunchKernelGGL((k_unique_lds<kAcks, 1>), dim3(g1), dim3(64), 0, s, a);
+        } else if (lds_big) {
             // big-object INVs, whose raises copy 287-B values: staged through LDS (cfg3: 460 -> 326 us per
             // round). ACKs touch the header and the meta only, so they stay in place (LDS-staged: 110 -> 191 us)
             hipLaunchKernelGGL(k_unique_big<kInvs>, dim3((unsigned)((n + kUbElems - 1) / kUbElems)), dim3(64), 0, s, a);
@@ -3940,13 +3643,9 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
         else HKV_UNIQUE(kAcks);
 #undef HKV_UNIQUE
     } else if (bl.type == kVals) {             // one pass (see k_lookup)
-        // elements per lane group (HKV_VAL_PAIR): 1 by default. Same box, VAL batch per step (gpurun_out/r04m,
-        // r04u): 49.6-50.2 us at 1, 52.3-53.9 at 2, 57 at 4
-        static const int vp = getenv("HKV_VAL_PAIR") ? atoi(getenv("HKV_VAL_PAIR")) : 1;
-        if (a.phys_hint) hipLaunchKernelGGL((k_lookup<1, true>), dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, a, (int64_t)0, n);
-        else if (vp == 4) hipLaunchKernelGGL(k_lookup<4>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, (int64_t)0, n);
-        else if (vp == 1) hipLaunchKernelGGL(k_lookup<1>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, a, (int64_t)0, n);
-        else hipLaunchKernelGGL(k_lookup<>, dim3((unsigned)((n + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, n);
+        // one element per lane group. Same box, VAL batch per step (gpurun_out/r04m, r04u): 49.6-50.2 us at 1,
+        // 52.3-53.9 at 2, 57 at 4
+        hipLaunchKernelGGL(k_lookup<1>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, a, (int64_t)0, n);
         return hipGetLastError() == hipSuccess ? 0 : -3;
     } else {
     // The head split pays off where one launch piles many candidates onto a few keys: local
@@ -3954,17 +3653,10 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     // round, so those launches take one pass (their launch-sized head took ~9 us at cfg2).
     const bool split = bl.type == kLocal || bl.type == kLocalAfterMemb;
     const int64_t head = split && n > kLookupHead ? kLookupHead : n;
-    // elements per lane group of the other lookups (HKV_LOOKUP_PAIR, 1 by default: configs[2] 0.627-0.635
-    // against 0.620-0.622 G ops/s at 2, same box, gpurun_out/r04v)
-    static const int lp = getenv("HKV_LOOKUP_PAIR") ? atoi(getenv("HKV_LOOKUP_PAIR")) : 1;
-    if (lp == 1) {
-        hipLaunchKernelGGL(k_lookup<1>, dim3((unsigned)((head + 63) / 64)), dim3(256), 0, s, a, (int64_t)0, head);
-        if (n > head) hipLaunchKernelGGL(k_lookup<1>, dim3((unsigned)((n - head + 63) / 64)), dim3(256), 0, s, a, head, n);
-    } else {
-        hipLaunchKernelGGL(k_lookup<>, dim3((unsigned)((head + kPer - 1) / kPer)), dim3(256), 0, s, a, (int64_t)0, head);
-        if (n > head)
-            hipLaunchKernelGGL(k_lookup<>, dim3((unsigned)((n - head + kPer - 1) / kPer)), dim3(256), 0, s, a, head, n);
-    }
+    // one element per lane group in the other lookups (configs[2] 0.627-0.635 against 0.620-0.622 G ops/s at
+    // two, same box, gpurun_out/r04v)
+    hipLaunchKernelGGL(k_lookup<1>, dim3((unsigned)((head + 63) / 64)), dim3(256), 0, s, a, (int64_t)0, head);
+    if (n > head) hipLaunchKernelGGL(k_lookup<1>, dim3((unsigned)((n - head + 63) / 64)), dim3(256), 0, s, a, head, n);
     if (a.ack_direct) {
         hipLaunchKernelGGL(k_ack_resolve, dim3(grid), dim3(256), 0, s, a);
     } else if (a.inv_direct) {
@@ -4007,13 +3699,6 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     }
     }
     if (hipGetLastError() != hipSuccess) return -3;
-    static const bool stats = getenv("HKV_STATS") != nullptr;
-    if (stats) {  // debug: what reached the fallback (synchronises the stream)
-        uint32_t c[4] = {0, 0, 0, 0};
-        hipMemcpyAsync(c, bl.ctr, sizeof c, hipMemcpyDeviceToHost, s);
-        hipStreamSynchronize(s);
-        fprintf(stderr, "[hkv] batch type %d n %lld: fallback members %u\n", bl.type, (long long)n, c[kCtrFbL]);
-    }
     if (bl.type == kInvs && bl.ns_idx && bl.node_suspected) {
         hipLaunchKernelGGL(k_node_suspected, dim3((bl.n_batches + 255) / 256), dim3(256), 0, s, bl.elems, bl.ns_idx,
                            bl.node_suspected, bl.n_batches, bl.stride, bl.esz, bl.offsets);

@@ -18,9 +18,7 @@ struct BatchLaunch {
     uint8_t *state_out;          // local launches: each element's final state byte (may be NULL)
     const uint8_t *opcode_in;    // local launches: the caller's mirror of each element's opcode (may be NULL)
     const uint8_t *patch;        // local launches: pending header writes, 16 B per element (may be NULL)
-    const uint64_t *phys_hint;   // INV / VAL launches: each element's located log offset (hkv_batch_desc.d_phys)
     uint8_t *rw_state;           // ACK launches: state-byte mirror of read_write_ops (may be NULL)
-    const uint64_t *put_keys;    // local launches: PUT-key mirror (state_out holds the entry states), or NULL
     const uint8_t *index;
     uint8_t *log;
     uint8_t *rw;
@@ -46,9 +44,6 @@ struct BatchLaunch {
     uint8_t g_membership;
     uint8_t w_ack_init;
     int32_t path;                             // kPath*: which engine runs the launch
-    int32_t stage;                            // 0 whole launch, 1 local prepass only, 2 after a prepass
-    int32_t pre_done;                         // stage 2: the prepass ran in stage 1 (else it runs now)
-    int32_t reset_defer;                      // stage 2: the scratch moved since stage 1 (zero its counter)
     int32_t unique;                           // HKV_BATCH_UNIQUE: no key twice in the launch
     int32_t n_rows, skip_row;                 // HKV_BATCH_ROWS (n_rows 0: a plain launch)
     uint8_t *ack_out;                         // INV launches: the ACK marshal's output (hkv_batch_desc.d_ack_out)
@@ -173,7 +168,7 @@ struct TableView {
 };
 int table_view(const hkv_table *t, TableView *out);
 
-int launch_batch(BatchLaunch &bl, hipStream_t s);   // sets bl.pre_done (stage 1)
+int launch_batch(BatchLaunch &bl, hipStream_t s);
 constexpr int64_t kSmallMaxElems = 4096;   // launches the single-workgroup kernel can take
 int launch_populate(const PopulateLaunch &pl, hipStream_t s);
 int launch_hash_ids(const uint32_t *ids, uint64_t *out, int64_t n, hipStream_t s);

@@ -590,21 +590,14 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.elems = d->d_elems;
     bl.counts = packed ? nullptr : d->d_counts;
     bl.state_out = d->d_state_out;
-    static const bool opc_off = getenv("HKV_OPCODE_IN") && atoi(getenv("HKV_OPCODE_IN")) == 0;  // experiments
-    bl.opcode_in = (d->type == kLocal || d->type == kAcks) && !opc_off ? d->d_opcode_in : nullptr;
+    bl.opcode_in = d->type == kLocal || d->type == kAcks ? d->d_opcode_in : nullptr;
     bl.patch = d->type == kLocal ? d->d_patch : nullptr;
     bl.rw_state = d->type == kAcks ? d->d_rw_state : nullptr;
-    // HKV_PUT_KEYS=0: the PUT-key mirror ignored (experiments)
-    static const bool pk_off = getenv("HKV_PUT_KEYS") && atoi(getenv("HKV_PUT_KEYS")) == 0;
-    bl.put_keys = d->type == kLocal && d->d_state_out && !pk_off ? d->d_put_keys : nullptr;
     if (bl.patch && ((uintptr_t)bl.patch & 15)) return fail(-1, "d_patch must be 16-byte aligned");
-    if (d->d_phys) {   // located entries: unique INV launches (not rows) and VAL launches, on the engine
-        if (!((d->type == kInvs && (d->flags & HKV_BATCH_UNIQUE) && d->n_rows <= 1) || d->type == kVals ||
-              d->type == kLocal) || ((uintptr_t)d->d_phys & 7))
-            return fail(-1, "d_phys: local, unique INV or VAL launches, 8-byte aligned");
-        bl.phys_hint = d->d_phys;
-    }
-    if (bl.put_keys && ((uintptr_t)bl.put_keys & 7)) return fail(-1, "d_put_keys must be 8-byte aligned");
+    // reserved since ABI 8 (the PUT-key mirror, located entries and the two-stage local launch were
+    // measured, not adopted, and removed): a caller that sets them gets an error, not a silent no-op
+    if (d->d_put_keys || d->d_phys) return fail(-1, "d_put_keys and d_phys are reserved (must be NULL)");
+    if (d->flags & HKV_BATCH_RESERVED_FLAGS) return fail(-1, "hkv_batch_desc.flags: reserved bits set");
     bl.offsets = packed ? d->d_counts : nullptr;
     bl.index = t->d_index;
     bl.log = t->d_log;
@@ -618,38 +611,12 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.fy = bl.fx + batch_fw_words(t->cfg.log_cap);
     bl.ft = bl.fy + batch_fw_words(t->cfg.log_cap);
 
-    const int stage = (d->flags & HKV_BATCH_PREPASS_CANCEL) ? 3 : (d->flags & HKV_BATCH_PREPASSED) ? 2
-                    : (d->flags & HKV_BATCH_PREPASS) ? 1 : 0;
-    if (stage && d->type != kLocal) return fail(-1, "HKV_BATCH_PREPASS/PREPASSED apply to local batches");
-    bool force_engine = false;
-    if (t->pre.valid && stage < 2) {
-        // between a prepass and the rest of its launch only VAL batches may run, on the engine's one-pass
-        // VAL lookup, which stores the state byte alone (the single-workgroup kernel writes whole metas
-        // back, and with them the seqlock bytes the prepass tagged)
-        if (d->type != kVals) return fail(-1, "a local launch's prepass is pending: finish or cancel it first");
-        force_engine = true;
+    if (++t->epoch > batch_max_epoch()) {  // round tags would wrap: start the F and T words over
+        HIP_TRY(hipMemsetAsync(t->d_fw, 0xFF, 8 * batch_fw_words(t->cfg.log_cap), s));
+        HIP_TRY(hipMemsetAsync(bl.ft, 0, 64 * batch_fw_words(t->cfg.log_cap), s));
+        t->epoch = 1;
     }
-    if (stage >= 2) {   // the rest of a launch whose prepass ran: its epoch (tags, F words), no new one
-        if (!t->pre.valid || t->pre.n != n || t->pre.elems != d->d_elems)
-            return fail(-1, "HKV_BATCH_PREPASSED without the matching HKV_BATCH_PREPASS launch");
-        t->pre.valid = false;
-        bl.epoch = t->pre.epoch;
-        bl.pre_done = t->pre.done;
-        bl.reset_defer = t->pre.scratch_gen != t->scratch_gen;
-    } else if (force_engine) {
-        // a VAL launch between a prepass and the rest of its launch: the one-pass VAL lookup uses no
-        // round tag, so it takes the current epoch and can never wrap it under the pending prepass
-        bl.epoch = t->epoch;
-    } else {
-        if (++t->epoch > batch_max_epoch()) {  // round tags would wrap: start the F and T words over
-            HIP_TRY(hipMemsetAsync(t->d_fw, 0xFF, 8 * batch_fw_words(t->cfg.log_cap), s));
-            HIP_TRY(hipMemsetAsync(bl.ft, 0, 64 * batch_fw_words(t->cfg.log_cap), s));
-            t->epoch = 1;
-            t->pre.valid = false;   // a pending prepass's offers are gone: its second call fails
-        }
-        bl.epoch = t->epoch;
-    }
-    bl.stage = stage;
+    bl.epoch = t->epoch;
     bl.error_flags = t->d_error_flags;
     bl.n = n;
     bl.n_batches = d->n_batches;
@@ -661,7 +628,6 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     bl.path = (d->flags & HKV_BATCH_ENGINE) || packed ? kPathEngine
             : (d->flags & HKV_BATCH_SMALL) ? kPathSmall : kPathAuto;
     bl.unique = (d->flags & HKV_BATCH_UNIQUE) && (d->type == kInvs || d->type == kAcks) ? 1 : 0;
-    if (force_engine) bl.path = kPathEngine;
     if (d->d_ack_out && d->type == kAcks) {   // the VAL callbacks, by the ACK rows launch
         if (!(d->flags & HKV_BATCH_ROWS) || !bl.unique || d->elem_size != 16 || d->ack_out_size != 16 ||
             t->geo.entry_size != 64 || t->geo.st_value != 31 || ((uintptr_t)d->d_ack_out & 15))
@@ -695,14 +661,6 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     TRACE("batch_async type=%d n=%lld", d->type, (long long)n);
     rc = launch_batch(bl, s);
     if (rc) return fail(rc, "batch launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));
-    if (stage == 1) {   // launch_batch set pre_done when the launch takes the direct path
-        t->pre.valid = true;
-        t->pre.done = bl.pre_done != 0;
-        t->pre.epoch = bl.epoch;
-        t->pre.scratch_gen = t->scratch_gen;
-        t->pre.n = n;
-        t->pre.elems = d->d_elems;
-    }
     return 0;
 }
 
@@ -827,7 +785,6 @@ static void host_stats_note(int nb)
     g_hs_batches += nb;
 }
 
-static const bool g_staging_nc = getenv("HKV_STAGING_NC") != nullptr;  // experiment: non-coherent staging
 
 // HKV_HOST_TIMING=1: where a host-pointer call's time goes (staging, queue + launch + GPU, copy-out),
 // averaged over the calls and printed at exit
@@ -867,7 +824,7 @@ static void host_set_reserve(HostSet *set, size_t total)
         set->d = set->h = set->hd = nullptr;
         const size_t cap = std::max(total + total / 2, (size_t)1 << 20);
         if (hipMalloc(&set->d, cap) != hipSuccess ||
-            hipHostMalloc((void **)&set->h, cap, hipHostMallocMapped | (g_staging_nc ? hipHostMallocNonCoherent : hipHostMallocCoherent)) != hipSuccess ||
+            hipHostMalloc((void **)&set->h, cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
             hipHostGetDevicePointer((void **)&set->hd, set->h, 0) != hipSuccess)
             die("staging alloc");
         set->cap = cap;
@@ -1075,8 +1032,7 @@ static void srv_ensure(hkv_table *t)
     sl.life_ticks = (uint64_t)1e8;                 // 1 s, then a fresh server
     static const int merge = getenv("HKV_SERVE_MERGE") ? std::max(1, atoi(getenv("HKV_SERVE_MERGE"))) : kServeMerge;
     sl.merge = std::min(merge, kRingN / 2);
-    static const int spec = !getenv("HKV_SERVE_SPEC") || atoi(getenv("HKV_SERVE_SPEC")) != 0;
-    sl.spec = spec;
+    sl.spec = 1;   // the first launch's headers read beside the merge scan (round 5: 1 thread 7.2 -> 8.5 M)
     for (int g = 0; g < kPartG; ++g) sl.start[g] = __atomic_load_n(t->pflags + g, __ATOMIC_ACQUIRE) + 1;
     srv_set_stop(t, 0u);
     if (!t->srv_ev && hipEventCreateWithFlags(&t->srv_ev, hipEventDisableTiming) != hipSuccess) die("event");
@@ -1116,12 +1072,10 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
     // (gpurun_out/r04z), 8.6-8.8 / 24.0-27.0 / 40.7-43.7 M local ops/s from 1 / 8 / 16 threads against
     // 6.1-6.9 / 23.0-26.0 / 35.6-44.1 M launched. HKV_HOST_SERVE=0 / 1 forces either.
     static const bool serve = getenv("HKV_HOST_SERVE") ? atoi(getenv("HKV_HOST_SERVE")) != 0 : stage_vram_usable();
-    // HKV_PART_STREAMS=n (at most kPartStreams): the launches go round n streams, each partition's
-    // launches ordered on the device. Measured, not adopted (round 4): 4 streams ran 8 / 16 caller
-    // threads at 7.9-9.3 / 14.5-15.7 M local ops/s against 20.4-21.0 / 34.9-36.0 M on the one table
-    // stream (1, the default), the same at 1 thread
-    static const int n_streams = serve ? 1 : std::max(1, std::min(kPartStreams, getenv("HKV_PART_STREAMS") ?
-                                                                    atoi(getenv("HKV_PART_STREAMS")) : 1));
+    // One stream: launches round 4 streams, each partition's launches ordered on the device, were
+    // measured (round 4) and ran 8 / 16 caller threads at 7.9-9.3 / 14.5-15.7 M local ops/s against
+    // 20.4-21.0 / 34.9-36.0 M on the one table stream; that switch is gone (kept in git history)
+    constexpr int n_streams = 1;
     static const int inflight = std::min(kRingN, getenv("HKV_PART_INFLIGHT") ? std::max(1, atoi(getenv("HKV_PART_INFLIGHT")))
                                                                               : serve ? 4 : n_streams > 1 ? 2 * n_streams : 2);
     if (n_streams > 1 && !t->n_pstreams) {
@@ -1419,7 +1373,7 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
     }
     srv_stop_locked(t);   // the launches below run on the table's stream, behind the serving kernel
     HostSet *set = nullptr;
-    static const int n_sets = getenv("HKV_HOST_SETS") ? std::max(1, std::min(kHostSets, atoi(getenv("HKV_HOST_SETS")))) : kHostSets;
+    constexpr int n_sets = kHostSets;
     for (;;) {
         for (int k = 0; k < n_sets; ++k) {
             HostSet &hs = t->sets[k];

@@ -488,8 +488,7 @@ __global__ __launch_bounds__(256) void k_refill_plan_w(uint8_t *states, int32_t 
                                                        uint32_t st_value, uint32_t shift, const uint64_t *tkey,
                                                        const uint8_t *top, int32_t tlen, uint32_t *cursor,
                                                        uint32_t machine_id, uint32_t flags,
-                                                       unsigned long long *counters, uint8_t *opc, uint8_t *patch,
-                                                       uint64_t *put_keys, const uint64_t *tphys, uint64_t *sphys)
+                                                       unsigned long long *counters, uint8_t *opc, uint8_t *patch)
 {
     const int lane = threadIdx.x & 63;
     const int wb = (blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * WPW;
@@ -537,7 +536,7 @@ __global__ __launch_bounds__(256) void k_refill_plan_w(uint8_t *states, int32_t 
         }
     }
     uint8_t oc[WPW][4];
-    uint64_t key[WPW][4], kph[WPW][4];
+    uint64_t key[WPW][4];
 #pragma unroll
     for (int v = 0; v < WPW; ++v)
 #pragma unroll
@@ -546,7 +545,6 @@ __global__ __launch_bounds__(256) void k_refill_plan_w(uint8_t *states, int32_t 
             const int64_t t = (int64_t)(wb + v) * tlen + (int64_t)((base[v] + (uint32_t)rank[v][r]) % (uint32_t)tlen);
             oc[v][r] = rf ? top[t] : (uint8_t)0;
             key[v][r] = rf ? tkey[t] : 0ull;
-            kph[v][r] = rf && tphys ? tphys[t] : ~0ull;   // the new key's located entry
         }
 #pragma unroll
     for (int v = 0; v < WPW; ++v) {
@@ -567,11 +565,6 @@ __global__ __launch_bounds__(256) void k_refill_plan_w(uint8_t *states, int32_t 
                       ((uint64_t)(get ? 0u : (uint8_t)('a' + machine_id)) << 32) |
                       ((uint64_t)(get && (flags & HKV_WL_READ_TS_RESET) ? 1u : 0u) << 40) | (1ull << 48);
                 opc[e] = o;
-                if (sphys) sphys[e] = kph[v][r];
-                if (put_keys) {   // the PUT-key mirror and the entry state of the patched op
-                    put_keys[e] = o == kOpPut ? p.a : HKV_NO_PUT;
-                    states[e] = kNew;
-                }
             }
             *reinterpret_cast<W16 *>(patch + e * 16) = p;
         }
@@ -779,19 +772,11 @@ __global__ __launch_bounds__(256) void k_marshal_invs_w(uint8_t *ops, int32_t n_
     }
 }
 
-// HKV_MARSHAL_WAVE: the INV marshals copy the sent ops four lanes per op (1, default) or one lane per op (0)
-static bool marshal_wave()
-{
-    static const bool v = !getenv("HKV_MARSHAL_WAVE") || atoi(getenv("HKV_MARSHAL_WAVE")) != 0;
-    return v;
-}
-
-// workers per wave of the wave-per-worker workload kernels (HKV_WL_WPW, 1 or 2)
-static int wl_wpw()
-{
-    static const int w = getenv("HKV_WL_WPW") && atoi(getenv("HKV_WL_WPW")) == 1 ? 1 : 2;
-    return w;
-}
+// The INV marshals copy the sent ops four lanes per op from a list in LDS (round 4: 4.18 -> 4.23 G ops/s
+// against one lane per op), and the wave-per-worker workload kernels take two workers per wave (round 4:
+// refill plan 34 -> 31 us, marshal 34 -> 33 us against one)
+static bool marshal_wave() { return true; }
+static int wl_wpw() { return 2; }
 
 // wings_issue_pkts(inv) with the INV callbacks of hermes_worker.c:12-65. At most out_stride
 // INVs per worker go out per round (the send credits); the rest keep their state and are
@@ -1806,8 +1791,9 @@ int hkv_wl_refill_st(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t o
     if (stride > 256 || n_workers <= 0 || tlen <= 0 || !states || !opc) return -1;
     if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET)) return -1;   // no hot-request coalescing
     if (!(op_size > 64 && op_size % 8 == 0 && st_value >= 6 && (kOpValueOff - 16 + st_value) / 8 + 7 <= 64)) return -1;
-    // one wave per worker (HKV_REFILL_ST_W=0: the workgroup-per-worker k_refill_direct)
-    static const bool st_w = !getenv("HKV_REFILL_ST_W") || atoi(getenv("HKV_REFILL_ST_W")) != 0;
+    // one wave per worker (round 4: level with the workgroup-per-worker k_refill_direct, kept for its
+    // ballot-only ranks)
+    constexpr bool st_w = true;
     if (st_w)
         hipLaunchKernelGGL(k_refill_st_w, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream, ops,
                            n_workers, stride, op_size, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
@@ -1818,43 +1804,17 @@ int hkv_wl_refill_st(uint8_t *ops, int32_t n_workers, int32_t stride, uint32_t o
     return ok();
 }
 
-static int refill_plan(uint8_t *states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
+int hkv_wl_refill_plan(uint8_t *states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
                        const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor, uint32_t machine_id,
-                       uint32_t flags, unsigned long long *counters, uint8_t *opc, uint8_t *patch,
-                       uint64_t *put_keys, const uint64_t *tphys, uint64_t *sphys, void *stream)
+                       uint32_t flags, unsigned long long *counters, uint8_t *opc, uint8_t *patch, void *stream)
 {
     if (stride > 256 || n_workers <= 0 || tlen <= 0 || !states || !opc || !patch) return -1;
     if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET)) return -1;   // no hot-request coalescing
-    if (((uintptr_t)patch & 15) || ((uintptr_t)put_keys & 7) || (st_value >> shift) > 255) return -1;   // val_len: a byte
-    if ((!tphys) != (!sphys) || ((uintptr_t)tphys & 7) || ((uintptr_t)sphys & 7)) return -1;
-    if (wl_wpw() == 2)
-        hipLaunchKernelGGL(k_refill_plan_w<2>, dim3((unsigned)((n_workers + 7) / 8)), dim3(256), 0, (hipStream_t)stream,
-                           states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
-                           counters, opc, patch, put_keys, tphys, sphys);
-    else
-        hipLaunchKernelGGL(k_refill_plan_w<1>, dim3((unsigned)((n_workers + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
-                           states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
-                           counters, opc, patch, put_keys, tphys, sphys);
+    if (((uintptr_t)patch & 15) || (st_value >> shift) > 255) return -1;   // val_len: a byte
+    hipLaunchKernelGGL(k_refill_plan_w<2>, dim3((unsigned)((n_workers + 7) / 8)), dim3(256), 0, (hipStream_t)stream,
+                       states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
+                       counters, opc, patch);
     return ok();
-}
-
-int hkv_wl_refill_plan(uint8_t *states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
-                       const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor, uint32_t machine_id,
-                       uint32_t flags, unsigned long long *counters, uint8_t *opc, uint8_t *patch,
-                       uint64_t *put_keys, void *stream)
-{
-    return refill_plan(states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags, counters,
-                       opc, patch, put_keys, nullptr, nullptr, stream);
-}
-
-int hkv_wl_refill_plan_located(uint8_t *states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
-                               const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor,
-                               uint32_t machine_id, uint32_t flags, unsigned long long *counters, uint8_t *opc,
-                               uint8_t *patch, uint64_t *put_keys, const uint64_t *tphys, uint64_t *sphys, void *stream)
-{
-    if (!tphys || !sphys) return -1;
-    return refill_plan(states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags, counters,
-                       opc, patch, put_keys, tphys, sphys, stream);
 }
 
 int hkv_wl_fold_counters(unsigned long long *counters, void *stream)
@@ -2201,17 +2161,6 @@ int hkv_wl_peer_ts_at(hkv_table *t, uint8_t *invs, uint8_t *vals, const uint64_t
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_peer_ts_at, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, tv, invs, vals, phys, n,
                        op_size, peer_ts, round, (const int64_t *)nullptr);
-    return ok();
-}
-
-int hkv_wl_peer_ts_rows(hkv_table *t, uint8_t *rows, const int64_t *inv_at, uint8_t *vals, const uint64_t *phys,
-                        int64_t n, uint32_t op_size, unsigned long long *peer_ts, uint32_t round, void *stream)
-{
-    TableView tv;
-    if (table_view(t, &tv) || n < 0 || op_size % 8 || !inv_at) return -1;
-    if (n == 0) return 0;
-    hipLaunchKernelGGL(k_peer_ts_at, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, tv, rows, vals, phys, n,
-                       op_size, peer_ts, round, inv_at);
     return ok();
 }
 

@@ -87,9 +87,6 @@ BATCH_SMALL = 2    # the single-workgroup kernel (launches of at most 4096 eleme
 BATCH_PACKED = 4   # INV / VAL batches back to back, d_counts = n_batches + 1 offsets
 BATCH_UNIQUE = 8   # no key twice in the launch (INV batches: one pass)
 BATCH_ROWS = 16    # with BATCH_UNIQUE: rows of one layout, element j of every row on one key
-BATCH_PREPASS = 32     # a local launch's prepass only (its own stream; see include/hermeskv.h)
-BATCH_PREPASSED = 64   # the rest of that launch
-BATCH_PREPASS_CANCEL = 128   # or: that launch will not run (its prepass's tags undone)
 
 
 class HermesKV:
@@ -174,9 +171,8 @@ class HermesKV:
               stream: torch.cuda.Stream | None = None, offsets: torch.Tensor | None = None,
               state_out: torch.Tensor | None = None, opcode_in: torch.Tensor | None = None,
               patch: torch.Tensor | None = None, rw_state: torch.Tensor | None = None,
-              unique: bool = False, put_keys: torch.Tensor | None = None,
-              rows: tuple[int, int, int] | None = None, stage: int = 0,
-              ack_out: torch.Tensor | None = None, ack_out_size: int = 16, phys: torch.Tensor | None = None,
+              unique: bool = False, rows: tuple[int, int, int] | None = None,
+              ack_out: torch.Tensor | None = None, ack_out_size: int = 16,
               rw_opcodes: torch.Tensor | None = None) -> None:
         """Apply n_batches batches of one type, concatenated in `elems` (uint8, on the GPU),
         in concatenation order, asynchronously on `stream` (default: torch's current).
@@ -184,16 +180,12 @@ class HermesKV:
         [offsets[b], offsets[b+1]); `stride` is then the total (HKV_BATCH_PACKED). patch (local
         batches): 16 B per element of pending header writes (hkv_batch_desc.d_patch); rw_state (ACK
         batches): the read_write_ops' state-byte mirror, kept up to date by the completions. unique
-        (INV batches): no key appears twice in the launch (HKV_BATCH_UNIQUE, one pass). put_keys (local
-        batches with state_out): the PUT-key mirror (hkv_batch_desc.d_put_keys); state_out must then hold
-        every element's state byte on entry too. rows (unique INV / ACK launches): (n_rows, row_stride,
-        skip_row) -- n_rows launches of this layout, row r at element r * row_stride of elems, applied in
-        row order in one pass (HKV_BATCH_ROWS; skip_row -1: none). stage (local batches): 1 runs only the
-        launch's prepass (HKV_BATCH_PREPASS), 2 the rest of it (HKV_BATCH_PREPASSED), 3 cancels it
-        (HKV_BATCH_PREPASS_CANCEL), 0 runs all of it. ack_out (unique INV launches): every element's ACK
-        as the worker's ACK callbacks make it, ack_out_size bytes each (hkv_batch_desc.d_ack_out). phys
-        (unique INV and VAL launches): each element's located log offset (hkv_wl_peer_locate; ~0 none), the
-        entry line read without the bucket first (hkv_batch_desc.d_phys). rw_opcodes (ACK batches): the
+        (INV batches): no key appears twice in the launch (HKV_BATCH_UNIQUE, one pass). rows (unique INV /
+        ACK launches): (n_rows, row_stride, skip_row) -- n_rows launches of this layout, row r at element
+        r * row_stride of elems, applied in row order in one pass (HKV_BATCH_ROWS; skip_row -1: none).
+        ack_out (unique INV launches): every element's ACK as the worker's ACK callbacks make it,
+        ack_out_size bytes each (hkv_batch_desc.d_ack_out); ACK rows launches: the VAL callbacks' output
+        in the ACKs' positions. rw_opcodes (ACK batches): the
         read_write_ops' opcode mirror, one byte per slot (hkv_batch_desc.d_opcode_in): completions read the
         opcode there instead of the op."""
         assert elems.is_cuda and elems.dtype == torch.uint8
@@ -209,8 +201,6 @@ class HermesKV:
         d.stride = int(stride)
         d.elem_size = int(elem_size)
         d.flags = self.default_flags | (BATCH_UNIQUE if unique else 0)
-        if stage:
-            d.flags |= {1: BATCH_PREPASS, 2: BATCH_PREPASSED, 3: BATCH_PREPASS_CANCEL}[stage]
         if rows is not None:
             d.flags |= BATCH_ROWS
             d.n_rows, d.row_stride, d.skip_row = int(rows[0]), int(rows[1]), int(rows[2])
@@ -231,18 +221,11 @@ class HermesKV:
         if rw_state is not None:
             assert rw_state.is_cuda and rw_state.dtype == torch.uint8
             d.d_rw_state = rw_state.data_ptr()
-        if phys is not None:
-            assert phys.is_cuda and phys.dtype == torch.int64 and phys.numel() >= total
-            d.d_phys = phys.data_ptr()
         if ack_out is not None:   # INV launches: the ACK callbacks; ACK rows launches: the VAL callbacks, per row
             span = total if rows is None else (rows[0] - 1) * rows[1] + total
             assert unique and ack_out.is_cuda and ack_out.dtype == torch.uint8 and ack_out.numel() >= span * ack_out_size
             d.d_ack_out = ack_out.data_ptr()
             d.ack_out_size = int(ack_out_size)
-        if put_keys is not None:
-            assert state_out is not None and put_keys.is_cuda and put_keys.dtype == torch.int64
-            assert put_keys.numel() >= n_batches * stride
-            d.d_put_keys = put_keys.data_ptr()
         if offsets is not None:
             assert counts is None and offsets.is_cuda and offsets.dtype == torch.int32
             assert offsets.numel() >= n_batches + 1

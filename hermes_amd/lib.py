@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 HERE = os.path.dirname(os.path.abspath(__file__))
 # HKV_LIB: another build of the same library (A/B timing of two revisions in one GPU session)
 LIB_PATH = os.environ.get("HKV_LIB") or os.path.join(HERE, "libhermeskv.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")

@@ -92,16 +92,13 @@ class ReplicaRound:
         # refills planned from the state mirror and applied by the next local launch (workload.Round)
         self.fused = fused_refill and self.op <= 64
         self.patch = torch.zeros(W * LOCAL * 16, **u8) if self.fused else None
-        self.put_keys = (torch.zeros(W * LOCAL, dtype=torch.int64, device=dev)
-                         if self.fused and os.environ.get("HKV_PUT_KEYS", "0") == "1" else None)   # d_put_keys
         # outgoing INVs: [W][C] rows, then packed (worker w at inv_off[w]; inv_off[W] = total)
-        self.inv_slab = torch.zeros(W * C * self.op, **u8)
         self.inv_count = torch.zeros(W, **i32)           # INVs each worker sends this round
         self.inv_sendable = torch.zeros(W, **i32)        # ... and could send (the rest are held)
         self.inv_off = torch.zeros(W + 1, **i32)
         # the INVs go straight into the packed slab, at most `cap` per rank and round (local(cap)), so the
-        # group can size its collectives without a host read (HKV_GROUP_PACKED_MARSHAL=0: rows, then packed)
-        self.packed_marshal = os.environ.get("HKV_GROUP_PACKED_MARSHAL", "1") != "0"
+        # group can size its collectives without a host read
+        self.packed_marshal = True
         self.inv_pack = torch.zeros(W * C * self.op, **u8)
         self.inv_totals = torch.zeros(N, **i32)          # all ranks' INV totals (this round's width: max)
         self.inv_maxc = torch.zeros(1, **i32)            # this rank's largest per-worker INV count
@@ -133,15 +130,14 @@ class ReplicaRound:
         # ACK rows applied as they arrive, one unique-key launch per peer (a peer answers each of this
         # replica's INVs once, and a key has one local write in flight), with no regroup pass; once any
         # replica has failed, its rows hold empty slots and the regrouped batch takes over for good
-        self.unique_acks = os.environ.get("HKV_GROUP_UNIQUE_ACKS", "1") != "0"
-        # ... all peers' rows in one launch (HKV_BATCH_ROWS, this rank's own row skipped; HKV_ACK_ROWS=0: one
-        # launch per peer)
-        self.ack_rows = os.environ.get("HKV_ACK_ROWS", "1") != "0" and self.sizes.entry == 64 and self.ack_size <= 64
+        self.unique_acks = True
+        # ... all peers' rows in one launch (HKV_BATCH_ROWS, this rank's own row skipped; 64-B entries and
+        # 16-B ACKs, otherwise one launch per peer)
+        self.ack_rows = self.sizes.entry == 64 and self.ack_size <= 64
         self.own_total = None          # this round's packed INV total, when read back (round_shape)
         # this replica's ACKs to a peer's INVs written by that peer's INV launch itself (hkv_batch_desc.d_ack_out,
-        # as at N = 1) instead of a marshal pass over the applied row (HKV_FUSED_ACKS=0: the pass)
-        self.fused_acks = (((self.sizes.entry == 64 and self.op <= 64) or (self.sizes.entry == 320 and self.op <= 320))
-                           and os.environ.get("HKV_FUSED_ACKS", "1") != "0")
+        # as at N = 1) instead of a marshal pass over the applied row
+        self.fused_acks = (self.sizes.entry == 64 and self.op <= 64) or (self.sizes.entry == 320 and self.op <= 320)
         self.refill(first=True)
 
     # -- Hades: one view-update period per round when enabled
@@ -175,14 +171,14 @@ class ReplicaRound:
             check(_L.hkv_wl_refill_plan(_ptr(self.states), self.W, LOCAL, self.sizes.st_value, self.sizes.shift,
                                         _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
                                         self.rank, self.rflags, _ptr(self.counters), _ptr(self.opcodes),
-                                        _ptr(self.patch), _ptr(self.put_keys), _s()), "refill_plan")
+                                        _ptr(self.patch), _s()), "refill_plan")
             return
         check(_L.hkv_wl_refill(_ptr(self.ops), self.W, LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
                                _ptr(self.trace_key), _ptr(self.trace_op), None, self.trace_len, _ptr(self.cursor),
                                self.rank, int(first), self.rflags, _ptr(self.counters), _ptr(self.opcodes), None,
                                _s()), "refill")
         if first:
-            init_mirrors(self.ops, self.op, self.states, self.put_keys)
+            init_mirrors(self.ops, self.op, self.states)
 
     def local(self, cap: int | None = None):
         """Local batch, then this round's INVs, packed (inv_pack; worker w at inv_off[w]); at most `cap` of
@@ -193,19 +189,11 @@ class ReplicaRound:
             self.inv_maxc.zero_()
             return
         self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, LOCAL, self.op, self.mb, state_out=self.states,
-                       opcode_in=self.opcodes, patch=self.patch, put_keys=self.put_keys)
-        if self.packed_marshal:
-            check(_L.hkv_wl_marshal_invs_packed(_ptr(self.ops), self.W, LOCAL, self.op, _ptr(self.states), self.C,
-                                                self.W * self.C if cap is None else int(cap), _ptr(self.inv_pack),
-                                                _ptr(self.inv_off), _ptr(self.inv_sendable), _ptr(self.inv_count),
-                                                self.rank, _ptr(self.held), _s()), "marshal_invs_packed")
-        else:
-            assert cap is None, "a capped round needs the packed marshal"
-            check(_L.hkv_wl_marshal_invs_cap(_ptr(self.ops), self.W, LOCAL, self.op, _ptr(self.inv_slab), self.C,
-                                             _ptr(self.inv_count), self.rank, _ptr(self.held), _ptr(self.states), _s()),
-                  "marshal_invs")
-            check(_L.hkv_wl_pack_rows(_ptr(self.inv_slab), _ptr(self.inv_count), self.W, self.C, self.op,
-                                      _ptr(self.inv_pack), _ptr(self.inv_off), _s()), "pack invs")
+                       opcode_in=self.opcodes, patch=self.patch)
+        check(_L.hkv_wl_marshal_invs_packed(_ptr(self.ops), self.W, LOCAL, self.op, _ptr(self.states), self.C,
+                                            self.W * self.C if cap is None else int(cap), _ptr(self.inv_pack),
+                                            _ptr(self.inv_off), _ptr(self.inv_sendable), _ptr(self.inv_count),
+                                            self.rank, _ptr(self.held), _s()), "marshal_invs_packed")
         torch.amax(self.inv_count, dim=0, keepdim=True, out=self.inv_maxc)
         if self.count_elems:
             self.inv_total += self.inv_off[self.W]
@@ -387,8 +375,8 @@ class ReplicaRound:
                                   _ptr(self.val_pack), _ptr(self.val_off), _s()), "pack vals")
 
     def _rwo(self):
-        """the opcode mirror the ACK launches complete from (HKV_ACK_OPCODES=0: they read the ops)"""
-        return self.opcodes if os.environ.get("HKV_ACK_OPCODES", "1") != "0" else None
+        """the opcode mirror the ACK launches complete from"""
+        return self.opcodes
 
     def vals(self, width: int):
         """Apply the gathered VALs of the peers ([N][width], row p: val_totals[p] VALs)."""

@@ -11,7 +11,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 
 import numpy as np
 import torch
@@ -38,10 +37,7 @@ _L.hkv_wl_fold_counters.argtypes = [_P, _P]
 _L.hkv_wl_refill_st.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                 _P, _P, ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _P]
 _L.hkv_wl_refill_plan.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, _P, _P,
-                                  ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _P, _P]
-_L.hkv_wl_refill_plan_located.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, _P, _P,
-                                          ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _P, _P, _P,
-                                          _P]
+                                  ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _P]
 _L.hkv_wl_marshal_invs.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_marshal_invs_cap.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, ctypes.c_int32, _P,
                                        ctypes.c_uint32, _P, _P, _P]
@@ -75,7 +71,6 @@ _L.hkv_wl_ack_offsets.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ct
 _L.hkv_wl_pack_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_peer_locate.argtypes = [_P, _P, ctypes.c_int64, ctypes.c_uint32, _P, _P]
 _L.hkv_wl_peer_ts_at.argtypes = [_P, _P, _P, _P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
-_L.hkv_wl_peer_ts_rows.argtypes = [_P, _P, _P, _P, _P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_peer_ts_words.restype = ctypes.c_uint64
 _L.hkv_wl_peer_ts_words.argtypes = [_P]
 
@@ -128,14 +123,10 @@ def _ptr(t: torch.Tensor | None):
     return _P(t.data_ptr()) if t is not None else None
 
 
-def init_mirrors(ops: torch.Tensor, op_size: int, states: torch.Tensor, put_keys: torch.Tensor | None):
-    """The state mirror and the PUT-key mirror (hkv_batch_desc.d_put_keys) of freshly written ops;
-    from then on the round's kernels keep them (local launch, marshals, ACK launches, refill plan)."""
-    v = ops.view(-1, op_size)
-    states.copy_(v[:, 9])
-    if put_keys is not None:
-        key = v[:, :8].contiguous().view(torch.int64).view(-1)
-        put_keys.copy_(torch.where(v[:, 8] == int(L.Op.PUT), key, torch.full_like(key, -1)))
+def init_mirrors(ops: torch.Tensor, op_size: int, states: torch.Tensor):
+    """The state mirror of freshly written ops; from then on the round's kernels keep it (local launch,
+    marshals, ACK launches, refill plan)."""
+    states.copy_(ops.view(-1, op_size)[:, 9])
 
 
 class CommitAudit:
@@ -262,15 +253,12 @@ class Round:
         # the next local launch as patches, so the op slab is read and written once per round. Not with
         # hot-request coalescing (a sequential walk over the ops), VAL credits (their marshal keeps no
         # mirror) or 312-B ops (refilled in place). Default: wherever it applies.
-        # HKV_BIG_FUSED=1: 312-B ops planned too, their patches written by the local launch's in-place
-        # resolve (k_resolve0_direct) beside the value copies instead of by hkv_wl_refill_st
-        big_fused = os.environ.get("HKV_BIG_FUSED", "0") == "1"
-        can_fuse = not coalesce_hot and val_credits is None and (self.op <= 64 or big_fused)
+        can_fuse = not coalesce_hot and val_credits is None and self.op <= 64
         self.fused = can_fuse if fused_refill is None else (fused_refill and can_fuse)
         # 312-B ops are refilled in place, but from the same state mirror (hkv_wl_refill_st), so a slot
-        # the refill keeps is not read (fused_refill=False or HKV_REFILL_ST=0: from the ops)
-        self.st_refill = (not self.fused and not coalesce_hot and val_credits is None and self.op > 64 and fused_refill is not False
-                          and os.environ.get("HKV_REFILL_ST", "1") != "0")
+        # the refill keeps is not read (fused_refill=False: from the ops)
+        self.st_refill = (not self.fused and not coalesce_hot and val_credits is None and self.op > 64
+                          and fused_refill is not False)
         self.machine_id = kvs.machine_id
         dev = torch.device("cuda", kvs.device)
         W, S = n_workers, self.LOCAL
@@ -279,20 +267,6 @@ class Round:
         self.states = torch.zeros(W * S, **u8)   # the local batch's mirror of every op's state byte
         self.opcodes = torch.zeros(W * S, **u8)  # the refill's mirror of every op's opcode byte
         self.patch = torch.zeros(W * S * 16, **u8) if self.fused else None   # planned refills (d_patch)
-        # the PUT-key mirror (d_put_keys) the plan keeps beside the state mirror, from which the local launch
-        # could find its PUTs without reading ops (HKV_PUT_KEYS=1). Measured, not adopted (round 4): the
-        # prepass stays at 83 us (its atomics and seqlock tags, not its loads, bound it now) and the mirror
-        # checks cost the fused pass 10-20 us
-        # located entries for the local launch (HKV_LOCAL_HINTS=1): every trace key's log offset, located once
-        # (at the first plan, the table populated), and each slot's word, kept by the plan (d_phys). Same box
-        # (gpurun_out/r04zi): local launch 381 -> 355 us, 4.26 -> 4.35 G ops/s; off by default, as
-        # HKV_PHYS_HINTS
-        self.ack_opcodes = os.environ.get("HKV_ACK_OPCODES", "1") != "0"   # ACK completions read the opcode mirror
-        self.local_hints = self.fused and os.environ.get("HKV_LOCAL_HINTS", "0") == "1"
-        self.trace_phys = None
-        self.slot_phys = torch.full((W * S,), -1, dtype=torch.int64, device=dev) if self.local_hints else None
-        self.put_keys = (torch.zeros(W * S, dtype=torch.int64, device=dev)
-                         if self.fused and os.environ.get("HKV_PUT_KEYS", "0") == "1" else None)
         self.C = slots_per_worker(write_permille, rmw_permille)   # INV send credits per worker
         self.inv_out = torch.zeros(W * self.C * self.op, **u8)
         self.inv_count = torch.zeros(W, dtype=torch.int32, device=dev)
@@ -318,9 +292,7 @@ class Round:
             self.val_overflow = torch.zeros(1, dtype=torch.int64, device=dev)
             self.val_totals = torch.zeros(2, dtype=torch.int64, device=dev)  # VALs sent, gated worker-rounds
         self.maxc_h = torch.zeros(4, dtype=torch.int32, pin_memory=True) if self.fit else None
-        # the host spins on the flag word the kernel writes after the total (ack_spin), or waits on
-        # an event after the kernel
-        self.ack_spin = os.environ.get("HKV_ACK_EVENT", "0") != "1"
+        # the host spins on the flag word the kernel writes after the total (no event, no gap)
         self._ack_seq = 0
         self._ack_flag = ctypes.c_int32.from_address(self.maxc_h.data_ptr() + 8) if self.fit else None
         self.ack_off = torch.zeros(W + 1, dtype=torch.int32, device=dev) if self.fit else None
@@ -328,25 +300,17 @@ class Round:
         # peer-major ACKs (fit path): each virtual peer's answers to the round's INVs as one block,
         # applied as a launch of its own with HKV_BATCH_UNIQUE (one ACK per key and peer: a key has at
         # most one local write in flight); ack_off then holds the INV offsets and inv_round the INV total
-        self.ack_pm = self.fit and os.environ.get("HKV_ACK_PM", "1") != "0"
+        self.ack_pm = self.fit
         # ... and all peers' blocks in one launch (HKV_BATCH_ROWS: each key looked up once, its ACKs applied
-        # in peer order; HKV_ACK_ROWS=0: one launch per peer, experiments)
-        self.ack_rows = (os.environ.get("HKV_ACK_ROWS", "1") != "0" and self.sizes.entry == 64
-                         and self.ack_size <= 64)
+        # in peer order; 64-B entries, 16-B ACKs; otherwise one launch per peer)
+        self.ack_rows = self.sizes.entry == 64 and self.ack_size <= 64
         # ... which also makes the VALs of the writes it completes (the VAL callbacks, hermes_worker.c:122-157,
         # into val_out in the ACKs' positions: hkv_batch_desc.d_ack_out on an ACK launch) instead of a
-        # collection pass over the ACK slab (HKV_FUSED_VALS=0: k_collect_vals, compacted per worker)
-        self.fused_vals = (self.ack_pm and self.ack_rows and self.ack_size == 16 and val_credits is None
-                           and os.environ.get("HKV_FUSED_VALS", "1") != "0")
+        # collection pass over the ACK slab (otherwise: k_collect_vals, compacted per worker)
+        self.fused_vals = self.ack_pm and self.ack_rows and self.ack_size == 16 and val_credits is None
         self._vals_made = False
         self.inv_round = 0
         self.ack_m = self.C
-        self.maxc_ev = torch.cuda.Event() if self.fit else None
-        # HKV_ACKOFF_SIDE=1: the one-workgroup ACK-offsets scan runs on a side stream beside the INV batch
-        self.ackoff_side = self.fit and self.ack_spin and os.environ.get("HKV_ACKOFF_SIDE", "0") == "1"
-        if self.ackoff_side:
-            self.side2 = torch.cuda.Stream(device=dev)
-            self.ao_start, self.ao_done = torch.cuda.Event(), torch.cuda.Event()
         self.acks = torch.zeros(W * self.ack_stride * self.ack_size, **u8)
         self.ack_count = torch.zeros(W, dtype=torch.int32, device=dev)
         self.val_out = torch.zeros(W * self.ack_stride * L.OP_META_SIZE, **u8)
@@ -381,26 +345,10 @@ class Round:
             self.peer_ts = torch.zeros(int(_L.hkv_wl_peer_ts_words(kvs.h)), dtype=torch.int64, device=dev)
         self.pack_remote = virtual_peers and self.R > 0 and pack_remote
         self.remote_packed = []        # per round index: (INVs, VALs, batch offsets, total, entry offsets)
-        # the peers' INVs of a round index also as rows (HKV_BATCH_ROWS), applied in one launch (64-B entries;
-        # HKV_INV_ROWS=1). Measured, not adopted (round 4): the rows launch takes what the two per-peer
-        # launches take (70.6 vs 2 x 36 us: each position loads both rows' 56-B elements, holes included)
-        # and the ACK marshal over the rows' holes costs 8 us more
-        self.inv_rows = (self.pack_remote and 1 < self.R <= 8 and kvs.sizes.entry == 64 and self.op <= 64
-                         and os.environ.get("HKV_INV_ROWS", "0") == "1")
-        self.remote_rows = []
-        self.rows_acks = None          # our ACKs to the rows (marshalled, not read back: the peers are virtual)
         # our ACKs to each peer's INVs written by that peer's INV launch itself (hkv_batch_desc.d_ack_out)
-        # instead of a marshal pass over the applied INVs (HKV_FUSED_ACKS=0: the pass, experiments)
-        # HKV_PHYS_HINTS=1: the peers' INVs and VALs launch with their entries located when drawn
-        # (hkv_batch_desc.d_phys). Same box, 3 reps each (gpurun_out/r04zh): INV 72 -> 59 us, VAL 50 -> 38 us,
-        # 4.24 -> 4.40 G ops/s. Off by default: it skips the bucket read the reference makes for every
-        # message (the location comes from a lookup made when the round's slabs were drawn), so the
-        # headline keeps the reference's per-element lookup ("Located entries")
-        self.phys_hints = os.environ.get("HKV_PHYS_HINTS", "0") == "1"
+        # instead of a marshal pass over the applied INVs
         self.fused_acks = (self.pack_remote and ((kvs.sizes.entry == 64 and self.op <= 64) or
-                                                 (kvs.sizes.entry == 320 and self.op <= 320))
-                           and os.environ.get("HKV_FUSED_ACKS", "1") != "0")
-        self.packed_prefix = os.environ.get("HKV_PACKED_PREFIX", "1") != "0"
+                                                 (kvs.sizes.entry == 320 and self.op <= 320)))
         self.drops = []                # peers dropped from the membership (membership_change)
         self.alive = self.R            # live peers: the first `alive` slots of the remote slabs
         self._counts = {}
@@ -408,29 +356,7 @@ class Round:
         if hades:
             self._hades_start()
         self._gen_remote()
-        # HKV_PEER_OVERLAP=1: the virtual peers take their timestamps on a side stream, beside the
-        # refill (which touches only the op slab): from the table as the previous round left it
-        # (tbl_ready, recorded before each refill) to the local batch, which waits for them.
-        # Measured slower (1.884 vs 1.907 G ops/s, 3 x 30 steps each), so in line by default.
-        self.overlap = os.environ.get("HKV_PEER_OVERLAP", "0") == "1" and self.pack_remote
         self.audit: CommitAudit | None = None   # audit_rounds(): per-outcome commit breakdown (untimed)
-        # the local launch in two stages (HKV_BATCH_PREPASS, HKV_PRE_SPLIT=1): the next round's prepass runs
-        # on a side stream right after this round's refill plan, beside this round's VAL batch and the next
-        # round's peer timestamps, which leave every key's PUT-mutability as it was. Measured, not adopted
-        # (round 4): 3.99-4.00 G against 4.04-4.07 G ops/s in line -- beside the VAL batch the prepass takes
-        # 120 us instead of 80 (both are random-access bound), and the local launch waits for it anyway
-        self.pre_split = (self.fused and virtual_peers and self.R > 0 and not kvs.rmw and self.op == 56
-                          and kvs.sizes.entry == 64 and val_credits is None
-                          and os.environ.get("HKV_PRE_SPLIT", "0") == "1")
-        self.pre_pending = False
-        if self.pre_split:
-            self.side_pre = torch.cuda.Stream(device=dev)
-            self.ev_plan, self.ev_pre = torch.cuda.Event(), torch.cuda.Event()
-
-        if self.overlap:
-            self.side = torch.cuda.Stream(device=dev)
-            self.tbl_ready, self.pts_done = torch.cuda.Event(), torch.cuda.Event()
-            self.tbl_ready.record()
         self.refill(first=True)
 
     def _gen_remote(self):
@@ -479,65 +405,15 @@ class Round:
                 phys = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
                 check(_L.hkv_wl_peer_locate(self.kvs.h, _ptr(pi), total, self.op, _ptr(phys), _s()), "peer_locate")
                 self.remote_packed.append((pi, pv, off32, total, phys, per_peer))
-                if self.inv_rows:
-                    self.remote_rows.append(self._inv_rows(pi, per_peer, total))
         del scratch
-
-    def _inv_rows(self, pi: torch.Tensor, per_peer, total: int):
-        """The peers' INVs of one round index as rows (HKV_BATCH_ROWS): row r = peer r, position j one key,
-        holes (opcode 0) where a peer sent nothing for it. Positions: peer 0's INVs in order, then each
-        later peer's keys no earlier peer wrote. Returns (rows slab, n positions, inv_at: the element of
-        the slab each packed INV went to, batch offsets [0, n])."""
-        dev, op, R = pi.device, self.op, self.R
-        keys = pi.view(-1, op)[:total, :8].contiguous().view(torch.int64).view(-1)
-        at = torch.empty(total, dtype=torch.int64, device=dev)
-        pos_keys = torch.empty(0, dtype=torch.int64, device=dev)
-        P = 0
-        for r, (base, n, _) in enumerate(per_peer):
-            kr = keys[base:base + n]
-            p = torch.full((n,), -1, dtype=torch.int64, device=dev)
-            if P and n:
-                sk, si = torch.sort(pos_keys)
-                idx = torch.searchsorted(sk, kr).clamp(max=P - 1)
-                hit = sk[idx] == kr
-                p[hit] = si[idx][hit]
-            new = p < 0
-            nn = int(new.sum().item())
-            p[new] = P + torch.arange(nn, device=dev)
-            pos_keys = torch.cat([pos_keys, kr[new]])
-            P += nn
-            at[base:base + n] = p
-        row_of = torch.repeat_interleave(torch.arange(R, device=dev), torch.tensor([n for _, n, _ in per_peer],
-                                                                                     device=dev))
-        inv_at = row_of * P + at
-        rows = torch.zeros(max(R * P, 1) * op, dtype=torch.uint8, device=dev)
-        if total:
-            rows.view(-1, op)[inv_at] = pi.view(-1, op)[:total]
-        if self.rows_acks is None or self.rows_acks.numel() < R * P * self.ack_size:
-            self.rows_acks = torch.zeros(max(R * P, 1) * self.ack_size, dtype=torch.uint8, device=dev)
-        off = torch.tensor([0, P], dtype=torch.int32, device=dev)
-        return rows, P, inv_at, off
 
     # -- pieces of one round
     def refill(self, first: bool = False):
-        if self.fused and not first and self.local_hints:   # the plan keeps each slot's located entry too
-            if self.trace_phys is None:
-                n = self.W * self.trace_len
-                self.trace_phys = torch.empty(n, dtype=torch.int64, device=self.ops.device)
-                check(_L.hkv_wl_peer_locate(self.kvs.h, _ptr(self.trace_key), n, 8, _ptr(self.trace_phys), _s()),
-                      "trace_locate")
-            check(_L.hkv_wl_refill_plan_located(_ptr(self.states), self.W, self.LOCAL, self.sizes.st_value,
-                                                self.sizes.shift, _ptr(self.trace_key), _ptr(self.trace_op),
-                                                self.trace_len, _ptr(self.cursor), self.machine_id, self.rflags,
-                                                _ptr(self.counters), _ptr(self.opcodes), _ptr(self.patch),
-                                                _ptr(self.put_keys), _ptr(self.trace_phys), _ptr(self.slot_phys),
-                                                _s()), "refill_plan_located")
-            return
         if self.fused and not first:   # a plan the next local launch applies (the ops stay as they are)
             check(_L.hkv_wl_refill_plan(_ptr(self.states), self.W, self.LOCAL, self.sizes.st_value, self.sizes.shift,
                                         _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
                                         self.machine_id, self.rflags, _ptr(self.counters), _ptr(self.opcodes),
-                                        _ptr(self.patch), _ptr(self.put_keys), _s()), "refill_plan")
+                                        _ptr(self.patch), _s()), "refill_plan")
             return
         if self.st_refill and not first:
             check(_L.hkv_wl_refill_st(_ptr(self.ops), self.W, self.LOCAL, self.op, self.sizes.st_value, self.sizes.shift,
@@ -551,47 +427,14 @@ class Round:
                                _ptr(self.opcodes), _ptr(self.hot), _s()),
               "refill")
         if first:
-            init_mirrors(self.ops, self.op, self.states, getattr(self, "put_keys", None))
-
-    def _local(self, stage: int, stream=None):
-        self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb, state_out=self.states,
-                       opcode_in=self.opcodes, patch=self.patch, put_keys=self.put_keys, stage=stage, stream=stream,
-                       phys=self.slot_phys)
-
-    def prepass(self, overlap: bool, events: dict | None = None):
-        """Stage 1 of the next local launch: on the side stream after what the current stream holds
-        (overlap), or in line. events: its (start, end) timing pair goes to events["local_pre"]."""
-        if overlap:
-            self.ev_plan.record()
-            self.side_pre.wait_event(self.ev_plan)
-        s = self.side_pre if overlap else torch.cuda.current_stream()
-        if events is not None:
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record(s)
-        self._local(1, s)
-        if events is not None:
-            ev[1].record(s)
-            events.setdefault("local_pre", []).append(ev)
-        self.ev_pre.record(s)
-        self.pre_pending = True
-
-    def close(self):
-        """A prepass issued for a round that will not run is undone (its tags cleared), so the table is
-        the reference's image again; call before the table serves anything else."""
-        if self.pre_split and self.pre_pending:
-            torch.cuda.current_stream().wait_event(self.ev_pre)
-            self._local(3)
-            self.pre_pending = False
+            init_mirrors(self.ops, self.op, self.states)
 
     def local_batch(self):
-        if not self.pre_split:
-            self._local(0)
-            return
-        if not self.pre_pending:
-            self.prepass(overlap=False)
-        torch.cuda.current_stream().wait_event(self.ev_pre)
-        self._local(2)
-        self.pre_pending = False
+        self.kvs.batch(L.BatchType.local_ops, self.ops, self.W, self.LOCAL, self.op, self.mb, state_out=self.states,
+                       opcode_in=self.opcodes, patch=self.patch)
+
+    def close(self):
+        """Nothing is left pending between rounds (kept for callers that close a round)."""
 
     def marshal_invs(self):
         if self.V is not None:
@@ -633,11 +476,6 @@ class Round:
         pi, pv, _, total, phys, _ = self.remote_packed[k]
         if n_peers is not None:
             total = self._packed_total(k, n_peers)
-        if self.inv_rows:
-            rows, _, inv_at, _ = self.remote_rows[k]
-            check(_L.hkv_wl_peer_ts_rows(self.kvs.h, _ptr(rows), _ptr(inv_at), _ptr(pv), _ptr(phys), total, self.op,
-                                         _ptr(self.peer_ts), self.clock, _s()), "peer_ts_rows")
-            return
         check(_L.hkv_wl_peer_ts_at(self.kvs.h, _ptr(pi), _ptr(pv), _ptr(phys), total, self.op, _ptr(self.peer_ts),
                                    self.clock, _s()), "peer_ts_at")
 
@@ -647,26 +485,17 @@ class Round:
                        unique=unique)
 
     def inv_batches_per_peer(self, k: int, n_peers: int | None = None):
-        """Every peer's INVs of round index k as a launch of its own (HKV_BATCH_UNIQUE), in peer order --
-        or all peers' as one rows launch (HKV_BATCH_ROWS): each key looked up once, its INVs applied in
-        peer order. n_peers: the first n_peers peers only (default all)"""
-        if self.inv_rows:
-            rows, P, _, off = self.remote_rows[k]
-            if P:
-                self.kvs.batch(L.BatchType.invs, rows, 1, P, self.op, self.mb, offsets=off, unique=True,
-                               rows=(self.R, P, -1))
-            return
-        pi, _, _, _, phys, per_peer = self.remote_packed[k]
+        """Every peer's INVs of round index k as a launch of its own (HKV_BATCH_UNIQUE), in peer order.
+        n_peers: the first n_peers peers only (default all)"""
+        pi, _, _, _, _, per_peer = self.remote_packed[k]
         for base, n, off in per_peer[:n_peers]:
             if n:
-                ph = phys[base:] if self.phys_hints else None
-                if self.fused_acks and not self.inv_rows:
+                if self.fused_acks:
                     self.kvs.batch(L.BatchType.invs, pi[base * self.op:], self.W, n, self.op, self.mb, offsets=off,
-                                   unique=True, ack_out=self.ack_out[base * self.ack_size:], ack_out_size=self.ack_size,
-                                   phys=ph)
+                                   unique=True, ack_out=self.ack_out[base * self.ack_size:], ack_out_size=self.ack_size)
                 else:
                     self.kvs.batch(L.BatchType.invs, pi[base * self.op:], self.W, n, self.op, self.mb, offsets=off,
-                                   unique=True, phys=ph)
+                                   unique=True)
 
     def marshal_acks(self, invs: torch.Tensor, n: int, out: torch.Tensor):
         check(_L.hkv_wl_marshal_acks(_ptr(invs), n, self.op, _ptr(out), self.ack_size, self.machine_id, _s()),
@@ -679,8 +508,8 @@ class Round:
 
     def _rwo(self):
         """the opcode mirror the ACK batch completes from (the refill keeps it; the local launch checks it
-        against every op; HKV_ACK_OPCODES=0: the completions read the ops)"""
-        return self.opcodes if self.ack_opcodes else None
+        against every op)"""
+        return self.opcodes
 
     def ack_batch(self, acks: torch.Tensor | None = None, n_batches: int | None = None, stride: int | None = None,
                   counts: torch.Tensor | None = None):
@@ -752,9 +581,9 @@ class Round:
             self.val_totals[0] += self.val_count.sum()
 
     def val_batch(self, vals: torch.Tensor, n_batches: int, stride: int, counts: torch.Tensor | None = None,
-                  offsets: torch.Tensor | None = None, phys: torch.Tensor | None = None):
+                  offsets: torch.Tensor | None = None):
         self.kvs.batch(L.BatchType.vals, vals, n_batches, stride, L.OP_META_SIZE, self.mb, counts=counts,
-                       offsets=offsets, phys=phys)
+                       offsets=offsets)
 
     # -- a whole round with virtual peers
     def step(self, events: dict | None = None, timed_batches=("local", "invs", "acks", "vals"),
@@ -774,31 +603,20 @@ class Round:
             events.setdefault(name, []).append((a, b))
 
         k = self.clock % max(len(self.remote_inv), 1)
-        early = False                              # refill and next prepass done before the VAL batch
         if drop is not None:
             assert self.virtual and self.alive and drop == self.peers[self.alive - 1], "drop the last live peer"
         sent = self.alive                          # peers whose INVs this round applies
         alive = self.alive - (drop is not None)    # peers that answer them (ACKs) and send VALs
         # the packed slabs (same elements, same order): the live peers are their first `alive` peers (a
         # failed peer is always the last live one), so after a failure the rounds apply a prefix of them
-        # (the rows layout holds every peer: only while all are live)
-        # (HKV_PACKED_PREFIX=0: the row layout once a peer has failed, as before round 5)
-        packed = self.pack_remote and ((sent == self.R and alive == self.R) or (self.packed_prefix and not self.inv_rows))
+        packed = self.pack_remote
         if self.R and sent:
-            if packed and self.overlap:
-                self.side.wait_event(self.tbl_ready)
-                with torch.cuda.stream(self.side):
-                    self.peer_timestamps_packed(k, sent)
-                self.pts_done.record(self.side)
-                torch.cuda.current_stream().wait_event(self.pts_done)
-            elif packed:
+            if packed:
                 self.peer_timestamps_packed(k, sent)
             else:
                 self.peer_timestamps(k, sent)
         if self.audit is not None:
             self.audit.pre_local()
-        if self.pre_split and self.pre_pending:   # the local launch's timing starts after its prepass
-            torch.cuda.current_stream().wait_event(self.ev_pre)
         timed("local", self.local_batch)
         if self.audit is not None:
             self.audit.post_local()
@@ -806,48 +624,29 @@ class Round:
         if self.count_elems:
             self.inv_total += self.inv_count.sum()
         if self.fit and alive:
-            self._ack_seq = self._ack_seq % 0x7FFFFFFF + 1 if self.ack_spin else 0
-            if self.ackoff_side:   # one workgroup: beside the INV batch, which does not need it
-                self.ao_start.record()
-                self.side2.wait_event(self.ao_start)
-                with torch.cuda.stream(self.side2):
-                    check(_L.hkv_wl_ack_offsets(_ptr(self.inv_count), self.W, 1 if self.ack_pm else alive,
-                                                _ptr(self.ack_off), _ptr(self.maxc_h), self._ack_seq, _s()),
-                          "ack_offsets")
-                self.ao_done.record(self.side2)
-            else:
-                check(_L.hkv_wl_ack_offsets(_ptr(self.inv_count), self.W, 1 if self.ack_pm else alive,
-                                            _ptr(self.ack_off), _ptr(self.maxc_h), self._ack_seq, _s()), "ack_offsets")
-            if not self.ack_spin:
-                self.maxc_ev.record()
+            self._ack_seq = self._ack_seq % 0x7FFFFFFF + 1
+            check(_L.hkv_wl_ack_offsets(_ptr(self.inv_count), self.W, 1 if self.ack_pm else alive,
+                                        _ptr(self.ack_off), _ptr(self.maxc_h), self._ack_seq, _s()), "ack_offsets")
         if self.R:
             ri, rv = self.remote_inv[k], self.remote_val[k]
             ic = self._slot_counts(k, sent)
             if packed:
                 pi, pv, off, total, _, _ = self.remote_packed[k]
                 timed("invs", lambda: self.inv_batches_per_peer(k, sent))
-                if self.inv_rows:   # our ACKs to the rows (holes answer nothing)
-                    rows, P, _, _ = self.remote_rows[k]
-                    self.marshal_acks(rows, self.R * P, self.rows_acks)
-                elif not self.fused_acks:   # (else the INV launches wrote them)
+                if not self.fused_acks:   # (else the INV launches wrote them)
                     self.marshal_acks(pi, self._packed_total(k, sent), self.ack_out)
             else:
                 timed("invs", lambda: self.inv_batch(ri, self.W, self.rstride, counts=ic))
                 self.marshal_acks(ri, self.W * self.rstride, self.ack_out)
             m = self.C
             if self.fit and alive:   # the GPU is still on the INV batch: this wait leaves no gap
-                if self.ack_spin:
-                    spins = 0
-                    while self._ack_flag.value != self._ack_seq:
-                        spins += 1
-                        if spins % 65536 == 0:   # a lost flag fails loudly instead of spinning on
-                            torch.cuda.synchronize()
-                            if self._ack_flag.value != self._ack_seq:
-                                raise RuntimeError("ACK layout flag never arrived")
-                else:
-                    self.maxc_ev.synchronize()
-                if self.ackoff_side:
-                    torch.cuda.current_stream().wait_event(self.ao_done)
+                spins = 0
+                while self._ack_flag.value != self._ack_seq:
+                    spins += 1
+                    if spins % 65536 == 0:   # a lost flag fails loudly instead of spinning on
+                        torch.cuda.synchronize()
+                        if self._ack_flag.value != self._ack_seq:
+                            raise RuntimeError("ACK layout flag never arrived")
                 self.ack_total = int(self.maxc_h[0])
                 if self.ack_pm:   # the offsets counted INVs: one block of them per answering peer
                     self.inv_round = self.ack_total
@@ -869,17 +668,8 @@ class Round:
                 self.collect_vals()
             # a dropped peer sent its INVs but fails before its VALs
             vc = self._slot_counts(k, alive)
-            # the round's ops are final: refill plan now, and the next round's prepass beside the VALs
-            early = self.pre_split and drop is None and self.hades is None and not self.overlap
-            if early:
-                if self.audit is not None:
-                    self.audit.end()
-                self.refill()
-                self.prepass(overlap=True, events=events if events is not None and "local" in timed_batches else None)
             if packed:
-                ph = self.remote_packed[k][4] if self.phys_hints else None
-                timed("vals", lambda: self.val_batch(pv, alive * self.W, self._packed_total(k, alive), offsets=off,
-                                                     phys=ph))
+                timed("vals", lambda: self.val_batch(pv, alive * self.W, self._packed_total(k, alive), offsets=off))
             else:
                 timed("vals", lambda: self.val_batch(rv, self.W, self.rstride, counts=vc))
             if self.count_elems:
@@ -892,12 +682,9 @@ class Round:
             self._hades_period()
         elif drop is not None:
             self.membership_change(drop)
-        if self.overlap:
-            self.tbl_ready.record()
-        if not early:
-            if self.audit is not None:
-                self.audit.end()
-            self.refill()
+        if self.audit is not None:
+            self.audit.end()
+        self.refill()
         self.clock += 1
 
     def _slot_counts(self, k: int, n_peers: int):

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HKV_ABI_VERSION 7
+#define HKV_ABI_VERSION 8
 
 /* ------------------------------------------------------------------ reference types
  * Declared here only when the reference's own spacetime.h has not been included; the
@@ -152,14 +152,8 @@ typedef struct hkv_batch_desc {
     uint8_t *d_rw_state;        /* device, ACK batches: a mirror of the read_write_ops' state bytes
                                    (rw_stride_bytes / op size per batch); every completion a launch writes
                                    into read_write_ops is also written here. NULL = none (ABI 5) */
-    const uint64_t *d_put_keys; /* device, local batches with d_state_out: the caller's PUT-key mirror, one
-                                   8-byte word per element (n_batches * stride): the key (op bytes 0..7) of
-                                   a PUT, HKV_NO_PUT for any other opcode, describing the (patched) ops.
-                                   d_state_out must then also hold every element's state byte (op byte 9)
-                                   on entry: with both, the launch finds its PUTs and applies the skip rule
-                                   from two dense arrays instead of the ops (hkv_wl_refill_plan keeps both).
-                                   An element the mirrors misdescribe raises error flag bit 3.
-                                   NULL = none (ABI 6) */
+    const uint64_t *d_put_keys; /* reserved, must be NULL (ABI 8; ABI 6-7: a PUT-key mirror for the local
+                                   launch's prepass, measured slower and removed) */
     int32_t  n_rows;            /* HKV_BATCH_ROWS: rows of elements, applied row after row (ABI 6) */
     int32_t  skip_row;          /* HKV_BATCH_ROWS: a row that is not applied (-1: none) */
     int64_t  row_stride;        /* HKV_BATCH_ROWS: elements from one row to the next in d_elems */
@@ -177,14 +171,9 @@ typedef struct hkv_batch_desc {
                                    opcode ST_EMPTY, and every non-empty element leaves with opcode ST_EMPTY
                                    (val_skip_or_get_sender_id, val_modify_elem_after_send); ack_out_size 16 */
     uint32_t ack_out_size;
-    const uint64_t *d_phys;     /* device, local, INV (HKV_BATCH_UNIQUE) and VAL launches: per element, the log offset
-                                   the lookup of its key gives (hkv_wl_peer_locate), or ~0 for none; valid only
-                                   while the index is unchanged since (no populate in between), which the caller
-                                   guarantees. The launch then reads the entry line straight away instead of the
-                                   bucket first; an element whose entry no longer holds its key, or without an
-                                   offset, is looked up as usual. NULL = none (ABI 7) */
+    const uint64_t *d_phys;     /* reserved, must be NULL (ABI 8; ABI 7: located entries that skipped the
+                                   bucket read the reference makes, never the default, removed) */
 } hkv_batch_desc;
-#define HKV_NO_PUT 0xFFFFFFFFFFFFFFFFull
 
 /* d_patch layout (16 bytes per element): key 0..7, opcode 8, val_len 9, flags (RMW_flag | no_coales
  * << 1) 10..11, value fill byte 12 (0: the value is kept), ts reset 13 (1: ts bytes 11..15 := 0),
@@ -219,17 +208,9 @@ typedef struct hkv_batch_desc {
  * An element whose key differs from its position's raises error flag bit 4. d_node_suspected must be
  * NULL. */
 #define HKV_BATCH_ROWS 16u   /* packed rows: elements past d_counts[n_batches] (<= stride) are in no batch */
-/* A local launch in two calls, so its first stage can overlap other work: HKV_BATCH_PREPASS runs only
- * the launch's prepass (on the direct path: every PUT that mutates its key offers itself), on its own
- * stream; a later call with the same descriptor and HKV_BATCH_PREPASSED runs the rest. In between, the
- * only launches on the table may be VAL batches (they leave every key's PUT-mutability as it was:
- * VALID or INVALID with an empty op buffer index). Results are those of one launch. The second call
- * fails if the table saw no matching first call. */
-#define HKV_BATCH_PREPASS 32u
-#define HKV_BATCH_PREPASSED 64u
-/* instead of HKV_BATCH_PREPASSED: the launch will not run; undo what its prepass left in the table
- * (the seqlock bytes it used as tags), so the table is the reference's image again */
-#define HKV_BATCH_PREPASS_CANCEL 128u
+/* Bits 5..7 are reserved (ABI 8; ABI 6-7: a local launch in two calls, HKV_BATCH_PREPASS / PREPASSED /
+ * PREPASS_CANCEL, measured slower and removed): a launch that sets them fails. */
+#define HKV_BATCH_RESERVED_FLAGS 0xE0u
 #define HKV_MAX_ROWS 8
 int  hkv_abi_version(void);
 /* 1 when the library was built with work-skipping timing modes (-DHKV_DEBUG_MODES, HKV_DBG):
@@ -262,11 +243,9 @@ void *hkv_device_index(hkv_table *t);
  * bit 0: an element resolved in parallel (not a key's first mutating element) changed the meta;
  * bit 1: the ACK direct path completed a write from an unexpected state;
  * bit 2: a local launch's mutating element had not offered itself in its prepass;
- * bit 3: d_opcode_in missed a PUT, or d_put_keys / the entry states of d_state_out disagree with the ops;
+ * bit 3: d_opcode_in missed a PUT;
  * bit 4: an HKV_BATCH_UNIQUE launch held a key twice (checked with HKV_CHECK_UNIQUE=1), or an
- *        HKV_BATCH_ROWS position's rows disagree on the key;
- * bit 5: (HKV_PART_STREAMS > 1 only) a partitioned host launch waited over 1 s for its partition's
- *        previous launch and applied nothing; hermes_batch_ops_to_KVS then aborts the process */
+ *        HKV_BATCH_ROWS position's rows disagree on the key */
 int  hkv_take_error_flags(hkv_table *t, uint32_t *out);
 void *hkv_device_log(hkv_table *t);
 

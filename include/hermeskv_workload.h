@@ -84,24 +84,12 @@ int hkv_wl_refill(uint8_t *d_ops, int32_t n_workers, int32_t stride, uint32_t op
  * membership marshals, the ACK launch's d_rw_state) -- instead of the ops. Each refilled op gets a
  * valid patch in d_patch (HKV_PATCH_BYTES per op, include/hermeskv.h), every other op an invalid one;
  * d_opcode (the opcode mirror) takes the refilled ops' opcodes. The ops themselves are untouched:
- * the next local launch, given d_patch, applies the patches as it reads them. With d_put_keys (may be
- * NULL), a refilled op's PUT-key word (hkv_batch_desc.d_put_keys: its key for a PUT, HKV_NO_PUT
- * otherwise) is written there and its d_states byte set to ST_NEW, so both mirrors describe the
- * patched ops the next local launch sees. */
+ * the next local launch, given d_patch, applies the patches as it reads them. (ABI 8: the PUT-key
+ * mirror argument and hkv_wl_refill_plan_located are gone.) */
 int hkv_wl_refill_plan(uint8_t *d_states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
                        const uint64_t *d_trace_key, const uint8_t *d_trace_op, int32_t trace_len, uint32_t *d_cursor,
                        uint32_t machine_id, uint32_t flags, unsigned long long *d_counters, uint8_t *d_opcode,
-                       uint8_t *d_patch, uint64_t *d_put_keys, void *stream);
-/* hkv_wl_refill_plan that also keeps each slot's located entry: d_trace_phys holds the located log
- * offset of every trace key (hkv_wl_peer_locate over the trace, ~0 for none) and a refilled slot's
- * word of d_slot_phys takes its new key's; the next local launch takes d_slot_phys as
- * hkv_batch_desc.d_phys (a kept slot's word still describes its op's key). */
-int hkv_wl_refill_plan_located(uint8_t *d_states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
-                               const uint64_t *d_trace_key, const uint8_t *d_trace_op, int32_t trace_len,
-                               uint32_t *d_cursor, uint32_t machine_id, uint32_t flags,
-                               unsigned long long *d_counters, uint8_t *d_opcode, uint8_t *d_patch,
-                               uint64_t *d_put_keys, const uint64_t *d_trace_phys, uint64_t *d_slot_phys,
-                               void *stream);
+                       uint8_t *d_patch, void *stream);
 /* hkv_wl_refill for big ops (op_size > 64, refilled in place; not on the first pass, flags
  * HKV_WL_REFILL_ALL and HKV_WL_READ_TS_RESET), deciding from d_states, the state mirror
  * hkv_wl_refill_plan reads: an op that is not refilled is not touched, a refilled one is only
@@ -167,13 +155,6 @@ int hkv_wl_peer_locate(hkv_table *t, const uint8_t *d_invs, int64_t n, uint32_t 
                        void *stream);
 int hkv_wl_peer_ts_at(hkv_table *t, uint8_t *d_invs, uint8_t *d_vals, const uint64_t *d_phys, int64_t n,
                       uint32_t op_size, unsigned long long *d_peer_ts, uint32_t round, void *stream);
-/* hkv_wl_peer_ts_at for INVs laid out as rows (hkv_batch_desc HKV_BATCH_ROWS: row r = peer r, element j
- * of every row on one key): INV g, whose VAL is d_vals[g] and entry d_phys[g], sits at element
- * d_inv_at[g] of d_rows. */
-int hkv_wl_peer_ts_rows(hkv_table *t, uint8_t *d_rows, const int64_t *d_inv_at, uint8_t *d_vals,
-                        const uint64_t *d_phys, int64_t n, uint32_t op_size, unsigned long long *d_peer_ts,
-                        uint32_t round, void *stream);
-
 /* The virtual peers' answers to this round's INVs: for INV j of worker w, the ack_size-byte
  * element d_acks[w*out_stride + j*n_peers + r] from peer_ids[r] is an ACK {key, ST_OP_ACK,
  * sender, ts = inv ts} (ack_copy_and_modify_elem, hermes_worker.c:100-118) -- or, with d_peer_ts

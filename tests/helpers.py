@@ -125,7 +125,6 @@ class Mirror:
     def __init__(self, g, o, name):
         self.g, self.o, self.name = g, o, name
         self.launches = 0
-        self.prepass = False                 # a local launch's prepass ran, the rest of it has not yet
         self.codes = collections.Counter()   # (batch type, "in8"/"out8"/"out9", code) over live elements
         self._orig = g.batch
         g.batch = self.batch
@@ -140,8 +139,8 @@ class Mirror:
 
     def batch(self, btype, elems, n_batches, stride, elem_size, membership, counts=None, rw=None,
               rw_stride_bytes=0, node_suspected=None, stream=None, offsets=None, state_out=None, opcode_in=None,
-              patch=None, rw_state=None, unique=False, put_keys=None, rows=None, stage=0, ack_out=None,
-              ack_out_size=16, phys=None, rw_opcodes=None):
+              patch=None, rw_state=None, unique=False, rows=None, ack_out=None,
+              ack_out_size=16, rw_opcodes=None):
         import torch
         if rw_opcodes is not None:   # the ACK launch's opcode mirror must be every read_write_ops slot's byte 8
             torch.cuda.synchronize()
@@ -149,21 +148,12 @@ class Mirror:
             assert np.array_equal(rw_opcodes[:nrw].cpu().numpy(),
                                   rw[: nrw * self.g.sizes.op].cpu().numpy().reshape(nrw, self.g.sizes.op)[:, 8]), \
                 "read_write_ops opcode mirror is stale"
-        if stage in (1, 3):   # a prepass (or its cancellation) changes no element and nothing of the meta
-            self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
-                       node_suspected, stream, state_out=state_out, opcode_in=opcode_in, patch=patch,
-                       rw_state=rw_state, unique=unique, put_keys=put_keys, stage=stage, phys=phys)
-            self.prepass = stage == 1
-            if stage == 3:
-                torch.cuda.synchronize()
-                self._check_log("prepass cancelled")
-            return
         if rows is not None:
             return self._rows(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
                               rw_stride_bytes, rw_state, rows, rw_opcodes, ack_out)
         if offsets is not None:
             return self._packed(btype, elems, n_batches, stride, elem_size, membership, offsets, stream, rw,
-                                rw_stride_bytes, rw_state, unique, ack_out, ack_out_size, phys, rw_opcodes)
+                                rw_stride_bytes, rw_state, unique, ack_out, ack_out_size, rw_opcodes)
         torch.cuda.synchronize()
         n = n_batches * stride * elem_size
         vt = np.dtype((np.void, elem_size))
@@ -178,11 +168,6 @@ class Mirror:
         if opcode_in is not None:   # the caller's opcode mirror must be every element's opcode byte
             assert np.array_equal(opcode_in[: n_batches * stride].cpu().numpy(),
                                   np.frombuffer(e_in.tobytes(), np.uint8).reshape(-1, elem_size)[:, 8])
-        if put_keys is not None:   # the PUT-key mirror and the entry states describe the (patched) elements
-            eb = np.frombuffer(e_in.tobytes(), np.uint8).reshape(-1, elem_size)
-            want = np.where(eb[:, 8] == int(L.Op.PUT), eb[:, :8].copy().view(np.int64)[:, 0], -1)
-            assert np.array_equal(put_keys[: n_batches * stride].cpu().numpy(), want), "PUT-key mirror is stale"
-            assert np.array_equal(state_out[: n_batches * stride].cpu().numpy(), eb[:, 9]), "entry state mirror is stale"
         self._count(btype, "in8", 8, np.frombuffer(e_in.tobytes(), np.uint8), n_batches, stride, elem_size, c_in)
         rw_in = rw_op = None
         if rw is not None:
@@ -191,10 +176,7 @@ class Mirror:
         rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
         self._orig(btype, elems, n_batches, stride, elem_size, membership, counts, rw, rw_stride_bytes,
                    node_suspected, stream, state_out=state_out, opcode_in=opcode_in, patch=patch, rw_state=rw_state,
-                   unique=unique, put_keys=put_keys, stage=stage, phys=phys, rw_opcodes=rw_opcodes,
-                   ack_out=ack_out, ack_out_size=ack_out_size)
-        if stage == 2:
-            self.prepass = False
+                   unique=unique, rw_opcodes=rw_opcodes, ack_out=ack_out, ack_out_size=ack_out_size)
         torch.cuda.synchronize()
         self.o.batch_multi(int(btype), e_in, n_batches, stride, c_in, membership, rw_in,
                            rw_stride_bytes // self.g.sizes.op if rw is not None else 0)
@@ -245,13 +227,8 @@ class Mirror:
         self.launches += 1
 
     def _check_log(self, what):
-        """the whole log against the oracle's; while a local launch's prepass is pending (HKV_BATCH_PREPASS),
-        the seqlock byte (entry byte 22) it uses as a tag is masked"""
+        """the whole log against the oracle's"""
         gl, ol = self.g.log_bytes(), self.o.log_bytes()[: self.g.cfg.log_cap]
-        if self.prepass:
-            e = self.g.sizes.entry
-            gl = gl.copy()
-            gl[22::e] = ol[22::e]
         if not np.array_equal(gl, ol):
             bad = np.nonzero(gl != ol)[0]
             e = self.g.sizes.entry
@@ -338,7 +315,7 @@ class Mirror:
         self.launches += 1
 
     def _packed(self, btype, elems, n_batches, total, elem_size, membership, offsets, stream, rw=None,
-                rw_stride_bytes=0, rw_state=None, unique=False, ack_out=None, ack_out_size=16, phys=None,
+                rw_stride_bytes=0, rw_state=None, unique=False, ack_out=None, ack_out_size=16,
                 rw_opcodes=None):
         """A packed (HKV_BATCH_PACKED) INV / ACK / VAL launch: the oracle applies the same batches
         laid out in rows; the device's packed output must equal the oracle's rows packed again."""
@@ -358,7 +335,7 @@ class Mirror:
         rws_in = rw_state.cpu().numpy().copy() if rw_state is not None else None
         self._orig(btype, elems, n_batches, total, elem_size, membership, rw=rw, rw_stride_bytes=rw_stride_bytes,
                    stream=stream, offsets=offsets, rw_state=rw_state, unique=unique, ack_out=ack_out,
-                   ack_out_size=ack_out_size, phys=phys, rw_opcodes=rw_opcodes)
+                   ack_out_size=ack_out_size, rw_opcodes=rw_opcodes)
         torch.cuda.synchronize()
         e_in = rows.reshape(-1).view(np.dtype((np.void, elem_size))).copy()
         self.o.batch_multi(int(btype), e_in, n_batches, width, cnt, membership, rw_in,

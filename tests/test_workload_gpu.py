@@ -21,14 +21,11 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("theta,workers,cfg3,big_fused", [(0.99, 40, False, False), (0.0, 40, False, False),
-                                                          (0.99, 160, False, False), (0.99, 40, True, False),
-                                                          (0.99, 40, True, True)])
-def test_bench_round_mirrored(theta, workers, cfg3, big_fused, monkeypatch):
+@pytest.mark.parametrize("theta,workers,cfg3", [(0.99, 40, False), (0.0, 40, False), (0.99, 160, False),
+                                                (0.99, 40, True)])
+def test_bench_round_mirrored(theta, workers, cfg3):
     """cfg3: bench.py --config cfg3 (RMWs on, big objects, 25 % PUT + 25 % RMW): the rounds engine,
-    op-sized ACKs from the virtual peers, RMW completions. big_fused (HKV_BIG_FUSED=1): the 312-B ops'
-    refills planned as patches, which k_lookup reads and k_resolve0_direct writes into the ops."""
-    monkeypatch.setenv("HKV_BIG_FUSED", "1" if big_fused else "0")
+    op-sized ACKs from the virtual peers, RMW completions."""
     from hermes_amd.kvs import HermesKV
     from hermes_amd.workload import Round, zipf_params
     n_keys, bkts = 60_000, 1 << 16
@@ -40,7 +37,7 @@ def test_bench_round_mirrored(theta, workers, cfg3, big_fused, monkeypatch):
     m = Mirror(g, o, "bench round")
     r = Round(g, workers, L.membership(3, 0), [1, 2], zipf_params(n_keys, theta), 500 if cfg3 else 200,
               500 if cfg3 else 0, seed=0x5EED, max_steps=8, trace_len=1024)
-    assert r.fused == (not cfg3 or big_fused)
+    assert r.fused == (not cfg3)
     for _ in range(steps):
         r.step()
     torch.cuda.synchronize()
@@ -141,6 +138,15 @@ def test_full_size_round_invariants():
     assert g.take_error_flags() == 0
 
 
+def _round_launches(r, k: int, sent: int, alive: int, changes: int) -> int:
+    """Launches one Round.step makes: the local batch, one INV launch per live peer with INVs in round
+    index k, the ACK rows launch (when any peer answers and the round sent INVs), the VAL batch, and one
+    after-membership-change batch per membership change in the round"""
+    n_inv = sum(1 for _, n, _ in r.remote_packed[k][5][:sent] if n)
+    acks = (1 if (not r.fit or r.inv_round) else 0) if alive else 0
+    return 1 + n_inv + acks + 1 + changes
+
+
 @pytest.mark.parametrize("machines", [3, 8])
 def test_membership_change_round_mirrored(machines):
     """BASELINE configs[4] on one GPU: the last virtual peer fails in round 2 after sending its
@@ -166,9 +172,12 @@ def test_membership_change_round_mirrored(machines):
         marshal()
     r.marshal_invs = counting_marshal
     for step in range(6):
-        r.step(drop=peers[-1] if step == 2 else None)
-    torch.cuda.synchronize()
-    assert m.launches == m.launches     # per-peer INV/ACK launches vary with the live peers
+        drop = peers[-1] if step == 2 else None
+        k, sent, before = r.clock % len(r.remote_inv), r.alive, m.launches
+        r.step(drop=drop)
+        torch.cuda.synchronize()
+        want = _round_launches(r, k, sent, sent - (drop is not None), int(drop is not None))
+        assert m.launches - before == want, (step, m.launches - before, want)
     assert r.mb[1] == ((1 << machines) - 1) & ~(1 << peers[-1]) and r.alive == machines - 2
     st = r.stats()
     assert st["committed"] > 0 and st["writes_completed"] > 0, st
@@ -205,13 +214,16 @@ def test_hades_membership_round_mirrored(machines):
     r.marshal_invs = counting_marshal
     steps = 8
     for step in range(steps):
-        r.step(drop=peers[-1] if step == 2 else None)
-    torch.cuda.synchronize()
+        drop = peers[-1] if step == 2 else None
+        k, sent, before, nch = r.clock % len(r.remote_inv), r.alive, m.launches, len(r.hades_changes)
+        r.step(drop=drop)
+        torch.cuda.synchronize()
+        want = _round_launches(r, k, sent, sent - (drop is not None), len(r.hades_changes) - nch)
+        assert m.launches - before == want, (step, m.launches - before, want)
     want = ((1 << machines) - 1) & ~(1 << peers[-1])
     assert len(r.hades_changes) == 1 and r.hades_changes[0][1] == want, r.hades_changes
     at = r.hades_changes[0][0]
     assert 2 <= at <= 4, r.hades_changes
-    assert m.launches == m.launches     # per-peer INV/ACK launches vary with the live peers
     assert r.mb[1] == want and r.mb[2] == (~want | 1) & 0xFF
     for i, h in r.hades.items():
         if i != peers[-1]:
@@ -504,11 +516,9 @@ def test_refill_plan_matches_refill(flags):
     opc0 = ops.reshape(W * S, osz)[:, 8].copy()
     d_opc = torch.from_numpy(opc0.copy()).cuda()
     d_patch = torch.full((W * S * 16,), 0xAB, dtype=torch.uint8, device="cuda")   # stale bytes get overwritten
-    pk0 = rng.integers(-2**62, 2**62, size=W * S, dtype=np.int64)                  # kept where not refilled
-    d_pk = torch.from_numpy(pk0.copy()).cuda()
     WL.check(WL._L.hkv_wl_refill_plan(WL._ptr(d_st), W, S, sz.st_value, sz.shift, WL._ptr(d_tkey), WL._ptr(d_top),
                                       tlen, WL._ptr(d_cur), mid, flags, WL._ptr(d_cnt), WL._ptr(d_opc),
-                                      WL._ptr(d_patch), WL._ptr(d_pk), None), "refill_plan")
+                                      WL._ptr(d_patch), None), "refill_plan")
     WL.check(WL._L.hkv_wl_fold_counters(WL._ptr(d_cnt), None), "fold")
     torch.cuda.synchronize()
     patch = d_patch.cpu().numpy()
@@ -518,14 +528,8 @@ def test_refill_plan_matches_refill(flags):
     assert np.array_equal(d_cur.cpu().numpy(), exp_cur)
     assert d_cnt[:5].cpu().tolist() == exp_cnt.tolist()
     assert np.array_equal(d_opc.cpu().numpy(), exp_ops.reshape(W * S, osz)[:, 8])
-    # the PUT-key mirror and the state mirror describe the patched ops (kept ops keep their words)
-    refilled = patch.reshape(-1, 16)[:, 14] == 1
-    e = exp_ops.reshape(W * S, osz)
-    want_pk = np.where(e[:, 8] == 112, e[:, :8].copy().view(np.int64)[:, 0], -1)
-    assert np.array_equal(d_pk.cpu().numpy()[refilled], want_pk[refilled])
-    assert np.array_equal(d_pk.cpu().numpy()[~refilled], pk0[~refilled])
-    assert np.array_equal(d_st.cpu().numpy()[refilled], e[refilled, 9])
-    assert np.array_equal(d_st.cpu().numpy()[~refilled], ops.reshape(W * S, osz)[~refilled, 9])
+    # the plan reads the state mirror and leaves it as it was (the local launch writes the new states)
+    assert np.array_equal(d_st.cpu().numpy(), ops.reshape(W * S, osz)[:, 9])
 
 
 @pytest.mark.parametrize("mirror", [False, True])

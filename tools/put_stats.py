@@ -3,6 +3,7 @@ one-GPU bench round, read right after the local launch (the ops then hold the pa
 their results):
 * elements, PUT elements that were not skipped (opcode PUT, not IN_PROGRESS_*), distinct keys among them;
 * the sum over 1024-element blocks of each block's distinct PUT keys (k_local_pre's lookups);
+* distinct (block, key) pairs over all looked-up elements at blocks of 32 ... 4096 elements;
 * PUTs that mutated (PUT_SUCCESS), elements whose key has a PUT in the launch (k_local_fused's tagged
   F loads), and the largest element count of one key.
 
@@ -59,7 +60,15 @@ def main():
         pair = torch.unique(torch.stack([blk, pk]), dim=1).shape[1] if pk.numel() else 0
         on_put_key = int(torch.isin(key, uk).sum())
         _, cnt = torch.unique(key, return_counts=True)
-        stats.append({"elements": n, "put_elems": int(put.sum()), "distinct_put_keys": int(uk.numel()),
+        # distinct (block, key) pairs over every looked-up element (not skipped: IN_PROGRESS_* stay skipped)
+        # at several block sizes: what a workgroup sharing its keys' lookups would fetch
+        looked = ~torch.isin(st, inprog)
+        lidx = torch.nonzero(looked).view(-1)
+        lkey = key[lidx]
+        shares = {}
+        for bs in (32, 256, 512, 1024, 2048, 4096):
+            shares[str(bs)] = torch.unique(torch.stack([lidx // bs, lkey]), dim=1).shape[1] if lidx.numel() else 0
+        stats.append({"looked_up": int(lidx.numel()), "block_key_pairs_all": shares, "elements": n, "put_elems": int(put.sum()), "distinct_put_keys": int(uk.numel()),
                       "block_key_pairs": pair, "put_success": int((st == int(L.Resp.PUT_SUCCESS)).sum()),
                       "elems_on_put_keys": on_put_key, "distinct_keys": int(cnt.numel()),
                       "max_elems_one_key": int(cnt.max())})

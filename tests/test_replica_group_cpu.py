@@ -337,3 +337,170 @@ def test_hades_membership_over_gloo(world, dead):
     assert len({x[1][0][0] for x in live}) == 1 and live[0][1][0][0] <= dead[1] + 2, res
     assert len({x[3] for x in live}) == 1                      # same membership and epoch
     assert all(x[2] == 1 for x in res), res                     # one VAL exchange, joined by all
+
+
+class _NullReplica:
+    """Stand-in for ReplicaRound with the exchange interface and no data: ReplicaGroupRound's order of
+    exchanges depends on the phase sequence only, not on what the slabs hold."""
+
+    def __init__(self, world, rank, W=4, C=5):
+        self.N, self.rank, self.W, self.C = world, rank, W, C
+        self.failed = False
+        z = lambda n: torch.zeros(n, dtype=torch.int64)  # noqa: E731
+        self.inv_pack, self.val_pack = z(W * C), z(W * C)
+        self.inv_recv, self.ack_slab, self.ack_recv, self.val_recv = (z(world * W * C) for _ in range(4))
+        self.inv_totals, self.val_totals = z(world), z(world)
+        self.inv_off, self.val_off = z(W + 1), z(W + 1)
+        self.counters, self.inv_total, self.elem_totals = z(4), z(1), z(3)
+        self.fold_counters = lambda: self.counters
+        self.count_elems = False
+        self.packed_marshal = True
+        self.unique_acks = True
+        self.own_total = None
+        self.kind = {}                # data_ptr of a send buffer -> exchange kind
+
+    def _k(self, kind, t):
+        self.kind[t.data_ptr()] = kind
+        return t
+
+    def local(self, cap=None):
+        pass
+
+    def inv_total_io(self):
+        return self.inv_totals, self.inv_off[self.W:]
+
+    def round_shape(self):
+        return self.W * self.C - 1, (self.N - 1) * self.C
+
+    def inv_io(self, width):
+        return self.inv_recv[:self.N * width], self.inv_pack[:width]
+
+    def inv_io_total(self, width):
+        return self.inv_io(width)
+
+    def take_inv_totals(self, width):
+        pass
+
+    def inv_row_io(self, p, width):
+        return self._k("inv", self.inv_pack[:width]), self.inv_recv[p * width:(p + 1) * width]
+
+    def ack_row_io(self, p, width):
+        return self._k("ack", self.ack_slab[p * width:(p + 1) * width]), self.ack_recv[p * width:(p + 1) * width]
+
+    def ack_io(self, width):
+        return self.ack_recv[:self.N * width], self.ack_slab[:self.N * width]
+
+    def invs(self, width):
+        pass
+
+    def invs_begin(self, width):
+        pass
+
+    def invs_peer(self, p, width, fold):
+        pass
+
+    def invs_end(self, width):
+        pass
+
+    def acks(self, width, stride):
+        pass
+
+    def val_total_io(self):
+        return self.val_totals, self.val_off[self.W:]
+
+    def val_io(self, width):
+        return self.val_recv[:self.N * width], self.val_pack[:width]
+
+    def val_io_total(self, width):
+        return self.val_io(width)
+
+    def take_val_totals(self, width):
+        pass
+
+    def val_width(self):
+        return 1
+
+    def vals(self, width):
+        pass
+
+    def refill(self):
+        pass
+
+    def peer_failing(self):
+        pass
+
+    def fail(self):
+        self.failed = True
+
+    def membership_change(self, peer=None, membership=None):
+        pass
+
+
+class _RecordingComm:
+    """comm= for ReplicaGroupRound that moves nothing and records every exchange in issue order"""
+
+    class _Done:
+        def wait(self):
+            pass
+
+    def __init__(self, rank, rep, log):
+        self.rank, self.rep, self.log = rank, rep, log
+
+    def gather(self, out, inp):
+        self.log.append(("gather",))
+
+    def gather_async(self, out, inp):
+        self.log.append(("gather",))
+        return self._Done()
+
+    def a2a(self, out, inp):
+        self.log.append(("a2a",))
+
+    def p2p(self, pairs):
+        for p, snd, _ in pairs:
+            self.log.append(("p2p", self.rep.kind[snd.data_ptr()], min(self.rank, p), max(self.rank, p)))
+        return {p: [self._Done()] for p, _, _ in pairs}
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
+@pytest.mark.parametrize("drop_round", [None, 3])
+def test_p2p_exchanges_follow_one_global_pair_order(world, drop_round):
+    """ReplicaGroupRound's per-peer exchanges (batch_isend_irecv with each peer) cannot
+    wait on one another in a cycle. Every rank's exchanges, in issue order, are recorded at world sizes
+    2-8 over 20 rounds (steady rounds at the planned width and calibrating ones, with and without a
+    failure): (1) within a round each rank's sequence of (phase, rank pair) is a subsequence of ONE
+    global order -- all INV pairs, then all ACK pairs, pairs ascending -- so the globally first pending
+    exchange is at the head of both its ranks' queues; (2) both ranks of a pair issue their exchanges of
+    that pair in the same order; (3) every rank issues the same sequence of collectives."""
+    from hermes_amd.replica_group import ReplicaGroupRound
+    rounds = 20
+    logs = {}
+    for rank in range(world):
+        rep = _NullReplica(world, rank)
+        log = []
+        drv = ReplicaGroupRound(None, rep.W, None, world=world, rank=rank, replica=rep, p2p=True,
+                                comm=_RecordingComm(rank, rep, log))
+        per_round = []
+        for k in range(rounds):
+            start = len(log)
+            drop = world - 1 if drop_round is not None and k == drop_round and world > 2 else None
+            drv.step(drop=drop)
+            per_round.append(log[start:])
+        logs[rank] = per_round
+    pairs = sorted((a, b) for a in range(world) for b in range(a + 1, world))
+    global_order = [("p2p", kind, a, b) for kind in ("inv", "ack") for a, b in pairs]
+    pos = {e: i for i, e in enumerate(global_order)}
+    for k in range(rounds):
+        colls = {r: [e for e in logs[r][k] if e[0] != "p2p"] for r in range(world)}
+        assert all(colls[r] == colls[0] for r in range(world)), (k, colls)
+        for r in range(world):
+            seq = [e for e in logs[r][k] if e[0] == "p2p"]
+            idx = [pos[e] for e in seq]
+            assert idx == sorted(idx) and len(set(idx)) == len(idx), (k, r, seq)
+            # every pair of this rank exchanged once per phase
+            assert sorted(e[2:] for e in seq if e[1] == "inv") == [p for p in pairs if r in p]
+            assert sorted(e[2:] for e in seq if e[1] == "ack") == [p for p in pairs if r in p]
+        for a, b in pairs:
+            sa = [e[1] for e in logs[a][k] if e[0] == "p2p" and e[2:] == (a, b)]
+            sb = [e[1] for e in logs[b][k] if e[0] == "p2p" and e[2:] == (a, b)]
+            assert sa == sb, (k, a, b, sa, sb)

@@ -342,7 +342,11 @@ def main():
             pmc_launches = pj.get("launches", {})
             traffic_src = (f"profiles/pmc_local_batch.json ({pj.get('source', 'rocprofv3 --pmc')}: FETCH_SIZE x2 + "
                            f"WRITE_SIZE in separate rocprofv3 passes of this configuration, median of "
-                           f"{pj.get('launches_counted', pj.get('launches'))} launches)")
+                           f"{pj.get('launches_counted', pj.get('launches'))} launches). Per-shape multipliers "
+                           f"(profiles/r06_counter_calibration.txt, tools/calib_bench.hip): reads x2 for every shape -- "
+                           f"random 8/16/64/128-B records and 16-B streaming lanes each cost one 128-B request, counted "
+                           f"as 64 B (RDREQ = lines, RDREQ_32B = 0); writes x1 -- exact for 64-B and 128-B blocks, "
+                           f"32-B granules below 64 B. Traffic = 128-B lines read + bytes written at the memory side")
     for k, v in launches.items():
         t = pmc_launches.get(k, {}).get("traffic_bytes")
         v["traffic"] = t

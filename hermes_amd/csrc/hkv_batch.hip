@@ -1456,8 +1456,13 @@ constexpr int kPrePair = HKV_PRE_PAIR;   // keys per lane group in flight in the
 #endif
 // No seqlock-byte tags (round 5): k_local_fused loads every hit's F word beside its log line and needs
 // no mark of the keys that have one
+#ifdef HKV_PRE_NUM_SGPR
+#define HKV_PRE_SGPR_ATTR __attribute__((amdgpu_num_sgpr(HKV_PRE_NUM_SGPR)))
+#else
+#define HKV_PRE_SGPR_ATTR
+#endif
 template <int HEAD = kPreHead>
-__global__ __launch_bounds__(kPreThreads) HKV_PRE_ATTR void k_local_pre(BatchArgs a)
+__global__ __launch_bounds__(kPreThreads) HKV_PRE_ATTR HKV_PRE_SGPR_ATTR void k_local_pre(BatchArgs a)
 {
     __shared__ uint64_t hk[kPreHash], gk[kPreHash];  // the block's PUT keys, the head's
     __shared__ uint32_t hv[kPreHash];
@@ -1598,6 +1603,49 @@ __global__ __launch_bounds__(kPreThreads) HKV_PRE_ATTR void k_local_pre(BatchArg
     }
 }
 
+// exec_read / exec_write (hermesKV.c:251-356, with the skew optimisations of :196-238) for a local op
+// of the direct path (RMWs off) that leaves its key's meta m as it is: the caller has excluded the
+// branches that change it (update_actions, write replays) -- the element is not its key's first
+// mutating element, so would_mutate is false against S_0, or m is the key's meta after that first write
+// -- and only the element's own bytes move, without the generic dispatch's meta updates. An element
+// that would mutate after all raises error flag bit 0, as the generic path's meta check does.
+__device__ __forceinline__ void local_resolve_nm(const BatchArgs &a, uint8_t *x, const uint8_t *ent, const Meta &m)
+{
+    const uint8_t oc = x[8], st = m_state(m);
+    const bool obi_empty = m_obi(m) == kObiEmpty;
+    bool mut = false;
+    if (oc == kOpGet) {
+        if (st == kValid) {
+            copy_value<31>(x + kOpValueOff, ent + kEntryValueOff, 31);
+            x[9] = kGetComplete;
+            x[10] = (uint8_t)((m_val_len(m) >> a.g.shift) - kOpMetaSize);
+        } else if (st == kInvalidWrite || st == kWrite || st == kReplay) {
+            x[9] = kGetStall;
+        } else {
+            x[9] = kEmpty;
+            if (st == kInvalid) {   // hermes_check_membership_n_write_replay_actions, hermesKV.c:179-194
+                const uint8_t lw = m_lwid(m);
+                if (lw < 8 && ((a.g_membership >> lw) & 1u)) x[9] = kGetStall;
+                else mut = obi_empty;
+            }
+        }
+        if (a.g.skew & kSkewReadComplete) hot_read_complete(x, m.ver, m_cid(m));
+    } else if (oc == kOpPut) {
+        mut = (st == kValid || st == kInvalid) && obi_empty;
+        x[9] = kPutStall;
+        if (a.g.skew & kSkewWriteCoalesce) {   // as exec_write (hkv_exec.h)
+            const uint32_t cv = m.ver & 0xFFFFu;
+            uint32_t over = ld32(x + 12);
+            if (st != kReplay && over == 0) {
+                st32(x + 12, cv);
+                over = cv;
+            }
+            if (over > 0 && over + 1u < cv) x[9] = kPutComplete;
+        }
+    }
+    if (mut && a.error_flags) atomicOr(a.error_flags, 1u);
+}
+
 // Every element, F final (except on INVALID keys): see the section comment. One wave per block and
 // nothing shared beyond it. The lookup runs four lanes per element (each lane holds 16 B of the op
 // and of the log line); the wave-private LDS copies of op and entry are then resolved one element
@@ -1607,7 +1655,10 @@ __global__ __launch_bounds__(kPreThreads) HKV_PRE_ATTR void k_local_pre(BatchArg
 // SGPR budget of the local launch's kernels (HKV_LOCAL_NUM_SGPR, a build macro for A/B): waves are admitted
 // per SIMD by ~800 SGPRs / (ceil(sgpr/16) * 16 + 16) (MI355X_MICROARCH.md, "Residency"), so 92 SGPRs allow
 // 7 waves and 80 allow 8
-#ifdef HKV_LOCAL_NUM_SGPR
+#ifndef HKV_LOCAL_NUM_SGPR
+#define HKV_LOCAL_NUM_SGPR 80   // round 6: local launch 353-355 -> 341-351 us (gpurun_out/r06c), 7 -> 8 waves per SIMD
+#endif
+#if HKV_LOCAL_NUM_SGPR > 0
 #define HKV_LOCAL_SGPR_ATTR __attribute__((amdgpu_num_sgpr(HKV_LOCAL_NUM_SGPR)))
 #else
 #define HKV_LOCAL_SGPR_ATTR
@@ -1658,11 +1709,17 @@ __global__ __launch_bounds__(64) HKV_LOCAL_SGPR_ATTR void k_local_fused(BatchArg
         key[k] = (uint64_t)(uint32_t)__shfl((int)op[k].x, 0, 4) | ((uint64_t)(uint32_t)__shfl((int)op[k].y, 0, 4) << 32);
         const uint32_t h0 = (uint32_t)__shfl((int)op[k].z, 0, 4);
         probe[k] = false;
-        if (live[k])
+        if (live[k] && !HKV_DBG_ON(a, 128))
             probe[k] = in_count(a, (uint32_t)(i0 + te[k])) && !skip_elem_os(kLocal, (uint8_t)h0, (uint8_t)(h0 >> 8));
     }
     unsigned long long fwv[P];   // every hit's F word, loaded beside its log line
-    lookup_pair_f<P>(a, key, probe, q, gbase, ok, phys, ln, fwv);
+    if (HKV_DBG_ON(a, 512)) {   // (timing modes) no F loads
+        lookup_pair<P>(a, key, probe, q, gbase, ok, phys, ln);
+#pragma unroll
+        for (int k = 0; k < P; ++k) fwv[k] = ~0ull;
+    } else {
+        lookup_pair_f<P>(a, key, probe, q, gbase, ok, phys, ln, fwv);
+    }
 #pragma unroll
     for (int k = 0; k < P; ++k) {
         Meta m;
@@ -1678,7 +1735,7 @@ __global__ __launch_bounds__(64) HKV_LOCAL_SGPR_ATTR void k_local_fused(BatchArg
         }
     }
     __syncthreads();
-    if (tid < E && i0 + tid < a.n) {
+    if (tid < E && i0 + tid < a.n && !HKV_DBG_ON(a, 64)) {
         const int64_t i = i0 + tid;
         uint8_t *x = reinterpret_cast<uint8_t *>(&sops[tid * 4]);
         uint8_t *ent = reinterpret_cast<uint8_t *>(&sln[tid * 4]);
@@ -1686,7 +1743,6 @@ __global__ __launch_bounds__(64) HKV_LOCAL_SGPR_ATTR void k_local_fused(BatchArg
         uint8_t st = kStDone;
         if (e != kNone) {
             Ctx c = make_ctx(a);
-            const uint8_t bidx = (uint8_t)((uint32_t)i % (uint32_t)a.stride);
             Meta m;
             meta_load(ent, m);
             const bool wm = would_mutate(kLocal, x, m, c);
@@ -1708,10 +1764,7 @@ __global__ __launch_bounds__(64) HKV_LOCAL_SGPR_ATTR void k_local_fused(BatchArg
                     st = kStCommit;
                 } else {
                     // F of a key that is not INVALID is its first PUT (k_local_pre)
-                    const Meta m0 = f != kNone && (uint32_t)i > f ? after_first<kLocal>(a, m, f, 1) : m;
-                    Meta tm = m0;
-                    dispatch<31>(kLocal, x, ent, bidx, tm, c);
-                    if (a.error_flags && !meta_equal(tm, m0)) atomicOr(a.error_flags, 1u);
+                    local_resolve_nm(a, x, ent, f != kNone && (uint32_t)i > f ? after_first<kLocal>(a, m, f, 1) : m);
                 }
             }
         } else if (sprb[tid]) {
@@ -1719,9 +1772,11 @@ __global__ __launch_bounds__(64) HKV_LOCAL_SGPR_ATTR void k_local_fused(BatchArg
         }
         // k_local_pre read only the PUTs the caller's opcode mirror names
         if (a.opc && sprb[tid] && x[8] == kOpPut && a.opc[i] != kOpPut && a.error_flags) atomicOr(a.error_flags, 8u);
-        a.ent[i] = e;
-        a.st[i] = st;
-        if (st != kStDefer) note_state(a, i, x);
+        if (!HKV_DBG_ON(a, 1024)) {
+            a.ent[i] = e;
+            a.st[i] = st;
+            if (st != kStDefer) note_state(a, i, x);
+        }
     }
     __syncthreads();
     // the waiting elements (keys INVALID at S_0: rare), appended once per block
@@ -1731,196 +1786,11 @@ __global__ __launch_bounds__(64) HKV_LOCAL_SGPR_ATTR void k_local_fused(BatchArg
     }
 #pragma unroll
     for (int k = 0; k < P; ++k) {
-        if (!live[k]) continue;
+        if (!live[k] || HKV_DBG_ON(a, 256)) continue;
         uint8_t *xg = a.elems + (i0 + te[k]) * 56 + 16 * q;
         const uint4 w = sops[te[k] * 4 + q];
         if (q < 3) *reinterpret_cast<uint4 *>(xg) = w;
         else *reinterpret_cast<uint64_t *>(xg) = (uint64_t)w.x | ((uint64_t)w.y << 32);
-    }
-}
-
-// k_local_fused with each distinct key's lookup shared by the block (a launch's 4.1 M
-// elements hold ~1.1 M distinct keys; at 256 / 512-element blocks 19 / 24 % of the lookups repeat a key
-// the block has already looked up, profiles/r06_put_stats_blocks.jsonl). NW waves of 32 elements each:
-//   1. each wave loads its elements' ops (four lanes per element, patches applied) into LDS, as
-//      k_local_fused does;
-//   2. lane 0 of every group puts its element's key into the block's LDS hash (H = 2E slots); a key's
-//      first arrival takes the next distinct index d;
-//   3. the block's lane groups look the distinct keys up (bucket, then log line and F word; two keys per
-//      group, all loads in flight together) into LDS: the entry's bytes 16..63 (meta and value), the F
-//      word, the entry id;
-//   4. lanes 0..31 of every wave resolve their wave's elements against their key's shared copy exactly
-//      as k_local_fused (i < F: against S_0, i == F: its shadow from the entry in HBM, i > F: after the
-//      first write; keys INVALID at S_0 deferred);
-//   5. the ops go back whole, per wave.
-// The entry copy is only read in step 4 (a mutating element writes its own shadow, never the copy).
-#ifndef HKV_LF_SHARED
-#define HKV_LF_SHARED 0
-#endif
-constexpr int kLfShared = HKV_LF_SHARED;   // waves per k_local_shared block; 0: k_local_fused (a build macro for A/B)
-
-template <int NW>
-__global__ __launch_bounds__(64 * NW) HKV_LOCAL_SGPR_ATTR void k_local_shared(BatchArgs a)
-{
-    constexpr int E = 32 * NW, H = 2 * E, G = 16 * NW;   // elements, hash slots, lane groups
-    constexpr int HB = __builtin_ctz(H);
-    static_assert(E <= 0x7FFF && (H & (H - 1)) == 0, "slot and distinct indices fit 15 bits");
-    __shared__ uint4 sops[E * 4];               // the block's ops, 64 B each (56 used)
-    __shared__ uint4 sln[E * 3];                // distinct key d: its entry's bytes 16..63
-    __shared__ unsigned long long sfw[E];       // d's F word (~0: none wanted)
-    __shared__ uint32_t sent[E];                // d's entry id (kNone: a miss)
-    __shared__ unsigned long long hkey[H];      // the hash: keys, ~0 empty
-    __shared__ unsigned long long dkey[E];      // d's key
-    __shared__ uint16_t hslot[H];               // slot -> d
-    __shared__ uint16_t eslot[E];               // element -> slot, 0x8000 | d (a key that cannot go in the
-                                                // hash), 0xFFFF: not looked up
-    __shared__ uint32_t nd;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, q = tid & 3, gbase = lane & ~3;
-    const int64_t i0 = (int64_t)blockIdx.x * E;
-    for (int j = tid; j < H; j += 64 * NW) hkey[j] = ~0ull;
-    if (tid == 0) nd = 0;
-    uint4 op[2];
-    bool live[2];
-    int be[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        be[k] = w * 32 + k * 16 + (lane >> 2);
-        const int64_t i = i0 + be[k];
-        live[k] = i < a.n;
-        op[k] = make_uint4(0u, 0u, 0u, 0u);
-        if (live[k]) {
-            const uint8_t *xg = a.elems + i * 56 + 16 * q;
-            U64x2 p{0, 0};
-            if (a.patch) p = *reinterpret_cast<const U64x2 *>(a.patch + i * 16);
-            if (q < 3) {
-                op[k] = *reinterpret_cast<const uint4 *>(xg);
-            } else {
-                const uint64_t t = *reinterpret_cast<const uint64_t *>(xg);
-                op[k].x = (uint32_t)t;
-                op[k].y = (uint32_t)(t >> 32);
-            }
-            if (patch_valid(p.b)) op[k] = patch_chunk(op[k], q, p.a, p.b);
-        }
-        sops[be[k] * 4 + q] = op[k];
-    }
-    __syncthreads();   // the hash's empty marks
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const uint64_t key = (uint64_t)(uint32_t)__shfl((int)op[k].x, 0, 4) | ((uint64_t)(uint32_t)__shfl((int)op[k].y, 0, 4) << 32);
-        const uint32_t h0 = (uint32_t)__shfl((int)op[k].z, 0, 4);
-        if (q != 0) continue;
-        uint16_t es = 0xFFFF;
-        if (live[k] && in_count(a, (uint32_t)(i0 + be[k])) && !skip_elem_os(kLocal, (uint8_t)h0, (uint8_t)(h0 >> 8))) {
-            if (key == ~0ull) {   // the hash's empty mark: a distinct entry of its own
-                const uint32_t d = atomicAdd(&nd, 1u);
-                dkey[d] = key;
-                es = (uint16_t)(0x8000u | d);
-            } else {
-                uint32_t sl = (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> (64 - HB));
-                for (;;) {   // H = 2E slots for at most E keys: never full
-                    const unsigned long long old = atomicCAS(&hkey[sl], ~0ull, key);
-                    if (old == ~0ull) {
-                        const uint32_t d = atomicAdd(&nd, 1u);
-                        hslot[sl] = (uint16_t)d;
-                        dkey[d] = key;
-                        break;
-                    }
-                    if (old == key) break;
-                    sl = (sl + 1) & (H - 1);
-                }
-                es = (uint16_t)sl;
-            }
-        }
-        eslot[be[k]] = es;
-    }
-    __syncthreads();
-    {
-        const uint32_t n_d = nd;
-        uint64_t key[2], phys[2];
-        bool probe[2], ok[2];
-        uint4 ln[2];
-        unsigned long long fwv[2];
-        uint32_t d[2];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            d[k] = (uint32_t)(tid >> 2) + (uint32_t)k * G;
-            probe[k] = d[k] < n_d;
-            key[k] = probe[k] ? dkey[d[k]] : 0ull;
-        }
-        lookup_pair_f<2>(a, key, probe, q, gbase, ok, phys, ln, fwv);
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            Meta m;
-            const uint64_t ek = line_key_meta(ln[k], m);
-            const bool hit = ok[k] && ek == key[k];
-            if (!probe[k]) continue;
-            if (q > 0) sln[d[k] * 3 + q - 1] = ln[k];
-            if (q == 0) {
-                // keys INVALID at S_0 take their F after this pass (k_local_deferred)
-                sfw[d[k]] = hit && m_state(m) != kInvalid ? fwv[k] : ~0ull;
-                sent[d[k]] = hit ? (uint32_t)(phys[k] / a.g.entry_unit) : kNone;
-            }
-        }
-    }
-    __syncthreads();
-    if (lane < 32 && i0 + w * 32 + lane < a.n) {
-        const int b = w * 32 + lane;
-        const int64_t i = i0 + b;
-        uint8_t *x = reinterpret_cast<uint8_t *>(&sops[b * 4]);
-        const uint16_t es = eslot[b];
-        const uint32_t d = es == 0xFFFF ? 0u : (es & 0x8000) ? (es & 0x7FFFu) : hslot[es];
-        const uint32_t e = es == 0xFFFF ? kNone : sent[d];
-        uint8_t *ent = reinterpret_cast<uint8_t *>(&sln[d * 3]) - 16;   // bytes 16..63 are held
-        uint8_t st = kStDone;
-        if (e != kNone) {
-            Ctx c = make_ctx(a);
-            const uint8_t bidx = (uint8_t)((uint32_t)i % (uint32_t)a.stride);
-            Meta m;
-            meta_load(ent, m);
-            const bool wm = would_mutate(kLocal, x, m, c);
-            if (m_state(m) == kInvalid) {
-                // GET replays may mutate: they offer F now, and the key's elements resolve later
-                if (wm) {
-                    const uint64_t ph = phys_of(a, e);
-                    offer(a.fw + fw_index(a, ph), a.rtag0, (uint32_t)i);
-                    if ((uint8_t)(m.w5 >> 16) != a.ltag) a.log[ph + kEntryMetaOff + 4] = a.ltag;
-                }
-                st = kStDefer;
-                a.fbl[atomicAdd(&a.ctr[kCtrDefer], 1u)] = (uint32_t)i;   // rare: no block list
-            } else {
-                const uint32_t f = first_cand(sfw[d], a.rtag0);
-                // a mutating element must have offered itself in k_local_pre
-                if (wm && (f == kNone || f > (uint32_t)i) && a.error_flags) atomicOr(a.error_flags, 4u);
-                if ((uint32_t)i == f) {
-                    // S_0 from the entry in HBM (the block holds only its bytes 16..63); nothing writes
-                    // entries before k_commit_w
-                    apply_to_shadow<kLocal, 31>(a, x, (uint32_t)i, entry_of(a, e));
-                    st = kStCommit;
-                } else {
-                    // F of a key that is not INVALID is its first PUT (k_local_pre)
-                    const Meta m0 = f != kNone && (uint32_t)i > f ? after_first<kLocal>(a, m, f, 1) : m;
-                    Meta tm = m0;
-                    dispatch<31>(kLocal, x, ent, bidx, tm, c);
-                    if (a.error_flags && !meta_equal(tm, m0)) atomicOr(a.error_flags, 1u);
-                }
-            }
-        } else if (es != 0xFFFF) {
-            x[9] = kMiss;
-        }
-        // k_local_pre read only the PUTs the caller's opcode mirror names
-        if (a.opc && es != 0xFFFF && x[8] == kOpPut && a.opc[i] != kOpPut && a.error_flags) atomicOr(a.error_flags, 8u);
-        a.ent[i] = e;
-        a.st[i] = st;
-        if (st != kStDefer) note_state(a, i, x);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        if (!live[k]) continue;
-        uint8_t *xg = a.elems + (i0 + be[k]) * 56 + 16 * q;
-        const uint4 v = sops[be[k] * 4 + q];
-        if (q < 3) *reinterpret_cast<uint4 *>(xg) = v;
-        else *reinterpret_cast<uint64_t *>(xg) = (uint64_t)v.x | ((uint64_t)v.y << 32);
     }
 }
 
@@ -2154,8 +2024,13 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
 // of the entry -- exactly the rows' launches one after another, since each row holds the key once --
 // and each element and the entry line are written back where they changed. An ACK's completion finds
 // its read_write_ops once per position (the rows share the batch layout).
+#ifdef HKV_ROWS_NUM_SGPR
+#define HKV_ROWS_SGPR_ATTR __attribute__((amdgpu_num_sgpr(HKV_ROWS_NUM_SGPR)))
+#else
+#define HKV_ROWS_SGPR_ATTR
+#endif
 template <int TYPE, int RMAX, int CH, int P = kLookupPair>
-__global__ __launch_bounds__(64) void k_unique_rows(BatchArgs a)
+__global__ __launch_bounds__(64) HKV_ROWS_SGPR_ATTR void k_unique_rows(BatchArgs a)
 {
     constexpr int E = 16 * P;   // positions per wave: P per lane group
     // CH: 16-B chunks of an element held in LDS (1 for 16-B ACKs, 4 for 56-B INVs)
@@ -3790,14 +3665,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     } else if (local_direct) {
         hipLaunchKernelGGL(k_local_pre<kPreHead>, dim3((unsigned)((n + kPreElems - 1) / kPreElems)), dim3(kPreThreads),
                            0, s, a);
-        if (kLfShared == 8)
-            hipLaunchKernelGGL(k_local_shared<8>, dim3((unsigned)((n + 255) / 256)), dim3(512), 0, s, a);
-        else if (kLfShared == 16)
-            hipLaunchKernelGGL(k_local_shared<16>, dim3((unsigned)((n + 511) / 512)), dim3(1024), 0, s, a);
-        else if (kLfShared == 4)
-            hipLaunchKernelGGL(k_local_shared<4>, dim3((unsigned)((n + 127) / 128)), dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL(k_local_fused<2>, dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(k_local_fused<2>, dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
         // the waiting elements' count is on the device: enough workgroups for the rounds after a
         // membership change (configs[4]: ~100 K elements of keys a failed peer left INVALID), which
         // return at once when there are few

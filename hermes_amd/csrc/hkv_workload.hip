@@ -483,8 +483,13 @@ __device__ __forceinline__ void wave_ranks(const unsigned long long *b, int lane
 // One wave per WPW workers: all their state loads, then all their trace loads, are in flight
 // together (a wave's work is two dependent loads; with WPW = 2 the 16384 workers of configs[1] fit
 // the chip's 8192 wave slots in one pass instead of two).
+#ifdef HKV_PLAN_NUM_SGPR
+#define HKV_PLAN_SGPR_ATTR __attribute__((amdgpu_num_sgpr(HKV_PLAN_NUM_SGPR)))
+#else
+#define HKV_PLAN_SGPR_ATTR
+#endif
 template <int WPW>
-__global__ __launch_bounds__(256) void k_refill_plan_w(uint8_t *states, int32_t n_workers, int32_t stride,
+__global__ __launch_bounds__(256) HKV_PLAN_SGPR_ATTR void k_refill_plan_w(uint8_t *states, int32_t n_workers, int32_t stride,
                                                        uint32_t st_value, uint32_t shift, const uint64_t *tkey,
                                                        const uint8_t *top, int32_t tlen, uint32_t *cursor,
                                                        uint32_t machine_id, uint32_t flags,

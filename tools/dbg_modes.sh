@@ -1,6 +1,8 @@
 #!/bin/bash
-# k_local_pre timed under the work-skipping modes (HKV_DBG bits: 1 no offers, 2 no lookups, 4 no head
-# filter, 8 empty kernel, 16 loads only, 32 no tags). Results are invalid by design, so the modes exist
+# The local launch timed under the work-skipping modes (HKV_DBG bits; k_local_pre: 1 no offers, 2 no lookups,
+# 4 no head filter, 8 empty kernel, 16 loads only; k_local_fused: 64 no resolve, 128 no lookups, 256 no op
+# write-back, 512 no F loads, 1024 no per-element scratch and state-mirror stores). Results are invalid by
+# design, so the modes exist
 # only in a separate build (-DHKV_DEBUG_MODES) and run through tools/round_probe.py: bench.py refuses
 # both HKV_DBG and such a library.
 #   here:        tools/dbg_modes.sh build      (build_ab/libhermeskv_dbg.so)

@@ -7,8 +7,11 @@ grouped the way bench.py times them:
 * invs:  every INV launch of the round (one unique-key launch per virtual peer: k_unique_lds<2, ...>);
 * acks:  the ACK launch (k_unique_rows<3, ...>, all peers' rows in one pass);
 * vals:  the VAL launch (the one-pass k_lookup after the ACKs).
-Counters are KB per dispatch; FETCH_SIZE is doubled (on gfx950 it reports half the bytes of wide
-reads, MI355X_MICROARCH.md, HBM section). The median over the run's rounds is written to OUT.json,
+Counters are KB per dispatch; FETCH_SIZE is doubled. Calibrated on this access mix (tools/calib_bench.hip,
+profiles/r06_counter_calibration.txt): every read shape the batch kernels use -- random 8-, 16-, 64- and
+128-byte records and 16-byte streaming lanes -- costs one 128-byte memory request, which FETCH_SIZE counts
+as 64 bytes (TCC_EA0_RDREQ = lines touched, RDREQ_32B = 0), and takes the same time per record whatever
+its width; WRITE_SIZE is exact for 64- and 128-byte writes and counts smaller ones as 32-byte granules. The median over the run's rounds is written to OUT.json,
 stamped with the bench configuration (bench.py reports it only for that configuration) as
 roofline.traffic and roofline.launches.*.traffic."""
 import csv

@@ -504,6 +504,7 @@ __device__ __forceinline__ void lookup_pair_f(const BatchArgs &a, const uint64_t
     }
 }
 
+
 template <int P = kLookupPair>
 __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, int64_t i_end)
 {
@@ -1663,20 +1664,34 @@ __device__ __forceinline__ void local_resolve_nm(const BatchArgs &a, uint8_t *x,
 #else
 #define HKV_LOCAL_SGPR_ATTR
 #endif
-template <int P>
-__global__ __launch_bounds__(64) HKV_LOCAL_SGPR_ATTR void k_local_fused(BatchArgs a)
+// NW waves per block (round 6): each wave works on its own 32 elements as before, and after the block's
+// barrier the stage bytes and the state mirror of all NW * 32 elements go out as whole 64-byte blocks (a
+// wave's 32 bytes alone are half a block, which HBM writes with a read-modify-write: tools/calib_bench.hip,
+// 16-B random writes 2.4x the time of 64-B ones).
+#ifndef HKV_LF_WAVES
+#define HKV_LF_WAVES 2
+#endif
+constexpr int kLfWaves = HKV_LF_WAVES;   // waves per k_local_fused block (a build macro for A/B)
+template <int P, int NW>
+__global__ __launch_bounds__(64 * NW) HKV_LOCAL_SGPR_ATTR void k_local_fused(BatchArgs a)
 {
     constexpr int E = 16 * P;   // elements per wave: P per lane group
-    __shared__ uint4 sops[E * 4];   // 64 B per op (56 used)
-    __shared__ uint4 sln[E * 4];
-    __shared__ unsigned long long sfw[E];
-    __shared__ uint32_t sent[E];     // entry id of a hit, kNone otherwise
-    __shared__ uint8_t sprb[E];      // probed (not skipped)
-    __shared__ uint32_t sdef[E];
+    constexpr int EB = E * NW;  // elements per block
+    __shared__ uint4 sops_b[NW][E * 4];   // 64 B per op (56 used)
+    __shared__ uint4 sln_b[NW][E * 4];
+    __shared__ unsigned long long sfw_b[NW][E];
+    __shared__ uint32_t sent_b[NW][E];    // entry id of a hit, kNone otherwise
+    __shared__ uint8_t sprb_b[NW][E];     // probed (not skipped)
+    __shared__ uint32_t sst[EB / 4], sstate[EB / 4];   // the block's stage bytes and state mirror
+    __shared__ uint32_t sdef[EB];
     __shared__ uint32_t ndef;
-    const int tid = threadIdx.x, q = tid & 3, gbase = tid & ~3;
-    const int64_t i0 = (int64_t)blockIdx.x * E;
-    if (tid == 0) ndef = 0;
+    const int w = threadIdx.x >> 6, tid = threadIdx.x & 63, q = tid & 3, gbase = tid & ~3;
+    uint4 *sops = sops_b[w], *sln = sln_b[w];
+    unsigned long long *sfw = sfw_b[w];
+    uint32_t *sent = sent_b[w];
+    uint8_t *sprb = sprb_b[w];
+    const int64_t ib = (int64_t)blockIdx.x * EB, i0 = ib + (int64_t)w * E;
+    if (threadIdx.x == 0) ndef = 0;
     uint64_t key[P];
     bool probe[P], ok[P], live[P];
     uint64_t phys[P];
@@ -1712,7 +1727,7 @@ __global__ __launch_bounds__(64) HKV_LOCAL_SGPR_ATTR void k_local_fused(BatchArg
         if (live[k] && !HKV_DBG_ON(a, 128))
             probe[k] = in_count(a, (uint32_t)(i0 + te[k])) && !skip_elem_os(kLocal, (uint8_t)h0, (uint8_t)(h0 >> 8));
     }
-    unsigned long long fwv[P];   // every hit's F word, loaded beside its log line
+    unsigned long long fwv[P];   // a hit's F word, loaded beside its log line
     if (HKV_DBG_ON(a, 512)) {   // (timing modes) no F loads
         lookup_pair<P>(a, key, probe, q, gbase, ok, phys, ln);
 #pragma unroll
@@ -1772,15 +1787,26 @@ __global__ __launch_bounds__(64) HKV_LOCAL_SGPR_ATTR void k_local_fused(BatchArg
         }
         // k_local_pre read only the PUTs the caller's opcode mirror names
         if (a.opc && sprb[tid] && x[8] == kOpPut && a.opc[i] != kOpPut && a.error_flags) atomicOr(a.error_flags, 8u);
-        if (!HKV_DBG_ON(a, 1024)) {
-            a.ent[i] = e;
-            a.st[i] = st;
-            if (st != kStDefer) note_state(a, i, x);
-        }
+        if (!HKV_DBG_ON(a, 1024)) a.ent[i] = e;
+        // a deferred element's state byte is written again by k_local_deferred, after this pass
+        reinterpret_cast<uint8_t *>(sst)[w * E + tid] = st;
+        reinterpret_cast<uint8_t *>(sstate)[w * E + tid] = x[9];
     }
     __syncthreads();
+    // the block's stage bytes and state mirror as whole blocks (a partial last block byte by byte)
+    if (!HKV_DBG_ON(a, 1024) && !HKV_DBG_ON(a, 64)) {
+        if (ib + EB <= a.n && ((uintptr_t)a.state_out & 3) == 0) {   // (st is 256-byte aligned)
+            if ((int)threadIdx.x < EB / 4) {
+                reinterpret_cast<uint32_t *>(a.st + ib)[threadIdx.x] = sst[threadIdx.x];
+                if (a.state_out) reinterpret_cast<uint32_t *>(a.state_out + ib)[threadIdx.x] = sstate[threadIdx.x];
+            }
+        } else if ((int)threadIdx.x < EB && ib + threadIdx.x < a.n) {
+            a.st[ib + threadIdx.x] = reinterpret_cast<const uint8_t *>(sst)[threadIdx.x];
+            if (a.state_out) a.state_out[ib + threadIdx.x] = reinterpret_cast<const uint8_t *>(sstate)[threadIdx.x];
+        }
+    }
     // the waiting elements (keys INVALID at S_0: rare), appended once per block
-    if (ndef && tid == 0) {
+    if (ndef && threadIdx.x == 0) {
         const uint32_t base = atomicAdd(&a.ctr[kCtrDefer], ndef);
         for (uint32_t j = 0; j < ndef; ++j) a.fbl[base + j] = sdef[j];
     }
@@ -1788,9 +1814,9 @@ __global__ __launch_bounds__(64) HKV_LOCAL_SGPR_ATTR void k_local_fused(BatchArg
     for (int k = 0; k < P; ++k) {
         if (!live[k] || HKV_DBG_ON(a, 256)) continue;
         uint8_t *xg = a.elems + (i0 + te[k]) * 56 + 16 * q;
-        const uint4 w = sops[te[k] * 4 + q];
-        if (q < 3) *reinterpret_cast<uint4 *>(xg) = w;
-        else *reinterpret_cast<uint64_t *>(xg) = (uint64_t)w.x | ((uint64_t)w.y << 32);
+        const uint4 v = sops[te[k] * 4 + q];
+        if (q < 3) *reinterpret_cast<uint4 *>(xg) = v;
+        else *reinterpret_cast<uint64_t *>(xg) = (uint64_t)v.x | ((uint64_t)v.y << 32);
     }
 }
 
@@ -3288,28 +3314,7 @@ __device__ void hp_partition(const HostPartCommon &p, HpLds &L, int g, int nb, u
     if (pr) p.prof[4] = wall_clock64();
     if (tid == 0) {
         __hip_atomic_store(p.flags + g, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        // the partition's next launch may start: the entry lines written above are visible to it
-        if (p.order) __hip_atomic_store(p.order + g, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
-}
-
-// Launches on several streams: workgroup g waits until its partition's previous launch is done
-// (order[g] == seq - 1). Every wait ends: after 1 s (wall_clock64 at 100 MHz) it gives up, raises
-// error flag bit 5 and applies nothing (the host API then fails loudly), so a lost predecessor cannot
-// hang the GPU and no launch is ever applied out of its partition's order.
-__device__ __forceinline__ bool hp_wait_turn(const HostPartCommon &c, int g, uint32_t seq)
-{
-    if (!c.order || threadIdx.x != 0) return true;
-    const uint64_t t0 = wall_clock64();
-    while (__hip_atomic_load(c.order + g, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != seq - 1u) {
-        __builtin_amdgcn_s_sleep(4);
-        if (wall_clock64() - t0 > 100000000ull) {   // 1 s: give up, apply nothing, tell the host
-            if (c.error_flags) atomicOr(c.error_flags, 32u);
-            __hip_atomic_store(c.flags + kPartG, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            return false;
-        }
-    }
-    return true;
 }
 
 // One launch, its headers in the kernel arguments
@@ -3323,16 +3328,7 @@ __global__ __launch_bounds__(kHpThreads) void k_hpart(HostPartLaunch p)
         L.prow[0][tid] = p.part[g][tid];
         L.prow[1][tid] = p.part[g + 1][tid];
     }
-    __shared__ int turn_ok;
-    if (tid == 0) turn_ok = hp_wait_turn(p.c, g, p.seq);
     __syncthreads();
-    if (!turn_ok) {   // out of order: nothing applied, the completion word set so no caller hangs
-        if (tid == 0) {
-            __hip_atomic_store(p.c.flags + g, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(p.c.order + g, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return;
-    }
     hp_scan(L, nb);
     __syncthreads();
     hp_partition(p.c, L, g, nb, p.seq);
@@ -3665,7 +3661,8 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     } else if (local_direct) {
         hipLaunchKernelGGL(k_local_pre<kPreHead>, dim3((unsigned)((n + kPreElems - 1) / kPreElems)), dim3(kPreThreads),
                            0, s, a);
-        hipLaunchKernelGGL(k_local_fused<2>, dim3((unsigned)((n + 31) / 32)), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((k_local_fused<2, kLfWaves>), dim3((unsigned)((n + 32 * kLfWaves - 1) / (32 * kLfWaves))),
+                           dim3(64 * kLfWaves), 0, s, a);
         // the waiting elements' count is on the device: enough workgroups for the rounds after a
         // membership change (configs[4]: ~100 K elements of keys a failed peer left INVALID), which
         // return at once when there are few

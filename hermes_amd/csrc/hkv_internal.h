@@ -104,12 +104,7 @@ struct HostPartCommon {
     unsigned int *error_flags;
     uint32_t *flags;             // device address: kPartG words, workgroup g stores seq into flags[g]
     unsigned long long *prof;    // HKV_PART_PROF: workgroup 0's phase timestamps (debug), or NULL
-    // launches on several streams: workgroup g of launch seq first waits until order[g] (device memory)
-    // is seq - 1, and stores seq there when done, so each partition's launches apply in launch order
-    // while different partitions' run side by side. NULL: stream order does it (one stream).
-    uint32_t *order;
 };
-constexpr int kPartStreams = 4;  // streams partitioned launches go round (GPU_MAX_HW_QUEUES is 4)
 struct HostPartLaunch {          // one launch, everything in the kernel arguments
     HostPartCommon c;
     uint32_t seq;

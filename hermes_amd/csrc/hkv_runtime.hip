@@ -82,7 +82,8 @@ struct CallerStage {
     // a caller returns only after its launch's flags arrived, so nothing reads the staging when its
     // thread exits. hipFree / hipHostFree synchronise the device, and the serving kernel may be busy
     // with other callers' launches for up to its lifetime limit: an exiting thread hands its buffers
-    // to a process-wide list that hkv_table_destroy frees once no serving kernel runs
+    // to a process-wide list, freed at the next quiet point (hkv_sync with no serving kernel of any table
+    // running, or hkv_table_destroy), so thread churn does not pile up pinned memory
     ~CallerStage();
 };
 static std::mutex g_stage_gy_mu;
@@ -159,18 +160,6 @@ struct hkv_table {
     // stream order, so each word only grows); pseq counts the launches
     uint32_t *pflags = nullptr, *pflags_d = nullptr;
     uint32_t pseq = 0;
-    // ... launched round the streams pstreams (HKV_PART_STREAMS, default kPartStreams), ordered per
-    // partition on the device (porder_d, HostPartCommon.order). pev[k]: the last launch on stream k;
-    // t->stream's other launches wait for all of them (part_join), and the partitioned launches after
-    // them wait for tev (recorded on t->stream when tev_gen moved past pgen[k])
-    hipStream_t pstreams[kPartStreams] = {};
-    hipEvent_t pev[kPartStreams] = {};
-    uint32_t pgen[kPartStreams] = {};
-    int n_pstreams = 0;
-    bool part_pending = false;
-    uint32_t *porder_d = nullptr;
-    hipEvent_t tev = nullptr;
-    uint32_t tev_gen = 0;
     // the serving kernel (k_hserve): launches are published in a pinned ring instead of launched
     HostRingSlot *ring = nullptr, *ring_d = nullptr;
     uint32_t *srv_words = nullptr, *srv_words_d = nullptr;   // [0] stop, [32..63] exited per workgroup
@@ -403,14 +392,10 @@ int hkv_table_create(const hkv_config *cfg, hkv_table **out)
     return 0;
 }
 
-static void part_quiesce(hkv_table *t);
-static void part_join(hkv_table *t);
-static void part_mark(hkv_table *t);
 
 int hkv_table_destroy(hkv_table *t)
 {
     if (!t) return 0;
-    part_quiesce(t);
     if (t->stream) hipStreamSynchronize(t->stream);
     hipFree(t->d_index);
     hipFree(t->d_log);
@@ -439,12 +424,6 @@ int hkv_table_destroy(hkv_table *t)
     if (t->ring_vram && t->srv_stop) (void)hipFree(t->srv_stop);
     if (t->srv_words) hipHostFree(t->srv_words);
     if (t->pflags) hipHostFree(t->pflags);
-    for (int k = 0; k < t->n_pstreams; ++k) {
-        hipStreamDestroy(t->pstreams[k]);
-        hipEventDestroy(t->pev[k]);
-    }
-    if (t->tev) hipEventDestroy(t->tev);
-    hipFree(t->porder_d);
     if (t->stream) hipStreamDestroy(t->stream);
     delete t;
     return 0;
@@ -518,7 +497,6 @@ int hkv_table_populate(hkv_table *t, int64_t n, int val_len)
     uint64_t final_head;
     pl.h0 = t->geo.log_head;
     plan_log(t->geo.log_head, t->geo.log_cap, t->geo.entry_size, t->geo.kvs_value, (uint64_t)n, pl.k, pl.hw, final_head);
-    part_quiesce(t);
     int rc = launch_populate(pl, t->stream);
     hipError_t se = hipStreamSynchronize(t->stream);
     release();
@@ -664,13 +642,31 @@ int hkv_batch_async(hkv_table *t, const hkv_batch_desc *d, void *stream)
     return 0;
 }
 
+// The staging buffers of exited caller threads, freed when no table's serving kernel runs: hipFree waits for
+// the device, and a persistent serving kernel may run for up to its 1-s lifetime (a server that starts after
+// the check only makes the free wait, as at table destruction)
+static bool srv_exited(const hkv_table *t);
+static void free_stage_graveyard_if_quiet()
+{
+    {
+        std::lock_guard<std::mutex> g(g_stage_gy_mu);
+        if (g_stage_graveyard.empty()) return;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_srv_mu);
+        for (hkv_table *u : g_srv_tables)
+            if (__atomic_load_n(&u->srv_running, __ATOMIC_ACQUIRE) && !srv_exited(u)) return;
+    }
+    free_stage_graveyard();
+}
+
 int hkv_sync(hkv_table *t, void *stream)
 {
     if (!t) return fail(-1, "null table");
     srv_stop(t);
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    part_quiesce(t);
     HIP_TRY(hipStreamSynchronize(t->stream));
+    free_stage_graveyard_if_quiet();
     return 0;
 }
 
@@ -679,7 +675,6 @@ int hkv_copy_index(hkv_table *t, void *dst, uint64_t off, uint64_t bytes)
     if (!t || !dst) return fail(-1, "null argument");
     if (off + bytes > t->cfg.num_bkts * 64) return fail(-1, "index range out of bounds");
     srv_stop(t);
-    part_quiesce(t);
     HIP_TRY(hipStreamSynchronize(t->stream));
     HIP_TRY(hipMemcpy(dst, t->d_index + off, bytes, hipMemcpyDeviceToHost));
     return 0;
@@ -690,7 +685,6 @@ int hkv_copy_log(hkv_table *t, void *dst, uint64_t off, uint64_t bytes)
     if (!t || !dst) return fail(-1, "null argument");
     if (off + bytes > t->cfg.log_cap + t->geo.entry_size) return fail(-1, "log range out of bounds");
     srv_stop(t);
-    part_quiesce(t);
     HIP_TRY(hipStreamSynchronize(t->stream));
     HIP_TRY(hipMemcpy(dst, t->d_log + off, bytes, hipMemcpyDeviceToHost));
     return 0;
@@ -923,9 +917,7 @@ static void host_launch_mixed(hkv_table *t, HostSet *set, std::unique_lock<std::
         // t->mu orders the launch against hkv_table_populate, which moves geo.log_head
         std::lock_guard<std::mutex> tl(t->mu);
         bl.g = t->geo;
-        part_join(t);
         if (launch_batch(bl, t->stream)) die("hermes_batch_ops_to_KVS (small launch)");
-        part_mark(t);
     }
     lk.lock();
     set->busy = true;
@@ -957,29 +949,6 @@ static void srv_stop_locked(hkv_table *t)
     if (hipEventSynchronize(t->srv_ev) != hipSuccess) die("serving kernel");
     srv_set_stop(t, 0u);
     t->srv_running = false;
-}
-
-// Partitioned launches go round t->pstreams; every other launch of the host API runs on t->stream.
-// part_join: t->stream waits for the partitioned launches so far; part_mark: the partitioned launches
-// after this point wait for what t->stream holds now (called after a launch on t->stream).
-static void part_join(hkv_table *t)
-{
-    if (!t->part_pending) return;
-    for (int k = 0; k < t->n_pstreams; ++k)
-        if (hipStreamWaitEvent(t->stream, t->pev[k], 0) != hipSuccess) die("stream wait");
-    t->part_pending = false;
-}
-
-static void part_mark(hkv_table *t)
-{
-    if (!t->n_pstreams) return;
-    if (hipEventRecord(t->tev, t->stream) != hipSuccess) die("event record");
-    ++t->tev_gen;
-}
-
-static void part_quiesce(hkv_table *t)
-{
-    for (int k = 0; k < t->n_pstreams; ++k) hipStreamSynchronize(t->pstreams[k]);
 }
 
 static void srv_stop(hkv_table *t)
@@ -1036,7 +1005,6 @@ static void srv_ensure(hkv_table *t)
     for (int g = 0; g < kPartG; ++g) sl.start[g] = __atomic_load_n(t->pflags + g, __ATOMIC_ACQUIRE) + 1;
     srv_set_stop(t, 0u);
     if (!t->srv_ev && hipEventCreateWithFlags(&t->srv_ev, hipEventDisableTiming) != hipSuccess) die("event");
-    part_join(t);
     if (launch_host_serve(sl, t->stream) || hipEventRecord(t->srv_ev, t->stream) != hipSuccess) die("serving kernel launch");
     t->srv_running = true;
     {
@@ -1075,24 +1043,10 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
     // One stream: launches round 4 streams, each partition's launches ordered on the device, were
     // measured (round 4) and ran 8 / 16 caller threads at 7.9-9.3 / 14.5-15.7 M local ops/s against
     // 20.4-21.0 / 34.9-36.0 M on the one table stream; that switch is gone (kept in git history)
-    constexpr int n_streams = 1;
     static const int inflight = std::min(kRingN, getenv("HKV_PART_INFLIGHT") ? std::max(1, atoi(getenv("HKV_PART_INFLIGHT")))
-                                                                              : serve ? 4 : n_streams > 1 ? 2 * n_streams : 2);
-    if (n_streams > 1 && !t->n_pstreams) {
-        for (int k = 0; k < n_streams; ++k)
-            if (hipStreamCreateWithFlags(&t->pstreams[k], hipStreamNonBlocking) != hipSuccess ||
-                hipEventCreateWithFlags(&t->pev[k], hipEventDisableTiming) != hipSuccess)
-                die("partition streams");
-        if (hipEventCreateWithFlags(&t->tev, hipEventDisableTiming) != hipSuccess ||
-            hipMalloc(&t->porder_d, 4 * kPartG) != hipSuccess || hipMemset(t->porder_d, 0, 4 * kPartG) != hipSuccess)
-            die("partition order words");
-        // the launches so far (t->stream) precede the first partitioned one
-        if (hipEventRecord(t->tev, t->stream) != hipSuccess) die("event record");
-        t->tev_gen = 1;
-        t->n_pstreams = n_streams;
-    }
+                                                                              : serve ? 4 : 2);
     if (!t->pflags) {
-        // kPartG completion words, then the order-timeout word hp_wait_turn raises (HKV_PART_STREAMS > 1)
+        // kPartG completion words (and one spare)
         if (hipHostMalloc((void **)&t->pflags, 4 * (kPartG + 1), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
             hipHostGetDevicePointer((void **)&t->pflags_d, t->pflags, 0) != hipSuccess)
             die("flag alloc");
@@ -1194,18 +1148,7 @@ static void host_launch_part(hkv_table *t, std::unique_lock<std::mutex> &lk)
         {
             std::lock_guard<std::mutex> tl(t->mu);   // against hkv_table_populate (geo.log_head)
             pl.c.g = t->geo;
-            if (t->n_pstreams) {   // round the streams; each partition's launches ordered on the device
-                const int k = (int)(seq % (uint32_t)t->n_pstreams);
-                hipStream_t ps = t->pstreams[k];
-                if (t->pgen[k] != t->tev_gen) {
-                    if (hipStreamWaitEvent(ps, t->tev, 0) != hipSuccess) die("stream wait");
-                    t->pgen[k] = t->tev_gen;
-                }
-                pl.c.order = t->porder_d;
-                if (launch_host_part(pl, ps)) die("hermes_batch_ops_to_KVS (partitioned launch)");
-                if (hipEventRecord(t->pev[k], ps) != hipSuccess) die("event record");
-                t->part_pending = true;
-            } else if (launch_host_part(pl, t->stream)) {
+            if (launch_host_part(pl, t->stream)) {
                 die("hermes_batch_ops_to_KVS (partitioned launch)");
             }
         }
@@ -1432,7 +1375,6 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
     }
     hipStream_t s = t->stream;
     set->mode = kModeEvent;
-    part_join(t);
     if (hipMemcpyAsync(set->d, set->h, total, hipMemcpyHostToDevice, s) != hipSuccess) die("copy in");
     hkv_batch_desc d;
     memset(&d, 0, sizeof d);
@@ -1454,7 +1396,6 @@ static void host_combine(hkv_table *t, std::unique_lock<std::mutex> &lk)
     }
     if (hipMemcpyAsync(set->h, set->d, total, hipMemcpyDeviceToHost, s) != hipSuccess) die("copy out");
     if (hipEventRecord(set->ev, s) != hipSuccess) die("event record");
-    part_mark(t);
     lk.lock();
     set->busy = true;
     set->refs = nb;
@@ -1569,10 +1510,6 @@ void hermes_batch_ops_to_KVS(enum hermes_batch_type_t type, uint8_t *op_array, i
     }
     const long t2 = g_host_timing ? now_ns() : 0;
     if (g_host_timing) g_hc_flagwait += t2 - tl;
-    // HKV_PART_STREAMS > 1: a workgroup that waited over 1 s for its partition's previous launch gave
-    // up without applying its elements (error bit 5): the table no longer follows any caller order
-    if (mode == kModePart && __atomic_load_n(t->pflags + kPartG, __ATOMIC_ACQUIRE))
-        die("partitioned launch gave up waiting for its partition's previous launch (error bit 5)");
     if (mode == kModePart) {
         // results from this thread's staging, back in element order; node_suspected is
         // hermes_skip_inv's, a function of the elements alone: the last membership-change INV's

@@ -167,9 +167,13 @@ typedef struct hkv_batch_desc {
                                    callbacks (hermes_worker.c:122-157) instead -- every row element of a batch
                                    whose result opcode is not ACK_SUCCESS, MEMBERSHIP_CHANGE or EMPTY is copied
                                    to d_ack_out + (r * row_stride + j) * 16 with opcode ST_OP_VAL and sender =
-                                   this machine (val_copy_and_modify_elem), every other position there gets
-                                   opcode ST_EMPTY, and every non-empty element leaves with opcode ST_EMPTY
-                                   (val_skip_or_get_sender_id, val_modify_elem_after_send); ack_out_size 16 */
+                                   this machine (val_copy_and_modify_elem), every other live position there
+                                   gets opcode ST_EMPTY, and every non-empty element leaves with opcode
+                                   ST_EMPTY (val_skip_or_get_sender_id, val_modify_elem_after_send);
+                                   ack_out_size 16. Live positions are those of a batch's range in a row other
+                                   than skip_row: the positions of skip_row and those past the last batch's
+                                   end are not written (they keep what the buffer held), so a caller reads
+                                   only live positions */
     uint32_t ack_out_size;
     const uint64_t *d_phys;     /* reserved, must be NULL (ABI 8; ABI 7: located entries that skipped the
                                    bucket read the reference makes, never the default, removed) */

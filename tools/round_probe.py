@@ -92,7 +92,9 @@ def main():
             line["audit"] = r.audit_rounds(3)
             c_prev = r.fold_counters()[:5].clone()
         print(json.dumps(line), flush=True)
-    assert kvs.take_error_flags() == 0
+    flags = kvs.take_error_flags()
+    # under the timing modes (HKV_DBG, a -DHKV_DEBUG_MODES build) skipped work raises flags by design
+    assert flags == 0 or os.environ.get("HKV_DBG"), flags
 
 
 if __name__ == "__main__":

@@ -64,7 +64,7 @@ def main():
         # the round, with its refill held back so the end-of-round states can be read
         t0 = time.perf_counter()
         refill = r.refill
-        r.refill = lambda first=False: None
+        r.refill = lambda *args, **kw: None
         r.step()
         r.refill = refill
         torch.cuda.synchronize()

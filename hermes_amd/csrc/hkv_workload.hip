@@ -488,15 +488,32 @@ __device__ __forceinline__ void wave_ranks(const unsigned long long *b, int lane
 #else
 #define HKV_PLAN_SGPR_ATTR
 #endif
+struct PlanArgs {   // hkv_wl_refill_plan's arguments
+    uint8_t *states;
+    int32_t n_workers, stride;
+    uint32_t st_value, shift;
+    const uint64_t *tkey;
+    const uint8_t *top;
+    int32_t tlen;
+    uint32_t *cursor;
+    uint32_t machine_id, flags;
+    unsigned long long *counters;
+    uint8_t *opc, *patch;
+};
+// (block bx of the plan's grid; every lane of a wave calls it)
 template <int WPW>
-__global__ __launch_bounds__(256) HKV_PLAN_SGPR_ATTR void k_refill_plan_w(uint8_t *states, int32_t n_workers, int32_t stride,
-                                                       uint32_t st_value, uint32_t shift, const uint64_t *tkey,
-                                                       const uint8_t *top, int32_t tlen, uint32_t *cursor,
-                                                       uint32_t machine_id, uint32_t flags,
-                                                       unsigned long long *counters, uint8_t *opc, uint8_t *patch)
+__device__ __forceinline__ void refill_plan_body(const PlanArgs &pa, int bx)
 {
+    uint8_t *states = pa.states;
+    const int32_t n_workers = pa.n_workers, stride = pa.stride, tlen = pa.tlen;
+    const uint32_t st_value = pa.st_value, shift = pa.shift, machine_id = pa.machine_id, flags = pa.flags;
+    const uint64_t *tkey = pa.tkey;
+    const uint8_t *top = pa.top;
+    uint32_t *cursor = pa.cursor;
+    unsigned long long *counters = pa.counters;
+    uint8_t *opc = pa.opc, *patch = pa.patch;
     const int lane = threadIdx.x & 63;
-    const int wb = (blockIdx.x * 4 + (int)(threadIdx.x >> 6)) * WPW;
+    const int wb = (bx * 4 + (int)(threadIdx.x >> 6)) * WPW;
     if (wb >= n_workers) return;
     uint8_t st[WPW][4];
     uint32_t base[WPW];
@@ -574,6 +591,12 @@ __global__ __launch_bounds__(256) HKV_PLAN_SGPR_ATTR void k_refill_plan_w(uint8_
             *reinterpret_cast<W16 *>(patch + e * 16) = p;
         }
     }
+}
+
+template <int WPW>
+__global__ __launch_bounds__(256) HKV_PLAN_SGPR_ATTR void k_refill_plan_w(PlanArgs pa)
+{
+    refill_plan_body<WPW>(pa, blockIdx.x);
 }
 
 // k_refill_direct from the state mirror (hkv_wl_refill_st: big ops refilled in place), one wave per
@@ -1691,14 +1714,26 @@ __global__ __launch_bounds__(256) void k_peer_locate(TableView t, const uint8_t 
 
 // k_peer_ts for located INVs (one thread each): the key is checked at the entry, and an INV
 // whose entry does not hold its key any more takes the full lookup
-// inv_at (may be NULL): INV g sits at element inv_at[g] of invs (a rows layout, hkv_wl_peer_ts_rows)
-__global__ __launch_bounds__(256) void k_peer_ts_at(TableView t, uint8_t *invs, uint8_t *vals, const uint64_t *phys_in,
-                                                    int64_t total, uint32_t op_size, unsigned long long *peer_ts,
-                                                    uint32_t round, const int64_t *inv_at)
+struct PeerTsArgs {   // hkv_wl_peer_ts_at's arguments
+    TableView t;
+    uint8_t *invs, *vals;
+    const uint64_t *phys_in;
+    int64_t total;
+    uint32_t op_size;
+    unsigned long long *peer_ts;
+    uint32_t round;
+};
+__device__ __forceinline__ void peer_ts_at_body(const PeerTsArgs &pt, int bx)
 {
-    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const TableView &t = pt.t;
+    uint8_t *invs = pt.invs, *vals = pt.vals;
+    const uint64_t *phys_in = pt.phys_in;
+    const int64_t total = pt.total;
+    const uint32_t op_size = pt.op_size, round = pt.round;
+    unsigned long long *peer_ts = pt.peer_ts;
+    const int64_t g = (int64_t)bx * 256 + threadIdx.x;
     if (g >= total) return;
-    uint8_t *x = invs + (inv_at ? inv_at[g] : g) * op_size;
+    uint8_t *x = invs + g * op_size;
     // every load that does not need the entry first: INV header, flags, location and the VAL's header
     uint8_t *vv = vals + g * kOpMetaSize;
     const uint64_t key = *reinterpret_cast<const uint64_t *>(x);
@@ -1736,6 +1771,18 @@ __global__ __launch_bounds__(256) void k_peer_ts_at(TableView t, uint8_t *invs, 
     const uint64_t nh = (h8 & 0xFFFFFF00ull & 0xFFFFFFFFull) | kOpInv | ((uint64_t)ver << 32);
     *reinterpret_cast<uint64_t *>(x + 8) = nh;
     *reinterpret_cast<uint64_t *>(vv + 8) = (vh & 0xFFFFFF00ull & 0xFFFFFFFFull) | kOpVal | ((uint64_t)ver << 32);
+}
+
+__global__ __launch_bounds__(256) void k_peer_ts_at(PeerTsArgs pt) { peer_ts_at_body(pt, blockIdx.x); }
+
+// The refill plan of this round and the virtual peers' timestamps of the next, in one launch (round 6): both
+// run between a round's VAL batch and the next local launch, touch disjoint data (op mirrors and patches; the
+// peers' slabs, reading the table) and are bound by dependent loads, so side by side in one grid they overlap
+// and the launch boundary between them goes. Blocks [0, plan_blocks) plan, the rest take timestamps.
+__global__ __launch_bounds__(256) HKV_PLAN_SGPR_ATTR void k_plan_peer_ts(PlanArgs pa, PeerTsArgs pt, int plan_blocks)
+{
+    if ((int)blockIdx.x < plan_blocks) refill_plan_body<2>(pa, blockIdx.x);
+    else peer_ts_at_body(pt, (int)blockIdx.x - plan_blocks);
 }
 
 }  // namespace hkv
@@ -1816,9 +1863,9 @@ int hkv_wl_refill_plan(uint8_t *states, int32_t n_workers, int32_t stride, uint3
     if (stride > 256 || n_workers <= 0 || tlen <= 0 || !states || !opc || !patch) return -1;
     if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET)) return -1;   // no hot-request coalescing
     if (((uintptr_t)patch & 15) || (st_value >> shift) > 255) return -1;   // val_len: a byte
-    hipLaunchKernelGGL(k_refill_plan_w<2>, dim3((unsigned)((n_workers + 7) / 8)), dim3(256), 0, (hipStream_t)stream,
-                       states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags,
-                       counters, opc, patch);
+    const PlanArgs pa{states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags, counters, opc,
+                      patch};
+    hipLaunchKernelGGL(k_refill_plan_w<2>, dim3((unsigned)((n_workers + 7) / 8)), dim3(256), 0, (hipStream_t)stream, pa);
     return ok();
 }
 
@@ -2164,8 +2211,33 @@ int hkv_wl_peer_ts_at(hkv_table *t, uint8_t *invs, uint8_t *vals, const uint64_t
     TableView tv;
     if (table_view(t, &tv) || n < 0 || op_size % 8) return -1;
     if (n == 0) return 0;
-    hipLaunchKernelGGL(k_peer_ts_at, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, tv, invs, vals, phys, n,
-                       op_size, peer_ts, round, (const int64_t *)nullptr);
+    const PeerTsArgs pt{tv, invs, vals, phys, n, op_size, peer_ts, round};
+    hipLaunchKernelGGL(k_peer_ts_at, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, pt);
+    return ok();
+}
+
+int hkv_wl_refill_plan_peer_ts(uint8_t *states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
+                               const uint64_t *tkey, const uint8_t *top, int32_t tlen, uint32_t *cursor,
+                               uint32_t machine_id, uint32_t flags, unsigned long long *counters, uint8_t *opc,
+                               uint8_t *patch, hkv_table *t, uint8_t *invs, uint8_t *vals, const uint64_t *phys, int64_t n,
+                               uint32_t op_size, unsigned long long *peer_ts, uint32_t round, void *stream)
+{
+    if (stride > 256 || n_workers <= 0 || tlen <= 0 || !states || !opc || !patch) return -1;
+    if (flags & ~(uint32_t)(HKV_WL_REFILL_ALL | HKV_WL_READ_TS_RESET)) return -1;
+    if (((uintptr_t)patch & 15) || (st_value >> shift) > 255) return -1;
+    TableView tv;
+    if (table_view(t, &tv) || n < 0 || op_size % 8) return -1;
+    const PlanArgs pa{states, n_workers, stride, st_value, shift, tkey, top, tlen, cursor, machine_id, flags, counters, opc,
+                      patch};
+    const PeerTsArgs pt{tv, invs, vals, phys, n, op_size, peer_ts, round};
+    const int plan_blocks = (n_workers + 7) / 8;
+#ifdef HKV_PLAN_PTS_SPLIT   // (a build macro for A/B: the two launches of before)
+    hipLaunchKernelGGL(k_refill_plan_w<2>, dim3((unsigned)plan_blocks), dim3(256), 0, (hipStream_t)stream, pa);
+    if (n) hipLaunchKernelGGL(k_peer_ts_at, dim3(blocks_for(n)), dim3(256), 0, (hipStream_t)stream, pt);
+#else
+    hipLaunchKernelGGL(k_plan_peer_ts, dim3((unsigned)plan_blocks + blocks_for(n)), dim3(256), 0, (hipStream_t)stream, pa,
+                       pt, plan_blocks);
+#endif
     return ok();
 }
 

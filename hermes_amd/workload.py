@@ -71,6 +71,9 @@ _L.hkv_wl_ack_offsets.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, _P, _P, ct
 _L.hkv_wl_pack_rows.argtypes = [_P, _P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _P, _P, _P]
 _L.hkv_wl_peer_locate.argtypes = [_P, _P, ctypes.c_int64, ctypes.c_uint32, _P, _P]
 _L.hkv_wl_peer_ts_at.argtypes = [_P, _P, _P, _P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
+_L.hkv_wl_refill_plan_peer_ts.argtypes = [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, _P, _P,
+                                          ctypes.c_int32, _P, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _P, _P, _P,
+                                          _P, ctypes.c_int64, ctypes.c_uint32, _P, ctypes.c_uint32, _P]
 _L.hkv_wl_peer_ts_words.restype = ctypes.c_uint64
 _L.hkv_wl_peer_ts_words.argtypes = [_P]
 
@@ -357,6 +360,7 @@ class Round:
             self._hades_start()
         self._gen_remote()
         self.audit: CommitAudit | None = None   # audit_rounds(): per-outcome commit breakdown (untimed)
+        self._pts_done = None          # (clock, live peers) whose virtual-peer timestamps the last refill took
         self.refill(first=True)
 
     def _gen_remote(self):
@@ -408,7 +412,22 @@ class Round:
         del scratch
 
     # -- pieces of one round
-    def refill(self, first: bool = False):
+    def refill(self, first: bool = False, next_round: bool = False):
+        """refill_ops for the next round. next_round (the end of Round.step, clock already advanced): the
+        plan and the next round's virtual-peer timestamps in one launch (hkv_wl_refill_plan_peer_ts), which
+        the next step then does not repeat."""
+        if self.fused and not first and next_round and self.pack_remote and self.R and self.alive:
+            k = self.clock % max(len(self.remote_inv), 1)
+            pi, pv, _, _, phys, _ = self.remote_packed[k]
+            total = self._packed_total(k, self.alive)
+            check(_L.hkv_wl_refill_plan_peer_ts(_ptr(self.states), self.W, self.LOCAL, self.sizes.st_value,
+                                                self.sizes.shift, _ptr(self.trace_key), _ptr(self.trace_op),
+                                                self.trace_len, _ptr(self.cursor), self.machine_id, self.rflags,
+                                                _ptr(self.counters), _ptr(self.opcodes), _ptr(self.patch), self.kvs.h,
+                                                _ptr(pi), _ptr(pv), _ptr(phys), total, self.op, _ptr(self.peer_ts),
+                                                self.clock, _s()), "refill_plan_peer_ts")
+            self._pts_done = (self.clock, self.alive)
+            return
         if self.fused and not first:   # a plan the next local launch applies (the ops stay as they are)
             check(_L.hkv_wl_refill_plan(_ptr(self.states), self.W, self.LOCAL, self.sizes.st_value, self.sizes.shift,
                                         _ptr(self.trace_key), _ptr(self.trace_op), self.trace_len, _ptr(self.cursor),
@@ -610,7 +629,8 @@ class Round:
         # the packed slabs (same elements, same order): the live peers are their first `alive` peers (a
         # failed peer is always the last live one), so after a failure the rounds apply a prefix of them
         packed = self.pack_remote
-        if self.R and sent:
+        pts_done, self._pts_done = self._pts_done == (self.clock, sent), None
+        if self.R and sent and not pts_done:   # (the last refill may have taken them already)
             if packed:
                 self.peer_timestamps_packed(k, sent)
             else:
@@ -684,8 +704,8 @@ class Round:
             self.membership_change(drop)
         if self.audit is not None:
             self.audit.end()
-        self.refill()
         self.clock += 1
+        self.refill(next_round=True)
 
     def _slot_counts(self, k: int, n_peers: int):
         """Per-worker counts applying the first n_peers peers' elements of round index k's

@@ -155,6 +155,15 @@ int hkv_wl_peer_locate(hkv_table *t, const uint8_t *d_invs, int64_t n, uint32_t 
                        void *stream);
 int hkv_wl_peer_ts_at(hkv_table *t, uint8_t *d_invs, uint8_t *d_vals, const uint64_t *d_phys, int64_t n,
                       uint32_t op_size, unsigned long long *d_peer_ts, uint32_t round, void *stream);
+/* hkv_wl_refill_plan and hkv_wl_peer_ts_at in one launch (round 6): the refill plan that ends a round and the
+ * virtual peers' timestamps that start the next touch disjoint data, so one grid runs both side by side.
+ * Same arguments and results as the two calls in that order. */
+int hkv_wl_refill_plan_peer_ts(uint8_t *d_states, int32_t n_workers, int32_t stride, uint32_t st_value, uint32_t shift,
+                               const uint64_t *d_trace_key, const uint8_t *d_trace_op, int32_t trace_len,
+                               uint32_t *d_cursor, uint32_t machine_id, uint32_t flags,
+                               unsigned long long *d_counters, uint8_t *d_opcode, uint8_t *d_patch, hkv_table *t,
+                               uint8_t *d_invs, uint8_t *d_vals, const uint64_t *d_phys, int64_t n, uint32_t op_size,
+                               unsigned long long *d_peer_ts, uint32_t round, void *stream);
 /* The virtual peers' answers to this round's INVs: for INV j of worker w, the ack_size-byte
  * element d_acks[w*out_stride + j*n_peers + r] from peer_ids[r] is an ACK {key, ST_OP_ACK,
  * sender, ts = inv ts} (ack_copy_and_modify_elem, hermes_worker.c:100-118) -- or, with d_peer_ts

@@ -249,7 +249,7 @@ def test_rmw_semantics_invariant_cfg3():
     rmws, writes = {}, {}
     refill = r.refill
 
-    def recording_refill(first=False):
+    def recording_refill(*args, **kw):
         ops = r.ops.view(-1, op).cpu().numpy()
         st = ops[:, 9]
         for kind, code in (("rmw", int(L.Resp.RMW_COMPLETE)), ("put", int(L.Resp.PUT_COMPLETE))):
@@ -257,7 +257,7 @@ def test_rmw_semantics_invariant_cfg3():
                 key = int(x[:8].view(np.uint64)[0])
                 ver, cid = int(x[12:16].view(np.uint32)[0]), int(x[11])
                 (rmws if kind == "rmw" else writes).setdefault(key, []).append((ver, cid))
-        refill(first)
+        refill(*args, **kw)
     r.refill = recording_refill
     for _ in range(8):
         r.step()

@@ -107,6 +107,9 @@ def parse():
     p.add_argument("--coalesce-hot", action="store_true",
                    help="refill_ops' ENABLE_COALESCE_OF_HOT_REQS: requests on the 100 hottest ids join the worker's "
                         "live op of that id (committed ops count them)")
+    p.add_argument("--inplace-refill", action="store_true",
+                   help="N=1: refill the ops in place (hkv_wl_refill_st / hkv_wl_refill) instead of planning patches "
+                        "that the next local launch writes into the ops (hkv_wl_refill_plan, the default)")
     p.add_argument("--policy-steps", "--retry-steps", type=int, default=10, dest="policy_steps",
                    help="N=1: also time this many steps of each other refill policy on the same table and "
                         "report them under detail.policies (0 = skip)")
@@ -225,7 +228,8 @@ def main():
         rnd = Round(kvs, a.workers, L.membership(machines, 0), list(range(1, machines)), z, a.write_permille,
                     a.rmw_permille, seed=a.seed,
                     max_steps=total_steps + 2, retry_stalled=retry, fit_ack_stride=not a.no_fit_acks,
-                    val_credits=a.val_credits, hades=cfg5, coalesce_hot=a.coalesce_hot)
+                    val_credits=a.val_credits, hades=cfg5, coalesce_hot=a.coalesce_hot,
+                    fused_refill=False if a.inplace_refill else None)
     torch.cuda.synchronize()
 
     for _ in range(a.warmup):

@@ -97,6 +97,9 @@ struct BatchArgs {
     uint8_t *state_out;          // local launches: each element's final state byte (may be NULL)
     const uint8_t *opc;          // local launches: the caller's opcode mirror (may be NULL, see k_local_pre)
     const uint8_t *patch;        // local direct path: pending header writes (hkv_batch_desc.d_patch), or NULL
+    uint64_t *hx;                // big local launches with patches (patch_in_resolve): [2 n] each patched element's
+                                 // header word (bytes 8..15) as patched and its op's last 8-byte word, from
+                                 // k_lookup for k_resolve0_direct; NULL otherwise
     uint8_t *rws;                // ACK launches: read_write_ops state mirror (hkv_batch_desc.d_rw_state), or NULL
     const uint8_t *rwo;          // ACK launches: read_write_ops opcode mirror (hkv_batch_desc.d_opcode_in), or NULL
     int32_t n_rows, skip_row;    // HKV_BATCH_ROWS: rows applied in order (k_unique_rows), one skipped (-1: none)
@@ -143,7 +146,12 @@ __device__ __forceinline__ Meta after_first(const BatchArgs &a, const Meta &m0, 
     Meta m1 = m0;
     m_set_state(m1, absorbing_state<TYPE>());
     if (TYPE != kLocal || a.g.skew == 0) return m1;
-    if (f_is_put || a.elems[(int64_t)f * a.esz + 8] != kOpGet) {
+    uint8_t foc = f_is_put ? (uint8_t)kOpPut : a.elems[(int64_t)f * a.esz + 8];
+    if (a.hx && !f_is_put) {   // patch_in_resolve: F's op may not be patched yet (its patch is valid at byte 14)
+        const uint64_t pb = *reinterpret_cast<const uint64_t *>(a.patch + (int64_t)f * 16 + 8);
+        if ((pb >> 48) & 0xFFu) foc = (uint8_t)pb;
+    }
+    if (foc != kOpGet) {
         m1.ver += 2;
         m_set_cid(m1, (uint8_t)a.g.machine_id);
     } else {
@@ -373,7 +381,7 @@ __device__ __forceinline__ void apply_to_shadow(const BatchArgs &a, uint8_t *x, 
 __device__ __forceinline__ void wave_block_copies(uint8_t *dst, const uint8_t *src, uint32_t bytes);
 template <int TYPE, int SV>
 __device__ __forceinline__ void apply_to_shadow_wave(const BatchArgs &a, bool cand, uint32_t i, const uint8_t *src,
-                                                     VCopy &vc)
+                                                     VCopy &vc, uint8_t *xl = nullptr, bool use_xl = false)
 {
     uint8_t *sh = cand ? shadow_of(a, i) : nullptr;
     wave_block_copies(sh, src, a.g.entry_size);
@@ -386,7 +394,8 @@ __device__ __forceinline__ void apply_to_shadow_wave(const BatchArgs &a, bool ca
     uint8_t *xg;
     uint8_t idx;
     elem_at(a, i, xg, idx, c);
-    dispatch<SV>(TYPE, xg, sh, idx, m, c);
+    if (use_xl) dispatch<SV>(TYPE, xl, sh, idx, m, c);   // xl: the element's patched copy (k_resolve0_direct)
+    else dispatch<SV>(TYPE, xg, sh, idx, m, c);
     meta_store(sh, m);
 }
 
@@ -517,20 +526,37 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
     }
     const bool vals_direct = a.type == kVals;
     int64_t gi[P];
-    uint64_t key[P], hdr[P];
+    uint64_t key[P], hdr[P], tail[P];
     int probe[P];
+    bool patched[P];
 #pragma unroll
     for (int k = 0; k < P; ++k) {
         gi[k] = i_begin + ((int64_t)blockIdx.x * P + k) * 64 + (threadIdx.x >> 2);
         uint64_t kk = 0, hh = 0;
         int p = 0;
+        patched[k] = false;
+        tail[k] = 0;
         if (gi[k] < i_end && q == 0) {
             const int32_t b = (int32_t)(gi[k] / a.stride);
             const int32_t idx = (int32_t)(gi[k] - (int64_t)b * a.stride);
-            if (a.counts == nullptr || idx < a.counts[b]) {
-                const U64x2 h = *reinterpret_cast<const U64x2 *>(a.elems + gi[k] * a.esz);
-                kk = h.a;
-                hh = h.b;
+            const bool counted = a.counts == nullptr || idx < a.counts[b];
+            if (a.hx) {
+                // patch_in_resolve: the element as its patch makes it (k_resolve0_direct writes the op), and
+                // its op's last word -- on the line of the next op's header, which the next lane group reads
+                const uint8_t *x = a.elems + gi[k] * a.esz;
+                const U64x2 h = *reinterpret_cast<const U64x2 *>(x);
+                const U64x2 pt = *reinterpret_cast<const U64x2 *>(a.patch + gi[k] * 16);
+                tail[k] = *reinterpret_cast<const uint64_t *>(x + a.esz - 8);
+                patched[k] = patch_valid(pt.b);
+                kk = patched[k] ? pt.a : h.a;
+                hh = patched[k] ? patched_hdr(h.b, pt.b) : h.b;
+            }
+            if (counted) {
+                if (!a.hx) {
+                    const U64x2 h = *reinterpret_cast<const U64x2 *>(a.elems + gi[k] * a.esz);
+                    kk = h.a;
+                    hh = h.b;
+                }
                 if (skip_elem_os(a.type, (uint8_t)hh, (uint8_t)(hh >> 8))) {
                     if (a.type == kInvs && a.ns_idx) {
                         int64_t start;  // packed: a search, for the rare membership-change INVs only
@@ -641,7 +667,12 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                 }
             }
         }
-        if (probe[k] && e == kNone) x[9] = kMiss;
+        if (patched[k]) {   // k_resolve0_direct writes the op's header from this word
+            const uint64_t h = probe[k] && e == kNone ? (hdr[k] & ~0xFF00ull) | ((uint64_t)kMiss << 8) : hdr[k];
+            *reinterpret_cast<U64x2 *>(a.hx + 2 * gi[k]) = U64x2{h, tail[k]};
+        } else if (probe[k] && e == kNone) {
+            x[9] = kMiss;
+        }
         a.ent[gi[k]] = e;
         if (a.inv_direct || a.ack_direct) a.st[gi[k]] = ifl;
     }
@@ -1097,10 +1128,12 @@ __device__ __forceinline__ void wave_value_words_n(const VCopy &v, uint32_t n)
     while (todo) {
         uint8_t *dp[VB];
         const uint8_t *sp[VB];
+        uint32_t fl[VB];
 #pragma unroll
         for (int u = 0; u < VB; ++u) {
             dp[u] = nullptr;
             sp[u] = nullptr;
+            fl[u] = 0;
             if (todo) {
                 const int j = __ffsll((long long)todo) - 1;
                 todo &= todo - 1;
@@ -1110,6 +1143,7 @@ __device__ __forceinline__ void wave_value_words_n(const VCopy &v, uint32_t n)
                                    ((uint64_t)(uint32_t)__shfl((int)(uint32_t)((uintptr_t)v.src >> 32), j, 64) << 32);
                 dp[u] = reinterpret_cast<uint8_t *>(d);
                 sp[u] = reinterpret_cast<const uint8_t *>(s);
+                fl[u] = (uint32_t)__shfl((int)v.fill, j, 64);
             }
         }
         uint64_t w[VB];
@@ -1120,7 +1154,8 @@ __device__ __forceinline__ void wave_value_words_n(const VCopy &v, uint32_t n)
             const uintptr_t ab = (s - d0) & ~(uintptr_t)7;
             const uintptr_t wa = ab + 8u * lane;
             w[u] = 0;
-            if (sp[u] && wa + 8 > s && wa < s + n) w[u] = *reinterpret_cast<const uint64_t *>(wa);
+            if (fl[u]) w[u] = 0x0101010101010101ull * (uint8_t)fl[u];   // every word (any shift of it is itself)
+            else if (sp[u] && wa + 8 > s && wa < s + n) w[u] = *reinterpret_cast<const uint64_t *>(wa);
         }
 #pragma unroll
         for (int u = 0; u < VB; ++u) {
@@ -1209,12 +1244,35 @@ __device__ __forceinline__ void wave_block_copies(uint8_t *dst, const uint8_t *s
     }
 }
 
+// patch_in_resolve (big local launches with refill patches, a.hx set; launch_batch): k_lookup read each
+// patch beside the op's header, so a patched element runs its exec function on a copy of its op's first 24
+// bytes in LDS -- key and header word as patched (k_lookup), flags from the patch -- and this pass writes the
+// op once: its header from the copy, a write's value fill (a copy with no source to load), the GET values
+// the exec functions copy, and the pad bytes after the value from the op's last word (k_lookup), so the op's
+// 64-byte blocks are written whole (a block written with holes costs HBM a read-modify-write:
+// tools/write_bench.hip). The refill's own pass over the slab (k_refill_st_w) goes, and this pass reads
+// no op line: the header came with k_lookup's read, a write's value is the patch's fill byte.
 template <int TYPE, int SV>
 __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
 {
+    constexpr bool kPir = TYPE == kLocal && SV != 31;
+    __shared__ uint64_t sop[kPir ? 256 * 3 : 1];
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const bool in = i < a.n;
     const uint32_t e = in ? a.ent[i] : kNone;
+    U64x2 pt{0, 0}, hw{0, 0};
+    if (kPir && a.hx && in) {   // beside the entry id: one trip
+        pt = *reinterpret_cast<const U64x2 *>(a.patch + i * 16);
+        hw = *reinterpret_cast<const U64x2 *>(a.hx + 2 * i);
+    }
+    const bool pd = kPir && a.hx && in && patch_valid(pt.b);
+    const uint32_t fb = (uint32_t)(pt.b >> 32) & 0xFFu;   // a patched element's value fill byte (0: none)
+    uint64_t *cop = &sop[kPir ? threadIdx.x * 3 : 0];
+    if (pd) {
+        cop[0] = pt.a;
+        cop[1] = hw.a;
+        cop[2] = ((pt.b >> 16) & 0xFFFFull) | (fb ? (0x0101010101010101ull * fb) << 16 : 0ull);
+    }
     uint8_t st = kStDone;
     uint8_t *xg = nullptr;
     uint8_t idx = 0;
@@ -1228,32 +1286,70 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
     const bool wave_shadow = SV != 31 && a.g.st_value <= 320;
     bool cand = false;
     if (in) elem_at(a, (uint32_t)i, xg, idx, c);
+    // the op the exec functions see: the LDS copy of a patched one, else the op (two calls, so each keeps
+    // its address space instead of flat accesses)
+    uint8_t *xl = reinterpret_cast<uint8_t *>(cop);
     if (e != kNone) {
         Meta m;
         meta_load(entry_of(a, e), m);
         const uint32_t f = (uint8_t)(m.w5 >> 16) == a.ltag ? first_cand(*fw_of(a, e), a.rtag0) : kNone;
-        if (f == kNone || (uint32_t)i < f) {
-            Meta tm = m;
-            dispatch<SV>(TYPE, xg, entry_of(a, e), idx, tm, c);
-            if (a.error_flags && !meta_equal(tm, m)) atomicOr(a.error_flags, 1u);
+        if (f == kNone || (uint32_t)i < f || ((uint32_t)i > f && a.rounds == 0)) {
+            const Meta m0 = (f == kNone || (uint32_t)i < f) ? m : after_first<TYPE>(a, m, f, 0);
+            Meta tm = m0;
+            if (pd) dispatch<SV>(TYPE, xl, entry_of(a, e), idx, tm, c);
+            else dispatch<SV>(TYPE, xg, entry_of(a, e), idx, tm, c);
+            if (a.error_flags && !meta_equal(tm, m0)) atomicOr(a.error_flags, 1u);
         } else if ((uint32_t)i == f) {
             if (wave_shadow) cand = true;
             else apply_to_shadow<TYPE, SV>(a, nullptr, (uint32_t)i, entry_of(a, e));
             st = kStCommit;
-        } else if (a.rounds == 0) {
-            const Meta m1 = after_first<TYPE>(a, m, f, 0);
-            Meta tm = m1;
-            dispatch<SV>(TYPE, xg, entry_of(a, e), idx, tm, c);
-            if (a.error_flags && !meta_equal(tm, m1)) atomicOr(a.error_flags, 1u);
         } else {
             a.pf[i] = f;
             st = kStPend;
         }
     }
-    if (wave_shadow) apply_to_shadow_wave<TYPE, SV>(a, cand, (uint32_t)i, cand ? entry_of(a, e) : nullptr, vc);
+    if (wave_shadow) apply_to_shadow_wave<TYPE, SV>(a, cand, (uint32_t)i, cand ? entry_of(a, e) : nullptr, vc, xl, pd);
+    bool whole = false;   // a patched op whose every byte is known here: written whole by its lane
+    if (pd) {
+        uint8_t *cv = reinterpret_cast<uint8_t *>(cop) + kOpValueOff;
+        if (vc.dst == cv) vc.dst = xg + kOpValueOff;
+        if (vc.src == cv) {
+            vc.src = fb ? nullptr : xg + kOpValueOff;
+            vc.fill = fb ? 0x100u | fb : 0u;
+        }
+        whole = fb && vc.dst != xg + kOpValueOff;   // (a value the exec copies into the op replaces the fill)
+    }
     if (SV != 31) wave_value_copies(vc, a.g.st_value, kVcBatch);
     if (!in) return;
     a.st[i] = st;
+    if (pd) {
+        const uint64_t h0 = cop[0], h1 = cop[1], h2 = cop[2];
+        const uint32_t vend = kOpValueOff + a.g.st_value, w0 = (uint32_t)a.esz - 8u;
+        if (whole) {
+            // key, header, flags, the value fill and the pad after it (launch_batch: at most 8 bytes, in
+            // the op's last word), 16 bytes a store, back to back, so every 64-byte block of the op is
+            // complete in L2 before it goes to HBM
+            const uint64_t pat = 0x0101010101010101ull * fb;
+            const uint32_t nlow = vend - w0;   // value bytes in the last word
+            const uint64_t lmask = nlow >= 8 ? ~0ull : (1ull << (8 * nlow)) - 1ull;
+            const uint64_t lastw = (pat & lmask) | (hw.b & ~lmask);
+            const uint32_t nw = (uint32_t)a.esz / 8u;
+            auto word = [&](uint32_t k) {
+                return k == 0 ? h0 : k == 1 ? h1 : k == 2 ? ((h2 & 0xFFFFull) | (pat << 16)) : k == nw - 1 ? lastw : pat;
+            };
+            uint32_t k = 0;
+            for (; k + 2 <= nw; k += 2) *reinterpret_cast<U64x2 *>(xg + 8 * k) = U64x2{word(k), word(k + 1)};
+            if (k < nw) *reinterpret_cast<uint64_t *>(xg + 8 * k) = word(k);
+        } else {   // the header from the copy, then the pad bytes after the value
+            uint64_t *o = reinterpret_cast<uint64_t *>(xg);
+            o[0] = h0;
+            o[1] = h1;
+            *reinterpret_cast<uint16_t *>(xg + 16) = (uint16_t)h2;
+            if (vend < (uint32_t)a.esz) store_word_part(xg + w0, hw.b, vend - w0, 8u);
+        }
+        if (a.state_out) a.state_out[i] = (uint8_t)(h1 >> 8);
+        return;
+    }
     note_state(a, i, xg);
 #if HKV_FULL_HDR
     // the op's first three and last 8-byte words stored again as they now stand, so that with the value a
@@ -3546,7 +3642,7 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t batch_scratch_bytes(int64_t cap, uint32_t entry_size)
 {
-    return align256(4 * (size_t)cap) * 3 + align256((size_t)cap) + align256(16 * (size_t)cap) + 256 +
+    return align256(4 * (size_t)cap) * 3 + align256((size_t)cap) + align256(16 * (size_t)cap) * 2 + 256 +
            align256((size_t)entry_size * (size_t)cap);
 }
 
@@ -3565,6 +3661,7 @@ void batch_carve(BatchLaunch &bl, uint8_t *base, int64_t cap, uint32_t entry_siz
     bl.pf = reinterpret_cast<uint32_t *>(take(4 * (size_t)cap));
     bl.shadow = take((size_t)entry_size * (size_t)cap);
     bl.ctr = reinterpret_cast<uint32_t *>(take(256));
+    bl.hx = reinterpret_cast<uint64_t *>(take(16 * (size_t)cap));
     bl.cap = (uint32_t)cap;
 }
 
@@ -3583,6 +3680,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.state_out = (bl.type == kLocal || bl.type == kLocalAfterMemb) ? bl.state_out : nullptr;
     a.opc = bl.type == kLocal ? bl.opcode_in : nullptr;
     a.patch = nullptr;
+    a.hx = nullptr;
     a.ack_out = bl.type == kInvs || (bl.type == kAcks && bl.n_rows > 0) ? bl.ack_out : nullptr;
     a.ack_out_size = bl.ack_out_size;
     a.n_rows = bl.n_rows;
@@ -3650,7 +3748,17 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     // local batches without RMWs in the default layout: the direct path (k_local_pre, k_local_fused)
     const bool local_direct = bl.type == kLocal && !bl.g.rmw_enabled && bl.esz == 56 && bl.g.st_value == 31 &&
                               bl.g.entry_size == 64 && !bl.offsets;
-    if (bl.patch && (small || !local_direct)) {  // the other paths take the patches as op writes first
+    // big local launches on the rounds engine (configs[2]): k_lookup reads the patches, k_resolve0_direct writes
+    // the patched ops (patch_in_resolve, see there): values of at most 320 bytes, the op's pad after its value
+    // within its last 8-byte word
+    const uint32_t vend = (uint32_t)kOpValueOff + bl.g.st_value;
+    const bool patch_in_resolve = bl.patch && !small && !local_direct && bl.type == kLocal && big && big_direct &&
+                                  !bl.offsets && bl.g.st_value != 31 && bl.g.st_value <= 320 && bl.esz % 8 == 0 &&
+                                  (uint32_t)bl.esz >= vend && (uint32_t)bl.esz <= vend + 8;
+    if (patch_in_resolve) {
+        a.patch = bl.patch;
+        a.hx = bl.hx;
+    } else if (bl.patch && (small || !local_direct)) {  // the other paths take the patches as op writes first
         hipLaunchKernelGGL(k_apply_patch, dim3(grid), dim3(256), 0, s, bl.elems, bl.patch, n, bl.esz, bl.g.st_value);
     } else if (bl.patch) {
         a.patch = bl.patch;

@@ -120,6 +120,7 @@ __device__ __forceinline__ void copy_value(uint8_t *__restrict__ dst, const uint
 struct VCopy {
     uint8_t *dst;
     const uint8_t *src;
+    uint32_t fill = 0;   // 0x100 | b: the source is n bytes b, nothing is loaded (a refill patch's value)
 };
 
 struct Ctx {           // per-launch constants

@@ -91,6 +91,7 @@ class BatchType(enum.IntEnum):  # enum hermes_batch_type_t, spacetime.h:219-226
 
 
 OP_META_SIZE = 16
+OP_VALUE_OFF = 18         # spacetime_op_t.value (after the 16-B meta and the 2-B flags)
 OBJ_META_SIZE = 15
 ENTRY_META_OFF = 18
 BUCKET_SIZE = 64

@@ -227,6 +227,14 @@ def _s(stream=None):
     return _P((stream or torch.cuda.current_stream()).cuda_stream)
 
 
+def patchable(sizes: L.Sizes) -> bool:
+    """Whether a local launch takes refill patches (hkv_batch_desc.d_patch) without a pass of its own over the
+    ops: ops of at most 64 B (k_local_pre / k_local_fused) or, for bigger ones, values of at most 320 B with the
+    op's pad after its value inside its last 8-byte word (k_lookup + k_resolve0_direct, patch_in_resolve)"""
+    pad = sizes.op - L.OP_VALUE_OFF - sizes.st_value
+    return sizes.op <= 64 or (sizes.st_value <= 320 and sizes.op % 8 == 0 and 0 <= pad <= 8)
+
+
 class Round:
     """Buffers and kernels of one replica's protocol round over `n_workers` virtual workers."""
 
@@ -254,14 +262,15 @@ class Round:
         self.rflags = refill_flags(kvs, retry_stalled, coalesce_hot)
         # fused_refill: the refill is planned from the state mirror (hkv_wl_refill_plan) and applied by
         # the next local launch as patches, so the op slab is read and written once per round. Not with
-        # hot-request coalescing (a sequential walk over the ops), VAL credits (their marshal keeps no
-        # mirror) or 312-B ops (refilled in place). Default: wherever it applies.
-        can_fuse = not coalesce_hot and val_credits is None and self.op <= 64
+        # hot-request coalescing (a sequential walk over the ops) or VAL credits (their marshal keeps no
+        # mirror). Big ops (configs[2]'s 312 B) take the patches in the launch's in-place resolve, which
+        # needs values of at most 320 B with the op's pad after the value inside its last 8-byte word
+        # (hkv_batch.hip, patch_in_resolve). Default: wherever it applies.
+        can_fuse = not coalesce_hot and val_credits is None and patchable(kvs.sizes)
         self.fused = can_fuse if fused_refill is None else (fused_refill and can_fuse)
-        # 312-B ops are refilled in place, but from the same state mirror (hkv_wl_refill_st), so a slot
-        # the refill keeps is not read (fused_refill=False: from the ops)
-        self.st_refill = (not self.fused and not coalesce_hot and val_credits is None and self.op > 64
-                          and fused_refill is not False)
+        # otherwise 312-B ops are refilled in place, but from the same state mirror (hkv_wl_refill_st), so a
+        # slot the refill keeps is not read
+        self.st_refill = not self.fused and not coalesce_hot and val_credits is None and self.op > 64
         self.machine_id = kvs.machine_id
         dev = torch.device("cuda", kvs.device)
         W, S = n_workers, self.LOCAL

@@ -21,11 +21,14 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("theta,workers,cfg3", [(0.99, 40, False), (0.0, 40, False), (0.99, 160, False),
-                                                (0.99, 40, True)])
-def test_bench_round_mirrored(theta, workers, cfg3):
+@pytest.mark.parametrize("theta,workers,cfg3,fused,retry", [
+    (0.99, 40, False, None, False), (0.0, 40, False, None, False), (0.99, 160, False, None, False),
+    (0.99, 40, True, None, False), (0.99, 40, True, False, False), (0.99, 40, True, None, True)])
+def test_bench_round_mirrored(theta, workers, cfg3, fused, retry):
     """cfg3: bench.py --config cfg3 (RMWs on, big objects, 25 % PUT + 25 % RMW): the rounds engine,
-    op-sized ACKs from the virtual peers, RMW completions."""
+    op-sized ACKs from the virtual peers, RMW completions. Its refills are planned as patches that the
+    local launch's in-place resolve writes (patch_in_resolve), or with fused=False refilled in place
+    (hkv_wl_refill_st); retry: refill_ops' policy, so patched and kept (stalled) ops share launches."""
     from hermes_amd.kvs import HermesKV
     from hermes_amd.workload import Round, zipf_params
     n_keys, bkts = 60_000, 1 << 16
@@ -36,20 +39,20 @@ def test_bench_round_mirrored(theta, workers, cfg3):
     o.populate(n_keys, g.sizes.kvs_value)
     m = Mirror(g, o, "bench round")
     r = Round(g, workers, L.membership(3, 0), [1, 2], zipf_params(n_keys, theta), 500 if cfg3 else 200,
-              500 if cfg3 else 0, seed=0x5EED, max_steps=8, trace_len=1024)
-    assert r.fused == (not cfg3)
+              500 if cfg3 else 0, seed=0x5EED, max_steps=8, trace_len=1024, fused_refill=fused, retry_stalled=retry)
+    assert r.fused == (fused is None)
     for _ in range(steps):
         r.step()
     torch.cuda.synchronize()
     # local, the peers' INVs (one launch per peer), their ACKs (one rows launch; cfg3: one per peer), VAL
     assert m.launches == steps * (6 if cfg3 else 5)
     st = r.stats()
-    assert st["committed"] > 0 and st["writes_completed"] > 0, st
+    assert st["committed"] > 0 and (st["writes_completed"] > 0 or retry), st
     assert g.take_error_flags() == 0
     # the virtual peers write with the keys' live timestamps: some of their INVs beat local writes
     # in flight on the cid tie-break (WRITE -> INVALID_WRITE / INVALID), and the ACK completes them
     assert m.codes[(int(L.BatchType.invs), "out8", int(L.Resp.INV_SUCCESS))] > 0
-    if cfg3:
+    if cfg3 and not retry:
         # configs[2]'s conflicts: peers INV-abort local RMWs their own write beats (received in the
         # ACK batch), the local replica INV-aborts peer RMWs below its key's timestamp, and the
         # aborted RMWs end as RMW_ABORT in the next local batch (hermesKV.c:372-394)
@@ -57,6 +60,65 @@ def test_bench_round_mirrored(theta, workers, cfg3):
         assert m.codes[(int(L.BatchType.invs), "out8", int(L.Resp.OP_INV_ABORT))] > 0, m.codes
         assert m.codes[(int(L.BatchType.local_ops), "out9", int(L.Resp.RMW_ABORT))] > 0, m.codes
         assert st["rmw_aborts"] > 0, st
+
+
+@pytest.mark.parametrize("skew", [0, 3])
+def test_big_patches_applied_in_resolve(skew):
+    """Refill patches of 312-B ops applied by the local launch itself (hkv_batch.hip patch_in_resolve:
+    k_lookup reads each patch beside the op header, k_resolve0_direct runs the exec functions on a patched
+    copy and writes the op once), against the oracle on the ops as the patches make them: every patch
+    flavour of include/hermeskv.h (GETs, PUTs, RMWs; a value fill byte or none, also on a GET; the ts
+    reset), invalid patches beside valid ones, patched elements past their batch's count (patched, not
+    run), random bytes in the pad after each value (kept), skewed keys over several launches."""
+    from hermes_amd.kvs import HermesKV
+    from oracle.oracle import gen_keys
+    from tests import gen
+    n_keys, bkts, cap = 3000, 512, 1 << 21
+    g = HermesKV(n_keys, bkts, cap, machine_id=1, rmw=True, big_objects=True, extra_cache_lines=4, skew=skew)
+    o = OracleKVS(bkts, cap, 1, True, True, 4, skew=skew)
+    o.populate(n_keys, g.sizes.kvs_value)
+    m = Mirror(g, o, "big patches")
+    sz = g.sizes
+    rng = np.random.default_rng(4242 + skew)
+    keys = gen_keys(n_keys)
+    tsp = gen.TsPool(rng)
+    mb = L.membership(3, 1)
+    W, S = 40, 250                       # 10,000 elements: the multi-kernel engine
+    vend = L.OP_VALUE_OFF + sz.st_value
+    assert 0 < sz.op - vend <= 8
+    hits = 0
+    for rnd in range(4):
+        pool = gen.key_pool(rng, keys, hot=40 if rnd % 2 else 400)
+        loc = gen.local_ops(rng, pool, W * S, sz, True, tsp)
+        raw = loc.view(np.uint8).reshape(W * S, sz.op)
+        raw[:, vend:] = rng.integers(0, 256, size=(W * S, sz.op - vend))
+        p = np.zeros((W * S, 16), np.uint8)
+        valid = rng.random(W * S) < 0.7
+        pk = gen.draw_keys(rng, pool, W * S)
+        p[:, 0:8] = pk.view(np.uint8).reshape(-1, 8)
+        p[:, 8] = rng.choice([int(L.Op.GET), int(L.Op.PUT), int(L.Op.RMW)], size=W * S, p=[0.5, 0.3, 0.2])
+        p[:, 9] = rng.integers(0, 256, size=W * S)
+        p[:, 10:12] = rng.integers(0, 256, size=(W * S, 2))
+        fill = rng.integers(1, 256, size=W * S)
+        getp = p[:, 8] == int(L.Op.GET)
+        p[:, 12] = np.where(getp, np.where(rng.random(W * S) < 0.1, fill, 0),
+                            np.where(rng.random(W * S) < 0.9, fill, 0))
+        p[:, 13] = rng.random(W * S) < 0.3
+        p[:, 14] = valid
+        p[~valid, 8:14] = rng.integers(0, 256, size=(int((~valid).sum()), 6))   # ignored bytes of invalid patches
+        counts = rng.integers(S // 2, S + 1, size=W).astype(np.int32)
+        ops = torch.from_numpy(raw.reshape(-1).copy()).cuda()
+        patch = torch.from_numpy(p.reshape(-1)).cuda()
+        state_out = torch.zeros(W * S, dtype=torch.uint8, device="cuda")
+        m.batch(L.BatchType.local_ops, ops, W, S, sz.op, mb, counts=torch.from_numpy(counts).cuda(), patch=patch,
+                state_out=state_out)
+        got = ops.cpu().numpy().reshape(W * S, sz.op)
+        hits += int(np.isin(got[:, 9], [int(L.Resp.GET_COMPLETE), int(L.Resp.PUT_SUCCESS),
+                                         int(L.Resp.RMW_SUCCESS)]).sum())
+        # a patched element past its batch's count is patched, not run
+        past = (np.arange(S)[None, :] >= counts[:, None]).reshape(-1) & valid
+        assert past.any() and (got[past, 9] == int(L.Bucket.NEW)).all()
+    assert hits > 1000 and m.launches == 4
 
 
 @pytest.mark.parametrize("skew,hot", [(0, False), (3, False), (3, True)])
@@ -584,32 +646,36 @@ def test_marshal_invs_kernel_matches_numpy(big, mirror):
 
 
 def test_big_op_refill_from_state_mirror():
-    """configs[2]'s refill (312-B ops, refilled in place) decides from the state mirror
-    (hkv_wl_refill_st) instead of each op's state byte: the mirror must equal the ops' state bytes
-    and the opcode mirror their opcodes after every round, and the ops, cursors and counters must
-    match a twin round refilled from the ops themselves, byte for byte."""
+    """configs[2]'s refill three ways over the same rounds: planned as patches that the next local launch
+    writes into the 312-B ops (the default, patch_in_resolve), in place deciding from the state mirror
+    (hkv_wl_refill_st, fused_refill=False) and in place from each op's state byte (hkv_wl_refill). After
+    every round the mirrors equal the ops' state and opcode bytes, and the ops -- the planned round's with
+    its patches applied (numpy) -- the cursors and the counters are the same byte for byte."""
     from hermes_amd.kvs import HermesKV
     from hermes_amd.workload import Round, zipf_params
     n_keys, bkts, cap = 60_000, 1 << 16, 1 << 25
     rounds = []
-    for st_refill in (True, False):
+    for mode in ("plan", "mirror", "ops"):
         g = HermesKV(n_keys, bkts, cap, machine_id=0, rmw=True, big_objects=True, extra_cache_lines=4, skew=3)
         r = Round(g, 40, L.membership(3, 0), [1, 2], zipf_params(n_keys, 0.99), 500, 500, seed=0x5EED,
-                  max_steps=8, trace_len=1024, retry_stalled=True)
-        r.st_refill = st_refill and r.st_refill
+                  max_steps=8, trace_len=1024, retry_stalled=True, fused_refill=None if mode == "plan" else False)
+        r.st_refill = mode == "mirror" and r.st_refill
         rounds.append((g, r))
-    assert rounds[0][1].st_refill, "configs[2] rounds refill from the state mirror"
+    assert rounds[0][1].fused and rounds[1][1].st_refill, "configs[2] rounds plan their refills, else use the mirror"
     for _ in range(6):
         for _, r in rounds:
             r.step()
         torch.cuda.synchronize()
-        a, b = rounds[0][1], rounds[1][1]
+        p, a, b = rounds[0][1], rounds[1][1], rounds[2][1]
         ops = a.ops.view(-1, a.op)
         assert torch.equal(a.states, ops[:, 9]), "state mirror differs from the ops' state bytes"
         assert torch.equal(a.opcodes, ops[:, 8]), "opcode mirror differs from the ops' opcodes"
         assert torch.equal(a.ops, b.ops), "refill from the mirror differs from the refill from the ops"
-        assert torch.equal(a.cursor, b.cursor)
-    assert rounds[0][1].stats() == rounds[1][1].stats()
+        planned = _apply_patches(p.ops.cpu().numpy(), p.patch.cpu().numpy(), p.op, p.sizes.st_value)
+        assert np.array_equal(planned, b.ops.cpu().numpy()), "planned refill differs from the refill in place"
+        assert torch.equal(p.opcodes, b.ops.view(-1, b.op)[:, 8]), "planned opcode mirror differs"
+        assert torch.equal(a.cursor, b.cursor) and torch.equal(p.cursor, b.cursor)
+    assert rounds[0][1].stats() == rounds[1][1].stats() == rounds[2][1].stats()
     assert rounds[0][1].stats()["committed"] > 0
     for g, _ in rounds:
         assert g.take_error_flags() == 0

@@ -1252,8 +1252,52 @@ __device__ __forceinline__ void wave_block_copies(uint8_t *dst, const uint8_t *s
 // 64-byte blocks are written whole (a block written with holes costs HBM a read-modify-write:
 // tools/write_bench.hip). The refill's own pass over the slab (k_refill_st_w) goes, and this pass reads
 // no op line: the header came with k_lookup's read, a write's value is the patch's fill byte.
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src)
+{
+    return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, src, 64) | ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64) << 32);
+}
+// Ops whose every byte is known (k_resolve0_direct's whole ones: key h0, header h1, flags and fill byte fl, the
+// fill, the last word lw; nw 8-byte words) written by the whole wave: (nw + 1) / 2 lanes per op, 16 B each, so
+// one store instruction writes 64 / that many ops contiguously. Every lane calls it.
+__device__ __forceinline__ void wave_whole_ops(uint8_t *xg, bool whole, uint64_t h0, uint64_t h1, uint32_t fl, uint64_t lw,
+                                               uint32_t nw)
+{
+    const int lane = threadIdx.x & 63;
+    const int C = (int)((nw + 1) / 2);
+    const int per = 64 / C;
+    const int slot = lane / C, ch = lane - slot * C;
+    unsigned long long todo = __ballot(whole);
+    while (todo) {
+        int mine = -1;
+        for (int k = 0; k < per; ++k) {   // (todo is the same in every lane)
+            if (!todo) break;
+            const int j = __ffsll((long long)todo) - 1;
+            todo &= todo - 1;
+            if (k == slot) mine = j;
+        }
+        const int sl = mine < 0 ? 0 : mine;
+        const uint64_t d = shfl_u64((uint64_t)(uintptr_t)xg, sl), a0 = shfl_u64(h0, sl), a1 = shfl_u64(h1, sl);
+        const uint64_t l = shfl_u64(lw, sl);
+        const uint32_t f = (uint32_t)__shfl((int)fl, sl, 64);
+        if (mine < 0 || slot >= per) continue;
+        const uint64_t pat = 0x0101010101010101ull * ((f >> 16) & 0xFFu);
+        auto word = [&](uint32_t k) {
+            return k == 0 ? a0 : k == 1 ? a1 : k == 2 ? ((uint64_t)(f & 0xFFFFu) | (pat << 16)) : k == nw - 1 ? l : pat;
+        };
+        const uint32_t k0 = 2u * (uint32_t)ch;
+        uint8_t *p = reinterpret_cast<uint8_t *>(d) + 8u * k0;
+        if (k0 + 1 < nw) *reinterpret_cast<U64x2 *>(p) = U64x2{word(k0), word(k0 + 1)};
+        else *reinterpret_cast<uint64_t *>(p) = word(k0);
+    }
+}
+
+#ifdef HKV_R0D_WAVES   // waves per SIMD k_resolve0_direct is compiled for (its registers: 512 / waves)
+#define HKV_R0D_ATTR __attribute__((amdgpu_waves_per_eu(HKV_R0D_WAVES, 8)))
+#else
+#define HKV_R0D_ATTR
+#endif
 template <int TYPE, int SV>
-__global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
+__global__ __launch_bounds__(256) HKV_R0D_ATTR void k_resolve0_direct(BatchArgs a)
 {
     constexpr bool kPir = TYPE == kLocal && SV != 31;
     __shared__ uint64_t sop[kPir ? 256 * 3 : 1];
@@ -1320,27 +1364,24 @@ __global__ __launch_bounds__(256) void k_resolve0_direct(BatchArgs a)
         whole = fb && vc.dst != xg + kOpValueOff;   // (a value the exec copies into the op replaces the fill)
     }
     if (SV != 31) wave_value_copies(vc, a.g.st_value, kVcBatch);
+    if (kPir && a.hx) {
+        // a whole op: key, header, flags, the value fill and the pad after it (launch_batch: at most 8 bytes,
+        // in the op's last word), written by the wave, three ops a store instruction, so every 64-byte block
+        // of the op is complete in L2 before it goes to HBM (whole ops stored by their own lane, 16 bytes
+        // at a time: 4 % slower at configs[2])
+        const uint32_t vend = kOpValueOff + a.g.st_value, w0 = (uint32_t)a.esz - 8u;
+        const uint64_t pat = 0x0101010101010101ull * fb;
+        const uint32_t nlow = vend - w0;
+        const uint64_t lmask = nlow >= 8 ? ~0ull : (1ull << (8 * nlow)) - 1ull;
+        wave_whole_ops(xg, whole, cop[0], cop[1], ((uint32_t)cop[2] & 0xFFFFu) | (fb << 16),
+                       (pat & lmask) | (hw.b & ~lmask), (uint32_t)a.esz / 8u);
+    }
     if (!in) return;
     a.st[i] = st;
     if (pd) {
         const uint64_t h0 = cop[0], h1 = cop[1], h2 = cop[2];
         const uint32_t vend = kOpValueOff + a.g.st_value, w0 = (uint32_t)a.esz - 8u;
-        if (whole) {
-            // key, header, flags, the value fill and the pad after it (launch_batch: at most 8 bytes, in
-            // the op's last word), 16 bytes a store, back to back, so every 64-byte block of the op is
-            // complete in L2 before it goes to HBM
-            const uint64_t pat = 0x0101010101010101ull * fb;
-            const uint32_t nlow = vend - w0;   // value bytes in the last word
-            const uint64_t lmask = nlow >= 8 ? ~0ull : (1ull << (8 * nlow)) - 1ull;
-            const uint64_t lastw = (pat & lmask) | (hw.b & ~lmask);
-            const uint32_t nw = (uint32_t)a.esz / 8u;
-            auto word = [&](uint32_t k) {
-                return k == 0 ? h0 : k == 1 ? h1 : k == 2 ? ((h2 & 0xFFFFull) | (pat << 16)) : k == nw - 1 ? lastw : pat;
-            };
-            uint32_t k = 0;
-            for (; k + 2 <= nw; k += 2) *reinterpret_cast<U64x2 *>(xg + 8 * k) = U64x2{word(k), word(k + 1)};
-            if (k < nw) *reinterpret_cast<uint64_t *>(xg + 8 * k) = word(k);
-        } else {   // the header from the copy, then the pad bytes after the value
+        if (!whole) {   // the header from the copy, then the pad bytes after the value
             uint64_t *o = reinterpret_cast<uint64_t *>(xg);
             o[0] = h0;
             o[1] = h1;

@@ -68,10 +68,19 @@ def _read_calls(path):
     return calls
 
 
-def test_concurrent_callers_match_oracle(tmp_path):
+# the host boundary's switches (hkv_runtime.hip), each a different serving path or limit for the same results:
+# the default (serving kernel over BAR-staged batches, partitioned launches), one launch per serving pass
+# (HKV_HOST_SERVE=0), batches staged in pinned host memory (HKV_STAGE_VRAM=0), launches not partitioned by
+# key (HKV_HOST_PART=0), and one launch in flight taking one published launch per pass
+SWITCHES = [{}, {"HKV_HOST_SERVE": "0"}, {"HKV_STAGE_VRAM": "0"}, {"HKV_HOST_PART": "0"},
+            {"HKV_SERVE_MERGE": "1", "HKV_PART_INFLIGHT": "1", "HKV_SERVE_IDLE_MS": "0.5"}]
+
+
+@pytest.mark.parametrize("env", SWITCHES, ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()) or "default")
+def test_concurrent_callers_match_oracle(tmp_path, env):
     threads, rounds = 8, 30
     p = subprocess.run([os.path.join(TOOLS, "capi_threads"), "trace", str(threads), str(rounds), str(tmp_path)],
-                       capture_output=True, text=True, timeout=240)
+                       capture_output=True, text=True, timeout=240, env=dict(os.environ, **env))
     assert p.returncode == 0, p.stdout + p.stderr
     o = OracleKVS(1 << 21, 1 << 30, machine_id=0)
     o.populate(1_000_000, L.DEFAULT.kvs_value)

@@ -1,4 +1,4 @@
-"""Print every kernel of one bench step (the last k_refill-delimited step of the timed region)
+"""Print every kernel of one bench step (the last step delimited by the refill (k_refill* or k_plan_peer_ts) of the timed region)
 from a rocprofv3 kernel trace: name, grid, duration, gap to the previous kernel.
     python tools/step_kernels.py TAG [step_from_end]"""
 import csv
@@ -9,7 +9,7 @@ tag = sys.argv[1]
 back = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 f = glob.glob(f"gpurun_out/{tag}/prof/**/*kernel_trace.csv", recursive=True)[0]
 rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "k_refill" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(rows) if "k_refill" in r["Kernel_Name"] or "k_plan_peer_ts" in r["Kernel_Name"]]
 a, b = starts[-back - 1], starts[-back]
 prev = None
 tot = 0.0

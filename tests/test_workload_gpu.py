@@ -62,20 +62,22 @@ def test_bench_round_mirrored(theta, workers, cfg3, fused, retry):
         assert st["rmw_aborts"] > 0, st
 
 
-@pytest.mark.parametrize("skew", [0, 3])
-def test_big_patches_applied_in_resolve(skew):
+@pytest.mark.parametrize("skew,rmw", [(0, True), (3, True), (3, False)])
+def test_big_patches_applied_in_resolve(skew, rmw):
     """Refill patches of 312-B ops applied by the local launch itself (hkv_batch.hip patch_in_resolve:
     k_lookup reads each patch beside the op header, k_resolve0_direct runs the exec functions on a patched
     copy and writes the op once), against the oracle on the ops as the patches make them: every patch
     flavour of include/hermeskv.h (GETs, PUTs, RMWs; a value fill byte or none, also on a GET; the ts
     reset), invalid patches beside valid ones, patched elements past their batch's count (patched, not
-    run), random bytes in the pad after each value (kept), skewed keys over several launches."""
+    run), random bytes in the pad after each value (kept), skewed keys over several launches. With RMWs off
+    an element after its key's first mutation resolves against S_1, whose kind (WRITE with version + 2, or
+    REPLAY) the skew flags take from that first element's opcode -- its patch's, as the op is not yet written."""
     from hermes_amd.kvs import HermesKV
     from oracle.oracle import gen_keys
     from tests import gen
     n_keys, bkts, cap = 3000, 512, 1 << 21
-    g = HermesKV(n_keys, bkts, cap, machine_id=1, rmw=True, big_objects=True, extra_cache_lines=4, skew=skew)
-    o = OracleKVS(bkts, cap, 1, True, True, 4, skew=skew)
+    g = HermesKV(n_keys, bkts, cap, machine_id=1, rmw=rmw, big_objects=True, extra_cache_lines=4, skew=skew)
+    o = OracleKVS(bkts, cap, 1, rmw, True, 4, skew=skew)
     o.populate(n_keys, g.sizes.kvs_value)
     m = Mirror(g, o, "big patches")
     sz = g.sizes
@@ -89,14 +91,15 @@ def test_big_patches_applied_in_resolve(skew):
     hits = 0
     for rnd in range(4):
         pool = gen.key_pool(rng, keys, hot=40 if rnd % 2 else 400)
-        loc = gen.local_ops(rng, pool, W * S, sz, True, tsp)
+        loc = gen.local_ops(rng, pool, W * S, sz, rmw, tsp)
         raw = loc.view(np.uint8).reshape(W * S, sz.op)
         raw[:, vend:] = rng.integers(0, 256, size=(W * S, sz.op - vend))
         p = np.zeros((W * S, 16), np.uint8)
         valid = rng.random(W * S) < 0.7
         pk = gen.draw_keys(rng, pool, W * S)
         p[:, 0:8] = pk.view(np.uint8).reshape(-1, 8)
-        p[:, 8] = rng.choice([int(L.Op.GET), int(L.Op.PUT), int(L.Op.RMW)], size=W * S, p=[0.5, 0.3, 0.2])
+        p[:, 8] = rng.choice([int(L.Op.GET), int(L.Op.PUT), int(L.Op.RMW)], size=W * S,
+                             p=[0.5, 0.3, 0.2] if rmw else [0.6, 0.4, 0.0])
         p[:, 9] = rng.integers(0, 256, size=W * S)
         p[:, 10:12] = rng.integers(0, 256, size=(W * S, 2))
         fill = rng.integers(1, 256, size=W * S)

@@ -109,7 +109,8 @@ def parse():
                         "live op of that id (committed ops count them)")
     p.add_argument("--inplace-refill", action="store_true",
                    help="N=1: refill the ops in place (hkv_wl_refill_st / hkv_wl_refill) instead of planning patches "
-                        "that the next local launch writes into the ops (hkv_wl_refill_plan, the default)")
+                        "that the next local launch writes into the ops (hkv_wl_refill_plan, the default; configs[2] "
+                        "under retry refills in place anyway, where that is faster)")
     p.add_argument("--policy-steps", "--retry-steps", type=int, default=10, dest="policy_steps",
                    help="N=1: also time this many steps of each other refill policy on the same table and "
                         "report them under detail.policies (0 = skip)")
@@ -401,7 +402,8 @@ def main():
         "roofline": {
             "bound": "hbm", "kernel": (f"{dom} batch launch (" + ("k_local_pre + k_local_fused + k_local_deferred + k_commit_w, the direct path" if dom == "local"
                                                   and not cfg3 else "k_lookup + element-order rounds, the refill patches "
-                                                  "written by k_resolve0_direct" if cfg3 else "k_lookup + element-order rounds") + ", hkv_batch.hip)"),
+                                                  "written by k_resolve0_direct" if cfg3 and getattr(rnd, "fused", False)
+                                                  else "k_lookup + element-order rounds") + ", hkv_batch.hip)"),
             "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
             "traffic": traffic, "traffic_source": traffic_src,
             "traffic_ratio": traffic / per_launch_bytes[dom] if traffic else None, "launch_ms": ms.get(dom),

@@ -265,9 +265,13 @@ class Round:
         # hot-request coalescing (a sequential walk over the ops) or VAL credits (their marshal keeps no
         # mirror). Big ops (configs[2]'s 312 B) take the patches in the launch's in-place resolve, which
         # needs values of at most 320 B with the op's pad after the value inside its last 8-byte word
-        # (hkv_batch.hip, patch_in_resolve). Default: wherever it applies.
+        # (hkv_batch.hip, patch_in_resolve); that pays where most slots are refilled each round (fresh
+        # batches: 0.655-0.659 -> 0.704-0.716 G ops/s), while under retry, with few slots refilled, the
+        # patch reads of every element cost more than the in-place refill saves (61.1-61.5 against
+        # 63.0-63.6 M, gpurun_out/r06q), so big ops plan only under fresh batches. Default: wherever it pays.
         can_fuse = not coalesce_hot and val_credits is None and patchable(kvs.sizes)
-        self.fused = can_fuse if fused_refill is None else (fused_refill and can_fuse)
+        pays = kvs.sizes.op <= 64 or not retry_stalled
+        self.fused = (can_fuse and pays) if fused_refill is None else (fused_refill and can_fuse)
         # otherwise 312-B ops are refilled in place, but from the same state mirror (hkv_wl_refill_st), so a
         # slot the refill keeps is not read
         self.st_refill = not self.fused and not coalesce_hot and val_credits is None and self.op > 64

@@ -23,12 +23,13 @@ def _need_gpu():
 
 @pytest.mark.parametrize("theta,workers,cfg3,fused,retry", [
     (0.99, 40, False, None, False), (0.0, 40, False, None, False), (0.99, 160, False, None, False),
-    (0.99, 40, True, None, False), (0.99, 40, True, False, False), (0.99, 40, True, None, True)])
+    (0.99, 40, True, None, False), (0.99, 40, True, False, False), (0.99, 40, True, True, True)])
 def test_bench_round_mirrored(theta, workers, cfg3, fused, retry):
     """cfg3: bench.py --config cfg3 (RMWs on, big objects, 25 % PUT + 25 % RMW): the rounds engine,
     op-sized ACKs from the virtual peers, RMW completions. Its refills are planned as patches that the
     local launch's in-place resolve writes (patch_in_resolve), or with fused=False refilled in place
-    (hkv_wl_refill_st); retry: refill_ops' policy, so patched and kept (stalled) ops share launches."""
+    (hkv_wl_refill_st); retry: refill_ops' policy (planned only when asked, fused=True), so patched and
+    kept (stalled) ops share launches."""
     from hermes_amd.kvs import HermesKV
     from hermes_amd.workload import Round, zipf_params
     n_keys, bkts = 60_000, 1 << 16
@@ -40,7 +41,7 @@ def test_bench_round_mirrored(theta, workers, cfg3, fused, retry):
     m = Mirror(g, o, "bench round")
     r = Round(g, workers, L.membership(3, 0), [1, 2], zipf_params(n_keys, theta), 500 if cfg3 else 200,
               500 if cfg3 else 0, seed=0x5EED, max_steps=8, trace_len=1024, fused_refill=fused, retry_stalled=retry)
-    assert r.fused == (fused is None)
+    assert r.fused == (fused is not False)   # (cfg3 under retry plans only when asked: fused=True)
     for _ in range(steps):
         r.step()
     torch.cuda.synchronize()
@@ -650,7 +651,7 @@ def test_marshal_invs_kernel_matches_numpy(big, mirror):
 
 def test_big_op_refill_from_state_mirror():
     """configs[2]'s refill three ways over the same rounds: planned as patches that the next local launch
-    writes into the 312-B ops (the default, patch_in_resolve), in place deciding from the state mirror
+    writes into the 312-B ops (patch_in_resolve; the default under fresh batches, asked for here), in place deciding from the state mirror
     (hkv_wl_refill_st, fused_refill=False) and in place from each op's state byte (hkv_wl_refill). After
     every round the mirrors equal the ops' state and opcode bytes, and the ops -- the planned round's with
     its patches applied (numpy) -- the cursors and the counters are the same byte for byte."""
@@ -661,7 +662,7 @@ def test_big_op_refill_from_state_mirror():
     for mode in ("plan", "mirror", "ops"):
         g = HermesKV(n_keys, bkts, cap, machine_id=0, rmw=True, big_objects=True, extra_cache_lines=4, skew=3)
         r = Round(g, 40, L.membership(3, 0), [1, 2], zipf_params(n_keys, 0.99), 500, 500, seed=0x5EED,
-                  max_steps=8, trace_len=1024, retry_stalled=True, fused_refill=None if mode == "plan" else False)
+                  max_steps=8, trace_len=1024, retry_stalled=True, fused_refill=mode == "plan")
         r.st_refill = mode == "mirror" and r.st_refill
         rounds.append((g, r))
     assert rounds[0][1].fused and rounds[1][1].st_refill, "configs[2] rounds plan their refills, else use the mirror"

@@ -97,6 +97,8 @@ struct BatchArgs {
     uint8_t *state_out;          // local launches: each element's final state byte (may be NULL)
     const uint8_t *opc;          // local launches: the caller's opcode mirror (may be NULL, see k_local_pre)
     const uint8_t *patch;        // local direct path: pending header writes (hkv_batch_desc.d_patch), or NULL
+    uint16_t *fk;                // local launches with RMWs: [n] each round-0 candidate's kind of mutation (fk_kind,
+                                 // k_lookup), so k_resolve0_direct can resolve the elements after an absorbing F
     uint64_t *hx;                // big local launches with patches (patch_in_resolve): [2 n] each patched element's
                                  // header word (bytes 8..15) as patched and its op's last 8-byte word, from
                                  // k_lookup for k_resolve0_direct; NULL otherwise
@@ -441,6 +443,50 @@ __device__ __forceinline__ uint64_t patched_hdr(uint64_t h, uint64_t pb)
 }
 __device__ __forceinline__ bool patch_valid(uint64_t pb);
 
+// Local launches with RMWs: how a round-0 candidate (would_mutate against S_0) changes its key, from its
+// header word h (bytes 8..15) and S_0 -- bits 0..1: 1 update_actions (a PUT, or an RMW from VALID;
+// hermesKV.c:100-141), 2 a write replay (a GET, or an RMW from INVALID: :155-194), 3 anything else (an
+// in-progress RMW's abort); bit 2 the RMW flag; bits 8..15 the op's val_len byte. The first two leave the
+// key in an absorbing state for the rest of the launch (WRITE or REPLAY with the op buffer index set: every
+// later GET, PUT and RMW stalls, and no in-progress RMW matches the new last-local-write timestamp), so the
+// elements after F resolve against S_1 (after_first_rmw) in k_resolve0_direct instead of later rounds.
+enum : uint16_t { kFkWrite = 1, kFkReplay = 2, kFkOther = 3 };
+__device__ __forceinline__ uint16_t fk_kind(uint64_t h, const Meta &m0)
+{
+    const uint8_t oc = (uint8_t)h, st = (uint8_t)(h >> 8);
+    uint16_t k = kFkOther;
+    if (oc == kOpPut) k = kFkWrite;
+    else if (oc == kOpGet) k = kFkReplay;
+    else if (oc == kOpRmw && st != kInProgressRmw) k = m_state(m0) == kValid ? kFkWrite : kFkReplay;
+    return (uint16_t)(k | (oc == kOpRmw ? 4u : 0u) | (((h >> 16) & 0xFFu) << 8));
+}
+// S_1 after F (kind fk, at batch index idx) from S_0, as update_actions / write_replay leave it
+__device__ __forceinline__ Meta after_first_rmw(const BatchArgs &a, const Meta &m0, uint16_t fk, uint8_t idx)
+{
+    Meta m = m0;
+    if ((fk & 3u) == kFkWrite) {
+        const uint8_t rmw_flag = (fk >> 2) & 1u;
+        m_set_val_len(m, (uint8_t)(((uint8_t)(fk >> 8) >> a.g.shift) + kOpMetaSize));
+        m_set_rmw(m, rmw_flag);
+        m_set_state(m, kWrite);
+        m_set_obi(m, idx);
+        const uint32_t step = (!a.g.rmw_enabled || rmw_flag == 1) ? 2u : 4u;
+        const uint8_t node = (uint8_t)a.g.machine_id;
+        m.llw_ver = m.ver + step;
+        m.llw_cid = node;
+        m_set_ack_bv(m, a.w_ack_init);
+        m.ver += step;
+        m_set_cid(m, node);
+    } else {
+        m_set_state(m, kReplay);
+        m_set_obi(m, idx);
+        m.llw_ver = m.ver;
+        m.llw_cid = m_cid(m);
+        m_set_ack_bv(m, a.w_ack_init);
+    }
+    return m;
+}
+
 constexpr int64_t kLookupHead = 8192;
 constexpr int kLookupPair = 2;
 // Four lanes (q = lane & 3) look up kLookupPair keys side by side: the 64-B bucket (16 B per
@@ -657,6 +703,7 @@ __global__ __launch_bounds__(256) void k_lookup(BatchArgs a, int64_t i_begin, in
                 uint64_t h2[2] = {0, hdr[k]};
                 Ctx c = make_ctx(a);
                 if (would_mutate(a.type, reinterpret_cast<const uint8_t *>(h2), m0[k], c)) {
+                    if (a.fk) a.fk[gi[k]] = fk_kind(hdr[k], m0[k]);
                     const unsigned long long vv = ((unsigned long long)(~a.rtag0) << 32) | (uint32_t)gi[k];
                     unsigned long long *fw = a.fw + fw_index(a, phys[k]);
                     if (vv < __hip_atomic_load(fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(fw, vv);
@@ -1337,8 +1384,22 @@ __global__ __launch_bounds__(256) HKV_R0D_ATTR void k_resolve0_direct(BatchArgs 
         Meta m;
         meta_load(entry_of(a, e), m);
         const uint32_t f = (uint8_t)(m.w5 >> 16) == a.ltag ? first_cand(*fw_of(a, e), a.rtag0) : kNone;
-        if (f == kNone || (uint32_t)i < f || ((uint32_t)i > f && a.rounds == 0)) {
-            const Meta m0 = (f == kNone || (uint32_t)i < f) ? m : after_first<TYPE>(a, m, f, 0);
+        // elements after F: resolved here when F's mutation is absorbing (no RMWs: always; with RMWs: F's kind)
+        uint16_t fkf = 0;
+        if (TYPE == kLocal && a.fk && f != kNone && (uint32_t)i > f) fkf = a.fk[f];
+        const bool after_abs = (uint32_t)i > f && f != kNone && (a.rounds == 0 || (fkf & 3u) == kFkWrite ||
+                                                                  (fkf & 3u) == kFkReplay);
+        if (f == kNone || (uint32_t)i < f || after_abs) {
+            Meta m0 = m;
+            if (after_abs) {
+                if (a.rounds == 0) {
+                    m0 = after_first<TYPE>(a, m, f, 0);
+                } else {
+                    int64_t fs;
+                    batch_of(a, f, fs);
+                    m0 = after_first_rmw(a, m, fkf, (uint8_t)(f - fs));
+                }
+            }
             Meta tm = m0;
             if (pd) dispatch<SV>(TYPE, xl, entry_of(a, e), idx, tm, c);
             else dispatch<SV>(TYPE, xg, entry_of(a, e), idx, tm, c);
@@ -3684,6 +3745,7 @@ static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 size_t batch_scratch_bytes(int64_t cap, uint32_t entry_size)
 {
     return align256(4 * (size_t)cap) * 3 + align256((size_t)cap) + align256(16 * (size_t)cap) * 2 + 256 +
+           align256(2 * (size_t)cap) +
            align256((size_t)entry_size * (size_t)cap);
 }
 
@@ -3703,6 +3765,7 @@ void batch_carve(BatchLaunch &bl, uint8_t *base, int64_t cap, uint32_t entry_siz
     bl.shadow = take((size_t)entry_size * (size_t)cap);
     bl.ctr = reinterpret_cast<uint32_t *>(take(256));
     bl.hx = reinterpret_cast<uint64_t *>(take(16 * (size_t)cap));
+    bl.fk = reinterpret_cast<uint16_t *>(take(2 * (size_t)cap));
     bl.cap = (uint32_t)cap;
 }
 
@@ -3722,6 +3785,7 @@ int launch_batch(BatchLaunch &bl, hipStream_t s)
     a.opc = bl.type == kLocal ? bl.opcode_in : nullptr;
     a.patch = nullptr;
     a.hx = nullptr;
+    a.fk = bl.type == kLocal && bl.g.rmw_enabled && bl.esz > 64 ? bl.fk : nullptr;   // (k_resolve0_direct's launches)
     a.ack_out = bl.type == kInvs || (bl.type == kAcks && bl.n_rows > 0) ? bl.ack_out : nullptr;
     a.ack_out_size = bl.ack_out_size;
     a.n_rows = bl.n_rows;

@@ -33,6 +33,7 @@ struct BatchLaunch {
     unsigned long long *mem;
     uint32_t *ent, *fbl, *pf, *ctr;
     uint64_t *hx;                // [2 cap] patched headers of big local launches (BatchArgs::hx)
+    uint16_t *fk;                // [cap] round-0 candidates' kinds of mutation (BatchArgs::fk)
     uint8_t *st, *shadow;
     uint32_t cap;                             // elements the scratch was carved for
     uint32_t epoch;                           // launch counter of the table, 1..batch_max_epoch()

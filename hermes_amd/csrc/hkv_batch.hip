@@ -1338,11 +1338,13 @@ __device__ __forceinline__ void wave_whole_ops(uint8_t *xg, bool whole, uint64_t
     }
 }
 
-#ifdef HKV_R0D_WAVES   // waves per SIMD k_resolve0_direct is compiled for (its registers: 512 / waves)
-#define HKV_R0D_ATTR __attribute__((amdgpu_waves_per_eu(HKV_R0D_WAVES, 8)))
-#else
-#define HKV_R0D_ATTR
+// waves per SIMD k_resolve0_direct is compiled for (its registers: 512 / waves). At 8 it fits 64 VGPRs
+// instead of 127 (4 waves per SIMD): configs[2] fresh 0.736-0.741 -> 0.772-0.782 G ops/s (gpurun_out/r06s;
+// in round 5's kernel, before the patches, it was level)
+#ifndef HKV_R0D_WAVES
+#define HKV_R0D_WAVES 8
 #endif
+#define HKV_R0D_ATTR __attribute__((amdgpu_waves_per_eu(HKV_R0D_WAVES, 8)))
 template <int TYPE, int SV>
 __global__ __launch_bounds__(256) HKV_R0D_ATTR void k_resolve0_direct(BatchArgs a)
 {

@@ -2256,7 +2256,12 @@ __global__ __launch_bounds__(64) void k_unique_lds(BatchArgs a)
 #define HKV_ROWS_SGPR_ATTR
 #endif
 template <int TYPE, int RMAX, int CH, int P = kLookupPair>
-__global__ __launch_bounds__(64) HKV_ROWS_SGPR_ATTR void k_unique_rows(BatchArgs a)
+#ifdef HKV_ROWS_WAVES   // (A/B builds) waves per SIMD k_unique_rows is compiled for
+#define HKV_ROWS_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(HKV_ROWS_WAVES, 8)))
+#else
+#define HKV_ROWS_WAVES_ATTR
+#endif
+__global__ __launch_bounds__(64) HKV_ROWS_SGPR_ATTR HKV_ROWS_WAVES_ATTR void k_unique_rows(BatchArgs a)
 {
     constexpr int E = 16 * P;   // positions per wave: P per lane group
     // CH: 16-B chunks of an element held in LDS (1 for 16-B ACKs, 4 for 56-B INVs)

@@ -178,17 +178,23 @@ class _DeviceBytes:
         self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False), "version": 3}
 
 
-def test_full_size_round_invariants():
-    """BASELINE configs[1] at full size (100M keys, 8192 virtual workers, the bench's round):
-    properties that hold at any size. After every round each key is VALID again (every local write
-    was ACKed by both virtual peers and completed, every INV's VAL applied, no membership change),
-    no INV was held back, writes completed, and the engine's consistency flags are clear."""
+@pytest.mark.parametrize("cfg3", [False, True])
+def test_full_size_round_invariants(cfg3):
+    """BASELINE configs[1] at full size (100M keys, 16384 virtual workers: the bench's round), and
+    configs[2] (the same keys in 320-B entries, RMWs, fresh batches: its refills planned as patches that
+    the local launch writes): properties that hold at any size. After every round each key is VALID again
+    (every local write was ACKed by both virtual peers and completed, every INV's VAL applied, no
+    membership change), no INV was held back, writes completed, and the engine's consistency flags are
+    clear."""
     from hermes_amd.kvs import HermesKV, sized_geometry
     from hermes_amd.workload import Round, zipf_params
     n_keys = 100_000_000
-    bkts, cap = sized_geometry(n_keys)
-    g = HermesKV(n_keys, bkts, cap, machine_id=0)
-    r = Round(g, 8192, L.membership(3, 0), [1, 2], zipf_params(n_keys, 0.99), 200, seed=0x5EED, max_steps=4)
+    sizes = L.Sizes(True, 4) if cfg3 else L.DEFAULT
+    bkts, cap = sized_geometry(n_keys, sizes)
+    g = HermesKV(n_keys, bkts, cap, machine_id=0, rmw=cfg3, big_objects=cfg3, extra_cache_lines=4 if cfg3 else 0)
+    r = Round(g, 16384, L.membership(3, 0), [1, 2], zipf_params(n_keys, 0.99), 500 if cfg3 else 200,
+              500 if cfg3 else 0, seed=0x5EED, max_steps=4)
+    assert r.fused
     entry = g.sizes.entry
     assert g.log_head == n_keys * entry       # populate wrote entries 0..n-1 back to back
     log = torch.as_tensor(_DeviceBytes(g.device_log(), n_keys * entry), device="cuda")
@@ -200,7 +206,7 @@ def test_full_size_round_invariants():
         bad = int((state != int(L.State.VALID)).sum())
         assert bad == 0, f"round {step}: {bad} keys not VALID"
     st = r.stats()
-    assert st["invs_held"] == 0 and st["committed"] > 2_000_000 and st["writes_completed"] > 300_000, st
+    assert st["invs_held"] == 0 and st["committed"] > 4_000_000 and st["writes_completed"] > 600_000, st
     assert g.take_error_flags() == 0
 
 

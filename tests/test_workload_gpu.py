@@ -63,6 +63,50 @@ def test_bench_round_mirrored(theta, workers, cfg3, fused, retry):
         assert st["rmw_aborts"] > 0, st
 
 
+@pytest.mark.parametrize("cfg3", [False, True])
+def test_merged_plan_peer_ts_equals_split(cfg3):
+    """hkv_wl_refill_plan_peer_ts (the refill plan and the next round's virtual-peer timestamps in one
+    launch at the end of Round.step) against hkv_wl_refill_plan at the end of the step and hkv_wl_peer_ts_at
+    at the start of the next: two rounds from the same seed, one forced to the split calls, must hold the
+    same ops, patches, cursors, counters, the round's peer slabs and table bytes after every step."""
+    from hermes_amd.kvs import HermesKV
+    from hermes_amd.workload import Round, zipf_params
+    n_keys, bkts = 60_000, 1 << 16
+    cap = 1 << 25 if cfg3 else 1 << 23
+    rounds = []
+    for split in (False, True):
+        g = HermesKV(n_keys, bkts, cap, machine_id=0, rmw=cfg3, big_objects=cfg3, extra_cache_lines=4 if cfg3 else 0)
+        r = Round(g, 40, L.membership(3, 0), [1, 2], zipf_params(n_keys, 0.99), 500 if cfg3 else 200,
+                  500 if cfg3 else 0, seed=0x5EED, max_steps=8, trace_len=1024)
+        assert r.fused
+        if split:
+            refill = r.refill
+            r.refill = lambda first=False, next_round=False, _f=refill: _f(first)
+        rounds.append((g, r))
+    for step in range(5):
+        for _, r in rounds:
+            r.step()
+        torch.cuda.synchronize()
+        (ga, a), (gb, b) = rounds
+        # (peer_ts, the RMW peers' write per entry and peer, is stamped a round ahead by the merged launch
+        # like the slabs below; the ops and the table show its use)
+        for name in ("ops", "patch", "cursor", "states", "opcodes"):
+            x, y = getattr(a, name), getattr(b, name)
+            assert (x is None and y is None) or torch.equal(x, y), f"step {step}: {name} differs"
+        # the peers' INV / VAL slabs of the round just run (the merged launch has already stamped the next
+        # round's; the split calls stamp them when that round starts)
+        n = len(a.remote_packed)
+        k = step % n
+        if n > 1:
+            for j, (x, y) in enumerate(zip(a.remote_packed[k], b.remote_packed[k])):
+                if isinstance(x, torch.Tensor):
+                    assert torch.equal(x, y), f"step {step}: remote slab {k}.{j} differs"
+        assert np.array_equal(ga.index_bytes(), gb.index_bytes()) and np.array_equal(ga.log_bytes(), gb.log_bytes())
+    assert rounds[0][1].stats() == rounds[1][1].stats() and rounds[0][1].stats()["committed"] > 0
+    for g, _ in rounds:
+        assert g.take_error_flags() == 0
+
+
 @pytest.mark.parametrize("skew,rmw", [(0, True), (3, True), (3, False)])
 def test_big_patches_applied_in_resolve(skew, rmw):
     """Refill patches of 312-B ops applied by the local launch itself (hkv_batch.hip patch_in_resolve:
